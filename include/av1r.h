@@ -1,0 +1,238 @@
+/*
+ * av1r.h -- C-ABI of the MI355X (gfx950) AV1 block-reconstruction backend.
+ *
+ * The boundary sits where the reference decoder (oddstone/av1dec) hands a parsed
+ * frame to reconstruction: `Decoder::decodeFrame` (decoder/Av1Decoder.cpp:128-156)
+ * walks every Tile's parsed SuperBlock->Partition->Block->TransformBlock tree with
+ * `decode()` and then runs `decode_frame_wrapup` (Av1Decoder.cpp:171-192:
+ * LoopFilter -> Cdef -> LoopRestoration).  Everything ABOVE that line (OBU/header
+ * parse, od_ec entropy decoding, mode-info and coefficient parse) stays on the host;
+ * everything BELOW it is this library.  The host ships one "frame batch": the frame
+ * header, the per-4x4 mode-info grid, the coded blocks and transform blocks in decode
+ * order, the non-zero quantized coefficients, palette maps, CDEF indices and loop
+ * restoration unit parameters.  All structs are POD, little-endian, no padding holes
+ * (sizes are asserted in av1r_abi.c / tests).
+ *
+ * Enumerations (BLOCK_SIZE, TX_SIZE, TX_TYPE, PREDICTION_MODE, ...) use the numeric
+ * values of the reference's aom/enums.h so a reference-side binding is a field copy.
+ *
+ * Entry points replace (reference file:line):
+ *   av1r_create / av1r_destroy        -- Decoder::Decoder / ~Decoder (Av1Decoder.cpp:40-47)
+ *   av1r_decode_frame                 -- Decoder::decodeFrame + decode_frame_wrapup
+ *                                        (Av1Decoder.cpp:128-156, 171-192)
+ *   av1r_frame_begin/submit_tile/end  -- the same, split per Tile (Tile::decode, Tile.cpp:168-178)
+ *   av1r_show_existing                -- Decoder::showExistingFrame (Av1Decoder.cpp:158-169)
+ *   av1r_output_pending/av1r_get_output -- Decoder::getOutput (Av1Decoder.cpp:203-211) +
+ *                                        the I420 row copy of DecodeOutput::output
+ *                                        (tests/DecodeOutput.cpp:48-69)
+ *   av1r_read_stage                   -- debug read-back of one pipeline stage
+ *                                        (the reference's DUMP hooks, Av1Decoder.cpp:142-152)
+ */
+#ifndef AV1R_H
+#define AV1R_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AV1R_VERSION 1u
+
+/* ---- status codes (map onto YamiStatus, interface/VideoCommonDefs.h:130-164) ---- */
+#define AV1R_OK 0
+#define AV1R_E_INVALID (-1)      /* malformed batch / bad argument  (YAMI_INVALID_PARAM) */
+#define AV1R_E_UNSUPPORTED (-2)  /* feature outside the reference's support (YAMI_UNSUPPORTED) */
+#define AV1R_E_DEVICE (-3)       /* HIP error (YAMI_FAIL) */
+#define AV1R_E_NOMEM (-4)        /* allocation failure (YAMI_OUT_MEMORY) */
+#define AV1R_E_NO_OUTPUT (-5)    /* output queue empty (getOutput() == nullptr) */
+
+/* ---- per-4x4 mode-info record: the subset of ModeInfoBlock (decoder/Parser.h:432-455)
+ *      read by reconstruction and the loop filters.  One per 4x4 of the SB-aligned grid
+ *      (AlignedMiRows x AlignedMiCols, Parser.cpp:551).  24 bytes. ---- */
+typedef struct av1r_mi {
+    int16_t mv[2][2];     /* Mvs[refList].mv[{0=row,1=col}] in 1/8 pel            */
+    int8_t ref_frame[2];  /* RefFrames[]: -1 NONE, 0 INTRA, 1..7 LAST..ALTREF       */
+    uint8_t mi_size;      /* MiSize (BLOCK_SIZE)                                    */
+    uint8_t y_mode;       /* YMode (PREDICTION_MODE)                                */
+    uint8_t filt;         /* InterpFilters[0] | InterpFilters[1] << 4               */
+    uint8_t flags;        /* AV1R_MI_SKIP | AV1R_MI_INTER                           */
+    uint8_t lf_tx[3];     /* LoopfilterTxSizes[plane] (TX_SIZE)                     */
+    int8_t delta_lf[4];   /* DeltaLFs[]                                             */
+    uint8_t uv_mode;      /* UVMode                                                 */
+    uint8_t pad[2];
+} av1r_mi;
+#define AV1R_MI_SKIP 1u
+#define AV1R_MI_INTER 2u
+
+/* ---- coded block (Block, decoder/Block.h:52-291).  One per Block in decode order. ---- */
+typedef struct av1r_block {
+    uint16_t mi_row, mi_col;
+    uint8_t mi_size;           /* BLOCK_SIZE                                         */
+    uint8_t qindex;            /* get_qindex(CurrentQIndex, segment_id) (Parser.cpp:1654) */
+    uint8_t y_mode, uv_mode;
+    int8_t angle_delta_y, angle_delta_uv;
+    uint8_t filter_intra_mode; /* FILTER_INTRA_MODE, valid when AV1R_BLK_FILTER_INTRA   */
+    int8_t cfl_alpha_u, cfl_alpha_v;
+    uint8_t palette_size_y, palette_size_uv;
+    uint8_t motion_mode;       /* SIMPLE_TRANSLATION / OBMC_CAUSAL / LOCALWARP        */
+    uint8_t compound_type;     /* COMPOUND_WEDGE .. COMPOUND_DISTANCE (aom/enums.h:474) */
+    uint8_t interintra_mode;   /* II_*                                               */
+    uint8_t wedge_index, wedge_sign;
+    uint8_t mask_type;
+    uint8_t ii_edge;           /* interintra block-level haveAboveRight(bit 2p) / haveBelowLeft(bit 2p+1) */
+    uint32_t flags;            /* AV1R_BLK_*                                          */
+    uint16_t max_luma_w, max_luma_h; /* MaxLumaW/H at chroma time (TransformBlock.cpp:2418-2421) */
+    int32_t local_warp[6];     /* LocalWarpParams (Block.cpp:1116-1169) when AV1R_BLK_LOCAL_VALID */
+    uint32_t palette_off;      /* byte offset of this block's av1r_palette record     */
+    uint32_t first_tb, n_tbs;  /* this block's transform blocks in the tb array       */
+} av1r_block;
+#define AV1R_BLK_INTER (1u << 0)
+#define AV1R_BLK_INTRABC (1u << 1)
+#define AV1R_BLK_LOSSLESS (1u << 2)
+#define AV1R_BLK_HAS_CHROMA (1u << 3)
+#define AV1R_BLK_FILTER_INTRA (1u << 4)
+#define AV1R_BLK_INTERINTRA (1u << 5)
+#define AV1R_BLK_WEDGE_II (1u << 6)
+#define AV1R_BLK_LOCAL_VALID (1u << 7)
+#define AV1R_BLK_AVAIL_L (1u << 8)
+#define AV1R_BLK_AVAIL_U (1u << 9)
+#define AV1R_BLK_AVAIL_L_UV (1u << 10)
+#define AV1R_BLK_AVAIL_U_UV (1u << 11)
+#define AV1R_BLK_SMOOTH_A_Y (1u << 12) /* getAboveSmooth() luma  (IntraPredict.cpp:232) */
+#define AV1R_BLK_SMOOTH_L_Y (1u << 13) /* getLeftSmooth()  luma  (IntraPredict.cpp:214) */
+#define AV1R_BLK_SMOOTH_A_UV (1u << 14)
+#define AV1R_BLK_SMOOTH_L_UV (1u << 15)
+#define AV1R_BLK_SKIP (1u << 16)
+
+/* ---- transform block (TransformBlock, decoder/TransformBlock.h:46-129). 20 bytes. ---- */
+typedef struct av1r_tb {
+    uint32_t block;     /* index of the owning av1r_block                              */
+    uint32_t coef_off;  /* first coefficient in the coefficient stream                 */
+    uint16_t x, y;      /* top-left in plane pixels (startX/startY)                    */
+    uint16_t coef_cnt;  /* number of non-zero coefficients (0 <=> eob == 0)            */
+    uint8_t plane;
+    uint8_t tx_size;    /* TX_SIZE                                                     */
+    uint8_t tx_type;    /* PlaneTxType (TX_TYPE), flips implied (TransformBlock.cpp:1658-1675) */
+    uint8_t flags;      /* AV1R_TB_*                                                   */
+    uint8_t pad[2];
+} av1r_tb;
+#define AV1R_TB_HAVE_LEFT 1u   /* predict_intra haveLeft  (TransformBlock.cpp:2411)   */
+#define AV1R_TB_HAVE_ABOVE 2u  /* predict_intra haveAbove (TransformBlock.cpp:2412)   */
+#define AV1R_TB_HAVE_AR 4u     /* haveAboveRight          (TransformBlock.cpp:2406)   */
+#define AV1R_TB_HAVE_BL 8u     /* haveBelowLeft           (TransformBlock.cpp:2407)   */
+
+/* Coefficient stream: one uint32 per non-zero quantized coefficient of a TB,
+ * (level << 10) | pos, pos = i * min(w,32) + j (Quant[] layout, TransformBlock.cpp:2266),
+ * level = signed Quant value (|level| < 2^21). */
+#define AV1R_COEF_POS(c) ((int)((c) & 1023u))
+#define AV1R_COEF_LEVEL(c) (((int32_t)(c)) >> 10)
+
+/* Palette record, at av1r_block.palette_off in the palette blob:
+ *   uint8 wy, hy, wuv, huv; uint8 colors[3][8];  uint8 map_y[hy*wy]; uint8 map_uv[huv*wuv]
+ * (Block::Palette, Block.cpp:2221-2298; maps already border-extended). */
+#define AV1R_PALETTE_HDR 28
+
+/* ---- loop restoration unit (LrType/LrWiener/LrSgrSet/LrSgrXqd, Parser.h:384-402). 12 B ---- */
+typedef struct av1r_lr_unit {
+    uint8_t type;       /* RESTORE_NONE / RESTORE_WIENER / RESTORE_SGRPROJ          */
+    uint8_t sgr_set;
+    int8_t sgr_xqd[2];
+    int8_t wiener[2][3]; /* [0] vertical, [1] horizontal (LoopRestoration.cpp:250-251) */
+    uint8_t pad[2];
+} av1r_lr_unit;
+
+/* ---- frame header: what reconstruction and the filters read from FrameHeader /
+ *      SequenceHeader (decoder/Parser.h:258-640). ---- */
+typedef struct av1r_frame_hdr {
+    uint32_t version;            /* AV1R_VERSION                                    */
+    int32_t frame_width, frame_height; /* FrameWidth / FrameHeight (no superres)    */
+    int32_t mi_cols, mi_rows;    /* MiCols / MiRows                                 */
+    int32_t mi_stride, mi_rows_alloc; /* AlignedMiCols / AlignedMiRows (mi grid dims) */
+    uint8_t sb128, subx, suby, bitdepth;
+    uint8_t show_frame, show_existing_frame, frame_to_show, refresh_frame_flags;
+    uint8_t frame_type, enable_intra_edge_filter, force_integer_mv, allow_intrabc;
+    int8_t ref_frame_idx[8];     /* ref_frame_idx[ref - LAST_FRAME] (7 used)         */
+    uint8_t gm_type[8];          /* GmType[ref]                                     */
+    int32_t gm_params[8][6];     /* gm_params[ref][]                                */
+    uint8_t ref_dist[8];         /* Clip3(0, MAX_FRAME_DISTANCE, |get_relative_dist(ref)|) */
+    int8_t delta_q_y_dc, delta_q_u_dc, delta_q_u_ac, delta_q_v_dc, delta_q_v_ac;
+    /* loop filter (LoopFilterParams, DeltaLf) */
+    uint8_t lf_level[4], lf_sharpness, lf_delta_enabled, delta_lf_multi;
+    int8_t lf_ref_deltas[8], lf_mode_deltas[2];
+    /* CDEF (CdefParams) */
+    uint8_t cdef_damping, cdef_bits;
+    uint8_t cdef_y_pri[8], cdef_y_sec[8], cdef_uv_pri[8], cdef_uv_sec[8];
+    int32_t cdef_rows, cdef_cols;  /* cdef_idx grid dims (64x64 units)               */
+    /* loop restoration */
+    uint8_t uses_lr, lr_type[3];   /* UsesLr, FrameRestorationType[]                 */
+    int32_t lr_unit_size[3];
+    int32_t lr_unit_rows[3], lr_unit_cols[3];
+    int32_t lr_unit_off[3];        /* first unit of each plane in the lr unit array  */
+    uint8_t reserved[16];
+} av1r_frame_hdr;
+
+/* ---- one frame's (or one tile's) payload ---- */
+typedef struct av1r_frame_batch {
+    const av1r_frame_hdr* hdr;
+    const av1r_mi* mi;             /* mi_rows_alloc * mi_stride records               */
+    const av1r_block* blocks;
+    uint32_t n_blocks;
+    const av1r_tb* tbs;
+    uint32_t n_tbs;
+    const uint32_t* coefs;
+    uint32_t n_coefs;
+    const uint8_t* palette;
+    uint32_t n_palette;            /* bytes                                           */
+    const int8_t* cdef_idx;        /* cdef_rows * cdef_cols, -1 = off                 */
+    const av1r_lr_unit* lr_units;
+    uint32_t n_lr_units;
+} av1r_frame_batch;
+
+typedef struct av1r_ctx av1r_ctx;
+
+/* Stage ids for av1r_read_stage. */
+#define AV1R_STAGE_RECON 0
+#define AV1R_STAGE_LF 1
+#define AV1R_STAGE_CDEF 2
+#define AV1R_STAGE_LR 3
+
+/* Create a decoding context bound to HIP device `device` and its own HIP stream. */
+int av1r_create(int device, av1r_ctx** out);
+void av1r_destroy(av1r_ctx* ctx);
+
+/* Decode (reconstruct + filter) one frame and update the reference store. */
+int av1r_decode_frame(av1r_ctx* ctx, const av1r_frame_batch* batch);
+
+/* Split form of av1r_decode_frame: header-level data first, then each tile's blocks
+ * (blocks/tbs/coefs/palette fields of the batch; block indices and offsets are local to
+ * the tile), then frame_end runs recon -> LF -> CDEF -> LR. */
+int av1r_frame_begin(av1r_ctx* ctx, const av1r_frame_batch* frame_level);
+int av1r_submit_tile(av1r_ctx* ctx, const av1r_frame_batch* tile);
+int av1r_frame_end(av1r_ctx* ctx);
+
+/* show_existing_frame: queue slot `slot` for output and refresh per `refresh_flags`. */
+int av1r_show_existing(av1r_ctx* ctx, int slot, int refresh_flags);
+
+/* Output queue.  av1r_get_output copies the oldest queued frame's visible I420 planes
+ * (width x height, (width>>1) x (height>>1)) into the caller's buffers and pops it. */
+int av1r_output_pending(av1r_ctx* ctx);
+int av1r_get_output(av1r_ctx* ctx, uint8_t* y, int y_stride, uint8_t* u, int u_stride,
+                    uint8_t* v, int v_stride, int* width, int* height);
+
+/* Copy the visible region of plane `plane` of stage `stage` of the last decoded frame. */
+int av1r_read_stage(av1r_ctx* ctx, int stage, int plane, uint8_t* dst, int dst_stride);
+
+/* Timing / profiling helpers (bench). */
+int av1r_synchronize(av1r_ctx* ctx);
+/* Average device time (ms) of the last frame's kernels, by class; filled by the bench. */
+int av1r_last_frame_times(av1r_ctx* ctx, float* recon_ms, float* lf_ms, float* cdef_ms,
+                          float* lr_ms);
+int av1r_set_timing(av1r_ctx* ctx, int enable);
+const char* av1r_last_error(av1r_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
