@@ -136,13 +136,13 @@ struct Dumper {
             f |= AV1R_BLK_INTER;
             r.motion_mode = b.motion_mode;
             r.compound_type = b.compound_type;
-            r.interintra_mode = b.interintra ? b.interintra_mode : 0;
+            r.interintra_mode = (b.interintra && !b.use_intrabc) ? b.interintra_mode : 0;
             r.wedge_index = b.wedge_index;
             r.wedge_sign = b.wedge_sign;
             r.mask_type = b.mask_type;
-            if (b.interintra)
+            if (b.interintra && !b.use_intrabc)
                 f |= AV1R_BLK_INTERINTRA;
-            if (b.interintra && b.wedge_interintra)
+            if (b.interintra && !b.use_intrabc && b.wedge_interintra)
                 f |= AV1R_BLK_WEDGE_II;
         }
         if (b.use_intrabc)
@@ -460,6 +460,21 @@ struct Dumper {
         dec.frame_end_update_cdf(tiles);
         fillFrameTables(h);
         std::string hRecon = md5_planes(*frame);
+        if (const char* dir = getenv("REFDUMP_PLANES")) {
+            // debug aid: raw visible planes of each stage, <dir>/f<N>_<stage>.yuv
+            auto dump = [&](const YuvFrame& f, const char* tag) {
+                char path[512];
+                snprintf(path, sizeof(path), "%s/f%d_%s.yuv", dir, frameNo, tag);
+                FILE* fp = fopen(path, "wb");
+                for (int p = 0; p < 3; p++) {
+                    int w = p ? f.width >> 1 : f.width, hh = p ? f.height >> 1 : f.height;
+                    for (int y = 0; y < hh; y++)
+                        fwrite(f.data[p] + y * f.strides[p], 1, w, fp);
+                }
+                fclose(fp);
+            };
+            dump(*frame, "recon");
+        }
         LoopFilter lf(dec.m_frame);
         lf.filter(frame);
         std::string hLf = md5_planes(*frame);
