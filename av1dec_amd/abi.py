@@ -66,3 +66,27 @@ SIZEOF_MI = 24
 SIZEOF_BLOCK = 68
 SIZEOF_TB = 20
 SIZEOF_LR_UNIT = 12
+
+
+# numpy record dtypes of the array structs (layouts of include/av1r.h)
+import numpy as _np  # noqa: E402
+
+MI_DTYPE = _np.dtype([
+    ("mv", "<i2", (2, 2)), ("ref_frame", "i1", (2,)), ("mi_size", "u1"), ("y_mode", "u1"),
+    ("filt", "u1"), ("flags", "u1"), ("lf_tx", "u1", (3,)), ("delta_lf", "i1", (4,)),
+    ("uv_mode", "u1"), ("pad", "u1", (2,))])
+BLOCK_DTYPE = _np.dtype([
+    ("mi_row", "<u2"), ("mi_col", "<u2"), ("mi_size", "u1"), ("qindex", "u1"), ("y_mode", "u1"),
+    ("uv_mode", "u1"), ("angle_delta_y", "i1"), ("angle_delta_uv", "i1"), ("filter_intra_mode", "u1"),
+    ("cfl_alpha_u", "i1"), ("cfl_alpha_v", "i1"), ("palette_size_y", "u1"), ("palette_size_uv", "u1"),
+    ("motion_mode", "u1"), ("compound_type", "u1"), ("interintra_mode", "u1"), ("wedge_index", "u1"),
+    ("wedge_sign", "u1"), ("mask_type", "u1"), ("ii_edge", "u1"), ("pad0", "u1", (2,)), ("flags", "<u4"),
+    ("max_luma_w", "<u2"), ("max_luma_h", "<u2"), ("local_warp", "<i4", (6,)), ("palette_off", "<u4"),
+    ("first_tb", "<u4"), ("n_tbs", "<u4")])
+TB_DTYPE = _np.dtype([
+    ("block", "<u4"), ("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("coef_cnt", "<u2"),
+    ("plane", "u1"), ("tx_size", "u1"), ("tx_type", "u1"), ("flags", "u1"), ("pad", "u1", (2,))])
+LR_DTYPE = _np.dtype([
+    ("type", "u1"), ("sgr_set", "u1"), ("sgr_xqd", "i1", (2,)), ("wiener", "i1", (2, 3)), ("pad", "u1", (2,))])
+assert MI_DTYPE.itemsize == SIZEOF_MI and BLOCK_DTYPE.itemsize == SIZEOF_BLOCK
+assert TB_DTYPE.itemsize == SIZEOF_TB and LR_DTYPE.itemsize == SIZEOF_LR_UNIT

@@ -1,0 +1,57 @@
+// av1r_dev.h -- shared device-side definitions of the gfx950 reconstruction backend.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "av1r.h"
+#include "av1r_consts.h"
+
+#define DEV __device__ __forceinline__
+
+// One plane of a device frame.  Frames are SB-aligned + 64 px margin, origin at (0,0);
+// w/h are the VISIBLE plane dims (YuvFrame::widths/heights, VideoFrame.cpp:49-51).
+struct DevPlane {
+    uint8_t* p;
+    int stride;
+    int w, h;
+};
+struct DevFrame {
+    DevPlane pl[3];
+    int width, height;  // FrameWidth / FrameHeight of the frame stored here
+};
+
+// Kernel arguments for every stage (passed by value).
+struct KParams {
+    const av1r_frame_hdr* hdr;
+    const av1r_mi* mi;
+    const av1r_block* blocks;
+    const av1r_tb* tbs;
+    const uint32_t* coefs;
+    const uint8_t* palette;
+    const int8_t* cdef_idx;
+    const av1r_lr_unit* lr;
+    const uint32_t* items;  // work list of this launch
+    uint32_t n_items;
+    int mi_stride;
+    int mi_cols, mi_rows;
+    int frame_w, frame_h;
+    DevFrame cur;     // frame under reconstruction / filter input
+    DevFrame out;     // filter output
+    DevFrame ref[8];  // reference store slots
+};
+
+#define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
+DEV int clip1(int v) { return CLIP3(0, 255, v); }
+DEV int r2(int x, int n) { return n == 0 ? x : ((x + (1 << (n - 1))) >> n); }
+DEV int r2s(int x, int n) { return x >= 0 ? r2(x, n) : -r2(-x, n); }
+DEV int64_t r2_64(int64_t x, int n) { return n == 0 ? x : ((x + ((int64_t)1 << (n - 1))) >> n); }
+DEV int64_t r2s_64(int64_t x, int n) { return x >= 0 ? r2_64(x, n) : -r2_64(-x, n); }
+DEV int iabs(int v) { return v < 0 ? -v : v; }
+DEV int imin(int a, int b) { return a < b ? a : b; }
+DEV int imax(int a, int b) { return a > b ? a : b; }
+DEV int floor_log2_u64(uint64_t x) { return x ? 63 - __builtin_clzll(x) : -1; }
+DEV int floor_log2(int x) { return x > 0 ? 31 - __builtin_clz((unsigned)x) : -1; }
+
+DEV const av1r_mi& mi_at(const KParams& k, int row, int col) { return k.mi[(size_t)row * k.mi_stride + col]; }
+DEV int plane_bsize(int bs, int plane) { return plane ? av1r_ss420[bs] : bs; }
+DEV uint8_t& px(const DevPlane& p, int x, int y) { return p.p[(size_t)y * p.stride + x]; }

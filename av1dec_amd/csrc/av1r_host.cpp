@@ -1,0 +1,738 @@
+// av1r_host.cpp -- host runtime of the gfx950 reconstruction backend and its C-ABI.
+//
+// Replaces, below the parse/reconstruct seam, the reference decoder's
+// Decoder::decodeFrame / decode_frame_wrapup / updateFrameStore / getOutput
+// (decoder/Av1Decoder.cpp:111-211).  Per frame it
+//   1. validates the batch (every index a kernel will follow is range-checked here),
+//   2. derives the dependency schedule: each inter block's prediction and each
+//      transform block becomes a work item whose level is 1 + the highest level of
+//      the items that produced the pixels it reads (intra edges, CFL luma, inter-intra
+//      edges, intra-block-copy source) -- the decode-order dependencies of
+//      TransformBlock::decode / IntraPredict::predict_intra made explicit,
+//   3. uploads batch + schedule with ONE async copy from pinned memory,
+//   4. launches per level {k_inter, k_tb}, then k_lf (2 passes), k_cdef, k_lr on the
+//      context's HIP stream, and updates the 8-slot device frame store.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "av1r_dev.h"
+
+void launch_k_tb(const KParams& k, unsigned n, hipStream_t s);
+void launch_k_inter(const KParams& k, unsigned n, hipStream_t s);
+void launch_k_lf(const KParams& k, int pass, int nY, int nC, int cCols, int planeMask, hipStream_t s);
+void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s);
+void launch_k_lr(const KParams& k, int plane, hipStream_t s);
+void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
+
+namespace {
+
+struct FrameBuf {
+    uint8_t* base = nullptr;
+    size_t bytes = 0;
+    int refcnt = 0;
+    DevFrame d;
+};
+
+struct Upload {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;  // all work that reads this upload has finished
+    bool pending = false;
+};
+
+struct Level {
+    uint32_t pOff = 0, pCnt = 0, tOff = 0, tCnt = 0;
+};
+
+inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct av1r_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<FrameBuf*> pool;
+    FrameBuf* slots[8] = {};
+    std::deque<FrameBuf*> outq;
+    FrameBuf* stage[4] = {};
+    bool keepStages = true;
+    Upload up[2];
+    int upIdx = 0;
+    std::string err;
+    // schedule scratch
+    std::vector<int16_t> lvlmap[3];
+    int mapW[3] = {}, mapH[3] = {};
+    std::vector<std::vector<uint32_t>> lvP, lvT;
+    std::vector<uint32_t> items;
+    std::vector<Level> levels;
+    // split submission (frame_begin / submit_tile / frame_end)
+    bool inFrame = false;
+    std::vector<uint8_t> fHdr;
+    std::vector<av1r_mi> fMi;
+    std::vector<int8_t> fCdef;
+    std::vector<av1r_lr_unit> fLr;
+    std::vector<av1r_block> fBlocks;
+    std::vector<av1r_tb> fTbs;
+    std::vector<uint32_t> fCoefs;
+    std::vector<uint8_t> fPal;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[5] = {};
+    int nLevelsLast = 0;
+    // stats of the last frame
+    uint64_t lastUploadBytes = 0;
+};
+
+static int fail(av1r_ctx* c, int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return fail(c, AV1R_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+static void frame_unref(av1r_ctx* c, FrameBuf* f)
+{
+    if (f && f->refcnt > 0) f->refcnt--;
+}
+static void frame_ref(FrameBuf* f)
+{
+    if (f) f->refcnt++;
+}
+
+static FrameBuf* frame_get(av1r_ctx* c, int width, int height)
+{
+    int aw = ((width + 127) & ~127) + 64, ah = ((height + 127) & ~127) + 64;
+    int strideY = (int)align256(aw), strideC = (int)align256(aw / 2);
+    size_t ySz = (size_t)strideY * ah, cSz = (size_t)strideC * (ah / 2);
+    size_t need = align256(ySz) + 2 * align256(cSz);
+    FrameBuf* f = nullptr;
+    for (FrameBuf* p : c->pool)
+        if (p->refcnt == 0 && p->bytes >= need) {
+            f = p;
+            break;
+        }
+    if (!f) {
+        f = new FrameBuf;
+        if (hipMalloc(&f->base, need) != hipSuccess) {
+            delete f;
+            return nullptr;
+        }
+        (void)hipMemsetAsync(f->base, 0, need, c->stream);
+        f->bytes = need;
+        c->pool.push_back(f);
+    }
+    f->refcnt = 1;
+    f->d.width = width;
+    f->d.height = height;
+    uint8_t* p = f->base;
+    f->d.pl[0] = {p, strideY, width, height};
+    p += align256(ySz);
+    f->d.pl[1] = {p, strideC, width >> 1, height >> 1};
+    p += align256(cSz);
+    f->d.pl[2] = {p, strideC, width >> 1, height >> 1};
+    return f;
+}
+
+// ------------------------------------------------------------------------------------
+// batch validation: everything a kernel dereferences is checked here
+// ------------------------------------------------------------------------------------
+static int validate(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    const av1r_frame_hdr* h = b->hdr;
+    if (h->bitdepth != 8 || h->subx != 1 || h->suby != 1)
+        return fail(c, AV1R_E_UNSUPPORTED, "only 8-bit 4:2:0 is supported (reference README)");
+    if ((h->frame_width & 1) || (h->frame_height & 1) || h->frame_width <= 0 || h->frame_height <= 0 || h->frame_width > 16384 || h->frame_height > 16384)
+        return fail(c, AV1R_E_UNSUPPORTED, "frame size %dx%d not supported", h->frame_width, h->frame_height);
+    if (h->mi_cols != 2 * ((h->frame_width + 7) >> 3) || h->mi_rows != 2 * ((h->frame_height + 7) >> 3))
+        return fail(c, AV1R_E_INVALID, "MiCols/MiRows inconsistent with the frame size");
+    int sb4 = h->sb128 ? 32 : 16;
+    if (h->mi_stride < ((h->mi_cols + sb4 - 1) / sb4) * sb4 || h->mi_rows_alloc < ((h->mi_rows + sb4 - 1) / sb4) * sb4)
+        return fail(c, AV1R_E_INVALID, "mode-info grid smaller than the SB-aligned frame");
+    if (!b->mi || !b->cdef_idx) return fail(c, AV1R_E_INVALID, "missing mode-info or cdef grid");
+    if (h->cdef_rows != (h->mi_rows + 15) / 16 || h->cdef_cols != (h->mi_cols + 15) / 16)
+        return fail(c, AV1R_E_INVALID, "cdef grid dims");
+    for (int i = 0; i < h->cdef_rows * h->cdef_cols; i++)
+        if (b->cdef_idx[i] < -1 || b->cdef_idx[i] > 7) return fail(c, AV1R_E_INVALID, "cdef_idx out of range");
+    const int aw4 = h->mi_stride, ah4 = h->mi_rows_alloc;
+    // mode info: sizes, tx sizes, refs (and the slots they resolve to)
+    bool usedRef[8] = {};
+    for (int i = 0; i < aw4 * ah4; i++) {
+        const av1r_mi& m = b->mi[i];
+        if (m.mi_size >= AV1R_BLOCK_SIZES) return fail(c, AV1R_E_INVALID, "mi_size");
+        for (int p = 0; p < 3; p++)
+            if (m.lf_tx[p] >= AV1R_TX_SIZES) return fail(c, AV1R_E_INVALID, "lf tx size");
+        for (int l = 0; l < 2; l++) {
+            if (m.ref_frame[l] < -1 || m.ref_frame[l] > 7) return fail(c, AV1R_E_INVALID, "ref_frame");
+            if (m.ref_frame[l] > 0) usedRef[m.ref_frame[l]] = true;
+        }
+        if ((m.filt & 15) > 3 || (m.filt >> 4) > 3) return fail(c, AV1R_E_INVALID, "interp filter");
+    }
+    for (int r = 1; r < 8; r++) {
+        if (!usedRef[r]) continue;
+        int slot = h->ref_frame_idx[r - 1];
+        if (slot < 0 || slot > 7 || !c->slots[slot])
+            return fail(c, AV1R_E_INVALID, "reference %d maps to an empty slot", r);
+    }
+    for (uint32_t i = 0; i < b->n_blocks; i++) {
+        const av1r_block& k = b->blocks[i];
+        if (k.mi_size >= AV1R_BLOCK_SIZES || k.mi_row >= ah4 || k.mi_col >= aw4
+            || k.mi_row + av1r_num4x4h[k.mi_size] > ah4 || k.mi_col + av1r_num4x4w[k.mi_size] > aw4)
+            return fail(c, AV1R_E_INVALID, "block %u geometry", i);
+        if ((uint64_t)k.first_tb + k.n_tbs > b->n_tbs) return fail(c, AV1R_E_INVALID, "block %u tb range", i);
+        if (k.palette_size_y > 8 || k.palette_size_uv > 8) return fail(c, AV1R_E_INVALID, "palette size");
+        if (k.palette_size_y || k.palette_size_uv) {
+            if ((uint64_t)k.palette_off + AV1R_PALETTE_HDR > b->n_palette) return fail(c, AV1R_E_INVALID, "palette offset");
+            const uint8_t* ph = b->palette + k.palette_off;
+            if ((uint64_t)k.palette_off + AV1R_PALETTE_HDR + ph[0] * ph[1] + ph[2] * ph[3] > b->n_palette)
+                return fail(c, AV1R_E_INVALID, "palette map size");
+        }
+        if (k.flags & AV1R_BLK_INTER) {
+            if (k.motion_mode > 2 || k.compound_type > 4 || k.interintra_mode > 3 || k.wedge_index > 15)
+                return fail(c, AV1R_E_INVALID, "block %u inter params", i);
+            if (k.compound_type == AV1R_COMPOUND_WEDGE && !av1r_wedge_bits[k.mi_size])
+                return fail(c, AV1R_E_INVALID, "wedge on a block size without wedges");
+            if (k.flags & AV1R_BLK_INTERINTRA)
+                if (k.mi_size < AV1R_BLOCK_8X8 || k.mi_size > AV1R_BLOCK_32X32) return fail(c, AV1R_E_INVALID, "interintra size");
+        } else {
+            if (k.y_mode > AV1R_PAETH_PRED || k.uv_mode > AV1R_UV_CFL_PRED || k.filter_intra_mode > 4)
+                return fail(c, AV1R_E_INVALID, "block %u intra modes", i);
+        }
+    }
+    for (uint32_t i = 0; i < b->n_tbs; i++) {
+        const av1r_tb& t = b->tbs[i];
+        if (t.block >= b->n_blocks || t.plane > 2 || t.tx_size >= AV1R_TX_SIZES || t.tx_type > 15)
+            return fail(c, AV1R_E_INVALID, "tb %u fields", i);
+        int sub = t.plane ? 1 : 0;
+        if (t.x + av1r_tx_w[t.tx_size] > ((aw4 * 4) >> sub) + 64 || t.y + av1r_tx_h[t.tx_size] > ((ah4 * 4) >> sub) + 64)
+            return fail(c, AV1R_E_INVALID, "tb %u outside the frame", i);
+        if ((uint64_t)t.coef_off + t.coef_cnt > b->n_coefs) return fail(c, AV1R_E_INVALID, "tb %u coefficients", i);
+        int tw = std::min<int>(av1r_tx_w[t.tx_size], 32), th = std::min<int>(av1r_tx_h[t.tx_size], 32);
+        for (int q = 0; q < t.coef_cnt; q++)
+            if (AV1R_COEF_POS(b->coefs[t.coef_off + q]) >= tw * th) return fail(c, AV1R_E_INVALID, "tb %u coefficient position", i);
+        const av1r_block& k = b->blocks[t.block];
+        if (!(k.flags & AV1R_BLK_INTER) && (t.plane ? k.palette_size_uv : k.palette_size_y)) {
+            const uint8_t* ph = b->palette + k.palette_off;
+            int bx = t.x - (k.mi_col >> sub) * 4, by = t.y - (k.mi_row >> sub) * 4;
+            int mw = t.plane ? ph[2] : ph[0], mh = t.plane ? ph[3] : ph[1];
+            if (bx < 0 || by < 0 || bx + av1r_tx_w[t.tx_size] > mw || by + av1r_tx_h[t.tx_size] > mh)
+                return fail(c, AV1R_E_INVALID, "tb %u palette map window", i);
+        }
+    }
+    if (h->uses_lr) {
+        for (int p = 0; p < 3; p++) {
+            if (h->lr_type[p] == AV1R_RESTORE_NONE) continue;
+            int us = h->lr_unit_size[p];
+            if (us != 32 && us != 64 && us != 128 && us != 256) return fail(c, AV1R_E_INVALID, "lr unit size");
+            if ((int64_t)h->lr_unit_off[p] + (int64_t)h->lr_unit_rows[p] * h->lr_unit_cols[p] > b->n_lr_units || h->lr_unit_rows[p] < 1 || h->lr_unit_cols[p] < 1)
+                return fail(c, AV1R_E_INVALID, "lr units");
+            for (int u = 0; u < h->lr_unit_rows[p] * h->lr_unit_cols[p]; u++)
+                if (b->lr_units[h->lr_unit_off[p] + u].sgr_set > 15 || b->lr_units[h->lr_unit_off[p] + u].type > 2)
+                    return fail(c, AV1R_E_INVALID, "lr unit params");
+        }
+    }
+    return AV1R_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// dependency levels
+// ------------------------------------------------------------------------------------
+static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    const av1r_frame_hdr* h = b->hdr;
+    for (int p = 0; p < 3; p++) {
+        int sub = p ? 1 : 0;
+        c->mapW[p] = (((h->mi_stride * 4) >> sub) + 64) / 4;
+        c->mapH[p] = (((h->mi_rows_alloc * 4) >> sub) + 64) / 4;
+        c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
+    }
+    c->lvP.clear();
+    c->lvT.clear();
+    auto region_max = [&](int p, int x0, int y0, int x1, int y1) {  // inclusive unit rect
+        x0 = std::max(x0, 0);
+        y0 = std::max(y0, 0);
+        x1 = std::min(x1, c->mapW[p] - 1);
+        y1 = std::min(y1, c->mapH[p] - 1);
+        int m = -1;
+        for (int y = y0; y <= y1; y++) {
+            const int16_t* row = &c->lvlmap[p][(size_t)y * c->mapW[p]];
+            for (int x = x0; x <= x1; x++) m = std::max<int>(m, row[x]);
+        }
+        return m;
+    };
+    auto region_set = [&](int p, int x0, int y0, int w4, int h4, int lv) {
+        int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
+        for (int y = y0; y < y1; y++) {
+            int16_t* row = &c->lvlmap[p][(size_t)y * c->mapW[p]];
+            for (int x = x0; x < x1; x++) row[x] = (int16_t)lv;
+        }
+    };
+    auto push = [&](std::vector<std::vector<uint32_t>>& v, int lv, uint32_t id) {
+        if ((int)v.size() <= lv) v.resize(lv + 1);
+        v[lv].push_back(id);
+    };
+    int globalMax = -1;
+    for (uint32_t bi = 0; bi < b->n_blocks; bi++) {
+        const av1r_block& blk = b->blocks[bi];
+        const bool inter = blk.flags & AV1R_BLK_INTER;
+        const int nPlanes = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
+        int pLevel = -1;
+        if (inter) {
+            const bool isII = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col].ref_frame[1] == AV1R_INTRA_FRAME;
+            int dep = -1;
+            if (blk.flags & AV1R_BLK_INTRABC) {
+                dep = globalMax;  // reads already-decoded pixels of the current frame
+            } else if (isII) {
+                for (int p = 0; p < nPlanes; p++) {
+                    int sub = p ? 1 : 0;
+                    int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
+                    int x4 = (blk.mi_col >> sub), y4 = (blk.mi_row >> sub);
+                    int w4 = av1r_num4x4w[psz], h4 = av1r_num4x4h[psz];
+                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 + 2 * w4 - 1, y4 - 1));
+                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 - 1, y4 + 2 * h4 - 1));
+                }
+            }
+            pLevel = dep + 1;
+            push(c->lvP, pLevel, bi);
+            globalMax = std::max(globalMax, pLevel);
+            for (int p = 0; p < nPlanes; p++) {
+                int sub = p ? 1 : 0;
+                int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
+                region_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], pLevel);
+            }
+        }
+        int lumaMax = -1;  // CFL reads this block's reconstructed luma
+        for (uint32_t ti = blk.first_tb; ti < blk.first_tb + blk.n_tbs; ti++) {
+            const av1r_tb& t = b->tbs[ti];
+            const int p = t.plane;
+            const int x4 = t.x >> 2, y4 = t.y >> 2;
+            const int w4 = av1r_tx_w[t.tx_size] >> 2, h4 = av1r_tx_h[t.tx_size] >> 2;
+            int lv;
+            if (inter) {
+                if (!t.coef_cnt) continue;  // prediction only: nothing to add
+                lv = pLevel + 1;
+            } else {
+                const bool pal = p ? blk.palette_size_uv : blk.palette_size_y;
+                int dep = -1;
+                if (!pal) {
+                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 + 2 * w4 - 1, y4 - 1));
+                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 - 1, y4 + 2 * h4 - 1));
+                    if (p && blk.uv_mode == AV1R_UV_CFL_PRED) dep = std::max(dep, lumaMax);
+                }
+                lv = dep + 1;
+            }
+            if (p == 0) lumaMax = std::max(lumaMax, lv);
+            push(c->lvT, lv, ti);
+            globalMax = std::max(globalMax, lv);
+            region_set(p, x4, y4, w4, h4, lv);
+        }
+    }
+    size_t nl = std::max(c->lvP.size(), c->lvT.size());
+    c->lvP.resize(nl);
+    c->lvT.resize(nl);
+    c->items.clear();
+    c->levels.assign(nl, Level());
+    for (size_t l = 0; l < nl; l++) {
+        c->levels[l].pOff = (uint32_t)c->items.size();
+        c->levels[l].pCnt = (uint32_t)c->lvP[l].size();
+        c->items.insert(c->items.end(), c->lvP[l].begin(), c->lvP[l].end());
+        c->levels[l].tOff = (uint32_t)c->items.size();
+        c->levels[l].tCnt = (uint32_t)c->lvT[l].size();
+        c->items.insert(c->items.end(), c->lvT[l].begin(), c->lvT[l].end());
+    }
+    c->nLevelsLast = (int)nl;
+}
+
+// ------------------------------------------------------------------------------------
+static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    const av1r_frame_hdr* h = b->hdr;
+    int rc = validate(c, b);
+    if (rc) return rc;
+    build_schedule(c, b);
+
+    // ---- one pinned staging buffer -> one H2D copy
+    const size_t szHdr = align256(sizeof(av1r_frame_hdr));
+    const size_t szMi = align256(sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc);
+    const size_t szBlk = align256(sizeof(av1r_block) * (size_t)b->n_blocks);
+    const size_t szTb = align256(sizeof(av1r_tb) * (size_t)b->n_tbs);
+    const size_t szCoef = align256(4 * (size_t)b->n_coefs);
+    const size_t szPal = align256(b->n_palette);
+    const size_t szCdef = align256((size_t)h->cdef_rows * h->cdef_cols);
+    const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
+    const size_t szItems = align256(4 * c->items.size() + 4);
+    const size_t total = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems;
+    Upload& U = c->up[c->upIdx];
+    c->upIdx ^= 1;
+    if (U.pending) {
+        HIPCHK(hipEventSynchronize(U.done));
+        U.pending = false;
+    }
+    if (U.cap < total) {
+        if (U.host) (void)hipHostFree(U.host);
+        if (U.dev) (void)hipFree(U.dev);
+        size_t cap = total + total / 2;
+        HIPCHK(hipHostMalloc(&U.host, cap));
+        HIPCHK(hipMalloc(&U.dev, cap));
+        U.cap = cap;
+    }
+    size_t off = 0;
+    auto put = [&](const void* src, size_t n, size_t sz) {
+        if (n) memcpy(U.host + off, src, n);
+        size_t o = off;
+        off += sz;
+        return U.dev + o;
+    };
+    KParams k;
+    memset(&k, 0, sizeof(k));
+    k.hdr = (const av1r_frame_hdr*)put(h, sizeof(av1r_frame_hdr), szHdr);
+    k.mi = (const av1r_mi*)put(b->mi, sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc, szMi);
+    k.blocks = (const av1r_block*)put(b->blocks, sizeof(av1r_block) * (size_t)b->n_blocks, szBlk);
+    k.tbs = (const av1r_tb*)put(b->tbs, sizeof(av1r_tb) * (size_t)b->n_tbs, szTb);
+    k.coefs = (const uint32_t*)put(b->coefs, 4 * (size_t)b->n_coefs, szCoef);
+    k.palette = put(b->palette, b->n_palette, szPal);
+    k.cdef_idx = (const int8_t*)put(b->cdef_idx, (size_t)h->cdef_rows * h->cdef_cols, szCdef);
+    k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
+    const uint32_t* dItems = (const uint32_t*)put(c->items.data(), 4 * c->items.size(), szItems);
+    c->lastUploadBytes = off;
+    HIPCHK(hipMemcpyAsync(U.dev, U.host, off, hipMemcpyHostToDevice, c->stream));
+    k.mi_stride = h->mi_stride;
+    k.mi_cols = h->mi_cols;
+    k.mi_rows = h->mi_rows;
+    k.frame_w = h->frame_width;
+    k.frame_h = h->frame_height;
+    for (int s = 0; s < 8; s++)
+        if (c->slots[s]) k.ref[s] = c->slots[s]->d;
+
+    FrameBuf* R = frame_get(c, h->frame_width, h->frame_height);
+    if (!R) return fail(c, AV1R_E_NOMEM, "frame allocation");
+    k.cur = R->d;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+
+    // ---- reconstruction, level by level
+    for (const Level& L : c->levels) {
+        if (L.pCnt) {
+            k.items = dItems + L.pOff;
+            k.n_items = L.pCnt;
+            launch_k_inter(k, L.pCnt, c->stream);
+        }
+        if (L.tCnt) {
+            k.items = dItems + L.tOff;
+            k.n_items = L.tCnt;
+            launch_k_tb(k, L.tCnt, c->stream);
+        }
+    }
+    HIPCHK(hipGetLastError());
+    auto snapshot = [&](int st, FrameBuf* src) -> int {
+        FrameBuf* s = frame_get(c, h->frame_width, h->frame_height);
+        if (!s) return fail(c, AV1R_E_NOMEM, "stage allocation");
+        for (int p = 0; p < 3; p++) launch_k_copy_plane(s->d.pl[p], src->d.pl[p], c->stream);
+        frame_unref(c, c->stage[st]);
+        c->stage[st] = s;
+        return AV1R_OK;
+    };
+    if (c->keepStages && (rc = snapshot(AV1R_STAGE_RECON, R))) return rc;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
+
+    // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place
+    if (h->lf_level[0] || h->lf_level[1]) {
+        int planeMask = 1 | (h->lf_level[2] ? 2 : 0) | (h->lf_level[3] ? 4 : 0);
+        int nY = h->mi_rows * h->mi_cols;
+        int cCols = (h->mi_cols + 1) / 2, nC = ((h->mi_rows + 1) / 2) * cCols;
+        launch_k_lf(k, 0, nY, nC, cCols, planeMask, c->stream);
+        launch_k_lf(k, 1, nY, nC, cCols, planeMask, c->stream);
+    }
+    if (c->keepStages && (rc = snapshot(AV1R_STAGE_LF, R))) return rc;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+
+    // ---- CDEF into a new frame (Cdef::filter copies the frame, Cdef.cpp:43)
+    FrameBuf* C = frame_get(c, h->frame_width, h->frame_height);
+    if (!C) return fail(c, AV1R_E_NOMEM, "frame allocation");
+    {
+        KParams kc = k;
+        kc.out = C->d;
+        int bCols = h->mi_cols / 2, nB = (h->mi_rows / 2) * bCols;
+        launch_k_cdef(kc, nB, bCols, c->stream);
+    }
+    if (c->keepStages) {
+        frame_ref(C);
+        frame_unref(c, c->stage[AV1R_STAGE_CDEF]);
+        c->stage[AV1R_STAGE_CDEF] = C;
+    }
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[3], c->stream));
+
+    // ---- loop restoration into a new frame (LoopRestoration::filter, LoopRestoration.cpp:191-219)
+    FrameBuf* out = C;
+    if (h->uses_lr) {
+        FrameBuf* L = frame_get(c, h->frame_width, h->frame_height);
+        if (!L) return fail(c, AV1R_E_NOMEM, "frame allocation");
+        KParams kl = k;
+        kl.cur = C->d;
+        kl.ref[0] = R->d;
+        kl.out = L->d;
+        for (int p = 0; p < 3; p++) launch_k_lr(kl, p, c->stream);
+        out = L;
+        frame_unref(c, C);
+    }
+    if (c->keepStages) {
+        frame_ref(out);
+        frame_unref(c, c->stage[AV1R_STAGE_LR]);
+        c->stage[AV1R_STAGE_LR] = out;
+    }
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(U.done, c->stream));
+    U.pending = true;
+    frame_unref(c, R);
+    if (h->show_frame) {
+        frame_ref(out);
+        c->outq.push_back(out);
+    }
+    for (int i = 0; i < 8; i++)
+        if (h->refresh_frame_flags & (1 << i)) {
+            frame_ref(out);
+            frame_unref(c, c->slots[i]);
+            c->slots[i] = out;
+        }
+    frame_unref(c, out);
+    return AV1R_OK;
+}
+
+// ====================================================================================
+// C-ABI
+// ====================================================================================
+extern "C" {
+
+int av1r_create(int device, av1r_ctx** out)
+{
+    if (!out) return AV1R_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return AV1R_E_DEVICE;
+    av1r_ctx* c = new av1r_ctx;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return AV1R_E_DEVICE;
+    }
+    for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
+    for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
+    *out = c;
+    return AV1R_OK;
+}
+
+void av1r_destroy(av1r_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (FrameBuf* f : c->pool) {
+        (void)hipFree(f->base);
+        delete f;
+    }
+    for (auto& u : c->up) {
+        if (u.host) (void)hipHostFree(u.host);
+        if (u.dev) (void)hipFree(u.dev);
+        (void)hipEventDestroy(u.done);
+    }
+    for (auto& e : c->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int av1r_decode_frame(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    if (!c || !b || !b->hdr) return AV1R_E_INVALID;
+    if (b->hdr->version != AV1R_VERSION) return fail(c, AV1R_E_INVALID, "batch version %u", b->hdr->version);
+    (void)hipSetDevice(c->device);
+    if (b->hdr->show_existing_frame) return av1r_show_existing(c, b->hdr->frame_to_show, b->hdr->refresh_frame_flags);
+    return run_frame(c, b);
+}
+
+int av1r_frame_begin(av1r_ctx* c, const av1r_frame_batch* f)
+{
+    if (!c || !f || !f->hdr || !f->mi || !f->cdef_idx) return AV1R_E_INVALID;
+    const av1r_frame_hdr* h = f->hdr;
+    c->fHdr.assign((const uint8_t*)h, (const uint8_t*)h + sizeof(*h));
+    c->fMi.assign(f->mi, f->mi + (size_t)h->mi_stride * h->mi_rows_alloc);
+    c->fCdef.assign(f->cdef_idx, f->cdef_idx + (size_t)h->cdef_rows * h->cdef_cols);
+    c->fLr.assign(f->lr_units, f->lr_units + f->n_lr_units);
+    c->fBlocks.clear();
+    c->fTbs.clear();
+    c->fCoefs.clear();
+    c->fPal.clear();
+    c->inFrame = true;
+    return AV1R_OK;
+}
+
+int av1r_submit_tile(av1r_ctx* c, const av1r_frame_batch* t)
+{
+    if (!c || !t || !c->inFrame) return AV1R_E_INVALID;
+    uint32_t bBase = (uint32_t)c->fBlocks.size(), tBase = (uint32_t)c->fTbs.size();
+    uint32_t cBase = (uint32_t)c->fCoefs.size(), pBase = (uint32_t)c->fPal.size();
+    for (uint32_t i = 0; i < t->n_blocks; i++) {
+        av1r_block b = t->blocks[i];
+        b.first_tb += tBase;
+        b.palette_off += pBase;
+        c->fBlocks.push_back(b);
+    }
+    for (uint32_t i = 0; i < t->n_tbs; i++) {
+        av1r_tb x = t->tbs[i];
+        x.block += bBase;
+        x.coef_off += cBase;
+        c->fTbs.push_back(x);
+    }
+    c->fCoefs.insert(c->fCoefs.end(), t->coefs, t->coefs + t->n_coefs);
+    c->fPal.insert(c->fPal.end(), t->palette, t->palette + t->n_palette);
+    return AV1R_OK;
+}
+
+int av1r_frame_end(av1r_ctx* c)
+{
+    if (!c || !c->inFrame) return AV1R_E_INVALID;
+    c->inFrame = false;
+    av1r_frame_batch b;
+    memset(&b, 0, sizeof(b));
+    b.hdr = (const av1r_frame_hdr*)c->fHdr.data();
+    b.mi = c->fMi.data();
+    b.blocks = c->fBlocks.data();
+    b.n_blocks = (uint32_t)c->fBlocks.size();
+    b.tbs = c->fTbs.data();
+    b.n_tbs = (uint32_t)c->fTbs.size();
+    b.coefs = c->fCoefs.data();
+    b.n_coefs = (uint32_t)c->fCoefs.size();
+    b.palette = c->fPal.data();
+    b.n_palette = (uint32_t)c->fPal.size();
+    b.cdef_idx = c->fCdef.data();
+    b.lr_units = c->fLr.data();
+    b.n_lr_units = (uint32_t)c->fLr.size();
+    return av1r_decode_frame(c, &b);
+}
+
+int av1r_show_existing(av1r_ctx* c, int slot, int refresh)
+{
+    if (!c || slot < 0 || slot > 7 || !c->slots[slot]) return AV1R_E_INVALID;
+    FrameBuf* f = c->slots[slot];
+    frame_ref(f);  // hold across the refresh
+    frame_ref(f);
+    c->outq.push_back(f);
+    for (int i = 0; i < 8; i++)
+        if (refresh & (1 << i)) {
+            frame_ref(f);
+            frame_unref(c, c->slots[i]);
+            c->slots[i] = f;
+        }
+    frame_unref(c, f);
+    return AV1R_OK;
+}
+
+int av1r_output_pending(av1r_ctx* c) { return c ? (int)c->outq.size() : 0; }
+
+static int copy_plane_d2h(av1r_ctx* c, const DevPlane& p, uint8_t* dst, int ds)
+{
+    HIPCHK(hipMemcpy2DAsync(dst, ds, p.p, p.stride, p.w, p.h, hipMemcpyDeviceToHost, c->stream));
+    return AV1R_OK;
+}
+
+int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height)
+{
+    if (!c) return AV1R_E_INVALID;
+    if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
+    FrameBuf* f = c->outq.front();
+    if (width) *width = f->d.width;
+    if (height) *height = f->d.height;
+    if (!y) return AV1R_OK;
+    (void)hipSetDevice(c->device);
+    int rc;
+    if ((rc = copy_plane_d2h(c, f->d.pl[0], y, ys)) || (rc = copy_plane_d2h(c, f->d.pl[1], u, us)) || (rc = copy_plane_d2h(c, f->d.pl[2], v, vs)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->outq.pop_front();
+    frame_unref(c, f);
+    return AV1R_OK;
+}
+
+int av1r_read_stage(av1r_ctx* c, int stage, int plane, uint8_t* dst, int ds)
+{
+    if (!c || stage < 0 || stage > 3 || plane < 0 || plane > 2 || !c->stage[stage]) return AV1R_E_INVALID;
+    (void)hipSetDevice(c->device);
+    int rc = copy_plane_d2h(c, c->stage[stage]->d.pl[plane], dst, ds);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return AV1R_OK;
+}
+
+int av1r_synchronize(av1r_ctx* c)
+{
+    if (!c) return AV1R_E_INVALID;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return AV1R_OK;
+}
+
+int av1r_set_timing(av1r_ctx* c, int enable)
+{
+    if (!c) return AV1R_E_INVALID;
+    c->timing = enable != 0;
+    return AV1R_OK;
+}
+
+int av1r_set_keep_stages(av1r_ctx* c, int keep)
+{
+    if (!c) return AV1R_E_INVALID;
+    c->keepStages = keep != 0;
+    return AV1R_OK;
+}
+
+int av1r_last_frame_times(av1r_ctx* c, float* recon, float* lf, float* cdef, float* lr)
+{
+    if (!c || !c->timing) return AV1R_E_INVALID;
+    HIPCHK(hipEventSynchronize(c->ev[4]));
+    float t[4] = {};
+    for (int i = 0; i < 4; i++) HIPCHK(hipEventElapsedTime(&t[i], c->ev[i], c->ev[i + 1]));
+    if (recon) *recon = t[0];
+    if (lf) *lf = t[1];
+    if (cdef) *cdef = t[2];
+    if (lr) *lr = t[3];
+    return AV1R_OK;
+}
+
+int av1r_last_frame_stats(av1r_ctx* c, int* levels, uint64_t* uploadBytes)
+{
+    if (!c) return AV1R_E_INVALID;
+    if (levels) *levels = c->nLevelsLast;
+    if (uploadBytes) *uploadBytes = c->lastUploadBytes;
+    return AV1R_OK;
+}
+
+const char* av1r_last_error(av1r_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+size_t av1r_sizeof(int which)
+{
+    switch (which) {
+    case 0: return sizeof(av1r_frame_hdr);
+    case 1: return sizeof(av1r_mi);
+    case 2: return sizeof(av1r_block);
+    case 3: return sizeof(av1r_tb);
+    case 4: return sizeof(av1r_lr_unit);
+    case 5: return sizeof(av1r_frame_batch);
+    default: return 0;
+    }
+}
+
+}  // extern "C"

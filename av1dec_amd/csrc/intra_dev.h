@@ -1,0 +1,312 @@
+// intra_dev.h -- workgroup-cooperative intra prediction for gfx950.
+//
+// Restates Block::IntraPredict (decoder/IntraPredict.cpp:563-667) as a cooperative
+// device routine: the edge arrays (AboveRow/LeftCol) are gathered by all lanes into
+// LDS, the 5-tap edge filter and the 2x upsampler run one output per lane on a
+// snapshot of the edge, and the predictors compute one pixel per lane.  Filter-intra's
+// serial 4x2 recursion (:112-149) runs as an anti-diagonal wavefront.  Usable from
+// any workgroup size (blockDim.x a multiple of 64).
+#pragma once
+#include "av1r_dev.h"
+
+#define EDGE_OFF 16
+#define EDGE_LEN (EDGE_OFF + 144)
+
+struct IntraLds {
+    uint8_t above[EDGE_LEN];
+    uint8_t left[EDGE_LEN];
+    uint8_t tmp[EDGE_LEN];
+    uint8_t upA[EDGE_LEN];
+    uint8_t upL[EDGE_LEN];
+    int sum[2];
+};
+
+struct IntraParams {
+    int plane, x, y, log2W, log2H;
+    int haveLeft, haveAbove, haveAR, haveBL;
+    int mode;          // PREDICTION_MODE (luma numbering); CFL handled by the caller
+    int angleDelta;
+    int filterIntra;   // plane 0 && use_filter_intra
+    int filterIntraMode;
+    int smooth;        // filterType: above/left neighbour uses a smooth mode
+    int edgeFilter;    // enable_intra_edge_filter
+};
+
+DEV int edge_strength(int w, int h, int filterType, int delta)
+{
+    int d = iabs(delta), blkWh = w + h, s = 0;
+    if (!filterType) {
+        if (blkWh <= 8) {
+            if (d >= 56) s = 1;
+        } else if (blkWh <= 16) {
+            if (d >= 40) s = 1;
+        } else if (blkWh <= 24) {
+            if (d >= 8) s = 1;
+            if (d >= 16) s = 2;
+            if (d >= 32) s = 3;
+        } else if (blkWh <= 32) {
+            s = 1;
+            if (d >= 4) s = 2;
+            if (d >= 32) s = 3;
+        } else {
+            s = 3;
+        }
+    } else {
+        if (blkWh <= 8) {
+            if (d >= 40) s = 1;
+            if (d >= 64) s = 2;
+        } else if (blkWh <= 16) {
+            if (d >= 20) s = 1;
+            if (d >= 48) s = 2;
+        } else if (blkWh <= 24) {
+            if (d >= 4) s = 3;
+        } else {
+            s = 3;
+        }
+    }
+    return s;
+}
+DEV int edge_upsample_used(int w, int h, int filterType, int delta)
+{
+    int d = iabs(delta), blkWh = w + h;
+    if (d <= 0 || d >= 40) return 0;
+    return filterType ? (blkWh <= 8) : (blkWh <= 16);
+}
+
+// intraEdgeFilter (IntraPredict.cpp:324-337) on edge e (e[-1..sz-2] rewritten).
+DEV void coop_edge_filter(uint8_t* e, uint8_t* tmp, int sz, int strength)
+{
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int i = t; i < sz; i += nt) tmp[i] = e[i - 1];
+    __syncthreads();
+    for (int i = 1 + t; i < sz; i += nt) {
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strength - 1][j] * tmp[CLIP3(0, sz - 1, i - 2 + j)];
+        e[i - 1] = (uint8_t)((s + 8) >> 4);
+    }
+    __syncthreads();
+}
+// intraEdgeUpsample (IntraPredict.cpp:354-370): out buf (index -2 .. 2*numPx-2) at up+EDGE_OFF.
+DEV void coop_edge_upsample(const uint8_t* e, uint8_t* up, int numPx)
+{
+    const int t = threadIdx.x, nt = blockDim.x;
+    uint8_t* buf = up + EDGE_OFF;
+    // dup[k] = k==0 ? e[-1] : k<=numPx+1 ? e[k-2] : e[numPx-1]
+    for (int i = t; i < numPx; i += nt) {
+        int d0 = i == 0 ? e[-1] : e[i - 2];
+        int d1 = e[i - 1];
+        int d2 = e[i];
+        int d3 = (i + 1 <= numPx - 1) ? e[i + 1] : e[numPx - 1];
+        int s = -d0 + 9 * d1 + 9 * d2 - d3;
+        buf[2 * i - 1] = (uint8_t)clip1(r2(s, 4));
+        buf[2 * i] = (uint8_t)d2;
+    }
+    if (t == 0) buf[-2] = e[-1];
+    __syncthreads();
+}
+
+DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) - 4); }
+
+// Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps).
+// `src` is the frame plane being reconstructed.  Ends with a __syncthreads().
+DEV void coop_intra_predict(const KParams& k, const DevPlane& src, const IntraParams& P,
+    IntraLds& L, uint8_t* pred, int ps)
+{
+    const int t = threadIdx.x, nt = blockDim.x;
+    const int w = 1 << P.log2W, h = 1 << P.log2H;
+    const int plane = P.plane, x = P.x, y = P.y;
+    // predict_intra uses subsampling_x for both axes (IntraPredict.cpp:566-567)
+    const int sub = plane ? 1 : 0;
+    const int maxX = ((k.mi_cols * 4) >> sub) - 1;
+    const int maxY = ((k.mi_rows * 4) >> sub) - 1;
+    uint8_t* above = L.above + EDGE_OFF;
+    uint8_t* left = L.left + EDGE_OFF;
+    const int n = w + h;
+    {
+        const bool hA = P.haveAbove, hL = P.haveLeft;
+        int aboveLimit = imin(maxX, x + (P.haveAR ? 2 * w : w) - 1);
+        int leftLimit = imin(maxY, y + (P.haveBL ? 2 * h : h) - 1);
+        for (int i = t; i < n; i += nt) {
+            uint8_t a, l;
+            if (!hA && hL) a = px(src, x - 1, y);
+            else if (!hA && !hL) a = 127;
+            else a = px(src, imin(aboveLimit, x + i), y - 1);
+            if (!hL && hA) l = px(src, x, y - 1);
+            else if (!hA && !hL) l = 129;
+            else l = px(src, x - 1, imin(leftLimit, y + i));
+            above[i] = a;
+            left[i] = l;
+        }
+        if (t == 0) {
+            uint8_t c;
+            if (hA && hL) c = px(src, x - 1, y - 1);
+            else if (hA) c = px(src, x, y - 1);
+            else if (hL) c = px(src, x - 1, y);
+            else c = 128;
+            above[-1] = c;
+            left[-1] = c;
+        }
+    }
+    __syncthreads();
+
+    if (P.filterIntra) {
+        // recursiveIntraPrediction (IntraPredict.cpp:112-149): cell (i2, j4) needs cells
+        // (i2-1, j4-1..j4) and (i2, j4-1): process anti-diagonals d = i2 + j4.
+        const int w4 = w >> 2, h2 = h >> 1;
+        const int8_t* taps = av1r_filter_intra_taps + P.filterIntraMode * 56;
+        for (int d = 0; d < w4 + h2 - 1; d++) {
+            int i2lo = imax(0, d - (w4 - 1)), i2hi = imin(h2 - 1, d);
+            int ncell = i2hi - i2lo + 1;
+            for (int q = t; q < ncell * 8; q += nt) {
+                int i2 = i2lo + (q >> 3), j4 = d - i2;
+                int o = q & 7, i1 = o >> 2, j1 = o & 3;
+                int p[7];
+#pragma unroll
+                for (int i = 0; i < 5; i++) {
+                    if (!i2) p[i] = above[(j4 << 2) + i - 1];
+                    else if (!j4 && !i) p[i] = left[(i2 << 1) - 1];
+                    else p[i] = pred[((i2 << 1) - 1) * ps + (j4 << 2) + i - 1];
+                }
+#pragma unroll
+                for (int i = 5; i < 7; i++) {
+                    if (!j4) p[i] = left[(i2 << 1) + i - 5];
+                    else p[i] = pred[((i2 << 1) + i - 5) * ps + (j4 << 2) - 1];
+                }
+                int pr = 0;
+#pragma unroll
+                for (int i = 0; i < 7; i++) pr += taps[((i1 << 2) + j1) * 7 + i] * p[i];
+                // all reads of this diagonal complete before any write (next barrier)
+                L.tmp[q] = (uint8_t)clip1(r2s(pr, 4));
+            }
+            __syncthreads();
+            for (int q = t; q < ncell * 8; q += nt) {
+                int i2 = i2lo + (q >> 3), j4 = d - i2;
+                int o = q & 7;
+                pred[((i2 << 1) + (o >> 2)) * ps + (j4 << 2) + (o & 3)] = L.tmp[q];
+            }
+            __syncthreads();
+        }
+        return;
+    }
+
+    const int mode = P.mode;
+    if (mode >= AV1R_V_PRED && mode <= AV1R_D67_PRED) {
+        // directionalIntraPredict (IntraPredict.cpp:379-483)
+        const int maxXd = (k.mi_cols * 4) >> sub;
+        const int maxYd = (k.mi_rows * 4) >> sub;  // subsampling_y == subsampling_x (4:2:0)
+        int pAngle = av1r_mode_to_angle[mode] + P.angleDelta * 3;
+        int upA = 0, upL = 0;
+        const uint8_t* A = above;
+        const uint8_t* Lc = left;
+        if (P.edgeFilter && pAngle != 90 && pAngle != 180) {
+            if (pAngle > 90 && pAngle < 180 && (w + h) >= 24) {
+                if (t == 0) {
+                    uint8_t s = (uint8_t)r2(left[0] * 5 + above[-1] * 6 + above[0] * 5, 4);
+                    left[-1] = s;
+                    above[-1] = s;
+                }
+                __syncthreads();
+            }
+            if (P.haveAbove) {
+                int strength = edge_strength(w, h, P.smooth, pAngle - 90);
+                int numPx = imin(w, maxXd - x + 1) + (pAngle < 90 ? h : 0) + 1;
+                if (strength) coop_edge_filter(above, L.tmp, numPx, strength);
+            }
+            if (P.haveLeft) {
+                int strength = edge_strength(w, h, P.smooth, pAngle - 180);
+                int numPx = imin(h, maxYd - y + 1) + (pAngle > 180 ? w : 0) + 1;
+                if (strength) coop_edge_filter(left, L.tmp, numPx, strength);
+            }
+            upA = edge_upsample_used(w, h, P.smooth, pAngle - 90);
+            if (upA) {
+                coop_edge_upsample(above, L.upA, w + (pAngle < 90 ? h : 0));
+                A = L.upA + EDGE_OFF;
+            }
+            upL = edge_upsample_used(w, h, P.smooth, pAngle - 180);
+            if (upL) {
+                coop_edge_upsample(left, L.upL, h + (pAngle > 180 ? w : 0));
+                Lc = L.upL + EDGE_OFF;
+            }
+        }
+        int dx = 0, dy = 0;
+        if (pAngle < 90) dx = av1r_dr_intra_derivative[pAngle];
+        else if (pAngle > 90 && pAngle < 180) dx = av1r_dr_intra_derivative[180 - pAngle];
+        if (pAngle > 90 && pAngle < 180) dy = av1r_dr_intra_derivative[pAngle - 90];
+        else if (pAngle > 180) dy = av1r_dr_intra_derivative[270 - pAngle];
+        for (int q = t; q < w * h; q += nt) {
+            int i = q >> P.log2W, j = q & (w - 1);
+            int v;
+            if (pAngle < 90) {
+                int idx = (i + 1) * dx;
+                int base = (idx >> (6 - upA)) + (j << upA);
+                int shift = ((idx << upA) >> 1) & 0x1F;
+                int maxBaseX = (w + h - 1) << upA;
+                v = base < maxBaseX ? r2(A[base] * (32 - shift) + A[base + 1] * shift, 5) : A[maxBaseX];
+            } else if (pAngle > 90 && pAngle < 180) {
+                int idx = (j << 6) - (i + 1) * dx;
+                int base = idx >> (6 - upA);
+                if (base >= -(1 << upA)) {
+                    int shift = ((idx << upA) >> 1) & 0x1F;
+                    v = r2(A[base] * (32 - shift) + A[base + 1] * shift, 5);
+                } else {
+                    idx = (i << 6) - (j + 1) * dy;
+                    base = idx >> (6 - upL);
+                    int shift = ((idx << upL) >> 1) & 0x1F;
+                    v = r2(Lc[base] * (32 - shift) + Lc[base + 1] * shift, 5);
+                }
+            } else if (pAngle > 180) {
+                int idx = (j + 1) * dy;
+                int base = (idx >> (6 - upL)) + (i << upL);
+                int shift = ((idx << upL) >> 1) & 0x1F;
+                v = r2(Lc[base] * (32 - shift) + Lc[base + 1] * shift, 5);
+            } else if (pAngle == 90) {
+                v = A[j];
+            } else {
+                v = Lc[i];
+            }
+            pred[i * ps + j] = (uint8_t)v;
+        }
+    } else if (mode == AV1R_DC_PRED) {
+        // dcPredict (IntraPredict.cpp:485-508): wave-level sums
+        int s = 0;
+        if (t < 64) {
+            if (P.haveAbove)
+                for (int j = t; j < w; j += 64) s += above[j];
+            if (P.haveLeft)
+                for (int i = t; i < h; i += 64) s += left[i];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+            if (t == 0) L.sum[0] = s;
+        }
+        __syncthreads();
+        s = L.sum[0];
+        int avg;
+        if (P.haveLeft && P.haveAbove) avg = (s + ((w + h) >> 1)) / (w + h);
+        else if (P.haveLeft) avg = clip1((s + (h >> 1)) >> P.log2H);
+        else if (P.haveAbove) avg = clip1((s + (w >> 1)) >> P.log2W);
+        else avg = 128;
+        for (int q = t; q < w * h; q += nt) pred[(q >> P.log2W) * ps + (q & (w - 1))] = (uint8_t)avg;
+    } else {
+        const uint8_t* wx = sm_weights(P.log2W);
+        const uint8_t* wy = sm_weights(P.log2H);
+        for (int q = t; q < w * h; q += nt) {
+            int i = q >> P.log2W, j = q & (w - 1);
+            int v;
+            if (mode == AV1R_PAETH_PRED) {
+                // paethPredict (IntraPredict.cpp:151-171)
+                int base = above[j] + left[i] - above[-1];
+                int pL = iabs(base - left[i]), pT = iabs(base - above[j]), pTL = iabs(base - above[-1]);
+                v = (pL <= pT && pL <= pTL) ? left[i] : (pT <= pTL ? above[j] : above[-1]);
+            } else if (mode == AV1R_SMOOTH_PRED) {
+                v = r2(wy[i] * above[j] + (256 - wy[i]) * left[h - 1] + wx[j] * left[i] + (256 - wx[j]) * above[w - 1], 9);
+            } else if (mode == AV1R_SMOOTH_V_PRED) {
+                v = r2(wy[i] * above[j] + (256 - wy[i]) * left[h - 1], 8);
+            } else {  // SMOOTH_H_PRED
+                v = r2(wx[j] * left[i] + (256 - wx[j]) * above[w - 1], 8);
+            }
+            pred[i * ps + j] = (uint8_t)v;
+        }
+    }
+    __syncthreads();
+}

@@ -1,0 +1,671 @@
+// recon.hip -- block reconstruction kernels for gfx950.
+//
+//   k_tb     one 64-lane workgroup per transform block of a dependency level:
+//            intra / palette / CFL prediction (or the already-predicted inter pixels),
+//            dequantisation, 2-D inverse transform (rows then columns, one lane per
+//            row/column, T[] in VGPRs), flip, add, clip, store.
+//            Restates TransformBlock::decode/reconstruct/inverseTransform
+//            (decoder/TransformBlock.cpp:2173-2456).
+//   k_inter  one 256-lane workgroup per inter-coded block: Block::compute_prediction
+//            (decoder/Block.cpp:100-174) -> InterPredict::predict_inter
+//            (decoder/InterPredict.cpp:962-1049): 8-tap sub-pel convolve or warp per
+//            reference, compound average / distance / wedge / difference-weighted /
+//            inter-intra blends, OBMC, assembled per plane in an LDS tile.
+// The host (av1r_host.cpp) orders launches by dependency level so every pixel a work
+// item reads was finalised by an earlier launch.
+#include "av1r_dev.h"
+#include "intra_dev.h"
+#include "txfm_dev.h"
+
+// ---------------------------------------------------------------------------------
+// Transform blocks
+// ---------------------------------------------------------------------------------
+#define RS 65  // LDS row stride of the residual tile (65 ints: conflict-free rows & columns)
+
+struct TbLds {
+    int res[64 * RS];
+    uint8_t pred[64 * 64];
+    IntraLds intra;
+    int sum;
+};
+
+template <int n>
+DEV void row_pass(int* row, int w, int kind, int rectScale, int rowShift, int lossless)
+{
+    int T[1 << n];
+#pragma unroll
+    for (int j = 0; j < (1 << n); j++) T[j] = (j < 32) ? row[j] : 0;
+    if (rectScale) {
+#pragma unroll
+        for (int j = 0; j < (1 << n); j++) T[j] = tx::rnd12(T[j] * 2896);
+    }
+    tx::run1d<n>(T, lossless ? 3 : kind, 16, 2);
+#pragma unroll
+    for (int j = 0; j < (1 << n); j++) row[j] = CLIP3(-32768, 32767, r2(T[j], rowShift));
+}
+template <int n>
+DEV void col_pass(int* col, int kind, int colShift, int lossless)
+{
+    int T[1 << n];
+#pragma unroll
+    for (int i = 0; i < (1 << n); i++) T[i] = col[i * RS];
+    tx::run1d<n>(T, lossless ? 3 : kind, 16, 0);
+#pragma unroll
+    for (int i = 0; i < (1 << n); i++) col[i * RS] = r2(T[i], colShift);
+}
+
+// reconstruct() + inverseTransform() into L.res (TransformBlock.cpp:2173-2276)
+DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds& L)
+{
+    const int t = threadIdx.x;
+    const int txSz = tb.tx_size;
+    const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
+    const int log2W = av1r_tx_w_log2[txSz], log2H = av1r_tx_h_log2[txSz];
+    const int tw = imin(w, 32), th = imin(h, 32);
+    const av1r_frame_hdr& hd = *k.hdr;
+    for (int q = t; q < th * w; q += 64) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
+    __syncthreads();
+    int dqDenom = 1;
+    if (txSz == AV1R_TX_32X32 || txSz == AV1R_TX_16X32 || txSz == AV1R_TX_32X16 || txSz == AV1R_TX_16X64 || txSz == AV1R_TX_64X16)
+        dqDenom = 2;
+    else if (txSz == AV1R_TX_64X64 || txSz == AV1R_TX_32X64 || txSz == AV1R_TX_64X32)
+        dqDenom = 4;
+    const int plane = tb.plane;
+    const int dcDelta = plane == 0 ? hd.delta_q_y_dc : plane == 1 ? hd.delta_q_u_dc : hd.delta_q_v_dc;
+    const int acDelta = plane == 0 ? 0 : plane == 1 ? hd.delta_q_u_ac : hd.delta_q_v_ac;
+    const int dcQ = av1r_dc_qlookup[CLIP3(0, 255, blk.qindex + dcDelta)];
+    const int acQ = av1r_ac_qlookup[CLIP3(0, 255, blk.qindex + acDelta)];
+    const uint32_t* cf = k.coefs + tb.coef_off;
+    for (int q = t; q < tb.coef_cnt; q += 64) {
+        uint32_t c = cf[q];
+        int pos = AV1R_COEF_POS(c), level = AV1R_COEF_LEVEL(c);
+        int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
+        int sign = d < 0 ? -1 : 1;
+        int d2 = sign * (iabs(d) & 0xffffff) / dqDenom;
+        L.res[(pos / tw) * RS + (pos % tw)] = CLIP3(-(1 << 15), (1 << 15) - 1, d2);
+    }
+    __syncthreads();
+    const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
+    const int type = tb.tx_type;
+    const int rowShift = lossless ? 0 : av1r_tx_row_shift[txSz];
+    const int colShift = lossless ? 0 : 4;
+    const int rect = iabs(log2W - log2H) == 1;
+    const int rk = tx::row_kind(type), ck = tx::col_kind(type);
+    // rows >= 32 of a 64-high transform have all-zero input and therefore zero output
+    if (t < th) {
+        int* row = L.res + t * RS;
+        switch (log2W) {
+        case 2: row_pass<2>(row, w, rk, rect, rowShift, lossless); break;
+        case 3: row_pass<3>(row, w, rk, rect, rowShift, lossless); break;
+        case 4: row_pass<4>(row, w, rk, rect, rowShift, lossless); break;
+        case 5: row_pass<5>(row, w, rk, rect, rowShift, lossless); break;
+        default: row_pass<6>(row, w, rk, rect, rowShift, lossless); break;
+        }
+    } else if (t < h) {
+        int* row = L.res + t * RS;
+        for (int j = 0; j < w; j++) row[j] = 0;
+    }
+    __syncthreads();
+    if (t < w) {
+        int* col = L.res + t;
+        switch (log2H) {
+        case 2: col_pass<2>(col, ck, colShift, lossless); break;
+        case 3: col_pass<3>(col, ck, colShift, lossless); break;
+        case 4: col_pass<4>(col, ck, colShift, lossless); break;
+        case 5: col_pass<5>(col, ck, colShift, lossless); break;
+        default: col_pass<6>(col, ck, colShift, lossless); break;
+        }
+    }
+    __syncthreads();
+}
+
+extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
+{
+    __shared__ TbLds L;
+    const int t = threadIdx.x;
+    const av1r_tb tb = k.tbs[k.items[blockIdx.x]];
+    const av1r_block& blk = k.blocks[tb.block];
+    const int plane = tb.plane, x = tb.x, y = tb.y, txSz = tb.tx_size;
+    const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
+    const int log2W = av1r_tx_w_log2[txSz];
+    const DevPlane& dst = k.cur.pl[plane];
+    const uint32_t bflags = blk.flags;
+    const int isInter = (bflags & AV1R_BLK_INTER) != 0;
+    const int palSize = plane ? blk.palette_size_uv : blk.palette_size_y;
+    const av1r_frame_hdr& hd = *k.hdr;
+
+    if (isInter) {
+        for (int q = t; q < w * h; q += 64) {
+            int i = q >> log2W, j = q & (w - 1);
+            L.pred[i * 64 + j] = px(dst, x + j, y + i);
+        }
+    } else if (palSize) {
+        // Block::Palette::predict_palette (Block.cpp:2279-2298)
+        const uint8_t* ph = k.palette + blk.palette_off;
+        int bx = x - (blk.mi_col >> (plane ? 1 : 0)) * 4, by = y - (blk.mi_row >> (plane ? 1 : 0)) * 4;
+        int mw = plane ? ph[2] : ph[0];
+        const uint8_t* map = ph + AV1R_PALETTE_HDR + (plane ? ph[0] * ph[1] : 0);
+        const uint8_t* colors = ph + 4 + 8 * plane;
+        for (int q = t; q < w * h; q += 64) {
+            int i = q >> log2W, j = q & (w - 1);
+            L.pred[i * 64 + j] = colors[map[(by + i) * mw + bx + j]];
+        }
+    } else {
+        const int isCfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
+        IntraParams P;
+        P.plane = plane;
+        P.x = x;
+        P.y = y;
+        P.log2W = log2W;
+        P.log2H = av1r_tx_h_log2[txSz];
+        P.haveLeft = (tb.flags & AV1R_TB_HAVE_LEFT) != 0;
+        P.haveAbove = (tb.flags & AV1R_TB_HAVE_ABOVE) != 0;
+        P.haveAR = (tb.flags & AV1R_TB_HAVE_AR) != 0;
+        P.haveBL = (tb.flags & AV1R_TB_HAVE_BL) != 0;
+        P.mode = plane == 0 ? blk.y_mode : (isCfl ? AV1R_DC_PRED : blk.uv_mode);
+        P.angleDelta = plane == 0 ? blk.angle_delta_y : blk.angle_delta_uv;
+        P.filterIntra = plane == 0 && (bflags & AV1R_BLK_FILTER_INTRA);
+        P.filterIntraMode = blk.filter_intra_mode;
+        P.smooth = plane ? ((bflags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
+                         : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
+        P.edgeFilter = hd.enable_intra_edge_filter;
+        coop_intra_predict(k, dst, P, L.intra, L.pred, 64);
+        if (isCfl) {
+            // predict_chroma_from_luma (IntraPredict.cpp:632-667)
+            const DevPlane& luma = k.cur.pl[0];
+            const int alpha = plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v;
+            const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
+            int s = 0;
+            for (int q = t; q < w * h; q += 64) {
+                int i = q >> log2W, j = q & (w - 1);
+                int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
+                int v = (px(luma, lx, ly) + px(luma, lx + 1, ly) + px(luma, lx, ly + 1) + px(luma, lx + 1, ly + 1)) << 1;
+                L.res[i * RS + j] = v;  // res is free until the residual pass
+                s += v;
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+            const int avg = r2(s, log2W + P.log2H);
+            for (int q = t; q < w * h; q += 64) {
+                int i = q >> log2W, j = q & (w - 1);
+                int dc = L.pred[i * 64 + j];
+                L.pred[i * 64 + j] = (uint8_t)clip1(dc + r2s(alpha * (L.res[i * RS + j] - avg), 6));
+            }
+        }
+    }
+    __syncthreads();
+    if (tb.coef_cnt) {
+        tb_residual(k, tb, blk, L);
+        const int tt = tb.tx_type;
+        const int flipUD = tt == AV1R_FLIPADST_DCT || tt == AV1R_FLIPADST_ADST || tt == AV1R_V_FLIPADST || tt == AV1R_FLIPADST_FLIPADST;
+        const int flipLR = tt == AV1R_DCT_FLIPADST || tt == AV1R_ADST_FLIPADST || tt == AV1R_H_FLIPADST || tt == AV1R_FLIPADST_FLIPADST;
+        for (int q = t; q < w * h; q += 64) {
+            int i = q >> log2W, j = q & (w - 1);
+            int xx = flipLR ? (w - j - 1) : j, yy = flipUD ? (h - i - 1) : i;
+            px(dst, x + j, y + i) = (uint8_t)clip1(L.res[yy * RS + xx] + L.pred[i * 64 + j]);
+        }
+    } else if (!isInter) {
+        for (int q = t; q < w * h; q += 64) {
+            int i = q >> log2W, j = q & (w - 1);
+            px(dst, x + j, y + i) = L.pred[i * 64 + j];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Inter prediction
+// ---------------------------------------------------------------------------------
+#define IT 256
+#define STRIP 16  // prediction rows per pass (registers: STRIP*128/IT px per lane per ref)
+
+struct InterLds {
+    uint8_t tile[128 * 128];  // this plane's block, assembled before the store
+    uint8_t mask[128 * 128];  // compute_prediction's Mask (persists across planes)
+    IntraLds intra;
+    uint8_t iipred[32 * 32];
+};
+
+struct RefSel {
+    DevPlane p;
+    int lastX, lastY;
+    int startX, startY, xStep, yStep;
+    int filtX, filtY;  // subpel filter sets (getFilterIdx)
+    int warp;          // 0 none, 1 local, 2 global
+    int alpha, beta, gamma, delta;
+    const int32_t* wp;
+};
+
+// Block::LocalWarp::setupShear (Block.cpp:1179-1200) incl. resolveDivisor (:1087-1095)
+DEV int setup_shear(const int32_t* wp, int& alpha, int& beta, int& gamma, int& delta)
+{
+    int alpha0 = CLIP3(-32768, 32767, wp[2] - (1 << 16));
+    int beta0 = CLIP3(-32768, 32767, wp[3]);
+    int64_t d = wp[2];
+    int64_t ad = d < 0 ? -d : d;
+    int n = floor_log2_u64((uint64_t)ad);
+    int64_t e = ad - ((int64_t)1 << n);
+    int64_t f = n > 8 ? r2_64(e, n - 8) : (e << (8 - n));
+    int divShift = n + 14;
+    int divFactor = d < 0 ? -(int)av1r_div_lut[f] : (int)av1r_div_lut[f];
+    int64_t v = (int64_t)(wp[4] << 16);
+    int gamma0 = CLIP3(-32768, 32767, (int)r2s_64(v * divFactor, divShift));
+    int64_t w = (int64_t)(wp[3] * wp[4]);
+    int delta0 = CLIP3(-32768, 32767, wp[5] - (int)r2s_64(w * divFactor, divShift) - (1 << 16));
+    alpha = r2s(alpha0, 6) << 6;
+    beta = r2s(beta0, 6) << 6;
+    gamma = r2s(gamma0, 6) << 6;
+    delta = r2s(delta0, 6) << 6;
+    if ((4 * iabs(alpha) + 7 * iabs(beta)) >= (1 << 16)) return 0;
+    if ((4 * iabs(gamma) + 4 * iabs(delta)) >= (1 << 16)) return 0;
+    return 1;
+}
+
+DEV int filter_idx(int filt, int size, int dir)
+{
+    int f = dir ? (filt >> 4) : (filt & 15);
+    if (size <= 4) {
+        if (f == AV1R_EIGHTTAP || f == AV1R_EIGHTTAP_SHARP) return 4;
+        if (f == AV1R_EIGHTTAP_SMOOTH) return 5;
+    }
+    return f;
+}
+
+// motionVectorScaling (InterPredict.cpp:66-83) + the ref geometry of blockInterPrediction
+DEV void select_ref(const KParams& k, RefSel& R, int refIdx, int plane, int x, int y, const int16_t* mv)
+{
+    const int sub = plane ? 1 : 0;
+    int rw, rh;
+    if (refIdx < 0) {  // intra block copy predicts from the current (pre-filter) frame
+        R.p = k.cur.pl[plane];
+        rw = k.frame_w;
+        rh = k.frame_h;
+        R.lastX = ((k.mi_cols * 4 + sub) >> sub) - 1;
+        R.lastY = ((k.mi_rows * 4 + sub) >> sub) - 1;
+    } else {
+        const DevFrame& f = k.ref[refIdx];
+        R.p = f.pl[plane];
+        rw = f.width;
+        rh = f.height;
+        R.lastX = ((rw + sub) >> sub) - 1;
+        R.lastY = ((rh + sub) >> sub) - 1;
+    }
+    int xs = ((rw << 14) + (k.frame_w / 2)) / k.frame_w;
+    int ys = ((rh << 14) + (k.frame_h / 2)) / k.frame_h;
+    int origX = ((x << 4) + ((2 * mv[1]) >> sub) + 8);
+    int origY = ((y << 4) + ((2 * mv[0]) >> sub) + 8);
+    int baseX = origX * xs - (8 << 14);
+    int baseY = origY * ys - (8 << 14);
+    R.startX = r2s(baseX, 8) + 32;
+    R.startY = r2s(baseY, 8) + 32;
+    R.xStep = r2s(xs, 4);
+    R.yStep = r2s(ys, 4);
+}
+
+// One predicted sample (row r, column c of the PU) before blending: blockPixelPredict /
+// blockSubPixelPredict (InterPredict.cpp:319-383) or blockWarp (:507-553).
+DEV int pred_sample(const RefSel& R, int r, int c, int R0, int R1, int puX, int puY, int plane, int w, int h)
+{
+    if (R.warp) {
+        const int sub = plane ? 1 : 0;
+        const int i8 = r >> 3, j8 = c >> 3;
+        const int32_t* wp = R.wp;
+        int srcX = (puX + j8 * 8 + 4) << sub;
+        int srcY = (puY + i8 * 8 + 4) << sub;
+        int dstX = wp[2] * srcX + wp[3] * srcY + wp[0];
+        int dstY = wp[4] * srcX + wp[5] * srcY + wp[1];
+        int x4 = dstX >> sub, y4 = dstY >> sub;
+        int ix4 = x4 >> 16, sx4 = x4 & 0xffff, iy4 = y4 >> 16, sy4 = y4 & 0xffff;
+        const int i1 = (r & 7) - 4, i2 = (c & 7) - 4;
+        int sy = sy4 + R.gamma * i2 + R.delta * i1;
+        const int8_t* vf = av1r_warped_filters + (r2(sy, 10) + 64) * 8;
+        int s = 0;
+#pragma unroll
+        for (int i3 = 0; i3 < 8; i3++) {
+            int ii1 = i1 + i3 - 3;  // intermediate row i1 + i3 + 4 - 7
+            int sx = sx4 + R.alpha * i2 + R.beta * ii1;
+            const int8_t* hf = av1r_warped_filters + (r2(sx, 10) + 64) * 8;
+            int yy = CLIP3(0, R.lastY, iy4 + ii1);
+            const uint8_t* row = R.p.p + (size_t)yy * R.p.stride;
+            int hs = 0;
+#pragma unroll
+            for (int k3 = 0; k3 < 8; k3++) hs += hf[k3] * row[CLIP3(0, R.lastX, ix4 + i2 - 3 + k3)];
+            s += vf[i3] * r2(hs, R0);
+        }
+        return (int16_t)r2(s, R1);
+    }
+    if (!((R.startX >> 6) & 15) && !((R.startY >> 6) & 15)) {
+        int xx = CLIP3(0, R.lastX, (R.startX >> 10) + c), yy = CLIP3(0, R.lastY, (R.startY >> 10) + r);
+        return (int16_t)(R.p.p[(size_t)yy * R.p.stride + xx] << (14 - R0 - R1));
+    }
+    int p = R.startX + R.xStep * c;
+    const int16_t* hf = av1r_subpel_filters + (R.filtX * 16 + ((p >> 6) & 15)) * 8;
+    int x0 = (p >> 10) - 3;
+    int pv = (R.startY & 1023) + R.yStep * r;
+    const int16_t* vf = av1r_subpel_filters + (R.filtY * 16 + ((pv >> 6) & 15)) * 8;
+    int ybase = (R.startY >> 10) + (pv >> 10) - 3;
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        if (!vf[t]) continue;
+        const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, ybase + t) * R.p.stride;
+        int hs = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) hs += hf[u] * row[CLIP3(0, R.lastX, x0 + u)];
+        s += vf[t] * r2(hs, R0);
+    }
+    return (int16_t)r2(s, R1);
+}
+
+DEV int wedge_master(int dir, int i, int j)
+{
+    // MasterMask (InterPredict.cpp:835-858) evaluated on the fly
+    switch (dir) {
+    case AV1R_WEDGE_VERTICAL: return av1r_wedge_master_vertical[j];
+    case AV1R_WEDGE_HORIZONTAL: return av1r_wedge_master_vertical[i];
+    case AV1R_WEDGE_OBLIQUE63: {
+        int shift = 16 - (i >> 1);
+        return (i & 1) ? av1r_wedge_master_oblique_odd[CLIP3(0, 63, j - (shift - 1))]
+                       : av1r_wedge_master_oblique_even[CLIP3(0, 63, j - shift)];
+    }
+    case AV1R_WEDGE_OBLIQUE27: return wedge_master(AV1R_WEDGE_OBLIQUE63, j, i);
+    case AV1R_WEDGE_OBLIQUE117: return 64 - wedge_master(AV1R_WEDGE_OBLIQUE63, i, 63 - j);
+    default: return 64 - wedge_master(AV1R_WEDGE_OBLIQUE63, j, 63 - i);  // OBLIQUE153
+    }
+}
+
+struct WedgeSel {
+    int dir, xoff, yoff, flip;
+};
+DEV WedgeSel wedge_select(int bs, int wedge)
+{
+    int w = av1r_num4x4w[bs] * 4, h = av1r_num4x4h[bs] * 4;
+    int shape = h > w ? 0 : (h < w ? 1 : 2);
+    const uint8_t* cb = av1r_wedge_codebook[shape][wedge];
+    WedgeSel s;
+    s.dir = cb[0];
+    s.xoff = 32 - ((cb[1] * w) >> 3);
+    s.yoff = 32 - ((cb[2] * h) >> 3);
+    // flipSign (initialise_wedge_mask_table, InterPredict.cpp:870-877)
+    int sum = 0;
+    for (int i = 0; i < w; i++) sum += wedge_master(s.dir, s.yoff, s.xoff + i);
+    for (int i = 1; i < h; i++) sum += wedge_master(s.dir, s.yoff + i, s.xoff);
+    int avg = (sum + (w + h - 1) / 2) / (w + h - 1);
+    s.flip = avg < 32;
+    return s;
+}
+
+// getDistanceWeights (InterPredict.cpp:917-960)
+DEV void distance_weights(const KParams& k, const av1r_mi& info, int& fwd, int& bck)
+{
+    int d1 = k.hdr->ref_dist[info.ref_frame[0] & 7];
+    int d0 = k.hdr->ref_dist[info.ref_frame[1] & 7];
+    int order = d0 <= d1;
+    if (d0 == 0 || d1 == 0) {
+        fwd = av1r_quant_dist_lookup[3][order];
+        bck = av1r_quant_dist_lookup[3][1 - order];
+        return;
+    }
+    int i;
+    for (i = 0; i < 3; i++) {
+        int c0 = av1r_quant_dist_weight[i][order], c1 = av1r_quant_dist_weight[i][1 - order];
+        if (order) {
+            if (d0 * c0 > d1 * c1) break;
+        } else {
+            if (d0 * c0 < d1 * c1) break;
+        }
+    }
+    fwd = av1r_quant_dist_lookup[i][order];
+    bck = av1r_quant_dist_lookup[i][1 - order];
+}
+
+// predict_inter for one PU of one plane; result blended into L.tile (block-relative
+// origin (ox, oy) in the tile).
+DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int x, int y,
+    int w, int h, int candRow, int candCol, int ox, int oy)
+{
+    const int t = threadIdx.x;
+    const av1r_frame_hdr& hd = *k.hdr;
+    const av1r_mi& info = mi_at(k, candRow, candCol);
+    const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
+    const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
+    const int isIntrabc = (blk.flags & AV1R_BLK_INTRABC) != 0;
+    const int isGlobalMode = blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV;
+    RefSel R[2];
+    int globalValid = 0;
+    for (int l = 0; l < 1 + isCompound; l++) {
+        int refFrame = info.ref_frame[l];
+        int a, b, c, d;
+        if (isGlobalMode && hd.gm_type[refFrame & 7] > AV1R_GM_TRANSLATION)
+            globalValid = setup_shear(hd.gm_params[refFrame & 7], a, b, c, d);
+        int refIdx = isIntrabc ? -1 : hd.ref_frame_idx[refFrame - 1];
+        select_ref(k, R[l], refIdx, plane, x, y, info.mv[l]);
+        R[l].warp = 0;
+        if (!(w < 8 || h < 8) && !hd.force_integer_mv) {
+            if (blk.motion_mode == AV1R_LOCALWARP && (blk.flags & AV1R_BLK_LOCAL_VALID)) {
+                R[l].warp = 1;
+                R[l].wp = blk.local_warp;
+            } else if (isGlobalMode && hd.gm_type[refFrame & 7] > AV1R_GM_TRANSLATION && globalValid) {
+                int rw = refIdx < 0 ? k.frame_w : k.ref[refIdx].width;
+                int rh = refIdx < 0 ? k.frame_h : k.ref[refIdx].height;
+                int xs = ((rw << 14) + (k.frame_w / 2)) / k.frame_w;
+                int ys = ((rh << 14) + (k.frame_h / 2)) / k.frame_h;
+                if (xs == (1 << 14) && ys == (1 << 14)) {
+                    R[l].warp = 2;
+                    R[l].wp = hd.gm_params[refFrame & 7];
+                }
+            }
+        }
+        if (R[l].warp) setup_shear(R[l].wp, R[l].alpha, R[l].beta, R[l].gamma, R[l].delta);
+        R[l].filtX = filter_idx(info.filt, w, 1);
+        R[l].filtY = filter_idx(info.filt, h, 0);
+    }
+    const int ct = blk.compound_type;
+    const int isII = mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] == AV1R_INTRA_FRAME;
+    const int sub = plane ? 1 : 0;
+    int mode;  // 0 plain, 1 average, 2 distance, 3 mask blend
+    if (!isCompound && !isII) mode = 0;
+    else if (ct == AV1R_COMPOUND_AVERAGE) mode = 1;
+    else if (ct == AV1R_COMPOUND_DISTANCE) mode = 2;
+    else mode = 3;
+    int fwd = 0, bck = 0;
+    if (mode == 2) distance_weights(k, info, fwd, bck);
+    WedgeSel ws = {0, 0, 0, 0};
+    if (ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
+    const int ii = (blk.flags & AV1R_BLK_INTERINTRA) != 0, wii = (blk.flags & AV1R_BLK_WEDGE_II) != 0;
+    const int diffwtdLuma = ct == AV1R_COMPOUND_DIFFWTD && plane == 0;
+    const int sizeScale = 128 / imax(h, w);
+    for (int q = t; q < w * h; q += IT) {
+        const int r = q / w, c = q - r * w;
+        int p0 = pred_sample(R[0], r, c, R0, R1, x, y, plane, w, h);
+        int p1 = isCompound ? pred_sample(R[1], r, c, R0, R1, x, y, plane, w, h) : 0;
+        int v;
+        if (mode == 0) {
+            v = clip1(p0);
+        } else if (mode == 1) {
+            v = clip1(r2(p0 + p1, 1 + PostRound));
+        } else if (mode == 2) {
+            v = clip1(r2(fwd * p0 + bck * p1, 4 + PostRound));
+        } else {
+            // mask value (wedgeMask / intraModeVariantMask / differenceWeightMask) then
+            // maskBlend (InterPredict.cpp:555-609)
+            int m;
+            if (diffwtdLuma) {
+                int diff = (int16_t)iabs(p0 - p1);
+                diff = r2(diff, PostRound);
+                int mm = CLIP3(0, 64, 38 + diff / 16);
+                m = blk.mask_type ? 64 - mm : mm;
+                L.mask[r * 128 + c] = (uint8_t)m;
+            } else if (ct == AV1R_COMPOUND_INTRA || (ii && !wii) || !sub) {
+                if (ct == AV1R_COMPOUND_WEDGE) {
+                    int mv = wedge_master(ws.dir, ws.yoff + r, ws.xoff + c);
+                    m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
+                } else if (ct == AV1R_COMPOUND_INTRA) {
+                    int im = blk.interintra_mode;
+                    m = im == AV1R_II_V_PRED ? av1r_ii_weights_1d[r * sizeScale]
+                        : im == AV1R_II_H_PRED ? av1r_ii_weights_1d[c * sizeScale]
+                        : im == AV1R_II_SMOOTH_PRED ? av1r_ii_weights_1d[imin(r, c) * sizeScale] : 32;
+                } else {
+                    m = L.mask[r * 128 + c];
+                }
+            } else {
+                // 4:2:0 chroma: average of the 2x2 luma-resolution mask entries
+                int s4 = 0;
+#pragma unroll
+                for (int dy = 0; dy < 2; dy++)
+#pragma unroll
+                    for (int dx = 0; dx < 2; dx++) {
+                        int rr = 2 * r + dy, cc = 2 * c + dx;
+                        int mv;
+                        if (ct == AV1R_COMPOUND_WEDGE) {
+                            int mw = wedge_master(ws.dir, ws.yoff + rr, ws.xoff + cc);
+                            mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
+                        } else {
+                            mv = L.mask[rr * 128 + cc];
+                        }
+                        s4 += mv;
+                    }
+                m = r2(s4, 2);
+            }
+            if (ii) {
+                int pp0 = clip1(r2(p0, PostRound));
+                int pp1 = L.tile[(oy + r) * 128 + ox + c];
+                v = clip1(r2(m * pp1 + (64 - m) * pp0, 6));
+            } else {
+                v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
+            }
+        }
+        L.tile[(oy + r) * 128 + ox + c] = (uint8_t)v;
+    }
+    __syncthreads();
+}
+
+// overlappedMotionCompensation (InterPredict.cpp:611-709) on the plane tile.
+DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int baseX, int baseY, int w, int h)
+{
+    const int t = threadIdx.x;
+    const int sub = plane ? 1 : 0;
+    const int bs = blk.mi_size;
+    const av1r_frame_hdr& hd = *k.hdr;
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 0 && !((blk.flags & AV1R_BLK_AVAIL_U) && plane_bsize(bs, plane) >= AV1R_BLOCK_8X8)) continue;
+        if (pass == 1 && !(blk.flags & AV1R_BLK_AVAIL_L)) continue;
+        const int n4 = pass ? av1r_num4x4h[bs] : av1r_num4x4w[bs];
+        const int nLimit = imin(4, pass ? av1r_mih_log2[bs] : av1r_miw_log2[bs]);
+        const int lim = pass ? imin(k.mi_rows, blk.mi_row + n4) : imin(k.mi_cols, blk.mi_col + n4);
+        int pos4 = pass ? blk.mi_row : blk.mi_col;
+        int nCount = 0;
+        // the neighbours of one pass cover disjoint pixel ranges: all lanes share them
+        while (nCount < nLimit && pos4 < lim) {
+            int candRow = pass ? (pos4 | 1) : blk.mi_row - 1;
+            int candCol = pass ? blk.mi_col - 1 : (pos4 | 1);
+            const av1r_mi& info = mi_at(k, candRow, candCol);
+            int step4 = CLIP3(2, 16, pass ? av1r_num4x4h[info.mi_size] : av1r_num4x4w[info.mi_size]);
+            if (info.ref_frame[0] > AV1R_INTRA_FRAME) {
+                nCount++;
+                int x4 = pass ? blk.mi_col : pos4, y4 = pass ? pos4 : blk.mi_row;
+                int predW = pass ? imin(w >> 1, 32 >> sub) : imin(w, (step4 * 4) >> sub);
+                int predH = pass ? imin(h, (step4 * 4) >> sub) : imin(h >> 1, 32 >> sub);
+                int len = pass ? predW : predH;
+                const uint8_t* mask = av1r_obmc_mask + (len == 2 ? 0 : len == 4 ? 2 : len == 8 ? 6 : len == 16 ? 14 : 30);
+                int predX = (x4 * 4) >> sub, predY = (y4 * 4) >> sub;
+                RefSel R;
+                select_ref(k, R, hd.ref_frame_idx[info.ref_frame[0] - 1], plane, predX, predY, info.mv[0]);
+                R.warp = 0;
+                R.filtX = filter_idx(info.filt, predW, 1);
+                R.filtY = filter_idx(info.filt, predH, 0);
+                for (int q = t; q < predW * predH; q += IT) {
+                    int i = q / predW, j = q - i * predW;
+                    int p = pred_sample(R, i, j, 3, 11, predX, predY, plane, predW, predH);
+                    int m = pass ? mask[j] : mask[i];
+                    uint8_t& d = L.tile[(predY - baseY + i) * 128 + predX - baseX + j];
+                    d = (uint8_t)clip1(r2(m * d + (64 - m) * clip1(p), 6));
+                }
+            }
+            pos4 += step4;
+        }
+        __syncthreads();
+    }
+}
+
+extern "C" __global__ __launch_bounds__(IT) void k_inter(KParams k)
+{
+    __shared__ InterLds L;
+    const int t = threadIdx.x;
+    const av1r_block& blk = k.blocks[k.items[blockIdx.x]];
+    const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
+    const int bs = blk.mi_size;
+    const int bw = av1r_num4x4w[bs] * 4, bh = av1r_num4x4h[bs] * 4;
+    const int isII = mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] == AV1R_INTRA_FRAME;
+    for (int plane = 0; plane < 1 + hasChroma * 2; plane++) {
+        const int psz = plane_bsize(bs, plane);
+        const int n4w = av1r_num4x4w[psz], n4h = av1r_num4x4h[psz];
+        const int sub = plane ? 1 : 0;
+        const int baseX = (blk.mi_col >> sub) * 4, baseY = (blk.mi_row >> sub) * 4;
+        const int pw = n4w * 4, ph = n4h * 4;
+        if (isII) {
+            // block-level intra prediction of an inter-intra block (Block.cpp:118-144)
+            int im = blk.interintra_mode;
+            IntraParams P;
+            P.plane = plane;
+            P.x = baseX;
+            P.y = baseY;
+            P.log2W = 2 + av1r_miw_log2[psz];
+            P.log2H = 2 + av1r_mih_log2[psz];
+            P.haveLeft = plane ? (blk.flags & AV1R_BLK_AVAIL_L_UV) != 0 : (blk.flags & AV1R_BLK_AVAIL_L) != 0;
+            P.haveAbove = plane ? (blk.flags & AV1R_BLK_AVAIL_U_UV) != 0 : (blk.flags & AV1R_BLK_AVAIL_U) != 0;
+            P.haveAR = (blk.ii_edge >> (2 * plane)) & 1;
+            P.haveBL = (blk.ii_edge >> (2 * plane + 1)) & 1;
+            P.mode = im == AV1R_II_DC_PRED ? AV1R_DC_PRED : im == AV1R_II_V_PRED ? AV1R_V_PRED
+                : im == AV1R_II_H_PRED ? AV1R_H_PRED : AV1R_SMOOTH_PRED;
+            P.angleDelta = 0;
+            P.filterIntra = 0;
+            P.filterIntraMode = 0;
+            P.smooth = 0;
+            P.edgeFilter = k.hdr->enable_intra_edge_filter;
+            coop_intra_predict(k, k.cur.pl[plane], P, L.intra, L.iipred, 32);
+            for (int q = t; q < pw * ph; q += IT) {
+                int i = q / pw, j = q - i * pw;
+                L.tile[i * 128 + j] = L.iipred[i * 32 + j];
+            }
+            __syncthreads();
+        }
+        int candRow = (blk.mi_row >> sub) << sub, candCol = (blk.mi_col >> sub) << sub;
+        int predW = bw >> sub, predH = bh >> sub;
+        int someUseIntra = 0;
+        for (int r = 0; r < (n4h << sub); r++)
+            for (int c = 0; c < (n4w << sub); c++)
+                if (mi_at(k, candRow + r, candCol + c).ref_frame[0] == AV1R_INTRA_FRAME) someUseIntra = 1;
+        if (someUseIntra) {
+            predW = pw;
+            predH = ph;
+            candRow = blk.mi_row;
+            candCol = blk.mi_col;
+        }
+        int r = 0;
+        for (int yy = 0; yy < ph; yy += predH) {
+            int c = 0;
+            for (int xx = 0; xx < pw; xx += predW) {
+                predict_pu(k, blk, L, plane, baseX + xx, baseY + yy, predW, predH, candRow + r, candCol + c, xx, yy);
+                c++;
+            }
+            r++;
+        }
+        if (blk.motion_mode == AV1R_OBMC_CAUSAL) obmc(k, blk, L, plane, baseX, baseY, predW, predH);
+        const DevPlane& dst = k.cur.pl[plane];
+        for (int q = t; q < pw * ph; q += IT) {
+            int i = q / pw, j = q - i * pw;
+            px(dst, baseX + j, baseY + i) = L.tile[i * 128 + j];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------
+void launch_k_tb(const KParams& k, unsigned n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_tb, dim3(n), dim3(64), 0, s, k);
+}
+void launch_k_inter(const KParams& k, unsigned n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_inter, dim3(n), dim3(IT), 0, s, k);
+}

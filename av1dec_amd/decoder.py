@@ -1,0 +1,92 @@
+"""Host-side mirror of the reference decoder API on top of the HIP backend.
+
+`Decoder` follows YamiAv1::Decoder (decoder/Av1Decoder.h:47-66): frames go in,
+`get_output()` pops shown frames in order or returns None (Av1Decoder.cpp:203-211).
+What goes in is the frame batch the host parser produces for each decoded frame (the
+reference's parsed Tile trees, see include/av1r.h), not OBU bytes."""
+import ctypes as C
+
+import numpy as np
+
+from . import abi, native
+
+
+class BackendError(RuntimeError):
+    pass
+
+
+class Decoder:
+    def __init__(self, device=0, keep_stages=False, timing=False):
+        self.l = native.lib()
+        self.c = C.c_void_p()
+        rc = self.l.av1r_create(device, C.byref(self.c))
+        if rc != 0:
+            raise BackendError(f"av1r_create({device}) failed: {rc}")
+        self.l.av1r_set_keep_stages(self.c, int(keep_stages))
+        self.l.av1r_set_timing(self.c, int(timing))
+        self.last = None
+
+    def close(self):
+        if self.c:
+            self.l.av1r_destroy(self.c)
+            self.c = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.l.av1r_last_error(self.c).decode()
+            raise BackendError(f"{what} failed ({rc}): {msg}")
+
+    def decode_frame(self, frame):
+        """frame: batchfile.Frame (keeps its buffers alive)."""
+        self.last = frame.hdr
+        self._check(self.l.av1r_decode_frame(self.c, C.cast(frame.byref(), C.c_void_p)), "av1r_decode_frame")
+
+    def decode_tiles(self, frame_level, tiles):
+        self._check(self.l.av1r_frame_begin(self.c, C.cast(frame_level.byref(), C.c_void_p)), "av1r_frame_begin")
+        for t in tiles:
+            self._check(self.l.av1r_submit_tile(self.c, C.cast(t.byref(), C.c_void_p)), "av1r_submit_tile")
+        self._check(self.l.av1r_frame_end(self.c), "av1r_frame_end")
+
+    def synchronize(self):
+        self._check(self.l.av1r_synchronize(self.c), "av1r_synchronize")
+
+    def output_pending(self):
+        return self.l.av1r_output_pending(self.c)
+
+    def get_output(self):
+        w, h = C.c_int(), C.c_int()
+        if self.l.av1r_get_output(self.c, None, 0, None, 0, None, 0, C.byref(w), C.byref(h)) != 0:
+            return None
+        W, H = w.value, h.value
+        y = np.empty((H, W), np.uint8)
+        u = np.empty((H >> 1, W >> 1), np.uint8)
+        v = np.empty((H >> 1, W >> 1), np.uint8)
+        self._check(self.l.av1r_get_output(self.c, y.ctypes.data, W, u.ctypes.data, W >> 1, v.ctypes.data,
+                                           W >> 1, None, None), "av1r_get_output")
+        return y, u, v
+
+    def read_stage(self, stage):
+        W, H = self.last.frame_width, self.last.frame_height
+        out = []
+        for p in range(3):
+            w, h = (W, H) if p == 0 else (W >> 1, H >> 1)
+            a = np.empty((h, w), np.uint8)
+            self._check(self.l.av1r_read_stage(self.c, stage, p, a.ctypes.data, w), "av1r_read_stage")
+            out.append(a)
+        return out
+
+    def last_frame_times(self):
+        t = [C.c_float() for _ in range(4)]
+        self._check(self.l.av1r_last_frame_times(self.c, *[C.byref(x) for x in t]), "av1r_last_frame_times")
+        return [x.value for x in t]
+
+    def last_frame_stats(self):
+        lv, ub = C.c_int(), C.c_uint64()
+        self.l.av1r_last_frame_stats(self.c, C.byref(lv), C.byref(ub))
+        return lv.value, ub.value

@@ -1,0 +1,91 @@
+"""Build and load the HIP backend library (libav1r.so, C-ABI of include/av1r.h).
+
+The library is built in-tree for gfx950 with hipcc (no JIT cache): it is the product
+path, and loading fails loudly if it is missing -- there is no CPU fallback."""
+import ctypes as C
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+BUILD = os.path.join(PKG, "_build")
+LIB = os.path.join(BUILD, "libav1r.so")
+SRCS = ["recon.hip", "filters.hip", "av1r_host.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(ROOT, "include")]
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc"))]
+    deps += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, jobs=3):
+    """Compile every HIP/C++ source for gfx950 and link libav1r.so in-tree."""
+    if not force and not _stale():
+        return LIB
+    os.makedirs(BUILD, exist_ok=True)
+    procs, objs = [], []
+    for s in SRCS:
+        src = os.path.join(PKG, "csrc", s)
+        obj = os.path.join(BUILD, os.path.splitext(s)[0] + ".o")
+        cmd = [HIPCC] + FLAGS + (["-x", "hip"] if s.endswith(".cpp") else []) + ["-c", src, "-o", obj]
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+        if len(procs) >= jobs:
+            if procs.pop(0).wait() != 0:
+                raise RuntimeError("hipcc failed")
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    tmp = LIB + ".tmp"
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        raise RuntimeError(f"{LIB} is missing: run av1dec_amd.native.build() (hipcc, gfx950)")
+    l = C.CDLL(LIB)
+    vp, i, u8p = C.c_void_p, C.c_int, C.c_void_p
+    l.av1r_create.argtypes = [i, C.POINTER(vp)]
+    l.av1r_destroy.argtypes = [vp]
+    l.av1r_destroy.restype = None
+    l.av1r_decode_frame.argtypes = [vp, vp]
+    l.av1r_frame_begin.argtypes = [vp, vp]
+    l.av1r_submit_tile.argtypes = [vp, vp]
+    l.av1r_frame_end.argtypes = [vp]
+    l.av1r_show_existing.argtypes = [vp, i, i]
+    l.av1r_output_pending.argtypes = [vp]
+    l.av1r_get_output.argtypes = [vp, u8p, i, u8p, i, u8p, i, C.POINTER(i), C.POINTER(i)]
+    l.av1r_read_stage.argtypes = [vp, i, i, u8p, i]
+    l.av1r_synchronize.argtypes = [vp]
+    l.av1r_set_timing.argtypes = [vp, i]
+    l.av1r_set_keep_stages.argtypes = [vp, i]
+    l.av1r_last_frame_times.argtypes = [vp] + [C.POINTER(C.c_float)] * 4
+    l.av1r_last_frame_stats.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_uint64)]
+    l.av1r_last_error.argtypes = [vp]
+    l.av1r_last_error.restype = C.c_char_p
+    l.av1r_sizeof.argtypes = [i]
+    l.av1r_sizeof.restype = C.c_size_t
+    _lib = l
+    return l
+
+
+EXPORTS = [
+    "av1r_create", "av1r_destroy", "av1r_decode_frame", "av1r_frame_begin", "av1r_submit_tile",
+    "av1r_frame_end", "av1r_show_existing", "av1r_output_pending", "av1r_get_output",
+    "av1r_read_stage", "av1r_synchronize", "av1r_last_frame_times", "av1r_set_timing",
+    "av1r_set_keep_stages", "av1r_last_frame_stats", "av1r_last_error", "av1r_sizeof",
+]

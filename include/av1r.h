@@ -11,7 +11,7 @@
  * header, the per-4x4 mode-info grid, the coded blocks and transform blocks in decode
  * order, the non-zero quantized coefficients, palette maps, CDEF indices and loop
  * restoration unit parameters.  All structs are POD, little-endian, no padding holes
- * (sizes are asserted in av1r_abi.c / tests).
+ * (sizes: av1r_sizeof(); checked against the Python mirror in tests/test_abi.py).
  *
  * Enumerations (BLOCK_SIZE, TX_SIZE, TX_TYPE, PREDICTION_MODE, ...) use the numeric
  * values of the reference's aom/enums.h so a reference-side binding is a field copy.
@@ -82,6 +82,7 @@ typedef struct av1r_block {
     uint8_t wedge_index, wedge_sign;
     uint8_t mask_type;
     uint8_t ii_edge;           /* interintra block-level haveAboveRight(bit 2p) / haveBelowLeft(bit 2p+1) */
+    uint8_t pad0[2];
     uint32_t flags;            /* AV1R_BLK_*                                          */
     uint16_t max_luma_w, max_luma_h; /* MaxLumaW/H at chroma time (TransformBlock.cpp:2418-2421) */
     int32_t local_warp[6];     /* LocalWarpParams (Block.cpp:1116-1169) when AV1R_BLK_LOCAL_VALID */
@@ -230,7 +231,13 @@ int av1r_synchronize(av1r_ctx* ctx);
 int av1r_last_frame_times(av1r_ctx* ctx, float* recon_ms, float* lf_ms, float* cdef_ms,
                           float* lr_ms);
 int av1r_set_timing(av1r_ctx* ctx, int enable);
+/* Keep per-stage snapshots for av1r_read_stage (default on; costs 2 frame copies). */
+int av1r_set_keep_stages(av1r_ctx* ctx, int keep);
+/* Dependency levels (recon launches) and uploaded batch bytes of the last frame. */
+int av1r_last_frame_stats(av1r_ctx* ctx, int* levels, uint64_t* upload_bytes);
 const char* av1r_last_error(av1r_ctx* ctx);
+/* sizeof of the ABI structs: 0 hdr, 1 mi, 2 block, 3 tb, 4 lr_unit, 5 frame_batch. */
+size_t av1r_sizeof(int which);
 
 #ifdef __cplusplus
 }

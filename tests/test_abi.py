@@ -1,0 +1,49 @@
+"""The C-ABI library builds for gfx950, loads, exports every entry point of
+include/av1r.h, and its struct layouts match the Python mirror and the fixtures."""
+import ctypes as C
+import os
+import re
+
+import golden
+from av1dec_amd import abi, batchfile, native
+
+
+def declared_functions():
+    src = open(os.path.join(native.ROOT, "include", "av1r.h")).read()
+    return sorted(set(re.findall(r"\b(av1r_\w+)\s*\(", src)) - {"av1r_ctx"})
+
+
+def test_exports_every_declared_symbol(native_lib):
+    decl = declared_functions()
+    assert decl, "no declarations parsed"
+    for name in decl:
+        assert hasattr(native_lib, name), name
+    assert sorted(native.EXPORTS) == decl
+
+
+def test_struct_sizes(native_lib):
+    assert native_lib.av1r_sizeof(0) == C.sizeof(abi.FrameHdr)
+    assert native_lib.av1r_sizeof(1) == abi.SIZEOF_MI
+    assert native_lib.av1r_sizeof(2) == abi.SIZEOF_BLOCK
+    assert native_lib.av1r_sizeof(3) == abi.SIZEOF_TB
+    assert native_lib.av1r_sizeof(4) == abi.SIZEOF_LR_UNIT
+    assert native_lib.av1r_sizeof(5) == C.sizeof(abi.FrameBatch)
+
+
+def test_batchfile_roundtrip(tmp_path):
+    frames = batchfile.load(golden.batch_path("av1-1-b8-06-mfmv"))
+    p = tmp_path / "x.av1b.gz"
+    batchfile.write(p, frames)
+    again = batchfile.load(p)
+    assert len(again) == len(frames)
+    for a, b in zip(frames, again):
+        assert a.to_bytes() == b.to_bytes()
+        assert a.hdr.frame_width == 352 and a.n_tbs == b.n_tbs
+
+
+def test_fixture_records_are_whole(native_lib):
+    for s in ("64x64", "av1-1-b8-02-allintra", "Halo_426x240_1frames_intrabc"):
+        for fr in batchfile.load(golden.batch_path(s)):
+            assert fr.sec["blocks"].size % abi.SIZEOF_BLOCK == 0
+            assert fr.sec["tbs"].size % abi.SIZEOF_TB == 0
+            assert fr.sec["mi"].size == abi.SIZEOF_MI * fr.hdr.mi_stride * fr.hdr.mi_rows_alloc or fr.show_existing
