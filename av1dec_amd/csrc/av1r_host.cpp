@@ -89,6 +89,7 @@ struct av1r_ctx {
     int nLevelsLast = 0;
     // stats of the last frame
     uint64_t lastUploadBytes = 0;
+    bool skipSlotCheck = false;  // av1r_check_batch: no frame store to resolve against
 };
 
 static int fail(av1r_ctx* c, int code, const char* fmt, ...)
@@ -184,7 +185,7 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
         }
         if ((m.filt & 15) > 3 || (m.filt >> 4) > 3) return fail(c, AV1R_E_INVALID, "interp filter");
     }
-    for (int r = 1; r < 8; r++) {
+    for (int r = 1; r < 8 && !c->skipSlotCheck; r++) {
         if (!usedRef[r]) continue;
         int slot = h->ref_frame_idx[r - 1];
         if (slot < 0 || slot > 7 || !c->slots[slot])
@@ -204,14 +205,16 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                 return fail(c, AV1R_E_INVALID, "palette map size");
         }
         if (k.flags & AV1R_BLK_INTER) {
-            if (k.motion_mode > 2 || k.compound_type > 4 || k.interintra_mode > 3 || k.wedge_index > 15)
+            if (k.motion_mode > 2 || k.compound_type > 4 || k.interintra_mode > 3
+                || (k.compound_type == AV1R_COMPOUND_WEDGE && k.wedge_index > 15))
                 return fail(c, AV1R_E_INVALID, "block %u inter params", i);
             if (k.compound_type == AV1R_COMPOUND_WEDGE && !av1r_wedge_bits[k.mi_size])
                 return fail(c, AV1R_E_INVALID, "wedge on a block size without wedges");
             if (k.flags & AV1R_BLK_INTERINTRA)
                 if (k.mi_size < AV1R_BLOCK_8X8 || k.mi_size > AV1R_BLOCK_32X32) return fail(c, AV1R_E_INVALID, "interintra size");
         } else {
-            if (k.y_mode > AV1R_PAETH_PRED || k.uv_mode > AV1R_UV_CFL_PRED || k.filter_intra_mode > 4)
+            if (k.y_mode > AV1R_PAETH_PRED || ((k.flags & AV1R_BLK_HAS_CHROMA) && k.uv_mode > AV1R_UV_CFL_PRED)
+                || ((k.flags & AV1R_BLK_FILTER_INTRA) && k.filter_intra_mode > 4))
                 return fail(c, AV1R_E_INVALID, "block %u intra modes", i);
         }
     }
@@ -721,6 +724,20 @@ int av1r_last_frame_stats(av1r_ctx* c, int* levels, uint64_t* uploadBytes)
 }
 
 const char* av1r_last_error(av1r_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+// Host-only validation + scheduling of a batch (no device): returns the status and, on
+// success, the number of dependency levels.  Used by the CPU test-suite.
+int av1r_check_batch(const av1r_frame_batch* b, int* levels, char* err, int errLen)
+{
+    if (!b || !b->hdr) return AV1R_E_INVALID;
+    av1r_ctx c;
+    c.skipSlotCheck = true;
+    int rc = b->hdr->show_existing_frame ? AV1R_OK : validate(&c, b);
+    if (!rc && !b->hdr->show_existing_frame) build_schedule(&c, b);
+    if (levels) *levels = rc ? 0 : c.nLevelsLast;
+    if (err && errLen > 0) snprintf(err, errLen, "%s", c.err.c_str());
+    return rc;
+}
 
 size_t av1r_sizeof(int which)
 {

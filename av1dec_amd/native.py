@@ -77,6 +77,7 @@ def lib():
     l.av1r_last_frame_stats.argtypes = [vp, C.POINTER(i), C.POINTER(C.c_uint64)]
     l.av1r_last_error.argtypes = [vp]
     l.av1r_last_error.restype = C.c_char_p
+    l.av1r_check_batch.argtypes = [vp, C.POINTER(i), C.c_char_p, i]
     l.av1r_sizeof.argtypes = [i]
     l.av1r_sizeof.restype = C.c_size_t
     _lib = l
@@ -88,4 +89,5 @@ EXPORTS = [
     "av1r_frame_end", "av1r_show_existing", "av1r_output_pending", "av1r_get_output",
     "av1r_read_stage", "av1r_synchronize", "av1r_last_frame_times", "av1r_set_timing",
     "av1r_set_keep_stages", "av1r_last_frame_stats", "av1r_last_error", "av1r_sizeof",
+    "av1r_check_batch",
 ]

@@ -236,6 +236,9 @@ int av1r_set_keep_stages(av1r_ctx* ctx, int keep);
 /* Dependency levels (recon launches) and uploaded batch bytes of the last frame. */
 int av1r_last_frame_stats(av1r_ctx* ctx, int* levels, uint64_t* upload_bytes);
 const char* av1r_last_error(av1r_ctx* ctx);
+/* Host-only check of a batch: validation + dependency schedule, no device needed.
+ * Returns the status; *levels = recon launch levels.  err receives the message. */
+int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);
 /* sizeof of the ABI structs: 0 hdr, 1 mi, 2 block, 3 tb, 4 lr_unit, 5 frame_batch. */
 size_t av1r_sizeof(int which);
 

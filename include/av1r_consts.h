@@ -50,7 +50,7 @@ enum { AV1R_RESTORE_NONE, AV1R_RESTORE_WIENER, AV1R_RESTORE_SGRPROJ, AV1R_RESTOR
 #define AV1R_INTRA_FRAME 0
 #define AV1R_MAX_FRAME_DISTANCE 31
 
-#ifdef __HIPCC__
+#if defined(__HIP_DEVICE_COMPILE__)
 #define AV1R_CT __device__ __constant__
 #else
 #define AV1R_CT

@@ -123,7 +123,7 @@ struct Dumper {
         r.mi_size = b.MiSize;
         r.qindex = (uint8_t)b.m_frame.get_qindex(b.CurrentQIndex, b.segment_id);
         r.y_mode = b.YMode;
-        r.uv_mode = b.UVMode;
+        r.uv_mode = b.HasChroma ? b.UVMode : 0;
         r.angle_delta_y = b.AngleDeltaY;
         r.angle_delta_uv = b.AngleDeltaUV;
         r.filter_intra_mode = b.use_filter_intra ? b.filter_intra_mode : 0;
@@ -137,9 +137,14 @@ struct Dumper {
             r.motion_mode = b.motion_mode;
             r.compound_type = b.compound_type;
             r.interintra_mode = (b.interintra && !b.use_intrabc) ? b.interintra_mode : 0;
-            r.wedge_index = b.wedge_index;
-            r.wedge_sign = b.wedge_sign;
-            r.mask_type = b.mask_type;
+            // only the fields the reference reads for this compound type (others may be
+            // uninitialised members of Block)
+            if (b.compound_type == COMPOUND_WEDGE) {
+                r.wedge_index = b.wedge_index;
+                r.wedge_sign = b.wedge_sign;
+            }
+            if (b.compound_type == COMPOUND_DIFFWTD)
+                r.mask_type = b.mask_type;
             if (b.interintra && !b.use_intrabc)
                 f |= AV1R_BLK_INTERINTRA;
             if (b.interintra && !b.use_intrabc && b.wedge_interintra)

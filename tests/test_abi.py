@@ -47,3 +47,35 @@ def test_fixture_records_are_whole(native_lib):
             assert fr.sec["blocks"].size % abi.SIZEOF_BLOCK == 0
             assert fr.sec["tbs"].size % abi.SIZEOF_TB == 0
             assert fr.sec["mi"].size == abi.SIZEOF_MI * fr.hdr.mi_stride * fr.hdr.mi_rows_alloc or fr.show_existing
+
+
+def test_host_validation_and_schedule_on_all_fixtures(native_lib):
+    """Every committed batch passes the backend's host-side validation (the checks that
+    guard every index a kernel follows) and yields a dependency schedule."""
+    import ctypes as C
+    err = C.create_string_buffer(256)
+    for s in golden.streams():
+        for i, fr in enumerate(batchfile.load(golden.batch_path(s))):
+            lv = C.c_int()
+            rc = native_lib.av1r_check_batch(C.cast(fr.byref(), C.c_void_p), C.byref(lv), err, 256)
+            assert rc == 0, f"{s} frame {i}: {err.value.decode()}"
+            if not fr.show_existing:
+                assert lv.value >= 1
+
+
+def test_validation_rejects_bad_batches(native_lib):
+    import ctypes as C
+    import numpy as np
+    fr = batchfile.load(golden.batch_path("av1-1-b8-06-mfmv"))[1]
+    err = C.create_string_buffer(256)
+    tb = np.frombuffer(fr.sec["tbs"].tobytes(), abi.TB_DTYPE).copy()
+    tb["block"][3] = 10 ** 6
+    secs = dict(fr.sec)
+    secs["tbs"] = tb.view(np.uint8).ravel()
+    bad = batchfile.Frame(secs)
+    assert native_lib.av1r_check_batch(C.cast(bad.byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_INVALID
+    hdr = abi.FrameHdr.from_buffer_copy(fr.sec["hdr"].tobytes())
+    hdr.bitdepth = 10
+    secs = dict(fr.sec)
+    secs["hdr"] = np.frombuffer(bytes(hdr), np.uint8).copy()
+    assert native_lib.av1r_check_batch(C.cast(batchfile.Frame(secs).byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_UNSUPPORTED
