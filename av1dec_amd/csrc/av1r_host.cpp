@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -28,7 +29,7 @@ void launch_k_tb(const KParams& k, unsigned n, hipStream_t s);
 void launch_k_inter(const KParams& k, unsigned n, hipStream_t s);
 void launch_k_lf(const KParams& k, int pass, int nY, int nC, int cCols, int planeMask, hipStream_t s);
 void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s);
-void launch_k_lr(const KParams& k, int plane, hipStream_t s);
+void launch_k_lr(const KParams& k, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 
 namespace {
@@ -55,6 +56,19 @@ struct Level {
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 }  // namespace
+
+// A frame whose batch and schedule are resident in device memory.
+struct Prepared {
+    uint8_t* dev = nullptr;  // owned buffer (prepared frames) or ring slot (streaming)
+    size_t cap = 0;
+    bool owned = false;
+    av1r_frame_hdr hdr;
+    KParams base;  // batch pointers into dev
+    const uint32_t* dItems = nullptr;
+    std::vector<Level> levels;
+    bool usedRef[8] = {};
+    uint64_t bytes = 0;
+};
 
 struct av1r_ctx {
     int device = 0;
@@ -83,13 +97,18 @@ struct av1r_ctx {
     std::vector<av1r_tb> fTbs;
     std::vector<uint32_t> fCoefs;
     std::vector<uint8_t> fPal;
-    // timing
+    // timing: one set of 5 stage-boundary events per frame since the last summary
     bool timing = false;
     hipEvent_t ev[5] = {};
+    std::vector<std::array<hipEvent_t, 5>> evPool;
+    size_t evUsed = 0;
     int nLevelsLast = 0;
     // stats of the last frame
     uint64_t lastUploadBytes = 0;
     bool skipSlotCheck = false;  // av1r_check_batch: no frame store to resolve against
+    bool discardOutput = false;  // bench: shown frames are not queued for read-back
+    Prepared streamP;
+    std::vector<Prepared*> prepared;
 };
 
 static int fail(av1r_ctx* c, int code, const char* fmt, ...)
@@ -363,14 +382,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
 }
 
 // ------------------------------------------------------------------------------------
-static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
+// validate + schedule + pack into `host` (capacity checked by caller via size query)
+static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8_t* host, uint8_t* dev, size_t* need)
 {
     const av1r_frame_hdr* h = b->hdr;
-    int rc = validate(c, b);
-    if (rc) return rc;
-    build_schedule(c, b);
-
-    // ---- one pinned staging buffer -> one H2D copy
     const size_t szHdr = align256(sizeof(av1r_frame_hdr));
     const size_t szMi = align256(sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc);
     const size_t szBlk = align256(sizeof(av1r_block) * (size_t)b->n_blocks);
@@ -380,29 +395,16 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
     const size_t szCdef = align256((size_t)h->cdef_rows * h->cdef_cols);
     const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
     const size_t szItems = align256(4 * c->items.size() + 4);
-    const size_t total = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems;
-    Upload& U = c->up[c->upIdx];
-    c->upIdx ^= 1;
-    if (U.pending) {
-        HIPCHK(hipEventSynchronize(U.done));
-        U.pending = false;
-    }
-    if (U.cap < total) {
-        if (U.host) (void)hipHostFree(U.host);
-        if (U.dev) (void)hipFree(U.dev);
-        size_t cap = total + total / 2;
-        HIPCHK(hipHostMalloc(&U.host, cap));
-        HIPCHK(hipMalloc(&U.dev, cap));
-        U.cap = cap;
-    }
+    *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems;
+    if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {
-        if (n) memcpy(U.host + off, src, n);
+        if (n) memcpy(host + off, src, n);
         size_t o = off;
         off += sz;
-        return U.dev + o;
+        return dev + o;
     };
-    KParams k;
+    KParams& k = P.base;
     memset(&k, 0, sizeof(k));
     k.hdr = (const av1r_frame_hdr*)put(h, sizeof(av1r_frame_hdr), szHdr);
     k.mi = (const av1r_mi*)put(b->mi, sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc, szMi);
@@ -412,31 +414,59 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
     k.palette = put(b->palette, b->n_palette, szPal);
     k.cdef_idx = (const int8_t*)put(b->cdef_idx, (size_t)h->cdef_rows * h->cdef_cols, szCdef);
     k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
-    const uint32_t* dItems = (const uint32_t*)put(c->items.data(), 4 * c->items.size(), szItems);
-    c->lastUploadBytes = off;
-    HIPCHK(hipMemcpyAsync(U.dev, U.host, off, hipMemcpyHostToDevice, c->stream));
+    P.dItems = (const uint32_t*)put(c->items.data(), 4 * c->items.size(), szItems);
     k.mi_stride = h->mi_stride;
     k.mi_cols = h->mi_cols;
     k.mi_rows = h->mi_rows;
     k.frame_w = h->frame_width;
     k.frame_h = h->frame_height;
+    P.hdr = *h;
+    P.levels = c->levels;
+    P.bytes = off;
+    memset(P.usedRef, 0, sizeof(P.usedRef));
+    for (int i = 0; i < h->mi_stride * h->mi_rows_alloc; i++)
+        for (int l = 0; l < 2; l++)
+            if (b->mi[i].ref_frame[l] > 0) P.usedRef[b->mi[i].ref_frame[l]] = true;
+    return AV1R_OK;
+}
+
+// recon -> LF -> CDEF -> LR on the context stream, then output / frame-store update.
+static int launch_frame(av1r_ctx* c, const Prepared& P)
+{
+    const av1r_frame_hdr* h = &P.hdr;
+    for (int r = 1; r < 8; r++) {
+        if (!P.usedRef[r]) continue;
+        int slot = h->ref_frame_idx[r - 1];
+        if (slot < 0 || slot > 7 || !c->slots[slot])
+            return fail(c, AV1R_E_INVALID, "reference %d maps to an empty slot", r);
+    }
+    KParams k = P.base;
     for (int s = 0; s < 8; s++)
         if (c->slots[s]) k.ref[s] = c->slots[s]->d;
-
+    int rc;
     FrameBuf* R = frame_get(c, h->frame_width, h->frame_height);
     if (!R) return fail(c, AV1R_E_NOMEM, "frame allocation");
     k.cur = R->d;
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    if (c->timing) {
+        if (c->evUsed == c->evPool.size()) {
+            std::array<hipEvent_t, 5> e;
+            for (auto& x : e) HIPCHK(hipEventCreate(&x));
+            c->evPool.push_back(e);
+        }
+        for (int i = 0; i < 5; i++) c->ev[i] = c->evPool[c->evUsed][i];
+        c->evUsed++;
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    }
 
     // ---- reconstruction, level by level
-    for (const Level& L : c->levels) {
+    for (const Level& L : P.levels) {
         if (L.pCnt) {
-            k.items = dItems + L.pOff;
+            k.items = P.dItems + L.pOff;
             k.n_items = L.pCnt;
             launch_k_inter(k, L.pCnt, c->stream);
         }
         if (L.tCnt) {
-            k.items = dItems + L.tOff;
+            k.items = P.dItems + L.tOff;
             k.n_items = L.tCnt;
             launch_k_tb(k, L.tCnt, c->stream);
         }
@@ -489,7 +519,7 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
         kl.cur = C->d;
         kl.ref[0] = R->d;
         kl.out = L->d;
-        for (int p = 0; p < 3; p++) launch_k_lr(kl, p, c->stream);
+        launch_k_lr(kl, c->stream);
         out = L;
         frame_unref(c, C);
     }
@@ -500,10 +530,8 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
     }
     if (c->timing) HIPCHK(hipEventRecord(c->ev[4], c->stream));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(U.done, c->stream));
-    U.pending = true;
     frame_unref(c, R);
-    if (h->show_frame) {
+    if (h->show_frame && !c->discardOutput) {
         frame_ref(out);
         c->outq.push_back(out);
     }
@@ -514,6 +542,42 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
             c->slots[i] = out;
         }
     frame_unref(c, out);
+    c->nLevelsLast = (int)P.levels.size();
+    c->lastUploadBytes = P.bytes;
+    return AV1R_OK;
+}
+
+// streaming path: one pinned staging buffer -> one async H2D copy (ring of 2)
+static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    c->skipSlotCheck = true;  // slot presence is checked at launch time
+    int rc = validate(c, b);
+    c->skipSlotCheck = false;
+    if (rc) return rc;
+    build_schedule(c, b);
+    Prepared& P = c->streamP;
+    size_t need = 0;
+    pack_frame(c, b, P, nullptr, nullptr, &need);
+    Upload& U = c->up[c->upIdx];
+    c->upIdx ^= 1;
+    if (U.pending) {
+        HIPCHK(hipEventSynchronize(U.done));
+        U.pending = false;
+    }
+    if (U.cap < need) {
+        if (U.host) (void)hipHostFree(U.host);
+        if (U.dev) (void)hipFree(U.dev);
+        size_t cap = need + need / 2;
+        HIPCHK(hipHostMalloc(&U.host, cap));
+        HIPCHK(hipMalloc(&U.dev, cap));
+        U.cap = cap;
+    }
+    pack_frame(c, b, P, U.host, U.dev, &need);
+    HIPCHK(hipMemcpyAsync(U.dev, U.host, need, hipMemcpyHostToDevice, c->stream));
+    rc = launch_frame(c, P);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(U.done, c->stream));
+    U.pending = true;
     return AV1R_OK;
 }
 
@@ -536,6 +600,7 @@ int av1r_create(int device, av1r_ctx** out)
     }
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
     for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
+    c->evPool.reserve(64);
     *out = c;
     return AV1R_OK;
 }
@@ -554,7 +619,13 @@ void av1r_destroy(av1r_ctx* c)
         if (u.dev) (void)hipFree(u.dev);
         (void)hipEventDestroy(u.done);
     }
-    for (auto& e : c->ev) (void)hipEventDestroy(e);
+    for (auto& e : c->evPool)
+        for (auto& x : e) (void)hipEventDestroy(x);
+    for (Prepared* P : c->prepared)
+        if (P) {
+            if (P->dev) (void)hipFree(P->dev);
+            delete P;
+        }
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -628,13 +699,77 @@ int av1r_frame_end(av1r_ctx* c)
     return av1r_decode_frame(c, &b);
 }
 
+int av1r_prepare(av1r_ctx* c, const av1r_frame_batch* b, int* handle)
+{
+    if (!c || !b || !b->hdr || !handle) return AV1R_E_INVALID;
+    if (b->hdr->version != AV1R_VERSION) return fail(c, AV1R_E_INVALID, "batch version %u", b->hdr->version);
+    (void)hipSetDevice(c->device);
+    Prepared* P = new Prepared;
+    P->hdr = *b->hdr;
+    if (!b->hdr->show_existing_frame) {
+        c->skipSlotCheck = true;
+        int rc = validate(c, b);
+        c->skipSlotCheck = false;
+        if (rc) {
+            delete P;
+            return rc;
+        }
+        build_schedule(c, b);
+        size_t need = 0;
+        pack_frame(c, b, *P, nullptr, nullptr, &need);
+        std::vector<uint8_t> host(need);
+        if (hipMalloc(&P->dev, need) != hipSuccess) {
+            delete P;
+            return fail(c, AV1R_E_NOMEM, "prepared batch allocation");
+        }
+        P->owned = true;
+        P->cap = need;
+        pack_frame(c, b, *P, host.data(), P->dev, &need);
+        if (hipMemcpy(P->dev, host.data(), need, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(P->dev);
+            delete P;
+            return fail(c, AV1R_E_DEVICE, "prepared batch upload");
+        }
+    }
+    c->prepared.push_back(P);
+    *handle = (int)c->prepared.size() - 1;
+    return AV1R_OK;
+}
+
+int av1r_decode_prepared(av1r_ctx* c, int handle)
+{
+    if (!c || handle < 0 || handle >= (int)c->prepared.size() || !c->prepared[handle]) return AV1R_E_INVALID;
+    (void)hipSetDevice(c->device);
+    const Prepared& P = *c->prepared[handle];
+    if (P.hdr.show_existing_frame) return av1r_show_existing(c, P.hdr.frame_to_show, P.hdr.refresh_frame_flags);
+    return launch_frame(c, P);
+}
+
+int av1r_release_prepared(av1r_ctx* c, int handle)
+{
+    if (!c || handle < 0 || handle >= (int)c->prepared.size() || !c->prepared[handle]) return AV1R_E_INVALID;
+    (void)hipStreamSynchronize(c->stream);
+    if (c->prepared[handle]->dev) (void)hipFree(c->prepared[handle]->dev);
+    delete c->prepared[handle];
+    c->prepared[handle] = nullptr;
+    return AV1R_OK;
+}
+
+int av1r_set_discard_output(av1r_ctx* c, int discard)
+{
+    if (!c) return AV1R_E_INVALID;
+    c->discardOutput = discard != 0;
+    return AV1R_OK;
+}
+
 int av1r_show_existing(av1r_ctx* c, int slot, int refresh)
 {
     if (!c || slot < 0 || slot > 7 || !c->slots[slot]) return AV1R_E_INVALID;
     FrameBuf* f = c->slots[slot];
     frame_ref(f);  // hold across the refresh
     frame_ref(f);
-    c->outq.push_back(f);
+    if (!c->discardOutput) c->outq.push_back(f);
+    else frame_unref(c, f);
     for (int i = 0; i < 8; i++)
         if (refresh & (1 << i)) {
             frame_ref(f);
@@ -704,7 +839,7 @@ int av1r_set_keep_stages(av1r_ctx* c, int keep)
 
 int av1r_last_frame_times(av1r_ctx* c, float* recon, float* lf, float* cdef, float* lr)
 {
-    if (!c || !c->timing) return AV1R_E_INVALID;
+    if (!c || !c->timing || !c->evUsed) return AV1R_E_INVALID;
     HIPCHK(hipEventSynchronize(c->ev[4]));
     float t[4] = {};
     for (int i = 0; i < 4; i++) HIPCHK(hipEventElapsedTime(&t[i], c->ev[i], c->ev[i + 1]));
@@ -712,6 +847,22 @@ int av1r_last_frame_times(av1r_ctx* c, float* recon, float* lf, float* cdef, flo
     if (lf) *lf = t[1];
     if (cdef) *cdef = t[2];
     if (lr) *lr = t[3];
+    return AV1R_OK;
+}
+
+int av1r_stage_times(av1r_ctx* c, float* totals, int* frames)
+{
+    if (!c || !totals) return AV1R_E_INVALID;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 4; i++) totals[i] = 0.f;
+    for (size_t f = 0; f < c->evUsed; f++)
+        for (int i = 0; i < 4; i++) {
+            float t = 0.f;
+            HIPCHK(hipEventElapsedTime(&t, c->evPool[f][i], c->evPool[f][i + 1]));
+            totals[i] += t;
+        }
+    if (frames) *frames = (int)c->evUsed;
+    c->evUsed = 0;
     return AV1R_OK;
 }
 

@@ -335,10 +335,11 @@ DEV int sgr_filter(const LrPix& S, const DevPlane& cdefP, int x, int y, int i, i
     return r2(v, 8 + shift - 4);
 }
 
-// one lane per visible pixel of plane `plane`; k.cur = CDEF frame, k.ref[0] = deblocked
-// frame, k.out = restored frame.
-extern "C" __global__ __launch_bounds__(256) void k_lr(KParams k, int plane)
+// one lane per visible pixel, all planes in one launch (blockIdx.z = plane);
+// k.cur = CDEF frame, k.ref[0] = deblocked frame, k.out = restored frame.
+extern "C" __global__ __launch_bounds__(256) void k_lr(KParams k)
 {
+    const int plane = blockIdx.z;
     const DevPlane C = k.cur.pl[plane];
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
@@ -418,10 +419,10 @@ void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s)
 {
     hipLaunchKernelGGL(k_cdef, dim3((nBlocks + 3) / 4), dim3(256), 0, s, k, nBlocks, bCols);
 }
-void launch_k_lr(const KParams& k, int plane, hipStream_t s)
+void launch_k_lr(const KParams& k, hipStream_t s)
 {
-    const DevPlane& p = k.cur.pl[plane];
-    hipLaunchKernelGGL(k_lr, dim3((p.w + 63) / 64, (p.h + 3) / 4), dim3(256), 0, s, k, plane);
+    const DevPlane& p = k.cur.pl[0];
+    hipLaunchKernelGGL(k_lr, dim3((p.w + 63) / 64, (p.h + 3) / 4, 3), dim3(256), 0, s, k);
 }
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s)
 {

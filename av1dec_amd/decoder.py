@@ -53,6 +53,21 @@ class Decoder:
             self._check(self.l.av1r_submit_tile(self.c, C.cast(t.byref(), C.c_void_p)), "av1r_submit_tile")
         self._check(self.l.av1r_frame_end(self.c), "av1r_frame_end")
 
+    def prepare(self, frame):
+        """Validate, schedule and upload a frame batch to HBM; returns a handle."""
+        h = C.c_int()
+        self._check(self.l.av1r_prepare(self.c, C.cast(frame.byref(), C.c_void_p), C.byref(h)), "av1r_prepare")
+        return h.value
+
+    def decode_prepared(self, handle):
+        self._check(self.l.av1r_decode_prepared(self.c, handle), "av1r_decode_prepared")
+
+    def release_prepared(self, handle):
+        self._check(self.l.av1r_release_prepared(self.c, handle), "av1r_release_prepared")
+
+    def set_discard_output(self, discard):
+        self._check(self.l.av1r_set_discard_output(self.c, int(discard)), "av1r_set_discard_output")
+
     def synchronize(self):
         self._check(self.l.av1r_synchronize(self.c), "av1r_synchronize")
 
@@ -85,6 +100,13 @@ class Decoder:
         t = [C.c_float() for _ in range(4)]
         self._check(self.l.av1r_last_frame_times(self.c, *[C.byref(x) for x in t]), "av1r_last_frame_times")
         return [x.value for x in t]
+
+    def stage_times(self):
+        """(totals_ms[recon, lf, cdef, lr], frames) since the previous call (timing=True)."""
+        t = (C.c_float * 4)()
+        n = C.c_int()
+        self._check(self.l.av1r_stage_times(self.c, t, C.byref(n)), "av1r_stage_times")
+        return list(t), n.value
 
     def last_frame_stats(self):
         lv, ub = C.c_int(), C.c_uint64()

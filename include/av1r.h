@@ -213,6 +213,14 @@ int av1r_frame_begin(av1r_ctx* ctx, const av1r_frame_batch* frame_level);
 int av1r_submit_tile(av1r_ctx* ctx, const av1r_frame_batch* tile);
 int av1r_frame_end(av1r_ctx* ctx);
 
+/* Device-resident frames: validate, schedule and upload a batch once (outside any
+ * timed region), then decode it from HBM.  Handles stay valid until released. */
+int av1r_prepare(av1r_ctx* ctx, const av1r_frame_batch* batch, int* handle);
+int av1r_decode_prepared(av1r_ctx* ctx, int handle);
+int av1r_release_prepared(av1r_ctx* ctx, int handle);
+/* Do not queue shown frames for read-back (they still refresh the reference store). */
+int av1r_set_discard_output(av1r_ctx* ctx, int discard);
+
 /* show_existing_frame: queue slot `slot` for output and refresh per `refresh_flags`. */
 int av1r_show_existing(av1r_ctx* ctx, int slot, int refresh_flags);
 
@@ -231,6 +239,9 @@ int av1r_synchronize(av1r_ctx* ctx);
 int av1r_last_frame_times(av1r_ctx* ctx, float* recon_ms, float* lf_ms, float* cdef_ms,
                           float* lr_ms);
 int av1r_set_timing(av1r_ctx* ctx, int enable);
+/* With timing on: synchronise, return the summed device time (ms) of the recon / LF /
+ * CDEF / LR stages of every frame launched since the previous call, and reset. */
+int av1r_stage_times(av1r_ctx* ctx, float* totals4, int* frames);
 /* Keep per-stage snapshots for av1r_read_stage (default on; costs 2 frame copies). */
 int av1r_set_keep_stages(av1r_ctx* ctx, int keep);
 /* Dependency levels (recon launches) and uploaded batch bytes of the last frame. */

@@ -1,0 +1,93 @@
+"""Synthetic bench workload (tools/synth): deterministic, valid batches, and -- on the
+GPU -- bit-exact with the CPU oracle at the bench's full 1080p size and the 4K 4x2-tile
+configuration (BASELINE.json configs[2], configs[3])."""
+import ctypes as C
+import hashlib
+
+import pytest
+
+import pyoracle
+import pysynth
+from av1dec_amd import Decoder
+
+
+def test_generator_deterministic():
+    a = pysynth.stream(352, 288, 3, 11)
+    b = pysynth.stream(352, 288, 3, 11)
+    c = pysynth.stream(352, 288, 3, 12)
+    assert [f.to_bytes() for f in a] == [f.to_bytes() for f in b]
+    assert a[1].to_bytes() != c[1].to_bytes()
+
+
+@pytest.mark.parametrize("w,h,tiles", [(352, 288, (1, 1)), (640, 360, (2, 2))])
+def test_generated_batches_validate(native_lib, w, h, tiles):
+    err = C.create_string_buffer(256)
+    for f in pysynth.stream(w, h, 4, 5, tiles=tiles):
+        lv = C.c_int()
+        assert native_lib.av1r_check_batch(C.cast(f.byref(), C.c_void_p), C.byref(lv), err, 256) == 0, err.value
+        assert lv.value >= 1
+
+
+def test_oracle_runs_synthetic():
+    o = pyoracle.Oracle(keep_stages=False)
+    for f in pysynth.stream(352, 288, 3, 3):
+        o.decode_frame(f)
+    n = 0
+    while o.output_pending():
+        y, u, v = o.get_output()
+        assert y.shape == (288, 352)
+        n += 1
+    assert n == 3
+
+
+def compare_gpu_oracle(frames, stages=True):
+    d = Decoder(0, keep_stages=stages)
+    o = pyoracle.Oracle(keep_stages=stages)
+    for i, f in enumerate(frames):
+        d.decode_frame(f)
+        o.decode_frame(f)
+        if stages:
+            for st in range(4):
+                a = d.read_stage(st)
+                b = o.read_stage(st)
+                for p in range(3):
+                    assert (a[p] == b[p]).all(), f"frame {i} stage {st} plane {p}"
+    n = 0
+    while o.output_pending():
+        a = d.get_output()
+        b = o.get_output()
+        for x, y in zip(a, b):
+            assert hashlib.md5(x.tobytes()).digest() == hashlib.md5(y.tobytes()).digest(), f"output {n}"
+        n += 1
+    assert d.output_pending() == 0
+    d.close()
+    return n
+
+
+@pytest.mark.gpu
+def test_gpu_synth_cif_all_stages():
+    assert compare_gpu_oracle(pysynth.stream(352, 288, 8, 21)) == 8
+
+
+@pytest.mark.gpu
+def test_gpu_synth_1080p():
+    assert compare_gpu_oracle(pysynth.stream(1920, 1080, 4, 0x5EED0001), stages=True) == 4
+
+
+@pytest.mark.gpu
+def test_gpu_synth_4k_tiles():
+    assert compare_gpu_oracle(pysynth.stream(3840, 2160, 2, 0x5EED0002, tiles=(4, 2)), stages=False) == 2
+
+
+@pytest.mark.gpu
+def test_gpu_prepared_path_matches_streaming():
+    frames = pysynth.stream(640, 360, 5, 9)
+    d1 = Decoder(0)
+    d2 = Decoder(0)
+    hs = [d2.prepare(f) for f in frames]
+    for f, hd in zip(frames, hs):
+        d1.decode_frame(f)
+        d2.decode_prepared(hd)
+    while d1.output_pending():
+        for x, y in zip(d1.get_output(), d2.get_output()):
+            assert (x == y).all()
