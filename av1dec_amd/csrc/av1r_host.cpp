@@ -26,7 +26,7 @@
 #include "av1r_dev.h"
 
 void launch_k_tb(const KParams& k, unsigned n, hipStream_t s);
-void launch_k_inter(const KParams& k, unsigned n, hipStream_t s);
+void launch_k_inter(const KParams& k, unsigned n, int large, hipStream_t s);
 void launch_k_lf(const KParams& k, int pass, int nY, int nC, int cCols, int planeMask, hipStream_t s);
 void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s);
 void launch_k_lr(const KParams& k, hipStream_t s);
@@ -50,7 +50,7 @@ struct Upload {
 };
 
 struct Level {
-    uint32_t pOff = 0, pCnt = 0, tOff = 0, tCnt = 0;
+    uint32_t pOff = 0, pCnt = 0, lOff = 0, lCnt = 0, tOff = 0, tCnt = 0;  // small / large inter blocks, TBs
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -84,7 +84,7 @@ struct av1r_ctx {
     // schedule scratch
     std::vector<int16_t> lvlmap[3];
     int mapW[3] = {}, mapH[3] = {};
-    std::vector<std::vector<uint32_t>> lvP, lvT;
+    std::vector<std::vector<uint32_t>> lvP, lvL, lvT;
     std::vector<uint32_t> items;
     std::vector<Level> levels;
     // split submission (frame_begin / submit_tile / frame_end)
@@ -285,6 +285,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
     }
     c->lvP.clear();
+    c->lvL.clear();
     c->lvT.clear();
     auto region_max = [&](int p, int x0, int y0, int x1, int y1) {  // inclusive unit rect
         x0 = std::max(x0, 0);
@@ -331,7 +332,8 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
                 }
             }
             pLevel = dep + 1;
-            push(c->lvP, pLevel, bi);
+            const bool large = av1r_num4x4w[blk.mi_size] > 8 || av1r_num4x4h[blk.mi_size] > 8;
+            push(large ? c->lvL : c->lvP, pLevel, bi);
             globalMax = std::max(globalMax, pLevel);
             for (int p = 0; p < nPlanes; p++) {
                 int sub = p ? 1 : 0;
@@ -365,8 +367,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             region_set(p, x4, y4, w4, h4, lv);
         }
     }
-    size_t nl = std::max(c->lvP.size(), c->lvT.size());
+    size_t nl = std::max(std::max(c->lvP.size(), c->lvL.size()), c->lvT.size());
     c->lvP.resize(nl);
+    c->lvL.resize(nl);
     c->lvT.resize(nl);
     c->items.clear();
     c->levels.assign(nl, Level());
@@ -374,6 +377,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         c->levels[l].pOff = (uint32_t)c->items.size();
         c->levels[l].pCnt = (uint32_t)c->lvP[l].size();
         c->items.insert(c->items.end(), c->lvP[l].begin(), c->lvP[l].end());
+        c->levels[l].lOff = (uint32_t)c->items.size();
+        c->levels[l].lCnt = (uint32_t)c->lvL[l].size();
+        c->items.insert(c->items.end(), c->lvL[l].begin(), c->lvL[l].end());
         c->levels[l].tOff = (uint32_t)c->items.size();
         c->levels[l].tCnt = (uint32_t)c->lvT[l].size();
         c->items.insert(c->items.end(), c->lvT[l].begin(), c->lvT[l].end());
@@ -460,10 +466,15 @@ static int launch_frame(av1r_ctx* c, const Prepared& P)
 
     // ---- reconstruction, level by level
     for (const Level& L : P.levels) {
+        if (L.lCnt) {
+            k.items = P.dItems + L.lOff;
+            k.n_items = L.lCnt;
+            launch_k_inter(k, L.lCnt, 1, c->stream);
+        }
         if (L.pCnt) {
             k.items = P.dItems + L.pOff;
             k.n_items = L.pCnt;
-            launch_k_inter(k, L.pCnt, c->stream);
+            launch_k_inter(k, L.pCnt, 0, c->stream);
         }
         if (L.tCnt) {
             k.items = P.dItems + L.tOff;

@@ -110,7 +110,7 @@ DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) 
 
 // Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps).
 // `src` is the frame plane being reconstructed.  Ends with a __syncthreads().
-DEV void coop_intra_predict(const KParams& k, const DevPlane& src, const IntraParams& P,
+DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const IntraParams& P,
     IntraLds& L, uint8_t* pred, int ps)
 {
     const int t = threadIdx.x, nt = blockDim.x;
@@ -118,8 +118,8 @@ DEV void coop_intra_predict(const KParams& k, const DevPlane& src, const IntraPa
     const int plane = P.plane, x = P.x, y = P.y;
     // predict_intra uses subsampling_x for both axes (IntraPredict.cpp:566-567)
     const int sub = plane ? 1 : 0;
-    const int maxX = ((k.mi_cols * 4) >> sub) - 1;
-    const int maxY = ((k.mi_rows * 4) >> sub) - 1;
+    const int maxX = ((miCols * 4) >> sub) - 1;
+    const int maxY = ((miRows * 4) >> sub) - 1;
     uint8_t* above = L.above + EDGE_OFF;
     uint8_t* left = L.left + EDGE_OFF;
     const int n = w + h;
@@ -193,8 +193,8 @@ DEV void coop_intra_predict(const KParams& k, const DevPlane& src, const IntraPa
     const int mode = P.mode;
     if (mode >= AV1R_V_PRED && mode <= AV1R_D67_PRED) {
         // directionalIntraPredict (IntraPredict.cpp:379-483)
-        const int maxXd = (k.mi_cols * 4) >> sub;
-        const int maxYd = (k.mi_rows * 4) >> sub;  // subsampling_y == subsampling_x (4:2:0)
+        const int maxXd = (miCols * 4) >> sub;
+        const int maxYd = (miRows * 4) >> sub;  // subsampling_y == subsampling_x (4:2:0)
         int pAngle = av1r_mode_to_angle[mode] + P.angleDelta * 3;
         int upA = 0, upL = 0;
         const uint8_t* A = above;

@@ -169,7 +169,7 @@ extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
         P.smooth = plane ? ((bflags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
                          : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
         P.edgeFilter = hd.enable_intra_edge_filter;
-        coop_intra_predict(k, dst, P, L.intra, L.pred, 64);
+        coop_intra_predict(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
         if (isCfl) {
             // predict_chroma_from_luma (IntraPredict.cpp:632-667)
             const DevPlane& luma = k.cur.pl[0];
@@ -214,13 +214,22 @@ extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
 
 // ---------------------------------------------------------------------------------
 // Inter prediction
+//
+// Work item = one inter-coded block, all its planes and prediction units.  Two launch
+// classes: blocks up to 32x32 (one wave, small LDS: many resident workgroups) and larger
+// blocks (256 lanes).  For every unscaled, non-warped reference the (h+7) x (w+7)
+// reference window of a 32-row strip is staged in LDS with one coalesced sweep, and the
+// 8x8 separable sub-pel filter (whose phase is constant over a prediction unit) reads
+// only LDS; the result is blended into an LDS tile of the block and stored once.
 // ---------------------------------------------------------------------------------
-#define IT 256
-#define STRIP 16  // prediction rows per pass (registers: STRIP*128/IT px per lane per ref)
+#define STRIPR 32  // output rows per LDS window
 
+template <int MAXB>
 struct InterLds {
-    uint8_t tile[128 * 128];  // this plane's block, assembled before the store
-    uint8_t mask[128 * 128];  // compute_prediction's Mask (persists across planes)
+    static constexpr int WC = MAXB + 8;  // window row stride
+    uint8_t tile[MAXB * MAXB];           // this plane's block, assembled before the store
+    uint8_t mask[MAXB * MAXB];           // compute_prediction's Mask (persists across planes)
+    uint8_t win[2][(STRIPR + 7) * WC];   // reference windows of the current strip
     IntraLds intra;
     uint8_t iipred[32 * 32];
 };
@@ -233,6 +242,9 @@ struct RefSel {
     int warp;          // 0 none, 1 local, 2 global
     int alpha, beta, gamma, delta;
     const int32_t* wp;
+    int useWin;        // unscaled + not warped: LDS window path
+    int scaled;        // FrameHeader::is_scaled (Parser.cpp:795-803)
+    int wx0, wy0;      // window origin in the reference plane
 };
 
 // Block::LocalWarp::setupShear (Block.cpp:1179-1200) incl. resolveDivisor (:1087-1095)
@@ -299,11 +311,15 @@ DEV void select_ref(const KParams& k, RefSel& R, int refIdx, int plane, int x, i
     R.startY = r2s(baseY, 8) + 32;
     R.xStep = r2s(xs, 4);
     R.yStep = r2s(ys, 4);
+    R.scaled = xs != (1 << 14) || ys != (1 << 14);
+    R.warp = 0;
+    R.useWin = 0;
 }
 
-// One predicted sample (row r, column c of the PU) before blending: blockPixelPredict /
-// blockSubPixelPredict (InterPredict.cpp:319-383) or blockWarp (:507-553).
-DEV int pred_sample(const RefSel& R, int r, int c, int R0, int R1, int puX, int puY, int plane, int w, int h)
+// One predicted sample straight from the reference plane: blockPixelPredict /
+// blockSubPixelPredict (InterPredict.cpp:319-383) or blockWarp (:507-553).  Used for
+// scaled references and warps.
+DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1, int puX, int puY, int plane)
 {
     if (R.warp) {
         const int sub = plane ? 1 : 0;
@@ -346,7 +362,6 @@ DEV int pred_sample(const RefSel& R, int r, int c, int R0, int R1, int puX, int 
     int s = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
-        if (!vf[t]) continue;
         const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, ybase + t) * R.p.stride;
         int hs = 0;
 #pragma unroll
@@ -356,20 +371,55 @@ DEV int pred_sample(const RefSel& R, int r, int c, int R0, int R1, int puX, int 
     return (int16_t)r2(s, R1);
 }
 
+// Stage rows [r0, r0+nr) (+3/+4 filter margin) x (w+7) of the reference into LDS.
+template <int MAXB, int NT>
+DEV void load_window(RefSel& R, uint8_t* win, int r0, int nr, int w)
+{
+    constexpr int WC = InterLds<MAXB>::WC;
+    R.wx0 = (R.startX >> 10) - 3;
+    R.wy0 = (R.startY >> 10) + r0 - 3;
+    const int wc = w + 7, wr = nr + 7;
+    for (int q = threadIdx.x; q < wc * wr; q += NT) {
+        int i = q / wc, j = q - i * wc;
+        int yy = CLIP3(0, R.lastY, R.wy0 + i), xx = CLIP3(0, R.lastX, R.wx0 + j);
+        win[i * WC + j] = R.p.p[(size_t)yy * R.p.stride + xx];
+    }
+}
+
+// The same sample as pred_direct for an unscaled, unwarped reference, from the window.
+template <int MAXB>
+DEV int pred_win(const RefSel& R, const uint8_t* win, int rr, int c, int R0, int R1, const int16_t* hf, const int16_t* vf, int integer)
+{
+    constexpr int WC = InterLds<MAXB>::WC;
+    if (integer) return (int16_t)(win[(rr + 3) * WC + c + 3] << (14 - R0 - R1));
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint8_t* row = win + (rr + t) * WC + c;
+        int hs = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) hs += hf[u] * row[u];
+        s += vf[t] * r2(hs, R0);
+    }
+    return (int16_t)r2(s, R1);
+}
+
+DEV int wedge_oblique63(int i, int j)
+{
+    int shift = 16 - (i >> 1);
+    return (i & 1) ? av1r_wedge_master_oblique_odd[CLIP3(0, 63, j - (shift - 1))]
+                   : av1r_wedge_master_oblique_even[CLIP3(0, 63, j - shift)];
+}
 DEV int wedge_master(int dir, int i, int j)
 {
     // MasterMask (InterPredict.cpp:835-858) evaluated on the fly
     switch (dir) {
     case AV1R_WEDGE_VERTICAL: return av1r_wedge_master_vertical[j];
     case AV1R_WEDGE_HORIZONTAL: return av1r_wedge_master_vertical[i];
-    case AV1R_WEDGE_OBLIQUE63: {
-        int shift = 16 - (i >> 1);
-        return (i & 1) ? av1r_wedge_master_oblique_odd[CLIP3(0, 63, j - (shift - 1))]
-                       : av1r_wedge_master_oblique_even[CLIP3(0, 63, j - shift)];
-    }
-    case AV1R_WEDGE_OBLIQUE27: return wedge_master(AV1R_WEDGE_OBLIQUE63, j, i);
-    case AV1R_WEDGE_OBLIQUE117: return 64 - wedge_master(AV1R_WEDGE_OBLIQUE63, i, 63 - j);
-    default: return 64 - wedge_master(AV1R_WEDGE_OBLIQUE63, j, 63 - i);  // OBLIQUE153
+    case AV1R_WEDGE_OBLIQUE63: return wedge_oblique63(i, j);
+    case AV1R_WEDGE_OBLIQUE27: return wedge_oblique63(j, i);
+    case AV1R_WEDGE_OBLIQUE117: return 64 - wedge_oblique63(i, 63 - j);
+    default: return 64 - wedge_oblique63(j, 63 - i);  // OBLIQUE153
     }
 }
 
@@ -419,8 +469,9 @@ DEV void distance_weights(const KParams& k, const av1r_mi& info, int& fwd, int& 
 }
 
 // predict_inter for one PU of one plane; result blended into L.tile (block-relative
-// origin (ox, oy) in the tile).
-DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int x, int y,
+// origin (ox, oy)).
+template <int MAXB, int NT>
+DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int plane, int x, int y,
     int w, int h, int candRow, int candCol, int ox, int oy)
 {
     const int t = threadIdx.x;
@@ -431,33 +482,39 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     const int isIntrabc = (blk.flags & AV1R_BLK_INTRABC) != 0;
     const int isGlobalMode = blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV;
     RefSel R[2];
+    int16_t hf[2][8], vf[2][8];
+    int integer[2];
     int globalValid = 0;
-    for (int l = 0; l < 1 + isCompound; l++) {
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+        if (l > isCompound) break;
         int refFrame = info.ref_frame[l];
         int a, b, c, d;
         if (isGlobalMode && hd.gm_type[refFrame & 7] > AV1R_GM_TRANSLATION)
             globalValid = setup_shear(hd.gm_params[refFrame & 7], a, b, c, d);
         int refIdx = isIntrabc ? -1 : hd.ref_frame_idx[refFrame - 1];
         select_ref(k, R[l], refIdx, plane, x, y, info.mv[l]);
-        R[l].warp = 0;
         if (!(w < 8 || h < 8) && !hd.force_integer_mv) {
             if (blk.motion_mode == AV1R_LOCALWARP && (blk.flags & AV1R_BLK_LOCAL_VALID)) {
                 R[l].warp = 1;
                 R[l].wp = blk.local_warp;
-            } else if (isGlobalMode && hd.gm_type[refFrame & 7] > AV1R_GM_TRANSLATION && globalValid) {
-                int rw = refIdx < 0 ? k.frame_w : k.ref[refIdx].width;
-                int rh = refIdx < 0 ? k.frame_h : k.ref[refIdx].height;
-                int xs = ((rw << 14) + (k.frame_w / 2)) / k.frame_w;
-                int ys = ((rh << 14) + (k.frame_h / 2)) / k.frame_h;
-                if (xs == (1 << 14) && ys == (1 << 14)) {
-                    R[l].warp = 2;
-                    R[l].wp = hd.gm_params[refFrame & 7];
-                }
+            } else if (isGlobalMode && hd.gm_type[refFrame & 7] > AV1R_GM_TRANSLATION && globalValid
+                && !R[l].scaled) {
+                R[l].warp = 2;
+                R[l].wp = hd.gm_params[refFrame & 7];
             }
         }
         if (R[l].warp) setup_shear(R[l].wp, R[l].alpha, R[l].beta, R[l].gamma, R[l].delta);
         R[l].filtX = filter_idx(info.filt, w, 1);
         R[l].filtY = filter_idx(info.filt, h, 0);
+        R[l].useWin = !R[l].warp && R[l].xStep == 1024 && R[l].yStep == 1024 && w <= MAXB;
+        const int hph = (R[l].startX >> 6) & 15, vph = (R[l].startY >> 6) & 15;
+        integer[l] = !hph && !vph;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            hf[l][u] = av1r_subpel_filters[(R[l].filtX * 16 + hph) * 8 + u];
+            vf[l][u] = av1r_subpel_filters[(R[l].filtY * 16 + vph) * 8 + u];
+        }
     }
     const int ct = blk.compound_type;
     const int isII = mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] == AV1R_INTRA_FRAME;
@@ -470,77 +527,88 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     int fwd = 0, bck = 0;
     if (mode == 2) distance_weights(k, info, fwd, bck);
     WedgeSel ws = {0, 0, 0, 0};
-    if (ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
+    if (mode == 3 && ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
     const int ii = (blk.flags & AV1R_BLK_INTERINTRA) != 0, wii = (blk.flags & AV1R_BLK_WEDGE_II) != 0;
     const int diffwtdLuma = ct == AV1R_COMPOUND_DIFFWTD && plane == 0;
     const int sizeScale = 128 / imax(h, w);
-    for (int q = t; q < w * h; q += IT) {
-        const int r = q / w, c = q - r * w;
-        int p0 = pred_sample(R[0], r, c, R0, R1, x, y, plane, w, h);
-        int p1 = isCompound ? pred_sample(R[1], r, c, R0, R1, x, y, plane, w, h) : 0;
-        int v;
-        if (mode == 0) {
-            v = clip1(p0);
-        } else if (mode == 1) {
-            v = clip1(r2(p0 + p1, 1 + PostRound));
-        } else if (mode == 2) {
-            v = clip1(r2(fwd * p0 + bck * p1, 4 + PostRound));
-        } else {
-            // mask value (wedgeMask / intraModeVariantMask / differenceWeightMask) then
-            // maskBlend (InterPredict.cpp:555-609)
-            int m;
-            if (diffwtdLuma) {
-                int diff = (int16_t)iabs(p0 - p1);
-                diff = r2(diff, PostRound);
-                int mm = CLIP3(0, 64, 38 + diff / 16);
-                m = blk.mask_type ? 64 - mm : mm;
-                L.mask[r * 128 + c] = (uint8_t)m;
-            } else if (ct == AV1R_COMPOUND_INTRA || (ii && !wii) || !sub) {
-                if (ct == AV1R_COMPOUND_WEDGE) {
-                    int mv = wedge_master(ws.dir, ws.yoff + r, ws.xoff + c);
-                    m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
-                } else if (ct == AV1R_COMPOUND_INTRA) {
-                    int im = blk.interintra_mode;
-                    m = im == AV1R_II_V_PRED ? av1r_ii_weights_1d[r * sizeScale]
-                        : im == AV1R_II_H_PRED ? av1r_ii_weights_1d[c * sizeScale]
-                        : im == AV1R_II_SMOOTH_PRED ? av1r_ii_weights_1d[imin(r, c) * sizeScale] : 32;
-                } else {
-                    m = L.mask[r * 128 + c];
-                }
+    for (int r0 = 0; r0 < h; r0 += STRIPR) {
+        const int nr = imin(STRIPR, h - r0);
+        if (R[0].useWin) load_window<MAXB, NT>(R[0], L.win[0], r0, nr, w);
+        if (isCompound && R[1].useWin) load_window<MAXB, NT>(R[1], L.win[1], r0, nr, w);
+        __syncthreads();
+        for (int q = t; q < w * nr; q += NT) {
+            const int rr = q / w, c = q - rr * w, r = r0 + rr;
+            int p0 = R[0].useWin ? pred_win<MAXB>(R[0], L.win[0], rr, c, R0, R1, hf[0], vf[0], integer[0])
+                                 : pred_direct(R[0], r, c, R0, R1, x, y, plane);
+            int p1 = 0;
+            if (isCompound)
+                p1 = R[1].useWin ? pred_win<MAXB>(R[1], L.win[1], rr, c, R0, R1, hf[1], vf[1], integer[1])
+                                 : pred_direct(R[1], r, c, R0, R1, x, y, plane);
+            int v;
+            if (mode == 0) {
+                v = clip1(p0);
+            } else if (mode == 1) {
+                v = clip1(r2(p0 + p1, 1 + PostRound));
+            } else if (mode == 2) {
+                v = clip1(r2(fwd * p0 + bck * p1, 4 + PostRound));
             } else {
-                // 4:2:0 chroma: average of the 2x2 luma-resolution mask entries
-                int s4 = 0;
-#pragma unroll
-                for (int dy = 0; dy < 2; dy++)
-#pragma unroll
-                    for (int dx = 0; dx < 2; dx++) {
-                        int rr = 2 * r + dy, cc = 2 * c + dx;
-                        int mv;
-                        if (ct == AV1R_COMPOUND_WEDGE) {
-                            int mw = wedge_master(ws.dir, ws.yoff + rr, ws.xoff + cc);
-                            mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
-                        } else {
-                            mv = L.mask[rr * 128 + cc];
-                        }
-                        s4 += mv;
+                // mask (wedgeMask / intraModeVariantMask / differenceWeightMask) and
+                // maskBlend (InterPredict.cpp:555-609)
+                int m;
+                if (diffwtdLuma) {
+                    int diff = (int16_t)iabs(p0 - p1);
+                    diff = r2(diff, PostRound);
+                    int mm = CLIP3(0, 64, 38 + diff / 16);
+                    m = blk.mask_type ? 64 - mm : mm;
+                    L.mask[r * MAXB + c] = (uint8_t)m;
+                } else if (ct == AV1R_COMPOUND_INTRA || (ii && !wii) || !sub) {
+                    if (ct == AV1R_COMPOUND_WEDGE) {
+                        int mv = wedge_master(ws.dir, ws.yoff + r, ws.xoff + c);
+                        m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
+                    } else if (ct == AV1R_COMPOUND_INTRA) {
+                        int im = blk.interintra_mode;
+                        m = im == AV1R_II_V_PRED ? av1r_ii_weights_1d[r * sizeScale]
+                            : im == AV1R_II_H_PRED ? av1r_ii_weights_1d[c * sizeScale]
+                            : im == AV1R_II_SMOOTH_PRED ? av1r_ii_weights_1d[imin(r, c) * sizeScale] : 32;
+                    } else {
+                        m = L.mask[r * MAXB + c];
                     }
-                m = r2(s4, 2);
+                } else {
+                    // 4:2:0 chroma: average of the 2x2 luma-resolution mask entries
+                    int s4 = 0;
+#pragma unroll
+                    for (int dy = 0; dy < 2; dy++)
+#pragma unroll
+                        for (int dx = 0; dx < 2; dx++) {
+                            int rr2 = 2 * r + dy, cc = 2 * c + dx;
+                            int mv;
+                            if (ct == AV1R_COMPOUND_WEDGE) {
+                                int mw = wedge_master(ws.dir, ws.yoff + rr2, ws.xoff + cc);
+                                mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
+                            } else {
+                                mv = L.mask[rr2 * MAXB + cc];
+                            }
+                            s4 += mv;
+                        }
+                    m = r2(s4, 2);
+                }
+                if (ii) {
+                    int pp0 = clip1(r2(p0, PostRound));
+                    int pp1 = L.tile[(oy + r) * MAXB + ox + c];
+                    v = clip1(r2(m * pp1 + (64 - m) * pp0, 6));
+                } else {
+                    v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
+                }
             }
-            if (ii) {
-                int pp0 = clip1(r2(p0, PostRound));
-                int pp1 = L.tile[(oy + r) * 128 + ox + c];
-                v = clip1(r2(m * pp1 + (64 - m) * pp0, 6));
-            } else {
-                v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
-            }
+            L.tile[(oy + r) * MAXB + ox + c] = (uint8_t)v;
         }
-        L.tile[(oy + r) * 128 + ox + c] = (uint8_t)v;
+        __syncthreads();
     }
-    __syncthreads();
 }
 
 // overlappedMotionCompensation (InterPredict.cpp:611-709) on the plane tile.
-DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int baseX, int baseY, int w, int h)
+template <int MAXB, int NT>
+DEV void obmc(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int plane, int baseX, int baseY, int w, int h)
 {
     const int t = threadIdx.x;
     const int sub = plane ? 1 : 0;
@@ -554,7 +622,7 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, i
         const int lim = pass ? imin(k.mi_rows, blk.mi_row + n4) : imin(k.mi_cols, blk.mi_col + n4);
         int pos4 = pass ? blk.mi_row : blk.mi_col;
         int nCount = 0;
-        // the neighbours of one pass cover disjoint pixel ranges: all lanes share them
+        // the neighbours of one pass cover disjoint pixel ranges
         while (nCount < nLimit && pos4 < lim) {
             int candRow = pass ? (pos4 | 1) : blk.mi_row - 1;
             int candCol = pass ? blk.mi_col - 1 : (pos4 | 1);
@@ -570,14 +638,13 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, i
                 int predX = (x4 * 4) >> sub, predY = (y4 * 4) >> sub;
                 RefSel R;
                 select_ref(k, R, hd.ref_frame_idx[info.ref_frame[0] - 1], plane, predX, predY, info.mv[0]);
-                R.warp = 0;
                 R.filtX = filter_idx(info.filt, predW, 1);
                 R.filtY = filter_idx(info.filt, predH, 0);
-                for (int q = t; q < predW * predH; q += IT) {
+                for (int q = t; q < predW * predH; q += NT) {
                     int i = q / predW, j = q - i * predW;
-                    int p = pred_sample(R, i, j, 3, 11, predX, predY, plane, predW, predH);
+                    int p = pred_direct(R, i, j, 3, 11, predX, predY, plane);
                     int m = pass ? mask[j] : mask[i];
-                    uint8_t& d = L.tile[(predY - baseY + i) * 128 + predX - baseX + j];
+                    uint8_t& d = L.tile[(predY - baseY + i) * MAXB + predX - baseX + j];
                     d = (uint8_t)clip1(r2(m * d + (64 - m) * clip1(p), 6));
                 }
             }
@@ -587,9 +654,15 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, i
     }
 }
 
-extern "C" __global__ __launch_bounds__(IT) void k_inter(KParams k)
+DEV void intra_noinline(int miCols, int miRows, DevPlane src, IntraParams P, IntraLds& L, uint8_t* pred)
 {
-    __shared__ InterLds L;
+    coop_intra_predict(miCols, miRows, src, P, L, pred, 32);
+}
+
+template <int MAXB, int NT>
+DEV void inter_block(const KParams& k)
+{
+    __shared__ InterLds<MAXB> L;
     const int t = threadIdx.x;
     const av1r_block& blk = k.blocks[k.items[blockIdx.x]];
     const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
@@ -622,10 +695,10 @@ extern "C" __global__ __launch_bounds__(IT) void k_inter(KParams k)
             P.filterIntraMode = 0;
             P.smooth = 0;
             P.edgeFilter = k.hdr->enable_intra_edge_filter;
-            coop_intra_predict(k, k.cur.pl[plane], P, L.intra, L.iipred, 32);
-            for (int q = t; q < pw * ph; q += IT) {
+            intra_noinline(k.mi_cols, k.mi_rows, k.cur.pl[plane], P, L.intra, L.iipred);
+            for (int q = t; q < pw * ph; q += NT) {
                 int i = q / pw, j = q - i * pw;
-                L.tile[i * 128 + j] = L.iipred[i * 32 + j];
+                L.tile[i * MAXB + j] = L.iipred[i * 32 + j];
             }
             __syncthreads();
         }
@@ -645,27 +718,33 @@ extern "C" __global__ __launch_bounds__(IT) void k_inter(KParams k)
         for (int yy = 0; yy < ph; yy += predH) {
             int c = 0;
             for (int xx = 0; xx < pw; xx += predW) {
-                predict_pu(k, blk, L, plane, baseX + xx, baseY + yy, predW, predH, candRow + r, candCol + c, xx, yy);
+                predict_pu<MAXB, NT>(k, blk, L, plane, baseX + xx, baseY + yy, predW, predH, candRow + r, candCol + c, xx, yy);
                 c++;
             }
             r++;
         }
-        if (blk.motion_mode == AV1R_OBMC_CAUSAL) obmc(k, blk, L, plane, baseX, baseY, predW, predH);
+        if (blk.motion_mode == AV1R_OBMC_CAUSAL) obmc<MAXB, NT>(k, blk, L, plane, baseX, baseY, predW, predH);
         const DevPlane& dst = k.cur.pl[plane];
-        for (int q = t; q < pw * ph; q += IT) {
+        for (int q = t; q < pw * ph; q += NT) {
             int i = q / pw, j = q - i * pw;
-            px(dst, baseX + j, baseY + i) = L.tile[i * 128 + j];
+            px(dst, baseX + j, baseY + i) = L.tile[i * MAXB + j];
         }
         __syncthreads();
     }
 }
+
+// blocks up to 32x32: one wave per block
+extern "C" __global__ __launch_bounds__(64) void k_inter_s(KParams k) { inter_block<32, 64>(k); }
+// larger blocks: 256 lanes
+extern "C" __global__ __launch_bounds__(256) void k_inter_l(KParams k) { inter_block<128, 256>(k); }
 
 // ---------------------------------------------------------------------------------
 void launch_k_tb(const KParams& k, unsigned n, hipStream_t s)
 {
     hipLaunchKernelGGL(k_tb, dim3(n), dim3(64), 0, s, k);
 }
-void launch_k_inter(const KParams& k, unsigned n, hipStream_t s)
+void launch_k_inter(const KParams& k, unsigned n, int large, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_inter, dim3(n), dim3(IT), 0, s, k);
+    if (large) hipLaunchKernelGGL(k_inter_l, dim3(n), dim3(256), 0, s, k);
+    else hipLaunchKernelGGL(k_inter_s, dim3(n), dim3(64), 0, s, k);
 }
