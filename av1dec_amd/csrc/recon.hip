@@ -230,6 +230,10 @@ struct InterLds {
     uint8_t tile[MAXB * MAXB];           // this plane's block, assembled before the store
     uint8_t mask[MAXB * MAXB];           // compute_prediction's Mask (persists across planes)
     uint8_t win[2][(STRIPR + 7) * WC];   // reference windows of the current strip
+    // horizontally filtered window rows, or the 15x8 warp intermediates of the strip's
+    // 8x8 blocks
+    static constexpr int HB = (STRIPR + 7) * MAXB > STRIPR * MAXB * 15 / 8 ? (STRIPR + 7) * MAXB : STRIPR * MAXB * 15 / 8;
+    int16_t hb[2][HB];
     IntraLds intra;
     uint8_t iipred[32 * 32];
 };
@@ -317,38 +321,9 @@ DEV void select_ref(const KParams& k, RefSel& R, int refIdx, int plane, int x, i
 }
 
 // One predicted sample straight from the reference plane: blockPixelPredict /
-// blockSubPixelPredict (InterPredict.cpp:319-383) or blockWarp (:507-553).  Used for
-// scaled references and warps.
-DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1, int puX, int puY, int plane)
+// blockSubPixelPredict (InterPredict.cpp:319-383).  Used for scaled references.
+DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1)
 {
-    if (R.warp) {
-        const int sub = plane ? 1 : 0;
-        const int i8 = r >> 3, j8 = c >> 3;
-        const int32_t* wp = R.wp;
-        int srcX = (puX + j8 * 8 + 4) << sub;
-        int srcY = (puY + i8 * 8 + 4) << sub;
-        int dstX = wp[2] * srcX + wp[3] * srcY + wp[0];
-        int dstY = wp[4] * srcX + wp[5] * srcY + wp[1];
-        int x4 = dstX >> sub, y4 = dstY >> sub;
-        int ix4 = x4 >> 16, sx4 = x4 & 0xffff, iy4 = y4 >> 16, sy4 = y4 & 0xffff;
-        const int i1 = (r & 7) - 4, i2 = (c & 7) - 4;
-        int sy = sy4 + R.gamma * i2 + R.delta * i1;
-        const int8_t* vf = av1r_warped_filters + (r2(sy, 10) + 64) * 8;
-        int s = 0;
-#pragma unroll
-        for (int i3 = 0; i3 < 8; i3++) {
-            int ii1 = i1 + i3 - 3;  // intermediate row i1 + i3 + 4 - 7
-            int sx = sx4 + R.alpha * i2 + R.beta * ii1;
-            const int8_t* hf = av1r_warped_filters + (r2(sx, 10) + 64) * 8;
-            int yy = CLIP3(0, R.lastY, iy4 + ii1);
-            const uint8_t* row = R.p.p + (size_t)yy * R.p.stride;
-            int hs = 0;
-#pragma unroll
-            for (int k3 = 0; k3 < 8; k3++) hs += hf[k3] * row[CLIP3(0, R.lastX, ix4 + i2 - 3 + k3)];
-            s += vf[i3] * r2(hs, R0);
-        }
-        return (int16_t)r2(s, R1);
-    }
     if (!((R.startX >> 6) & 15) && !((R.startY >> 6) & 15)) {
         int xx = CLIP3(0, R.lastX, (R.startX >> 10) + c), yy = CLIP3(0, R.lastY, (R.startY >> 10) + r);
         return (int16_t)(R.p.p[(size_t)yy * R.p.stride + xx] << (14 - R0 - R1));
@@ -386,21 +361,82 @@ DEV void load_window(RefSel& R, uint8_t* win, int r0, int nr, int w)
     }
 }
 
-// The same sample as pred_direct for an unscaled, unwarped reference, from the window.
-template <int MAXB>
-DEV int pred_win(const RefSel& R, const uint8_t* win, int rr, int c, int R0, int R1, const int16_t* hf, const int16_t* vf, int integer)
+// Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the strip's
+// (nr + 7) window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).
+template <int MAXB, int NT>
+DEV void hpass(const uint8_t* win, int16_t* hb, int nr, int w, const int16_t* hf, int R0)
 {
     constexpr int WC = InterLds<MAXB>::WC;
-    if (integer) return (int16_t)(win[(rr + 3) * WC + c + 3] << (14 - R0 - R1));
-    int s = 0;
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint8_t* row = win + (rr + t) * WC + c;
+    for (int q = threadIdx.x; q < (nr + 7) * w; q += NT) {
+        const int i = q / w, j = q - i * w;
+        const uint8_t* row = win + i * WC + j;
         int hs = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) hs += hf[u] * row[u];
-        s += vf[t] * r2(hs, R0);
+        hb[i * MAXB + j] = (int16_t)r2(hs, R0);
     }
+}
+
+// The same sample as pred_direct for an unscaled, unwarped reference: the vertical pass
+// over the staged intermediate rows (or the integer-position copy from the window).
+template <int MAXB>
+DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int c, int R0, int R1, const int16_t* vf, int integer)
+{
+    constexpr int WC = InterLds<MAXB>::WC;
+    if (integer) return (int16_t)(win[(rr + 3) * WC + c + 3] << (14 - R0 - R1));
+    const int16_t* col = hb + rr * MAXB + c;
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) s += vf[t] * col[t * MAXB];
+    return (int16_t)r2(s, R1);
+}
+
+// blockWarp (InterPredict.cpp:507-553), split like the reference into its horizontal
+// pass -- the 15 x 8 intermediate of every 8x8 block of strip rows [r0, r0 + nr), read
+// straight from the reference plane -- and the vertical pass per output sample.
+DEV void warp_origin(const RefSel& R, int i8, int j8, int puX, int puY, int sub, int& ix4, int& sx4, int& iy4, int& sy4)
+{
+    const int32_t* wp = R.wp;
+    int srcX = (puX + j8 * 8 + 4) << sub;
+    int srcY = (puY + i8 * 8 + 4) << sub;
+    int dstX = wp[2] * srcX + wp[3] * srcY + wp[0];
+    int dstY = wp[4] * srcX + wp[5] * srcY + wp[1];
+    int x4 = dstX >> sub, y4 = dstY >> sub;
+    ix4 = x4 >> 16;
+    sx4 = x4 & 0xffff;
+    iy4 = y4 >> 16;
+    sy4 = y4 & 0xffff;
+}
+template <int NT>
+DEV void warp_hpass(const RefSel& R, int16_t* hb, int r0, int nr, int w, int puX, int puY, int sub, int R0)
+{
+    const int nb = (nr >> 3) * (w >> 3), w8 = w >> 3;
+    for (int q = threadIdx.x; q < nb * 120; q += NT) {
+        const int b = q / 120, e = q - b * 120;
+        const int i8 = (r0 >> 3) + b / w8, j8 = b - (b / w8) * w8;
+        int ix4, sx4, iy4, sy4;
+        warp_origin(R, i8, j8, puX, puY, sub, ix4, sx4, iy4, sy4);
+        const int i1 = (e >> 3) - 7, i2 = (e & 7) - 4;
+        const int sx = sx4 + R.alpha * i2 + R.beta * i1;
+        const int8_t* hf = av1r_warped_filters + (r2(sx, 10) + 64) * 8;
+        const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, iy4 + i1) * R.p.stride;
+        int hs = 0;
+#pragma unroll
+        for (int k3 = 0; k3 < 8; k3++) hs += hf[k3] * row[CLIP3(0, R.lastX, ix4 + i2 - 3 + k3)];
+        hb[q] = (int16_t)r2(hs, R0);
+    }
+}
+DEV int warp_v(const RefSel& R, const int16_t* hb, int rr, int r, int c, int w, int puX, int puY, int sub, int R1)
+{
+    int ix4, sx4, iy4, sy4;
+    warp_origin(R, r >> 3, c >> 3, puX, puY, sub, ix4, sx4, iy4, sy4);
+    const int i1 = (r & 7) - 4, i2 = (c & 7) - 4;
+    const int sy = sy4 + R.gamma * i2 + R.delta * i1;
+    const int8_t* vf = av1r_warped_filters + (r2(sy, 10) + 64) * 8;
+    const int16_t* col = hb + ((rr >> 3) * (w >> 3) + (c >> 3)) * 120 + (r & 7) * 8 + (c & 7);
+    int s = 0;
+#pragma unroll
+    for (int i3 = 0; i3 < 8; i3++) s += vf[i3] * col[i3 * 8];
     return (int16_t)r2(s, R1);
 }
 
@@ -536,14 +572,21 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, 
         if (R[0].useWin) load_window<MAXB, NT>(R[0], L.win[0], r0, nr, w);
         if (isCompound && R[1].useWin) load_window<MAXB, NT>(R[1], L.win[1], r0, nr, w);
         __syncthreads();
+        if (R[0].useWin && !integer[0]) hpass<MAXB, NT>(L.win[0], L.hb[0], nr, w, hf[0], R0);
+        if (R[0].warp) warp_hpass<NT>(R[0], L.hb[0], r0, nr, w, x, y, sub, R0);
+        if (isCompound && R[1].useWin && !integer[1]) hpass<MAXB, NT>(L.win[1], L.hb[1], nr, w, hf[1], R0);
+        if (isCompound && R[1].warp) warp_hpass<NT>(R[1], L.hb[1], r0, nr, w, x, y, sub, R0);
+        __syncthreads();
         for (int q = t; q < w * nr; q += NT) {
             const int rr = q / w, c = q - rr * w, r = r0 + rr;
-            int p0 = R[0].useWin ? pred_win<MAXB>(R[0], L.win[0], rr, c, R0, R1, hf[0], vf[0], integer[0])
-                                 : pred_direct(R[0], r, c, R0, R1, x, y, plane);
+            int p0 = R[0].useWin ? pred_win<MAXB>(L.win[0], L.hb[0], rr, c, R0, R1, vf[0], integer[0])
+                     : R[0].warp ? warp_v(R[0], L.hb[0], rr, r, c, w, x, y, sub, R1)
+                                 : pred_direct(R[0], r, c, R0, R1);
             int p1 = 0;
             if (isCompound)
-                p1 = R[1].useWin ? pred_win<MAXB>(R[1], L.win[1], rr, c, R0, R1, hf[1], vf[1], integer[1])
-                                 : pred_direct(R[1], r, c, R0, R1, x, y, plane);
+                p1 = R[1].useWin ? pred_win<MAXB>(L.win[1], L.hb[1], rr, c, R0, R1, vf[1], integer[1])
+                     : R[1].warp ? warp_v(R[1], L.hb[1], rr, r, c, w, x, y, sub, R1)
+                                 : pred_direct(R[1], r, c, R0, R1);
             int v;
             if (mode == 0) {
                 v = clip1(p0);
@@ -640,12 +683,32 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int pl
                 select_ref(k, R, hd.ref_frame_idx[info.ref_frame[0] - 1], plane, predX, predY, info.mv[0]);
                 R.filtX = filter_idx(info.filt, predW, 1);
                 R.filtY = filter_idx(info.filt, predH, 0);
-                for (int q = t; q < predW * predH; q += NT) {
-                    int i = q / predW, j = q - i * predW;
-                    int p = pred_direct(R, i, j, 3, 11, predX, predY, plane);
-                    int m = pass ? mask[j] : mask[i];
-                    uint8_t& d = L.tile[(predY - baseY + i) * MAXB + predX - baseX + j];
-                    d = (uint8_t)clip1(r2(m * d + (64 - m) * clip1(p), 6));
+                R.useWin = R.xStep == 1024 && R.yStep == 1024;
+                const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
+                const int integer = !hph && !vph;
+                int16_t hf[8], vf[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    hf[u] = av1r_subpel_filters[(R.filtX * 16 + hph) * 8 + u];
+                    vf[u] = av1r_subpel_filters[(R.filtY * 16 + vph) * 8 + u];
+                }
+                for (int r0 = 0; r0 < predH; r0 += STRIPR) {
+                    const int nr = imin(STRIPR, predH - r0);
+                    if (R.useWin) {
+                        load_window<MAXB, NT>(R, L.win[0], r0, nr, predW);
+                        __syncthreads();
+                        if (!integer) hpass<MAXB, NT>(L.win[0], L.hb[0], nr, predW, hf, 3);
+                        __syncthreads();
+                    }
+                    for (int q = t; q < predW * nr; q += NT) {
+                        const int rr = q / predW, j = q - rr * predW, i = r0 + rr;
+                        int p = R.useWin ? pred_win<MAXB>(L.win[0], L.hb[0], rr, j, 3, 11, vf, integer)
+                                         : pred_direct(R, i, j, 3, 11);
+                        int m = pass ? mask[j] : mask[i];
+                        uint8_t& d = L.tile[(predY - baseY + i) * MAXB + predX - baseX + j];
+                        d = (uint8_t)clip1(r2(m * d + (64 - m) * clip1(p), 6));
+                    }
+                    __syncthreads();
                 }
             }
             pos4 += step4;
