@@ -55,3 +55,13 @@ DEV int floor_log2(int x) { return x > 0 ? 31 - __builtin_clz((unsigned)x) : -1;
 DEV const av1r_mi& mi_at(const KParams& k, int row, int col) { return k.mi[(size_t)row * k.mi_stride + col]; }
 DEV int plane_bsize(int bs, int plane) { return plane ? av1r_ss420[bs] : bs; }
 DEV uint8_t& px(const DevPlane& p, int x, int y) { return p.p[(size_t)y * p.stride + x]; }
+
+// Work-item encoding of the per-level item lists (host schedule -> k_level):
+// bits 31..30 kind, 29..0 index (TB index; block index for inter-intra blends;
+// block index << 4 | tile row << 2 | tile column for inter tiles).
+#define AV1R_ITEM_TB 0u
+#define AV1R_ITEM_INTER 1u
+#define AV1R_ITEM_II 2u
+#define AV1R_ITEM(kind, idx) (((uint32_t)(kind) << 30) | (uint32_t)(idx))
+#define AV1R_ITEM_KIND(v) ((v) >> 30)
+#define AV1R_ITEM_INDEX(v) ((v) & 0x3fffffffu)

@@ -25,8 +25,7 @@
 
 #include "av1r_dev.h"
 
-void launch_k_tb(const KParams& k, unsigned n, hipStream_t s);
-void launch_k_inter(const KParams& k, unsigned n, int large, hipStream_t s);
+void launch_k_level(const KParams& k, unsigned n, hipStream_t s);
 void launch_k_lf(const KParams& k, int pass, int nY, int nC, int cCols, int planeMask, hipStream_t s);
 void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s);
 void launch_k_lr(const KParams& k, hipStream_t s);
@@ -50,7 +49,7 @@ struct Upload {
 };
 
 struct Level {
-    uint32_t pOff = 0, pCnt = 0, lOff = 0, lCnt = 0, tOff = 0, tCnt = 0;  // small / large inter blocks, TBs
+    uint32_t off = 0, cnt = 0;  // items [off, off + cnt) of the schedule
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -84,7 +83,7 @@ struct av1r_ctx {
     // schedule scratch
     std::vector<int16_t> lvlmap[3];
     int mapW[3] = {}, mapH[3] = {};
-    std::vector<std::vector<uint32_t>> lvP, lvL, lvT;
+    std::vector<std::vector<uint32_t>> lvP, lvB, lvT;  // inter tiles, inter-intra blends, TBs per level
     std::vector<uint32_t> items;
     std::vector<Level> levels;
     // split submission (frame_begin / submit_tile / frame_end)
@@ -210,6 +209,8 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
         if (slot < 0 || slot > 7 || !c->slots[slot])
             return fail(c, AV1R_E_INVALID, "reference %d maps to an empty slot", r);
     }
+    if (b->n_blocks >= (1u << 26) || b->n_tbs >= (1u << 30))
+        return fail(c, AV1R_E_UNSUPPORTED, "too many blocks / transform blocks in one frame");
     for (uint32_t i = 0; i < b->n_blocks; i++) {
         const av1r_block& k = b->blocks[i];
         if (k.mi_size >= AV1R_BLOCK_SIZES || k.mi_row >= ah4 || k.mi_col >= aw4
@@ -284,10 +285,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         c->mapH[p] = (((h->mi_rows_alloc * 4) >> sub) + 64) / 4;
         c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
     }
-    c->lvP.clear();
-    c->lvL.clear();
-    c->lvT.clear();
-    auto region_max = [&](int p, int x0, int y0, int x1, int y1) {  // inclusive unit rect
+    for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
+        for (auto& l : *v) l.clear();
+    auto region_max = [&](int p, int x0, int y0, int x1, int y1) {  // inclusive 4x4-unit rect
         x0 = std::max(x0, 0);
         y0 = std::max(y0, 0);
         x1 = std::min(x1, c->mapW[p] - 1);
@@ -306,83 +306,91 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             for (int x = x0; x < x1; x++) row[x] = (int16_t)lv;
         }
     };
-    auto push = [&](std::vector<std::vector<uint32_t>>& v, int lv, uint32_t id) {
+    // Latest level among the pixels coop_intra_predict reads for a w x h prediction at
+    // pixel (x, y) of plane p with the given edge availability (IntraPredict.cpp:563-631):
+    // row y-1 over [x-1 | x, x + (AR ? 2w : w) - 1], column x-1 over [y-1 | y, y + (BL ? 2h : h) - 1];
+    // with only one edge available its neighbouring corner pixel stands in for the other.
+    auto edge_level = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL) {
+        int m = -1;
+        if (hA) m = std::max(m, region_max(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2));
+        if (hL) m = std::max(m, region_max(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2));
+        return m;
+    };
+    auto push = [&](std::vector<std::vector<uint32_t>>& v, int lv, uint32_t item) {
         if ((int)v.size() <= lv) v.resize(lv + 1);
-        v[lv].push_back(id);
+        v[lv].push_back(item);
     };
     int globalMax = -1;
     for (uint32_t bi = 0; bi < b->n_blocks; bi++) {
         const av1r_block& blk = b->blocks[bi];
         const bool inter = blk.flags & AV1R_BLK_INTER;
         const int nPlanes = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
-        int pLevel = -1;
+        int blkLevel = -1;  // level after which the block's prediction is complete
         if (inter) {
             const bool isII = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col].ref_frame[1] == AV1R_INTRA_FRAME;
-            int dep = -1;
-            if (blk.flags & AV1R_BLK_INTRABC) {
-                dep = globalMax;  // reads already-decoded pixels of the current frame
-            } else if (isII) {
+            // intra block copy reads already-decoded pixels of the current frame
+            const int pLevel = (blk.flags & AV1R_BLK_INTRABC) ? globalMax + 1 : 0;
+            const int bw = av1r_num4x4w[blk.mi_size] * 4, bh = av1r_num4x4h[blk.mi_size] * 4;
+            for (int ty = 0; ty < (bh + 31) / 32; ty++)
+                for (int tx = 0; tx < (bw + 31) / 32; tx++)
+                    push(c->lvP, pLevel, AV1R_ITEM(AV1R_ITEM_INTER, (bi << 4) | (ty << 2) | tx));
+            blkLevel = pLevel;
+            if (isII) {
+                int dep = pLevel;
                 for (int p = 0; p < nPlanes; p++) {
                     int sub = p ? 1 : 0;
                     int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
-                    int x4 = (blk.mi_col >> sub), y4 = (blk.mi_row >> sub);
-                    int w4 = av1r_num4x4w[psz], h4 = av1r_num4x4h[psz];
-                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 + 2 * w4 - 1, y4 - 1));
-                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 - 1, y4 + 2 * h4 - 1));
+                    bool hL = p ? (blk.flags & AV1R_BLK_AVAIL_L_UV) : (blk.flags & AV1R_BLK_AVAIL_L);
+                    bool hA = p ? (blk.flags & AV1R_BLK_AVAIL_U_UV) : (blk.flags & AV1R_BLK_AVAIL_U);
+                    dep = std::max(dep, edge_level(p, (blk.mi_col >> sub) * 4, (blk.mi_row >> sub) * 4,
+                                            av1r_num4x4w[psz] * 4, av1r_num4x4h[psz] * 4, hL, hA,
+                                            (blk.ii_edge >> (2 * p)) & 1, (blk.ii_edge >> (2 * p + 1)) & 1));
                 }
+                blkLevel = dep + 1;
+                push(c->lvB, blkLevel, AV1R_ITEM(AV1R_ITEM_II, bi));
             }
-            pLevel = dep + 1;
-            const bool large = av1r_num4x4w[blk.mi_size] > 8 || av1r_num4x4h[blk.mi_size] > 8;
-            push(large ? c->lvL : c->lvP, pLevel, bi);
-            globalMax = std::max(globalMax, pLevel);
+            globalMax = std::max(globalMax, blkLevel);
             for (int p = 0; p < nPlanes; p++) {
                 int sub = p ? 1 : 0;
                 int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
-                region_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], pLevel);
+                region_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], blkLevel);
             }
         }
         int lumaMax = -1;  // CFL reads this block's reconstructed luma
         for (uint32_t ti = blk.first_tb; ti < blk.first_tb + blk.n_tbs; ti++) {
             const av1r_tb& t = b->tbs[ti];
             const int p = t.plane;
-            const int x4 = t.x >> 2, y4 = t.y >> 2;
-            const int w4 = av1r_tx_w[t.tx_size] >> 2, h4 = av1r_tx_h[t.tx_size] >> 2;
+            const int w = av1r_tx_w[t.tx_size], hh = av1r_tx_h[t.tx_size];
             int lv;
             if (inter) {
                 if (!t.coef_cnt) continue;  // prediction only: nothing to add
-                lv = pLevel + 1;
+                lv = blkLevel + 1;
             } else {
                 const bool pal = p ? blk.palette_size_uv : blk.palette_size_y;
                 int dep = -1;
                 if (!pal) {
-                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 + 2 * w4 - 1, y4 - 1));
-                    dep = std::max(dep, region_max(p, x4 - 1, y4 - 1, x4 - 1, y4 + 2 * h4 - 1));
-                    if (p && blk.uv_mode == AV1R_UV_CFL_PRED) dep = std::max(dep, lumaMax);
+                    dep = edge_level(p, t.x, t.y, w, hh, t.flags & AV1R_TB_HAVE_LEFT, t.flags & AV1R_TB_HAVE_ABOVE,
+                                     t.flags & AV1R_TB_HAVE_AR, t.flags & AV1R_TB_HAVE_BL);
+                    if (p && blk.uv_mode == AV1R_UV_CFL_PRED)  // the co-located luma (incl. sub-8x8 neighbours)
+                        dep = std::max({dep, lumaMax, region_max(0, t.x >> 1, t.y >> 1, (2 * (t.x + w) - 1) >> 2, (2 * (t.y + hh) - 1) >> 2)});
                 }
                 lv = dep + 1;
             }
             if (p == 0) lumaMax = std::max(lumaMax, lv);
-            push(c->lvT, lv, ti);
+            push(c->lvT, lv, AV1R_ITEM(AV1R_ITEM_TB, ti));
             globalMax = std::max(globalMax, lv);
-            region_set(p, x4, y4, w4, h4, lv);
+            region_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv);
         }
     }
-    size_t nl = std::max(std::max(c->lvP.size(), c->lvL.size()), c->lvT.size());
-    c->lvP.resize(nl);
-    c->lvL.resize(nl);
-    c->lvT.resize(nl);
+    const size_t nl = (size_t)(globalMax + 1);
+    for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
+        if (v->size() < nl) v->resize(nl);
     c->items.clear();
     c->levels.assign(nl, Level());
     for (size_t l = 0; l < nl; l++) {
-        c->levels[l].pOff = (uint32_t)c->items.size();
-        c->levels[l].pCnt = (uint32_t)c->lvP[l].size();
-        c->items.insert(c->items.end(), c->lvP[l].begin(), c->lvP[l].end());
-        c->levels[l].lOff = (uint32_t)c->items.size();
-        c->levels[l].lCnt = (uint32_t)c->lvL[l].size();
-        c->items.insert(c->items.end(), c->lvL[l].begin(), c->lvL[l].end());
-        c->levels[l].tOff = (uint32_t)c->items.size();
-        c->levels[l].tCnt = (uint32_t)c->lvT[l].size();
-        c->items.insert(c->items.end(), c->lvT[l].begin(), c->lvT[l].end());
+        c->levels[l].off = (uint32_t)c->items.size();
+        for (auto* v : {&c->lvP, &c->lvB, &c->lvT}) c->items.insert(c->items.end(), (*v)[l].begin(), (*v)[l].end());
+        c->levels[l].cnt = (uint32_t)c->items.size() - c->levels[l].off;
     }
     c->nLevelsLast = (int)nl;
 }
@@ -466,21 +474,10 @@ static int launch_frame(av1r_ctx* c, const Prepared& P)
 
     // ---- reconstruction, level by level
     for (const Level& L : P.levels) {
-        if (L.lCnt) {
-            k.items = P.dItems + L.lOff;
-            k.n_items = L.lCnt;
-            launch_k_inter(k, L.lCnt, 1, c->stream);
-        }
-        if (L.pCnt) {
-            k.items = P.dItems + L.pOff;
-            k.n_items = L.pCnt;
-            launch_k_inter(k, L.pCnt, 0, c->stream);
-        }
-        if (L.tCnt) {
-            k.items = P.dItems + L.tOff;
-            k.n_items = L.tCnt;
-            launch_k_tb(k, L.tCnt, c->stream);
-        }
+        if (!L.cnt) continue;
+        k.items = P.dItems + L.off;
+        k.n_items = L.cnt;
+        launch_k_level(k, L.cnt, c->stream);
     }
     HIPCHK(hipGetLastError());
     auto snapshot = [&](int st, FrameBuf* src) -> int {

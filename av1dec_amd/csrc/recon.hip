@@ -1,16 +1,18 @@
 // recon.hip -- block reconstruction kernels for gfx950.
 //
-//   k_tb     one 64-lane workgroup per transform block of a dependency level:
+//   k_level  one 64-lane workgroup per work item of a dependency level.  Transform
+//            block items:
 //            intra / palette / CFL prediction (or the already-predicted inter pixels),
 //            dequantisation, 2-D inverse transform (rows then columns, one lane per
 //            row/column, T[] in VGPRs), flip, add, clip, store.
 //            Restates TransformBlock::decode/reconstruct/inverseTransform
 //            (decoder/TransformBlock.cpp:2173-2456).
-//   k_inter  one 256-lane workgroup per inter-coded block: Block::compute_prediction
+//            Inter items (one <= 32x32 tile of a block): Block::compute_prediction
 //            (decoder/Block.cpp:100-174) -> InterPredict::predict_inter
 //            (decoder/InterPredict.cpp:962-1049): 8-tap sub-pel convolve or warp per
 //            reference, compound average / distance / wedge / difference-weighted /
 //            inter-intra blends, OBMC, assembled per plane in an LDS tile.
+//            Inter-intra items: the intra half of an inter-intra block, blended in place.
 // The host (av1r_host.cpp) orders launches by dependency level so every pixel a work
 // item reads was finalised by an earlier launch.
 #include "av1r_dev.h"
@@ -20,17 +22,17 @@
 // ---------------------------------------------------------------------------------
 // Transform blocks
 // ---------------------------------------------------------------------------------
-#define RS 65  // LDS row stride of the residual tile (65 ints: conflict-free rows & columns)
+#define RS 66  // LDS row stride (int16) of the residual tile: 33 dwords, conflict-free rows & columns
 
 struct TbLds {
-    int res[64 * RS];
+    int16_t res[64 * RS];
     uint8_t pred[64 * 64];
     IntraLds intra;
     int sum;
 };
 
 template <int n>
-DEV void row_pass(int* row, int w, int kind, int rectScale, int rowShift, int lossless)
+DEV void row_pass(int16_t* row, int w, int kind, int rectScale, int rowShift, int lossless)
 {
     int T[1 << n];
 #pragma unroll
@@ -41,21 +43,28 @@ DEV void row_pass(int* row, int w, int kind, int rectScale, int rowShift, int lo
     }
     tx::run1d<n>(T, lossless ? 3 : kind, 16, 2);
 #pragma unroll
-    for (int j = 0; j < (1 << n); j++) row[j] = CLIP3(-32768, 32767, r2(T[j], rowShift));
+    for (int j = 0; j < (1 << n); j++) row[j] = (int16_t)CLIP3(-32768, 32767, r2(T[j], rowShift));
 }
+// Column pass fused with the reconstruction of one output column: out/pred point at
+// the column's row 0 (after the left-right flip); rows are written flipped if flipUD.
 template <int n>
-DEV void col_pass(int* col, int kind, int colShift, int lossless)
+DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, const uint8_t* pred, uint8_t* out,
+    int stride, int flipUD)
 {
     int T[1 << n];
 #pragma unroll
     for (int i = 0; i < (1 << n); i++) T[i] = col[i * RS];
     tx::run1d<n>(T, lossless ? 3 : kind, 16, 0);
 #pragma unroll
-    for (int i = 0; i < (1 << n); i++) col[i * RS] = r2(T[i], colShift);
+    for (int yy = 0; yy < (1 << n); yy++) {
+        const int i = flipUD ? (1 << n) - 1 - yy : yy;
+        out[i * stride] = (uint8_t)clip1(pred[i * 64] + r2(T[yy], colShift));
+    }
 }
 
-// reconstruct() + inverseTransform() into L.res (TransformBlock.cpp:2173-2276)
-DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds& L)
+// reconstruct() + inverseTransform() (TransformBlock.cpp:2173-2276), the flip and the
+// add-and-clip onto the prediction in L.pred, stored to the frame at (x, y).
+DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds& L, const DevPlane& dst)
 {
     const int t = threadIdx.x;
     const int txSz = tb.tx_size;
@@ -82,7 +91,7 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
         int sign = d < 0 ? -1 : 1;
         int d2 = sign * (iabs(d) & 0xffffff) / dqDenom;
-        L.res[(pos / tw) * RS + (pos % tw)] = CLIP3(-(1 << 15), (1 << 15) - 1, d2);
+        L.res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
     }
     __syncthreads();
     const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
@@ -93,7 +102,7 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
     const int rk = tx::row_kind(type), ck = tx::col_kind(type);
     // rows >= 32 of a 64-high transform have all-zero input and therefore zero output
     if (t < th) {
-        int* row = L.res + t * RS;
+        int16_t* row = L.res + t * RS;
         switch (log2W) {
         case 2: row_pass<2>(row, w, rk, rect, rowShift, lossless); break;
         case 3: row_pass<3>(row, w, rk, rect, rowShift, lossless); break;
@@ -102,28 +111,32 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         default: row_pass<6>(row, w, rk, rect, rowShift, lossless); break;
         }
     } else if (t < h) {
-        int* row = L.res + t * RS;
+        int16_t* row = L.res + t * RS;
         for (int j = 0; j < w; j++) row[j] = 0;
     }
     __syncthreads();
+    const int flipUD = type == AV1R_FLIPADST_DCT || type == AV1R_FLIPADST_ADST || type == AV1R_V_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
+    const int flipLR = type == AV1R_DCT_FLIPADST || type == AV1R_ADST_FLIPADST || type == AV1R_H_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     if (t < w) {
-        int* col = L.res + t;
+        const int16_t* col = L.res + t;
+        const int j = flipLR ? w - 1 - t : t;
+        const uint8_t* pred = L.pred + j;
+        uint8_t* out = dst.p + (size_t)tb.y * dst.stride + tb.x + j;
         switch (log2H) {
-        case 2: col_pass<2>(col, ck, colShift, lossless); break;
-        case 3: col_pass<3>(col, ck, colShift, lossless); break;
-        case 4: col_pass<4>(col, ck, colShift, lossless); break;
-        case 5: col_pass<5>(col, ck, colShift, lossless); break;
-        default: col_pass<6>(col, ck, colShift, lossless); break;
+        case 2: col_pass<2>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 3: col_pass<3>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 4: col_pass<4>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 5: col_pass<5>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        default: col_pass<6>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
         }
     }
-    __syncthreads();
 }
 
-extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
+// One transform block (TransformBlock::decode, TransformBlock.cpp:2400-2456).
+DEV void tb_item(const KParams& k, uint32_t idx, TbLds& L)
 {
-    __shared__ TbLds L;
     const int t = threadIdx.x;
-    const av1r_tb tb = k.tbs[k.items[blockIdx.x]];
+    const av1r_tb tb = k.tbs[idx];
     const av1r_block& blk = k.blocks[tb.block];
     const int plane = tb.plane, x = tb.x, y = tb.y, txSz = tb.tx_size;
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
@@ -180,7 +193,7 @@ extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
                 int i = q >> log2W, j = q & (w - 1);
                 int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
                 int v = (px(luma, lx, ly) + px(luma, lx + 1, ly) + px(luma, lx, ly + 1) + px(luma, lx + 1, ly + 1)) << 1;
-                L.res[i * RS + j] = v;  // res is free until the residual pass
+                L.res[i * RS + j] = (int16_t)v;  // res is free until the residual pass
                 s += v;
             }
 #pragma unroll
@@ -195,15 +208,7 @@ extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
     }
     __syncthreads();
     if (tb.coef_cnt) {
-        tb_residual(k, tb, blk, L);
-        const int tt = tb.tx_type;
-        const int flipUD = tt == AV1R_FLIPADST_DCT || tt == AV1R_FLIPADST_ADST || tt == AV1R_V_FLIPADST || tt == AV1R_FLIPADST_FLIPADST;
-        const int flipLR = tt == AV1R_DCT_FLIPADST || tt == AV1R_ADST_FLIPADST || tt == AV1R_H_FLIPADST || tt == AV1R_FLIPADST_FLIPADST;
-        for (int q = t; q < w * h; q += 64) {
-            int i = q >> log2W, j = q & (w - 1);
-            int xx = flipLR ? (w - j - 1) : j, yy = flipUD ? (h - i - 1) : i;
-            px(dst, x + j, y + i) = (uint8_t)clip1(L.res[yy * RS + xx] + L.pred[i * 64 + j]);
-        }
+        tb_residual(k, tb, blk, L, dst);
     } else if (!isInter) {
         for (int q = t; q < w * h; q += 64) {
             int i = q >> log2W, j = q & (w - 1);
@@ -215,27 +220,26 @@ extern "C" __global__ __launch_bounds__(64) void k_tb(KParams k)
 // ---------------------------------------------------------------------------------
 // Inter prediction
 //
-// Work item = one inter-coded block, all its planes and prediction units.  Two launch
-// classes: blocks up to 32x32 (one wave, small LDS: many resident workgroups) and larger
-// blocks (256 lanes).  For every unscaled, non-warped reference the (h+7) x (w+7)
-// reference window of a 32-row strip is staged in LDS with one coalesced sweep, and the
-// 8x8 separable sub-pel filter (whose phase is constant over a prediction unit) reads
-// only LDS; the result is blended into an LDS tile of the block and stored once.
+// Work item = one <= 32x32 luma tile (+ its 4:2:0 chroma) of an inter-coded block: every
+// sample of Block::compute_prediction (decoder/Block.cpp:100-174) ->
+// InterPredict::predict_inter (decoder/InterPredict.cpp:962-1049) depends only on its
+// own position, so a 128x128 block becomes 16 independent tiles of identical cost.  Per
+// tile and reference, the (h + 7) x (w + 7) reference window is staged in LDS with one
+// sweep, the horizontal sub-pel pass runs once per window row into LDS, and the vertical
+// pass produces each sample; warps stage their 15 x 8 intermediates per 8x8 block.  The
+// compound blend is applied per sample and the tile is stored once.  Inter-intra blocks
+// store their plain inter prediction here; ii_item blends the intra part once the
+// block's edges are final.
 // ---------------------------------------------------------------------------------
-#define STRIPR 32  // output rows per LDS window
+#define TS 32                     // tile edge (luma)
+#define WC (TS + 8)               // window row stride
+#define HBN (TS * TS * 15 / 8)    // >= (TS + 7) * TS horizontal rows; = warp intermediates
 
-template <int MAXB>
 struct InterLds {
-    static constexpr int WC = MAXB + 8;  // window row stride
-    uint8_t tile[MAXB * MAXB];           // this plane's block, assembled before the store
-    uint8_t mask[MAXB * MAXB];           // compute_prediction's Mask (persists across planes)
-    uint8_t win[2][(STRIPR + 7) * WC];   // reference windows of the current strip
-    // horizontally filtered window rows, or the 15x8 warp intermediates of the strip's
-    // 8x8 blocks
-    static constexpr int HB = (STRIPR + 7) * MAXB > STRIPR * MAXB * 15 / 8 ? (STRIPR + 7) * MAXB : STRIPR * MAXB * 15 / 8;
-    int16_t hb[2][HB];
-    IntraLds intra;
-    uint8_t iipred[32 * 32];
+    uint8_t tile[TS * TS];        // this plane's tile, assembled before the store
+    uint8_t mask[TS * TS];        // compute_prediction's Mask (luma, persists across planes)
+    uint8_t win[2][(TS + 7) * WC];  // reference windows
+    int16_t hb[2][HBN];           // horizontally filtered window rows / warp intermediates
 };
 
 struct RefSel {
@@ -248,7 +252,6 @@ struct RefSel {
     const int32_t* wp;
     int useWin;        // unscaled + not warped: LDS window path
     int scaled;        // FrameHeader::is_scaled (Parser.cpp:795-803)
-    int wx0, wy0;      // window origin in the reference plane
 };
 
 // Block::LocalWarp::setupShear (Block.cpp:1179-1200) incl. resolveDivisor (:1087-1095)
@@ -346,54 +349,48 @@ DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1)
     return (int16_t)r2(s, R1);
 }
 
-// Stage rows [r0, r0+nr) (+3/+4 filter margin) x (w+7) of the reference into LDS.
-template <int MAXB, int NT>
-DEV void load_window(RefSel& R, uint8_t* win, int r0, int nr, int w)
+// Stage the (rh + 7) x (rw + 7) reference window of PU-relative region
+// [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin).
+DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, int rh)
 {
-    constexpr int WC = InterLds<MAXB>::WC;
-    R.wx0 = (R.startX >> 10) - 3;
-    R.wy0 = (R.startY >> 10) + r0 - 3;
-    const int wc = w + 7, wr = nr + 7;
-    for (int q = threadIdx.x; q < wc * wr; q += NT) {
+    const int wx0 = (R.startX >> 10) - 3 + rx0, wy0 = (R.startY >> 10) - 3 + ry0;
+    const int wc = rw + 7, wr = rh + 7;
+    for (int q = threadIdx.x; q < wc * wr; q += 64) {
         int i = q / wc, j = q - i * wc;
-        int yy = CLIP3(0, R.lastY, R.wy0 + i), xx = CLIP3(0, R.lastX, R.wx0 + j);
+        int yy = CLIP3(0, R.lastY, wy0 + i), xx = CLIP3(0, R.lastX, wx0 + j);
         win[i * WC + j] = R.p.p[(size_t)yy * R.p.stride + xx];
     }
 }
 
-// Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the strip's
-// (nr + 7) window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).
-template <int MAXB, int NT>
-DEV void hpass(const uint8_t* win, int16_t* hb, int nr, int w, const int16_t* hf, int R0)
+// Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the (rh + 7)
+// window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).
+DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0)
 {
-    constexpr int WC = InterLds<MAXB>::WC;
-    for (int q = threadIdx.x; q < (nr + 7) * w; q += NT) {
-        const int i = q / w, j = q - i * w;
+    for (int q = threadIdx.x; q < (rh + 7) * rw; q += 64) {
+        const int i = q / rw, j = q - i * rw;
         const uint8_t* row = win + i * WC + j;
         int hs = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) hs += hf[u] * row[u];
-        hb[i * MAXB + j] = (int16_t)r2(hs, R0);
+        hb[i * TS + j] = (int16_t)r2(hs, R0);
     }
 }
 
 // The same sample as pred_direct for an unscaled, unwarped reference: the vertical pass
 // over the staged intermediate rows (or the integer-position copy from the window).
-template <int MAXB>
-DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int c, int R0, int R1, const int16_t* vf, int integer)
+DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer)
 {
-    constexpr int WC = InterLds<MAXB>::WC;
-    if (integer) return (int16_t)(win[(rr + 3) * WC + c + 3] << (14 - R0 - R1));
-    const int16_t* col = hb + rr * MAXB + c;
+    if (integer) return (int16_t)(win[(rr + 3) * WC + cc + 3] << (14 - R0 - R1));
+    const int16_t* col = hb + rr * TS + cc;
     int s = 0;
 #pragma unroll
-    for (int t = 0; t < 8; t++) s += vf[t] * col[t * MAXB];
+    for (int t = 0; t < 8; t++) s += vf[t] * col[t * TS];
     return (int16_t)r2(s, R1);
 }
 
 // blockWarp (InterPredict.cpp:507-553), split like the reference into its horizontal
-// pass -- the 15 x 8 intermediate of every 8x8 block of strip rows [r0, r0 + nr), read
-// straight from the reference plane -- and the vertical pass per output sample.
+// pass -- the 15 x 8 intermediate of every 8x8 block of the region, read straight from
+// the reference plane -- and the vertical pass per output sample.
 DEV void warp_origin(const RefSel& R, int i8, int j8, int puX, int puY, int sub, int& ix4, int& sx4, int& iy4, int& sy4)
 {
     const int32_t* wp = R.wp;
@@ -407,13 +404,13 @@ DEV void warp_origin(const RefSel& R, int i8, int j8, int puX, int puY, int sub,
     iy4 = y4 >> 16;
     sy4 = y4 & 0xffff;
 }
-template <int NT>
-DEV void warp_hpass(const RefSel& R, int16_t* hb, int r0, int nr, int w, int puX, int puY, int sub, int R0)
+DEV void warp_hpass(const RefSel& R, int16_t* hb, int rx0, int ry0, int rw, int rh, int puX, int puY, int sub, int R0)
 {
-    const int nb = (nr >> 3) * (w >> 3), w8 = w >> 3;
-    for (int q = threadIdx.x; q < nb * 120; q += NT) {
+    const int w8 = rw >> 3, nb = (rh >> 3) * w8;
+    for (int q = threadIdx.x; q < nb * 120; q += 64) {
         const int b = q / 120, e = q - b * 120;
-        const int i8 = (r0 >> 3) + b / w8, j8 = b - (b / w8) * w8;
+        const int bi = b / w8;
+        const int i8 = (ry0 >> 3) + bi, j8 = (rx0 >> 3) + (b - bi * w8);
         int ix4, sx4, iy4, sy4;
         warp_origin(R, i8, j8, puX, puY, sub, ix4, sx4, iy4, sy4);
         const int i1 = (e >> 3) - 7, i2 = (e & 7) - 4;
@@ -426,14 +423,14 @@ DEV void warp_hpass(const RefSel& R, int16_t* hb, int r0, int nr, int w, int puX
         hb[q] = (int16_t)r2(hs, R0);
     }
 }
-DEV int warp_v(const RefSel& R, const int16_t* hb, int rr, int r, int c, int w, int puX, int puY, int sub, int R1)
+DEV int warp_v(const RefSel& R, const int16_t* hb, int rr, int cc, int r, int c, int rw, int puX, int puY, int sub, int R1)
 {
     int ix4, sx4, iy4, sy4;
     warp_origin(R, r >> 3, c >> 3, puX, puY, sub, ix4, sx4, iy4, sy4);
     const int i1 = (r & 7) - 4, i2 = (c & 7) - 4;
     const int sy = sy4 + R.gamma * i2 + R.delta * i1;
     const int8_t* vf = av1r_warped_filters + (r2(sy, 10) + 64) * 8;
-    const int16_t* col = hb + ((rr >> 3) * (w >> 3) + (c >> 3)) * 120 + (r & 7) * 8 + (c & 7);
+    const int16_t* col = hb + ((rr >> 3) * (rw >> 3) + (cc >> 3)) * 120 + (r & 7) * 8 + (c & 7);
     int s = 0;
 #pragma unroll
     for (int i3 = 0; i3 < 8; i3++) s += vf[i3] * col[i3 * 8];
@@ -504,11 +501,11 @@ DEV void distance_weights(const KParams& k, const av1r_mi& info, int& fwd, int& 
     bck = av1r_quant_dist_lookup[i][1 - order];
 }
 
-// predict_inter for one PU of one plane; result blended into L.tile (block-relative
-// origin (ox, oy)).
-template <int MAXB, int NT>
-DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int plane, int x, int y,
-    int w, int h, int candRow, int candCol, int ox, int oy)
+// predict_inter for the PU-relative region [rx0, rx0 + rw) x [ry0, ry0 + rh) of the
+// w x h prediction unit at plane position (x, y); sample (r, c) of the PU lands in
+// L.tile[(toy + r) * TS + tox + c].  Ends with a barrier.
+DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int x, int y,
+    int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy)
 {
     const int t = threadIdx.x;
     const av1r_frame_hdr& hd = *k.hdr;
@@ -517,6 +514,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, 
     const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
     const int isIntrabc = (blk.flags & AV1R_BLK_INTRABC) != 0;
     const int isGlobalMode = blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV;
+    const int sub = plane ? 1 : 0;
     RefSel R[2];
     int16_t hf[2][8], vf[2][8];
     int integer[2];
@@ -543,7 +541,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, 
         if (R[l].warp) setup_shear(R[l].wp, R[l].alpha, R[l].beta, R[l].gamma, R[l].delta);
         R[l].filtX = filter_idx(info.filt, w, 1);
         R[l].filtY = filter_idx(info.filt, h, 0);
-        R[l].useWin = !R[l].warp && R[l].xStep == 1024 && R[l].yStep == 1024 && w <= MAXB;
+        R[l].useWin = !R[l].warp && R[l].xStep == 1024 && R[l].yStep == 1024;
         const int hph = (R[l].startX >> 6) & 15, vph = (R[l].startY >> 6) & 15;
         integer[l] = !hph && !vph;
 #pragma unroll
@@ -553,10 +551,8 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, 
         }
     }
     const int ct = blk.compound_type;
-    const int isII = mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] == AV1R_INTRA_FRAME;
-    const int sub = plane ? 1 : 0;
-    int mode;  // 0 plain, 1 average, 2 distance, 3 mask blend
-    if (!isCompound && !isII) mode = 0;
+    int mode;  // 0 single reference (inter-intra: blended later by ii_item), 1 average, 2 distance, 3 mask
+    if (!isCompound) mode = 0;
     else if (ct == AV1R_COMPOUND_AVERAGE) mode = 1;
     else if (ct == AV1R_COMPOUND_DISTANCE) mode = 2;
     else mode = 3;
@@ -564,94 +560,79 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, 
     if (mode == 2) distance_weights(k, info, fwd, bck);
     WedgeSel ws = {0, 0, 0, 0};
     if (mode == 3 && ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
-    const int ii = (blk.flags & AV1R_BLK_INTERINTRA) != 0, wii = (blk.flags & AV1R_BLK_WEDGE_II) != 0;
     const int diffwtdLuma = ct == AV1R_COMPOUND_DIFFWTD && plane == 0;
-    const int sizeScale = 128 / imax(h, w);
-    for (int r0 = 0; r0 < h; r0 += STRIPR) {
-        const int nr = imin(STRIPR, h - r0);
-        if (R[0].useWin) load_window<MAXB, NT>(R[0], L.win[0], r0, nr, w);
-        if (isCompound && R[1].useWin) load_window<MAXB, NT>(R[1], L.win[1], r0, nr, w);
-        __syncthreads();
-        if (R[0].useWin && !integer[0]) hpass<MAXB, NT>(L.win[0], L.hb[0], nr, w, hf[0], R0);
-        if (R[0].warp) warp_hpass<NT>(R[0], L.hb[0], r0, nr, w, x, y, sub, R0);
-        if (isCompound && R[1].useWin && !integer[1]) hpass<MAXB, NT>(L.win[1], L.hb[1], nr, w, hf[1], R0);
-        if (isCompound && R[1].warp) warp_hpass<NT>(R[1], L.hb[1], r0, nr, w, x, y, sub, R0);
-        __syncthreads();
-        for (int q = t; q < w * nr; q += NT) {
-            const int rr = q / w, c = q - rr * w, r = r0 + rr;
-            int p0 = R[0].useWin ? pred_win<MAXB>(L.win[0], L.hb[0], rr, c, R0, R1, vf[0], integer[0])
-                     : R[0].warp ? warp_v(R[0], L.hb[0], rr, r, c, w, x, y, sub, R1)
-                                 : pred_direct(R[0], r, c, R0, R1);
-            int p1 = 0;
-            if (isCompound)
-                p1 = R[1].useWin ? pred_win<MAXB>(L.win[1], L.hb[1], rr, c, R0, R1, vf[1], integer[1])
-                     : R[1].warp ? warp_v(R[1], L.hb[1], rr, r, c, w, x, y, sub, R1)
-                                 : pred_direct(R[1], r, c, R0, R1);
-            int v;
-            if (mode == 0) {
-                v = clip1(p0);
-            } else if (mode == 1) {
-                v = clip1(r2(p0 + p1, 1 + PostRound));
-            } else if (mode == 2) {
-                v = clip1(r2(fwd * p0 + bck * p1, 4 + PostRound));
+
+    if (R[0].useWin) load_window(R[0], L.win[0], rx0, ry0, rw, rh);
+    if (isCompound && R[1].useWin) load_window(R[1], L.win[1], rx0, ry0, rw, rh);
+    __syncthreads();
+    if (R[0].useWin && !integer[0]) hpass(L.win[0], L.hb[0], rw, rh, hf[0], R0);
+    if (R[0].warp) warp_hpass(R[0], L.hb[0], rx0, ry0, rw, rh, x, y, sub, R0);
+    if (isCompound && R[1].useWin && !integer[1]) hpass(L.win[1], L.hb[1], rw, rh, hf[1], R0);
+    if (isCompound && R[1].warp) warp_hpass(R[1], L.hb[1], rx0, ry0, rw, rh, x, y, sub, R0);
+    __syncthreads();
+    for (int q = t; q < rw * rh; q += 64) {
+        const int rr = q / rw, cc = q - rr * rw, r = ry0 + rr, c = rx0 + cc;
+        int p0 = R[0].useWin ? pred_win(L.win[0], L.hb[0], rr, cc, R0, R1, vf[0], integer[0])
+                 : R[0].warp ? warp_v(R[0], L.hb[0], rr, cc, r, c, rw, x, y, sub, R1)
+                             : pred_direct(R[0], r, c, R0, R1);
+        int p1 = 0;
+        if (isCompound)
+            p1 = R[1].useWin ? pred_win(L.win[1], L.hb[1], rr, cc, R0, R1, vf[1], integer[1])
+                 : R[1].warp ? warp_v(R[1], L.hb[1], rr, cc, r, c, rw, x, y, sub, R1)
+                             : pred_direct(R[1], r, c, R0, R1);
+        int v;
+        if (mode == 0) {
+            v = clip1(p0);
+        } else if (mode == 1) {
+            v = clip1(r2(p0 + p1, 1 + PostRound));
+        } else if (mode == 2) {
+            v = clip1(r2(fwd * p0 + bck * p1, 4 + PostRound));
+        } else {
+            // mask (wedgeMask / differenceWeightMask) and maskBlend (InterPredict.cpp:555-609);
+            // mask blocks are single-PU, so PU and block coordinates coincide
+            int m;
+            if (diffwtdLuma) {
+                int diff = (int16_t)iabs(p0 - p1);
+                diff = r2(diff, PostRound);
+                int mm = CLIP3(0, 64, 38 + diff / 16);
+                m = blk.mask_type ? 64 - mm : mm;
+                L.mask[(toy + r) * TS + tox + c] = (uint8_t)m;
+            } else if (!sub) {
+                if (ct == AV1R_COMPOUND_WEDGE) {
+                    int mv = wedge_master(ws.dir, ws.yoff + r, ws.xoff + c);
+                    m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
+                } else {
+                    m = L.mask[(toy + r) * TS + tox + c];
+                }
             } else {
-                // mask (wedgeMask / intraModeVariantMask / differenceWeightMask) and
-                // maskBlend (InterPredict.cpp:555-609)
-                int m;
-                if (diffwtdLuma) {
-                    int diff = (int16_t)iabs(p0 - p1);
-                    diff = r2(diff, PostRound);
-                    int mm = CLIP3(0, 64, 38 + diff / 16);
-                    m = blk.mask_type ? 64 - mm : mm;
-                    L.mask[r * MAXB + c] = (uint8_t)m;
-                } else if (ct == AV1R_COMPOUND_INTRA || (ii && !wii) || !sub) {
-                    if (ct == AV1R_COMPOUND_WEDGE) {
-                        int mv = wedge_master(ws.dir, ws.yoff + r, ws.xoff + c);
-                        m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
-                    } else if (ct == AV1R_COMPOUND_INTRA) {
-                        int im = blk.interintra_mode;
-                        m = im == AV1R_II_V_PRED ? av1r_ii_weights_1d[r * sizeScale]
-                            : im == AV1R_II_H_PRED ? av1r_ii_weights_1d[c * sizeScale]
-                            : im == AV1R_II_SMOOTH_PRED ? av1r_ii_weights_1d[imin(r, c) * sizeScale] : 32;
-                    } else {
-                        m = L.mask[r * MAXB + c];
-                    }
-                } else {
-                    // 4:2:0 chroma: average of the 2x2 luma-resolution mask entries
-                    int s4 = 0;
+                // 4:2:0 chroma: average of the 2x2 luma-resolution mask entries
+                int s4 = 0;
 #pragma unroll
-                    for (int dy = 0; dy < 2; dy++)
+                for (int dy = 0; dy < 2; dy++)
 #pragma unroll
-                        for (int dx = 0; dx < 2; dx++) {
-                            int rr2 = 2 * r + dy, cc = 2 * c + dx;
-                            int mv;
-                            if (ct == AV1R_COMPOUND_WEDGE) {
-                                int mw = wedge_master(ws.dir, ws.yoff + rr2, ws.xoff + cc);
-                                mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
-                            } else {
-                                mv = L.mask[rr2 * MAXB + cc];
-                            }
-                            s4 += mv;
+                    for (int dx = 0; dx < 2; dx++) {
+                        int mv;
+                        if (ct == AV1R_COMPOUND_WEDGE) {
+                            int mw = wedge_master(ws.dir, ws.yoff + 2 * r + dy, ws.xoff + 2 * c + dx);
+                            mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
+                        } else {
+                            mv = L.mask[(2 * (toy + r) + dy) * TS + 2 * (tox + c) + dx];
                         }
-                    m = r2(s4, 2);
-                }
-                if (ii) {
-                    int pp0 = clip1(r2(p0, PostRound));
-                    int pp1 = L.tile[(oy + r) * MAXB + ox + c];
-                    v = clip1(r2(m * pp1 + (64 - m) * pp0, 6));
-                } else {
-                    v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
-                }
+                        s4 += mv;
+                    }
+                m = r2(s4, 2);
             }
-            L.tile[(oy + r) * MAXB + ox + c] = (uint8_t)v;
+            v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
         }
-        __syncthreads();
+        L.tile[(toy + r) * TS + tox + c] = (uint8_t)v;
     }
+    __syncthreads();
 }
 
-// overlappedMotionCompensation (InterPredict.cpp:611-709) on the plane tile.
-template <int MAXB, int NT>
-DEV void obmc(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int plane, int baseX, int baseY, int w, int h)
+// overlappedMotionCompensation (InterPredict.cpp:611-709) restricted to the tile
+// [TX0, TX0 + TW) x [TY0, TY0 + TH) (block-relative plane coordinates).
+DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int baseX, int baseY, int w, int h,
+    int TX0, int TY0, int TW, int TH)
 {
     const int t = threadIdx.x;
     const int sub = plane ? 1 : 0;
@@ -665,7 +646,6 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int pl
         const int lim = pass ? imin(k.mi_rows, blk.mi_row + n4) : imin(k.mi_cols, blk.mi_col + n4);
         int pos4 = pass ? blk.mi_row : blk.mi_col;
         int nCount = 0;
-        // the neighbours of one pass cover disjoint pixel ranges
         while (nCount < nLimit && pos4 < lim) {
             int candRow = pass ? (pos4 | 1) : blk.mi_row - 1;
             int candCol = pass ? blk.mi_col - 1 : (pos4 | 1);
@@ -679,33 +659,36 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int pl
                 int len = pass ? predW : predH;
                 const uint8_t* mask = av1r_obmc_mask + (len == 2 ? 0 : len == 4 ? 2 : len == 8 ? 6 : len == 16 ? 14 : 30);
                 int predX = (x4 * 4) >> sub, predY = (y4 * 4) >> sub;
-                RefSel R;
-                select_ref(k, R, hd.ref_frame_idx[info.ref_frame[0] - 1], plane, predX, predY, info.mv[0]);
-                R.filtX = filter_idx(info.filt, predW, 1);
-                R.filtY = filter_idx(info.filt, predH, 0);
-                R.useWin = R.xStep == 1024 && R.yStep == 1024;
-                const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
-                const int integer = !hph && !vph;
-                int16_t hf[8], vf[8];
+                const int ox = predX - baseX, oy = predY - baseY;
+                const int ix0 = imax(ox, TX0), ix1 = imin(ox + predW, TX0 + TW);
+                const int iy0 = imax(oy, TY0), iy1 = imin(oy + predH, TY0 + TH);
+                if (ix0 < ix1 && iy0 < iy1) {
+                    const int rx0 = ix0 - ox, ry0 = iy0 - oy, rw = ix1 - ix0, rh = iy1 - iy0;
+                    RefSel R;
+                    select_ref(k, R, hd.ref_frame_idx[info.ref_frame[0] - 1], plane, predX, predY, info.mv[0]);
+                    R.filtX = filter_idx(info.filt, predW, 1);
+                    R.filtY = filter_idx(info.filt, predH, 0);
+                    R.useWin = R.xStep == 1024 && R.yStep == 1024;
+                    const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
+                    const int integer = !hph && !vph;
+                    int16_t hf[8], vf[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    hf[u] = av1r_subpel_filters[(R.filtX * 16 + hph) * 8 + u];
-                    vf[u] = av1r_subpel_filters[(R.filtY * 16 + vph) * 8 + u];
-                }
-                for (int r0 = 0; r0 < predH; r0 += STRIPR) {
-                    const int nr = imin(STRIPR, predH - r0);
+                    for (int u = 0; u < 8; u++) {
+                        hf[u] = av1r_subpel_filters[(R.filtX * 16 + hph) * 8 + u];
+                        vf[u] = av1r_subpel_filters[(R.filtY * 16 + vph) * 8 + u];
+                    }
                     if (R.useWin) {
-                        load_window<MAXB, NT>(R, L.win[0], r0, nr, predW);
+                        load_window(R, L.win[0], rx0, ry0, rw, rh);
                         __syncthreads();
-                        if (!integer) hpass<MAXB, NT>(L.win[0], L.hb[0], nr, predW, hf, 3);
+                        if (!integer) hpass(L.win[0], L.hb[0], rw, rh, hf, 3);
                         __syncthreads();
                     }
-                    for (int q = t; q < predW * nr; q += NT) {
-                        const int rr = q / predW, j = q - rr * predW, i = r0 + rr;
-                        int p = R.useWin ? pred_win<MAXB>(L.win[0], L.hb[0], rr, j, 3, 11, vf, integer)
+                    for (int q = t; q < rw * rh; q += 64) {
+                        const int rr = q / rw, cc = q - rr * rw, i = ry0 + rr, j = rx0 + cc;
+                        int p = R.useWin ? pred_win(L.win[0], L.hb[0], rr, cc, 3, 11, vf, integer)
                                          : pred_direct(R, i, j, 3, 11);
                         int m = pass ? mask[j] : mask[i];
-                        uint8_t& d = L.tile[(predY - baseY + i) * MAXB + predX - baseX + j];
+                        uint8_t& d = L.tile[(oy + i - TY0) * TS + ox + j - TX0];
                         d = (uint8_t)clip1(r2(m * d + (64 - m) * clip1(p), 6));
                     }
                     __syncthreads();
@@ -713,58 +696,26 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds<MAXB>& L, int pl
             }
             pos4 += step4;
         }
-        __syncthreads();
     }
 }
 
-DEV void intra_noinline(int miCols, int miRows, DevPlane src, IntraParams P, IntraLds& L, uint8_t* pred)
+// One tile (tx, ty) of inter block `bi`: all planes.
+DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L)
 {
-    coop_intra_predict(miCols, miRows, src, P, L, pred, 32);
-}
-
-template <int MAXB, int NT>
-DEV void inter_block(const KParams& k)
-{
-    __shared__ InterLds<MAXB> L;
     const int t = threadIdx.x;
-    const av1r_block& blk = k.blocks[k.items[blockIdx.x]];
+    const av1r_block& blk = k.blocks[bi];
     const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
     const int bs = blk.mi_size;
     const int bw = av1r_num4x4w[bs] * 4, bh = av1r_num4x4h[bs] * 4;
-    const int isII = mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] == AV1R_INTRA_FRAME;
     for (int plane = 0; plane < 1 + hasChroma * 2; plane++) {
         const int psz = plane_bsize(bs, plane);
         const int n4w = av1r_num4x4w[psz], n4h = av1r_num4x4h[psz];
         const int sub = plane ? 1 : 0;
         const int baseX = (blk.mi_col >> sub) * 4, baseY = (blk.mi_row >> sub) * 4;
         const int pw = n4w * 4, ph = n4h * 4;
-        if (isII) {
-            // block-level intra prediction of an inter-intra block (Block.cpp:118-144)
-            int im = blk.interintra_mode;
-            IntraParams P;
-            P.plane = plane;
-            P.x = baseX;
-            P.y = baseY;
-            P.log2W = 2 + av1r_miw_log2[psz];
-            P.log2H = 2 + av1r_mih_log2[psz];
-            P.haveLeft = plane ? (blk.flags & AV1R_BLK_AVAIL_L_UV) != 0 : (blk.flags & AV1R_BLK_AVAIL_L) != 0;
-            P.haveAbove = plane ? (blk.flags & AV1R_BLK_AVAIL_U_UV) != 0 : (blk.flags & AV1R_BLK_AVAIL_U) != 0;
-            P.haveAR = (blk.ii_edge >> (2 * plane)) & 1;
-            P.haveBL = (blk.ii_edge >> (2 * plane + 1)) & 1;
-            P.mode = im == AV1R_II_DC_PRED ? AV1R_DC_PRED : im == AV1R_II_V_PRED ? AV1R_V_PRED
-                : im == AV1R_II_H_PRED ? AV1R_H_PRED : AV1R_SMOOTH_PRED;
-            P.angleDelta = 0;
-            P.filterIntra = 0;
-            P.filterIntraMode = 0;
-            P.smooth = 0;
-            P.edgeFilter = k.hdr->enable_intra_edge_filter;
-            intra_noinline(k.mi_cols, k.mi_rows, k.cur.pl[plane], P, L.intra, L.iipred);
-            for (int q = t; q < pw * ph; q += NT) {
-                int i = q / pw, j = q - i * pw;
-                L.tile[i * MAXB + j] = L.iipred[i * 32 + j];
-            }
-            __syncthreads();
-        }
+        const int TX0 = (tx * TS) >> sub, TY0 = (ty * TS) >> sub;
+        const int TW = imin(TS >> sub, pw - TX0), TH = imin(TS >> sub, ph - TY0);
+        // prediction units (Block.cpp:146-174): sub-8x8 chroma may gather several
         int candRow = (blk.mi_row >> sub) << sub, candCol = (blk.mi_col >> sub) << sub;
         int predW = bw >> sub, predH = bh >> sub;
         int someUseIntra = 0;
@@ -781,33 +732,107 @@ DEV void inter_block(const KParams& k)
         for (int yy = 0; yy < ph; yy += predH) {
             int c = 0;
             for (int xx = 0; xx < pw; xx += predW) {
-                predict_pu<MAXB, NT>(k, blk, L, plane, baseX + xx, baseY + yy, predW, predH, candRow + r, candCol + c, xx, yy);
+                const int ix0 = imax(xx, TX0), ix1 = imin(xx + predW, TX0 + TW);
+                const int iy0 = imax(yy, TY0), iy1 = imin(yy + predH, TY0 + TH);
+                if (ix0 < ix1 && iy0 < iy1)
+                    predict_pu(k, blk, L, plane, baseX + xx, baseY + yy, predW, predH, candRow + r, candCol + c,
+                        ix0 - xx, iy0 - yy, ix1 - ix0, iy1 - iy0, xx - TX0, yy - TY0);
                 c++;
             }
             r++;
         }
-        if (blk.motion_mode == AV1R_OBMC_CAUSAL) obmc<MAXB, NT>(k, blk, L, plane, baseX, baseY, predW, predH);
+        if (blk.motion_mode == AV1R_OBMC_CAUSAL) obmc(k, blk, L, plane, baseX, baseY, predW, predH, TX0, TY0, TW, TH);
         const DevPlane& dst = k.cur.pl[plane];
-        for (int q = t; q < pw * ph; q += NT) {
-            int i = q / pw, j = q - i * pw;
-            px(dst, baseX + j, baseY + i) = L.tile[i * MAXB + j];
+        for (int q = t; q < TW * TH; q += 64) {
+            int i = q / TW, j = q - i * TW;
+            px(dst, baseX + TX0 + j, baseY + TY0 + i) = L.tile[i * TS + j];
         }
         __syncthreads();
     }
 }
 
-// blocks up to 32x32: one wave per block
-extern "C" __global__ __launch_bounds__(64) void k_inter_s(KParams k) { inter_block<32, 64>(k); }
-// larger blocks: 256 lanes
-extern "C" __global__ __launch_bounds__(256) void k_inter_l(KParams k) { inter_block<128, 256>(k); }
+// Inter-intra blend of block `bi` (Block.cpp:118-144 + maskBlend, InterPredict.cpp:555-609):
+// the block's intra prediction (its edges are final when this item runs) blended with the
+// inter prediction inter_tile stored in the frame.
+DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
+{
+    const int t = threadIdx.x;
+    const av1r_block& blk = k.blocks[bi];
+    const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
+    const int bs = blk.mi_size;
+    const int im = blk.interintra_mode;
+    const int isWedge = blk.compound_type == AV1R_COMPOUND_WEDGE;
+    WedgeSel ws = {0, 0, 0, 0};
+    if (isWedge) ws = wedge_select(bs, blk.wedge_index);
+    for (int plane = 0; plane < 1 + hasChroma * 2; plane++) {
+        const int psz = plane_bsize(bs, plane);
+        const int sub = plane ? 1 : 0;
+        const int baseX = (blk.mi_col >> sub) * 4, baseY = (blk.mi_row >> sub) * 4;
+        const int pw = av1r_num4x4w[psz] * 4, ph = av1r_num4x4h[psz] * 4;
+        const DevPlane& dst = k.cur.pl[plane];
+        IntraParams P;
+        P.plane = plane;
+        P.x = baseX;
+        P.y = baseY;
+        P.log2W = 2 + av1r_miw_log2[psz];
+        P.log2H = 2 + av1r_mih_log2[psz];
+        P.haveLeft = plane ? (blk.flags & AV1R_BLK_AVAIL_L_UV) != 0 : (blk.flags & AV1R_BLK_AVAIL_L) != 0;
+        P.haveAbove = plane ? (blk.flags & AV1R_BLK_AVAIL_U_UV) != 0 : (blk.flags & AV1R_BLK_AVAIL_U) != 0;
+        P.haveAR = (blk.ii_edge >> (2 * plane)) & 1;
+        P.haveBL = (blk.ii_edge >> (2 * plane + 1)) & 1;
+        P.mode = im == AV1R_II_DC_PRED ? AV1R_DC_PRED : im == AV1R_II_V_PRED ? AV1R_V_PRED
+            : im == AV1R_II_H_PRED ? AV1R_H_PRED : AV1R_SMOOTH_PRED;
+        P.angleDelta = 0;
+        P.filterIntra = 0;
+        P.filterIntraMode = 0;
+        P.smooth = 0;
+        P.edgeFilter = k.hdr->enable_intra_edge_filter;
+        coop_intra_predict(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
+        const int sizeScale = 128 / imax(ph, pw);
+        for (int q = t; q < pw * ph; q += 64) {
+            const int i = q / pw, j = q - i * pw;
+            int m;
+            if (!isWedge) {
+                m = im == AV1R_II_V_PRED ? av1r_ii_weights_1d[i * sizeScale]
+                    : im == AV1R_II_H_PRED ? av1r_ii_weights_1d[j * sizeScale]
+                    : im == AV1R_II_SMOOTH_PRED ? av1r_ii_weights_1d[imin(i, j) * sizeScale] : 32;
+            } else if (!sub) {
+                int mv = wedge_master(ws.dir, ws.yoff + i, ws.xoff + j);
+                m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
+            } else {
+                int s4 = 0;
+#pragma unroll
+                for (int dy = 0; dy < 2; dy++)
+#pragma unroll
+                    for (int dx = 0; dx < 2; dx++) {
+                        int mw = wedge_master(ws.dir, ws.yoff + 2 * i + dy, ws.xoff + 2 * j + dx);
+                        s4 += blk.wedge_sign == ws.flip ? mw : 64 - mw;
+                    }
+                m = r2(s4, 2);
+            }
+            uint8_t& d = px(dst, baseX + j, baseY + i);
+            d = (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6));
+        }
+        __syncthreads();
+    }
+}
 
 // ---------------------------------------------------------------------------------
-void launch_k_tb(const KParams& k, unsigned n, hipStream_t s)
+// One launch per dependency level: every work item of the level (inter tiles, inter-
+// intra blends, transform blocks) is one 64-lane workgroup.
+// ---------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(64) void k_level(KParams k)
 {
-    hipLaunchKernelGGL(k_tb, dim3(n), dim3(64), 0, s, k);
+    constexpr size_t kLds = sizeof(TbLds) > sizeof(InterLds) ? sizeof(TbLds) : sizeof(InterLds);
+    __shared__ __align__(16) uint8_t smem[kLds];
+    const uint32_t it = k.items[blockIdx.x];
+    const uint32_t kind = AV1R_ITEM_KIND(it), idx = AV1R_ITEM_INDEX(it);
+    if (kind == AV1R_ITEM_TB) tb_item(k, idx, *reinterpret_cast<TbLds*>(smem));
+    else if (kind == AV1R_ITEM_INTER) inter_tile(k, idx >> 4, idx & 3, (idx >> 2) & 3, *reinterpret_cast<InterLds*>(smem));
+    else ii_item(k, idx, *reinterpret_cast<TbLds*>(smem));
 }
-void launch_k_inter(const KParams& k, unsigned n, int large, hipStream_t s)
+
+void launch_k_level(const KParams& k, unsigned n, hipStream_t s)
 {
-    if (large) hipLaunchKernelGGL(k_inter_l, dim3(n), dim3(256), 0, s, k);
-    else hipLaunchKernelGGL(k_inter_s, dim3(n), dim3(64), 0, s, k);
+    hipLaunchKernelGGL(k_level, dim3(n), dim3(64), 0, s, k);
 }
