@@ -469,9 +469,12 @@ DEV WedgeSel wedge_select(int bs, int wedge)
     s.xoff = 32 - ((cb[1] * w) >> 3);
     s.yoff = 32 - ((cb[2] * h) >> 3);
     // flipSign (initialise_wedge_mask_table, InterPredict.cpp:870-877)
+    // (the w + h - 1 edge samples summed across the wave; call with all 64 lanes active)
     int sum = 0;
-    for (int i = 0; i < w; i++) sum += wedge_master(s.dir, s.yoff, s.xoff + i);
-    for (int i = 1; i < h; i++) sum += wedge_master(s.dir, s.yoff + i, s.xoff);
+    for (int i = threadIdx.x; i < w + h - 1; i += 64)
+        sum += i < w ? wedge_master(s.dir, s.yoff, s.xoff + i) : wedge_master(s.dir, s.yoff + i - w + 1, s.xoff);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     int avg = (sum + (w + h - 1) / 2) / (w + h - 1);
     s.flip = avg < 32;
     return s;
@@ -719,9 +722,12 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L)
         int candRow = (blk.mi_row >> sub) << sub, candCol = (blk.mi_col >> sub) << sub;
         int predW = bw >> sub, predH = bh >> sub;
         int someUseIntra = 0;
-        for (int r = 0; r < (n4h << sub); r++)
-            for (int c = 0; c < (n4w << sub); c++)
-                if (mi_at(k, candRow + r, candCol + c).ref_frame[0] == AV1R_INTRA_FRAME) someUseIntra = 1;
+        // only a sub-8x8 chroma block can change its PU layout (otherwise the gathered
+        // geometry equals the block's own)
+        if (predW != pw || predH != ph || candRow != blk.mi_row || candCol != blk.mi_col)
+            for (int r = 0; r < (n4h << sub); r++)
+                for (int c = 0; c < (n4w << sub); c++)
+                    if (mi_at(k, candRow + r, candCol + c).ref_frame[0] == AV1R_INTRA_FRAME) someUseIntra = 1;
         if (someUseIntra) {
             predW = pw;
             predH = ph;
