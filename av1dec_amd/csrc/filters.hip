@@ -8,9 +8,10 @@
 //   k_cdef  one wave per 8x8 luma block, lane = pixel: Cdef::cdef_block (Cdef.cpp:72-101),
 //           cdefDirection via LDS partial sums (:203-261), cdefFilter (:158-198) into a
 //           separate output frame (blocks that are skipped are copied).
-//   k_lr    one lane per output pixel: LoopRestoration Wiener (LoopRestoration.cpp:247-277)
-//           and self-guided (:284-479) with the stripe/unit geometry of :33-189; the
-//           3-pixel border extension (:196-198) is coordinate clamping.
+//   k_lr    one workgroup per 64-column tile of a (half-)stripe, source staged in LDS:
+//           LoopRestoration Wiener (LoopRestoration.cpp:247-277) and self-guided
+//           (:284-479) with the stripe/unit geometry of :33-189; the 3-pixel border
+//           extension (:196-198) is coordinate clamping.
 #include "av1r_dev.h"
 
 // ------------------------------------------------------------------------------------
@@ -35,6 +36,29 @@ DEV int lf_level(const KParams& k, int row, int col, int plane, int pass)
         l = (int8_t)CLIP3(0, 63, l);
     }
     return l;
+}
+
+// wideFilter (LoopFilter.cpp:246-289): F[i] = Round2(sum_j tap(j) * clamp(i + j), log2Size)
+// over the 2n samples around the edge; taps are 2 for |j| <= n2, else 1.
+template <int n, int log2Size, int n2>
+DEV void lf_wide(uint8_t* c, int step)
+{
+    int v[2 * n + 2];  // v[p + n + 1] = pixel at offset p, p in [-(n + 1), n]
+#pragma unroll
+    for (int p = -(n + 1); p <= n; p++) v[p + n + 1] = c[step * p];
+    int F[2 * n];
+#pragma unroll
+    for (int i = -n; i < n; i++) {
+        int t = 0;
+#pragma unroll
+        for (int j = -n; j <= n; j++) {
+            int p = CLIP3(-(n + 1), n, i + j);
+            t += v[p + n + 1] * ((j <= n2 && j >= -n2) ? 2 : 1);
+        }
+        F[i + n] = r2(t, log2Size);
+    }
+#pragma unroll
+    for (int i = -n; i < n; i++) c[step * i] = (uint8_t)F[i + n];
 }
 
 DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int blimit, int thresh, int dx, int dy, int filterSize)
@@ -78,22 +102,11 @@ DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int bl
         }
         return;
     }
-    const int log2Size = (filterSize == 8 || !flat2) ? 3 : 4;
-    const int n = log2Size == 4 ? 6 : (!plane ? 3 : 2);
-    const int n2 = (log2Size == 3 && !plane) ? 0 : 1;
-    int v[14];  // v[p + 7] = pixel at offset p, p in [-7, 6]
-#pragma unroll
-    for (int p = -7; p <= 6; p++) v[p + 7] = (p >= -(n + 1) && p <= n) ? c[step * p] : 0;
-    int F[12];
-    for (int i = -n; i < n; i++) {
-        int t = 0;
-        for (int j = -n; j <= n; j++) {
-            int p = CLIP3(-(n + 1), n, i + j);
-            t += v[p + 7] * ((iabs(j) <= n2) ? 2 : 1);
-        }
-        F[i + n] = r2(t, log2Size);
-    }
-    for (int i = -n; i < n; i++) c[step * i] = (uint8_t)F[i + n];
+    // wideFilter with compile-time taps (a runtime-indexed tap window would be lowered to
+    // per-lane waterfall loops)
+    if (filterSize >= 16 && flat2) lf_wide<6, 4, 1>(c, step);
+    else if (!plane) lf_wide<3, 3, 0>(c, step);
+    else lf_wide<2, 3, 1>(c, step);
 #undef PP
 #undef QQ
 }
@@ -285,22 +298,41 @@ DEV int lr_src(const LrPix& S, int x, int y)
     const bool pre = y < S.start || y >= S.end;
     if (y < S.start) y = imax(S.start - 2, y);
     else if (y >= S.end) y = imin(S.end + 1, y);
-    const DevPlane& P = pre ? S.preP : S.cdefP;
-    x = CLIP3(0, P.w - 1, x);
-    y = CLIP3(0, P.h - 1, y);
-    return P.p[(size_t)y * P.stride + x];
+    const uint8_t* base = pre ? S.preP.p : S.cdefP.p;  // (selects values: no struct address)
+    const int stride = pre ? S.preP.stride : S.cdefP.stride;
+    x = CLIP3(0, S.cdefP.w - 1, x);
+    y = CLIP3(0, S.cdefP.h - 1, y);
+    return base[(size_t)y * stride + x];
 }
 
-DEV void sgr_ab(const LrPix& S, int x, int y, int r, int set, int pass, int& A, int& B)
+// Tiles of LR_TW columns x one half-stripe (luma) / one stripe (chroma) rows: inside a
+// tile the stripe (hence get_source_sample's row mapping) and the restoration-unit row are
+// fixed, so the source is staged once in LDS with its 3-pixel halo and every filter reads
+// only LDS.  Restoration units are at least 32 wide: a tile meets at most 3 unit columns.
+#define LR_TW 64
+#define LR_TH 32
+#define LR_SW (LR_TW + 8)
+struct LrLds {
+    uint8_t src[LR_TH + 6][LR_SW];        // get_source_sample over rows ty0-3.., cols x0-3..
+    int16_t hw[LR_TH + 6][LR_TW];         // Wiener horizontal pass
+    int16_t A[2][LR_TH + 2][LR_TW + 2];   // self-guided a per pass, rows ty0-1.., cols x0-1..
+    int32_t B[2][LR_TH + 2][LR_TW + 2];
+    av1r_lr_unit unit[3];
+};
+
+// a, b of the self-guided box at staged position (si, sj) = source (row, col) index of the
+// box centre (LoopRestoration.cpp:284-380, restated per position; 32-bit arithmetic as
+// the reference's)
+DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, int& A, int& B)
 {
-    int eps = av1r_sgr_params[set][pass * 2 + 1];
-    int n = (2 * r + 1) * (2 * r + 1);
-    int n2e = n * n * eps;
-    int s = ((1 << 20) + n2e / 2) / n2e;
+    const int eps = av1r_sgr_params[set][pass * 2 + 1];
+    const int n = (2 * r + 1) * (2 * r + 1);
+    const int n2e = n * n * eps;
+    const int s = ((1 << 20) + n2e / 2) / n2e;
     int a = 0, b = 0;
     for (int dy = -r; dy <= r; dy++)
         for (int dx = -r; dx <= r; dx++) {
-            int cv = lr_src(S, x + dx, y + dy);
+            int cv = L.src[si + dy][sj + dx];
             a += cv * cv;
             b += cv;
         }
@@ -316,89 +348,139 @@ DEV void sgr_ab(const LrPix& S, int x, int y, int r, int set, int pass, int& A, 
     B = r2(b2, 12);
 }
 
-// boxFilter output for pixel (x, y) = row i of the block that starts at row y0
-DEV int sgr_filter(const LrPix& S, const DevPlane& cdefP, int x, int y, int i, int set, int pass, int r)
-{
-    int shift = (pass == 0 && (i & 1)) ? 4 : 5;
-    int a = 0, b = 0;
-    for (int dy = -1; dy <= 1; dy++) {
-        if (pass == 0 && !((i + dy) & 1)) continue;
-        for (int dx = -1; dx <= 1; dx++) {
-            int wt = pass == 0 ? (dx == 0 ? 6 : 5) : ((dx == 0 || dy == 0) ? 4 : 3);
-            int A, B;
-            sgr_ab(S, x + dx, y + dy, r, set, pass, A, B);
-            a += wt * A;
-            b += wt * B;
-        }
-    }
-    int v = a * cdefP.p[(size_t)y * cdefP.stride + x] + b;
-    return r2(v, 8 + shift - 4);
-}
-
-// one lane per visible pixel, all planes in one launch (blockIdx.z = plane);
-// k.cur = CDEF frame, k.ref[0] = deblocked frame, k.out = restored frame.
+// one 256-lane workgroup per tile; blockIdx.z = plane.  k.cur = CDEF frame, k.ref[0] =
+// deblocked frame, k.out = restored frame.
 extern "C" __global__ __launch_bounds__(256) void k_lr(KParams k)
 {
-    const int plane = blockIdx.z;
+    __shared__ LrLds L;
+    const int t = threadIdx.x;
+    const int plane = blockIdx.z, sub = plane ? 1 : 0;
     const DevPlane C = k.cur.pl[plane];
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= C.w || y >= C.h) return;
+    const DevPlane O = k.out.pl[plane];
+    const int x0 = blockIdx.x * LR_TW;
+    if (x0 >= C.w) return;
+    const int stripeH = 64 >> sub, off = 8 >> sub;
+    const int perStripe = stripeH / LR_TH;
+    const int sNum = blockIdx.y / perStripe, half = blockIdx.y - sNum * perStripe;
+    LrPix S;
+    S.cdefP = C;
+    S.preP = k.ref[0].pl[plane];
+    S.start = sNum * stripeH - off;
+    S.end = S.start + stripeH;
+    const int ty0 = imax(0, S.start + half * LR_TH), ty1 = imin(S.start + (half + 1) * LR_TH, C.h);
+    if (ty0 >= ty1) return;
+    const int tw = imin(LR_TW, C.w - x0), th = ty1 - ty0;
     const av1r_frame_hdr& h = *k.hdr;
-    const int sub = plane ? 1 : 0;
-    uint8_t outv = C.p[(size_t)y * C.stride + x];
-    if (h.lr_type[plane] != AV1R_RESTORE_NONE) {
-        const int us = h.lr_unit_size[plane];
-        const int rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
-        const int off = 8 >> sub;
-        const int planeEndX = r2(k.frame_w, sub), planeEndY = r2(k.frame_h, sub);
-        if (x < planeEndX && y < planeEndY) {
-            int uc = imin(x / us, cols - 1);
-            int ur = imin((y + off) / us, rows - 1);
-            const av1r_lr_unit& u = k.lr[h.lr_unit_off[plane] + ur * cols + uc];
-            if (u.type != AV1R_RESTORE_NONE) {
-                int uy = ur * us;
-                if (uy) uy -= off;
-                int stripeNum = (y + off) / (64 >> sub);
-                LrPix S;
-                S.cdefP = C;
-                S.preP = k.ref[0].pl[plane];
-                S.start = (-8 + stripeNum * 64) >> sub;
-                S.end = S.start + (64 >> sub);
-                const int y0 = imax(S.start, uy);  // forEachBlock's y
-                if (u.type == AV1R_RESTORE_WIENER) {
-                    int vf[7], hf[7];
-                    vf[3] = hf[3] = 128;
-                    for (int q = 0; q < 3; q++) {
-                        vf[q] = vf[6 - q] = u.wiener[0][q];
-                        hf[q] = hf[6 - q] = u.wiener[1][q];
-                        vf[3] -= 2 * u.wiener[0][q];
-                        hf[3] -= 2 * u.wiener[1][q];
-                    }
-                    const int offset = 1 << (8 + 7 - 3 - 1), limit = (1 << (8 + 1 + 7 - 3)) - 1;
-                    int s = 0;
-                    for (int t = 0; t < 7; t++) {
-                        int hs = 0;
-                        for (int q = 0; q < 7; q++) hs += hf[q] * lr_src(S, x + q - 3, y + t - 3);
-                        int v = CLIP3(-offset, limit - offset, r2(hs, 3));
-                        s += vf[t] * v;
-                    }
-                    outv = (uint8_t)clip1(r2(s, 11));
-                } else {
-                    const int set = u.sgr_set;
-                    const int r0 = av1r_sgr_params[set][0], r1 = av1r_sgr_params[set][2];
-                    const int i = y - y0;
-                    int uu = C.p[(size_t)y * C.stride + x] << 4;
-                    int w0 = u.sgr_xqd[0], w1 = u.sgr_xqd[1], w2 = (1 << 7) - w0 - w1;
-                    int v = w1 * uu;
-                    v += r0 ? w0 * sgr_filter(S, C, x, y, i, set, 0, r0) : w0 * uu;
-                    v += r1 ? w2 * sgr_filter(S, C, x, y, i, set, 1, r1) : w2 * uu;
-                    outv = (uint8_t)clip1(r2(v, 4 + 7));
-                }
-            }
+    if (h.lr_type[plane] == AV1R_RESTORE_NONE) {
+        for (int q = t; q < tw * th; q += 256) {
+            int r = q / tw, c = q - r * tw;
+            O.p[(size_t)(ty0 + r) * O.stride + x0 + c] = C.p[(size_t)(ty0 + r) * C.stride + x0 + c];
+        }
+        return;
+    }
+    const int us = h.lr_unit_size[plane];
+    const int rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
+    const int planeEndX = r2(k.frame_w, sub), planeEndY = r2(k.frame_h, sub);
+    const int ur = imin((ty0 + off) / us, rows - 1);  // one unit row per stripe
+    const int uc0 = imin(x0 / us, cols - 1);
+    const int nU = imin((x0 + tw - 1) / us, cols - 1) - uc0 + 1;
+    if (t < nU) L.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
+    const int y0 = imax(S.start, 0);  // forEachBlock's y: the stripe's first row
+    // stage the source rows ty0-3 .. ty1+2, cols x0-3 .. x0+tw+2
+    for (int q = t; q < (th + 6) * (tw + 6); q += 256) {
+        int i = q / (tw + 6), j = q - i * (tw + 6);
+        L.src[i][j] = (uint8_t)lr_src(S, x0 - 3 + j, ty0 - 3 + i);
+    }
+    __syncthreads();
+    int anyW = 0, anyS = 0;
+    for (int u = 0; u < nU; u++) {
+        anyW |= L.unit[u].type == AV1R_RESTORE_WIENER;
+        anyS |= L.unit[u].type == AV1R_RESTORE_SGRPROJ;
+    }
+    auto unitOf = [&](int c) { return imin((x0 + CLIP3(0, tw - 1, c)) / us, cols - 1) - uc0; };
+    if (anyW) {
+        // wienerFilter horizontal pass (LoopRestoration.cpp:253-265)
+        const int offset = 1 << (8 + 7 - 3 - 1), limit = (1 << (8 + 1 + 7 - 3)) - 1;
+        for (int q = t; q < (th + 6) * tw; q += 256) {
+            int i = q / tw, c = q - i * tw;
+            const av1r_lr_unit& u = L.unit[unitOf(c)];
+            if (u.type != AV1R_RESTORE_WIENER) continue;
+            int hf3 = 128 - 2 * (u.wiener[1][0] + u.wiener[1][1] + u.wiener[1][2]);
+            const uint8_t* sp = &L.src[i][c];
+            int hs = u.wiener[1][0] * (sp[0] + sp[6]) + u.wiener[1][1] * (sp[1] + sp[5]) + u.wiener[1][2] * (sp[2] + sp[4]) + hf3 * sp[3];
+            L.hw[i][c] = (int16_t)CLIP3(-offset, limit - offset, r2(hs, 3));
         }
     }
-    k.out.pl[plane].p[(size_t)y * k.out.pl[plane].stride + x] = outv;
+    if (anyS) {
+        // a, b of both passes at rows ty0-1 .. ty1, cols x0-1 .. x0+tw
+        for (int q = t; q < 2 * (th + 2) * (tw + 2); q += 256) {
+            const int pass = q >= (th + 2) * (tw + 2);
+            const int e = q - pass * (th + 2) * (tw + 2);
+            const int ii = e / (tw + 2), cc = e - ii * (tw + 2);
+            const av1r_lr_unit& u = L.unit[unitOf(cc - 1)];
+            if (u.type != AV1R_RESTORE_SGRPROJ) continue;
+            const int r = av1r_sgr_params[u.sgr_set][pass * 2];
+            if (!r) continue;
+            if (pass == 0 && !((ty0 - 1 + ii - y0) & 1)) continue;  // pass 0 uses odd rows only
+            int A, B;
+            sgr_ab_lds(L, ii + 2, cc + 2, r, u.sgr_set, pass, A, B);
+            L.A[pass][ii][cc] = (int16_t)A;
+            L.B[pass][ii][cc] = B;
+        }
+    }
+    __syncthreads();
+    for (int q = t; q < tw * th; q += 256) {
+        const int r = q / tw, c = q - r * tw;
+        const int x = x0 + c, y = ty0 + r;
+        const int cdef = L.src[r + 3][c + 3];
+        int outv = cdef;
+        const int ui = unitOf(c);
+        const av1r_lr_unit& u = L.unit[ui];
+        if (x < planeEndX && y < planeEndY && u.type != AV1R_RESTORE_NONE) {
+            if (u.type == AV1R_RESTORE_WIENER) {
+                int vf3 = 128 - 2 * (u.wiener[0][0] + u.wiener[0][1] + u.wiener[0][2]);
+                int s = u.wiener[0][0] * (L.hw[r][c] + L.hw[r + 6][c]) + u.wiener[0][1] * (L.hw[r + 1][c] + L.hw[r + 5][c])
+                    + u.wiener[0][2] * (L.hw[r + 2][c] + L.hw[r + 4][c]) + vf3 * L.hw[r + 3][c];
+                outv = clip1(r2(s, 11));
+            } else {
+                // selfGuidedFilter (LoopRestoration.cpp:420-479)
+                const int set = u.sgr_set;
+                const int i = y - y0;
+                const int uu = cdef << 4;
+                const int w0 = u.sgr_xqd[0], w1 = u.sgr_xqd[1], w2 = (1 << 7) - w0 - w1;
+                int v = w1 * uu;
+#pragma unroll
+                for (int pass = 0; pass < 2; pass++) {
+                    const int rad = av1r_sgr_params[set][pass * 2];
+                    const int w = pass ? w2 : w0;
+                    if (!rad) {
+                        v += w * uu;
+                        continue;
+                    }
+                    const int shift = (pass == 0 && (i & 1)) ? 4 : 5;
+                    int a = 0, b = 0;
+                    for (int dy = -1; dy <= 1; dy++) {
+                        if (pass == 0 && !((i + dy) & 1)) continue;
+                        for (int dx = -1; dx <= 1; dx++) {
+                            const int wt = pass == 0 ? (dx == 0 ? 6 : 5) : ((dx == 0 || dy == 0) ? 4 : 3);
+                            int A, B;
+                            if (unitOf(c + dx) == ui) {
+                                A = L.A[pass][r + 1 + dy][c + 1 + dx];
+                                B = L.B[pass][r + 1 + dy][c + 1 + dx];
+                            } else {  // neighbour column in another unit: this unit's parameters
+                                sgr_ab_lds(L, r + 3 + dy, c + 3 + dx, rad, set, pass, A, B);
+                            }
+                            a += wt * A;
+                            b += wt * B;
+                        }
+                    }
+                    v += w * r2(a * cdef + b, 8 + shift - 4);
+                }
+                outv = clip1(r2(v, 4 + 7));
+            }
+        }
+        O.p[(size_t)y * O.stride + x] = (uint8_t)outv;
+    }
 }
 
 // plain visible-region copy (stage snapshots)
@@ -421,8 +503,10 @@ void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s)
 }
 void launch_k_lr(const KParams& k, hipStream_t s)
 {
+    // tile rows: luma stripes (64 rows from -8) in halves; chroma stripes whole
     const DevPlane& p = k.cur.pl[0];
-    hipLaunchKernelGGL(k_lr, dim3((p.w + 63) / 64, (p.h + 3) / 4, 3), dim3(256), 0, s, k);
+    const int tilesY = 2 * ((p.h + 8 + 63) / 64);
+    hipLaunchKernelGGL(k_lr, dim3((p.w + LR_TW - 1) / LR_TW, tilesY, 3), dim3(256), 0, s, k);
 }
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s)
 {
