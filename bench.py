@@ -61,6 +61,27 @@ def stage_bytes(frame):
     }
 
 
+def stream_seed(config_seed, rank):
+    """Stream i -> GPU i: every rank decodes its own independent stream."""
+    return config_seed + rank
+
+
+def max_over_ranks(elapsed, dist=None):
+    """The timed region's MAX over ranks (barrier after, so no rank races ahead)."""
+    if dist is None:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    return float(t.item())
+
+
+def aggregate_fps(world, steps, elapsed):
+    """Whole-job frames/s: every rank decodes `steps` frames of its own stream."""
+    return world * steps / elapsed
+
+
 def cpu_baseline(frames, budget_s):
     """The C oracle (reference algorithm restated, single-threaded) on the first frames."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -106,7 +127,7 @@ def main():
 
     native.lib()
     W, H, tiles, seed = CONFIGS[args.config]
-    frames = pysynth.stream(W, H, args.frames, seed + rank, sb128=True, tiles=tiles)
+    frames = pysynth.stream(W, H, args.frames, stream_seed(seed, rank), sb128=True, tiles=tiles)
 
     dec = Decoder(local, keep_stages=False, timing=False)
     dec.set_discard_output(True)
@@ -122,14 +143,8 @@ def main():
     for i in order[args.warmup:]:
         dec.decode_prepared(handles[i])
     dec.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-    fps = world * args.steps / elapsed
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+    fps = aggregate_fps(world, args.steps, elapsed)
 
     # per-stage device time over the same frames (HIP events on the decoder's stream)
     dec.l.av1r_set_timing(dec.c, 1)
