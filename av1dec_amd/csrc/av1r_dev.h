@@ -20,7 +20,9 @@ struct DevFrame {
     int width, height;  // FrameWidth / FrameHeight of the frame stored here
 };
 
-// Kernel arguments for every stage (passed by value).
+// Everything the stage kernels read about one frame.  A launch covers n frames (one per
+// stream of a batch): the kernels receive a device array of n KParams and pick theirs
+// by blockIdx (see k_level / k_lf / k_cdef / k_lr).
 struct KParams {
     const av1r_frame_hdr* hdr;
     const av1r_mi* mi;
@@ -30,13 +32,14 @@ struct KParams {
     const uint8_t* palette;
     const int8_t* cdef_idx;
     const av1r_lr_unit* lr;
-    const uint32_t* items;  // work list of this launch
+    const uint32_t* items;  // this frame's level-ordered work items
     uint32_t n_items;
     int mi_stride;
     int mi_cols, mi_rows;
     int frame_w, frame_h;
-    DevFrame cur;     // frame under reconstruction / filter input
-    DevFrame out;     // filter output
+    DevFrame cur;     // frame under reconstruction, deblocked in place
+    DevFrame cdef;    // CDEF output (Cdef::filter's copy, Cdef.cpp:43)
+    DevFrame lrout;   // loop-restoration output (LoopRestoration.cpp:216)
     DevFrame ref[8];  // reference store slots
 };
 

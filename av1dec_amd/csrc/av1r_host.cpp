@@ -25,10 +25,10 @@
 
 #include "av1r_dev.h"
 
-void launch_k_level(const KParams& k, unsigned n, hipStream_t s);
-void launch_k_lf(const KParams& k, int pass, int nY, int nC, int cCols, int planeMask, hipStream_t s);
-void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s);
-void launch_k_lr(const KParams& k, hipStream_t s);
+void launch_k_level(const KParams* kps, const uint32_t* tab, int n, unsigned items, hipStream_t s);
+void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
+void launch_k_cdef(const KParams* kps, int n, int maxBlocks, hipStream_t s);
+void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 
 namespace {
@@ -79,6 +79,9 @@ struct av1r_ctx {
     bool keepStages = true;
     Upload up[2];
     int upIdx = 0;
+    Upload meta[2];  // per-launch KParams + level tables
+    int metaIdx = 0;
+    hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
     std::string err;
     // schedule scratch
     std::vector<int16_t> lvlmap[3];
@@ -100,6 +103,7 @@ struct av1r_ctx {
     bool timing = false;
     hipEvent_t ev[5] = {};
     std::vector<std::array<hipEvent_t, 5>> evPool;
+    std::vector<int> evFrames;  // frames covered by each event set (batched launches)
     size_t evUsed = 0;
     int nLevelsLast = 0;
     // stats of the last frame
@@ -444,9 +448,23 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     return AV1R_OK;
 }
 
-// recon -> LF -> CDEF -> LR on the context stream, then output / frame-store update.
-static int launch_frame(av1r_ctx* c, const Prepared& P)
+// ------------------------------------------------------------------------------------
+// Launching: a batch of n frames (one per context/stream, n = 1 for the plain API) goes
+// through recon -> LF -> CDEF -> LR in shared launches on one HIP stream: every level of
+// every frame in one k_level launch, every frame's filters in one launch per filter.
+// ------------------------------------------------------------------------------------
+struct FrameJob {
+    av1r_ctx* c = nullptr;
+    const Prepared* P = nullptr;
+    KParams k;
+    FrameBuf *R = nullptr, *C = nullptr, *L = nullptr;
+};
+
+// resolve references, allocate the frame's buffers, fill its KParams
+static int job_begin(FrameJob& j)
 {
+    av1r_ctx* c = j.c;
+    const Prepared& P = *j.P;
     const av1r_frame_hdr* h = &P.hdr;
     for (int r = 1; r < 8; r++) {
         if (!P.usedRef[r]) continue;
@@ -454,91 +472,33 @@ static int launch_frame(av1r_ctx* c, const Prepared& P)
         if (slot < 0 || slot > 7 || !c->slots[slot])
             return fail(c, AV1R_E_INVALID, "reference %d maps to an empty slot", r);
     }
-    KParams k = P.base;
+    j.k = P.base;
+    j.k.items = P.dItems;
     for (int s = 0; s < 8; s++)
-        if (c->slots[s]) k.ref[s] = c->slots[s]->d;
-    int rc;
-    FrameBuf* R = frame_get(c, h->frame_width, h->frame_height);
-    if (!R) return fail(c, AV1R_E_NOMEM, "frame allocation");
-    k.cur = R->d;
-    if (c->timing) {
-        if (c->evUsed == c->evPool.size()) {
-            std::array<hipEvent_t, 5> e;
-            for (auto& x : e) HIPCHK(hipEventCreate(&x));
-            c->evPool.push_back(e);
-        }
-        for (int i = 0; i < 5; i++) c->ev[i] = c->evPool[c->evUsed][i];
-        c->evUsed++;
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    }
+        if (c->slots[s]) j.k.ref[s] = c->slots[s]->d;
+    j.R = frame_get(c, h->frame_width, h->frame_height);
+    j.C = frame_get(c, h->frame_width, h->frame_height);
+    j.L = h->uses_lr ? frame_get(c, h->frame_width, h->frame_height) : nullptr;
+    if (!j.R || !j.C || (h->uses_lr && !j.L)) return fail(c, AV1R_E_NOMEM, "frame allocation");
+    j.k.cur = j.R->d;
+    j.k.cdef = j.C->d;
+    if (j.L) j.k.lrout = j.L->d;
+    return AV1R_OK;
+}
 
-    // ---- reconstruction, level by level
-    for (const Level& L : P.levels) {
-        if (!L.cnt) continue;
-        k.items = P.dItems + L.off;
-        k.n_items = L.cnt;
-        launch_k_level(k, L.cnt, c->stream);
-    }
-    HIPCHK(hipGetLastError());
-    auto snapshot = [&](int st, FrameBuf* src) -> int {
-        FrameBuf* s = frame_get(c, h->frame_width, h->frame_height);
-        if (!s) return fail(c, AV1R_E_NOMEM, "stage allocation");
-        for (int p = 0; p < 3; p++) launch_k_copy_plane(s->d.pl[p], src->d.pl[p], c->stream);
-        frame_unref(c, c->stage[st]);
-        c->stage[st] = s;
-        return AV1R_OK;
-    };
-    if (c->keepStages && (rc = snapshot(AV1R_STAGE_RECON, R))) return rc;
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
-
-    // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place
-    if (h->lf_level[0] || h->lf_level[1]) {
-        int planeMask = 1 | (h->lf_level[2] ? 2 : 0) | (h->lf_level[3] ? 4 : 0);
-        int nY = h->mi_rows * h->mi_cols;
-        int cCols = (h->mi_cols + 1) / 2, nC = ((h->mi_rows + 1) / 2) * cCols;
-        launch_k_lf(k, 0, nY, nC, cCols, planeMask, c->stream);
-        launch_k_lf(k, 1, nY, nC, cCols, planeMask, c->stream);
-    }
-    if (c->keepStages && (rc = snapshot(AV1R_STAGE_LF, R))) return rc;
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
-
-    // ---- CDEF into a new frame (Cdef::filter copies the frame, Cdef.cpp:43)
-    FrameBuf* C = frame_get(c, h->frame_width, h->frame_height);
-    if (!C) return fail(c, AV1R_E_NOMEM, "frame allocation");
-    {
-        KParams kc = k;
-        kc.out = C->d;
-        int bCols = h->mi_cols / 2, nB = (h->mi_rows / 2) * bCols;
-        launch_k_cdef(kc, nB, bCols, c->stream);
-    }
-    if (c->keepStages) {
-        frame_ref(C);
-        frame_unref(c, c->stage[AV1R_STAGE_CDEF]);
-        c->stage[AV1R_STAGE_CDEF] = C;
-    }
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[3], c->stream));
-
-    // ---- loop restoration into a new frame (LoopRestoration::filter, LoopRestoration.cpp:191-219)
-    FrameBuf* out = C;
-    if (h->uses_lr) {
-        FrameBuf* L = frame_get(c, h->frame_width, h->frame_height);
-        if (!L) return fail(c, AV1R_E_NOMEM, "frame allocation");
-        KParams kl = k;
-        kl.cur = C->d;
-        kl.ref[0] = R->d;
-        kl.out = L->d;
-        launch_k_lr(kl, c->stream);
-        out = L;
-        frame_unref(c, C);
-    }
+// output queue / frame-store refresh (Av1Decoder.cpp:150-153, 111-119)
+static void job_end(FrameJob& j)
+{
+    av1r_ctx* c = j.c;
+    const av1r_frame_hdr* h = &j.P->hdr;
+    FrameBuf* out = j.L ? j.L : j.C;
+    if (j.L) frame_unref(c, j.C);
+    frame_unref(c, j.R);
     if (c->keepStages) {
         frame_ref(out);
         frame_unref(c, c->stage[AV1R_STAGE_LR]);
         c->stage[AV1R_STAGE_LR] = out;
     }
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    HIPCHK(hipGetLastError());
-    frame_unref(c, R);
     if (h->show_frame && !c->discardOutput) {
         frame_ref(out);
         c->outq.push_back(out);
@@ -550,9 +510,126 @@ static int launch_frame(av1r_ctx* c, const Prepared& P)
             c->slots[i] = out;
         }
     frame_unref(c, out);
-    c->nLevelsLast = (int)P.levels.size();
-    c->lastUploadBytes = P.bytes;
+    c->nLevelsLast = (int)j.P->levels.size();
+    c->lastUploadBytes = j.P->bytes;
+}
+
+static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
+{
+    av1r_ctx* c = lc;  // errors are reported on the launching context
+    const int n = (int)jobs.size();
+    hipStream_t st = lc->stream;
+    int rc;
+    size_t nLevels = 0;
+    int maxUnits = 0, maxBlocks = 0, maxW = 0, maxH = 0;
+    bool anyLr = false;
+    for (auto& j : jobs) {
+        const av1r_frame_hdr* h = &j.P->hdr;
+        nLevels = std::max(nLevels, j.P->levels.size());
+        maxUnits = std::max(maxUnits, h->mi_rows * h->mi_cols + 2 * ((h->mi_rows + 1) / 2) * ((h->mi_cols + 1) / 2));
+        maxBlocks = std::max(maxBlocks, (h->mi_rows / 2) * (h->mi_cols / 2));
+        maxW = std::max(maxW, h->frame_width);
+        maxH = std::max(maxH, h->frame_height);
+        anyLr |= h->uses_lr != 0;
+    }
+    // launch metadata: [KParams x n][per level: n + 1 prefix counts, n item offsets]
+    const size_t tabW = 2 * (size_t)n + 1;
+    const size_t kBytes = align256(sizeof(KParams) * n);
+    const size_t need = kBytes + 4 * tabW * std::max<size_t>(nLevels, 1);
+    Upload& M = lc->meta[lc->metaIdx];
+    lc->metaIdx = (lc->metaIdx + 1) % 2;
+    if (M.pending) {
+        HIPCHK(hipEventSynchronize(M.done));
+        M.pending = false;
+    }
+    if (M.cap < need) {
+        if (M.host) (void)hipHostFree(M.host);
+        if (M.dev) (void)hipFree(M.dev);
+        size_t cap = need + need / 2 + 4096;
+        HIPCHK(hipHostMalloc(&M.host, cap));
+        HIPCHK(hipMalloc(&M.dev, cap));
+        M.cap = cap;
+    }
+    KParams* hk = reinterpret_cast<KParams*>(M.host);
+    for (int i = 0; i < n; i++) hk[i] = jobs[i].k;
+    uint32_t* tab = reinterpret_cast<uint32_t*>(M.host + kBytes);
+    std::vector<uint32_t> total(nLevels, 0);
+    for (size_t l = 0; l < nLevels; l++) {
+        uint32_t* t = tab + l * tabW;
+        t[0] = 0;
+        for (int i = 0; i < n; i++) {
+            const auto& lv = jobs[i].P->levels;
+            const uint32_t cnt = l < lv.size() ? lv[l].cnt : 0;
+            t[i + 1] = t[i] + cnt;
+            t[n + 1 + i] = l < lv.size() ? lv[l].off : 0;
+        }
+        total[l] = t[n];
+    }
+    HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
+    const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
+    const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
+
+    if (lc->timing) {
+        if (lc->evUsed == lc->evPool.size()) {
+            std::array<hipEvent_t, 5> e;
+            for (auto& x : e) HIPCHK(hipEventCreate(&x));
+            lc->evPool.push_back(e);
+            lc->evFrames.push_back(0);
+        }
+        for (int i = 0; i < 5; i++) lc->ev[i] = lc->evPool[lc->evUsed][i];
+        lc->evFrames[lc->evUsed] = n;
+        lc->evUsed++;
+        HIPCHK(hipEventRecord(lc->ev[0], st));
+    }
+    // the single-frame path keeps per-stage snapshots for av1r_read_stage
+    const bool snap = n == 1 && lc->keepStages;
+    auto snapshot = [&](int stg, FrameBuf* src) -> int {
+        const av1r_frame_hdr* h = &jobs[0].P->hdr;
+        FrameBuf* s = frame_get(lc, h->frame_width, h->frame_height);
+        if (!s) return fail(c, AV1R_E_NOMEM, "stage allocation");
+        for (int p = 0; p < 3; p++) launch_k_copy_plane(s->d.pl[p], src->d.pl[p], st);
+        frame_unref(lc, lc->stage[stg]);
+        lc->stage[stg] = s;
+        return AV1R_OK;
+    };
+
+    // ---- reconstruction, level by level
+    for (size_t l = 0; l < nLevels; l++)
+        if (total[l]) launch_k_level(dk, dtab + l * tabW, n, total[l], st);
+    HIPCHK(hipGetLastError());
+    if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
+    // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place, 2 passes
+    launch_k_lf(dk, n, 0, maxUnits, st);
+    launch_k_lf(dk, n, 1, maxUnits, st);
+    if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
+    // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
+    launch_k_cdef(dk, n, maxBlocks, st);
+    if (snap) {
+        frame_ref(jobs[0].C);
+        frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
+        lc->stage[AV1R_STAGE_CDEF] = jobs[0].C;
+    }
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
+    // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
+    if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(M.done, st));
+    M.pending = true;
+    for (auto& j : jobs) job_end(j);
     return AV1R_OK;
+}
+
+static int launch_frame(av1r_ctx* c, const Prepared& P)
+{
+    std::vector<FrameJob> jobs(1);
+    jobs[0].c = c;
+    jobs[0].P = &P;
+    int rc = job_begin(jobs[0]);
+    if (rc) return rc;
+    return launch_jobs(c, jobs);
 }
 
 // streaming path: one pinned staging buffer -> one async H2D copy (ring of 2)
@@ -607,6 +684,8 @@ int av1r_create(int device, av1r_ctx** out)
         return AV1R_E_DEVICE;
     }
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
+    for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->meta[i].done, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
     for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     *out = c;
@@ -622,11 +701,14 @@ void av1r_destroy(av1r_ctx* c)
         (void)hipFree(f->base);
         delete f;
     }
-    for (auto& u : c->up) {
-        if (u.host) (void)hipHostFree(u.host);
-        if (u.dev) (void)hipFree(u.dev);
-        (void)hipEventDestroy(u.done);
-    }
+    for (auto* ring : {c->up, c->meta})
+        for (int i = 0; i < 2; i++) {
+            Upload& u = ring[i];
+            if (u.host) (void)hipHostFree(u.host);
+            if (u.dev) (void)hipFree(u.dev);
+            (void)hipEventDestroy(u.done);
+        }
+    (void)hipEventDestroy(c->sync);
     for (auto& e : c->evPool)
         for (auto& x : e) (void)hipEventDestroy(x);
     for (Prepared* P : c->prepared)
@@ -753,6 +835,52 @@ int av1r_decode_prepared(av1r_ctx* c, int handle)
     return launch_frame(c, P);
 }
 
+int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n)
+{
+    if (!ctxs || !handles || n <= 0) return AV1R_E_INVALID;
+    av1r_ctx* lc = ctxs[0];
+    if (!lc) return AV1R_E_INVALID;
+    for (int i = 0; i < n; i++) {
+        av1r_ctx* c = ctxs[i];
+        if (!c || c->device != lc->device) return fail(lc, AV1R_E_INVALID, "batch contexts must share one device");
+        for (int j = 0; j < i; j++)
+            if (ctxs[j] == c) return fail(lc, AV1R_E_INVALID, "a context appears twice in one batch");
+        if (handles[i] < 0 || handles[i] >= (int)c->prepared.size() || !c->prepared[handles[i]])
+            return fail(lc, AV1R_E_INVALID, "bad prepared handle %d", handles[i]);
+    }
+    (void)hipSetDevice(lc->device);
+    std::vector<FrameJob> jobs;
+    jobs.reserve(n);
+    for (int i = 0; i < n; i++) {
+        const Prepared& P = *ctxs[i]->prepared[handles[i]];
+        if (P.hdr.show_existing_frame) {
+            int rc = av1r_show_existing(ctxs[i], P.hdr.frame_to_show, P.hdr.refresh_frame_flags);
+            if (rc) return rc;
+            continue;
+        }
+        FrameJob j;
+        j.c = ctxs[i];
+        j.P = &P;
+        int rc = job_begin(j);
+        if (rc) return rc;
+        jobs.push_back(j);
+    }
+    if (jobs.empty()) return AV1R_OK;
+    av1r_ctx* c = lc;
+    // the launch stream waits for every member's earlier work, and they for the batch
+    for (auto& j : jobs)
+        if (j.c != lc) {
+            HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
+            HIPCHK(hipStreamWaitEvent(lc->stream, j.c->sync, 0));
+        }
+    int rc = launch_jobs(lc, jobs);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(lc->sync, lc->stream));
+    for (auto& j : jobs)
+        if (j.c != lc) HIPCHK(hipStreamWaitEvent(j.c->stream, lc->sync, 0));
+    return AV1R_OK;
+}
+
 int av1r_release_prepared(av1r_ctx* c, int handle)
 {
     if (!c || handle < 0 || handle >= (int)c->prepared.size() || !c->prepared[handle]) return AV1R_E_INVALID;
@@ -869,7 +997,11 @@ int av1r_stage_times(av1r_ctx* c, float* totals, int* frames)
             HIPCHK(hipEventElapsedTime(&t, c->evPool[f][i], c->evPool[f][i + 1]));
             totals[i] += t;
         }
-    if (frames) *frames = (int)c->evUsed;
+    if (frames) {
+        int nf = 0;
+        for (size_t f = 0; f < c->evUsed; f++) nf += c->evFrames[f];
+        *frames = nf;
+    }
     c->evUsed = 0;
     return AV1R_OK;
 }

@@ -112,8 +112,14 @@ DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int bl
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
-extern "C" __global__ __launch_bounds__(256) void k_lf(KParams k, int pass, int nY, int nC, int cCols, int planeMask)
+extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* __restrict__ kps, int pass)
 {
+    const KParams& k = kps[blockIdx.y];  // frame of this launch row
+    const av1r_frame_hdr& hd = *k.hdr;
+    if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
+    const int planeMask = 1 | (hd.lf_level[2] ? 2 : 0) | (hd.lf_level[3] ? 4 : 0);
+    const int nY = k.mi_rows * k.mi_cols;
+    const int cCols = (k.mi_cols + 1) / 2, nC = ((k.mi_rows + 1) / 2) * cCols;
     int id = blockIdx.x * blockDim.x + threadIdx.x;
     int plane, row0, col0;
     if (id < nY) {
@@ -200,12 +206,14 @@ DEV void cdef_plane(const KParams& k, int plane, int r, int c, int priStr, int s
                 mx = imax(p, mx);
                 mn = imin(p, mn);
             }
-    px(k.out.pl[plane], X, Y) = (uint8_t)CLIP3(mn, mx, x + ((8 + sum - (sum < 0)) >> 4));
+    px(k.cdef.pl[plane], X, Y) = (uint8_t)CLIP3(mn, mx, x + ((8 + sum - (sum < 0)) >> 4));
 }
 
 // one wave per 8x8 luma block (lane = luma pixel; lanes 0..31 also do the 4x4 U/V)
-extern "C" __global__ __launch_bounds__(256) void k_cdef(KParams k, int nBlocks, int bCols)
+extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* __restrict__ kps)
 {
+    const KParams& k = kps[blockIdx.y];
+    const int bCols = k.mi_cols / 2, nBlocks = (k.mi_rows / 2) * bCols;
     __shared__ int partial[4][8][16];
     __shared__ int cost[4][8];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -222,10 +230,10 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(KParams k, int nBlocks,
     const bool filt = active && idx != -1 && !skip;
     // the reference filters into a copy of the frame (Cdef.cpp:43): unfiltered blocks copy
     if (active && !filt) {
-        px(k.out.pl[0], c * 4 + j, r * 4 + i) = px(k.cur.pl[0], c * 4 + j, r * 4 + i);
+        px(k.cdef.pl[0], c * 4 + j, r * 4 + i) = px(k.cur.pl[0], c * 4 + j, r * 4 + i);
         if (lane < 32) {
             int pl = 1 + (lane >> 4), q = lane & 15;
-            px(k.out.pl[pl], c * 2 + (q & 3), r * 2 + (q >> 2)) = px(k.cur.pl[pl], c * 2 + (q & 3), r * 2 + (q >> 2));
+            px(k.cdef.pl[pl], c * 2 + (q & 3), r * 2 + (q >> 2)) = px(k.cur.pl[pl], c * 2 + (q & 3), r * 2 + (q >> 2));
         }
     }
     for (int q = lane; q < 8 * 16; q += 64) partial[wv][q >> 4][q & 15] = 0;
@@ -289,7 +297,7 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(KParams k, int nBlocks,
 // ------------------------------------------------------------------------------------
 struct LrPix {
     DevPlane cdefP;  // CDEF output (k.cur)
-    DevPlane preP;   // deblocked, pre-CDEF frame (k.ref[0] slot reused by the host)
+    DevPlane preP;   // deblocked, pre-CDEF frame (k.cur)
     int start, end;  // stripe
 };
 // get_source_sample (LoopRestoration.cpp:234-246) + extendBorder(3) as clamping
@@ -348,15 +356,17 @@ DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, in
     B = r2(b2, 12);
 }
 
-// one 256-lane workgroup per tile; blockIdx.z = plane.  k.cur = CDEF frame, k.ref[0] =
-// deblocked frame, k.out = restored frame.
-extern "C" __global__ __launch_bounds__(256) void k_lr(KParams k)
+// one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
+// frame (k.cdef) and the deblocked frame (k.cur, stripe rows), writes k.lrout.
+extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* __restrict__ kps)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-    const int plane = blockIdx.z, sub = plane ? 1 : 0;
-    const DevPlane C = k.cur.pl[plane];
-    const DevPlane O = k.out.pl[plane];
+    const KParams& k = kps[blockIdx.z / 3];
+    if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
+    const int plane = blockIdx.z % 3, sub = plane ? 1 : 0;
+    const DevPlane C = k.cdef.pl[plane];
+    const DevPlane O = k.lrout.pl[plane];
     const int x0 = blockIdx.x * LR_TW;
     if (x0 >= C.w) return;
     const int stripeH = 64 >> sub, off = 8 >> sub;
@@ -364,7 +374,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(KParams k)
     const int sNum = blockIdx.y / perStripe, half = blockIdx.y - sNum * perStripe;
     LrPix S;
     S.cdefP = C;
-    S.preP = k.ref[0].pl[plane];
+    S.preP = k.cur.pl[plane];
     S.start = sNum * stripeH - off;
     S.end = S.start + stripeH;
     const int ty0 = imax(0, S.start + half * LR_TH), ty1 = imin(S.start + (half + 1) * LR_TH, C.h);
@@ -492,21 +502,20 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 }
 
 // ------------------------------------------------------------------------------------
-void launch_k_lf(const KParams& k, int pass, int nY, int nC, int cCols, int planeMask, hipStream_t s)
+// launches over n frames: grid row / slice per frame, sized for the largest
+void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
-    int n = nY + 2 * nC;
-    hipLaunchKernelGGL(k_lf, dim3((n + 255) / 256), dim3(256), 0, s, k, pass, nY, nC, cCols, planeMask);
+    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
 }
-void launch_k_cdef(const KParams& k, int nBlocks, int bCols, hipStream_t s)
+void launch_k_cdef(const KParams* kps, int n, int maxBlocks, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((nBlocks + 3) / 4), dim3(256), 0, s, k, nBlocks, bCols);
+    hipLaunchKernelGGL(k_cdef, dim3((maxBlocks + 3) / 4, n), dim3(256), 0, s, kps);
 }
-void launch_k_lr(const KParams& k, hipStream_t s)
+void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {
     // tile rows: luma stripes (64 rows from -8) in halves; chroma stripes whole
-    const DevPlane& p = k.cur.pl[0];
-    const int tilesY = 2 * ((p.h + 8 + 63) / 64);
-    hipLaunchKernelGGL(k_lr, dim3((p.w + LR_TW - 1) / LR_TW, tilesY, 3), dim3(256), 0, s, k);
+    const int tilesY = 2 * ((maxH + 8 + 63) / 64);
+    hipLaunchKernelGGL(k_lr, dim3((maxW + LR_TW - 1) / LR_TW, tilesY, 3 * n), dim3(256), 0, s, kps);
 }
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s)
 {

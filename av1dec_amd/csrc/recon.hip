@@ -827,18 +827,24 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
 // One launch per dependency level: every work item of the level (inter tiles, inter-
 // intra blends, transform blocks) is one 64-lane workgroup.
 // ---------------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(64) void k_level(KParams k)
+// Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
+// counts at this level; tab[n + 1 + s]: offset of frame s's level in its item list).
+extern "C" __global__ __launch_bounds__(64) void k_level(const KParams* __restrict__ kps, const uint32_t* __restrict__ tab, int n)
 {
     constexpr size_t kLds = sizeof(TbLds) > sizeof(InterLds) ? sizeof(TbLds) : sizeof(InterLds);
     __shared__ __align__(16) uint8_t smem[kLds];
-    const uint32_t it = k.items[blockIdx.x];
+    const uint32_t b = blockIdx.x;
+    int s = 0;
+    while (s + 1 < n && b >= tab[s + 1]) s++;
+    const KParams& k = kps[s];
+    const uint32_t it = k.items[tab[n + 1 + s] + (b - tab[s])];
     const uint32_t kind = AV1R_ITEM_KIND(it), idx = AV1R_ITEM_INDEX(it);
     if (kind == AV1R_ITEM_TB) tb_item(k, idx, *reinterpret_cast<TbLds*>(smem));
     else if (kind == AV1R_ITEM_INTER) inter_tile(k, idx >> 4, idx & 3, (idx >> 2) & 3, *reinterpret_cast<InterLds*>(smem));
     else ii_item(k, idx, *reinterpret_cast<TbLds*>(smem));
 }
 
-void launch_k_level(const KParams& k, unsigned n, hipStream_t s)
+void launch_k_level(const KParams* kps, const uint32_t* tab, int n, unsigned items, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_level, dim3(n), dim3(64), 0, s, k);
+    hipLaunchKernelGGL(k_level, dim3(items), dim3(64), 0, s, kps, tab, n);
 }

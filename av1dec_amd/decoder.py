@@ -62,6 +62,17 @@ class Decoder:
     def decode_prepared(self, handle):
         self._check(self.l.av1r_decode_prepared(self.c, handle), "av1r_decode_prepared")
 
+    @staticmethod
+    def decode_prepared_batch(decoders, handles):
+        """One frame per decoder (independent streams, one device) in shared launches
+        (av1r_decode_prepared_batch); launched on decoders[0]'s stream."""
+        n = len(decoders)
+        if n == 0 or n != len(handles):
+            raise ValueError("need one handle per decoder")
+        ctxs = (C.c_void_p * n)(*[d.c.value for d in decoders])
+        hs = (C.c_int * n)(*handles)
+        decoders[0]._check(decoders[0].l.av1r_decode_prepared_batch(ctxs, hs, n), "av1r_decode_prepared_batch")
+
     def release_prepared(self, handle):
         self._check(self.l.av1r_release_prepared(self.c, handle), "av1r_release_prepared")
 

@@ -1,21 +1,23 @@
 #!/usr/bin/env python3
 """bench.py -- frames/s of the MI355X AV1 reconstruction + in-loop filter backend.
 
-Workload (BASELINE.json configs[2]): a synthetic 1920x1080 8-bit 4:2:0 stream of frame
-batches (tools/synth: 1 key frame + 59 inter frames, seed 0x5EED0001 + rank, 8-tap subpel,
-compound avg/dist/wedge/diff-weighted, inter-intra, OBMC, local warp, LF + CDEF + LR),
-cycled.  One "step" = one frame through recon -> deblock -> CDEF -> loop restoration on
-one GPU with its batch already resident in HBM (av1r_prepare); the host-inclusive rate
-(validation + scheduling + PCIe upload per frame) is reported beside it.
+Workload (BASELINE.json configs[2] streams, batched as configs[4]): S = 8 independent
+synthetic 1920x1080 8-bit 4:2:0 streams per GPU -- the per-GPU share of the 64-stream
+batch over 8 GPUs -- each 1 key + 59 inter frames (tools/synth: 8-tap subpel, compound
+avg/dist/wedge/diff-weighted, inter-intra, OBMC, local warp, LF + CDEF + LR), cycled.
+One step = one frame of every stream through recon -> deblock -> CDEF -> loop restoration
+in shared launches (av1r_decode_prepared_batch) with all batches already resident in HBM
+(av1r_prepare).  Reported beside it: one stream alone (single_stream_fps) and the
+host-inclusive rate (validation + scheduling + PCIe upload per frame).
 
 Multi-GPU (--gpus N, launched by torch.distributed.run): every rank decodes its own
-independent stream on its own GPU -- streams shard one per GPU with no data-path
-collective; a gloo barrier brackets the timed region and the MAX elapsed
-over ranks is used.  value = N * steps / max_elapsed ("weak" scaling).
+streams on its own GPU -- streams shard over GPUs with no data-path collective (SURVEY.md
+8e); a gloo barrier brackets the timed region and the MAX elapsed over ranks is used.
+value = N * S * steps / max_elapsed ("weak" scaling).
 
 Also reported: roofline of the dominant stage (algorithmic bytes / device time, vs the
 8 TB/s HBM3E peak) and the CPU baseline (the C oracle -- a restatement of the
-reference's algorithm -- on a bounded sample of the same stream, 1 core).
+reference's algorithm -- on a bounded sample of stream 0, 1 core).
 """
 import argparse
 import json
@@ -33,8 +35,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 
 CONFIGS = {
     # name: (width, height, tiles, seed)
-    "1080p": (1920, 1080, (1, 1), 0x5EED0001),
-    "4k": (3840, 2160, (4, 2), 0x5EED0002),
+    "1080p": (1920, 1080, (1, 1), 0x5EED1000),
+    "4k": (3840, 2160, (4, 2), 0x5EED2000),
 }
 
 
@@ -104,14 +106,16 @@ def cpu_baseline(frames, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--steps", type=int, default=60, help="timed batch steps (one frame of every stream each)")
     ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
+    ap.add_argument("--streams", type=int, default=8,
+                    help="independent streams per GPU, decoded in shared launches (configs[4]: 64 streams / 8 GPUs)")
     ap.add_argument("--frames", type=int, default=60, help="stream length (1 key + inter)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
+                    help="PMC-derived HBM bytes per frame (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -127,67 +131,87 @@ def main():
 
     native.lib()
     W, H, tiles, seed = CONFIGS[args.config]
-    frames = pysynth.stream(W, H, args.frames, stream_seed(seed, rank), sb128=True, tiles=tiles)
+    S = max(1, args.streams)
+    # stream i of the job = rank * S + j (independent streams, one GPU each)
+    streams = [pysynth.stream(W, H, args.frames, stream_seed(seed, rank * S + j), sb128=True, tiles=tiles)
+               for j in range(S)]
+    decs = [Decoder(local, keep_stages=False, timing=False) for _ in range(S)]
+    for d in decs:
+        d.set_discard_output(True)
+    handles = [[d.prepare(f) for f in fr] for d, fr in zip(decs, streams)]
+    F = args.frames
 
-    dec = Decoder(local, keep_stages=False, timing=False)
-    dec.set_discard_output(True)
-    handles = [dec.prepare(f) for f in frames]
-    order = [i % len(frames) for i in range(args.warmup + args.steps)]
+    def step(t):
+        Decoder.decode_prepared_batch(decs, [hs[t % F] for hs in handles])
 
-    for i in order[:args.warmup]:
-        dec.decode_prepared(handles[i])
-    dec.synchronize()
+    def sync():
+        for d in decs:
+            d.synchronize()
+
+    for t in range(args.warmup):
+        step(t)
+    sync()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    for i in order[args.warmup:]:
-        dec.decode_prepared(handles[i])
-    dec.synchronize()
+    for t in range(args.warmup, args.warmup + args.steps):
+        step(t)
+    sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
-    fps = aggregate_fps(world, args.steps, elapsed)
+    fps = aggregate_fps(world, args.steps * S, elapsed)
 
-    # per-stage device time over the same frames (HIP events on the decoder's stream)
-    dec.l.av1r_set_timing(dec.c, 1)
-    for i in order[args.warmup:]:
-        dec.decode_prepared(handles[i])
-    totals, nfr = dec.stage_times()
-    dec.l.av1r_set_timing(dec.c, 0)
+    # per-stage device time over the same batches (HIP events on the launch stream)
+    lead = decs[0]
+    lead.l.av1r_set_timing(lead.c, 1)
+    for t in range(args.warmup, args.warmup + args.steps):
+        step(t)
+    totals, nfr = lead.stage_times()
+    lead.l.av1r_set_timing(lead.c, 0)
     names = ["recon", "lf", "cdef", "lr"]
     per_frame_ms = {n: totals[k] / max(nfr, 1) for k, n in enumerate(names)}
     sb = {n: 0.0 for n in names}
-    for i in order[args.warmup:]:
-        for n, v in stage_bytes(frames[i]).items():
-            sb[n] += v / args.steps
+    for t in range(args.warmup, args.warmup + args.steps):
+        for fr in streams:
+            for n, v in stage_bytes(fr[t % F]).items():
+                sb[n] += v / (args.steps * S)
     dominant = max(names, key=lambda n: per_frame_ms[n])
     achieved = sb[dominant] / (per_frame_ms[dominant] * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("config") == args.config and dominant in tj.get("stages", {}):
+            if tj.get("config") == args.config and tj.get("streams", 1) == S and dominant in tj.get("stages", {}):
                 traffic = tj["stages"][dominant]
         except Exception:
             traffic = None
 
+    # one stream alone (latency-bound) on the same frames
+    sync()
+    t1 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        lead.decode_prepared(handles[0][t % F])
+    lead.synchronize()
+    single_fps = args.steps / (time.perf_counter() - t1)
+
     # host-inclusive rate: batches from host memory (validate + schedule + H2D per frame)
-    n_host = min(len(frames), 24)
-    dec.synchronize()
+    n_host = min(F, 24)
     t1 = time.perf_counter()
     for i in range(n_host):
-        dec.decode_frame(frames[i])
-    dec.synchronize()
+        lead.decode_frame(streams[0][i])
+    lead.synchronize()
     host_fps = n_host / (time.perf_counter() - t1)
-    levels, _ = dec.last_frame_stats()
+    levels, _ = lead.last_frame_stats()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cfps, cn, cdt = cpu_baseline(frames, args.cpu_budget)
+        cfps, cn, cdt = cpu_baseline(streams[0], args.cpu_budget)
         cpu = {"value": round(cfps, 4), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"frames 0..{cn - 1} of the same synthetic {args.config} stream "
+               "sample": f"frames 0..{cn - 1} of synthetic {args.config} stream 0 "
                          f"({cn} frames, {cdt:.1f} s): oracle/av1r_oracle.c, -O2, 1 thread"}
-    for hd in handles:
-        dec.release_prepared(hd)
-    dec.close()
+    for d, hs in zip(decs, handles):
+        for hd in hs:
+            d.release_prepared(hd)
+        d.close()
 
     if rank == 0:
         line = {
@@ -204,17 +228,20 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"synthetic {W}x{H} 8-bit 4:2:0 inter stream "
-                                   f"({args.frames} frames: 1 key + {args.frames - 1} inter, cycled; "
-                                   f"tiles {tiles[0]}x{tiles[1]}; seed {seed:#x}+rank)",
-                       "frames_per_rank": args.steps, "parallelism": f"stream-per-GPU x{world}"},
+            "config": {"workload": f"{S} independent synthetic {W}x{H} 8-bit 4:2:0 inter streams per GPU "
+                                   f"(BASELINE configs[4] share; each {F} frames: 1 key + {F - 1} inter, cycled; "
+                                   f"tiles {tiles[0]}x{tiles[1]}; seeds {seed:#x}+stream), one frame of every "
+                                   f"stream per step in shared launches",
+                       "streams_per_gpu": S, "frames_per_step": S,
+                       "parallelism": f"stream-per-GPU x{world}"},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic,
-                         "bytes_per_launch": int(sb[dominant]),
-                         "ms_per_launch": round(per_frame_ms[dominant], 4)},
+                         "bytes_per_frame": int(sb[dominant]),
+                         "ms_per_frame": round(per_frame_ms[dominant], 4)},
             "stage_ms_per_frame": {n: round(v, 4) for n, v in per_frame_ms.items()},
             "stage_algorithmic_GBps": {n: round(sb[n] / max(per_frame_ms[n], 1e-9) / 1e6, 2) for n in names},
+            "single_stream_fps": round(single_fps, 3),
             "host_inclusive_fps": round(host_fps, 3),
             "recon_levels_last_frame": levels,
             "cpu_baseline": cpu,

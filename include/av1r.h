@@ -217,6 +217,12 @@ int av1r_frame_end(av1r_ctx* ctx);
  * timed region), then decode it from HBM.  Handles stay valid until released. */
 int av1r_prepare(av1r_ctx* ctx, const av1r_frame_batch* batch, int* handle);
 int av1r_decode_prepared(av1r_ctx* ctx, int handle);
+/* Batched form over n independent streams: frame handles[i] of context
+ * ctxs[i] (all on one device, each context at most once) go through recon -> LF -> CDEF
+ * -> LR in shared launches on ctxs[0]'s stream -- every stream's dependency level in one
+ * k_level launch, every stream's frame in one launch per filter.  Same results as n
+ * av1r_decode_prepared calls. */
+int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n);
 int av1r_release_prepared(av1r_ctx* ctx, int handle);
 /* Do not queue shown frames for read-back (they still refresh the reference store). */
 int av1r_set_discard_output(av1r_ctx* ctx, int discard);

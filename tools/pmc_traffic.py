@@ -21,7 +21,7 @@ def fold(path, counter):
     if not files:
         raise SystemExit(f"no counter_collection csv under {path}")
     tot = defaultdict(float)
-    frames = 0
+    rows = []
     for f in files:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
@@ -32,7 +32,10 @@ def fold(path, counter):
                 continue
             tot[st] += float(r["Counter_Value"]) * (1024 if counter.endswith("_SIZE") else 1)
             if st == "cdef":
-                frames += 1
+                rows.append(int(r["Grid_Size"]))
+    # one k_cdef launch covers every frame of its batch: frames = grid / one frame's grid
+    one = min(rows) if rows else 1
+    frames = sum(round(g / one) for g in rows)
     return tot, frames
 
 
@@ -47,7 +50,8 @@ def main():
         w = write.get(st, 0.0) / max(nw, 1)
         stages[st] = {"fetch_bytes_raw": round(f), "fetch_bytes_x2": round(2 * f), "write_bytes": round(w),
                       "traffic_bytes": round(2 * f + w)}
-    res = {"config": "1080p", "frames_fetch": nf, "frames_write": nw,
+    res = {"config": "1080p", "streams": int(sys.argv[3]) if len(sys.argv) > 3 else 8,
+           "frames_fetch": nf, "frames_write": nw,
            "unit": "bytes per frame (per stage, all launches of the frame)",
            "stages": {k: v["traffic_bytes"] for k, v in stages.items()}, "detail": stages}
     json.dump(res, open(out, "w"), indent=1)
