@@ -27,7 +27,7 @@
 
 void launch_k_level(const KParams* kps, const uint32_t* tab, int n, unsigned items, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
-void launch_k_cdef(const KParams* kps, int n, int maxBlocks, hipStream_t s);
+void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 
@@ -521,13 +521,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     hipStream_t st = lc->stream;
     int rc;
     size_t nLevels = 0;
-    int maxUnits = 0, maxBlocks = 0, maxW = 0, maxH = 0;
+    int maxUnits = 0, maxMiCols = 0, maxMiRows = 0, maxW = 0, maxH = 0;
     bool anyLr = false;
     for (auto& j : jobs) {
         const av1r_frame_hdr* h = &j.P->hdr;
         nLevels = std::max(nLevels, j.P->levels.size());
         maxUnits = std::max(maxUnits, h->mi_rows * h->mi_cols + 2 * ((h->mi_rows + 1) / 2) * ((h->mi_cols + 1) / 2));
-        maxBlocks = std::max(maxBlocks, (h->mi_rows / 2) * (h->mi_cols / 2));
+        maxMiCols = std::max(maxMiCols, h->mi_cols);
+        maxMiRows = std::max(maxMiRows, h->mi_rows);
         maxW = std::max(maxW, h->frame_width);
         maxH = std::max(maxH, h->frame_height);
         anyLr |= h->uses_lr != 0;
@@ -605,7 +606,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
     // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
-    launch_k_cdef(dk, n, maxBlocks, st);
+    launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
     if (snap) {
         frame_ref(jobs[0].C);
         frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);

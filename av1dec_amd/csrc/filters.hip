@@ -5,9 +5,10 @@
 //           (decoder/LoopFilter.cpp:85-289).  Edges of one pass never overlap their
 //           read/write footprints (the filter length is bounded by the transform sizes
 //           on both sides), so a pass is embarrassingly parallel, in place.
-//   k_cdef  one wave per 8x8 luma block, lane = pixel: Cdef::cdef_block (Cdef.cpp:72-101),
-//           cdefDirection via LDS partial sums (:203-261), cdefFilter (:158-198) into a
-//           separate output frame (blocks that are skipped are copied).
+//   k_cdef  one workgroup per 64x64 filter region staged in LDS: Cdef::cdef_block
+//           (Cdef.cpp:72-101), cdefDirection (:203-261) one lane per (block, direction),
+//           cdefFilter (:158-198) one lane per pixel, into a separate output frame
+//           (blocks that are skipped are copied).
 //   k_lr    one workgroup per 64-column tile of a (half-)stripe, source staged in LDS:
 //           LoopRestoration Wiener (LoopRestoration.cpp:247-277) and self-guided
 //           (:284-479) with the stripe/unit geometry of :33-189; the 3-pixel border
@@ -181,13 +182,75 @@ DEV int constrain(int diff, int threshold, int damping)
     return diff < 0 ? -v : v;
 }
 
-DEV void cdef_plane(const KParams& k, int plane, int r, int c, int priStr, int secStr, int damping, int dir, int i, int j)
+// One workgroup per 64x64 luma region (one cdef_idx, Cdef.cpp:47-55) and its two 32x32
+// chroma regions.  The deblocked pixels with a 2-pixel halo are staged in LDS once; the
+// direction search runs one lane per (8x8 block, direction) pair summing each partial
+// line straight from LDS; the filter runs one lane per pixel from LDS.
+#define CD_H 2                     // tap reach (Cdef_Directions)
+#define CD_LW (64 + 2 * CD_H)      // luma tile edge
+#define CD_CW (32 + 2 * CD_H)      // chroma tile edge
+struct CdefLds {
+    uint8_t y[CD_LW][CD_LW + 4];
+    uint8_t uv[2][CD_CW][CD_CW + 4];
+    int cost[64][8];
+    uint8_t dir[64];               // yDir
+    int16_t pri[64];               // adjusted luma primary strength
+    uint8_t filt[64];              // block is filtered (not skip)
+};
+
+// partial[d][k] of cdefDirection (Cdef.cpp:203-261) for one line k of direction d, summed
+// over the 8x8 block at (bx, by) of the staged luma tile
+template <int d>
+DEV int cdef_cost(const CdefLds& L, int bx, int by)
 {
-    const int sub = plane ? 1 : 0;
-    const DevPlane& in = k.cur.pl[plane];
-    const int x0 = (c * 4) >> sub, y0 = (r * 4) >> sub;
-    const int X = x0 + j, Y = y0 + i;
-    const int x = px(in, X, Y);
+    auto px8 = [&](int i, int j) { return (int)L.y[CD_H + by + i][CD_H + bx + j] - 128; };
+    int cost = 0;
+    if (d == 2 || d == 6) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            int s = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) s += d == 2 ? px8(k, q) : px8(q, k);
+            cost += s * s;
+        }
+        return cost * av1r_cdef_div_table[8];
+    }
+    if (d == 0 || d == 4) {
+#pragma unroll
+        for (int k = 0; k < 15; k++) {
+            int s = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int j = d == 0 ? k - i : 7 + i - k;  // d0: k = i + j; d4: k = 7 + i - j
+                if (j >= 0 && j < 8) s += px8(i, j);
+            }
+            cost += s * s * av1r_cdef_div_table[k < 7 ? k + 1 : (k == 7 ? 8 : 15 - k)];
+        }
+        return cost;
+    }
+    // odd directions: 11 lines; the centre 5 weigh Div_Table[8], the outer pairs 2j+2
+#pragma unroll
+    for (int k = 0; k < 11; k++) {
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int kk = d == 1 ? i + j / 2 : d == 3 ? 3 + i - j / 2 : d == 5 ? 3 - i / 2 + j : i / 2 + j;
+                if (kk == k) s += px8(i, j);
+            }
+        const int w = (k >= 3 && k <= 7) ? av1r_cdef_div_table[8] : av1r_cdef_div_table[2 * (k < 3 ? k : 10 - k) + 2];
+        cost += s * s * w;
+    }
+    return cost;
+}
+
+// cdefFilter (Cdef.cpp:158-198) for one pixel (X, Y) of the plane, reading the staged tile
+// t (row stride ts, origin (ox, oy) = plane coordinate of t[0][0])
+DEV int cdef_px(const KParams& k, const uint8_t* t, int ts, int ox, int oy, int sub, int X, int Y, int priStr,
+    int secStr, int damping, int dir)
+{
+    const int x = t[(Y - oy) * ts + X - ox];
     int sum = 0, mx = x, mn = x;
 #pragma unroll
     for (int kk = 0; kk < 2; kk++)
@@ -198,97 +261,130 @@ DEV void cdef_plane(const KParams& k, int plane, int r, int c, int priStr, int s
                 int d = s == 0 ? dir : ((dir + (s == 1 ? -2 : 2)) & 7);
                 int yy = Y + sgn * av1r_cdef_directions[d][kk][0];
                 int xx = X + sgn * av1r_cdef_directions[d][kk][1];
-                int cr = (yy << sub) >> 2, cc = (xx << sub) >> 2;
+                int cr = (yy << sub) >> 2, cc = (xx << sub) >> 2;  // is_inside_filter_region
                 if (!(cc >= 0 && cc < k.mi_cols && cr >= 0 && cr < k.mi_rows)) continue;
-                int p = px(in, xx, yy);
+                int p = t[(yy - oy) * ts + xx - ox];
                 if (s == 0) sum += av1r_cdef_pri_taps[priStr & 1][kk] * constrain(p - x, priStr, damping);
                 else sum += av1r_cdef_sec_taps[priStr & 1][kk] * constrain(p - x, secStr, damping);
                 mx = imax(p, mx);
                 mn = imin(p, mn);
             }
-    px(k.cdef.pl[plane], X, Y) = (uint8_t)CLIP3(mn, mx, x + ((8 + sum - (sum < 0)) >> 4));
+    return CLIP3(mn, mx, x + ((8 + sum - (sum < 0)) >> 4));
 }
 
-// one wave per 8x8 luma block (lane = luma pixel; lanes 0..31 also do the 4x4 U/V)
+// grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.cur, writes k.cdef
 extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* __restrict__ kps)
 {
-    const KParams& k = kps[blockIdx.y];
-    const int bCols = k.mi_cols / 2, nBlocks = (k.mi_rows / 2) * bCols;
-    __shared__ int partial[4][8][16];
-    __shared__ int cost[4][8];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.x * 4 + wv;
-    const bool active = b < nBlocks;
-    const int r = active ? (b / bCols) * 2 : 0, c = active ? (b % bCols) * 2 : 0;
-    const int i = lane >> 3, j = lane & 7;
-    int idx = -1, skip = 1;
-    if (active) {
-        idx = k.cdef_idx[(r >> 4) * k.hdr->cdef_cols + (c >> 4)];
-        skip = (mi_at(k, r, c).flags & AV1R_MI_SKIP) && (mi_at(k, r + 1, c).flags & AV1R_MI_SKIP)
-            && (mi_at(k, r, c + 1).flags & AV1R_MI_SKIP) && (mi_at(k, r + 1, c + 1).flags & AV1R_MI_SKIP);
-    }
-    const bool filt = active && idx != -1 && !skip;
-    // the reference filters into a copy of the frame (Cdef.cpp:43): unfiltered blocks copy
-    if (active && !filt) {
-        px(k.cdef.pl[0], c * 4 + j, r * 4 + i) = px(k.cur.pl[0], c * 4 + j, r * 4 + i);
-        if (lane < 32) {
-            int pl = 1 + (lane >> 4), q = lane & 15;
-            px(k.cdef.pl[pl], c * 2 + (q & 3), r * 2 + (q >> 2)) = px(k.cur.pl[pl], c * 2 + (q & 3), r * 2 + (q >> 2));
-        }
-    }
-    for (int q = lane; q < 8 * 16; q += 64) partial[wv][q >> 4][q & 15] = 0;
-    __syncthreads();
-    int x = 0;
-    if (filt) {
-        x = px(k.cur.pl[0], c * 4 + j, r * 4 + i) - 128;
-        atomicAdd(&partial[wv][0][i + j], x);
-        atomicAdd(&partial[wv][1][i + j / 2], x);
-        atomicAdd(&partial[wv][2][i], x);
-        atomicAdd(&partial[wv][3][3 + i - j / 2], x);
-        atomicAdd(&partial[wv][4][7 + i - j], x);
-        atomicAdd(&partial[wv][5][3 - i / 2 + j], x);
-        atomicAdd(&partial[wv][6][j], x);
-        atomicAdd(&partial[wv][7][i / 2 + j], x);
-    }
-    __syncthreads();
-    if (filt && lane < 8) {
-        // cdefDirection costs (Cdef.cpp:229-253), lane = direction
-        const int d = lane;
-        const int* pp = partial[wv][d];
-        int cst = 0;
-        if (d == 2 || d == 6) {
-            for (int q = 0; q < 8; q++) cst += pp[q] * pp[q];
-            cst *= av1r_cdef_div_table[8];
-        } else if (d == 0 || d == 4) {
-            for (int q = 0; q < 7; q++) cst += (pp[q] * pp[q] + pp[14 - q] * pp[14 - q]) * av1r_cdef_div_table[q + 1];
-            cst += pp[7] * pp[7] * av1r_cdef_div_table[8];
-        } else {
-            for (int q = 0; q < 5; q++) cst += pp[3 + q] * pp[3 + q];
-            cst *= av1r_cdef_div_table[8];
-            for (int q = 0; q < 3; q++) cst += (pp[q] * pp[q] + pp[10 - q] * pp[10 - q]) * av1r_cdef_div_table[2 * q + 2];
-        }
-        cost[wv][d] = cst;
-    }
-    __syncthreads();
-    if (!filt) return;
-    int best = 0, yDir = 0;
-    for (int d = 0; d < 8; d++)
-        if (cost[wv][d] > best) {
-            best = cost[wv][d];
-            yDir = d;
-        }
-    const int var = (best - cost[wv][(yDir + 4) & 7]) >> 10;
+    __shared__ CdefLds L;
+    const KParams& k = kps[blockIdx.z];
+    const int t = threadIdx.x;
+    const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;  // mi units
+    if (r0 >= k.mi_rows || c0 >= k.mi_cols) return;
     const av1r_frame_hdr& h = *k.hdr;
-    int priStr = h.cdef_y_pri[idx], secStr = h.cdef_y_sec[idx];
-    int dir = priStr == 0 ? 0 : yDir;
-    int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
-    priStr = var ? (priStr * (4 + varStr) + 8) >> 4 : 0;
-    cdef_plane(k, 0, r, c, priStr, secStr, h.cdef_damping, dir, i, j);
-    if (lane < 32) {
-        int pl = 1 + (lane >> 4), q = lane & 15;
-        int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
-        int uvDir = uvPri == 0 ? 0 : av1r_cdef_uv_dir420[yDir];
-        cdef_plane(k, pl, r, c, uvPri, uvSec, h.cdef_damping - 1, uvDir, q >> 2, q & 3);
+    const int idx = k.cdef_idx[(r0 >> 4) * h.cdef_cols + (c0 >> 4)];
+    const int rows4 = imin(16, k.mi_rows - r0), cols4 = imin(16, k.mi_cols - c0);
+    const int x0 = c0 * 4, y0 = r0 * 4;
+    if (idx == -1) {
+        // not filtered: the output is the input (the reference filters into a copy)
+        for (int q = t; q < rows4 * 4 * cols4 * 4; q += 256) {
+            int i = q / (cols4 * 4), j = q - i * (cols4 * 4);
+            px(k.cdef.pl[0], x0 + j, y0 + i) = px(k.cur.pl[0], x0 + j, y0 + i);
+        }
+        for (int q = t; q < 2 * rows4 * 2 * cols4 * 2; q += 256) {
+            int pl = 1 + (q >= rows4 * 2 * cols4 * 2), e = q - (pl - 1) * rows4 * 2 * cols4 * 2;
+            int i = e / (cols4 * 2), j = e - i * (cols4 * 2);
+            px(k.cdef.pl[pl], x0 / 2 + j, y0 / 2 + i) = px(k.cur.pl[pl], x0 / 2 + j, y0 / 2 + i);
+        }
+        return;
+    }
+    // stage the deblocked region + halo; coordinates clamped into the mi grid (taps that
+    // fall outside it are never used: is_inside_filter_region)
+    {
+        const DevPlane& P = k.cur.pl[0];
+        const int mx = k.mi_cols * 4 - 1, my = k.mi_rows * 4 - 1;
+        for (int q = t; q < CD_LW * CD_LW; q += 256) {
+            int i = q / CD_LW, j = q - i * CD_LW;
+            L.y[i][j] = px(P, CLIP3(0, mx, x0 - CD_H + j), CLIP3(0, my, y0 - CD_H + i));
+        }
+        const int cmx = k.mi_cols * 2 - 1, cmy = k.mi_rows * 2 - 1;
+        for (int q = t; q < 2 * CD_CW * CD_CW; q += 256) {
+            int pl = q >= CD_CW * CD_CW, e = q - pl * CD_CW * CD_CW;
+            int i = e / CD_CW, j = e - i * CD_CW;
+            L.uv[pl][i][j] = px(k.cur.pl[1 + pl], CLIP3(0, cmx, x0 / 2 - CD_H + j), CLIP3(0, cmy, y0 / 2 - CD_H + i));
+        }
+    }
+    if (t < 64) {
+        const int br = r0 + (t >> 3) * 2, bc = c0 + (t & 7) * 2;
+        int f = 0;
+        if ((t >> 3) * 2 < rows4 && (t & 7) * 2 < cols4) {
+            // cdef_block's skip test (Cdef.cpp:79-82)
+            f = !((mi_at(k, br, bc).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc).flags & AV1R_MI_SKIP)
+                && (mi_at(k, br, bc + 1).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc + 1).flags & AV1R_MI_SKIP));
+        }
+        L.filt[t] = (uint8_t)f;
+    }
+    __syncthreads();
+    // direction costs: lane = (direction d = t >> 5, blocks t & 31 and (t & 31) + 32)
+    {
+        const int d = t >> 5;
+#pragma unroll
+        for (int hb = 0; hb < 2; hb++) {
+            const int b = (t & 31) + 32 * hb;
+            if (!L.filt[b]) continue;
+            const int bx = (b & 7) * 8, by = (b >> 3) * 8;
+            int c;
+            switch (d) {
+            case 0: c = cdef_cost<0>(L, bx, by); break;
+            case 1: c = cdef_cost<1>(L, bx, by); break;
+            case 2: c = cdef_cost<2>(L, bx, by); break;
+            case 3: c = cdef_cost<3>(L, bx, by); break;
+            case 4: c = cdef_cost<4>(L, bx, by); break;
+            case 5: c = cdef_cost<5>(L, bx, by); break;
+            case 6: c = cdef_cost<6>(L, bx, by); break;
+            default: c = cdef_cost<7>(L, bx, by); break;
+            }
+            L.cost[b][d] = c;
+        }
+    }
+    __syncthreads();
+    if (t < 64 && L.filt[t]) {
+        int best = 0, yDir = 0;
+        for (int d = 0; d < 8; d++)
+            if (L.cost[t][d] > best) {
+                best = L.cost[t][d];
+                yDir = d;
+            }
+        const int var = (best - L.cost[t][(yDir + 4) & 7]) >> 10;
+        int priStr = h.cdef_y_pri[idx];
+        const int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
+        L.dir[t] = (uint8_t)yDir;
+        L.pri[t] = (int16_t)(var ? (priStr * (4 + varStr) + 8) >> 4 : 0);
+    }
+    __syncthreads();
+    // luma
+    const int yPri = h.cdef_y_pri[idx], ySec = h.cdef_y_sec[idx];
+    for (int q = t; q < rows4 * 4 * cols4 * 4; q += 256) {
+        const int i = q / (cols4 * 4), j = q - i * (cols4 * 4);
+        const int b = (i >> 3) * 8 + (j >> 3);
+        const int X = x0 + j, Y = y0 + i;
+        int v;
+        if (!L.filt[b]) v = L.y[CD_H + i][CD_H + j];
+        else v = cdef_px(k, &L.y[0][0], CD_LW + 4, x0 - CD_H, y0 - CD_H, 0, X, Y, L.pri[b], ySec,
+                         h.cdef_damping, yPri == 0 ? 0 : L.dir[b]);
+        px(k.cdef.pl[0], X, Y) = (uint8_t)v;
+    }
+    // chroma (4:2:0: Cdef_Uv_Dir is the identity)
+    const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
+    for (int q = t; q < 2 * rows4 * 2 * cols4 * 2; q += 256) {
+        const int pl = q >= rows4 * 2 * cols4 * 2, e = q - pl * rows4 * 2 * cols4 * 2;
+        const int i = e / (cols4 * 2), j = e - i * (cols4 * 2);
+        const int b = (i >> 2) * 8 + (j >> 2);
+        const int X = x0 / 2 + j, Y = y0 / 2 + i;
+        int v;
+        if (!L.filt[b]) v = L.uv[pl][CD_H + i][CD_H + j];
+        else v = cdef_px(k, &L.uv[pl][0][0], CD_CW + 4, x0 / 2 - CD_H, y0 / 2 - CD_H, 1, X, Y, uvPri, uvSec,
+                         h.cdef_damping - 1, uvPri == 0 ? 0 : av1r_cdef_uv_dir420[L.dir[b]]);
+        px(k.cdef.pl[1 + pl], X, Y) = (uint8_t)v;
     }
 }
 
@@ -507,9 +603,9 @@ void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t 
 {
     hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
 }
-void launch_k_cdef(const KParams* kps, int n, int maxBlocks, hipStream_t s)
+void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((maxBlocks + 3) / 4, n), dim3(256), 0, s, kps);
+    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
 }
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {
