@@ -43,6 +43,11 @@ struct KParams {
     DevFrame ref[8];  // reference store slots
 };
 
+// launch batches: at most AV1R_MAX_BATCH frames per launch, AV1R_KP_SLOTS batches in
+// flight per device (recon.hip: g_kp)
+#define AV1R_MAX_BATCH 32
+#define AV1R_KP_SLOTS 8
+
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
 DEV int clip1(int v) { return CLIP3(0, 255, v); }
 DEV int r2(int x, int n) { return n == 0 ? x : ((x + (1 << (n - 1))) >> n); }

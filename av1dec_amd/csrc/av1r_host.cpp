@@ -25,7 +25,9 @@
 
 #include "av1r_dev.h"
 
-void launch_k_level(const KParams* kps, const uint32_t* tab, int n, unsigned items, hipStream_t s);
+void launch_k_level(int slot, const uint32_t* tab, int n, unsigned items, hipStream_t s);
+int kp_upload(int device, const KParams* host, int n, hipStream_t s);
+int kp_release(int device, int slot, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
@@ -518,6 +520,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 {
     av1r_ctx* c = lc;  // errors are reported on the launching context
     const int n = (int)jobs.size();
+    if (n > AV1R_MAX_BATCH) return fail(c, AV1R_E_INVALID, "at most %d frames per batch", AV1R_MAX_BATCH);
     hipStream_t st = lc->stream;
     int rc;
     size_t nLevels = 0;
@@ -594,9 +597,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         return AV1R_OK;
     };
 
-    // ---- reconstruction, level by level
+    // ---- reconstruction, level by level (frame parameters in a constant-memory slot)
+    const int slot = kp_upload(lc->device, hk, n, st);
+    if (slot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
     for (size_t l = 0; l < nLevels; l++)
-        if (total[l]) launch_k_level(dk, dtab + l * tabW, n, total[l], st);
+        if (total[l]) launch_k_level(slot, dtab + l * tabW, n, total[l], st);
+    if (kp_release(lc->device, slot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
     HIPCHK(hipGetLastError());
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));

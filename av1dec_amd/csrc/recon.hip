@@ -15,6 +15,8 @@
 //            Inter-intra items: the intra half of an inter-intra block, blended in place.
 // The host (av1r_host.cpp) orders launches by dependency level so every pixel a work
 // item reads was finalised by an earlier launch.
+#include <mutex>
+
 #include "av1r_dev.h"
 #include "intra_dev.h"
 #include "txfm_dev.h"
@@ -350,11 +352,25 @@ DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1)
 }
 
 // Stage the (rh + 7) x (rw + 7) reference window of PU-relative region
-// [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin).
+// [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin).  Rows are
+// clamped per row; when no column needs clamping the row is moved as aligned dwords
+// (two loads funnel-shifted into one aligned LDS dword), otherwise byte by byte.
 DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, int rh)
 {
     const int wx0 = (R.startX >> 10) - 3 + rx0, wy0 = (R.startY >> 10) - 3 + ry0;
     const int wc = rw + 7, wr = rh + 7;
+    if (wx0 >= 0 && wx0 + wc - 1 <= R.lastX) {
+        const int ndw = (wc + 3) >> 2, sh = (wx0 & 3) * 8;
+        const int ax0 = wx0 & ~3;
+        for (int q = threadIdx.x; q < ndw * wr; q += 64) {
+            const int i = q / ndw, d = q - i * ndw;
+            const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, wy0 + i) * R.p.stride + ax0 + 4 * d;
+            const uint32_t lo = *reinterpret_cast<const uint32_t*>(row);
+            const uint32_t hi = *reinterpret_cast<const uint32_t*>(row + 4);
+            *reinterpret_cast<uint32_t*>(win + i * WC + 4 * d) = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+        }
+        return;
+    }
     for (int q = threadIdx.x; q < wc * wr; q += 64) {
         int i = q / wc, j = q - i * wc;
         int yy = CLIP3(0, R.lastY, wy0 + i), xx = CLIP3(0, R.lastX, wx0 + j);
@@ -363,9 +379,38 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
 }
 
 // Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the (rh + 7)
-// window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).
+// window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).  Four
+// outputs per lane from three LDS dwords when rw is a multiple of 4.
 DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0)
 {
+    if ((rw & 3) == 0) {
+        const int g4 = rw >> 2;
+        for (int q = threadIdx.x; q < (rh + 7) * g4; q += 64) {
+            const int i = q / g4, g = q - i * g4;
+            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + i * WC) + g;
+            const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2];
+            int b[12];
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                b[m] = (d0 >> (8 * m)) & 0xff;
+                b[m + 4] = (d1 >> (8 * m)) & 0xff;
+                b[m + 8] = (d2 >> (8 * m)) & 0xff;
+            }
+            int o[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                int hs = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) hs += hf[u] * b[m + u];
+                o[m] = r2(hs, R0) & 0xffff;
+            }
+            uint2 v;
+            v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+            v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+            *reinterpret_cast<uint2*>(hb + i * TS + 4 * g) = v;
+        }
+        return;
+    }
     for (int q = threadIdx.x; q < (rh + 7) * rw; q += 64) {
         const int i = q / rw, j = q - i * rw;
         const uint8_t* row = win + i * WC + j;
@@ -386,6 +431,26 @@ DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, 
 #pragma unroll
     for (int t = 0; t < 8; t++) s += vf[t] * col[t * TS];
     return (int16_t)r2(s, R1);
+}
+// Four horizontally adjacent samples (cc a multiple of 4): 8 LDS reads of 4 int16.
+DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer, int* out)
+{
+    if (integer) {
+#pragma unroll
+        for (int m = 0; m < 4; m++) out[m] = (int16_t)(win[(rr + 3) * WC + cc + 3 + m] << (14 - R0 - R1));
+        return;
+    }
+    int s[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint2 v = *reinterpret_cast<const uint2*>(hb + (rr + t) * TS + cc);
+        s[0] += vf[t] * (int16_t)(v.x & 0xffff);
+        s[1] += vf[t] * (int16_t)(v.x >> 16);
+        s[2] += vf[t] * (int16_t)(v.y & 0xffff);
+        s[3] += vf[t] * (int16_t)(v.y >> 16);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) out[m] = (int16_t)r2(s[m], R1);
 }
 
 // blockWarp (InterPredict.cpp:507-553), split like the reference into its horizontal
@@ -573,16 +638,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     if (isCompound && R[1].useWin && !integer[1]) hpass(L.win[1], L.hb[1], rw, rh, hf[1], R0);
     if (isCompound && R[1].warp) warp_hpass(R[1], L.hb[1], rx0, ry0, rw, rh, x, y, sub, R0);
     __syncthreads();
-    for (int q = t; q < rw * rh; q += 64) {
-        const int rr = q / rw, cc = q - rr * rw, r = ry0 + rr, c = rx0 + cc;
-        int p0 = R[0].useWin ? pred_win(L.win[0], L.hb[0], rr, cc, R0, R1, vf[0], integer[0])
-                 : R[0].warp ? warp_v(R[0], L.hb[0], rr, cc, r, c, rw, x, y, sub, R1)
-                             : pred_direct(R[0], r, c, R0, R1);
-        int p1 = 0;
-        if (isCompound)
-            p1 = R[1].useWin ? pred_win(L.win[1], L.hb[1], rr, cc, R0, R1, vf[1], integer[1])
-                 : R[1].warp ? warp_v(R[1], L.hb[1], rr, cc, r, c, rw, x, y, sub, R1)
-                             : pred_direct(R[1], r, c, R0, R1);
+    auto blend = [&](int p0, int p1, int r, int c) {
         int v;
         if (mode == 0) {
             v = clip1(p0);
@@ -628,6 +684,36 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
             v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
         }
         L.tile[(toy + r) * TS + tox + c] = (uint8_t)v;
+    };
+    auto sample = [&](int l, int rr, int cc) {
+        const int r = ry0 + rr, c = rx0 + cc;
+        return R[l].useWin ? pred_win(L.win[l], L.hb[l], rr, cc, R0, R1, vf[l], integer[l])
+             : R[l].warp   ? warp_v(R[l], L.hb[l], rr, cc, r, c, rw, x, y, sub, R1)
+                           : pred_direct(R[l], r, c, R0, R1);
+    };
+    if ((rw & 3) == 0 && R[0].useWin && (!isCompound || R[1].useWin)) {
+        // four adjacent samples per lane (window references only)
+        const int g4 = rw >> 2;
+        for (int q = t; q < rh * g4; q += 64) {
+            const int rr = q / g4, cc = (q - rr * g4) * 4;
+            int p0[4], p1[4] = {0, 0, 0, 0};
+            pred_win4(L.win[0], L.hb[0], rr, cc, R0, R1, vf[0], integer[0], p0);
+            if (isCompound) pred_win4(L.win[1], L.hb[1], rr, cc, R0, R1, vf[1], integer[1], p1);
+            // one blend body, the four samples rotated through it (no unrolled copies)
+            int a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
+            int b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
+#pragma nounroll
+            for (int m = 0; m < 4; m++) {
+                blend(a0, b0, ry0 + rr, rx0 + cc + m);
+                a0 = a1; a1 = a2; a2 = a3;
+                b0 = b1; b1 = b2; b2 = b3;
+            }
+        }
+    } else {
+        for (int q = t; q < rw * rh; q += 64) {
+            const int rr = q / rw, cc = q - rr * rw;
+            blend(sample(0, rr, cc), isCompound ? sample(1, rr, cc) : 0, ry0 + rr, rx0 + cc);
+        }
     }
     __syncthreads();
 }
@@ -827,16 +913,23 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
 // One launch per dependency level: every work item of the level (inter tiles, inter-
 // intra blends, transform blocks) is one 64-lane workgroup.
 // ---------------------------------------------------------------------------------
+// Per-launch frame parameters live in the constant address space so that every field a
+// work item reads is a scalar load (a KParams array behind a plain global pointer costs
+// ~100 VGPRs of hoisted vector loads and halves occupancy).  Launch batches rotate over
+// AV1R_KP_SLOTS slots of AV1R_MAX_BATCH frames; a slot is rewritten only after the
+// previous batch that used it has finished (event per slot, waited for on the GPU).
+__constant__ KParams g_kp[AV1R_KP_SLOTS][AV1R_MAX_BATCH];
+
 // Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
 // counts at this level; tab[n + 1 + s]: offset of frame s's level in its item list).
-extern "C" __global__ __launch_bounds__(64) void k_level(const KParams* __restrict__ kps, const uint32_t* __restrict__ tab, int n)
+extern "C" __global__ __launch_bounds__(64) void k_level(int slot, const uint32_t* __restrict__ tab, int n)
 {
     constexpr size_t kLds = sizeof(TbLds) > sizeof(InterLds) ? sizeof(TbLds) : sizeof(InterLds);
     __shared__ __align__(16) uint8_t smem[kLds];
     const uint32_t b = blockIdx.x;
     int s = 0;
     while (s + 1 < n && b >= tab[s + 1]) s++;
-    const KParams& k = kps[s];
+    const KParams& k = g_kp[slot][s];
     const uint32_t it = k.items[tab[n + 1 + s] + (b - tab[s])];
     const uint32_t kind = AV1R_ITEM_KIND(it), idx = AV1R_ITEM_INDEX(it);
     if (kind == AV1R_ITEM_TB) tb_item(k, idx, *reinterpret_cast<TbLds*>(smem));
@@ -844,7 +937,44 @@ extern "C" __global__ __launch_bounds__(64) void k_level(const KParams* __restri
     else ii_item(k, idx, *reinterpret_cast<TbLds*>(smem));
 }
 
-void launch_k_level(const KParams* kps, const uint32_t* tab, int n, unsigned items, hipStream_t s)
+void launch_k_level(int slot, const uint32_t* tab, int n, unsigned items, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_level, dim3(items), dim3(64), 0, s, kps, tab, n);
+    hipLaunchKernelGGL(k_level, dim3(items), dim3(64), 0, s, slot, tab, n);
+}
+
+namespace {
+struct KpSlots {
+    std::mutex m;
+    int next = 0;
+    hipEvent_t ev[AV1R_KP_SLOTS] = {};
+    bool used[AV1R_KP_SLOTS] = {};
+};
+KpSlots g_slots[64];  // per device
+}  // namespace
+
+// Claim a slot on `device`, order the stream after its previous user, and copy the n
+// frame parameters (pinned host memory) into it.  Returns the slot or -1.
+int kp_upload(int device, const KParams* host, int n, hipStream_t s)
+{
+    if (device < 0 || device >= 64 || n < 1 || n > AV1R_MAX_BATCH) return -1;
+    KpSlots& S = g_slots[device];
+    std::lock_guard<std::mutex> lock(S.m);
+    const int slot = S.next;
+    S.next = (S.next + 1) % AV1R_KP_SLOTS;
+    if (!S.ev[slot] && hipEventCreateWithFlags(&S.ev[slot], hipEventDisableTiming) != hipSuccess) return -1;
+    if (S.used[slot] && hipStreamWaitEvent(s, S.ev[slot], 0) != hipSuccess) return -1;
+    void* base = nullptr;
+    if (hipGetSymbolAddress(&base, HIP_SYMBOL(g_kp)) != hipSuccess) return -1;
+    uint8_t* dst = static_cast<uint8_t*>(base) + (size_t)slot * AV1R_MAX_BATCH * sizeof(KParams);
+    if (hipMemcpyAsync(dst, host, sizeof(KParams) * n, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+    return slot;
+}
+
+// The last launch reading `slot` has been queued on `s`.
+int kp_release(int device, int slot, hipStream_t s)
+{
+    KpSlots& S = g_slots[device];
+    std::lock_guard<std::mutex> lock(S.m);
+    S.used[slot] = true;
+    return hipEventRecord(S.ev[slot], s) == hipSuccess ? 0 : -1;
 }
