@@ -20,6 +20,23 @@ struct DevFrame {
     int width, height;  // FrameWidth / FrameHeight of the frame stored here
 };
 
+// One work item of a frame's level-ordered schedule (built by the host, 32 bytes: one
+// scalar load gives a transform block everything it needs before its block record).
+struct WorkItem {
+    uint32_t code;      // AV1R_ITEM(kind, index)
+    uint32_t block;     // owning block
+    uint32_t coef_off;  // TB: first coefficient
+    uint16_t x, y;      // TB: plane position
+    uint16_t coef_cnt;  // TB
+    uint8_t plane, tx_size, tx_type, flags;  // TB (flags: AV1R_TB_*)
+    uint8_t pred;       // TB prediction source: AV1R_PRED_INTRA / _PALETTE / _INTER
+    uint8_t pad[9];
+};
+static_assert(sizeof(WorkItem) == 32, "WorkItem layout");
+#define AV1R_PRED_INTRA 0
+#define AV1R_PRED_PALETTE 1
+#define AV1R_PRED_INTER 2
+
 // Everything the stage kernels read about one frame.  A launch covers n frames (one per
 // stream of a batch): the kernels receive a device array of n KParams and pick theirs
 // by blockIdx (see k_level / k_lf / k_cdef / k_lr).
@@ -32,7 +49,7 @@ struct KParams {
     const uint8_t* palette;
     const int8_t* cdef_idx;
     const av1r_lr_unit* lr;
-    const uint32_t* items;  // this frame's level-ordered work items
+    const WorkItem* items;  // this frame's level-ordered work items
     uint32_t n_items;
     int mi_stride;
     int mi_cols, mi_rows;

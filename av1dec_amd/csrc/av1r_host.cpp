@@ -18,6 +18,7 @@
 #include <array>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -25,7 +26,8 @@
 
 #include "av1r_dev.h"
 
-void launch_k_level(int slot, const uint32_t* tab, int n, unsigned items, hipStream_t s);
+void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
+    uint32_t traceBase, hipStream_t s);
 int kp_upload(int device, const KParams* host, int n, hipStream_t s);
 int kp_release(int device, int slot, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
@@ -51,7 +53,9 @@ struct Upload {
 };
 
 struct Level {
-    uint32_t off = 0, cnt = 0;  // items [off, off + cnt) of the schedule
+    // items [off, off + cnt) per kernel: [0] inter tiles (k_inter), [1] inter-intra blends
+    // then transform blocks (k_tb)
+    uint32_t off[2] = {}, cnt[2] = {};
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -65,7 +69,7 @@ struct Prepared {
     bool owned = false;
     av1r_frame_hdr hdr;
     KParams base;  // batch pointers into dev
-    const uint32_t* dItems = nullptr;
+    const WorkItem* dItems = nullptr;
     std::vector<Level> levels;
     bool usedRef[8] = {};
     uint64_t bytes = 0;
@@ -84,12 +88,16 @@ struct av1r_ctx {
     Upload meta[2];  // per-launch KParams + level tables
     int metaIdx = 0;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
+    // debug timeline of every recon work item (env AV1R_TRACE_FILE): 8 x u64 per item
+    FILE* traceFile = nullptr;
+    unsigned long long* traceDev = nullptr;
+    size_t traceCap = 0;
     std::string err;
     // schedule scratch
     std::vector<int16_t> lvlmap[3];
     int mapW[3] = {}, mapH[3] = {};
     std::vector<std::vector<uint32_t>> lvP, lvB, lvT;  // inter tiles, inter-intra blends, TBs per level
-    std::vector<uint32_t> items;
+    std::vector<WorkItem> items;
     std::vector<Level> levels;
     // split submission (frame_begin / submit_tile / frame_end)
     bool inFrame = false;
@@ -394,9 +402,39 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
     c->items.clear();
     c->levels.assign(nl, Level());
     for (size_t l = 0; l < nl; l++) {
-        c->levels[l].off = (uint32_t)c->items.size();
-        for (auto* v : {&c->lvP, &c->lvB, &c->lvT}) c->items.insert(c->items.end(), (*v)[l].begin(), (*v)[l].end());
-        c->levels[l].cnt = (uint32_t)c->items.size() - c->levels[l].off;
+        c->levels[l].off[0] = (uint32_t)c->items.size();
+        c->levels[l].cnt[0] = (uint32_t)c->lvP[l].size();
+        c->levels[l].off[1] = c->levels[l].off[0] + c->levels[l].cnt[0];
+        c->levels[l].cnt[1] = (uint32_t)(c->lvB[l].size() + c->lvT[l].size());
+        for (auto* v : {&c->lvP, &c->lvB, &c->lvT}) {
+            for (uint32_t code : (*v)[l]) {
+                WorkItem w;
+                memset(&w, 0, sizeof(w));
+                w.code = code;
+                const uint32_t idx = AV1R_ITEM_INDEX(code);
+                switch (AV1R_ITEM_KIND(code)) {
+                case AV1R_ITEM_INTER: w.block = idx >> 4; break;
+                case AV1R_ITEM_II: w.block = idx; break;
+                default: {
+                    const av1r_tb& t = b->tbs[idx];
+                    const av1r_block& blk = b->blocks[t.block];
+                    w.block = t.block;
+                    w.coef_off = t.coef_off;
+                    w.x = t.x;
+                    w.y = t.y;
+                    w.coef_cnt = t.coef_cnt;
+                    w.plane = t.plane;
+                    w.tx_size = t.tx_size;
+                    w.tx_type = t.tx_type;
+                    w.flags = t.flags;
+                    w.pred = (blk.flags & AV1R_BLK_INTER) ? AV1R_PRED_INTER
+                           : (t.plane ? blk.palette_size_uv : blk.palette_size_y) ? AV1R_PRED_PALETTE
+                                                                                  : AV1R_PRED_INTRA;
+                }
+                }
+                c->items.push_back(w);
+            }
+        }
     }
     c->nLevelsLast = (int)nl;
 }
@@ -414,7 +452,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szPal = align256(b->n_palette);
     const size_t szCdef = align256((size_t)h->cdef_rows * h->cdef_cols);
     const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
-    const size_t szItems = align256(4 * c->items.size() + 4);
+    const size_t szItems = align256(sizeof(WorkItem) * c->items.size() + 4);
     *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems;
     if (!host) return AV1R_OK;
     size_t off = 0;
@@ -434,7 +472,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.palette = put(b->palette, b->n_palette, szPal);
     k.cdef_idx = (const int8_t*)put(b->cdef_idx, (size_t)h->cdef_rows * h->cdef_cols, szCdef);
     k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
-    P.dItems = (const uint32_t*)put(c->items.data(), 4 * c->items.size(), szItems);
+    P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
     k.mi_stride = h->mi_stride;
     k.mi_cols = h->mi_cols;
     k.mi_rows = h->mi_rows;
@@ -536,10 +574,10 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         maxH = std::max(maxH, h->frame_height);
         anyLr |= h->uses_lr != 0;
     }
-    // launch metadata: [KParams x n][per level: n + 1 prefix counts, n item offsets]
+    // launch metadata: [KParams x n][per level and item kind: n + 1 prefix counts, n item offsets]
     const size_t tabW = 2 * (size_t)n + 1;
     const size_t kBytes = align256(sizeof(KParams) * n);
-    const size_t need = kBytes + 4 * tabW * std::max<size_t>(nLevels, 1);
+    const size_t need = kBytes + 4 * tabW * 2 * std::max<size_t>(nLevels, 1);
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % 2;
     if (M.pending) {
@@ -557,18 +595,19 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     KParams* hk = reinterpret_cast<KParams*>(M.host);
     for (int i = 0; i < n; i++) hk[i] = jobs[i].k;
     uint32_t* tab = reinterpret_cast<uint32_t*>(M.host + kBytes);
-    std::vector<uint32_t> total(nLevels, 0);
-    for (size_t l = 0; l < nLevels; l++) {
-        uint32_t* t = tab + l * tabW;
-        t[0] = 0;
-        for (int i = 0; i < n; i++) {
-            const auto& lv = jobs[i].P->levels;
-            const uint32_t cnt = l < lv.size() ? lv[l].cnt : 0;
-            t[i + 1] = t[i] + cnt;
-            t[n + 1 + i] = l < lv.size() ? lv[l].off : 0;
+    std::vector<uint32_t> total(nLevels * 2, 0);
+    for (size_t l = 0; l < nLevels; l++)
+        for (int kk = 0; kk < 2; kk++) {
+            uint32_t* t = tab + (l * 2 + kk) * tabW;
+            t[0] = 0;
+            for (int i = 0; i < n; i++) {
+                const auto& lv = jobs[i].P->levels;
+                const uint32_t cnt = l < lv.size() ? lv[l].cnt[kk] : 0;
+                t[i + 1] = t[i] + cnt;
+                t[n + 1 + i] = l < lv.size() ? lv[l].off[kk] : 0;
+            }
+            total[l * 2 + kk] = t[n];
         }
-        total[l] = t[n];
-    }
     HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
     const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
@@ -600,8 +639,34 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // ---- reconstruction, level by level (frame parameters in a constant-memory slot)
     const int slot = kp_upload(lc->device, hk, n, st);
     if (slot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
+    size_t allItems = 0;
+    for (uint32_t v : total) allItems += v;
+    if (lc->traceFile && lc->traceCap < allItems) {
+        if (lc->traceDev) (void)hipFree(lc->traceDev);
+        lc->traceCap = allItems + allItems / 2;
+        HIPCHK(hipMalloc(&lc->traceDev, lc->traceCap * 64));
+    }
+    unsigned long long* trace = lc->traceFile ? lc->traceDev : nullptr;
+    uint32_t traceBase = 0;
     for (size_t l = 0; l < nLevels; l++)
-        if (total[l]) launch_k_level(slot, dtab + l * tabW, n, total[l], st);
+        for (int kk = 0; kk < 2; kk++) {
+            const uint32_t cnt = total[l * 2 + kk];
+            if (!cnt) continue;
+            launch_k_level(kk, slot, dtab + (l * 2 + kk) * tabW, n, cnt, trace, traceBase, st);
+            traceBase += cnt;
+        }
+    if (trace) {
+        // rows: code, stream << 32 | tx_size << 8 | pred, t_entry, t_item, t_pred, t_end, level, 0
+        std::vector<unsigned long long> hv((size_t)allItems * 8);
+        HIPCHK(hipMemcpyAsync(hv.data(), trace, hv.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        size_t q = 0;
+        for (size_t l = 0; l < nLevels; l++)
+            for (int kk = 0; kk < 2; kk++)
+                for (uint32_t i = 0; i < total[l * 2 + kk]; i++, q++) hv[q * 8 + 6] = l;
+        fwrite(hv.data(), 8, hv.size(), lc->traceFile);
+        fflush(lc->traceFile);
+    }
     if (kp_release(lc->device, slot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
     HIPCHK(hipGetLastError());
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
@@ -695,6 +760,7 @@ int av1r_create(int device, av1r_ctx** out)
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
     for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
+    if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
     *out = c;
     return AV1R_OK;
 }
@@ -716,6 +782,8 @@ void av1r_destroy(av1r_ctx* c)
             (void)hipEventDestroy(u.done);
         }
     (void)hipEventDestroy(c->sync);
+    if (c->traceDev) (void)hipFree(c->traceDev);
+    if (c->traceFile) fclose(c->traceFile);
     for (auto& e : c->evPool)
         for (auto& x : e) (void)hipEventDestroy(x);
     for (Prepared* P : c->prepared)

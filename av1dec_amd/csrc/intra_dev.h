@@ -108,14 +108,14 @@ DEV void coop_edge_upsample(const uint8_t* e, uint8_t* up, int numPx)
 
 DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) - 4); }
 
-// Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps).
-// `src` is the frame plane being reconstructed.  Ends with a __syncthreads().
-DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const IntraParams& P,
-    IntraLds& L, uint8_t* pred, int ps)
+// Gathers AboveRow / LeftCol (IntraPredict.cpp:571-611) of a (1<<log2W) x (1<<log2H)
+// prediction at (x, y) of plane `plane` into L (global loads only; the caller issues the
+// barrier before the edges are read, so independent loads can be overlapped with it).
+DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
+    int log2H, bool hL, bool hA, bool hAR, bool hBL, IntraLds& L)
 {
     const int t = threadIdx.x, nt = blockDim.x;
-    const int w = 1 << P.log2W, h = 1 << P.log2H;
-    const int plane = P.plane, x = P.x, y = P.y;
+    const int w = 1 << log2W, h = 1 << log2H;
     // predict_intra uses subsampling_x for both axes (IntraPredict.cpp:566-567)
     const int sub = plane ? 1 : 0;
     const int maxX = ((miCols * 4) >> sub) - 1;
@@ -123,33 +123,40 @@ DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const I
     uint8_t* above = L.above + EDGE_OFF;
     uint8_t* left = L.left + EDGE_OFF;
     const int n = w + h;
-    {
-        const bool hA = P.haveAbove, hL = P.haveLeft;
-        int aboveLimit = imin(maxX, x + (P.haveAR ? 2 * w : w) - 1);
-        int leftLimit = imin(maxY, y + (P.haveBL ? 2 * h : h) - 1);
-        for (int i = t; i < n; i += nt) {
-            uint8_t a, l;
-            if (!hA && hL) a = px(src, x - 1, y);
-            else if (!hA && !hL) a = 127;
-            else a = px(src, imin(aboveLimit, x + i), y - 1);
-            if (!hL && hA) l = px(src, x, y - 1);
-            else if (!hA && !hL) l = 129;
-            else l = px(src, x - 1, imin(leftLimit, y + i));
-            above[i] = a;
-            left[i] = l;
-        }
-        if (t == 0) {
-            uint8_t c;
-            if (hA && hL) c = px(src, x - 1, y - 1);
-            else if (hA) c = px(src, x, y - 1);
-            else if (hL) c = px(src, x - 1, y);
-            else c = 128;
-            above[-1] = c;
-            left[-1] = c;
-        }
+    const int aboveLimit = imin(maxX, x + (hAR ? 2 * w : w) - 1);
+    const int leftLimit = imin(maxY, y + (hBL ? 2 * h : h) - 1);
+    for (int i = t; i < n; i += nt) {
+        uint8_t a, l;
+        if (!hA && hL) a = px(src, x - 1, y);
+        else if (!hA && !hL) a = 127;
+        else a = px(src, imin(aboveLimit, x + i), y - 1);
+        if (!hL && hA) l = px(src, x, y - 1);
+        else if (!hA && !hL) l = 129;
+        else l = px(src, x - 1, imin(leftLimit, y + i));
+        above[i] = a;
+        left[i] = l;
     }
-    __syncthreads();
+    if (t == 0) {
+        uint8_t c;
+        if (hA && hL) c = px(src, x - 1, y - 1);
+        else if (hA) c = px(src, x, y - 1);
+        else if (hL) c = px(src, x - 1, y);
+        else c = 128;
+        above[-1] = c;
+        left[-1] = c;
+    }
+}
 
+// Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps) from edges already
+// gathered into L (coop_intra_edges + a barrier).  Ends with a __syncthreads().
+DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, IntraLds& L, uint8_t* pred, int ps)
+{
+    const int t = threadIdx.x, nt = blockDim.x;
+    const int w = 1 << P.log2W, h = 1 << P.log2H;
+    const int plane = P.plane, x = P.x, y = P.y;
+    const int sub = plane ? 1 : 0;
+    uint8_t* above = L.above + EDGE_OFF;
+    uint8_t* left = L.left + EDGE_OFF;
     if (P.filterIntra) {
         // recursiveIntraPrediction (IntraPredict.cpp:112-149): cell (i2, j4) needs cells
         // (i2-1, j4-1..j4) and (i2, j4-1): process anti-diagonals d = i2 + j4.
@@ -309,4 +316,15 @@ DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const I
         }
     }
     __syncthreads();
+}
+
+// Gather + predict (IntraPredict::predict_intra, IntraPredict.cpp:563-630).  Ends with a
+// __syncthreads().
+DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const IntraParams& P,
+    IntraLds& L, uint8_t* pred, int ps)
+{
+    coop_intra_edges(miCols, miRows, src, P.plane, P.x, P.y, P.log2W, P.log2H, P.haveLeft, P.haveAbove, P.haveAR,
+        P.haveBL, L);
+    __syncthreads();
+    coop_intra_from_edges(miCols, miRows, P, L, pred, ps);
 }

@@ -21,6 +21,22 @@
 #include "intra_dev.h"
 #include "txfm_dev.h"
 
+// Debug timeline (AV1R_TRACE_FILE): lane 0 of each item stamps the 100 MHz real-time
+// counter at entry, once the item record is in, after the prediction and at the end.
+// Compiled in only with -DAV1R_TRACE (the stamps' waits constrain scheduling).
+DEV void trace_stamp(unsigned long long* tr, int slot)
+{
+#ifdef AV1R_TRACE
+    if (tr && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        tr[slot] = __builtin_amdgcn_s_memrealtime();
+    }
+#else
+    (void)tr;
+    (void)slot;
+#endif
+}
+
 // ---------------------------------------------------------------------------------
 // Transform blocks
 // ---------------------------------------------------------------------------------
@@ -66,7 +82,8 @@ DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, cons
 
 // reconstruct() + inverseTransform() (TransformBlock.cpp:2173-2276), the flip and the
 // add-and-clip onto the prediction in L.pred, stored to the frame at (x, y).
-DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds& L, const DevPlane& dst)
+DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds& L, const DevPlane& dst,
+    uint32_t c0)
 {
     const int t = threadIdx.x;
     const int txSz = tb.tx_size;
@@ -88,7 +105,7 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
     const int acQ = av1r_ac_qlookup[CLIP3(0, 255, blk.qindex + acDelta)];
     const uint32_t* cf = k.coefs + tb.coef_off;
     for (int q = t; q < tb.coef_cnt; q += 64) {
-        uint32_t c = cf[q];
+        const uint32_t c = q == t ? c0 : cf[q];  // the first 64 were prefetched by the caller
         int pos = AV1R_COEF_POS(c), level = AV1R_COEF_LEVEL(c);
         int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
         int sign = d < 0 ? -1 : 1;
@@ -134,27 +151,42 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
     }
 }
 
-// One transform block (TransformBlock::decode, TransformBlock.cpp:2400-2456).
-DEV void tb_item(const KParams& k, uint32_t idx, TbLds& L)
+// One transform block (TransformBlock::decode, TransformBlock.cpp:2400-2456).  The
+// item record carries the TB, so its first coefficients and its prediction inputs (intra
+// edges or the inter-predicted pixels) are in flight before the block record is read.
+DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long long* tr)
 {
     const int t = threadIdx.x;
-    const av1r_tb tb = k.tbs[idx];
-    const av1r_block& blk = k.blocks[tb.block];
+    av1r_tb tb;
+    tb.block = wi.block;
+    tb.coef_off = wi.coef_off;
+    tb.x = wi.x;
+    tb.y = wi.y;
+    tb.coef_cnt = wi.coef_cnt;
+    tb.plane = wi.plane;
+    tb.tx_size = wi.tx_size;
+    tb.tx_type = wi.tx_type;
+    tb.flags = wi.flags;
     const int plane = tb.plane, x = tb.x, y = tb.y, txSz = tb.tx_size;
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
     const int log2W = av1r_tx_w_log2[txSz];
     const DevPlane& dst = k.cur.pl[plane];
+    const int src = wi.pred;
+    const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
+    if (src == AV1R_PRED_INTRA)
+        coop_intra_edges(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+            (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
+            (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
+    const av1r_block& blk = k.blocks[tb.block];
     const uint32_t bflags = blk.flags;
-    const int isInter = (bflags & AV1R_BLK_INTER) != 0;
-    const int palSize = plane ? blk.palette_size_uv : blk.palette_size_y;
     const av1r_frame_hdr& hd = *k.hdr;
 
-    if (isInter) {
+    if (src == AV1R_PRED_INTER) {
         for (int q = t; q < w * h; q += 64) {
             int i = q >> log2W, j = q & (w - 1);
             L.pred[i * 64 + j] = px(dst, x + j, y + i);
         }
-    } else if (palSize) {
+    } else if (src == AV1R_PRED_PALETTE) {
         // Block::Palette::predict_palette (Block.cpp:2279-2298)
         const uint8_t* ph = k.palette + blk.palette_off;
         int bx = x - (blk.mi_col >> (plane ? 1 : 0)) * 4, by = y - (blk.mi_row >> (plane ? 1 : 0)) * 4;
@@ -184,7 +216,8 @@ DEV void tb_item(const KParams& k, uint32_t idx, TbLds& L)
         P.smooth = plane ? ((bflags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
                          : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
         P.edgeFilter = hd.enable_intra_edge_filter;
-        coop_intra_predict(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
+        __syncthreads();  // edges gathered
+        coop_intra_from_edges(k.mi_cols, k.mi_rows, P, L.intra, L.pred, 64);
         if (isCfl) {
             // predict_chroma_from_luma (IntraPredict.cpp:632-667)
             const DevPlane& luma = k.cur.pl[0];
@@ -209,9 +242,10 @@ DEV void tb_item(const KParams& k, uint32_t idx, TbLds& L)
         }
     }
     __syncthreads();
+    trace_stamp(tr, 4);
     if (tb.coef_cnt) {
-        tb_residual(k, tb, blk, L, dst);
-    } else if (!isInter) {
+        tb_residual(k, tb, blk, L, dst, c0);
+    } else if (src != AV1R_PRED_INTER) {
         for (int q = t; q < w * h; q += 64) {
             int i = q >> log2W, j = q & (w - 1);
             px(dst, x + j, y + i) = L.pred[i * 64 + j];
@@ -240,8 +274,10 @@ DEV void tb_item(const KParams& k, uint32_t idx, TbLds& L)
 struct InterLds {
     uint8_t tile[TS * TS];        // this plane's tile, assembled before the store
     uint8_t mask[TS * TS];        // compute_prediction's Mask (luma, persists across planes)
-    uint8_t win[2][(TS + 7) * WC];  // reference windows
-    int16_t hb[2][HBN];           // horizontally filtered window rows / warp intermediates
+    uint8_t win[2][(TS + 7) * WC];  // reference windows (luma, or the current plane)
+    struct {
+        int16_t hbw[2][HBN];      // horizontally filtered window rows / warp intermediates
+    } u;
 };
 
 struct RefSel {
@@ -355,7 +391,7 @@ DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1)
 // [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin).  Rows are
 // clamped per row; when no column needs clamping the row is moved as aligned dwords
 // (two loads funnel-shifted into one aligned LDS dword), otherwise byte by byte.
-DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, int rh)
+DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, int rh, int wcs = WC)
 {
     const int wx0 = (R.startX >> 10) - 3 + rx0, wy0 = (R.startY >> 10) - 3 + ry0;
     const int wc = rw + 7, wr = rh + 7;
@@ -367,27 +403,27 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
             const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, wy0 + i) * R.p.stride + ax0 + 4 * d;
             const uint32_t lo = *reinterpret_cast<const uint32_t*>(row);
             const uint32_t hi = *reinterpret_cast<const uint32_t*>(row + 4);
-            *reinterpret_cast<uint32_t*>(win + i * WC + 4 * d) = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+            *reinterpret_cast<uint32_t*>(win + i * wcs + 4 * d) = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
         }
         return;
     }
     for (int q = threadIdx.x; q < wc * wr; q += 64) {
         int i = q / wc, j = q - i * wc;
         int yy = CLIP3(0, R.lastY, wy0 + i), xx = CLIP3(0, R.lastX, wx0 + j);
-        win[i * WC + j] = R.p.p[(size_t)yy * R.p.stride + xx];
+        win[i * wcs + j] = R.p.p[(size_t)yy * R.p.stride + xx];
     }
 }
 
 // Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the (rh + 7)
 // window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).  Four
 // outputs per lane from three LDS dwords when rw is a multiple of 4.
-DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0)
+DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0, int wcs = WC)
 {
     if ((rw & 3) == 0) {
         const int g4 = rw >> 2;
         for (int q = threadIdx.x; q < (rh + 7) * g4; q += 64) {
             const int i = q / g4, g = q - i * g4;
-            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + i * WC) + g;
+            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + i * wcs) + g;
             const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2];
             int b[12];
 #pragma unroll
@@ -413,7 +449,7 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
     }
     for (int q = threadIdx.x; q < (rh + 7) * rw; q += 64) {
         const int i = q / rw, j = q - i * rw;
-        const uint8_t* row = win + i * WC + j;
+        const uint8_t* row = win + i * wcs + j;
         int hs = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) hs += hf[u] * row[u];
@@ -423,9 +459,10 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
 
 // The same sample as pred_direct for an unscaled, unwarped reference: the vertical pass
 // over the staged intermediate rows (or the integer-position copy from the window).
-DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer)
+DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer,
+    int wcs = WC)
 {
-    if (integer) return (int16_t)(win[(rr + 3) * WC + cc + 3] << (14 - R0 - R1));
+    if (integer) return (int16_t)(win[(rr + 3) * wcs + cc + 3] << (14 - R0 - R1));
     const int16_t* col = hb + rr * TS + cc;
     int s = 0;
 #pragma unroll
@@ -433,11 +470,12 @@ DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, 
     return (int16_t)r2(s, R1);
 }
 // Four horizontally adjacent samples (cc a multiple of 4): 8 LDS reads of 4 int16.
-DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer, int* out)
+DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer, int* out,
+    int wcs = WC)
 {
     if (integer) {
 #pragma unroll
-        for (int m = 0; m < 4; m++) out[m] = (int16_t)(win[(rr + 3) * WC + cc + 3 + m] << (14 - R0 - R1));
+        for (int m = 0; m < 4; m++) out[m] = (int16_t)(win[(rr + 3) * wcs + cc + 3 + m] << (14 - R0 - R1));
         return;
     }
     int s[4] = {0, 0, 0, 0};
@@ -572,20 +610,17 @@ DEV void distance_weights(const KParams& k, const av1r_mi& info, int& fwd, int& 
 // predict_inter for the PU-relative region [rx0, rx0 + rw) x [ry0, ry0 + rh) of the
 // w x h prediction unit at plane position (x, y); sample (r, c) of the PU lands in
 // L.tile[(toy + r) * TS + tox + c].  Ends with a barrier.
-DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int x, int y,
-    int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy)
+// The references of one prediction unit (predict_inter, InterPredict.cpp:962-1021):
+// motion vector scaling, warp choice (local / global, Block.cpp:1179-1200) and filters.
+// Returns isCompound.
+DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, int y, int w, int h,
+    int candRow, int candCol, RefSel* R)
 {
-    const int t = threadIdx.x;
     const av1r_frame_hdr& hd = *k.hdr;
     const av1r_mi& info = mi_at(k, candRow, candCol);
     const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
-    const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
     const int isIntrabc = (blk.flags & AV1R_BLK_INTRABC) != 0;
     const int isGlobalMode = blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV;
-    const int sub = plane ? 1 : 0;
-    RefSel R[2];
-    int16_t hf[2][8], vf[2][8];
-    int integer[2];
     int globalValid = 0;
 #pragma unroll
     for (int l = 0; l < 2; l++) {
@@ -610,6 +645,27 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
         R[l].filtX = filter_idx(info.filt, w, 1);
         R[l].filtY = filter_idx(info.filt, h, 0);
         R[l].useWin = !R[l].warp && R[l].xStep == 1024 && R[l].yStep == 1024;
+    }
+    return isCompound;
+}
+
+// predict_inter for the PU-relative region [rx0, rx0 + rw) x [ry0, ry0 + rh) of the
+// w x h prediction unit at plane position (x, y); sample (r, c) of the PU lands in
+// L.tile[(toy + r) * TS + tox + c].  Ends with a barrier.
+DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int x, int y,
+    int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy)
+{
+    const int t = threadIdx.x;
+    const av1r_mi& info = mi_at(k, candRow, candCol);
+    const int sub = plane ? 1 : 0;
+    RefSel R[2];
+    const int isCompound = setup_refs(k, blk, plane, x, y, w, h, candRow, candCol, R);
+    const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
+    int16_t hf[2][8], vf[2][8];
+    int integer[2];
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+        if (l > isCompound) break;
         const int hph = (R[l].startX >> 6) & 15, vph = (R[l].startY >> 6) & 15;
         integer[l] = !hph && !vph;
 #pragma unroll
@@ -633,10 +689,10 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     if (R[0].useWin) load_window(R[0], L.win[0], rx0, ry0, rw, rh);
     if (isCompound && R[1].useWin) load_window(R[1], L.win[1], rx0, ry0, rw, rh);
     __syncthreads();
-    if (R[0].useWin && !integer[0]) hpass(L.win[0], L.hb[0], rw, rh, hf[0], R0);
-    if (R[0].warp) warp_hpass(R[0], L.hb[0], rx0, ry0, rw, rh, x, y, sub, R0);
-    if (isCompound && R[1].useWin && !integer[1]) hpass(L.win[1], L.hb[1], rw, rh, hf[1], R0);
-    if (isCompound && R[1].warp) warp_hpass(R[1], L.hb[1], rx0, ry0, rw, rh, x, y, sub, R0);
+    if (R[0].useWin && !integer[0]) hpass(L.win[0], L.u.hbw[0], rw, rh, hf[0], R0);
+    if (R[0].warp) warp_hpass(R[0], L.u.hbw[0], rx0, ry0, rw, rh, x, y, sub, R0);
+    if (isCompound && R[1].useWin && !integer[1]) hpass(L.win[1], L.u.hbw[1], rw, rh, hf[1], R0);
+    if (isCompound && R[1].warp) warp_hpass(R[1], L.u.hbw[1], rx0, ry0, rw, rh, x, y, sub, R0);
     __syncthreads();
     auto blend = [&](int p0, int p1, int r, int c) {
         int v;
@@ -687,8 +743,8 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     };
     auto sample = [&](int l, int rr, int cc) {
         const int r = ry0 + rr, c = rx0 + cc;
-        return R[l].useWin ? pred_win(L.win[l], L.hb[l], rr, cc, R0, R1, vf[l], integer[l])
-             : R[l].warp   ? warp_v(R[l], L.hb[l], rr, cc, r, c, rw, x, y, sub, R1)
+        return R[l].useWin ? pred_win(L.win[l], L.u.hbw[l], rr, cc, R0, R1, vf[l], integer[l])
+             : R[l].warp   ? warp_v(R[l], L.u.hbw[l], rr, cc, r, c, rw, x, y, sub, R1)
                            : pred_direct(R[l], r, c, R0, R1);
     };
     if ((rw & 3) == 0 && R[0].useWin && (!isCompound || R[1].useWin)) {
@@ -697,8 +753,8 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
         for (int q = t; q < rh * g4; q += 64) {
             const int rr = q / g4, cc = (q - rr * g4) * 4;
             int p0[4], p1[4] = {0, 0, 0, 0};
-            pred_win4(L.win[0], L.hb[0], rr, cc, R0, R1, vf[0], integer[0], p0);
-            if (isCompound) pred_win4(L.win[1], L.hb[1], rr, cc, R0, R1, vf[1], integer[1], p1);
+            pred_win4(L.win[0], L.u.hbw[0], rr, cc, R0, R1, vf[0], integer[0], p0);
+            if (isCompound) pred_win4(L.win[1], L.u.hbw[1], rr, cc, R0, R1, vf[1], integer[1], p1);
             // one blend body, the four samples rotated through it (no unrolled copies)
             int a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
             int b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
@@ -769,12 +825,12 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, i
                     if (R.useWin) {
                         load_window(R, L.win[0], rx0, ry0, rw, rh);
                         __syncthreads();
-                        if (!integer) hpass(L.win[0], L.hb[0], rw, rh, hf, 3);
+                        if (!integer) hpass(L.win[0], L.u.hbw[0], rw, rh, hf, 3);
                         __syncthreads();
                     }
                     for (int q = t; q < rw * rh; q += 64) {
                         const int rr = q / rw, cc = q - rr * rw, i = ry0 + rr, j = rx0 + cc;
-                        int p = R.useWin ? pred_win(L.win[0], L.hb[0], rr, cc, 3, 11, vf, integer)
+                        int p = R.useWin ? pred_win(L.win[0], L.u.hbw[0], rr, cc, 3, 11, vf, integer)
                                          : pred_direct(R, i, j, 3, 11);
                         int m = pass ? mask[j] : mask[i];
                         uint8_t& d = L.tile[(oy + i - TY0) * TS + ox + j - TX0];
@@ -789,55 +845,76 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, i
 }
 
 // One tile (tx, ty) of inter block `bi`: all planes.
-DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L)
+struct PlaneGeo {
+    int baseX, baseY, pw, ph;      // the block in this plane
+    int TX0, TY0, TW, TH;          // the tile, block-relative
+    int candRow, candCol, predW, predH;  // prediction units (Block.cpp:146-174)
+};
+DEV PlaneGeo plane_geo(const KParams& k, const av1r_block& blk, int plane, int tx, int ty)
+{
+    PlaneGeo G;
+    const int bs = blk.mi_size;
+    const int psz = plane_bsize(bs, plane);
+    const int n4w = av1r_num4x4w[psz], n4h = av1r_num4x4h[psz];
+    const int sub = plane ? 1 : 0;
+    G.baseX = (blk.mi_col >> sub) * 4;
+    G.baseY = (blk.mi_row >> sub) * 4;
+    G.pw = n4w * 4;
+    G.ph = n4h * 4;
+    G.TX0 = (tx * TS) >> sub;
+    G.TY0 = (ty * TS) >> sub;
+    G.TW = imin(TS >> sub, G.pw - G.TX0);
+    G.TH = imin(TS >> sub, G.ph - G.TY0);
+    // sub-8x8 chroma may gather several prediction units
+    G.candRow = (blk.mi_row >> sub) << sub;
+    G.candCol = (blk.mi_col >> sub) << sub;
+    G.predW = (av1r_num4x4w[bs] * 4) >> sub;
+    G.predH = (av1r_num4x4h[bs] * 4) >> sub;
+    int someUseIntra = 0;
+    // only a sub-8x8 chroma block can change its PU layout (otherwise the gathered
+    // geometry equals the block's own)
+    if (G.predW != G.pw || G.predH != G.ph || G.candRow != blk.mi_row || G.candCol != blk.mi_col)
+        for (int r = 0; r < (n4h << sub); r++)
+            for (int c = 0; c < (n4w << sub); c++)
+                if (mi_at(k, G.candRow + r, G.candCol + c).ref_frame[0] == AV1R_INTRA_FRAME) someUseIntra = 1;
+    if (someUseIntra) {
+        G.predW = G.pw;
+        G.predH = G.ph;
+        G.candRow = blk.mi_row;
+        G.candCol = blk.mi_col;
+    }
+    return G;
+}
+
+// One tile (tx, ty) of inter block `bi`: all planes.
+DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, unsigned long long* tr)
 {
     const int t = threadIdx.x;
     const av1r_block& blk = k.blocks[bi];
-    const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
-    const int bs = blk.mi_size;
-    const int bw = av1r_num4x4w[bs] * 4, bh = av1r_num4x4h[bs] * 4;
-    for (int plane = 0; plane < 1 + hasChroma * 2; plane++) {
-        const int psz = plane_bsize(bs, plane);
-        const int n4w = av1r_num4x4w[psz], n4h = av1r_num4x4h[psz];
-        const int sub = plane ? 1 : 0;
-        const int baseX = (blk.mi_col >> sub) * 4, baseY = (blk.mi_row >> sub) * 4;
-        const int pw = n4w * 4, ph = n4h * 4;
-        const int TX0 = (tx * TS) >> sub, TY0 = (ty * TS) >> sub;
-        const int TW = imin(TS >> sub, pw - TX0), TH = imin(TS >> sub, ph - TY0);
-        // prediction units (Block.cpp:146-174): sub-8x8 chroma may gather several
-        int candRow = (blk.mi_row >> sub) << sub, candCol = (blk.mi_col >> sub) << sub;
-        int predW = bw >> sub, predH = bh >> sub;
-        int someUseIntra = 0;
-        // only a sub-8x8 chroma block can change its PU layout (otherwise the gathered
-        // geometry equals the block's own)
-        if (predW != pw || predH != ph || candRow != blk.mi_row || candCol != blk.mi_col)
-            for (int r = 0; r < (n4h << sub); r++)
-                for (int c = 0; c < (n4w << sub); c++)
-                    if (mi_at(k, candRow + r, candCol + c).ref_frame[0] == AV1R_INTRA_FRAME) someUseIntra = 1;
-        if (someUseIntra) {
-            predW = pw;
-            predH = ph;
-            candRow = blk.mi_row;
-            candCol = blk.mi_col;
-        }
-        int r = 0;
-        for (int yy = 0; yy < ph; yy += predH) {
-            int c = 0;
-            for (int xx = 0; xx < pw; xx += predW) {
-                const int ix0 = imax(xx, TX0), ix1 = imin(xx + predW, TX0 + TW);
-                const int iy0 = imax(yy, TY0), iy1 = imin(yy + predH, TY0 + TH);
-                if (ix0 < ix1 && iy0 < iy1)
-                    predict_pu(k, blk, L, plane, baseX + xx, baseY + yy, predW, predH, candRow + r, candCol + c,
-                        ix0 - xx, iy0 - yy, ix1 - ix0, iy1 - iy0, xx - TX0, yy - TY0);
-                c++;
+    const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
+    for (int plane = 0; plane < nPl; plane++) {
+        const PlaneGeo G = plane_geo(k, blk, plane, tx, ty);
+        {
+            int r = 0;
+            for (int yy = 0; yy < G.ph; yy += G.predH) {
+                int c = 0;
+                for (int xx = 0; xx < G.pw; xx += G.predW) {
+                    const int ix0 = imax(xx, G.TX0), ix1 = imin(xx + G.predW, G.TX0 + G.TW);
+                    const int iy0 = imax(yy, G.TY0), iy1 = imin(yy + G.predH, G.TY0 + G.TH);
+                    if (ix0 < ix1 && iy0 < iy1)
+                        predict_pu(k, blk, L, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
+                            G.candCol + c, ix0 - xx, iy0 - yy, ix1 - ix0, iy1 - iy0, xx - G.TX0, yy - G.TY0);
+                    c++;
+                }
+                r++;
             }
-            r++;
         }
-        if (blk.motion_mode == AV1R_OBMC_CAUSAL) obmc(k, blk, L, plane, baseX, baseY, predW, predH, TX0, TY0, TW, TH);
+        if (blk.motion_mode == AV1R_OBMC_CAUSAL)
+            obmc(k, blk, L, plane, G.baseX, G.baseY, G.predW, G.predH, G.TX0, G.TY0, G.TW, G.TH);
         const DevPlane& dst = k.cur.pl[plane];
-        for (int q = t; q < TW * TH; q += 64) {
-            int i = q / TW, j = q - i * TW;
-            px(dst, baseX + TX0 + j, baseY + TY0 + i) = L.tile[i * TS + j];
+        for (int q = t; q < G.TW * G.TH; q += 64) {
+            int i = q / G.TW, j = q - i * G.TW;
+            px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[i * TS + j];
         }
         __syncthreads();
     }
@@ -921,25 +998,75 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
 __constant__ KParams g_kp[AV1R_KP_SLOTS][AV1R_MAX_BATCH];
 
 // Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
-// counts at this level; tab[n + 1 + s]: offset of frame s's level in its item list).
-extern "C" __global__ __launch_bounds__(64) void k_level(int slot, const uint32_t* __restrict__ tab, int n)
+// counts of this kind at this level; tab[n + 1 + s]: offset of frame s's items in its
+// item list).  Returns the frame's parameters and the work item.
+DEV const WorkItem& level_item(int slot, const uint32_t* __restrict__ tab, int n, const KParams*& kp, int& s)
 {
-    constexpr size_t kLds = sizeof(TbLds) > sizeof(InterLds) ? sizeof(TbLds) : sizeof(InterLds);
-    __shared__ __align__(16) uint8_t smem[kLds];
     const uint32_t b = blockIdx.x;
-    int s = 0;
-    while (s + 1 < n && b >= tab[s + 1]) s++;
-    const KParams& k = g_kp[slot][s];
-    const uint32_t it = k.items[tab[n + 1 + s] + (b - tab[s])];
-    const uint32_t kind = AV1R_ITEM_KIND(it), idx = AV1R_ITEM_INDEX(it);
-    if (kind == AV1R_ITEM_TB) tb_item(k, idx, *reinterpret_cast<TbLds*>(smem));
-    else if (kind == AV1R_ITEM_INTER) inter_tile(k, idx >> 4, idx & 3, (idx >> 2) & 3, *reinterpret_cast<InterLds*>(smem));
-    else ii_item(k, idx, *reinterpret_cast<TbLds*>(smem));
+    // frame of this workgroup: the number of frames whose items all precede b (one
+    // vector load of the prefix table + a ballot instead of a dependent scan)
+    const uint32_t pre = (int)threadIdx.x + 1 < n ? tab[threadIdx.x + 1] : 0xffffffffu;
+    s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    kp = &g_kp[slot][s];
+    return kp->items[tab[n + 1 + s] + (b - tab[s])];
 }
 
-void launch_k_level(int slot, const uint32_t* tab, int n, unsigned items, hipStream_t s)
+// One launch per dependency level and kernel: inter tiles (k_inter) and transform blocks +
+// inter-intra blends (k_tb) have their own kernels, so each gets the register budget and
+// LDS of its own work (one 64-lane workgroup per item).
+extern "C" __global__ __launch_bounds__(64) void k_tb(int slot, const uint32_t* __restrict__ tab, int n,
+    unsigned long long* trace, uint32_t traceBase)
 {
-    hipLaunchKernelGGL(k_level, dim3(items), dim3(64), 0, s, slot, tab, n);
+    __shared__ TbLds L;
+#ifdef AV1R_TRACE
+    unsigned long long* tr = trace ? trace + (size_t)(traceBase + blockIdx.x) * 8 : nullptr;
+#else
+    unsigned long long* tr = nullptr;
+    (void)trace;
+    (void)traceBase;
+#endif
+    trace_stamp(tr, 2);
+    const KParams* kp;
+    int s;
+    const WorkItem& wi = level_item(slot, tab, n, kp, s);
+    if (tr && threadIdx.x == 0) {
+        tr[0] = wi.code;
+        tr[1] = ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred;
+    }
+    trace_stamp(tr, 3);
+    // inter-intra blends share the launch (and the LDS layout) of the level's TBs
+    if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) ii_item(*kp, AV1R_ITEM_INDEX(wi.code), L);
+    else tb_item(*kp, wi, L, tr);
+    trace_stamp(tr, 5);
+}
+
+extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_t* __restrict__ tab, int n,
+    unsigned long long* trace, uint32_t traceBase)
+{
+    __shared__ InterLds L;
+#ifdef AV1R_TRACE
+    unsigned long long* tr = trace ? trace + (size_t)(traceBase + blockIdx.x) * 8 : nullptr;
+#else
+    unsigned long long* tr = nullptr;
+    (void)trace;
+    (void)traceBase;
+#endif
+    trace_stamp(tr, 2);
+    const KParams* kp;
+    int s;
+    const WorkItem& wi = level_item(slot, tab, n, kp, s);
+    const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
+    if (tr && threadIdx.x == 0) tr[0] = wi.code;
+    trace_stamp(tr, 3);
+    inter_tile(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
+    trace_stamp(tr, 5);
+}
+
+void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
+    uint32_t traceBase, hipStream_t s)
+{
+    if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
+    else hipLaunchKernelGGL(k_tb, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
 }
 
 namespace {

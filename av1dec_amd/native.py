@@ -24,16 +24,20 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, jobs=3):
-    """Compile every HIP/C++ source for gfx950 and link libav1r.so in-tree."""
-    if not force and not _stale():
+def build(force=False, jobs=3, out=None, defines=()):
+    """Compile every HIP/C++ source for gfx950 and link libav1r.so in-tree (or `out`, e.g.
+    a -DAV1R_TRACE build for tools/trace_run.py)."""
+    lib_path = out or LIB
+    if out is None and not defines and not force and not _stale():
         return LIB
     os.makedirs(BUILD, exist_ok=True)
+    tag = "" if out is None else "_" + os.path.splitext(os.path.basename(out))[0]
     procs, objs = [], []
     for s in SRCS:
         src = os.path.join(PKG, "csrc", s)
-        obj = os.path.join(BUILD, os.path.splitext(s)[0] + ".o")
-        cmd = [HIPCC] + FLAGS + (["-x", "hip"] if s.endswith(".cpp") else []) + ["-c", src, "-o", obj]
+        obj = os.path.join(BUILD, os.path.splitext(s)[0] + tag + ".o")
+        cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + (["-x", "hip"] if s.endswith(".cpp") else []) \
+            + ["-c", src, "-o", obj]
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
         if len(procs) >= jobs:
@@ -42,10 +46,10 @@ def build(force=False, jobs=3):
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    tmp = LIB + ".tmp"
+    tmp = lib_path + ".tmp"
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 _lib = None
@@ -55,9 +59,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB):
-        raise RuntimeError(f"{LIB} is missing: run av1dec_amd.native.build() (hipcc, gfx950)")
-    l = C.CDLL(LIB)
+    # AV1R_LIB: an alternative build of the same library (A/B measurements)
+    path = os.environ.get("AV1R_LIB", LIB)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run av1dec_amd.native.build() (hipcc, gfx950)")
+    l = C.CDLL(path)
     vp, i, u8p = C.c_void_p, C.c_int, C.c_void_p
     l.av1r_create.argtypes = [i, C.POINTER(vp)]
     l.av1r_destroy.argtypes = [vp]

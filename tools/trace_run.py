@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Per-item timeline of the recon kernels (debug): decodes a few frames of one synthetic
+stream with AV1R_TRACE_FILE set and summarises where each work item's time goes.
+Run on the GPU box:  python3 tools/trace_run.py [frames] [out.bin]"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
+
+
+def run(nfr, path):
+    if os.path.exists(path):
+        os.remove(path)
+    os.environ["AV1R_TRACE_FILE"] = path
+    # the timeline needs the -DAV1R_TRACE build (av1dec_amd.native.build(out=..., defines=["AV1R_TRACE"]))
+    os.environ.setdefault("AV1R_LIB", os.path.join(ROOT, "av1dec_amd", "_build", "libav1r_trace.so"))
+    import pysynth
+    from av1dec_amd import Decoder
+    frames = pysynth.stream(1920, 1080, nfr, 0x5EED1000, sb128=True)
+    d = Decoder(0, keep_stages=False)
+    d.set_discard_output(True)
+    hs = [d.prepare(f) for f in frames]
+    for h in hs:
+        d.decode_prepared(h)
+    d.synchronize()
+    d.close()
+
+
+def summarise(path):
+    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    code, misc, t0, t1, t2, t3, lvl = a[:, 0], a[:, 1], a[:, 2], a[:, 3], a[:, 4], a[:, 5], a[:, 6]
+    kind = code >> 30
+    pred = misc & 0xff
+    txs = (misc >> 8) & 0xff
+    # frames: level index resets to 0
+    starts = np.flatnonzero((lvl == 0) & np.r_[True, lvl[1:] != lvl[:-1]][: len(lvl)])
+    print(f"{len(a)} items, {len(starts)} frame(s)")
+    us = lambda x: x / 100.0  # 100 MHz counter -> us
+    for name, m in (("TB intra", (kind == 0) & (pred == 0)), ("TB inter", (kind == 0) & (pred == 2)),
+                    ("inter tile", kind == 1), ("ii blend", kind == 2)):
+        if not m.any():
+            continue
+        d_item = us(t1[m] - t0[m]); d_pred = us(np.where(kind[m] == 0, t2[m] - t1[m], 0)); d_all = us(t3[m] - t0[m])
+        print(f"{name:11s} n={m.sum():7d}  item-load p50 {np.median(d_item):6.2f}  pred p50 {np.median(d_pred):6.2f}"
+              f"  total p50 {np.median(d_all):6.2f} p90 {np.percentile(d_all, 90):6.2f} max {d_all.max():7.2f} us")
+    # inter tiles by motion mode / compound: setup+plane-0 prediction, plane 0 total, rest
+    m = kind == 1
+    t7 = a[:, 7]
+    mm_mode = (misc >> 16) & 0xf
+    comp = (misc >> 20) & 1
+    for mode in np.unique(mm_mode[m]):
+        for cp in (0, 1):
+            mm = m & (mm_mode == mode) & (comp == cp)
+            if not mm.any():
+                continue
+            print(f"   inter tile motion {mode} compound {cp}: n={mm.sum():6d} item {np.median(us(t1[mm]-t0[mm])):5.2f}"
+                  f" luma-pred {np.median(us(t2[mm]-t1[mm])):5.2f} luma-store {np.median(us(t7[mm]-t2[mm])):5.2f}"
+                  f" chroma {np.median(us(t3[mm]-t7[mm])):5.2f} total {np.median(us(t3[mm]-t0[mm])):5.2f}")
+    # per tx size, intra TBs
+    m = (kind == 0) & (pred == 0)
+    for ts in np.unique(txs[m]):
+        mm = m & (txs == ts)
+        print(f"   intra tx_size {ts:2d}: n={mm.sum():6d} total p50 {np.median(us(t3[mm]-t0[mm])):6.2f} pred {np.median(us(t2[mm]-t1[mm])):6.2f} resid {np.median(us(t3[mm]-t2[mm])):6.2f}")
+    # level timeline of the last frame: start of first item -> end of last item per level
+    f0 = starts[-1]
+    sl = slice(f0, len(a))
+    L = lvl[sl]
+    spans = []
+    for l in np.unique(L):
+        mm = L == l
+        s0, e0 = t0[sl][mm].min(), t3[sl][mm].max()
+        spans.append((l, us(e0 - s0), mm.sum()))
+    gaps = [us(t0[sl][L == l2].min() - t3[sl][L == l1].max()) for l1, l2 in zip(np.unique(L)[:-1], np.unique(L)[1:])]
+    print("last frame: levels", len(spans), "sum of level spans %.1f us, sum of gaps %.1f us (median gap %.2f)"
+          % (sum(x[1] for x in spans), sum(gaps), np.median(gaps) if gaps else 0))
+
+
+if __name__ == "__main__":
+    nfr = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "trace.bin")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    run(nfr, path)
+    summarise(path)
