@@ -30,9 +30,11 @@ void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned ite
     uint32_t traceBase, hipStream_t s);
 int kp_upload(int device, const KParams* host, int n, hipStream_t s);
 int kp_release(int device, int slot, hipStream_t s);
-void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
-void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
-void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
+void launch_k_lf(int slot, int n, int pass, int maxUnits, hipStream_t s);
+void launch_k_cdef(int slot, int n, int maxMiCols, int maxMiRows, hipStream_t s);
+void launch_k_lr(int slot, int n, int maxW, int maxH, hipStream_t s);
+int kpf_upload(int device, const KParams* host, int n, hipStream_t s);
+int kpf_release(int device, int slot, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 
 namespace {
@@ -609,7 +611,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             total[l * 2 + kk] = t[n];
         }
     HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
-    const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
 
     if (lc->timing) {
@@ -672,12 +673,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
     // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place, 2 passes
-    launch_k_lf(dk, n, 0, maxUnits, st);
-    launch_k_lf(dk, n, 1, maxUnits, st);
+    const int fslot = kpf_upload(lc->device, hk, n, st);
+    if (fslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
+    launch_k_lf(fslot, n, 0, maxUnits, st);
+    launch_k_lf(fslot, n, 1, maxUnits, st);
     if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
     // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
-    launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
+    launch_k_cdef(fslot, n, maxMiCols, maxMiRows, st);
     if (snap) {
         frame_ref(jobs[0].C);
         frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
@@ -685,7 +688,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
     // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
-    if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
+    if (anyLr) launch_k_lr(fslot, n, maxW, maxH, st);
+    if (kpf_release(lc->device, fslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(M.done, st));

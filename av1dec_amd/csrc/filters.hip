@@ -14,6 +14,10 @@
 //           (:284-479) with the stripe/unit geometry of :33-189; the 3-pixel border
 //           extension (:196-198) is coordinate clamping.
 #include "av1r_dev.h"
+#include "kp_const.h"
+
+// Frame parameters of a launch: constant-address-space slots (kp_const.h).
+AV1R_KP_TABLE(g_kpf, kpf_upload, kpf_release)
 
 // ------------------------------------------------------------------------------------
 // Deblocking
@@ -113,9 +117,9 @@ DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int bl
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
-extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* __restrict__ kps, int pass)
+extern "C" __global__ __launch_bounds__(256) void k_lf(int slot, int pass)
 {
-    const KParams& k = kps[blockIdx.y];  // frame of this launch row
+    const KParams& k = g_kpf[slot][blockIdx.y];  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
     if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
     const int planeMask = 1 | (hd.lf_level[2] ? 2 : 0) | (hd.lf_level[3] ? 4 : 0);
@@ -196,6 +200,7 @@ struct CdefLds {
     uint8_t dir[64];               // yDir
     int16_t pri[64];               // adjusted luma primary strength
     uint8_t filt[64];              // block is filtered (not skip)
+    int16_t offY[64][6], offC[64][6];  // tap offsets in the staged tiles (cdef_px)
 };
 
 // partial[d][k] of cdefDirection (Cdef.cpp:203-261) for one line k of direction d, summed
@@ -228,55 +233,76 @@ DEV int cdef_cost(const CdefLds& L, int bx, int by)
         }
         return cost;
     }
-    // odd directions: 11 lines; the centre 5 weigh Div_Table[8], the outer pairs 2j+2
+    // odd directions: 11 lines; the centre 5 weigh Div_Table[8], the outer pairs 2j+2.
+    // Line k of row i holds the pixels j with d1: i + j/2 == k, d3: 3 + i - j/2 == k,
+    // d5: 3 - i/2 + j == k, d7: i/2 + j == k (all indices compile-time after unrolling).
 #pragma unroll
     for (int k = 0; k < 11; k++) {
         int s = 0;
 #pragma unroll
-        for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int kk = d == 1 ? i + j / 2 : d == 3 ? 3 + i - j / 2 : d == 5 ? 3 - i / 2 + j : i / 2 + j;
-                if (kk == k) s += px8(i, j);
+        for (int i = 0; i < 8; i++) {
+            if (d == 1 || d == 3) {
+                const int h = d == 1 ? k - i : 3 + i - k;  // j / 2
+                if (h >= 0 && h <= 3) s += px8(i, 2 * h) + px8(i, 2 * h + 1);
+            } else {
+                const int j = d == 5 ? k - 3 + i / 2 : k - i / 2;
+                if (j >= 0 && j <= 7) s += px8(i, j);
             }
+        }
         const int w = (k >= 3 && k <= 7) ? av1r_cdef_div_table[8] : av1r_cdef_div_table[2 * (k < 3 ? k : 10 - k) + 2];
         cost += s * s * w;
     }
     return cost;
 }
 
-// cdefFilter (Cdef.cpp:158-198) for one pixel (X, Y) of the plane, reading the staged tile
-// t (row stride ts, origin (ox, oy) = plane coordinate of t[0][0])
-DEV int cdef_px(const KParams& k, const uint8_t* t, int ts, int ox, int oy, int sub, int X, int Y, int priStr,
-    int secStr, int damping, int dir)
+// cdefFilter (Cdef.cpp:158-198) for one pixel at tile offset p of the staged tile t.
+// off[s * 2 + kk] = tile offset of tap kk of direction dir (s = 0), dir - 2 (s = 1),
+// dir + 2 (s = 2); taps at -off and +off.  Per-block constants are folded: the damping
+// shifts (constrain, :111-118) and the primary tap weights.  `check`: the region touches
+// the frame edge, so each tap is tested against is_inside_filter_region (X, Y = plane
+// position of the pixel, limX / limY = plane extent of the mi grid).
+template <bool check>
+DEV int cdef_px(const uint8_t* t, int p, const int16_t* off, int pri, int sec, int damping, int X, int Y, int ts,
+    int limX, int limY)
 {
-    const int x = t[(Y - oy) * ts + X - ox];
+    const int x = t[p];
     int sum = 0, mx = x, mn = x;
+    const int adjP = imax(0, damping - floor_log2(imax(pri, 1)));
+    const int adjS = imax(0, damping - floor_log2(imax(sec, 1)));
+    const int tap0 = (pri & 1) ? 3 : 4, tap1 = (pri & 1) ? 3 : 2;  // Cdef_Pri_Taps
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++)
+    for (int s = 0; s < 3; s++)
 #pragma unroll
-        for (int sgn = -1; sgn <= 1; sgn += 2)
+        for (int kk = 0; kk < 2; kk++) {
+            const int o = off[s * 2 + kk];
 #pragma unroll
-            for (int s = 0; s < 3; s++) {
-                int d = s == 0 ? dir : ((dir + (s == 1 ? -2 : 2)) & 7);
-                int yy = Y + sgn * av1r_cdef_directions[d][kk][0];
-                int xx = X + sgn * av1r_cdef_directions[d][kk][1];
-                int cr = (yy << sub) >> 2, cc = (xx << sub) >> 2;  // is_inside_filter_region
-                if (!(cc >= 0 && cc < k.mi_cols && cr >= 0 && cr < k.mi_rows)) continue;
-                int p = t[(yy - oy) * ts + xx - ox];
-                if (s == 0) sum += av1r_cdef_pri_taps[priStr & 1][kk] * constrain(p - x, priStr, damping);
-                else sum += av1r_cdef_sec_taps[priStr & 1][kk] * constrain(p - x, secStr, damping);
-                mx = imax(p, mx);
-                mn = imin(p, mn);
+            for (int sg = 0; sg < 2; sg++) {
+                const int oo = sg ? o : -o;
+                if (check) {
+                    // tile offset -> plane position of the tap
+                    const int dy = (oo + 2 * ts + 2) / ts - 2;  // |dx|, |dy| <= 2
+                    const int dx = oo - dy * ts;
+                    const int xx = X + dx, yy = Y + dy;
+                    if (!(xx >= 0 && xx < limX && yy >= 0 && yy < limY)) continue;
+                }
+                const int q = t[p + oo];
+                const int d = q - x, ad = iabs(d);
+                const int thr = s == 0 ? pri : sec, adj = s == 0 ? adjP : adjS;
+                const int v = imin(ad, imax(0, thr - (ad >> adj)));  // constrain (0 for thr 0)
+                const int w = s == 0 ? (kk ? tap1 : tap0) : (kk ? 1 : 2);  // Cdef_Sec_Taps = {2, 1}
+                sum += w * (d < 0 ? -v : v);
+                mx = imax(q, mx);
+                mn = imin(q, mn);
             }
+        }
     return CLIP3(mn, mx, x + ((8 + sum - (sum < 0)) >> 4));
 }
 
 // grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.cur, writes k.cdef
-extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* __restrict__ kps)
+extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
 {
     __shared__ CdefLds L;
-    const KParams& k = kps[blockIdx.z];
+    const KParams& k = g_kpf[slot][blockIdx.z];
     const int t = threadIdx.x;
     const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;  // mi units
     if (r0 >= k.mi_rows || c0 >= k.mi_cols) return;
@@ -359,32 +385,53 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* __restri
         const int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
         L.dir[t] = (uint8_t)yDir;
         L.pri[t] = (int16_t)(var ? (priStr * (4 + varStr) + 8) >> 4 : 0);
+        // tap offsets: luma direction (0 when the primary strength is 0), chroma direction
+        // Cdef_Uv_Dir (identity for 4:2:0; 0 when the chroma primary strength is 0)
+        const int dy0 = priStr == 0 ? 0 : yDir, dc0 = h.cdef_uv_pri[idx] == 0 ? 0 : av1r_cdef_uv_dir420[yDir];
+#pragma unroll
+        for (int s = 0; s < 3; s++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                const int dl = s == 0 ? dy0 : ((dy0 + (s == 1 ? -2 : 2)) & 7);
+                const int dc = s == 0 ? dc0 : ((dc0 + (s == 1 ? -2 : 2)) & 7);
+                L.offY[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dl][kk][0] * (CD_LW + 4) + av1r_cdef_directions[dl][kk][1]);
+                L.offC[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dc][kk][0] * (CD_CW + 4) + av1r_cdef_directions[dc][kk][1]);
+            }
     }
     __syncthreads();
     // luma
-    const int yPri = h.cdef_y_pri[idx], ySec = h.cdef_y_sec[idx];
+    const int ySec = h.cdef_y_sec[idx];
+    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
+    const bool edge = x0 < CD_H || y0 < CD_H || x0 + 64 + CD_H > limX || y0 + 64 + CD_H > limY;
     for (int q = t; q < rows4 * 4 * cols4 * 4; q += 256) {
         const int i = q / (cols4 * 4), j = q - i * (cols4 * 4);
         const int b = (i >> 3) * 8 + (j >> 3);
-        const int X = x0 + j, Y = y0 + i;
+        const int p = (CD_H + i) * (CD_LW + 4) + CD_H + j;
         int v;
-        if (!L.filt[b]) v = L.y[CD_H + i][CD_H + j];
-        else v = cdef_px(k, &L.y[0][0], CD_LW + 4, x0 - CD_H, y0 - CD_H, 0, X, Y, L.pri[b], ySec,
-                         h.cdef_damping, yPri == 0 ? 0 : L.dir[b]);
-        px(k.cdef.pl[0], X, Y) = (uint8_t)v;
+        if (!L.filt[b]) v = (&L.y[0][0])[p];
+        else if (edge)
+            v = cdef_px<true>(&L.y[0][0], p, L.offY[b], L.pri[b], ySec, h.cdef_damping, x0 + j, y0 + i, CD_LW + 4, limX, limY);
+        else
+            v = cdef_px<false>(&L.y[0][0], p, L.offY[b], L.pri[b], ySec, h.cdef_damping, 0, 0, CD_LW + 4, 0, 0);
+        px(k.cdef.pl[0], x0 + j, y0 + i) = (uint8_t)v;
     }
-    // chroma (4:2:0: Cdef_Uv_Dir is the identity)
+    // chroma
     const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
+    const int cx0 = x0 / 2, cy0 = y0 / 2, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
+    const bool cedge = cx0 < CD_H || cy0 < CD_H || cx0 + 32 + CD_H > climX || cy0 + 32 + CD_H > climY;
     for (int q = t; q < 2 * rows4 * 2 * cols4 * 2; q += 256) {
         const int pl = q >= rows4 * 2 * cols4 * 2, e = q - pl * rows4 * 2 * cols4 * 2;
         const int i = e / (cols4 * 2), j = e - i * (cols4 * 2);
         const int b = (i >> 2) * 8 + (j >> 2);
-        const int X = x0 / 2 + j, Y = y0 / 2 + i;
+        const uint8_t* tile = &L.uv[pl][0][0];
+        const int p = (CD_H + i) * (CD_CW + 4) + CD_H + j;
         int v;
-        if (!L.filt[b]) v = L.uv[pl][CD_H + i][CD_H + j];
-        else v = cdef_px(k, &L.uv[pl][0][0], CD_CW + 4, x0 / 2 - CD_H, y0 / 2 - CD_H, 1, X, Y, uvPri, uvSec,
-                         h.cdef_damping - 1, uvPri == 0 ? 0 : av1r_cdef_uv_dir420[L.dir[b]]);
-        px(k.cdef.pl[1 + pl], X, Y) = (uint8_t)v;
+        if (!L.filt[b]) v = tile[p];
+        else if (cedge)
+            v = cdef_px<true>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j, cy0 + i, CD_CW + 4, climX, climY);
+        else
+            v = cdef_px<false>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, 0, 0, CD_CW + 4, 0, 0);
+        px(k.cdef.pl[1 + pl], cx0 + j, cy0 + i) = (uint8_t)v;
     }
 }
 
@@ -454,11 +501,11 @@ DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, in
 
 // one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
 // frame (k.cdef) and the deblocked frame (k.cur, stripe rows), writes k.lrout.
-extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* __restrict__ kps)
+extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-    const KParams& k = kps[blockIdx.z / 3];
+    const KParams& k = g_kpf[slot][blockIdx.z / 3];
     if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
     const int plane = blockIdx.z % 3, sub = plane ? 1 : 0;
     const DevPlane C = k.cdef.pl[plane];
@@ -599,19 +646,19 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 
 // ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
-void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
+void launch_k_lf(int slot, int n, int pass, int maxUnits, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
+    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, slot, pass);
 }
-void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
+void launch_k_cdef(int slot, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
+    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, slot);
 }
-void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
+void launch_k_lr(int slot, int n, int maxW, int maxH, hipStream_t s)
 {
     // tile rows: luma stripes (64 rows from -8) in halves; chroma stripes whole
     const int tilesY = 2 * ((maxH + 8 + 63) / 64);
-    hipLaunchKernelGGL(k_lr, dim3((maxW + LR_TW - 1) / LR_TW, tilesY, 3 * n), dim3(256), 0, s, kps);
+    hipLaunchKernelGGL(k_lr, dim3((maxW + LR_TW - 1) / LR_TW, tilesY, 3 * n), dim3(256), 0, s, slot);
 }
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s)
 {

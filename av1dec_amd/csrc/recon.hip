@@ -15,10 +15,9 @@
 //            Inter-intra items: the intra half of an inter-intra block, blended in place.
 // The host (av1r_host.cpp) orders launches by dependency level so every pixel a work
 // item reads was finalised by an earlier launch.
-#include <mutex>
-
 #include "av1r_dev.h"
 #include "intra_dev.h"
+#include "kp_const.h"
 #include "txfm_dev.h"
 
 // Debug timeline (AV1R_TRACE_FILE): lane 0 of each item stamps the 100 MHz real-time
@@ -990,12 +989,8 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
 // One launch per dependency level: every work item of the level (inter tiles, inter-
 // intra blends, transform blocks) is one 64-lane workgroup.
 // ---------------------------------------------------------------------------------
-// Per-launch frame parameters live in the constant address space so that every field a
-// work item reads is a scalar load (a KParams array behind a plain global pointer costs
-// ~100 VGPRs of hoisted vector loads and halves occupancy).  Launch batches rotate over
-// AV1R_KP_SLOTS slots of AV1R_MAX_BATCH frames; a slot is rewritten only after the
-// previous batch that used it has finished (event per slot, waited for on the GPU).
-__constant__ KParams g_kp[AV1R_KP_SLOTS][AV1R_MAX_BATCH];
+// Frame parameters of a launch: constant-address-space slots (kp_const.h).
+AV1R_KP_TABLE(g_kp, kp_upload, kp_release)
 
 // Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
 // counts of this kind at this level; tab[n + 1 + s]: offset of frame s's items in its
@@ -1067,41 +1062,4 @@ void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned ite
 {
     if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
     else hipLaunchKernelGGL(k_tb, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
-}
-
-namespace {
-struct KpSlots {
-    std::mutex m;
-    int next = 0;
-    hipEvent_t ev[AV1R_KP_SLOTS] = {};
-    bool used[AV1R_KP_SLOTS] = {};
-};
-KpSlots g_slots[64];  // per device
-}  // namespace
-
-// Claim a slot on `device`, order the stream after its previous user, and copy the n
-// frame parameters (pinned host memory) into it.  Returns the slot or -1.
-int kp_upload(int device, const KParams* host, int n, hipStream_t s)
-{
-    if (device < 0 || device >= 64 || n < 1 || n > AV1R_MAX_BATCH) return -1;
-    KpSlots& S = g_slots[device];
-    std::lock_guard<std::mutex> lock(S.m);
-    const int slot = S.next;
-    S.next = (S.next + 1) % AV1R_KP_SLOTS;
-    if (!S.ev[slot] && hipEventCreateWithFlags(&S.ev[slot], hipEventDisableTiming) != hipSuccess) return -1;
-    if (S.used[slot] && hipStreamWaitEvent(s, S.ev[slot], 0) != hipSuccess) return -1;
-    void* base = nullptr;
-    if (hipGetSymbolAddress(&base, HIP_SYMBOL(g_kp)) != hipSuccess) return -1;
-    uint8_t* dst = static_cast<uint8_t*>(base) + (size_t)slot * AV1R_MAX_BATCH * sizeof(KParams);
-    if (hipMemcpyAsync(dst, host, sizeof(KParams) * n, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
-    return slot;
-}
-
-// The last launch reading `slot` has been queued on `s`.
-int kp_release(int device, int slot, hipStream_t s)
-{
-    KpSlots& S = g_slots[device];
-    std::lock_guard<std::mutex> lock(S.m);
-    S.used[slot] = true;
-    return hipEventRecord(S.ev[slot], s) == hipSuccess ? 0 : -1;
 }
