@@ -77,6 +77,23 @@ DEV int imax(int a, int b) { return a > b ? a : b; }
 DEV int floor_log2_u64(uint64_t x) { return x ? 63 - __builtin_clzll(x) : -1; }
 DEV int floor_log2(int x) { return x > 0 ? 31 - __builtin_clz((unsigned)x) : -1; }
 
+// Cooperating lanes of one work item: the whole workgroup (NT = blockDim.x) or one wave
+// (NT = 64 inside a larger workgroup, one item per wave: wave-level synchronisation --
+// a wave's LDS operations complete in order, so only the compiler must not reorder).
+template <int NT>
+DEV int coop_lane() { return NT == 64 ? (int)(threadIdx.x & 63) : (int)threadIdx.x; }
+template <int NT>
+DEV void coop_sync()
+{
+    if (NT == 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 DEV const av1r_mi& mi_at(const KParams& k, int row, int col) { return k.mi[(size_t)row * k.mi_stride + col]; }
 DEV int plane_bsize(int bs, int plane) { return plane ? av1r_ss420[bs] : bs; }
 DEV uint8_t& px(const DevPlane& p, int x, int y) { return p.p[(size_t)y * p.stride + x]; }

@@ -55,9 +55,9 @@ struct Upload {
 };
 
 struct Level {
-    // items [off, off + cnt) per kernel: [0] inter tiles (k_inter), [1] inter-intra blends
-    // then transform blocks (k_tb)
-    uint32_t off[2] = {}, cnt[2] = {};
+    // items [off, off + cnt): [0] inter tiles (k_inter); k_tb's [1] large items (inter-intra
+    // blends, TBs with a side >= 32: a workgroup each) and [2] small TBs (one per wave)
+    uint32_t off[3] = {}, cnt[3] = {};
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -404,10 +404,21 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
     c->items.clear();
     c->levels.assign(nl, Level());
     for (size_t l = 0; l < nl; l++) {
+        // order: inter tiles, then k_tb's large items, then its small ones
+        auto large = [&](uint32_t code) {
+            if (AV1R_ITEM_KIND(code) != AV1R_ITEM_TB) return true;
+            const av1r_tb& t = b->tbs[AV1R_ITEM_INDEX(code)];
+            return av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
+        };
+        std::vector<uint32_t>& T = c->lvT[l];
+        std::stable_partition(T.begin(), T.end(), large);
+        const uint32_t nLargeT = (uint32_t)std::count_if(T.begin(), T.end(), large);
         c->levels[l].off[0] = (uint32_t)c->items.size();
         c->levels[l].cnt[0] = (uint32_t)c->lvP[l].size();
         c->levels[l].off[1] = c->levels[l].off[0] + c->levels[l].cnt[0];
-        c->levels[l].cnt[1] = (uint32_t)(c->lvB[l].size() + c->lvT[l].size());
+        c->levels[l].cnt[1] = (uint32_t)c->lvB[l].size() + nLargeT;
+        c->levels[l].off[2] = c->levels[l].off[1] + c->levels[l].cnt[1];
+        c->levels[l].cnt[2] = (uint32_t)T.size() - nLargeT;
         for (auto* v : {&c->lvP, &c->lvB, &c->lvT}) {
             for (uint32_t code : (*v)[l]) {
                 WorkItem w;
@@ -576,10 +587,11 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         maxH = std::max(maxH, h->frame_height);
         anyLr |= h->uses_lr != 0;
     }
-    // launch metadata: [KParams x n][per level and item kind: n + 1 prefix counts, n item offsets]
-    const size_t tabW = 2 * (size_t)n + 1;
+    // launch metadata: [KParams x n][per level: k_inter table (n + 1 prefix counts, n item
+    // offsets), k_tb table (large prefix, small prefix, large offsets, small offsets)]
+    const size_t tabI = 2 * (size_t)n + 1, tabT = 4 * (size_t)n + 2, tabW = tabI + tabT;
     const size_t kBytes = align256(sizeof(KParams) * n);
-    const size_t need = kBytes + 4 * tabW * 2 * std::max<size_t>(nLevels, 1);
+    const size_t need = kBytes + 4 * tabW * std::max<size_t>(nLevels, 1);
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % 2;
     if (M.pending) {
@@ -597,19 +609,26 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     KParams* hk = reinterpret_cast<KParams*>(M.host);
     for (int i = 0; i < n; i++) hk[i] = jobs[i].k;
     uint32_t* tab = reinterpret_cast<uint32_t*>(M.host + kBytes);
-    std::vector<uint32_t> total(nLevels * 2, 0);
-    for (size_t l = 0; l < nLevels; l++)
-        for (int kk = 0; kk < 2; kk++) {
-            uint32_t* t = tab + (l * 2 + kk) * tabW;
-            t[0] = 0;
-            for (int i = 0; i < n; i++) {
-                const auto& lv = jobs[i].P->levels;
-                const uint32_t cnt = l < lv.size() ? lv[l].cnt[kk] : 0;
-                t[i + 1] = t[i] + cnt;
-                t[n + 1 + i] = l < lv.size() ? lv[l].off[kk] : 0;
-            }
-            total[l * 2 + kk] = t[n];
+    // total[l * 3 + kind]: items of the level's inter / large / small lists
+    std::vector<uint32_t> total(nLevels * 3, 0);
+    for (size_t l = 0; l < nLevels; l++) {
+        uint32_t* ti = tab + l * tabW;       // k_inter
+        uint32_t* tt = ti + tabI;            // k_tb
+        ti[0] = tt[0] = tt[n + 1] = 0;
+        for (int i = 0; i < n; i++) {
+            const auto& lv = jobs[i].P->levels;
+            const bool has = l < lv.size();
+            ti[i + 1] = ti[i] + (has ? lv[l].cnt[0] : 0);
+            ti[n + 1 + i] = has ? lv[l].off[0] : 0;
+            tt[i + 1] = tt[i] + (has ? lv[l].cnt[1] : 0);
+            tt[n + 2 + i] = tt[n + 1 + i] + (has ? lv[l].cnt[2] : 0);
+            tt[2 * n + 2 + i] = has ? lv[l].off[1] : 0;
+            tt[3 * n + 2 + i] = has ? lv[l].off[2] : 0;
         }
+        total[l * 3 + 0] = ti[n];
+        total[l * 3 + 1] = tt[n];
+        total[l * 3 + 2] = tt[2 * n + 1];
+    }
     HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
 
@@ -649,13 +668,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     unsigned long long* trace = lc->traceFile ? lc->traceDev : nullptr;
     uint32_t traceBase = 0;
-    for (size_t l = 0; l < nLevels; l++)
-        for (int kk = 0; kk < 2; kk++) {
-            const uint32_t cnt = total[l * 2 + kk];
-            if (!cnt) continue;
-            launch_k_level(kk, slot, dtab + (l * 2 + kk) * tabW, n, cnt, trace, traceBase, st);
-            traceBase += cnt;
-        }
+    for (size_t l = 0; l < nLevels; l++) {
+        const uint32_t nInter = total[l * 3], nLarge = total[l * 3 + 1], nSmall = total[l * 3 + 2];
+        if (nInter) launch_k_level(0, slot, dtab + l * tabW, n, nInter, trace, traceBase, st);
+        traceBase += nInter;
+        if (nLarge + nSmall) launch_k_level(1, slot, dtab + l * tabW + tabI, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
+        traceBase += nLarge + nSmall;
+    }
     if (trace) {
         // rows: code, stream << 32 | tx_size << 8 | pred, t_entry, t_item, t_pred, t_end, level, 0
         std::vector<unsigned long long> hv((size_t)allItems * 8);
@@ -663,8 +682,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         HIPCHK(hipStreamSynchronize(st));
         size_t q = 0;
         for (size_t l = 0; l < nLevels; l++)
-            for (int kk = 0; kk < 2; kk++)
-                for (uint32_t i = 0; i < total[l * 2 + kk]; i++, q++) hv[q * 8 + 6] = l;
+            for (int kk = 0; kk < 3; kk++)
+                for (uint32_t i = 0; i < total[l * 3 + kk]; i++, q++) hv[q * 8 + 6] = l;
         fwrite(hv.data(), 8, hv.size(), lc->traceFile);
         fflush(lc->traceFile);
     }

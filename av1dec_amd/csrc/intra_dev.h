@@ -5,7 +5,8 @@
 // LDS, the 5-tap edge filter and the 2x upsampler run one output per lane on a
 // snapshot of the edge, and the predictors compute one pixel per lane.  Filter-intra's
 // serial 4x2 recursion (:112-149) runs as an anti-diagonal wavefront.  Usable from
-// any workgroup size (blockDim.x a multiple of 64).
+// group of NT cooperating lanes: a whole 256-lane workgroup or a single wave (NT = 64,
+// several items per workgroup, wave-level synchronisation; see coop_sync in av1r_dev.h).
 #pragma once
 #include "av1r_dev.h"
 
@@ -74,23 +75,25 @@ DEV int edge_upsample_used(int w, int h, int filterType, int delta)
 }
 
 // intraEdgeFilter (IntraPredict.cpp:324-337) on edge e (e[-1..sz-2] rewritten).
+template <int NT>
 DEV void coop_edge_filter(uint8_t* e, uint8_t* tmp, int sz, int strength)
 {
-    const int t = threadIdx.x, nt = blockDim.x;
+    const int t = coop_lane<NT>(), nt = NT;
     for (int i = t; i < sz; i += nt) tmp[i] = e[i - 1];
-    __syncthreads();
+    coop_sync<NT>();
     for (int i = 1 + t; i < sz; i += nt) {
         int s = 0;
 #pragma unroll
         for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strength - 1][j] * tmp[CLIP3(0, sz - 1, i - 2 + j)];
         e[i - 1] = (uint8_t)((s + 8) >> 4);
     }
-    __syncthreads();
+    coop_sync<NT>();
 }
 // intraEdgeUpsample (IntraPredict.cpp:354-370): out buf (index -2 .. 2*numPx-2) at up+EDGE_OFF.
+template <int NT>
 DEV void coop_edge_upsample(const uint8_t* e, uint8_t* up, int numPx)
 {
-    const int t = threadIdx.x, nt = blockDim.x;
+    const int t = coop_lane<NT>(), nt = NT;
     uint8_t* buf = up + EDGE_OFF;
     // dup[k] = k==0 ? e[-1] : k<=numPx+1 ? e[k-2] : e[numPx-1]
     for (int i = t; i < numPx; i += nt) {
@@ -103,7 +106,7 @@ DEV void coop_edge_upsample(const uint8_t* e, uint8_t* up, int numPx)
         buf[2 * i] = (uint8_t)d2;
     }
     if (t == 0) buf[-2] = e[-1];
-    __syncthreads();
+    coop_sync<NT>();
 }
 
 DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) - 4); }
@@ -111,10 +114,11 @@ DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) 
 // Gathers AboveRow / LeftCol (IntraPredict.cpp:571-611) of a (1<<log2W) x (1<<log2H)
 // prediction at (x, y) of plane `plane` into L (global loads only; the caller issues the
 // barrier before the edges are read, so independent loads can be overlapped with it).
+template <int NT>
 DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
     int log2H, bool hL, bool hA, bool hAR, bool hBL, IntraLds& L)
 {
-    const int t = threadIdx.x, nt = blockDim.x;
+    const int t = coop_lane<NT>(), nt = NT;
     const int w = 1 << log2W, h = 1 << log2H;
     // predict_intra uses subsampling_x for both axes (IntraPredict.cpp:566-567)
     const int sub = plane ? 1 : 0;
@@ -148,10 +152,11 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
 }
 
 // Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps) from edges already
-// gathered into L (coop_intra_edges + a barrier).  Ends with a __syncthreads().
+// gathered into L (coop_intra_edges + a barrier).  Ends with a coop_sync.
+template <int NT>
 DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, IntraLds& L, uint8_t* pred, int ps)
 {
-    const int t = threadIdx.x, nt = blockDim.x;
+    const int t = coop_lane<NT>(), nt = NT;
     const int w = 1 << P.log2W, h = 1 << P.log2H;
     const int plane = P.plane, x = P.x, y = P.y;
     const int sub = plane ? 1 : 0;
@@ -186,13 +191,13 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
                 // all reads of this diagonal complete before any write (next barrier)
                 L.tmp[q] = (uint8_t)clip1(r2s(pr, 4));
             }
-            __syncthreads();
+            coop_sync<NT>();
             for (int q = t; q < ncell * 8; q += nt) {
                 int i2 = i2lo + (q >> 3), j4 = d - i2;
                 int o = q & 7;
                 pred[((i2 << 1) + (o >> 2)) * ps + (j4 << 2) + (o & 3)] = L.tmp[q];
             }
-            __syncthreads();
+            coop_sync<NT>();
         }
         return;
     }
@@ -213,26 +218,26 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
                     left[-1] = s;
                     above[-1] = s;
                 }
-                __syncthreads();
+                coop_sync<NT>();
             }
             if (P.haveAbove) {
                 int strength = edge_strength(w, h, P.smooth, pAngle - 90);
                 int numPx = imin(w, maxXd - x + 1) + (pAngle < 90 ? h : 0) + 1;
-                if (strength) coop_edge_filter(above, L.tmp, numPx, strength);
+                if (strength) coop_edge_filter<NT>(above, L.tmp, numPx, strength);
             }
             if (P.haveLeft) {
                 int strength = edge_strength(w, h, P.smooth, pAngle - 180);
                 int numPx = imin(h, maxYd - y + 1) + (pAngle > 180 ? w : 0) + 1;
-                if (strength) coop_edge_filter(left, L.tmp, numPx, strength);
+                if (strength) coop_edge_filter<NT>(left, L.tmp, numPx, strength);
             }
             upA = edge_upsample_used(w, h, P.smooth, pAngle - 90);
             if (upA) {
-                coop_edge_upsample(above, L.upA, w + (pAngle < 90 ? h : 0));
+                coop_edge_upsample<NT>(above, L.upA, w + (pAngle < 90 ? h : 0));
                 A = L.upA + EDGE_OFF;
             }
             upL = edge_upsample_used(w, h, P.smooth, pAngle - 180);
             if (upL) {
-                coop_edge_upsample(left, L.upL, h + (pAngle > 180 ? w : 0));
+                coop_edge_upsample<NT>(left, L.upL, h + (pAngle > 180 ? w : 0));
                 Lc = L.upL + EDGE_OFF;
             }
         }
@@ -286,7 +291,7 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
             for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
             if (t == 0) L.sum[0] = s;
         }
-        __syncthreads();
+        coop_sync<NT>();
         s = L.sum[0];
         int avg;
         if (P.haveLeft && P.haveAbove) avg = (s + ((w + h) >> 1)) / (w + h);
@@ -315,16 +320,17 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
             pred[i * ps + j] = (uint8_t)v;
         }
     }
-    __syncthreads();
+    coop_sync<NT>();
 }
 
 // Gather + predict (IntraPredict::predict_intra, IntraPredict.cpp:563-630).  Ends with a
-// __syncthreads().
+// coop_sync.
+template <int NT>
 DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const IntraParams& P,
     IntraLds& L, uint8_t* pred, int ps)
 {
-    coop_intra_edges(miCols, miRows, src, P.plane, P.x, P.y, P.log2W, P.log2H, P.haveLeft, P.haveAbove, P.haveAR,
+    coop_intra_edges<NT>(miCols, miRows, src, P.plane, P.x, P.y, P.log2W, P.log2H, P.haveLeft, P.haveAbove, P.haveAR,
         P.haveBL, L);
-    __syncthreads();
-    coop_intra_from_edges(miCols, miRows, P, L, pred, ps);
+    coop_sync<NT>();
+    coop_intra_from_edges<NT>(miCols, miRows, P, L, pred, ps);
 }

@@ -39,11 +39,13 @@ DEV void trace_stamp(unsigned long long* tr, int slot)
 // ---------------------------------------------------------------------------------
 // Transform blocks
 // ---------------------------------------------------------------------------------
-#define RS 66  // LDS row stride (int16) of the residual tile: 33 dwords, conflict-free rows & columns
-
+// LDS of one transform block of at most MAX x MAX samples.  The residual tile's row stride
+// RS = MAX + 2 int16 is an odd number of dwords: rows and columns are bank-conflict free.
+template <int MAX>
 struct TbLds {
-    int16_t res[64 * RS];
-    uint8_t pred[64 * 64];
+    static constexpr int RS = MAX + 2;
+    int16_t res[MAX * RS];
+    uint8_t pred[MAX * MAX];
     IntraLds intra;
     int sum;
 };
@@ -64,7 +66,7 @@ DEV void row_pass(int16_t* row, int w, int kind, int rectScale, int rowShift, in
 }
 // Column pass fused with the reconstruction of one output column: out/pred point at
 // the column's row 0 (after the left-right flip); rows are written flipped if flipUD.
-template <int n>
+template <int n, int RS, int PS>
 DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, const uint8_t* pred, uint8_t* out,
     int stride, int flipUD)
 {
@@ -75,23 +77,25 @@ DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, cons
 #pragma unroll
     for (int yy = 0; yy < (1 << n); yy++) {
         const int i = flipUD ? (1 << n) - 1 - yy : yy;
-        out[i * stride] = (uint8_t)clip1(pred[i * 64] + r2(T[yy], colShift));
+        out[i * stride] = (uint8_t)clip1(pred[i * PS] + r2(T[yy], colShift));
     }
 }
 
 // reconstruct() + inverseTransform() (TransformBlock.cpp:2173-2276), the flip and the
 // add-and-clip onto the prediction in L.pred, stored to the frame at (x, y).
-DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds& L, const DevPlane& dst,
+template <int NT, int MAX>
+DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds<MAX>& L, const DevPlane& dst,
     uint32_t c0)
 {
-    const int t = threadIdx.x;
+    constexpr int RS = TbLds<MAX>::RS;
+    const int t = coop_lane<NT>();
     const int txSz = tb.tx_size;
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
     const int log2W = av1r_tx_w_log2[txSz], log2H = av1r_tx_h_log2[txSz];
     const int tw = imin(w, 32), th = imin(h, 32);
     const av1r_frame_hdr& hd = *k.hdr;
-    for (int q = t; q < th * w; q += 64) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
-    __syncthreads();
+    for (int q = t; q < th * w; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
+    coop_sync<NT>();
     int dqDenom = 1;
     if (txSz == AV1R_TX_32X32 || txSz == AV1R_TX_16X32 || txSz == AV1R_TX_32X16 || txSz == AV1R_TX_16X64 || txSz == AV1R_TX_64X16)
         dqDenom = 2;
@@ -103,15 +107,15 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
     const int dcQ = av1r_dc_qlookup[CLIP3(0, 255, blk.qindex + dcDelta)];
     const int acQ = av1r_ac_qlookup[CLIP3(0, 255, blk.qindex + acDelta)];
     const uint32_t* cf = k.coefs + tb.coef_off;
-    for (int q = t; q < tb.coef_cnt; q += 64) {
-        const uint32_t c = q == t ? c0 : cf[q];  // the first 64 were prefetched by the caller
+    for (int q = t; q < tb.coef_cnt; q += NT) {
+        const uint32_t c = q == t ? c0 : cf[q];  // the first NT were prefetched by the caller
         int pos = AV1R_COEF_POS(c), level = AV1R_COEF_LEVEL(c);
         int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
         int sign = d < 0 ? -1 : 1;
         int d2 = sign * (iabs(d) & 0xffffff) / dqDenom;
         L.res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
     }
-    __syncthreads();
+    coop_sync<NT>();
     const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
     const int type = tb.tx_type;
     const int rowShift = lossless ? 0 : av1r_tx_row_shift[txSz];
@@ -125,14 +129,14 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         case 2: row_pass<2>(row, w, rk, rect, rowShift, lossless); break;
         case 3: row_pass<3>(row, w, rk, rect, rowShift, lossless); break;
         case 4: row_pass<4>(row, w, rk, rect, rowShift, lossless); break;
-        case 5: row_pass<5>(row, w, rk, rect, rowShift, lossless); break;
-        default: row_pass<6>(row, w, rk, rect, rowShift, lossless); break;
+        case 5: if constexpr (MAX >= 32) row_pass<5>(row, w, rk, rect, rowShift, lossless); break;
+        default: if constexpr (MAX >= 64) row_pass<6>(row, w, rk, rect, rowShift, lossless); break;
         }
     } else if (t < h) {
         int16_t* row = L.res + t * RS;
         for (int j = 0; j < w; j++) row[j] = 0;
     }
-    __syncthreads();
+    coop_sync<NT>();
     const int flipUD = type == AV1R_FLIPADST_DCT || type == AV1R_FLIPADST_ADST || type == AV1R_V_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     const int flipLR = type == AV1R_DCT_FLIPADST || type == AV1R_ADST_FLIPADST || type == AV1R_H_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     if (t < w) {
@@ -141,11 +145,11 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         const uint8_t* pred = L.pred + j;
         uint8_t* out = dst.p + (size_t)tb.y * dst.stride + tb.x + j;
         switch (log2H) {
-        case 2: col_pass<2>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        case 3: col_pass<3>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        case 4: col_pass<4>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        case 5: col_pass<5>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        default: col_pass<6>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 2: col_pass<2, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 3: col_pass<3, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 4: col_pass<4, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 5: if constexpr (MAX >= 32) col_pass<5, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        default: if constexpr (MAX >= 64) col_pass<6, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
         }
     }
 }
@@ -153,9 +157,11 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
 // One transform block (TransformBlock::decode, TransformBlock.cpp:2400-2456).  The
 // item record carries the TB, so its first coefficients and its prediction inputs (intra
 // edges or the inter-predicted pixels) are in flight before the block record is read.
-DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long long* tr)
+template <int NT, int MAX>
+DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned long long* tr)
 {
-    const int t = threadIdx.x;
+    constexpr int RS = TbLds<MAX>::RS;
+    const int t = coop_lane<NT>();
     av1r_tb tb;
     tb.block = wi.block;
     tb.coef_off = wi.coef_off;
@@ -173,7 +179,7 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long l
     const int src = wi.pred;
     const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
     if (src == AV1R_PRED_INTRA)
-        coop_intra_edges(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+        coop_intra_edges<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
             (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
             (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
     const av1r_block& blk = k.blocks[tb.block];
@@ -181,9 +187,9 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long l
     const av1r_frame_hdr& hd = *k.hdr;
 
     if (src == AV1R_PRED_INTER) {
-        for (int q = t; q < w * h; q += 64) {
+        for (int q = t; q < w * h; q += NT) {
             int i = q >> log2W, j = q & (w - 1);
-            L.pred[i * 64 + j] = px(dst, x + j, y + i);
+            L.pred[i * MAX + j] = px(dst, x + j, y + i);
         }
     } else if (src == AV1R_PRED_PALETTE) {
         // Block::Palette::predict_palette (Block.cpp:2279-2298)
@@ -192,9 +198,9 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long l
         int mw = plane ? ph[2] : ph[0];
         const uint8_t* map = ph + AV1R_PALETTE_HDR + (plane ? ph[0] * ph[1] : 0);
         const uint8_t* colors = ph + 4 + 8 * plane;
-        for (int q = t; q < w * h; q += 64) {
+        for (int q = t; q < w * h; q += NT) {
             int i = q >> log2W, j = q & (w - 1);
-            L.pred[i * 64 + j] = colors[map[(by + i) * mw + bx + j]];
+            L.pred[i * MAX + j] = colors[map[(by + i) * mw + bx + j]];
         }
     } else {
         const int isCfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
@@ -215,15 +221,15 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long l
         P.smooth = plane ? ((bflags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
                          : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
         P.edgeFilter = hd.enable_intra_edge_filter;
-        __syncthreads();  // edges gathered
-        coop_intra_from_edges(k.mi_cols, k.mi_rows, P, L.intra, L.pred, 64);
+        coop_sync<NT>();  // edges gathered
+        coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, MAX);
         if (isCfl) {
             // predict_chroma_from_luma (IntraPredict.cpp:632-667)
             const DevPlane& luma = k.cur.pl[0];
             const int alpha = plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v;
             const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
             int s = 0;
-            for (int q = t; q < w * h; q += 64) {
+            for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
                 int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
                 int v = (px(luma, lx, ly) + px(luma, lx + 1, ly) + px(luma, lx, ly + 1) + px(luma, lx + 1, ly + 1)) << 1;
@@ -232,22 +238,29 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds& L, unsigned long l
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+            if (NT > 64) {  // across the waves of the workgroup
+                if (t == 0) L.sum = 0;
+                coop_sync<NT>();
+                if ((t & 63) == 0) atomicAdd(&L.sum, s);
+                coop_sync<NT>();
+                s = L.sum;
+            }
             const int avg = r2(s, log2W + P.log2H);
-            for (int q = t; q < w * h; q += 64) {
+            for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
-                int dc = L.pred[i * 64 + j];
-                L.pred[i * 64 + j] = (uint8_t)clip1(dc + r2s(alpha * (L.res[i * RS + j] - avg), 6));
+                int dc = L.pred[i * MAX + j];
+                L.pred[i * MAX + j] = (uint8_t)clip1(dc + r2s(alpha * (L.res[i * RS + j] - avg), 6));
             }
         }
     }
-    __syncthreads();
+    coop_sync<NT>();
     trace_stamp(tr, 4);
     if (tb.coef_cnt) {
-        tb_residual(k, tb, blk, L, dst, c0);
+        tb_residual<NT, MAX>(k, tb, blk, L, dst, c0);
     } else if (src != AV1R_PRED_INTER) {
-        for (int q = t; q < w * h; q += 64) {
+        for (int q = t; q < w * h; q += NT) {
             int i = q >> log2W, j = q & (w - 1);
-            px(dst, x + j, y + i) = L.pred[i * 64 + j];
+            px(dst, x + j, y + i) = L.pred[i * MAX + j];
         }
     }
 }
@@ -571,9 +584,9 @@ DEV WedgeSel wedge_select(int bs, int wedge)
     s.xoff = 32 - ((cb[1] * w) >> 3);
     s.yoff = 32 - ((cb[2] * h) >> 3);
     // flipSign (initialise_wedge_mask_table, InterPredict.cpp:870-877)
-    // (the w + h - 1 edge samples summed across the wave; call with all 64 lanes active)
+    // (the w + h - 1 edge samples summed across each wave; call with all 64 lanes active)
     int sum = 0;
-    for (int i = threadIdx.x; i < w + h - 1; i += 64)
+    for (int i = threadIdx.x & 63; i < w + h - 1; i += 64)  // every wave sums all of them
         sum += i < w ? wedge_master(s.dir, s.yoff, s.xoff + i) : wedge_master(s.dir, s.yoff + i - w + 1, s.xoff);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
@@ -922,9 +935,10 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
 // Inter-intra blend of block `bi` (Block.cpp:118-144 + maskBlend, InterPredict.cpp:555-609):
 // the block's intra prediction (its edges are final when this item runs) blended with the
 // inter prediction inter_tile stored in the frame.
-DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
+template <int NT>
+DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
 {
-    const int t = threadIdx.x;
+    const int t = coop_lane<NT>();
     const av1r_block& blk = k.blocks[bi];
     const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
     const int bs = blk.mi_size;
@@ -955,9 +969,9 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
         P.filterIntraMode = 0;
         P.smooth = 0;
         P.edgeFilter = k.hdr->enable_intra_edge_filter;
-        coop_intra_predict(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
+        coop_intra_predict<NT>(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
         const int sizeScale = 128 / imax(ph, pw);
-        for (int q = t; q < pw * ph; q += 64) {
+        for (int q = t; q < pw * ph; q += NT) {
             const int i = q / pw, j = q - i * pw;
             int m;
             if (!isWedge) {
@@ -981,7 +995,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
             uint8_t& d = px(dst, baseX + j, baseY + i);
             d = (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6));
         }
-        __syncthreads();
+        coop_sync<NT>();
     }
 }
 
@@ -993,45 +1007,83 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds& L)
 AV1R_KP_TABLE(g_kp, kp_upload, kp_release)
 
 // Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
-// counts of this kind at this level; tab[n + 1 + s]: offset of frame s's items in its
-// item list).  Returns the frame's parameters and the work item.
-DEV const WorkItem& level_item(int slot, const uint32_t* __restrict__ tab, int n, const KParams*& kp, int& s)
+// counts; tab[n + 1 + s]: offset of frame s's items in its item list).  `lane` indexes the
+// table (one lane per frame); item `b` of the launch.  Returns the frame's parameters.
+DEV const WorkItem& table_item(int slot, const uint32_t* __restrict__ tab, int n, uint32_t b, const KParams*& kp,
+    int& s)
 {
-    const uint32_t b = blockIdx.x;
-    // frame of this workgroup: the number of frames whose items all precede b (one
-    // vector load of the prefix table + a ballot instead of a dependent scan)
-    const uint32_t pre = (int)threadIdx.x + 1 < n ? tab[threadIdx.x + 1] : 0xffffffffu;
+    // frame of item b: the number of frames whose items all precede it (one vector load
+    // of the prefix table + a ballot instead of a dependent scan)
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     kp = &g_kp[slot][s];
     return kp->items[tab[n + 1 + s] + (b - tab[s])];
 }
 
-// One launch per dependency level and kernel: inter tiles (k_inter) and transform blocks +
-// inter-intra blends (k_tb) have their own kernels, so each gets the register budget and
-// LDS of its own work (one 64-lane workgroup per item).
-extern "C" __global__ __launch_bounds__(64) void k_tb(int slot, const uint32_t* __restrict__ tab, int n,
+// Transform blocks and inter-intra blends of one level.  Large items (a side of 32 or
+// more, and the blends) take a whole 256-lane workgroup each; small TBs (up to 16x16) are
+// packed four per workgroup, one per wave, each wave with its own small LDS tiles.
+// tab: [big prefix (n + 1)][small prefix (n + 1)][big offsets (n)][small offsets (n)].
+#define TB_SMALL 16
+extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
 {
-    __shared__ TbLds L;
+    constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
+    __shared__ __align__(16) uint8_t smem[kLds];
+    const uint32_t* tabS = tab + n + 1;  // small prefix
+    const uint32_t nBig = tab[n], nSmall = tabS[n];
+    const uint32_t b = blockIdx.x;
+    const KParams* kp;
+    int s;
+    if (b < nBig) {
+        // big: a whole workgroup; offsets follow both prefix tables
+        const int lane = threadIdx.x & 63;
+        const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+        s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+        kp = &g_kp[slot][s];
+        const WorkItem& wi = kp->items[tab[2 * n + 2 + s] + (b - tab[s])];
 #ifdef AV1R_TRACE
-    unsigned long long* tr = trace ? trace + (size_t)(traceBase + blockIdx.x) * 8 : nullptr;
+        unsigned long long* tr = trace ? trace + (size_t)(traceBase + b) * 8 : nullptr;
+        if (tr && threadIdx.x == 0) {
+            tr[0] = wi.code;
+            tr[1] = ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred;
+        }
+#else
+        unsigned long long* tr = nullptr;
+#endif
+        trace_stamp(tr, 2);  // (after the item record: entry and record stamps coincide)
+        trace_stamp(tr, 3);
+        TbLds<64>& L = *reinterpret_cast<TbLds<64>*>(smem);
+        if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) ii_item<256>(*kp, AV1R_ITEM_INDEX(wi.code), L);
+        else tb_item<256, 64>(*kp, wi, L, tr);
+        trace_stamp(tr, 5);
+        return;
+    }
+    // small: item i of the small list, one per wave
+    const int wave = threadIdx.x >> 6;
+    const uint32_t i = (b - nBig) * 4 + wave;
+    if (i >= nSmall) return;  // (no workgroup barrier in this mode)
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tabS[lane + 1] : 0xffffffffu;
+    s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(i >= pre)));
+    kp = &g_kp[slot][s];
+    const WorkItem& wi = kp->items[tab[3 * n + 2 + s] + (i - tabS[s])];
+#ifdef AV1R_TRACE
+    unsigned long long* tr = trace ? trace + (size_t)(traceBase + nBig + i) * 8 : nullptr;
+    if (tr && lane == 0) {
+        tr[0] = wi.code;
+        tr[1] = ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred;
+    }
 #else
     unsigned long long* tr = nullptr;
     (void)trace;
     (void)traceBase;
 #endif
     trace_stamp(tr, 2);
-    const KParams* kp;
-    int s;
-    const WorkItem& wi = level_item(slot, tab, n, kp, s);
-    if (tr && threadIdx.x == 0) {
-        tr[0] = wi.code;
-        tr[1] = ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred;
-    }
     trace_stamp(tr, 3);
-    // inter-intra blends share the launch (and the LDS layout) of the level's TBs
-    if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) ii_item(*kp, AV1R_ITEM_INDEX(wi.code), L);
-    else tb_item(*kp, wi, L, tr);
+    TbLds<TB_SMALL>& L = reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave];
+    tb_item<64, TB_SMALL>(*kp, wi, L, tr);
     trace_stamp(tr, 5);
 }
 
@@ -1049,7 +1101,7 @@ extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_
     trace_stamp(tr, 2);
     const KParams* kp;
     int s;
-    const WorkItem& wi = level_item(slot, tab, n, kp, s);
+    const WorkItem& wi = table_item(slot, tab, n, blockIdx.x, kp, s);
     const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
     if (tr && threadIdx.x == 0) tr[0] = wi.code;
     trace_stamp(tr, 3);
@@ -1057,9 +1109,10 @@ extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_
     trace_stamp(tr, 5);
 }
 
+// kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4)
 void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
 {
     if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
-    else hipLaunchKernelGGL(k_tb, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
+    else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, slot, tab, n, trace, traceBase);
 }
