@@ -26,7 +26,7 @@
 DEV void trace_stamp(unsigned long long* tr, int slot)
 {
 #ifdef AV1R_TRACE
-    if (tr && threadIdx.x == 0) {
+    if (tr && (threadIdx.x & 63) == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         tr[slot] = __builtin_amdgcn_s_memrealtime();
     }

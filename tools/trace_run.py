@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
 
 
-def run(nfr, path):
+def run(nfr, path, streams=1):
     if os.path.exists(path):
         os.remove(path)
     os.environ["AV1R_TRACE_FILE"] = path
@@ -20,14 +20,21 @@ def run(nfr, path):
     os.environ.setdefault("AV1R_LIB", os.path.join(ROOT, "av1dec_amd", "_build", "libav1r_trace.so"))
     import pysynth
     from av1dec_amd import Decoder
-    frames = pysynth.stream(1920, 1080, nfr, 0x5EED1000, sb128=True)
-    d = Decoder(0, keep_stages=False)
-    d.set_discard_output(True)
-    hs = [d.prepare(f) for f in frames]
-    for h in hs:
-        d.decode_prepared(h)
-    d.synchronize()
-    d.close()
+    decs, hss = [], []
+    for i in range(streams):
+        frames = pysynth.stream(1920, 1080, nfr, 0x5EED1000 + i, sb128=True)
+        d = Decoder(0, keep_stages=False)
+        d.set_discard_output(True)
+        decs.append(d)
+        hss.append([d.prepare(f) for f in frames])
+    for t in range(nfr):
+        if streams == 1:
+            decs[0].decode_prepared(hss[0][t])
+        else:
+            Decoder.decode_prepared_batch(decs, [h[t] for h in hss])
+    for d in decs:
+        d.synchronize()
+        d.close()
 
 
 def summarise(path):
@@ -65,23 +72,47 @@ def summarise(path):
     for ts in np.unique(txs[m]):
         mm = m & (txs == ts)
         print(f"   intra tx_size {ts:2d}: n={mm.sum():6d} total p50 {np.median(us(t3[mm]-t0[mm])):6.2f} pred {np.median(us(t2[mm]-t1[mm])):6.2f} resid {np.median(us(t3[mm]-t2[mm])):6.2f}")
-    # level timeline of the last frame: start of first item -> end of last item per level
-    f0 = starts[-1]
-    sl = slice(f0, len(a))
+    for fi in sorted({0, len(starts) - 1}):
+        level_report(a, starts, fi)
+
+
+def level_report(a, starts, fi):
+    import collections
+    code, misc, t0, t3, lvl = a[:, 0], a[:, 1], a[:, 2], a[:, 5], a[:, 6]
+    kind = code >> 30
+    txs = (misc >> 8) & 0xff
+    us = lambda x: x / 100.0
+    f0 = starts[fi]
+    f1 = starts[fi + 1] if fi + 1 < len(starts) else len(a)
+    sl = slice(f0, f1)
     L = lvl[sl]
-    spans = []
-    for l in np.unique(L):
-        mm = L == l
-        s0, e0 = t0[sl][mm].min(), t3[sl][mm].max()
-        spans.append((l, us(e0 - s0), mm.sum()))
-    gaps = [us(t0[sl][L == l2].min() - t3[sl][L == l1].max()) for l1, l2 in zip(np.unique(L)[:-1], np.unique(L)[1:])]
-    print("last frame: levels", len(spans), "sum of level spans %.1f us, sum of gaps %.1f us (median gap %.2f)"
-          % (sum(x[1] for x in spans), sum(gaps), np.median(gaps) if gaps else 0))
+    ul = np.unique(L)
+    spans = [us(t3[sl][L == l].max() - t0[sl][L == l].min()) for l in ul]
+    gaps = [us(t0[sl][L == l2].min() - t3[sl][L == l1].max()) for l1, l2 in zip(ul[:-1], ul[1:])]
+    print(f"frame {fi}: levels {len(ul)}, sum of level spans {sum(spans):.1f} us, sum of gaps {sum(gaps):.1f} us"
+          f" (median gap {np.median(gaps) if gaps else 0:.2f})")
+    names = {0: "TB", 1: "tile", 2: "ii"}
+    rows = []
+    for l in ul:
+        mm = np.flatnonzero(L == l)
+        ends = t3[sl][mm]
+        j = mm[np.argmax(ends)]
+        rows.append((l, len(mm), names[int(kind[sl][j])], int(txs[sl][j]), us(t3[sl][j] - t0[sl][j]),
+                     np.median(us(t3[sl][mm] - t0[sl][mm])), us(ends.max() - t0[sl][mm].min())))
+    print("level  items straggler(kind,tx) dur  median  span")
+    for r in rows[:10] + rows[-4:]:
+        print("%5d %6d %6s %3d %7.2f %7.2f %7.2f" % r)
+    c = collections.Counter((r[2], r[3]) for r in rows)
+    print("stragglers by (kind, tx_size):", c.most_common(8))
+    # span histogram
+    sp = np.array(spans)
+    print("level span percentiles (us): p10 %.1f p50 %.1f p90 %.1f max %.1f" % tuple(np.percentile(sp, [10, 50, 90, 100])))
 
 
 if __name__ == "__main__":
     nfr = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "trace.bin")
+    streams = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    run(nfr, path)
+    run(nfr, path, streams)
     summarise(path)
