@@ -664,7 +664,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (lc->traceFile && lc->traceCap < allItems) {
         if (lc->traceDev) (void)hipFree(lc->traceDev);
         lc->traceCap = allItems + allItems / 2;
-        HIPCHK(hipMalloc(&lc->traceDev, lc->traceCap * 64));
+        HIPCHK(hipMalloc(&lc->traceDev, lc->traceCap * 128));
     }
     unsigned long long* trace = lc->traceFile ? lc->traceDev : nullptr;
     uint32_t traceBase = 0;
@@ -676,14 +676,15 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         traceBase += nLarge + nSmall;
     }
     if (trace) {
-        // rows: code, stream << 32 | tx_size << 8 | pred, t_entry, t_item, t_pred, t_end, level, 0
-        std::vector<unsigned long long> hv((size_t)allItems * 8);
+        // rows of 16: code, stream << 32 | tx_size << 8 | pred, t_entry, t_item, t_pred, t_end, level,
+        // then sub-phase stamps (TB: 8 edges, 9 predicted, 11 zeroed, 12 dequantised, 13 rows)
+        std::vector<unsigned long long> hv((size_t)allItems * 16);
         HIPCHK(hipMemcpyAsync(hv.data(), trace, hv.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         size_t q = 0;
         for (size_t l = 0; l < nLevels; l++)
             for (int kk = 0; kk < 3; kk++)
-                for (uint32_t i = 0; i < total[l * 3 + kk]; i++, q++) hv[q * 8 + 6] = l;
+                for (uint32_t i = 0; i < total[l * 3 + kk]; i++, q++) hv[q * 16 + 6] = l;
         fwrite(hv.data(), 8, hv.size(), lc->traceFile);
         fflush(lc->traceFile);
     }

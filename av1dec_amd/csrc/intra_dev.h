@@ -17,6 +17,7 @@ struct IntraLds {
     uint8_t above[EDGE_LEN];
     uint8_t left[EDGE_LEN];
     uint8_t tmp[EDGE_LEN];
+    uint8_t tmp2[EDGE_LEN];
     uint8_t upA[EDGE_LEN];
     uint8_t upL[EDGE_LEN];
     int sum[2];
@@ -74,39 +75,60 @@ DEV int edge_upsample_used(int w, int h, int filterType, int delta)
     return filterType ? (blkWh <= 8) : (blkWh <= 16);
 }
 
-// intraEdgeFilter (IntraPredict.cpp:324-337) on edge e (e[-1..sz-2] rewritten).
+// The edge preparation of directionalIntraPredict (IntraPredict.cpp:394-437) for both
+// edges at once, three barriers in all: the corner filter (filterCorner, :204-209) folded
+// into the copy pass, both intraEdgeFilter passes (:324-337) in one, both upsamples
+// (:354-370) in one.  nA / nL: filter lengths (numPx), strA / strL: strengths (0: none),
+// nUA / nUL: upsampled lengths (0: no upsampling).
 template <int NT>
-DEV void coop_edge_filter(uint8_t* e, uint8_t* tmp, int sz, int strength)
+DEV void coop_edge_prepare(uint8_t* above, uint8_t* left, IntraLds& L, bool corner, int strA, int nA, int strL,
+    int nL, int nUA, int nUL)
 {
     const int t = coop_lane<NT>(), nt = NT;
-    for (int i = t; i < sz; i += nt) tmp[i] = e[i - 1];
-    coop_sync<NT>();
-    for (int i = 1 + t; i < sz; i += nt) {
-        int s = 0;
+    const int cs = corner ? r2(left[0] * 5 + above[-1] * 6 + above[0] * 5, 4) : above[-1];
+    if (strA)
+        for (int i = t; i < nA; i += nt) L.tmp[i] = i == 0 ? (uint8_t)cs : above[i - 1];
+    if (strL)
+        for (int i = t; i < nL; i += nt) L.tmp2[i] = i == 0 ? (uint8_t)cs : left[i - 1];
+    if (strA || strL || corner) coop_sync<NT>();
+    if (strA)
+        for (int i = 1 + t; i < nA; i += nt) {
+            int s = 0;
 #pragma unroll
-        for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strength - 1][j] * tmp[CLIP3(0, sz - 1, i - 2 + j)];
-        e[i - 1] = (uint8_t)((s + 8) >> 4);
+            for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strA - 1][j] * L.tmp[CLIP3(0, nA - 1, i - 2 + j)];
+            above[i - 1] = (uint8_t)((s + 8) >> 4);
+        }
+    if (strL)
+        for (int i = 1 + t; i < nL; i += nt) {
+            int s = 0;
+#pragma unroll
+            for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strL - 1][j] * L.tmp2[CLIP3(0, nL - 1, i - 2 + j)];
+            left[i - 1] = (uint8_t)((s + 8) >> 4);
+        }
+    if (corner && t == 0) {
+        above[-1] = (uint8_t)cs;
+        left[-1] = (uint8_t)cs;
     }
-    coop_sync<NT>();
-}
-// intraEdgeUpsample (IntraPredict.cpp:354-370): out buf (index -2 .. 2*numPx-2) at up+EDGE_OFF.
-template <int NT>
-DEV void coop_edge_upsample(const uint8_t* e, uint8_t* up, int numPx)
-{
-    const int t = coop_lane<NT>(), nt = NT;
-    uint8_t* buf = up + EDGE_OFF;
-    // dup[k] = k==0 ? e[-1] : k<=numPx+1 ? e[k-2] : e[numPx-1]
-    for (int i = t; i < numPx; i += nt) {
-        int d0 = i == 0 ? e[-1] : e[i - 2];
-        int d1 = e[i - 1];
-        int d2 = e[i];
-        int d3 = (i + 1 <= numPx - 1) ? e[i + 1] : e[numPx - 1];
-        int s = -d0 + 9 * d1 + 9 * d2 - d3;
-        buf[2 * i - 1] = (uint8_t)clip1(r2(s, 4));
-        buf[2 * i] = (uint8_t)d2;
+    if (strA || strL || corner) coop_sync<NT>();
+    // upsampled buffers: index -2 .. 2 * numPx - 2 at up + EDGE_OFF; dup[k] = k == 0 ? e[-1]
+    // : k <= numPx + 1 ? e[k - 2] : e[numPx - 1]
+    for (int side = 0; side < 2; side++) {
+        const int n = side ? nUL : nUA;
+        if (!n) continue;
+        const uint8_t* e = side ? left : above;
+        uint8_t* buf = (side ? L.upL : L.upA) + EDGE_OFF;
+        for (int i = t; i < n; i += nt) {
+            int d0 = i == 0 ? e[-1] : e[i - 2];
+            int d1 = e[i - 1];
+            int d2 = e[i];
+            int d3 = (i + 1 <= n - 1) ? e[i + 1] : e[n - 1];
+            int s = -d0 + 9 * d1 + 9 * d2 - d3;
+            buf[2 * i - 1] = (uint8_t)clip1(r2(s, 4));
+            buf[2 * i] = (uint8_t)d2;
+        }
+        if (t == 0) buf[-2] = e[-1];
     }
-    if (t == 0) buf[-2] = e[-1];
-    coop_sync<NT>();
+    if (nUA || nUL) coop_sync<NT>();
 }
 
 DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) - 4); }
@@ -212,34 +234,17 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
         const uint8_t* A = above;
         const uint8_t* Lc = left;
         if (P.edgeFilter && pAngle != 90 && pAngle != 180) {
-            if (pAngle > 90 && pAngle < 180 && (w + h) >= 24) {
-                if (t == 0) {
-                    uint8_t s = (uint8_t)r2(left[0] * 5 + above[-1] * 6 + above[0] * 5, 4);
-                    left[-1] = s;
-                    above[-1] = s;
-                }
-                coop_sync<NT>();
-            }
-            if (P.haveAbove) {
-                int strength = edge_strength(w, h, P.smooth, pAngle - 90);
-                int numPx = imin(w, maxXd - x + 1) + (pAngle < 90 ? h : 0) + 1;
-                if (strength) coop_edge_filter<NT>(above, L.tmp, numPx, strength);
-            }
-            if (P.haveLeft) {
-                int strength = edge_strength(w, h, P.smooth, pAngle - 180);
-                int numPx = imin(h, maxYd - y + 1) + (pAngle > 180 ? w : 0) + 1;
-                if (strength) coop_edge_filter<NT>(left, L.tmp, numPx, strength);
-            }
+            const bool corner = pAngle > 90 && pAngle < 180 && (w + h) >= 24;
+            const int strA = P.haveAbove ? edge_strength(w, h, P.smooth, pAngle - 90) : 0;
+            const int strL = P.haveLeft ? edge_strength(w, h, P.smooth, pAngle - 180) : 0;
+            const int nA = imin(w, maxXd - x + 1) + (pAngle < 90 ? h : 0) + 1;
+            const int nL = imin(h, maxYd - y + 1) + (pAngle > 180 ? w : 0) + 1;
             upA = edge_upsample_used(w, h, P.smooth, pAngle - 90);
-            if (upA) {
-                coop_edge_upsample<NT>(above, L.upA, w + (pAngle < 90 ? h : 0));
-                A = L.upA + EDGE_OFF;
-            }
             upL = edge_upsample_used(w, h, P.smooth, pAngle - 180);
-            if (upL) {
-                coop_edge_upsample<NT>(left, L.upL, h + (pAngle > 180 ? w : 0));
-                Lc = L.upL + EDGE_OFF;
-            }
+            coop_edge_prepare<NT>(above, left, L, corner, strA, nA, strL, nL, upA ? w + (pAngle < 90 ? h : 0) : 0,
+                upL ? h + (pAngle > 180 ? w : 0) : 0);
+            if (upA) A = L.upA + EDGE_OFF;
+            if (upL) Lc = L.upL + EDGE_OFF;
         }
         int dx = 0, dy = 0;
         if (pAngle < 90) dx = av1r_dr_intra_derivative[pAngle];

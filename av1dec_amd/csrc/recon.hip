@@ -20,6 +20,7 @@
 #include "kp_const.h"
 #include "txfm_dev.h"
 
+#define AV1R_TRACE_W 16  // u64 per item in the debug timeline
 // Debug timeline (AV1R_TRACE_FILE): lane 0 of each item stamps the 100 MHz real-time
 // counter at entry, once the item record is in, after the prediction and at the end.
 // Compiled in only with -DAV1R_TRACE (the stamps' waits constrain scheduling).
@@ -85,7 +86,7 @@ DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, cons
 // add-and-clip onto the prediction in L.pred, stored to the frame at (x, y).
 template <int NT, int MAX>
 DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds<MAX>& L, const DevPlane& dst,
-    uint32_t c0)
+    uint32_t c0, bool zeroed, unsigned long long* tr)
 {
     constexpr int RS = TbLds<MAX>::RS;
     const int t = coop_lane<NT>();
@@ -94,8 +95,11 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
     const int log2W = av1r_tx_w_log2[txSz], log2H = av1r_tx_h_log2[txSz];
     const int tw = imin(w, 32), th = imin(h, 32);
     const av1r_frame_hdr& hd = *k.hdr;
-    for (int q = t; q < th * w; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
-    coop_sync<NT>();
+    if (!zeroed) {
+        for (int q = t; q < th * w; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
+        coop_sync<NT>();
+    }
+    trace_stamp(tr, 11);
     int dqDenom = 1;
     if (txSz == AV1R_TX_32X32 || txSz == AV1R_TX_16X32 || txSz == AV1R_TX_32X16 || txSz == AV1R_TX_16X64 || txSz == AV1R_TX_64X16)
         dqDenom = 2;
@@ -116,6 +120,7 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         L.res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
     }
     coop_sync<NT>();
+    trace_stamp(tr, 12);
     const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
     const int type = tb.tx_type;
     const int rowShift = lossless ? 0 : av1r_tx_row_shift[txSz];
@@ -137,6 +142,7 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         for (int j = 0; j < w; j++) row[j] = 0;
     }
     coop_sync<NT>();
+    trace_stamp(tr, 13);
     const int flipUD = type == AV1R_FLIPADST_DCT || type == AV1R_FLIPADST_ADST || type == AV1R_V_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     const int flipLR = type == AV1R_DCT_FLIPADST || type == AV1R_ADST_FLIPADST || type == AV1R_H_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     if (t < w) {
@@ -185,6 +191,12 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
     const av1r_block& blk = k.blocks[tb.block];
     const uint32_t bflags = blk.flags;
     const av1r_frame_hdr& hd = *k.hdr;
+    // the residual tile is cleared under the prediction (CFL borrows it as scratch first)
+    const bool zeroEarly = tb.coef_cnt && !(plane > 0 && src == AV1R_PRED_INTRA && blk.uv_mode == AV1R_UV_CFL_PRED);
+    if (zeroEarly) {
+        const int tw2 = w, th2 = imin(h, 32);
+        for (int q = t; q < th2 * tw2; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
+    }
 
     if (src == AV1R_PRED_INTER) {
         for (int q = t; q < w * h; q += NT) {
@@ -222,7 +234,9 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
                          : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
         P.edgeFilter = hd.enable_intra_edge_filter;
         coop_sync<NT>();  // edges gathered
+        trace_stamp(tr, 8);
         coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, MAX);
+        trace_stamp(tr, 9);
         if (isCfl) {
             // predict_chroma_from_luma (IntraPredict.cpp:632-667)
             const DevPlane& luma = k.cur.pl[0];
@@ -256,7 +270,7 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
     coop_sync<NT>();
     trace_stamp(tr, 4);
     if (tb.coef_cnt) {
-        tb_residual<NT, MAX>(k, tb, blk, L, dst, c0);
+        tb_residual<NT, MAX>(k, tb, blk, L, dst, c0, zeroEarly, tr);
     } else if (src != AV1R_PRED_INTER) {
         for (int q = t; q < w * h; q += NT) {
             int i = q >> log2W, j = q & (w - 1);
@@ -1044,7 +1058,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
         kp = &g_kp[slot][s];
         const WorkItem& wi = kp->items[tab[2 * n + 2 + s] + (b - tab[s])];
 #ifdef AV1R_TRACE
-        unsigned long long* tr = trace ? trace + (size_t)(traceBase + b) * 8 : nullptr;
+        unsigned long long* tr = trace ? trace + (size_t)(traceBase + b) * AV1R_TRACE_W : nullptr;
         if (tr && threadIdx.x == 0) {
             tr[0] = wi.code;
             tr[1] = ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred;
@@ -1070,7 +1084,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
     kp = &g_kp[slot][s];
     const WorkItem& wi = kp->items[tab[3 * n + 2 + s] + (i - tabS[s])];
 #ifdef AV1R_TRACE
-    unsigned long long* tr = trace ? trace + (size_t)(traceBase + nBig + i) * 8 : nullptr;
+    unsigned long long* tr = trace ? trace + (size_t)(traceBase + nBig + i) * AV1R_TRACE_W : nullptr;
     if (tr && lane == 0) {
         tr[0] = wi.code;
         tr[1] = ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred;
@@ -1092,7 +1106,7 @@ extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_
 {
     __shared__ InterLds L;
 #ifdef AV1R_TRACE
-    unsigned long long* tr = trace ? trace + (size_t)(traceBase + blockIdx.x) * 8 : nullptr;
+    unsigned long long* tr = trace ? trace + (size_t)(traceBase + blockIdx.x) * AV1R_TRACE_W : nullptr;
 #else
     unsigned long long* tr = nullptr;
     (void)trace;

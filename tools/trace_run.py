@@ -38,7 +38,7 @@ def run(nfr, path, streams=1):
 
 
 def summarise(path):
-    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
     code, misc, t0, t1, t2, t3, lvl = a[:, 0], a[:, 1], a[:, 2], a[:, 3], a[:, 4], a[:, 5], a[:, 6]
     kind = code >> 30
     pred = misc & 0xff
@@ -67,6 +67,14 @@ def summarise(path):
             print(f"   inter tile motion {mode} compound {cp}: n={mm.sum():6d} item {np.median(us(t1[mm]-t0[mm])):5.2f}"
                   f" luma-pred {np.median(us(t2[mm]-t1[mm])):5.2f} luma-store {np.median(us(t7[mm]-t2[mm])):5.2f}"
                   f" chroma {np.median(us(t3[mm]-t7[mm])):5.2f} total {np.median(us(t3[mm]-t0[mm])):5.2f}")
+    # sub-phases of intra TBs (small mode: 4x4, 8x8, 16x16)
+    for ts in (0, 1, 2, 3):
+        mm = (kind == 0) & (pred == 0) & (txs == ts) & (a[:, 8] > 0) & (a[:, 13] > 0)
+        if not mm.any():
+            continue
+        ph = lambda i, j: np.median(us(a[mm, j] - a[mm, i]))
+        print(f"   intra tx {ts}: item {ph(2,3):.2f} edges {ph(3,8):.2f} predict {ph(8,9):.2f} cfl/sync {ph(9,4):.2f}"
+              f" zero {ph(4,11):.2f} dequant {ph(11,12):.2f} rows {ph(12,13):.2f} cols+store {ph(13,5):.2f}")
     # per tx size, intra TBs
     m = (kind == 0) & (pred == 0)
     for ts in np.unique(txs[m]):
