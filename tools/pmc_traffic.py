@@ -13,7 +13,7 @@ import os
 import sys
 from collections import defaultdict
 
-STAGES = {"k_level": "recon", "k_lf": "lf", "k_cdef": "cdef", "k_lr": "lr"}
+STAGES = {"k_inter": "recon", "k_tb": "recon", "k_lf": "lf", "k_cdef": "cdef", "k_lr": "lr"}
 
 
 def fold(path, counter):
@@ -45,7 +45,7 @@ def main():
     fetch, nf = fold(os.path.join(base, "FETCH_SIZE"), "FETCH_SIZE")
     write, nw = fold(os.path.join(base, "WRITE_SIZE"), "WRITE_SIZE")
     stages = {}
-    for st in STAGES.values():
+    for st in dict.fromkeys(STAGES.values()):
         f = fetch.get(st, 0.0) / max(nf, 1)
         w = write.get(st, 0.0) / max(nw, 1)
         stages[st] = {"fetch_bytes_raw": round(f), "fetch_bytes_x2": round(2 * f), "write_bytes": round(w),
