@@ -15,8 +15,10 @@ def build(force=False):
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
             os.path.getmtime(src), os.path.getmtime(os.path.join(ROOT, "include", "av1r.h"))):
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        tmp = f"{LIB}.{os.getpid()}.tmp"  # build aside, then rename: concurrent test workers never see a partial file
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"),
-                               src, "-o", LIB])
+                               src, "-o", tmp])
+        os.replace(tmp, LIB)
     return LIB
 
 
