@@ -30,7 +30,10 @@ struct WorkItem {
     uint16_t coef_cnt;  // TB
     uint8_t plane, tx_size, tx_type, flags;  // TB (flags: AV1R_TB_*)
     uint8_t pred;       // TB prediction source: AV1R_PRED_INTRA / _PALETTE / _INTER
-    uint8_t pad[9];
+    uint8_t pad0;
+    uint16_t dep_cnt;   // k_flow: the items whose pixels this one reads ...
+    uint16_t pad1;
+    uint32_t dep_off;   // ... at KParams::deps[dep_off, dep_off + dep_cnt) (item positions)
 };
 static_assert(sizeof(WorkItem) == 32, "WorkItem layout");
 #define AV1R_PRED_INTRA 0
@@ -50,6 +53,8 @@ struct KParams {
     const int8_t* cdef_idx;
     const av1r_lr_unit* lr;
     const WorkItem* items;  // this frame's level-ordered work items
+    const uint32_t* deps;   // k_flow: dependency lists (positions in items)
+    uint32_t* done;         // k_flow: per item, the epoch of the launch that completed it
     uint32_t n_items;
     int mi_stride;
     int mi_cols, mi_rows;
@@ -64,6 +69,13 @@ struct KParams {
 // flight per device (recon.hip: g_kp)
 #define AV1R_MAX_BATCH 32
 #define AV1R_KP_SLOTS 8
+
+// k_flow control block (recon.hip): FLOW_QUEUES queue heads, one 128-B line each, then
+// the error word; zeroed by the host before every launch
+#define FLOW_QUEUES 8
+#define FLOW_LINE 32
+#define FLOW_ERR (FLOW_QUEUES * FLOW_LINE)
+#define FLOW_CTL_BYTES 1280
 
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
 DEV int clip1(int v) { return CLIP3(0, 255, v); }
@@ -97,6 +109,43 @@ DEV void coop_sync()
 DEV const av1r_mi& mi_at(const KParams& k, int row, int col) { return k.mi[(size_t)row * k.mi_stride + col]; }
 DEV int plane_bsize(int bs, int plane) { return plane ? av1r_ss420[bs] : bs; }
 DEV uint8_t& px(const DevPlane& p, int x, int y) { return p.p[(size_t)y * p.stride + x]; }
+
+// Pixel access of the frame under reconstruction.  COH = false: plain loads / stores (the
+// level launches: every pixel an item reads was finalised by an earlier launch).  COH =
+// true: agent-scope coherent accesses (global_load / global_store ... sc1) for the
+// dataflow kernel k_flow, where producer and consumer items run in the SAME launch on
+// different CUs / XCDs: sc1 stores write through to the device coherence point and sc1
+// loads bypass the (never refreshed) vector L1, so after a producer's
+// `s_waitcnt vmcnt(0)` + sc1 flag store (flow_publish) a consumer that has seen the flag
+// (flow_wait) reads the final bytes.  x of the 4-byte forms is a multiple of 4.
+template <bool COH>
+DEV uint8_t ldp(const DevPlane& p, int x, int y)
+{
+    uint8_t* a = p.p + (size_t)y * p.stride + x;
+    if constexpr (COH) return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *a;
+}
+template <bool COH>
+DEV void stp(const DevPlane& p, int x, int y, uint8_t v)
+{
+    uint8_t* a = p.p + (size_t)y * p.stride + x;
+    if constexpr (COH) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *a = v;
+}
+template <bool COH>
+DEV uint32_t ldp4(const DevPlane& p, int x, int y)
+{
+    uint32_t* a = reinterpret_cast<uint32_t*>(p.p + (size_t)y * p.stride + x);
+    if constexpr (COH) return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *a;
+}
+template <bool COH>
+DEV void stp4(const DevPlane& p, int x, int y, uint32_t v)
+{
+    uint32_t* a = reinterpret_cast<uint32_t*>(p.p + (size_t)y * p.stride + x);
+    if constexpr (COH) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *a = v;
+}
 
 // Work-item encoding of the per-level item lists (host schedule -> k_level):
 // bits 31..30 kind, 29..0 index (TB index; block index for inter-intra blends;

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -36,6 +37,8 @@ void launch_k_lr(int slot, int n, int maxW, int maxH, hipStream_t s);
 int kpf_upload(int device, const KParams* host, int n, hipStream_t s);
 int kpf_release(int device, int slot, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
+int flow_grid(int device);
+void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid, hipStream_t s);
 
 namespace {
 
@@ -52,6 +55,7 @@ struct Upload {
     size_t cap = 0;
     hipEvent_t done = nullptr;  // all work that reads this upload has finished
     bool pending = false;
+    uint32_t* err = nullptr;    // meta: pinned copy of the launch's k_flow error word
 };
 
 struct Level {
@@ -73,6 +77,7 @@ struct Prepared {
     KParams base;  // batch pointers into dev
     const WorkItem* dItems = nullptr;
     std::vector<Level> levels;
+    bool flowOk = false;  // k_flow can run it: no inter tile after level 0 (intra block copy)
     bool usedRef[8] = {};
     uint64_t bytes = 0;
 };
@@ -101,6 +106,14 @@ struct av1r_ctx {
     std::vector<std::vector<uint32_t>> lvP, lvB, lvT;  // inter tiles, inter-intra blends, TBs per level
     std::vector<WorkItem> items;
     std::vector<Level> levels;
+    // k_flow dependencies: per 4x4 unit the node (TB / inter-intra item, decode order) that
+    // last wrote it (-1: nothing, or an inter tile of the preceding launch); per node its
+    // dependency nodes (CSR); then, in item order, the dependencies' item positions
+    std::vector<int32_t> owner[3];
+    std::vector<uint32_t> nodeDepStart;
+    std::vector<int32_t> nodeDeps, nodeOfTb, nodeOfBlk, nodePos;
+    std::vector<uint32_t> deps;
+    bool flowOk = false;
     // split submission (frame_begin / submit_tile / frame_end)
     bool inFrame = false;
     std::vector<uint8_t> fHdr;
@@ -300,7 +313,44 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         c->mapW[p] = (((h->mi_stride * 4) >> sub) + 64) / 4;
         c->mapH[p] = (((h->mi_rows_alloc * 4) >> sub) + 64) / 4;
         c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
+        c->owner[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
     }
+    c->nodeDepStart.assign(1, 0);
+    c->nodeDeps.clear();
+    c->nodeOfTb.assign(b->n_tbs, -1);
+    c->nodeOfBlk.assign(b->n_blocks, -1);
+    std::vector<int32_t> dl;  // dependencies of the node being built
+    auto owners = [&](int p, int x0, int y0, int x1, int y1) {  // inclusive 4x4-unit rect
+        x0 = std::max(x0, 0);
+        y0 = std::max(y0, 0);
+        x1 = std::min(x1, c->mapW[p] - 1);
+        y1 = std::min(y1, c->mapH[p] - 1);
+        for (int y = y0; y <= y1; y++) {
+            const int32_t* row = &c->owner[p][(size_t)y * c->mapW[p]];
+            int32_t last = -1;
+            for (int x = x0; x <= x1; x++)
+                if (row[x] >= 0 && row[x] != last) dl.push_back(last = row[x]);
+        }
+    };
+    auto edge_owners = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL) {
+        if (hA) owners(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2);
+        if (hL) owners(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2);
+    };
+    auto own_set = [&](int p, int x0, int y0, int w4, int h4, int32_t node) {
+        int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
+        for (int y = y0; y < y1; y++) {
+            int32_t* row = &c->owner[p][(size_t)y * c->mapW[p]];
+            for (int x = x0; x < x1; x++) row[x] = node;
+        }
+    };
+    auto end_node = [&]() {  // closes the node's dependency list; returns its id
+        std::sort(dl.begin(), dl.end());
+        dl.erase(std::unique(dl.begin(), dl.end()), dl.end());
+        c->nodeDeps.insert(c->nodeDeps.end(), dl.begin(), dl.end());
+        dl.clear();
+        c->nodeDepStart.push_back((uint32_t)c->nodeDeps.size());
+        return (int32_t)c->nodeDepStart.size() - 2;
+    };
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
         for (auto& l : *v) l.clear();
     auto region_max = [&](int p, int x0, int y0, int x1, int y1) {  // inclusive 4x4-unit rect
@@ -351,6 +401,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
                 for (int tx = 0; tx < (bw + 31) / 32; tx++)
                     push(c->lvP, pLevel, AV1R_ITEM(AV1R_ITEM_INTER, (bi << 4) | (ty << 2) | tx));
             blkLevel = pLevel;
+            int32_t iiNode = -1;
             if (isII) {
                 int dep = pLevel;
                 for (int p = 0; p < nPlanes; p++) {
@@ -358,18 +409,22 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
                     int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
                     bool hL = p ? (blk.flags & AV1R_BLK_AVAIL_L_UV) : (blk.flags & AV1R_BLK_AVAIL_L);
                     bool hA = p ? (blk.flags & AV1R_BLK_AVAIL_U_UV) : (blk.flags & AV1R_BLK_AVAIL_U);
-                    dep = std::max(dep, edge_level(p, (blk.mi_col >> sub) * 4, (blk.mi_row >> sub) * 4,
-                                            av1r_num4x4w[psz] * 4, av1r_num4x4h[psz] * 4, hL, hA,
-                                            (blk.ii_edge >> (2 * p)) & 1, (blk.ii_edge >> (2 * p + 1)) & 1));
+                    const int ex = (blk.mi_col >> sub) * 4, ey = (blk.mi_row >> sub) * 4;
+                    const int ew = av1r_num4x4w[psz] * 4, eh = av1r_num4x4h[psz] * 4;
+                    const bool hAR = (blk.ii_edge >> (2 * p)) & 1, hBL = (blk.ii_edge >> (2 * p + 1)) & 1;
+                    dep = std::max(dep, edge_level(p, ex, ey, ew, eh, hL, hA, hAR, hBL));
+                    edge_owners(p, ex, ey, ew, eh, hL, hA, hAR, hBL);
                 }
                 blkLevel = dep + 1;
                 push(c->lvB, blkLevel, AV1R_ITEM(AV1R_ITEM_II, bi));
+                iiNode = c->nodeOfBlk[bi] = end_node();
             }
             globalMax = std::max(globalMax, blkLevel);
             for (int p = 0; p < nPlanes; p++) {
                 int sub = p ? 1 : 0;
                 int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
                 region_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], blkLevel);
+                own_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], iiNode);
             }
         }
         int lumaMax = -1;  // CFL reads this block's reconstructed luma
@@ -381,14 +436,24 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             if (inter) {
                 if (!t.coef_cnt) continue;  // prediction only: nothing to add
                 lv = blkLevel + 1;
+                // the prediction it adds to: the inter tile (preceding launch) or the blend
+                if (c->nodeOfBlk[bi] >= 0) dl.push_back(c->nodeOfBlk[bi]);
             } else {
                 const bool pal = p ? blk.palette_size_uv : blk.palette_size_y;
                 int dep = -1;
                 if (!pal) {
-                    dep = edge_level(p, t.x, t.y, w, hh, t.flags & AV1R_TB_HAVE_LEFT, t.flags & AV1R_TB_HAVE_ABOVE,
-                                     t.flags & AV1R_TB_HAVE_AR, t.flags & AV1R_TB_HAVE_BL);
-                    if (p && blk.uv_mode == AV1R_UV_CFL_PRED)  // the co-located luma (incl. sub-8x8 neighbours)
-                        dep = std::max({dep, lumaMax, region_max(0, t.x >> 1, t.y >> 1, (2 * (t.x + w) - 1) >> 2, (2 * (t.y + hh) - 1) >> 2)});
+                    const bool hL = t.flags & AV1R_TB_HAVE_LEFT, hA = t.flags & AV1R_TB_HAVE_ABOVE;
+                    const bool hAR = t.flags & AV1R_TB_HAVE_AR, hBL = t.flags & AV1R_TB_HAVE_BL;
+                    dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
+                    edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
+                    if (p && blk.uv_mode == AV1R_UV_CFL_PRED) {  // the co-located luma (incl. sub-8x8 neighbours)
+                        const int lx0 = t.x >> 1, ly0 = t.y >> 1, lx1 = (2 * (t.x + w) - 1) >> 2, ly1 = (2 * (t.y + hh) - 1) >> 2;
+                        dep = std::max({dep, lumaMax, region_max(0, lx0, ly0, lx1, ly1)});
+                        owners(0, lx0, ly0, lx1, ly1);
+                        // (lumaMax: this block's luma TBs, all earlier nodes of the block)
+                        for (uint32_t tj = blk.first_tb; tj < ti; tj++)
+                            if (b->tbs[tj].plane == 0 && c->nodeOfTb[tj] >= 0) dl.push_back(c->nodeOfTb[tj]);
+                    }
                 }
                 lv = dep + 1;
             }
@@ -396,6 +461,8 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             push(c->lvT, lv, AV1R_ITEM(AV1R_ITEM_TB, ti));
             globalMax = std::max(globalMax, lv);
             region_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv);
+            const int32_t node = c->nodeOfTb[ti] = end_node();
+            own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, node);
         }
     }
     const size_t nl = (size_t)(globalMax + 1);
@@ -450,6 +517,43 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         }
     }
     c->nLevelsLast = (int)nl;
+    // k_flow: dependency lists as item positions (every dependency is an earlier item: it
+    // has a lower level); inter tiles after level 0 (intra block copy) keep the frame on
+    // the level launches
+    c->flowOk = true;
+    for (size_t l = 1; l < nl; l++) c->flowOk &= c->lvP[l].empty();
+    c->nodePos.assign(c->nodeDepStart.size() - 1, -1);
+    for (size_t i = 0; i < c->items.size(); i++) {
+        const uint32_t code = c->items[i].code;
+        const uint32_t idx = AV1R_ITEM_INDEX(code);
+        const int32_t node = AV1R_ITEM_KIND(code) == AV1R_ITEM_TB ? c->nodeOfTb[idx]
+                           : AV1R_ITEM_KIND(code) == AV1R_ITEM_II ? c->nodeOfBlk[idx] : -1;
+        if (node >= 0) c->nodePos[node] = (int32_t)i;
+    }
+    c->deps.clear();
+    for (size_t i = 0; i < c->items.size() && c->flowOk; i++) {
+        WorkItem& w = c->items[i];
+        const uint32_t code = w.code;
+        const uint32_t idx = AV1R_ITEM_INDEX(code);
+        const int32_t node = AV1R_ITEM_KIND(code) == AV1R_ITEM_TB ? c->nodeOfTb[idx]
+                           : AV1R_ITEM_KIND(code) == AV1R_ITEM_II ? c->nodeOfBlk[idx] : -1;
+        if (node < 0) continue;
+        const uint32_t d0 = c->nodeDepStart[node], d1 = c->nodeDepStart[node + 1];
+        if (d1 - d0 > 0xffff) {
+            c->flowOk = false;
+            break;
+        }
+        w.dep_off = (uint32_t)c->deps.size();
+        w.dep_cnt = (uint16_t)(d1 - d0);
+        for (uint32_t d = d0; d < d1; d++) {
+            const int32_t pos = c->nodePos[c->nodeDeps[d]];
+            if (pos < 0 || pos >= (int32_t)i) {  // cannot happen: levels order the items
+                c->flowOk = false;
+                break;
+            }
+            c->deps.push_back((uint32_t)pos);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -466,7 +570,9 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szCdef = align256((size_t)h->cdef_rows * h->cdef_cols);
     const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
     const size_t szItems = align256(sizeof(WorkItem) * c->items.size() + 4);
-    *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems;
+    const size_t szDeps = align256(4 * c->deps.size() + 4);
+    const size_t szDone = align256(4 * c->items.size() + 4);  // zeroed: no launch's epoch
+    *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone;
     if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {
@@ -486,6 +592,10 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.cdef_idx = (const int8_t*)put(b->cdef_idx, (size_t)h->cdef_rows * h->cdef_cols, szCdef);
     k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
     P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
+    k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);
+    memset(host + off, 0, szDone);
+    k.done = (uint32_t*)put(nullptr, 0, szDone);
+    P.flowOk = c->flowOk;
     k.mi_stride = h->mi_stride;
     k.mi_cols = h->mi_cols;
     k.mi_rows = h->mi_rows;
@@ -591,12 +701,29 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // offsets), k_tb table (large prefix, small prefix, large offsets, small offsets)]
     const size_t tabI = 2 * (size_t)n + 1, tabT = 4 * (size_t)n + 2, tabW = tabI + tabT;
     const size_t kBytes = align256(sizeof(KParams) * n);
-    const size_t need = kBytes + 4 * tabW * std::max<size_t>(nLevels, 1);
+    const size_t tabBytes = align256(4 * tabW * std::max<size_t>(nLevels, 1));
+    // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
+    static const bool flowEnv = !getenv("AV1R_FLOW") || atoi(getenv("AV1R_FLOW")) != 0;
+    bool flow = flowEnv && !lc->traceFile;
+    size_t nGroups = 0;
+    for (auto& j : jobs) {
+        flow &= j.P->flowOk;
+        for (const Level& lv : j.P->levels) nGroups += lv.cnt[1] + (lv.cnt[2] + 3) / 4;
+    }
+    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups : 0);
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % 2;
     if (M.pending) {
         HIPCHK(hipEventSynchronize(M.done));
         M.pending = false;
+        if (M.err && *M.err) {
+            *M.err = 0;
+            return fail(c, AV1R_E_DEVICE, "k_flow: a dependency wait timed out (output of an earlier batch is invalid)");
+        }
+    }
+    if (!M.err) {
+        HIPCHK(hipHostMalloc(&M.err, 256));
+        *M.err = 0;
     }
     if (M.cap < need) {
         if (M.host) (void)hipHostFree(M.host);
@@ -628,6 +755,28 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         total[l * 3 + 0] = ti[n];
         total[l * 3 + 1] = tt[n];
         total[l * 3 + 2] = tt[2 * n + 1];
+    }
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(M.dev + kBytes + tabBytes);
+    if (flow) {
+        // control block (zeroed) + the groups in topological order: level by level, the
+        // frames interleaved; {frame << 8 | n, first item}: n = 0 one large item, else
+        // 1..4 small items
+        memset(M.host + kBytes + tabBytes, 0, FLOW_CTL_BYTES);
+        uint32_t* g = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES);
+        for (size_t l = 0; l < nLevels; l++)
+            for (int i = 0; i < n; i++) {
+                const auto& lvs = jobs[i].P->levels;
+                if (l >= lvs.size()) continue;
+                const Level& lv = lvs[l];
+                for (uint32_t q = 0; q < lv.cnt[1]; q++, g += 2) {
+                    g[0] = (uint32_t)i << 8;
+                    g[1] = lv.off[1] + q;
+                }
+                for (uint32_t q = 0; q < lv.cnt[2]; q += 4, g += 2) {
+                    g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(4, lv.cnt[2] - q);
+                    g[1] = lv.off[2] + q;
+                }
+            }
     }
     HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
@@ -668,7 +817,19 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     unsigned long long* trace = lc->traceFile ? lc->traceDev : nullptr;
     uint32_t traceBase = 0;
-    for (size_t l = 0; l < nLevels; l++) {
+    static std::atomic<uint32_t> epochs{0};
+    if (flow) {
+        // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
+        if (total[0]) launch_k_level(0, slot, dtab, n, total[0], nullptr, 0, st);
+        if (nGroups) {
+            uint32_t epoch = ++epochs;
+            if (!epoch) epoch = ++epochs;
+            const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            launch_k_flow(slot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, st);
+            HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, st));
+        }
+    }
+    for (size_t l = 0; l < nLevels && !flow; l++) {
         const uint32_t nInter = total[l * 3], nLarge = total[l * 3 + 1], nSmall = total[l * 3 + 2];
         if (nInter) launch_k_level(0, slot, dtab + l * tabW, n, nInter, trace, traceBase, st);
         traceBase += nInter;
@@ -803,6 +964,7 @@ void av1r_destroy(av1r_ctx* c)
             Upload& u = ring[i];
             if (u.host) (void)hipHostFree(u.host);
             if (u.dev) (void)hipFree(u.dev);
+            if (u.err) (void)hipHostFree(u.err);
             (void)hipEventDestroy(u.done);
         }
     (void)hipEventDestroy(c->sync);

@@ -136,7 +136,7 @@ DEV const uint8_t* sm_weights(int log2) { return av1r_sm_weights + ((1 << log2) 
 // Gathers AboveRow / LeftCol (IntraPredict.cpp:571-611) of a (1<<log2W) x (1<<log2H)
 // prediction at (x, y) of plane `plane` into L (global loads only; the caller issues the
 // barrier before the edges are read, so independent loads can be overlapped with it).
-template <int NT>
+template <int NT, bool COH>
 DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
     int log2H, bool hL, bool hA, bool hAR, bool hBL, IntraLds& L)
 {
@@ -153,20 +153,20 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
     const int leftLimit = imin(maxY, y + (hBL ? 2 * h : h) - 1);
     for (int i = t; i < n; i += nt) {
         uint8_t a, l;
-        if (!hA && hL) a = px(src, x - 1, y);
+        if (!hA && hL) a = ldp<COH>(src, x - 1, y);
         else if (!hA && !hL) a = 127;
-        else a = px(src, imin(aboveLimit, x + i), y - 1);
-        if (!hL && hA) l = px(src, x, y - 1);
+        else a = ldp<COH>(src, imin(aboveLimit, x + i), y - 1);
+        if (!hL && hA) l = ldp<COH>(src, x, y - 1);
         else if (!hA && !hL) l = 129;
-        else l = px(src, x - 1, imin(leftLimit, y + i));
+        else l = ldp<COH>(src, x - 1, imin(leftLimit, y + i));
         above[i] = a;
         left[i] = l;
     }
     if (t == 0) {
         uint8_t c;
-        if (hA && hL) c = px(src, x - 1, y - 1);
-        else if (hA) c = px(src, x, y - 1);
-        else if (hL) c = px(src, x - 1, y);
+        if (hA && hL) c = ldp<COH>(src, x - 1, y - 1);
+        else if (hA) c = ldp<COH>(src, x, y - 1);
+        else if (hL) c = ldp<COH>(src, x - 1, y);
         else c = 128;
         above[-1] = c;
         left[-1] = c;
@@ -330,11 +330,11 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
 
 // Gather + predict (IntraPredict::predict_intra, IntraPredict.cpp:563-630).  Ends with a
 // coop_sync.
-template <int NT>
+template <int NT, bool COH>
 DEV void coop_intra_predict(int miCols, int miRows, const DevPlane& src, const IntraParams& P,
     IntraLds& L, uint8_t* pred, int ps)
 {
-    coop_intra_edges<NT>(miCols, miRows, src, P.plane, P.x, P.y, P.log2W, P.log2H, P.haveLeft, P.haveAbove, P.haveAR,
+    coop_intra_edges<NT, COH>(miCols, miRows, src, P.plane, P.x, P.y, P.log2W, P.log2H, P.haveLeft, P.haveAbove, P.haveAR,
         P.haveBL, L);
     coop_sync<NT>();
     coop_intra_from_edges<NT>(miCols, miRows, P, L, pred, ps);

@@ -45,8 +45,10 @@ DEV void trace_stamp(unsigned long long* tr, int slot)
 template <int MAX>
 struct TbLds {
     static constexpr int RS = MAX + 2;
-    int16_t res[MAX * RS];
+    static constexpr int CM = MAX > 32 ? 32 : MAX;  // largest chroma (CFL) transform side
+    int16_t res[MAX * RS];  // the final residual, flips applied (tb_residual)
     uint8_t pred[MAX * MAX];
+    int16_t cfl[CM * CM];   // CFL: the averaged co-located luma
     IntraLds intra;
     int sum;
 };
@@ -65,11 +67,13 @@ DEV void row_pass(int16_t* row, int w, int kind, int rectScale, int rowShift, in
 #pragma unroll
     for (int j = 0; j < (1 << n); j++) row[j] = (int16_t)CLIP3(-32768, 32767, r2(T[j], rowShift));
 }
-// Column pass fused with the reconstruction of one output column: out/pred point at
-// the column's row 0 (after the left-right flip); rows are written flipped if flipUD.
-template <int n, int RS, int PS>
-DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, const uint8_t* pred, uint8_t* out,
-    int stride, int flipUD)
+// Column pass of one column, written back as the final residual of output column `out`
+// (the left-right flip), rows flipped if flipUD.  Only ever one wave runs it (w <= 64), and
+// a wave's LDS accesses complete in order, so every lane has read its column before any
+// lane overwrites one.  The residual is saturated to int16: clip1(pred + r) is unchanged
+// by that for any 8-bit prediction.
+template <int n, int RS>
+DEV void col_pass(const int16_t* col, int16_t* out, int kind, int colShift, int lossless, int flipUD)
 {
     int T[1 << n];
 #pragma unroll
@@ -78,15 +82,16 @@ DEV void col_pass(const int16_t* col, int kind, int colShift, int lossless, cons
 #pragma unroll
     for (int yy = 0; yy < (1 << n); yy++) {
         const int i = flipUD ? (1 << n) - 1 - yy : yy;
-        out[i * stride] = (uint8_t)clip1(pred[i * PS] + r2(T[yy], colShift));
+        out[i * RS] = (int16_t)CLIP3(-32768, 32767, r2(T[yy], colShift));
     }
 }
 
-// reconstruct() + inverseTransform() (TransformBlock.cpp:2173-2276), the flip and the
-// add-and-clip onto the prediction in L.pred, stored to the frame at (x, y).
+// reconstruct() + inverseTransform() (TransformBlock.cpp:2173-2276) into L.res, flips
+// applied.  Reads only the batch (coefficients, block record), never the frame: the
+// dataflow kernel runs it before the item's dependencies are complete.  c0: the lane's
+// first coefficient, prefetched by the caller.  Ends with a coop_sync.
 template <int NT, int MAX>
-DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk, TbLds<MAX>& L, const DevPlane& dst,
-    uint32_t c0, bool zeroed, unsigned long long* tr)
+DEV void tb_residual(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, uint32_t c0)
 {
     constexpr int RS = TbLds<MAX>::RS;
     const int t = coop_lane<NT>();
@@ -95,11 +100,8 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
     const int log2W = av1r_tx_w_log2[txSz], log2H = av1r_tx_h_log2[txSz];
     const int tw = imin(w, 32), th = imin(h, 32);
     const av1r_frame_hdr& hd = *k.hdr;
-    if (!zeroed) {
-        for (int q = t; q < th * w; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
-        coop_sync<NT>();
-    }
-    trace_stamp(tr, 11);
+    for (int q = t; q < th * w; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
+    coop_sync<NT>();
     int dqDenom = 1;
     if (txSz == AV1R_TX_32X32 || txSz == AV1R_TX_16X32 || txSz == AV1R_TX_32X16 || txSz == AV1R_TX_16X64 || txSz == AV1R_TX_64X16)
         dqDenom = 2;
@@ -120,7 +122,6 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         L.res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
     }
     coop_sync<NT>();
-    trace_stamp(tr, 12);
     const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
     const int type = tb.tx_type;
     const int rowShift = lossless ? 0 : av1r_tx_row_shift[txSz];
@@ -142,69 +143,37 @@ DEV void tb_residual(const KParams& k, const av1r_tb& tb, const av1r_block& blk,
         for (int j = 0; j < w; j++) row[j] = 0;
     }
     coop_sync<NT>();
-    trace_stamp(tr, 13);
     const int flipUD = type == AV1R_FLIPADST_DCT || type == AV1R_FLIPADST_ADST || type == AV1R_V_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     const int flipLR = type == AV1R_DCT_FLIPADST || type == AV1R_ADST_FLIPADST || type == AV1R_H_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     if (t < w) {
         const int16_t* col = L.res + t;
-        const int j = flipLR ? w - 1 - t : t;
-        const uint8_t* pred = L.pred + j;
-        uint8_t* out = dst.p + (size_t)tb.y * dst.stride + tb.x + j;
+        int16_t* out = L.res + (flipLR ? w - 1 - t : t);
         switch (log2H) {
-        case 2: col_pass<2, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        case 3: col_pass<3, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        case 4: col_pass<4, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        case 5: if constexpr (MAX >= 32) col_pass<5, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
-        default: if constexpr (MAX >= 64) col_pass<6, RS, MAX>(col, ck, colShift, lossless, pred, out, dst.stride, flipUD); break;
+        case 2: col_pass<2, RS>(col, out, ck, colShift, lossless, flipUD); break;
+        case 3: col_pass<3, RS>(col, out, ck, colShift, lossless, flipUD); break;
+        case 4: col_pass<4, RS>(col, out, ck, colShift, lossless, flipUD); break;
+        case 5: if constexpr (MAX >= 32) col_pass<5, RS>(col, out, ck, colShift, lossless, flipUD); break;
+        default: if constexpr (MAX >= 64) col_pass<6, RS>(col, out, ck, colShift, lossless, flipUD); break;
         }
     }
+    coop_sync<NT>();
 }
 
-// One transform block (TransformBlock::decode, TransformBlock.cpp:2400-2456).  The
-// item record carries the TB, so its first coefficients and its prediction inputs (intra
-// edges or the inter-predicted pixels) are in flight before the block record is read.
-template <int NT, int MAX>
-DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned long long* tr)
+// The prediction of an intra or palette transform block into L.pred (TransformBlock::decode,
+// TransformBlock.cpp:2400-2420): palette colours (Block.cpp:2279-2298), or
+// IntraPredict::predict_intra with CFL (IntraPredict.cpp:563-667).  Inter TBs predict
+// nothing here (their prediction is already in the frame).  Ends with a coop_sync.
+template <int NT, int MAX, bool COH>
+DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L)
 {
-    constexpr int RS = TbLds<MAX>::RS;
+    constexpr int CM = TbLds<MAX>::CM;
     const int t = coop_lane<NT>();
-    av1r_tb tb;
-    tb.block = wi.block;
-    tb.coef_off = wi.coef_off;
-    tb.x = wi.x;
-    tb.y = wi.y;
-    tb.coef_cnt = wi.coef_cnt;
-    tb.plane = wi.plane;
-    tb.tx_size = wi.tx_size;
-    tb.tx_type = wi.tx_type;
-    tb.flags = wi.flags;
     const int plane = tb.plane, x = tb.x, y = tb.y, txSz = tb.tx_size;
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
     const int log2W = av1r_tx_w_log2[txSz];
     const DevPlane& dst = k.cur.pl[plane];
-    const int src = wi.pred;
-    const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
-    if (src == AV1R_PRED_INTRA)
-        coop_intra_edges<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
-            (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
-            (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
-    const av1r_block& blk = k.blocks[tb.block];
     const uint32_t bflags = blk.flags;
-    const av1r_frame_hdr& hd = *k.hdr;
-    // the residual tile is cleared under the prediction (CFL borrows it as scratch first)
-    const bool zeroEarly = tb.coef_cnt && !(plane > 0 && src == AV1R_PRED_INTRA && blk.uv_mode == AV1R_UV_CFL_PRED);
-    if (zeroEarly) {
-        const int tw2 = w, th2 = imin(h, 32);
-        for (int q = t; q < th2 * tw2; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
-    }
-
-    if (src == AV1R_PRED_INTER) {
-        for (int q = t; q < w * h; q += NT) {
-            int i = q >> log2W, j = q & (w - 1);
-            L.pred[i * MAX + j] = px(dst, x + j, y + i);
-        }
-    } else if (src == AV1R_PRED_PALETTE) {
-        // Block::Palette::predict_palette (Block.cpp:2279-2298)
+    if (tb.pred == AV1R_PRED_PALETTE) {
         const uint8_t* ph = k.palette + blk.palette_off;
         int bx = x - (blk.mi_col >> (plane ? 1 : 0)) * 4, by = y - (blk.mi_row >> (plane ? 1 : 0)) * 4;
         int mw = plane ? ph[2] : ph[0];
@@ -214,7 +183,10 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
             int i = q >> log2W, j = q & (w - 1);
             L.pred[i * MAX + j] = colors[map[(by + i) * mw + bx + j]];
         }
-    } else {
+    } else if (tb.pred == AV1R_PRED_INTRA) {
+        coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+            (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
+            (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
         const int isCfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
         IntraParams P;
         P.plane = plane;
@@ -232,24 +204,25 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
         P.filterIntraMode = blk.filter_intra_mode;
         P.smooth = plane ? ((bflags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
                          : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
-        P.edgeFilter = hd.enable_intra_edge_filter;
-        coop_sync<NT>();  // edges gathered
-        trace_stamp(tr, 8);
-        coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, MAX);
-        trace_stamp(tr, 9);
+        P.edgeFilter = k.hdr->enable_intra_edge_filter;
+        int s = 0;
         if (isCfl) {
-            // predict_chroma_from_luma (IntraPredict.cpp:632-667)
+            // predict_chroma_from_luma (IntraPredict.cpp:632-667): the luma loads go out
+            // together with the edge loads
             const DevPlane& luma = k.cur.pl[0];
-            const int alpha = plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v;
             const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
-            int s = 0;
             for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
                 int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
-                int v = (px(luma, lx, ly) + px(luma, lx + 1, ly) + px(luma, lx, ly + 1) + px(luma, lx + 1, ly + 1)) << 1;
-                L.res[i * RS + j] = (int16_t)v;  // res is free until the residual pass
+                int v = (ldp<COH>(luma, lx, ly) + ldp<COH>(luma, lx + 1, ly) + ldp<COH>(luma, lx, ly + 1) +
+                            ldp<COH>(luma, lx + 1, ly + 1)) << 1;
+                L.cfl[i * CM + j] = (int16_t)v;
                 s += v;
             }
+        }
+        coop_sync<NT>();  // edges gathered
+        coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, MAX);
+        if (isCfl) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
             if (NT > 64) {  // across the waves of the workgroup
@@ -259,24 +232,61 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
                 coop_sync<NT>();
                 s = L.sum;
             }
+            const int alpha = plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v;
             const int avg = r2(s, log2W + P.log2H);
             for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
                 int dc = L.pred[i * MAX + j];
-                L.pred[i * MAX + j] = (uint8_t)clip1(dc + r2s(alpha * (L.res[i * RS + j] - avg), 6));
+                L.pred[i * MAX + j] = (uint8_t)clip1(dc + r2s(alpha * (L.cfl[i * CM + j] - avg), 6));
             }
         }
     }
     coop_sync<NT>();
-    trace_stamp(tr, 4);
-    if (tb.coef_cnt) {
-        tb_residual<NT, MAX>(k, tb, blk, L, dst, c0, zeroEarly, tr);
-    } else if (src != AV1R_PRED_INTER) {
-        for (int q = t; q < w * h; q += NT) {
-            int i = q >> log2W, j = q & (w - 1);
-            px(dst, x + j, y + i) = L.pred[i * MAX + j];
+}
+
+// Add and clip (TransformBlock.cpp:2440-2456) four samples per lane with dword frame
+// accesses: prediction from L.pred (intra / palette) or from the frame (inter), plus the
+// residual in L.res when the TB has coefficients.
+template <int NT, int MAX, bool COH>
+DEV void tb_store(const KParams& k, const WorkItem& tb, TbLds<MAX>& L)
+{
+    constexpr int RS = TbLds<MAX>::RS;
+    const int t = coop_lane<NT>();
+    const int txSz = tb.tx_size;
+    const int l2q = av1r_tx_w_log2[txSz] - 2;  // log2 of the dwords per row
+    const int nq = (av1r_tx_w[txSz] * av1r_tx_h[txSz]) >> 2;
+    const DevPlane& dst = k.cur.pl[tb.plane];
+    const bool hasRes = tb.coef_cnt != 0;
+    for (int q = t; q < nq; q += NT) {
+        const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
+        const uint32_t p = tb.pred == AV1R_PRED_INTER ? ldp4<COH>(dst, tb.x + j, tb.y + i)
+                                                      : *reinterpret_cast<const uint32_t*>(&L.pred[i * MAX + j]);
+        uint32_t o = p;
+        if (hasRes) {
+            const uint32_t r01 = *reinterpret_cast<const uint32_t*>(&L.res[i * RS + j]);
+            const uint32_t r23 = *reinterpret_cast<const uint32_t*>(&L.res[i * RS + j + 2]);
+            const int r[4] = {(int16_t)(r01 & 0xffff), (int16_t)(r01 >> 16), (int16_t)(r23 & 0xffff), (int16_t)(r23 >> 16)};
+            o = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) o |= (uint32_t)clip1((int)((p >> (8 * b)) & 0xff) + r[b]) << (8 * b);
         }
+        stp4<COH>(dst, tb.x + j, tb.y + i, o);
     }
+}
+
+// One transform block of the level launches (TransformBlock::decode,
+// TransformBlock.cpp:2400-2456): the prediction inputs are final before the launch.
+template <int NT, int MAX>
+DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned long long* tr)
+{
+    const int t = coop_lane<NT>();
+    const uint32_t c0 = t < wi.coef_cnt ? k.coefs[wi.coef_off + t] : 0u;
+    const av1r_block& blk = k.blocks[wi.block];
+    tb_predict<NT, MAX, false>(k, wi, blk, L);
+    trace_stamp(tr, 4);
+    if (wi.coef_cnt) tb_residual<NT, MAX>(k, wi, blk, L, c0);
+    trace_stamp(tr, 13);
+    tb_store<NT, MAX, false>(k, wi, L);
 }
 
 // ---------------------------------------------------------------------------------
@@ -949,7 +959,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
 // Inter-intra blend of block `bi` (Block.cpp:118-144 + maskBlend, InterPredict.cpp:555-609):
 // the block's intra prediction (its edges are final when this item runs) blended with the
 // inter prediction inter_tile stored in the frame.
-template <int NT>
+template <int NT, bool COH>
 DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
 {
     const int t = coop_lane<NT>();
@@ -983,7 +993,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
         P.filterIntraMode = 0;
         P.smooth = 0;
         P.edgeFilter = k.hdr->enable_intra_edge_filter;
-        coop_intra_predict<NT>(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
+        coop_intra_predict<NT, COH>(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
         const int sizeScale = 128 / imax(ph, pw);
         for (int q = t; q < pw * ph; q += NT) {
             const int i = q / pw, j = q - i * pw;
@@ -1006,8 +1016,8 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
                     }
                 m = r2(s4, 2);
             }
-            uint8_t& d = px(dst, baseX + j, baseY + i);
-            d = (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6));
+            const int d = ldp<COH>(dst, baseX + j, baseY + i);
+            stp<COH>(dst, baseX + j, baseY + i, (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6)));
         }
         coop_sync<NT>();
     }
@@ -1069,7 +1079,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
         trace_stamp(tr, 2);  // (after the item record: entry and record stamps coincide)
         trace_stamp(tr, 3);
         TbLds<64>& L = *reinterpret_cast<TbLds<64>*>(smem);
-        if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) ii_item<256>(*kp, AV1R_ITEM_INDEX(wi.code), L);
+        if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) ii_item<256, false>(*kp, AV1R_ITEM_INDEX(wi.code), L);
         else tb_item<256, 64>(*kp, wi, L, tr);
         trace_stamp(tr, 5);
         return;
@@ -1121,6 +1131,140 @@ extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_
     trace_stamp(tr, 3);
     inter_tile(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
     trace_stamp(tr, 5);
+}
+
+// ---------------------------------------------------------------------------------
+// k_flow: all transform-block and inter-intra items of a batch in ONE persistent launch,
+// ordered by their data dependencies instead of by one launch per level.
+//
+// The host lists the items' groups (one large item, or up to four small ones: the same
+// packing as k_tb) in a topological order: level by level, frames interleaved.  Group g
+// belongs to queue g % 8; workgroup b pulls queue b % 8's next group with one atomic add,
+// so a queue's groups are taken in order.  Every item waits only for items of EARLIER
+// groups (its dependency list, built by the host from the 4x4 units whose pixels it reads:
+// intra edges, CFL luma, the inter-intra prediction), so the earliest unfinished group is
+// either held by a running workgroup whose dependencies are all complete, or is the next
+// group of a queue whose workgroups are all free: the launch always progresses, whatever
+// the residency, as long as each queue has one resident workgroup (grid >= 8, dealt
+// round-robin).
+//
+// Hand-off between items (cdna_hip_programming.md §6 Guideline 16, R1): a producer stores
+// its pixels write-through (stp/stp4<true>: sc1), every storing wave drains them
+// (s_waitcnt vmcnt(0)), then one lane stores the item's done word = the launch's epoch
+// (sc1).  A consumer polls its dependencies' done words (one lane each, sc1 loads), then
+// reads every pixel another item of the launch may have written with sc1 loads (ldp /
+// ldp4<true>), which bypass the CU's L1.  The residual of a TB reads only the batch, so it
+// is computed BEFORE the wait, off the dependency chain.  Every spin is bounded: after
+// FLOW_TIMEOUT ticks (or once any wave has timed out) the wave gives up and sets the
+// launch's error word, which the host reports.
+// ---------------------------------------------------------------------------------
+#define FLOW_TIMEOUT 100000000ull  // 1 s of the 100 MHz real-time counter
+
+template <int NT>
+DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint32_t epoch, uint32_t* ctl)
+{
+    if (nd && (NT == 64 || threadIdx.x < 64)) {
+        const int lane = threadIdx.x & 63;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t b = 0; b < nd; b += 64) {
+            const bool mine = b + lane < nd;
+            const uint32_t d = mine ? deps[b + lane] : 0u;
+            for (;;) {
+                const bool ok = !mine || __hip_atomic_load(done + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+                if (__all(ok)) break;
+                const bool dead = __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (dead || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT) {
+                    if (lane == 0) __hip_atomic_store(ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    b = nd;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    if (NT > 64) __syncthreads();
+    asm volatile("" ::: "memory");  // no pixel load moves above the poll
+}
+
+// every storing wave drains its write-through stores, then one lane publishes
+template <int NT>
+DEV void flow_publish(uint32_t* flag, uint32_t epoch)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NT > 64) __syncthreads();
+    if (coop_lane<NT>() == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NT, int MAX>
+DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl)
+{
+    const WorkItem& wi = k.items[pos];
+    if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
+        if constexpr (MAX == 64) {  // blends are always large items
+            flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L);
+        }
+    } else {
+        const int t = coop_lane<NT>();
+        const uint32_t c0 = t < wi.coef_cnt ? k.coefs[wi.coef_off + t] : 0u;
+        const av1r_block& blk = k.blocks[wi.block];
+        if (wi.coef_cnt) tb_residual<NT, MAX>(k, wi, blk, L, c0);
+        flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+        tb_predict<NT, MAX, true>(k, wi, blk, L);
+        tb_store<NT, MAX, true>(k, wi, L);
+    }
+    flow_publish<NT>(k.done + pos, epoch);
+}
+
+// groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
+// workgroup), n = 1..4 small items (one per wave)
+extern "C" __global__ __launch_bounds__(256) void k_flow(int slot, const uint2* __restrict__ groups, uint32_t nGroups,
+    uint32_t* ctl, uint32_t epoch)
+{
+    constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
+    __shared__ __align__(16) uint8_t smem[kLds];
+    __shared__ uint32_t ticket;
+    const uint32_t q = blockIdx.x % FLOW_QUEUES;
+    for (;;) {
+        if (threadIdx.x == 0)
+            ticket = __hip_atomic_fetch_add(ctl + q * FLOW_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t g = __builtin_amdgcn_readfirstlane(ticket) * FLOW_QUEUES + q;
+        if (g >= nGroups) return;
+        const uint2 gd = groups[g];
+        const KParams& k = g_kp[slot][gd.x >> 8];
+        const uint32_t n = gd.x & 0xff;
+        if (n == 0) {
+            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl);
+        } else {
+            const uint32_t wave = threadIdx.x >> 6;
+            if (wave < n) flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl);
+        }
+        __syncthreads();  // the LDS tiles and `ticket` are free again
+    }
+}
+
+// persistent grid of k_flow on `device`: every CU's resident workgroups (capped at 8 per
+// CU), a multiple of FLOW_QUEUES
+int flow_grid(int device)
+{
+    static int cache[64] = {};
+    if (device < 0 || device >= 64) return FLOW_QUEUES;
+    if (!cache[device]) {
+        int cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 32;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k_flow), 256, 0) != hipSuccess || per <= 0)
+            per = 1;
+        per = per > 8 ? 8 : per;
+        cache[device] = ((cus * per) / FLOW_QUEUES) * FLOW_QUEUES;
+        if (cache[device] < FLOW_QUEUES) cache[device] = FLOW_QUEUES;
+    }
+    return cache[device];
+}
+
+void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, slot, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch);
 }
 
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4)
