@@ -93,7 +93,14 @@ DEV int floor_log2(int x) { return x > 0 ? 31 - __builtin_clz((unsigned)x) : -1;
 // (NT = 64 inside a larger workgroup, one item per wave: wave-level synchronisation --
 // a wave's LDS operations complete in order, so only the compiler must not reorder).
 template <int NT>
-DEV int coop_lane() { return NT == 64 ? (int)(threadIdx.x & 63) : (int)threadIdx.x; }
+DEV int coop_lane()
+{
+    // opaque to the optimiser: in k_flow's persistent loop, lane-derived addresses would
+    // otherwise be hoisted out of the loop for every code path and kept live (2x VGPRs)
+    int t = NT == 64 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
 template <int NT>
 DEV void coop_sync()
 {

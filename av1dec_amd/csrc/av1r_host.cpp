@@ -38,6 +38,8 @@ int kpf_upload(int device, const KParams* host, int n, hipStream_t s);
 int kpf_release(int device, int slot, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 int flow_grid(int device);
+int kpw_upload(int device, const KParams* host, int n, hipStream_t s);
+int kpw_release(int device, int slot, hipStream_t s);
 void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid, hipStream_t s);
 
 namespace {
@@ -825,7 +827,10 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
             const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
-            launch_k_flow(slot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, st);
+            const int wslot = kpw_upload(lc->device, hk, n, st);
+            if (wslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
+            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, st);
+            if (kpw_release(lc->device, wslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
             HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, st));
         }
     }

@@ -1028,8 +1028,20 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
 // intra blends, transform blocks) is one 64-lane workgroup.
 // ---------------------------------------------------------------------------------
 // Frame parameters of a launch: constant-address-space slots (kp_const.h).
+// recon.hip is compiled twice (native.py): the level kernels (k_inter, k_tb), and with
+// -DAV1R_FLOW_PART k_flow alone -- built without machine-level loop-invariant hoisting,
+// which in its persistent loop keeps ~50 constants in VGPRs (177 instead of 124 VGPRs:
+// half the occupancy) but which k_inter's pixel loops want.  Each object has its own
+// constant-memory parameter table.
+#define TB_SMALL 16  // the largest TB side handled one per wave (k_tb, k_flow)
+#ifndef AV1R_FLOW_PART
 AV1R_KP_TABLE(g_kp, kp_upload, kp_release)
+#else
+AV1R_KP_TABLE(g_kpw, kpw_upload, kpw_release)
+#define g_kp g_kpw
+#endif
 
+#ifndef AV1R_FLOW_PART
 // Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
 // counts; tab[n + 1 + s]: offset of frame s's items in its item list).  `lane` indexes the
 // table (one lane per frame); item `b` of the launch.  Returns the frame's parameters.
@@ -1049,7 +1061,6 @@ DEV const WorkItem& table_item(int slot, const uint32_t* __restrict__ tab, int n
 // more, and the blends) take a whole 256-lane workgroup each; small TBs (up to 16x16) are
 // packed four per workgroup, one per wave, each wave with its own small LDS tiles.
 // tab: [big prefix (n + 1)][small prefix (n + 1)][big offsets (n)][small offsets (n)].
-#define TB_SMALL 16
 extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
 {
@@ -1133,6 +1144,9 @@ extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_
     trace_stamp(tr, 5);
 }
 
+#endif  // !AV1R_FLOW_PART
+
+#ifdef AV1R_FLOW_PART
 // ---------------------------------------------------------------------------------
 // k_flow: all transform-block and inter-intra items of a batch in ONE persistent launch,
 // ordered by their data dependencies instead of by one launch per level.
@@ -1218,19 +1232,26 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
 // workgroup), n = 1..4 small items (one per wave)
-extern "C" __global__ __launch_bounds__(256) void k_flow(int slot, const uint2* __restrict__ groups, uint32_t nGroups,
+extern "C" __global__ __launch_bounds__(256, 4) void k_flow(int slot, const uint2* __restrict__ groups, uint32_t nGroups,
     uint32_t* ctl, uint32_t epoch)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
     __shared__ __align__(16) uint8_t smem[kLds];
-    __shared__ uint32_t ticket;
+    __shared__ uint32_t ticket[2];  // double-buffered: a slow wave may still read the old one
     const uint32_t q = blockIdx.x % FLOW_QUEUES;
-    for (;;) {
-        if (threadIdx.x == 0)
-            ticket = __hip_atomic_fetch_add(ctl + q * FLOW_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const uint32_t g = __builtin_amdgcn_readfirstlane(ticket) * FLOW_QUEUES + q;
+    uint32_t* head = ctl + q * FLOW_LINE;
+    if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    for (uint32_t it = 0;; it ^= 1) {
+        const uint32_t g = __builtin_amdgcn_readfirstlane(ticket[it]) * FLOW_QUEUES + q;
         if (g >= nGroups) return;
+        // AV1R_TICKET_PREFETCH: take the next ticket before running this group (holding it
+        // early keeps the progress argument: a held group waits only for earlier ones);
+        // measured no faster, so off
+        uint32_t next = 0;
+#ifdef AV1R_TICKET_PREFETCH
+        if (threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         const uint2 gd = groups[g];
         const KParams& k = g_kp[slot][gd.x >> 8];
         const uint32_t n = gd.x & 0xff;
@@ -1240,7 +1261,11 @@ extern "C" __global__ __launch_bounds__(256) void k_flow(int slot, const uint2* 
             const uint32_t wave = threadIdx.x >> 6;
             if (wave < n) flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl);
         }
-        __syncthreads();  // the LDS tiles and `ticket` are free again
+#ifndef AV1R_TICKET_PREFETCH
+        if (threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        if (threadIdx.x == 0) ticket[it ^ 1] = next;
+        __syncthreads();  // the LDS tiles are free again; the next ticket is published
     }
 }
 
@@ -1267,6 +1292,9 @@ void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl
     hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, slot, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch);
 }
 
+#endif  // AV1R_FLOW_PART
+
+#ifndef AV1R_FLOW_PART
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4)
 void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
@@ -1274,3 +1302,4 @@ void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned ite
     if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
     else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, slot, tab, n, trace, traceBase);
 }
+#endif  // !AV1R_FLOW_PART
