@@ -55,7 +55,15 @@ struct KParams {
     const WorkItem* items;  // this frame's level-ordered work items
     const uint32_t* deps;   // k_flow: dependency lists (positions in items)
     uint32_t* done;         // k_flow: per item, the epoch of the launch that completed it
+    // k_flow mode: residuals precomputed by k_resid.  tb_res[tb]: the TB's residual tile
+    // (w x h int16, row-major) at res + tb_res[tb], or ~0u (no coefficients, or an inter
+    // TB outside an inter-intra block: k_resid adds it into the frame directly)
+    const uint32_t* tb_res;
+    int16_t* res;
+    const uint32_t* resid_s;  // TBs with coefficients and sides <= 16 (16 per workgroup, ~0u pads)
+    const uint32_t* resid_l;  // the larger ones
     uint32_t n_items;
+    uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;
     int mi_cols, mi_rows;
     int frame_w, frame_h;
@@ -89,22 +97,23 @@ DEV int imax(int a, int b) { return a > b ? a : b; }
 DEV int floor_log2_u64(uint64_t x) { return x ? 63 - __builtin_clzll(x) : -1; }
 DEV int floor_log2(int x) { return x > 0 ? 31 - __builtin_clz((unsigned)x) : -1; }
 
-// Cooperating lanes of one work item: the whole workgroup (NT = blockDim.x) or one wave
-// (NT = 64 inside a larger workgroup, one item per wave: wave-level synchronisation --
-// a wave's LDS operations complete in order, so only the compiler must not reorder).
+// Cooperating lanes of one work item: the whole workgroup (NT = blockDim.x = 256), one
+// wave (NT = 64, several items per workgroup), or a 16-lane quarter of a wave (NT = 16,
+// k_resid_s).  Below a workgroup, synchronisation is wave-level: a wave's LDS operations
+// complete in order, so only the compiler must not reorder.
 template <int NT>
 DEV int coop_lane()
 {
     // opaque to the optimiser: in k_flow's persistent loop, lane-derived addresses would
     // otherwise be hoisted out of the loop for every code path and kept live (2x VGPRs)
-    int t = NT == 64 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    int t = NT >= 256 ? (int)threadIdx.x : (int)(threadIdx.x & (NT - 1));
     asm volatile("" : "+v"(t));
     return t;
 }
 template <int NT>
 DEV void coop_sync()
 {
-    if (NT == 64) {
+    if (NT <= 64) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

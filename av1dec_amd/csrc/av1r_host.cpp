@@ -38,9 +38,11 @@ int kpf_upload(int device, const KParams* host, int n, hipStream_t s);
 int kpf_release(int device, int slot, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 int flow_grid(int device);
+void launch_k_resid(int large, int slot, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
 int kpw_upload(int device, const KParams* host, int n, hipStream_t s);
 int kpw_release(int device, int slot, hipStream_t s);
-void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid, hipStream_t s);
+void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid,
+    unsigned long long* trace, hipStream_t s);
 
 namespace {
 
@@ -62,8 +64,10 @@ struct Upload {
 
 struct Level {
     // items [off, off + cnt): [0] inter tiles (k_inter); k_tb's [1] large items (inter-intra
-    // blends, TBs with a side >= 32: a workgroup each) and [2] small TBs (one per wave)
-    uint32_t off[3] = {}, cnt[3] = {};
+    // blends, TBs with a side >= 32: a workgroup each) and [2] small TBs (one per wave).
+    // Within [1] and [2] the inter TBs come last: k_flow takes the first fcnt (inter TBs
+    // are finished by k_resid there)
+    uint32_t off[3] = {}, cnt[3] = {}, fcnt[3] = {};
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -80,6 +84,8 @@ struct Prepared {
     const WorkItem* dItems = nullptr;
     std::vector<Level> levels;
     bool flowOk = false;  // k_flow can run it: no inter tile after level 0 (intra block copy)
+    uint32_t nResidS = 0, nResidL = 0;  // k_resid workgroups (16 TBs / 1 TB each)
+    size_t resElems = 0;                // int16 residual tiles of the frame
     bool usedRef[8] = {};
     uint64_t bytes = 0;
 };
@@ -116,6 +122,10 @@ struct av1r_ctx {
     std::vector<int32_t> nodeDeps, nodeOfTb, nodeOfBlk, nodePos;
     std::vector<uint32_t> deps;
     bool flowOk = false;
+    // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
+    // the small and large TB lists, the tiles' total size
+    std::vector<uint32_t> tbRes, residS, residL;
+    size_t resElems = 0;
     // split submission (frame_begin / submit_tile / frame_end)
     bool inFrame = false;
     std::vector<uint8_t> fHdr;
@@ -139,6 +149,8 @@ struct av1r_ctx {
     bool discardOutput = false;  // bench: shown frames are not queued for read-back
     Prepared streamP;
     std::vector<Prepared*> prepared;
+    int16_t* resDev = nullptr;  // k_flow mode: the frame's residual tiles (k_resid)
+    size_t resCap = 0;
 };
 
 static int fail(av1r_ctx* c, int code, const char* fmt, ...)
@@ -464,7 +476,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             globalMax = std::max(globalMax, lv);
             region_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv);
             const int32_t node = c->nodeOfTb[ti] = end_node();
-            own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, node);
+            // an inter TB's pixels are final before k_flow (k_inter + k_resid) unless the
+            // block is inter-intra, whose blend item adds the residuals
+            if (!inter) own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, node);
         }
     }
     const size_t nl = (size_t)(globalMax + 1);
@@ -479,15 +493,30 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             const av1r_tb& t = b->tbs[AV1R_ITEM_INDEX(code)];
             return av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
         };
+        auto interTb = [&](uint32_t code) { return (b->blocks[b->tbs[AV1R_ITEM_INDEX(code)].block].flags & AV1R_BLK_INTER) != 0; };
         std::vector<uint32_t>& T = c->lvT[l];
-        std::stable_partition(T.begin(), T.end(), large);
-        const uint32_t nLargeT = (uint32_t)std::count_if(T.begin(), T.end(), large);
+        // [large intra][large inter][small intra][small inter]
+        std::stable_sort(T.begin(), T.end(), [&](uint32_t a, uint32_t b2) {
+            return (large(a) ? 0 : 2) + interTb(a) < (large(b2) ? 0 : 2) + interTb(b2);
+        });
+        uint32_t nLargeT = 0, nLargeIntra = 0, nSmallIntra = 0;
+        for (uint32_t code : T) {
+            if (large(code)) {
+                nLargeT++;
+                nLargeIntra += !interTb(code);
+            } else {
+                nSmallIntra += !interTb(code);
+            }
+        }
         c->levels[l].off[0] = (uint32_t)c->items.size();
         c->levels[l].cnt[0] = (uint32_t)c->lvP[l].size();
         c->levels[l].off[1] = c->levels[l].off[0] + c->levels[l].cnt[0];
         c->levels[l].cnt[1] = (uint32_t)c->lvB[l].size() + nLargeT;
         c->levels[l].off[2] = c->levels[l].off[1] + c->levels[l].cnt[1];
         c->levels[l].cnt[2] = (uint32_t)T.size() - nLargeT;
+        c->levels[l].fcnt[0] = 0;
+        c->levels[l].fcnt[1] = (uint32_t)c->lvB[l].size() + nLargeIntra;
+        c->levels[l].fcnt[2] = nSmallIntra;
         for (auto* v : {&c->lvP, &c->lvB, &c->lvT}) {
             for (uint32_t code : (*v)[l]) {
                 WorkItem w;
@@ -519,10 +548,28 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         }
     }
     c->nLevelsLast = (int)nl;
+    // k_resid: residual tiles for intra TBs and the TBs of inter-intra blocks; the other
+    // inter TBs are added in place
+    c->tbRes.assign(b->n_tbs, ~0u);
+    c->residS.clear();
+    c->residL.clear();
+    c->resElems = 0;
+    for (uint32_t ti = 0; ti < b->n_tbs; ti++) {
+        const av1r_tb& t = b->tbs[ti];
+        if (!t.coef_cnt) continue;
+        const int w = av1r_tx_w[t.tx_size], hh = av1r_tx_h[t.tx_size];
+        const bool inPlace = (b->blocks[t.block].flags & AV1R_BLK_INTER) && c->nodeOfBlk[t.block] < 0;
+        if (!inPlace) {
+            c->tbRes[ti] = (uint32_t)c->resElems;
+            c->resElems += (size_t)w * hh;
+        }
+        (w <= 16 && hh <= 16 ? c->residS : c->residL).push_back(ti);
+    }
+    while (c->residS.size() % 16) c->residS.push_back(~0u);
     // k_flow: dependency lists as item positions (every dependency is an earlier item: it
     // has a lower level); inter tiles after level 0 (intra block copy) keep the frame on
     // the level launches
-    c->flowOk = true;
+    c->flowOk = c->resElems < 0xffffffffu;
     for (size_t l = 1; l < nl; l++) c->flowOk &= c->lvP[l].empty();
     c->nodePos.assign(c->nodeDepStart.size() - 1, -1);
     for (size_t i = 0; i < c->items.size(); i++) {
@@ -574,7 +621,10 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szItems = align256(sizeof(WorkItem) * c->items.size() + 4);
     const size_t szDeps = align256(4 * c->deps.size() + 4);
     const size_t szDone = align256(4 * c->items.size() + 4);  // zeroed: no launch's epoch
-    *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone;
+    const size_t szTbRes = align256(4 * c->tbRes.size() + 4);
+    const size_t szResS = align256(4 * c->residS.size() + 4);
+    const size_t szResL = align256(4 * c->residL.size() + 4);
+    *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL;
     if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {
@@ -597,7 +647,13 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);
     memset(host + off, 0, szDone);
     k.done = (uint32_t*)put(nullptr, 0, szDone);
+    k.tb_res = (const uint32_t*)put(c->tbRes.data(), 4 * c->tbRes.size(), szTbRes);
+    k.resid_s = (const uint32_t*)put(c->residS.data(), 4 * c->residS.size(), szResS);
+    k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
     P.flowOk = c->flowOk;
+    P.nResidS = (uint32_t)(c->residS.size() / 16);
+    P.nResidL = (uint32_t)c->residL.size();
+    P.resElems = c->resElems;
     k.mi_stride = h->mi_stride;
     k.mi_cols = h->mi_cols;
     k.mi_rows = h->mi_rows;
@@ -646,6 +702,16 @@ static int job_begin(FrameJob& j)
     j.L = h->uses_lr ? frame_get(c, h->frame_width, h->frame_height) : nullptr;
     if (!j.R || !j.C || (h->uses_lr && !j.L)) return fail(c, AV1R_E_NOMEM, "frame allocation");
     j.k.cur = j.R->d;
+    if (P.resElems > c->resCap) {
+        if (c->resDev) {
+            HIPCHK(hipStreamSynchronize(c->stream));  // in-flight frames may still read it
+            (void)hipFree(c->resDev);
+            c->resDev = nullptr;
+        }
+        c->resCap = P.resElems + P.resElems / 4 + 4096;
+        HIPCHK(hipMalloc(&c->resDev, 2 * c->resCap));
+    }
+    j.k.res = c->resDev;
     j.k.cdef = j.C->d;
     if (j.L) j.k.lrout = j.L->d;
     return AV1R_OK;
@@ -706,13 +772,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     const size_t tabBytes = align256(4 * tabW * std::max<size_t>(nLevels, 1));
     // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
     static const bool flowEnv = !getenv("AV1R_FLOW") || atoi(getenv("AV1R_FLOW")) != 0;
-    bool flow = flowEnv && !lc->traceFile;
+    bool flow = flowEnv;
     size_t nGroups = 0;
     for (auto& j : jobs) {
         flow &= j.P->flowOk;
-        for (const Level& lv : j.P->levels) nGroups += lv.cnt[1] + (lv.cnt[2] + 3) / 4;
+        for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
     }
-    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups : 0);
+    const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
+    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups + resTabBytes : 0);
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % 2;
     if (M.pending) {
@@ -736,7 +803,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         M.cap = cap;
     }
     KParams* hk = reinterpret_cast<KParams*>(M.host);
-    for (int i = 0; i < n; i++) hk[i] = jobs[i].k;
+    uint32_t frameRows = 0;  // k_flow-mode timeline: frame-major rows
+    for (int i = 0; i < n; i++) {
+        hk[i] = jobs[i].k;
+        hk[i].trace_base = frameRows;
+        for (const Level& lv : jobs[i].P->levels) frameRows += lv.cnt[0] + lv.cnt[1] + lv.cnt[2];
+    }
     uint32_t* tab = reinterpret_cast<uint32_t*>(M.host + kBytes);
     // total[l * 3 + kind]: items of the level's inter / large / small lists
     std::vector<uint32_t> total(nLevels * 3, 0);
@@ -770,15 +842,22 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                 const auto& lvs = jobs[i].P->levels;
                 if (l >= lvs.size()) continue;
                 const Level& lv = lvs[l];
-                for (uint32_t q = 0; q < lv.cnt[1]; q++, g += 2) {
+                for (uint32_t q = 0; q < lv.fcnt[1]; q++, g += 2) {
                     g[0] = (uint32_t)i << 8;
                     g[1] = lv.off[1] + q;
                 }
-                for (uint32_t q = 0; q < lv.cnt[2]; q += 4, g += 2) {
-                    g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(4, lv.cnt[2] - q);
+                for (uint32_t q = 0; q < lv.fcnt[2]; q += 4, g += 2) {
+                    g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(4, lv.fcnt[2] - q);
                     g[1] = lv.off[2] + q;
                 }
             }
+        // k_resid tables: prefix sums of the frames' workgroup counts (small, large)
+        uint32_t* rt = g;
+        rt[0] = rt[n + 1] = 0;
+        for (int i = 0; i < n; i++) {
+            rt[i + 1] = rt[i] + jobs[i].P->nResidS;
+            rt[n + 2 + i] = rt[n + 1 + i] + jobs[i].P->nResidL;
+        }
     }
     HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
@@ -812,6 +891,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (slot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
     size_t allItems = 0;
     for (uint32_t v : total) allItems += v;
+    allItems = std::max<size_t>(allItems, frameRows);
     if (lc->traceFile && lc->traceCap < allItems) {
         if (lc->traceDev) (void)hipFree(lc->traceDev);
         lc->traceCap = allItems + allItems / 2;
@@ -822,14 +902,19 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     static std::atomic<uint32_t> epochs{0};
     if (flow) {
         // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
-        if (total[0]) launch_k_level(0, slot, dtab, n, total[0], nullptr, 0, st);
+        if (total[0]) launch_k_level(0, slot, dtab, n, total[0], trace, ~0u, st);
+        // every residual (inter TBs outside inter-intra blocks added in place)
+        const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
+        const uint32_t* hrt = reinterpret_cast<const uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
+        if (hrt[n]) launch_k_resid(0, slot, drt, n, hrt[n], st);
+        if (hrt[2 * n + 1]) launch_k_resid(1, slot, drt + n + 1, n, hrt[2 * n + 1], st);
         if (nGroups) {
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
             const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             const int wslot = kpw_upload(lc->device, hk, n, st);
             if (wslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
-            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, st);
+            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, trace, st);
             if (kpw_release(lc->device, wslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
             HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, st));
         }
@@ -847,10 +932,19 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         std::vector<unsigned long long> hv((size_t)allItems * 16);
         HIPCHK(hipMemcpyAsync(hv.data(), trace, hv.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        size_t q = 0;
-        for (size_t l = 0; l < nLevels; l++)
-            for (int kk = 0; kk < 3; kk++)
-                for (uint32_t i = 0; i < total[l * 3 + kk]; i++, q++) hv[q * 16 + 6] = l;
+        if (flow) {  // frame-major rows: each frame's items in its level order
+            size_t q = 0;
+            for (auto& j : jobs)
+                for (size_t l = 0; l < j.P->levels.size(); l++)
+                    for (int kk = 0; kk < 3; kk++)
+                        for (uint32_t i = 0; i < j.P->levels[l].cnt[kk]; i++, q++) hv[q * 16 + 6] = l;
+            hv.resize(q * 16);
+        } else {
+            size_t q = 0;
+            for (size_t l = 0; l < nLevels; l++)
+                for (int kk = 0; kk < 3; kk++)
+                    for (uint32_t i = 0; i < total[l * 3 + kk]; i++, q++) hv[q * 16 + 6] = l;
+        }
         fwrite(hv.data(), 8, hv.size(), lc->traceFile);
         fflush(lc->traceFile);
     }
@@ -972,6 +1066,7 @@ void av1r_destroy(av1r_ctx* c)
             if (u.err) (void)hipHostFree(u.err);
             (void)hipEventDestroy(u.done);
         }
+    if (c->resDev) (void)hipFree(c->resDev);
     (void)hipEventDestroy(c->sync);
     if (c->traceDev) (void)hipFree(c->traceDev);
     if (c->traceFile) fclose(c->traceFile);

@@ -24,6 +24,25 @@
 // Debug timeline (AV1R_TRACE_FILE): lane 0 of each item stamps the 100 MHz real-time
 // counter at entry, once the item record is in, after the prediction and at the end.
 // Compiled in only with -DAV1R_TRACE (the stamps' waits constrain scheduling).
+DEV void trace_put(unsigned long long* tr, int slot, unsigned long long v)
+{
+#ifdef AV1R_TRACE
+    if (tr && (threadIdx.x & 63) == 0) tr[slot] = v;
+#else
+    (void)tr;
+    (void)slot;
+    (void)v;
+#endif
+}
+DEV unsigned long long trace_now()
+{
+#ifdef AV1R_TRACE
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memrealtime();
+#else
+    return 0;
+#endif
+}
 DEV void trace_stamp(unsigned long long* tr, int slot)
 {
 #ifdef AV1R_TRACE
@@ -90,17 +109,17 @@ DEV void col_pass(const int16_t* col, int16_t* out, int kind, int colShift, int 
 // applied.  Reads only the batch (coefficients, block record), never the frame: the
 // dataflow kernel runs it before the item's dependencies are complete.  c0: the lane's
 // first coefficient, prefetched by the caller.  Ends with a coop_sync.
-template <int NT, int MAX>
-DEV void tb_residual(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, uint32_t c0)
+template <int NT, int MAX, class TB>
+DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int16_t* res, uint32_t c0)
 {
-    constexpr int RS = TbLds<MAX>::RS;
+    constexpr int RS = MAX + 2;
     const int t = coop_lane<NT>();
     const int txSz = tb.tx_size;
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
     const int log2W = av1r_tx_w_log2[txSz], log2H = av1r_tx_h_log2[txSz];
     const int tw = imin(w, 32), th = imin(h, 32);
     const av1r_frame_hdr& hd = *k.hdr;
-    for (int q = t; q < th * w; q += NT) L.res[(q >> log2W) * RS + (q & (w - 1))] = 0;
+    for (int q = t; q < th * w; q += NT) res[(q >> log2W) * RS + (q & (w - 1))] = 0;
     coop_sync<NT>();
     int dqDenom = 1;
     if (txSz == AV1R_TX_32X32 || txSz == AV1R_TX_16X32 || txSz == AV1R_TX_32X16 || txSz == AV1R_TX_16X64 || txSz == AV1R_TX_64X16)
@@ -119,7 +138,7 @@ DEV void tb_residual(const KParams& k, const WorkItem& tb, const av1r_block& blk
         int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
         int sign = d < 0 ? -1 : 1;
         int d2 = sign * (iabs(d) & 0xffffff) / dqDenom;
-        L.res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
+        res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
     }
     coop_sync<NT>();
     const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
@@ -130,7 +149,7 @@ DEV void tb_residual(const KParams& k, const WorkItem& tb, const av1r_block& blk
     const int rk = tx::row_kind(type), ck = tx::col_kind(type);
     // rows >= 32 of a 64-high transform have all-zero input and therefore zero output
     if (t < th) {
-        int16_t* row = L.res + t * RS;
+        int16_t* row = res + t * RS;
         switch (log2W) {
         case 2: row_pass<2>(row, w, rk, rect, rowShift, lossless); break;
         case 3: row_pass<3>(row, w, rk, rect, rowShift, lossless); break;
@@ -139,15 +158,15 @@ DEV void tb_residual(const KParams& k, const WorkItem& tb, const av1r_block& blk
         default: if constexpr (MAX >= 64) row_pass<6>(row, w, rk, rect, rowShift, lossless); break;
         }
     } else if (t < h) {
-        int16_t* row = L.res + t * RS;
+        int16_t* row = res + t * RS;
         for (int j = 0; j < w; j++) row[j] = 0;
     }
     coop_sync<NT>();
     const int flipUD = type == AV1R_FLIPADST_DCT || type == AV1R_FLIPADST_ADST || type == AV1R_V_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     const int flipLR = type == AV1R_DCT_FLIPADST || type == AV1R_ADST_FLIPADST || type == AV1R_H_FLIPADST || type == AV1R_FLIPADST_FLIPADST;
     if (t < w) {
-        const int16_t* col = L.res + t;
-        int16_t* out = L.res + (flipLR ? w - 1 - t : t);
+        const int16_t* col = res + t;
+        int16_t* out = res + (flipLR ? w - 1 - t : t);
         switch (log2H) {
         case 2: col_pass<2, RS>(col, out, ck, colShift, lossless, flipUD); break;
         case 3: col_pass<3, RS>(col, out, ck, colShift, lossless, flipUD); break;
@@ -274,6 +293,52 @@ DEV void tb_store(const KParams& k, const WorkItem& tb, TbLds<MAX>& L)
     }
 }
 
+// k_flow's add and store: as tb_store, with the residual quads (4 int16 each) of the TB's
+// precomputed tile already in registers (loaded before the dependency wait)
+template <int NT, int MAX>
+struct ResQuads {
+    static constexpr int N = (MAX * MAX / 4 + NT - 1) / NT;
+    uint2 r[N];
+};
+template <int NT, int MAX>
+DEV void res_prefetch(const KParams& k, const WorkItem& tb, ResQuads<NT, MAX>& R)
+{
+    const int t = coop_lane<NT>();
+    const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
+    const uint32_t ro = tb.coef_cnt ? k.tb_res[AV1R_ITEM_INDEX(tb.code)] : ~0u;
+    const uint2* q4 = reinterpret_cast<const uint2*>(k.res + ro);
+#pragma unroll
+    for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
+        const int q = t + u * NT;
+        R.r[u] = (ro != ~0u && q < nq) ? q4[q] : make_uint2(0, 0);
+    }
+}
+DEV uint32_t add4(uint32_t p, uint2 r)
+{
+    const int v[4] = {(int16_t)(r.x & 0xffff), (int16_t)(r.x >> 16), (int16_t)(r.y & 0xffff), (int16_t)(r.y >> 16)};
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) o |= (uint32_t)clip1((int)((p >> (8 * b)) & 0xff) + v[b]) << (8 * b);
+    return o;
+}
+template <int NT, int MAX>
+DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R)
+{
+    const int t = coop_lane<NT>();
+    const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;
+    const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
+    const DevPlane& dst = k.cur.pl[tb.plane];
+#pragma unroll
+    for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
+        const int q = t + u * NT;
+        if (q < nq) {
+            const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
+            const uint32_t p = *reinterpret_cast<const uint32_t*>(&L.pred[i * MAX + j]);
+            stp4<true>(dst, tb.x + j, tb.y + i, add4(p, R.r[u]));
+        }
+    }
+}
+
 // One transform block of the level launches (TransformBlock::decode,
 // TransformBlock.cpp:2400-2456): the prediction inputs are final before the launch.
 template <int NT, int MAX>
@@ -284,7 +349,7 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
     const av1r_block& blk = k.blocks[wi.block];
     tb_predict<NT, MAX, false>(k, wi, blk, L);
     trace_stamp(tr, 4);
-    if (wi.coef_cnt) tb_residual<NT, MAX>(k, wi, blk, L, c0);
+    if (wi.coef_cnt) tb_residual<NT, MAX>(k, wi, blk, L.res, c0);
     trace_stamp(tr, 13);
     tb_store<NT, MAX, false>(k, wi, L);
 }
@@ -995,6 +1060,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
         P.edgeFilter = k.hdr->enable_intra_edge_filter;
         coop_intra_predict<NT, COH>(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
         const int sizeScale = 128 / imax(ph, pw);
+        const bool addRes = COH;  // k_flow: the block's residuals are added here (tiles)
         for (int q = t; q < pw * ph; q += NT) {
             const int i = q / pw, j = q - i * pw;
             int m;
@@ -1017,9 +1083,32 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
                 m = r2(s4, 2);
             }
             const int d = ldp<COH>(dst, baseX + j, baseY + i);
-            stp<COH>(dst, baseX + j, baseY + i, (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6)));
+            const uint8_t v = (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6));
+            if (addRes) L.pred[i * 64 + j] = v;
+            else stp<COH>(dst, baseX + j, baseY + i, v);
         }
         coop_sync<NT>();
+        if (addRes) {
+            // TransformBlock::decode's add and clip for this plane's TBs with coefficients
+            // (TBs never overlap: in place in L.pred), then the whole plane is stored
+            for (uint32_t ti = blk.first_tb; ti < blk.first_tb + blk.n_tbs; ti++) {
+                const av1r_tb& tb = k.tbs[ti];
+                if (tb.plane != plane || !tb.coef_cnt) continue;
+                const int tw = av1r_tx_w[tb.tx_size], th = av1r_tx_h[tb.tx_size];
+                const int16_t* rt = k.res + k.tb_res[ti];
+                for (int q = t; q < tw * th; q += NT) {
+                    const int i = q / tw, j = q - i * tw;
+                    uint8_t& v = L.pred[(tb.y - baseY + i) * 64 + tb.x - baseX + j];
+                    v = (uint8_t)clip1(v + rt[q]);
+                }
+                coop_sync<NT>();
+            }
+            for (int q = t; q < pw * ph; q += NT) {
+                const int i = q / pw, j = q - i * pw;
+                stp<COH>(dst, baseX + j, baseY + i, L.pred[i * 64 + j]);
+            }
+            coop_sync<NT>();
+        }
     }
 }
 
@@ -1126,19 +1215,22 @@ extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_
     unsigned long long* trace, uint32_t traceBase)
 {
     __shared__ InterLds L;
+    const unsigned long long tEntry = trace ? trace_now() : 0;
+    const KParams* kp;
+    int s;
+    const WorkItem& wi = table_item(slot, tab, n, blockIdx.x, kp, s);
+    const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
 #ifdef AV1R_TRACE
-    unsigned long long* tr = trace ? trace + (size_t)(traceBase + blockIdx.x) * AV1R_TRACE_W : nullptr;
+    // traceBase ~0u (k_flow mode): frame-major rows, this frame's base + the item position
+    const size_t row = traceBase == ~0u ? kp->trace_base + (size_t)(&wi - kp->items) : (size_t)traceBase + blockIdx.x;
+    unsigned long long* tr = trace ? trace + row * AV1R_TRACE_W : nullptr;
 #else
     unsigned long long* tr = nullptr;
     (void)trace;
     (void)traceBase;
 #endif
-    trace_stamp(tr, 2);
-    const KParams* kp;
-    int s;
-    const WorkItem& wi = table_item(slot, tab, n, blockIdx.x, kp, s);
-    const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
-    if (tr && threadIdx.x == 0) tr[0] = wi.code;
+    trace_put(tr, 2, tEntry);
+    trace_put(tr, 0, wi.code);
     trace_stamp(tr, 3);
     inter_tile(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
     trace_stamp(tr, 5);
@@ -1209,31 +1301,51 @@ DEV void flow_publish(uint32_t* flag, uint32_t epoch)
     if (coop_lane<NT>() == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// -DAV1R_TRACE timeline row (frame-major): 0 code, 1 frame << 32 | tx_size << 8 | pred,
+// 2 entry, 3 residual done, 4 dependencies complete, 5 published, 6 level (host),
+// 7 XCC id << 16 | dependency count
 template <int NT, int MAX>
-DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl)
+DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl,
+    unsigned long long* trace, uint32_t s)
 {
     const WorkItem& wi = k.items[pos];
+#ifdef AV1R_TRACE
+    unsigned long long* tr = trace ? trace + (size_t)(k.trace_base + pos) * AV1R_TRACE_W : nullptr;
+    trace_stamp(tr, 2);
+    trace_put(tr, 0, wi.code);
+    trace_put(tr, 1, ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred);
+    trace_put(tr, 7, ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 16) | wi.dep_cnt);
+#else
+    unsigned long long* tr = nullptr;
+    (void)trace;
+    (void)s;
+#endif
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
         if constexpr (MAX == 64) {  // blends are always large items
+            trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+            trace_stamp(tr, 4);
             ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L);
         }
     } else {
-        const int t = coop_lane<NT>();
-        const uint32_t c0 = t < wi.coef_cnt ? k.coefs[wi.coef_off + t] : 0u;
+        // intra / palette TB: its residual tile (k_resid) is fetched before the wait
+        ResQuads<NT, MAX> R;
+        res_prefetch<NT, MAX>(k, wi, R);
         const av1r_block& blk = k.blocks[wi.block];
-        if (wi.coef_cnt) tb_residual<NT, MAX>(k, wi, blk, L, c0);
+        trace_stamp(tr, 3);
         flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+        trace_stamp(tr, 4);
         tb_predict<NT, MAX, true>(k, wi, blk, L);
-        tb_store<NT, MAX, true>(k, wi, L);
+        tb_store_flow<NT, MAX>(k, wi, L, R);
     }
     flow_publish<NT>(k.done + pos, epoch);
+    trace_stamp(tr, 5);
 }
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
 // workgroup), n = 1..4 small items (one per wave)
 extern "C" __global__ __launch_bounds__(256, 4) void k_flow(int slot, const uint2* __restrict__ groups, uint32_t nGroups,
-    uint32_t* ctl, uint32_t epoch)
+    uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
     __shared__ __align__(16) uint8_t smem[kLds];
@@ -1256,10 +1368,12 @@ extern "C" __global__ __launch_bounds__(256, 4) void k_flow(int slot, const uint
         const KParams& k = g_kp[slot][gd.x >> 8];
         const uint32_t n = gd.x & 0xff;
         if (n == 0) {
-            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl);
+            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8);
         } else {
             const uint32_t wave = threadIdx.x >> 6;
-            if (wave < n) flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl);
+            if (wave < n)
+                flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
+                    gd.x >> 8);
         }
 #ifndef AV1R_TICKET_PREFETCH
         if (threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1287,14 +1401,78 @@ int flow_grid(int device)
     return cache[device];
 }
 
-void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid, hipStream_t s)
+void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid,
+    unsigned long long* trace, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, slot, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch);
+    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, slot, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
+        trace);
 }
 
 #endif  // AV1R_FLOW_PART
 
 #ifndef AV1R_FLOW_PART
+// ---------------------------------------------------------------------------------
+// k_resid (k_flow mode, after k_inter): the residual of every TB with coefficients
+// (TransformBlock::reconstruct + inverseTransform, TransformBlock.cpp:2173-2276), with no
+// dependencies at all.  An inter TB outside an inter-intra block is added to its
+// prediction in the frame right here (TransformBlock.cpp:2440-2456); every other residual
+// is stored as an int16 tile for the k_flow item (intra TB, inter-intra blend) that adds
+// it.  k_resid_s: 16 TBs with sides <= 16 per 256-lane workgroup, 16 lanes each;
+// k_resid_l: one larger TB per 64-lane workgroup.  tab: [prefix of the frames' workgroup
+// counts (n + 1)].
+// ---------------------------------------------------------------------------------
+template <int NT, int MAX>
+DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
+{
+    constexpr int RS = MAX + 2;
+    const int t = coop_lane<NT>();
+    const av1r_tb& tb = k.tbs[ti];
+    const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
+    const av1r_block& blk = k.blocks[tb.block];
+    const uint32_t ro = k.tb_res[ti];
+    tb_residual<NT, MAX>(k, tb, blk, res, c0);
+    const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;
+    const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
+    const DevPlane& dst = k.cur.pl[tb.plane];
+    for (int q = t; q < nq; q += NT) {
+        const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
+        const uint32_t r01 = *reinterpret_cast<const uint32_t*>(&res[i * RS + j]);
+        const uint32_t r23 = *reinterpret_cast<const uint32_t*>(&res[i * RS + j + 2]);
+        if (ro == ~0u) stp4<false>(dst, tb.x + j, tb.y + i, add4(ldp4<false>(dst, tb.x + j, tb.y + i), make_uint2(r01, r23)));
+        else reinterpret_cast<uint2*>(k.res + ro)[q] = make_uint2(r01, r23);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_resid_s(int slot, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ __align__(16) int16_t res[16][16 * 18];
+    const uint32_t b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+    const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    const KParams& k = g_kp[slot][s];
+    const int g = threadIdx.x >> 4;
+    const uint32_t ti = k.resid_s[(b - tab[s]) * 16 + g];
+    if (ti != ~0u) resid_one<16, 16>(k, ti, res[g]);
+}
+
+extern "C" __global__ __launch_bounds__(64) void k_resid_l(int slot, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ __align__(16) int16_t res[64 * 66];
+    const uint32_t b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+    const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    const KParams& k = g_kp[slot][s];
+    resid_one<64, 64>(k, k.resid_l[b - tab[s]], res);
+}
+
+void launch_k_resid(int large, int slot, const uint32_t* tab, int n, unsigned groups, hipStream_t s)
+{
+    if (large) hipLaunchKernelGGL(k_resid_l, dim3(groups), dim3(64), 0, s, slot, tab, n);
+    else hipLaunchKernelGGL(k_resid_s, dim3(groups), dim3(256), 0, s, slot, tab, n);
+}
+
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4)
 void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)

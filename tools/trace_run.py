@@ -27,14 +27,18 @@ def run(nfr, path, streams=1):
         d.set_discard_output(True)
         decs.append(d)
         hss.append([d.prepare(f) for f in frames])
+    sizes = [0]
     for t in range(nfr):
         if streams == 1:
             decs[0].decode_prepared(hss[0][t])
         else:
             Decoder.decode_prepared_batch(decs, [h[t] for h in hss])
+        for d in decs:
+            d.synchronize()
+        sizes.append(os.path.getsize(path))
     for d in decs:
-        d.synchronize()
         d.close()
+    return sizes
 
 
 def summarise(path):
@@ -117,10 +121,63 @@ def level_report(a, starts, fi):
     print("level span percentiles (us): p10 %.1f p50 %.1f p90 %.1f max %.1f" % tuple(np.percentile(sp, [10, 50, 90, 100])))
 
 
+def summarise_flow(path, lo=0, hi=None):
+    """k_flow-mode timeline (frame-major rows): per item entry (2), residual done (3),
+    dependencies complete (4), published (5); inter tiles (k_inter) stamp 2, 3, 5."""
+    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
+    a = a[lo // 128: (hi // 128 if hi else None)]
+    code, misc, t2, t3, t4, t5, lvl, x7 = (a[:, i] for i in (0, 1, 2, 3, 4, 5, 6, 7))
+    kind = code >> 30
+    pred = misc & 0xff
+    txs = (misc >> 8) & 0xff
+    us = lambda x: x / 100.0
+    flow = kind != 1
+    tiles = kind == 1
+    t0 = t2[tiles].min() if tiles.any() else t2[flow].min()
+    print(f"{len(a)} items: {tiles.sum()} inter tiles, {flow.sum()} flow items")
+    if tiles.any():
+        print(f"k_inter: first entry 0, last end {us(t5[tiles].max() - t0):.1f} us; tile p50 {np.median(us(t5[tiles]-t2[tiles])):.2f} us")
+    f0 = t2[flow].min()
+    print(f"k_flow: first entry {us(f0 - t0):.1f} us, last publish {us(t5[flow].max() - t0):.1f} us (span {us(t5[flow].max() - f0):.1f})")
+    for name, m in (("TB intra", flow & (kind == 0) & (pred == 0)), ("TB palette", flow & (kind == 0) & (pred == 1)),
+                    ("TB inter", flow & (kind == 0) & (pred == 2)), ("ii blend", kind == 2)):
+        if not m.any():
+            continue
+        r = us(t3[m] - t2[m]); w = us(t4[m] - t3[m]); f = us(t5[m] - t4[m])
+        print(f"{name:10s} n={m.sum():7d} resid p50 {np.median(r):5.2f} wait p50 {np.median(w):6.2f} p90 {np.percentile(w, 90):7.2f}"
+              f" finish p50 {np.median(f):5.2f} p90 {np.percentile(f, 90):5.2f}  last publish {us(t5[m].max() - t0):8.1f} us")
+    m = flow & (kind == 0) & (pred == 0)
+    for ts in np.unique(txs[m]):
+        mm = m & (txs == ts)
+        print(f"   intra tx {ts:2d}: n={mm.sum():6d} resid {np.median(us(t3[mm]-t2[mm])):5.2f} finish {np.median(us(t5[mm]-t4[mm])):5.2f}"
+              f" finish p90 {np.percentile(us(t5[mm]-t4[mm]), 90):5.2f}")
+    # busy vs waiting items over time (10 us buckets)
+    end = t5[flow].max()
+    edges = np.arange(f0, end + 1000, 1000)
+    def active(s_, e_):
+        c = np.zeros(len(edges) - 1)
+        for lo, hi in zip(s_, e_):
+            i0 = np.searchsorted(edges, lo, "right") - 1
+            i1 = np.searchsorted(edges, hi, "right") - 1
+            c[max(i0, 0):i1 + 1] += 1
+        return c
+    wait = active(t3[flow], t4[flow])
+    work = active(t2[flow], t3[flow]) + active(t4[flow], t5[flow])
+    print("10-us buckets of k_flow: items waiting / working (every 10th bucket)")
+    for i in range(0, len(wait), max(1, len(wait) // 25)):
+        print(f"  t={us(edges[i] - f0):7.0f} us  waiting {wait[i]:6.0f}  working {work[i]:6.0f}")
+
+
 if __name__ == "__main__":
     nfr = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "trace.bin")
     streams = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    run(nfr, path, streams)
-    summarise(path)
+    sizes = run(nfr, path, streams)
+    if os.environ.get("AV1R_FLOW", "1") != "0":
+        print("=== first step (key frames) ===")
+        summarise_flow(path, sizes[0], sizes[1])
+        print("=== last step ===")
+        summarise_flow(path, sizes[-2], sizes[-1])
+    else:
+        summarise(path)
