@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -103,6 +104,7 @@ struct av1r_ctx {
     Upload meta[2];  // per-launch KParams + level tables
     int metaIdx = 0;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
+    hipEvent_t flowIn = nullptr, flowOut = nullptr;  // hand-off to / from the device's flow stream
     // debug timeline of every recon work item (env AV1R_TRACE_FILE): 8 x u64 per item
     FILE* traceFile = nullptr;
     unsigned long long* traceDev = nullptr;
@@ -745,6 +747,21 @@ static void job_end(FrameJob& j)
     c->lastUploadBytes = j.P->bytes;
 }
 
+// Every k_flow launch of a device runs on ONE stream.  Two k_flow grids resident at once
+// can starve each other: each one's progress needs a resident workgroup on every one of its
+// queues, and spinning workgroups of the other grid may hold the slots (measured: a
+// dependency wait timed out with four batches on four streams).  Other kernels always
+// finish, so they may overlap a k_flow freely.
+static hipStream_t flow_stream(int device)
+{
+    static std::mutex m;
+    static hipStream_t st[64] = {};
+    if (device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> lock(m);
+    if (!st[device] && hipStreamCreateWithFlags(&st[device], hipStreamNonBlocking) != hipSuccess) st[device] = nullptr;
+    return st[device];
+}
+
 static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 {
     av1r_ctx* c = lc;  // errors are reported on the launching context
@@ -898,6 +915,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         HIPCHK(hipMalloc(&lc->traceDev, lc->traceCap * 128));
     }
     unsigned long long* trace = lc->traceFile ? lc->traceDev : nullptr;
+    if (trace) HIPCHK(hipMemsetAsync(trace, 0, allItems * 128, st));  // rows of items not run stay 0
     uint32_t traceBase = 0;
     static std::atomic<uint32_t> epochs{0};
     if (flow) {
@@ -912,11 +930,17 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
             const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
-            const int wslot = kpw_upload(lc->device, hk, n, st);
+            hipStream_t fs = flow_stream(lc->device);
+            if (!fs) return fail(c, AV1R_E_DEVICE, "flow stream");
+            HIPCHK(hipEventRecord(lc->flowIn, st));
+            HIPCHK(hipStreamWaitEvent(fs, lc->flowIn, 0));
+            const int wslot = kpw_upload(lc->device, hk, n, fs);
             if (wslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
-            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, trace, st);
-            if (kpw_release(lc->device, wslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
-            HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, st));
+            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, trace, fs);
+            if (kpw_release(lc->device, wslot, fs)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
+            HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, fs));
+            HIPCHK(hipEventRecord(lc->flowOut, fs));
+            HIPCHK(hipStreamWaitEvent(st, lc->flowOut, 0));
         }
     }
     for (size_t l = 0; l < nLevels && !flow; l++) {
@@ -1042,6 +1066,8 @@ int av1r_create(int device, av1r_ctx** out)
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->meta[i].done, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->flowIn, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->flowOut, hipEventDisableTiming);
     for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
@@ -1068,6 +1094,8 @@ void av1r_destroy(av1r_ctx* c)
         }
     if (c->resDev) (void)hipFree(c->resDev);
     (void)hipEventDestroy(c->sync);
+    (void)hipEventDestroy(c->flowIn);
+    (void)hipEventDestroy(c->flowOut);
     if (c->traceDev) (void)hipFree(c->traceDev);
     if (c->traceFile) fclose(c->traceFile);
     for (auto& e : c->evPool)
@@ -1227,18 +1255,26 @@ int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n)
         jobs.push_back(j);
     }
     if (jobs.empty()) return AV1R_OK;
-    av1r_ctx* c = lc;
-    // the launch stream waits for every member's earlier work, and they for the batch
-    for (auto& j : jobs)
-        if (j.c != lc) {
-            HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
-            HIPCHK(hipStreamWaitEvent(lc->stream, j.c->sync, 0));
-        }
-    int rc = launch_jobs(lc, jobs);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(lc->sync, lc->stream));
-    for (auto& j : jobs)
-        if (j.c != lc) HIPCHK(hipStreamWaitEvent(j.c->stream, lc->sync, 0));
+    // AV1R_SPLIT=k: k sub-batches, each launched on its first member's stream, so that one
+    // sub-batch's low-parallelism phases (the k_flow tail) overlap another's launches
+    static const int split = std::max(1, getenv("AV1R_SPLIT") ? atoi(getenv("AV1R_SPLIT")) : 1);
+    const size_t k = std::min<size_t>(split, jobs.size());
+    for (size_t part = 0; part < k; part++) {
+        std::vector<FrameJob> sub(jobs.begin() + part * jobs.size() / k, jobs.begin() + (part + 1) * jobs.size() / k);
+        av1r_ctx* sl = sub[0].c;
+        av1r_ctx* c = sl;
+        // the launch stream waits for every member's earlier work, and they for the batch
+        for (auto& j : sub)
+            if (j.c != sl) {
+                HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
+                HIPCHK(hipStreamWaitEvent(sl->stream, j.c->sync, 0));
+            }
+        int rc = launch_jobs(sl, sub);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(sl->sync, sl->stream));
+        for (auto& j : sub)
+            if (j.c != sl) HIPCHK(hipStreamWaitEvent(j.c->stream, sl->sync, 0));
+    }
     return AV1R_OK;
 }
 

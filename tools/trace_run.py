@@ -126,6 +126,7 @@ def summarise_flow(path, lo=0, hi=None):
     dependencies complete (4), published (5); inter tiles (k_inter) stamp 2, 3, 5."""
     a = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
     a = a[lo // 128: (hi // 128 if hi else None)]
+    a = a[a[:, 2] != 0]  # rows of items that did not run in this mode (inter TBs: k_resid)
     code, misc, t2, t3, t4, t5, lvl, x7 = (a[:, i] for i in (0, 1, 2, 3, 4, 5, 6, 7))
     kind = code >> 30
     pred = misc & 0xff
