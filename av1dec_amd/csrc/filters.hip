@@ -187,20 +187,24 @@ DEV int constrain(int diff, int threshold, int damping)
 }
 
 // One workgroup per 64x64 luma region (one cdef_idx, Cdef.cpp:47-55) and its two 32x32
-// chroma regions.  The deblocked pixels with a 2-pixel halo are staged in LDS once; the
-// direction search runs one lane per (8x8 block, direction) pair summing each partial
-// line straight from LDS; the filter runs one lane per pixel from LDS.
-#define CD_H 2                     // tap reach (Cdef_Directions)
-#define CD_LW (64 + 2 * CD_H)      // luma tile edge
-#define CD_CW (32 + 2 * CD_H)      // chroma tile edge
+// chroma regions.  The deblocked pixels with a 2-pixel halo are staged in LDS once (rows
+// of aligned dwords away from the frame edge); the direction search runs one lane per
+// (8x8 block, direction) pair summing each partial line straight from LDS; the filter
+// runs two horizontally adjacent pixels per packed 16-bit operation, each lane on rows of
+// one block (luma: 4 lanes per 8x8 block, chroma: 2 lanes per 4x4 block and plane).
+#define CD_H 2            // tap reach (Cdef_Directions)
+#define CD_X 4            // LDS column of plane column x0 (dword-aligned staging from x0 - 4)
+#define CD_LS 72          // luma tile: columns x0 - 4 .. x0 + 67
+#define CD_LR (64 + 2 * CD_H)
+#define CD_CS 40          // chroma tile: columns x0 / 2 - 4 .. x0 / 2 + 35
+#define CD_CR (32 + 2 * CD_H)
 struct CdefLds {
-    uint8_t y[CD_LW][CD_LW + 4];
-    uint8_t uv[2][CD_CW][CD_CW + 4];
+    uint8_t y[CD_LR][CD_LS];
+    uint8_t uv[2][CD_CR][CD_CS];
     int cost[64][8];
-    uint8_t dir[64];               // yDir
     int16_t pri[64];               // adjusted luma primary strength
     uint8_t filt[64];              // block is filtered (not skip)
-    int16_t offY[64][6], offC[64][6];  // tap offsets in the staged tiles (cdef_px)
+    int16_t offY[64][6], offC[64][6];  // tap offsets in the staged tiles (cdef_pair)
 };
 
 // partial[d][k] of cdefDirection (Cdef.cpp:203-261) for one line k of direction d, summed
@@ -208,7 +212,7 @@ struct CdefLds {
 template <int d>
 DEV int cdef_cost(const CdefLds& L, int bx, int by)
 {
-    auto px8 = [&](int i, int j) { return (int)L.y[CD_H + by + i][CD_H + bx + j] - 128; };
+    auto px8 = [&](int i, int j) { return (int)L.y[CD_H + by + i][CD_X + bx + j] - 128; };
     int cost = 0;
     if (d == 2 || d == 6) {
 #pragma unroll
@@ -255,21 +259,24 @@ DEV int cdef_cost(const CdefLds& L, int bx, int by)
     return cost;
 }
 
-// cdefFilter (Cdef.cpp:158-198) for one pixel at tile offset p of the staged tile t.
-// off[s * 2 + kk] = tile offset of tap kk of direction dir (s = 0), dir - 2 (s = 1),
-// dir + 2 (s = 2); taps at -off and +off.  Per-block constants are folded: the damping
-// shifts (constrain, :111-118) and the primary tap weights.  `check`: the region touches
-// the frame edge, so each tap is tested against is_inside_filter_region (X, Y = plane
-// position of the pixel, limX / limY = plane extent of the mi grid).
+// cdefFilter (Cdef.cpp:158-198) for the two horizontally adjacent pixels at tile offsets
+// p, p + 1 of the staged tile t (row stride ts), in packed 16-bit lanes.  off[s * 2 + kk] =
+// tile offset of tap kk of direction dir (s = 0), dir - 2 (s = 1), dir + 2 (s = 2); taps
+// at -off and +off.  `check`: the region touches the frame edge; a tap outside
+// is_inside_filter_region (X, Y = plane position of the first pixel, limX / limY = plane
+// extent of the mi grid) is replaced by the centre pixel, which contributes nothing to
+// the sum, the minimum or the maximum -- exactly the reference's skipped tap.
+typedef short cd2 __attribute__((ext_vector_type(2)));
+DEV cd2 cd_pack(const uint8_t* t, int p) { return cd2{(short)t[p], (short)t[p + 1]}; }
 template <bool check>
-DEV int cdef_px(const uint8_t* t, int p, const int16_t* off, int pri, int sec, int damping, int X, int Y, int ts,
+DEV cd2 cdef_pair(const uint8_t* t, int p, const int16_t* off, int pri, int sec, int damping, int X, int Y, int ts,
     int limX, int limY)
 {
-    const int x = t[p];
-    int sum = 0, mx = x, mn = x;
-    const int adjP = imax(0, damping - floor_log2(imax(pri, 1)));
-    const int adjS = imax(0, damping - floor_log2(imax(sec, 1)));
-    const int tap0 = (pri & 1) ? 3 : 4, tap1 = (pri & 1) ? 3 : 2;  // Cdef_Pri_Taps
+    const cd2 x = cd_pack(t, p);
+    cd2 sum = cd2{0, 0}, mx = x, mn = x;
+    const short adjP = (short)imax(0, damping - floor_log2(imax(pri, 1)));
+    const short adjS = (short)imax(0, damping - floor_log2(imax(sec, 1)));
+    const short tap0 = (pri & 1) ? 3 : 4, tap1 = (pri & 1) ? 3 : 2;  // Cdef_Pri_Taps
 #pragma unroll
     for (int s = 0; s < 3; s++)
 #pragma unroll
@@ -278,24 +285,49 @@ DEV int cdef_px(const uint8_t* t, int p, const int16_t* off, int pri, int sec, i
 #pragma unroll
             for (int sg = 0; sg < 2; sg++) {
                 const int oo = sg ? o : -o;
+                cd2 q = cd_pack(t, p + oo);
                 if (check) {
-                    // tile offset -> plane position of the tap
                     const int dy = (oo + 2 * ts + 2) / ts - 2;  // |dx|, |dy| <= 2
                     const int dx = oo - dy * ts;
-                    const int xx = X + dx, yy = Y + dy;
-                    if (!(xx >= 0 && xx < limX && yy >= 0 && yy < limY)) continue;
+                    const int yy = Y + dy, xx = X + dx;
+                    const bool rowIn = yy >= 0 && yy < limY;
+                    q.x = (rowIn && xx >= 0 && xx < limX) ? q.x : x.x;
+                    q.y = (rowIn && xx + 1 >= 0 && xx + 1 < limX) ? q.y : x.y;
                 }
-                const int q = t[p + oo];
-                const int d = q - x, ad = iabs(d);
-                const int thr = s == 0 ? pri : sec, adj = s == 0 ? adjP : adjS;
-                const int v = imin(ad, imax(0, thr - (ad >> adj)));  // constrain (0 for thr 0)
-                const int w = s == 0 ? (kk ? tap1 : tap0) : (kk ? 1 : 2);  // Cdef_Sec_Taps = {2, 1}
-                sum += w * (d < 0 ? -v : v);
-                mx = imax(q, mx);
-                mn = imin(q, mn);
+                const cd2 d = q - x;
+                const cd2 ad = __builtin_elementwise_max(d, -d);
+                const short thr = s == 0 ? (short)pri : (short)sec, adj = s == 0 ? adjP : adjS;
+                cd2 v = __builtin_elementwise_min(ad, __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0}));
+                const cd2 neg = d >> cd2{15, 15};
+                v = (v ^ neg) - neg;  // constrain (0 for thr 0)
+                const short w = s == 0 ? (kk ? tap1 : tap0) : (kk ? 1 : 2);  // Cdef_Sec_Taps = {2, 1}
+                sum += cd2{w, w} * v;
+                mx = __builtin_elementwise_max(q, mx);
+                mn = __builtin_elementwise_min(q, mn);
             }
         }
-    return CLIP3(mn, mx, x + ((8 + sum - (sum < 0)) >> 4));
+    const cd2 r = x + ((sum + cd2{8, 8} + (sum >> cd2{15, 15})) >> cd2{4, 4});  // (8 + sum - (sum < 0)) >> 4
+    return __builtin_elementwise_min(__builtin_elementwise_max(r, mn), mx);
+}
+
+// Stage rows [y0 - 2, y0 + rows + 2) x columns [x0 - 4, x0 + cols + 4) of plane P into the
+// tile t (row stride ts): aligned dwords where no coordinate needs clamping, else bytes
+// with the coordinates clamped into the mi grid (taps beyond it are never used).
+DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int y0, bool clamp, int mx, int my)
+{
+    const int ndw = ts / 4;
+    if (!clamp) {
+        for (int q = threadIdx.x; q < nrows * ndw; q += 256) {
+            const int i = q / ndw, d = q - i * ndw;
+            *reinterpret_cast<uint32_t*>(t + i * ts + 4 * d) =
+                *reinterpret_cast<const uint32_t*>(P.p + (size_t)(y0 - CD_H + i) * P.stride + x0 - CD_X + 4 * d);
+        }
+        return;
+    }
+    for (int q = threadIdx.x; q < nrows * ts; q += 256) {
+        const int i = q / ts, j = q - i * ts;
+        t[i * ts + j] = px(P, CLIP3(0, mx, x0 - CD_X + j), CLIP3(0, my, y0 - CD_H + i));
+    }
 }
 
 // grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.cur, writes k.cdef
@@ -323,22 +355,13 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
         }
         return;
     }
-    // stage the deblocked region + halo; coordinates clamped into the mi grid (taps that
-    // fall outside it are never used: is_inside_filter_region)
-    {
-        const DevPlane& P = k.cur.pl[0];
-        const int mx = k.mi_cols * 4 - 1, my = k.mi_rows * 4 - 1;
-        for (int q = t; q < CD_LW * CD_LW; q += 256) {
-            int i = q / CD_LW, j = q - i * CD_LW;
-            L.y[i][j] = px(P, CLIP3(0, mx, x0 - CD_H + j), CLIP3(0, my, y0 - CD_H + i));
-        }
-        const int cmx = k.mi_cols * 2 - 1, cmy = k.mi_rows * 2 - 1;
-        for (int q = t; q < 2 * CD_CW * CD_CW; q += 256) {
-            int pl = q >= CD_CW * CD_CW, e = q - pl * CD_CW * CD_CW;
-            int i = e / CD_CW, j = e - i * CD_CW;
-            L.uv[pl][i][j] = px(k.cur.pl[1 + pl], CLIP3(0, cmx, x0 / 2 - CD_H + j), CLIP3(0, cmy, y0 / 2 - CD_H + i));
-        }
-    }
+    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
+    const bool edge = x0 < CD_H || y0 < CD_H || x0 + 64 + CD_H > limX || y0 + 64 + CD_H > limY;
+    const int cx0 = x0 / 2, cy0 = y0 / 2, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
+    const bool cedge = cx0 < CD_H || cy0 < CD_H || cx0 + 32 + CD_H > climX || cy0 + 32 + CD_H > climY;
+    cd_stage(&L.y[0][0], CD_LS, CD_LR, k.cur.pl[0], x0, y0, edge, limX - 1, limY - 1);
+    cd_stage(&L.uv[0][0][0], CD_CS, CD_CR, k.cur.pl[1], cx0, cy0, cedge, climX - 1, climY - 1);
+    cd_stage(&L.uv[1][0][0], CD_CS, CD_CR, k.cur.pl[2], cx0, cy0, cedge, climX - 1, climY - 1);
     if (t < 64) {
         const int br = r0 + (t >> 3) * 2, bc = c0 + (t & 7) * 2;
         int f = 0;
@@ -383,7 +406,6 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
         const int var = (best - L.cost[t][(yDir + 4) & 7]) >> 10;
         int priStr = h.cdef_y_pri[idx];
         const int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
-        L.dir[t] = (uint8_t)yDir;
         L.pri[t] = (int16_t)(var ? (priStr * (4 + varStr) + 8) >> 4 : 0);
         // tap offsets: luma direction (0 when the primary strength is 0), chroma direction
         // Cdef_Uv_Dir (identity for 4:2:0; 0 when the chroma primary strength is 0)
@@ -394,44 +416,72 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
             for (int kk = 0; kk < 2; kk++) {
                 const int dl = s == 0 ? dy0 : ((dy0 + (s == 1 ? -2 : 2)) & 7);
                 const int dc = s == 0 ? dc0 : ((dc0 + (s == 1 ? -2 : 2)) & 7);
-                L.offY[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dl][kk][0] * (CD_LW + 4) + av1r_cdef_directions[dl][kk][1]);
-                L.offC[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dc][kk][0] * (CD_CW + 4) + av1r_cdef_directions[dc][kk][1]);
+                L.offY[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dl][kk][0] * CD_LS + av1r_cdef_directions[dl][kk][1]);
+                L.offC[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dc][kk][0] * CD_CS + av1r_cdef_directions[dc][kk][1]);
             }
     }
     __syncthreads();
-    // luma
-    const int ySec = h.cdef_y_sec[idx];
-    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
-    const bool edge = x0 < CD_H || y0 < CD_H || x0 + 64 + CD_H > limX || y0 + 64 + CD_H > limY;
-    for (int q = t; q < rows4 * 4 * cols4 * 4; q += 256) {
-        const int i = q / (cols4 * 4), j = q - i * (cols4 * 4);
-        const int b = (i >> 3) * 8 + (j >> 3);
-        const int p = (CD_H + i) * (CD_LW + 4) + CD_H + j;
-        int v;
-        if (!L.filt[b]) v = (&L.y[0][0])[p];
-        else if (edge)
-            v = cdef_px<true>(&L.y[0][0], p, L.offY[b], L.pri[b], ySec, h.cdef_damping, x0 + j, y0 + i, CD_LW + 4, limX, limY);
-        else
-            v = cdef_px<false>(&L.y[0][0], p, L.offY[b], L.pri[b], ySec, h.cdef_damping, 0, 0, CD_LW + 4, 0, 0);
-        px(k.cdef.pl[0], x0 + j, y0 + i) = (uint8_t)v;
+    // luma: 4 lanes per 8x8 block, two rows of 8 (4 pixel pairs) each
+    {
+        const int b = t >> 2, bi = b >> 3, bj = b & 7;
+        const int j0 = bj * 8;
+        const int ySec = h.cdef_y_sec[idx];
+        if (j0 < cols4 * 4) {
+            const bool full = j0 + 8 <= cols4 * 4;  // else only the left 4 columns are in the grid
+            const bool f = L.filt[b];
+            const int pri = L.pri[b];
+            for (int r = 0; r < 2; r++) {
+                const int i = bi * 8 + (t & 3) * 2 + r;
+                if (i >= rows4 * 4) break;
+                const int p = (CD_H + i) * CD_LS + CD_X + j0;
+                uint32_t o[2] = {0, 0};
+#pragma unroll
+                for (int pp = 0; pp < 4; pp++) {
+                    if (pp >= 2 && !full) break;
+                    cd2 v;
+                    if (!f) v = cd_pack(&L.y[0][0], p + 2 * pp);
+                    else if (edge)
+                        v = cdef_pair<true>(&L.y[0][0], p + 2 * pp, L.offY[b], pri, ySec, h.cdef_damping, x0 + j0 + 2 * pp, y0 + i, CD_LS, limX, limY);
+                    else
+                        v = cdef_pair<false>(&L.y[0][0], p + 2 * pp, L.offY[b], pri, ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
+                    o[pp >> 1] |= ((uint32_t)(uint8_t)v.x | ((uint32_t)(uint8_t)v.y << 8)) << (16 * (pp & 1));
+                }
+                uint8_t* dst = &px(k.cdef.pl[0], x0 + j0, y0 + i);
+                if (full) *reinterpret_cast<uint2*>(dst) = make_uint2(o[0], o[1]);
+                else *reinterpret_cast<uint32_t*>(dst) = o[0];
+            }
+        }
     }
-    // chroma
-    const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
-    const int cx0 = x0 / 2, cy0 = y0 / 2, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
-    const bool cedge = cx0 < CD_H || cy0 < CD_H || cx0 + 32 + CD_H > climX || cy0 + 32 + CD_H > climY;
-    for (int q = t; q < 2 * rows4 * 2 * cols4 * 2; q += 256) {
-        const int pl = q >= rows4 * 2 * cols4 * 2, e = q - pl * rows4 * 2 * cols4 * 2;
-        const int i = e / (cols4 * 2), j = e - i * (cols4 * 2);
-        const int b = (i >> 2) * 8 + (j >> 2);
-        const uint8_t* tile = &L.uv[pl][0][0];
-        const int p = (CD_H + i) * (CD_CW + 4) + CD_H + j;
-        int v;
-        if (!L.filt[b]) v = tile[p];
-        else if (cedge)
-            v = cdef_px<true>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j, cy0 + i, CD_CW + 4, climX, climY);
-        else
-            v = cdef_px<false>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, 0, 0, CD_CW + 4, 0, 0);
-        px(k.cdef.pl[1 + pl], cx0 + j, cy0 + i) = (uint8_t)v;
+    // chroma: 2 lanes per 4x4 block and plane, two rows of 4 (2 pixel pairs) each
+    {
+        const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
+        const int pl = t >> 7, b = (t >> 1) & 63, bi = b >> 3, bj = b & 7;
+        const int j0 = bj * 4;
+        if (j0 < cols4 * 2) {
+            const bool full = j0 + 4 <= cols4 * 2;  // else only the left 2 columns are in the grid
+            const bool f = L.filt[b];
+            const uint8_t* tile = &L.uv[pl][0][0];
+            for (int r = 0; r < 2; r++) {
+                const int i = bi * 4 + (t & 1) * 2 + r;
+                if (i >= rows4 * 2) break;
+                const int p = (CD_H + i) * CD_CS + CD_X + j0;
+                uint32_t o = 0;
+#pragma unroll
+                for (int pp = 0; pp < 2; pp++) {
+                    if (pp && !full) break;
+                    cd2 v;
+                    if (!f) v = cd_pack(tile, p + 2 * pp);
+                    else if (cedge)
+                        v = cdef_pair<true>(tile, p + 2 * pp, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j0 + 2 * pp, cy0 + i, CD_CS, climX, climY);
+                    else
+                        v = cdef_pair<false>(tile, p + 2 * pp, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, 0, 0, CD_CS, 0, 0);
+                    o |= ((uint32_t)(uint8_t)v.x | ((uint32_t)(uint8_t)v.y << 8)) << (16 * pp);
+                }
+                uint8_t* dst = &px(k.cdef.pl[1 + pl], cx0 + j0, cy0 + i);
+                if (full) *reinterpret_cast<uint32_t*>(dst) = o;
+                else *reinterpret_cast<uint16_t*>(dst) = (uint16_t)o;
+            }
+        }
     }
 }
 

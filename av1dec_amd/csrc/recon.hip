@@ -370,7 +370,8 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
 // ---------------------------------------------------------------------------------
 #define TS 32                     // tile edge (luma)
 #define WC (TS + 8)               // window row stride
-#define HBN (TS * TS * 15 / 8)    // >= (TS + 7) * TS horizontal rows; = warp intermediates
+#define WARP_ROWS 16              // warped regions are predicted in chunks of 16 rows
+#define HBN ((TS + 7) * TS)       // horizontal rows; >= warp intermediates (TS * WARP_ROWS / 64 * 120)
 
 struct InterLds {
     uint8_t tile[TS * TS];        // this plane's tile, assembled before the store
@@ -787,6 +788,12 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     if (mode == 3 && ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
     const int diffwtdLuma = ct == AV1R_COMPOUND_DIFFWTD && plane == 0;
 
+    // a warped region goes in chunks of WARP_ROWS rows (its 15 x 8 intermediates per 8x8
+    // block would not fit the LDS budget of 16 workgroups per CU otherwise)
+    const int chunkH = (R[0].warp || (isCompound && R[1].warp)) ? WARP_ROWS : rh;
+    const int ryA = ry0, rhA = rh;
+    for (int cy = 0; cy < rhA; cy += chunkH) {
+    const int ry0 = ryA + cy, rh = imin(chunkH, rhA - cy);  // this chunk
     if (R[0].useWin) load_window(R[0], L.win[0], rx0, ry0, rw, rh);
     if (isCompound && R[1].useWin) load_window(R[1], L.win[1], rx0, ry0, rw, rh);
     __syncthreads();
@@ -873,6 +880,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
         }
     }
     __syncthreads();
+    }
 }
 
 // overlappedMotionCompensation (InterPredict.cpp:611-709) restricted to the tile
@@ -993,8 +1001,13 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
     const int t = threadIdx.x;
     const av1r_block& blk = k.blocks[bi];
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
+    // timeline (-DAV1R_TRACE): 1 = block size | motion mode << 8 | compound << 12, 8 + plane
+    // after each plane's store, 11 after the luma geometry, 12 after the luma prediction
+    trace_put(tr, 1, blk.mi_size | (blk.motion_mode << 8) |
+        ((mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] > AV1R_INTRA_FRAME) << 12));
     for (int plane = 0; plane < nPl; plane++) {
         const PlaneGeo G = plane_geo(k, blk, plane, tx, ty);
+        if (plane == 0) trace_stamp(tr, 11);
         {
             int r = 0;
             for (int yy = 0; yy < G.ph; yy += G.predH) {
@@ -1010,6 +1023,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
                 r++;
             }
         }
+        if (plane == 0) trace_stamp(tr, 12);
         if (blk.motion_mode == AV1R_OBMC_CAUSAL)
             obmc(k, blk, L, plane, G.baseX, G.baseY, G.predW, G.predH, G.TX0, G.TY0, G.TW, G.TH);
         const DevPlane& dst = k.cur.pl[plane];
@@ -1018,6 +1032,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
             px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[i * TS + j];
         }
         __syncthreads();
+        trace_stamp(tr, 8 + plane);
     }
 }
 
@@ -1211,7 +1226,14 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
     trace_stamp(tr, 5);
 }
 
-extern "C" __global__ __launch_bounds__(64) void k_inter(int slot, const uint32_t* __restrict__ tab, int n,
+// 4 waves/SIMD (128 VGPRs, 64 B/lane of spills; LDS 10160 B: 16 workgroups/CU); the
+// -DAV1R_TRACE build keeps its registers (with the stamps it would spill ~1.9 KB/lane)
+#ifdef AV1R_TRACE
+#define K_INTER_BOUNDS __launch_bounds__(64)
+#else
+#define K_INTER_BOUNDS __launch_bounds__(64, 4)
+#endif
+extern "C" __global__ K_INTER_BOUNDS void k_inter(int slot, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
 {
     __shared__ InterLds L;

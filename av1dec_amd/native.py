@@ -10,10 +10,11 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(BUILD, "libav1r.so")
-# (source, object, extra flags): recon.hip twice -- the level kernels, and k_flow alone
-# without machine-level loop-invariant hoisting (in k_flow's persistent loop it hoists ~50
-# constants into VGPRs for every code path: 177 instead of 124 VGPRs, half the occupancy)
-SRCS = [("recon.hip", "recon", []),
+# (source, object, extra flags): recon.hip twice -- the level kernels, and k_flow alone.
+# Both without machine-level loop-invariant hoisting: in k_flow's persistent loop it hoists
+# ~50 constants into VGPRs for every code path (177 instead of 124 VGPRs, half the
+# occupancy); k_inter at 4 waves/SIMD spills less without it (64 vs 96 B/lane; 6 % faster)
+SRCS = [("recon.hip", "recon", ["-mllvm", "-disable-machine-licm"]),
         ("recon.hip", "recon_flow", ["-DAV1R_FLOW_PART", "-mllvm", "-disable-machine-licm"]),
         ("filters.hip", "filters", []),
         ("av1r_host.cpp", "av1r_host", [])]

@@ -138,6 +138,22 @@ def summarise_flow(path, lo=0, hi=None):
     print(f"{len(a)} items: {tiles.sum()} inter tiles, {flow.sum()} flow items")
     if tiles.any():
         print(f"k_inter: first entry 0, last end {us(t5[tiles].max() - t0):.1f} us; tile p50 {np.median(us(t5[tiles]-t2[tiles])):.2f} us")
+        bs = misc & 0xff
+        mm_ = (misc >> 8) & 0xf
+        cp = (misc >> 12) & 1
+        t8, t9, t10, t11, t12 = (a[:, i] for i in (8, 9, 10, 11, 12))
+        names = ["4x4", "4x8", "8x4", "8x8", "8x16", "16x8", "16x16", "16x32", "32x16", "32x32", "32x64", "64x32",
+                 "64x64", "64x128", "128x64", "128x128", "4x16", "16x4", "8x32", "32x8", "16x64", "64x16"]
+        print("  tile class            n   entry->item  item->geo  geo->lumapred  ->luma-store  ->U  ->V  total (us, p50)")
+        for b_ in np.unique(bs[tiles]):
+            for mo in np.unique(mm_[tiles]):
+                for c_ in (0, 1):
+                    m = tiles & (bs == b_) & (mm_ == mo) & (cp == c_)
+                    if m.sum() < 50:
+                        continue
+                    med = lambda x, y: np.median(us(x[m] - y[m]))
+                    print(f"  {names[b_]:7s} motion {mo} comp {c_} {m.sum():6d}   {med(t3, t2):6.2f}  {med(t11, t3):6.2f}"
+                          f"  {med(t12, t11):6.2f}  {med(t8, t12):6.2f}  {med(t9, t8):6.2f}  {med(t10, t9):6.2f}  {med(t5, t2):6.2f}")
     f0 = t2[flow].min()
     print(f"k_flow: first entry {us(f0 - t0):.1f} us, last publish {us(t5[flow].max() - t0):.1f} us (span {us(t5[flow].max() - f0):.1f})")
     for name, m in (("TB intra", flow & (kind == 0) & (pred == 0)), ("TB palette", flow & (kind == 0) & (pred == 1)),
