@@ -259,21 +259,34 @@ DEV int cdef_cost(const CdefLds& L, int bx, int by)
     return cost;
 }
 
-// cdefFilter (Cdef.cpp:158-198) for the two horizontally adjacent pixels at tile offsets
-// p, p + 1 of the staged tile t (row stride ts), in packed 16-bit lanes.  off[s * 2 + kk] =
-// tile offset of tap kk of direction dir (s = 0), dir - 2 (s = 1), dir + 2 (s = 2); taps
-// at -off and +off.  `check`: the region touches the frame edge; a tap outside
-// is_inside_filter_region (X, Y = plane position of the first pixel, limX / limY = plane
-// extent of the mi grid) is replaced by the centre pixel, which contributes nothing to
-// the sum, the minimum or the maximum -- exactly the reference's skipped tap.
+// cdefFilter (Cdef.cpp:158-198) for the four horizontally adjacent pixels at tile offset
+// p (a multiple of 4) of the staged tile t (row stride ts, a multiple of 4), as two pairs
+// in packed 16-bit lanes.  Each tap's four pixels come from one ds_read2_b32 and a byte
+// align.  off[s * 2 + kk] = tile offset of tap kk of direction dir (s = 0), dir - 2
+// (s = 1), dir + 2 (s = 2); taps at -off and +off.  `check`: the region touches the
+// frame edge; a tap outside is_inside_filter_region (X, Y = plane position of the first
+// pixel, limX / limY = plane extent of the mi grid) is replaced by the centre pixel,
+// which contributes nothing to the sum, the minimum or the maximum -- exactly the
+// reference's skipped tap.
 typedef short cd2 __attribute__((ext_vector_type(2)));
-DEV cd2 cd_pack(const uint8_t* t, int p) { return cd2{(short)t[p], (short)t[p + 1]}; }
-template <bool check>
-DEV cd2 cdef_pair(const uint8_t* t, int p, const int16_t* off, int pri, int sec, int damping, int X, int Y, int ts,
-    int limX, int limY)
+DEV uint32_t cd_bytes(const uint8_t* t, int p)  // t[p .. p + 3], any alignment of p
 {
-    const cd2 x = cd_pack(t, p);
-    cd2 sum = cd2{0, 0}, mx = x, mn = x;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(t + (p & ~3));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(p & 3));
+}
+DEV cd2 cd_lo(uint32_t w) { return __builtin_bit_cast(cd2, __builtin_amdgcn_perm(0u, w, 0x0c010c00u)); }
+DEV cd2 cd_hi(uint32_t w) { return __builtin_bit_cast(cd2, __builtin_amdgcn_perm(0u, w, 0x0c030c02u)); }
+DEV uint32_t cd_join(cd2 a, cd2 b)
+{
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06040200u);
+}
+template <bool check>
+DEV uint32_t cdef_quad(const uint8_t* t, int p, const int16_t* off, int pri, int sec, int damping, int X, int Y,
+    int ts, int limX, int limY)
+{
+    const uint32_t xw = *reinterpret_cast<const uint32_t*>(t + p);
+    const cd2 x[2] = {cd_lo(xw), cd_hi(xw)};
+    cd2 sum[2] = {cd2{0, 0}, cd2{0, 0}}, mx[2] = {x[0], x[1]}, mn[2] = {x[0], x[1]};
     const short adjP = (short)imax(0, damping - floor_log2(imax(pri, 1)));
     const short adjS = (short)imax(0, damping - floor_log2(imax(sec, 1)));
     const short tap0 = (pri & 1) ? 3 : 4, tap1 = (pri & 1) ? 3 : 2;  // Cdef_Pri_Taps
@@ -285,29 +298,40 @@ DEV cd2 cdef_pair(const uint8_t* t, int p, const int16_t* off, int pri, int sec,
 #pragma unroll
             for (int sg = 0; sg < 2; sg++) {
                 const int oo = sg ? o : -o;
-                cd2 q = cd_pack(t, p + oo);
+                const uint32_t qw = cd_bytes(t, p + oo);
+                cd2 q[2] = {cd_lo(qw), cd_hi(qw)};
                 if (check) {
                     const int dy = (oo + 2 * ts + 2) / ts - 2;  // |dx|, |dy| <= 2
                     const int dx = oo - dy * ts;
                     const int yy = Y + dy, xx = X + dx;
                     const bool rowIn = yy >= 0 && yy < limY;
-                    q.x = (rowIn && xx >= 0 && xx < limX) ? q.x : x.x;
-                    q.y = (rowIn && xx + 1 >= 0 && xx + 1 < limX) ? q.y : x.y;
+                    q[0].x = (rowIn && xx >= 0 && xx < limX) ? q[0].x : x[0].x;
+                    q[0].y = (rowIn && xx + 1 >= 0 && xx + 1 < limX) ? q[0].y : x[0].y;
+                    q[1].x = (rowIn && xx + 2 >= 0 && xx + 2 < limX) ? q[1].x : x[1].x;
+                    q[1].y = (rowIn && xx + 3 >= 0 && xx + 3 < limX) ? q[1].y : x[1].y;
                 }
-                const cd2 d = q - x;
-                const cd2 ad = __builtin_elementwise_max(d, -d);
                 const short thr = s == 0 ? (short)pri : (short)sec, adj = s == 0 ? adjP : adjS;
-                cd2 v = __builtin_elementwise_min(ad, __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0}));
-                const cd2 neg = d >> cd2{15, 15};
-                v = (v ^ neg) - neg;  // constrain (0 for thr 0)
                 const short w = s == 0 ? (kk ? tap1 : tap0) : (kk ? 1 : 2);  // Cdef_Sec_Taps = {2, 1}
-                sum += cd2{w, w} * v;
-                mx = __builtin_elementwise_max(q, mx);
-                mn = __builtin_elementwise_min(q, mn);
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const cd2 d = q[h] - x[h];
+                    const cd2 ad = __builtin_elementwise_max(d, -d);
+                    cd2 v = __builtin_elementwise_min(ad, __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0}));
+                    const cd2 neg = d >> cd2{15, 15};
+                    v = (v ^ neg) - neg;  // constrain (0 for thr 0)
+                    sum[h] += cd2{w, w} * v;
+                    mx[h] = __builtin_elementwise_max(q[h], mx[h]);
+                    mn[h] = __builtin_elementwise_min(q[h], mn[h]);
+                }
             }
         }
-    const cd2 r = x + ((sum + cd2{8, 8} + (sum >> cd2{15, 15})) >> cd2{4, 4});  // (8 + sum - (sum < 0)) >> 4
-    return __builtin_elementwise_min(__builtin_elementwise_max(r, mn), mx);
+    cd2 r[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        r[h] = x[h] + ((sum[h] + cd2{8, 8} + (sum[h] >> cd2{15, 15})) >> cd2{4, 4});  // (8 + sum - (sum < 0)) >> 4
+        r[h] = __builtin_elementwise_min(__builtin_elementwise_max(r[h], mn[h]), mx[h]);
+    }
+    return cd_join(r[0], r[1]);
 }
 
 // Stage rows [y0 - 2, y0 + rows + 2) x columns [x0 - 4, x0 + cols + 4) of plane P into the
@@ -421,7 +445,7 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
             }
     }
     __syncthreads();
-    // luma: 4 lanes per 8x8 block, two rows of 8 (4 pixel pairs) each
+    // luma: 4 lanes per 8x8 block, two rows of 8 (two 4-pixel groups) each
     {
         const int b = t >> 2, bi = b >> 3, bj = b & 7;
         const int j0 = bj * 8;
@@ -436,15 +460,13 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
                 const int p = (CD_H + i) * CD_LS + CD_X + j0;
                 uint32_t o[2] = {0, 0};
 #pragma unroll
-                for (int pp = 0; pp < 4; pp++) {
-                    if (pp >= 2 && !full) break;
-                    cd2 v;
-                    if (!f) v = cd_pack(&L.y[0][0], p + 2 * pp);
+                for (int g = 0; g < 2; g++) {
+                    if (g && !full) break;
+                    if (!f) o[g] = *reinterpret_cast<const uint32_t*>(&L.y[0][0] + p + 4 * g);
                     else if (edge)
-                        v = cdef_pair<true>(&L.y[0][0], p + 2 * pp, L.offY[b], pri, ySec, h.cdef_damping, x0 + j0 + 2 * pp, y0 + i, CD_LS, limX, limY);
+                        o[g] = cdef_quad<true>(&L.y[0][0], p + 4 * g, L.offY[b], pri, ySec, h.cdef_damping, x0 + j0 + 4 * g, y0 + i, CD_LS, limX, limY);
                     else
-                        v = cdef_pair<false>(&L.y[0][0], p + 2 * pp, L.offY[b], pri, ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
-                    o[pp >> 1] |= ((uint32_t)(uint8_t)v.x | ((uint32_t)(uint8_t)v.y << 8)) << (16 * (pp & 1));
+                        o[g] = cdef_quad<false>(&L.y[0][0], p + 4 * g, L.offY[b], pri, ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
                 }
                 uint8_t* dst = &px(k.cdef.pl[0], x0 + j0, y0 + i);
                 if (full) *reinterpret_cast<uint2*>(dst) = make_uint2(o[0], o[1]);
@@ -452,7 +474,7 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
             }
         }
     }
-    // chroma: 2 lanes per 4x4 block and plane, two rows of 4 (2 pixel pairs) each
+    // chroma: 2 lanes per 4x4 block and plane, two rows of 4 each
     {
         const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
         const int pl = t >> 7, b = (t >> 1) & 63, bi = b >> 3, bj = b & 7;
@@ -465,18 +487,12 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
                 const int i = bi * 4 + (t & 1) * 2 + r;
                 if (i >= rows4 * 2) break;
                 const int p = (CD_H + i) * CD_CS + CD_X + j0;
-                uint32_t o = 0;
-#pragma unroll
-                for (int pp = 0; pp < 2; pp++) {
-                    if (pp && !full) break;
-                    cd2 v;
-                    if (!f) v = cd_pack(tile, p + 2 * pp);
-                    else if (cedge)
-                        v = cdef_pair<true>(tile, p + 2 * pp, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j0 + 2 * pp, cy0 + i, CD_CS, climX, climY);
-                    else
-                        v = cdef_pair<false>(tile, p + 2 * pp, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, 0, 0, CD_CS, 0, 0);
-                    o |= ((uint32_t)(uint8_t)v.x | ((uint32_t)(uint8_t)v.y << 8)) << (16 * pp);
-                }
+                uint32_t o;
+                if (!f) o = *reinterpret_cast<const uint32_t*>(tile + p);
+                else if (cedge)
+                    o = cdef_quad<true>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j0, cy0 + i, CD_CS, climX, climY);
+                else
+                    o = cdef_quad<false>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, 0, 0, CD_CS, 0, 0);
                 uint8_t* dst = &px(k.cdef.pl[1 + pl], cx0 + j0, cy0 + i);
                 if (full) *reinterpret_cast<uint32_t*>(dst) = o;
                 else *reinterpret_cast<uint16_t*>(dst) = (uint16_t)o;
