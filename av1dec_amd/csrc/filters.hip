@@ -530,22 +530,46 @@ DEV int lr_src(const LrPix& S, int x, int y)
 #define LR_TH 32
 #define LR_SW (LR_TW + 8)
 struct LrLds {
-    uint8_t src[LR_TH + 6][LR_SW];        // get_source_sample over rows ty0-3.., cols x0-3..
+    uint8_t src[LR_TH + 6][LR_SW];        // get_source_sample over rows ty0-3.., cols x0-4..
     int16_t hw[LR_TH + 6][LR_TW];         // Wiener horizontal pass
     int16_t A[2][LR_TH + 2][LR_TW + 2];   // self-guided a per pass, rows ty0-1.., cols x0-1..
     int32_t B[2][LR_TH + 2][LR_TW + 2];
     av1r_lr_unit unit[3];
 };
 
+// Per-set constants of the self-guided filter, folded at compile time: s = the box
+// scale of LoopRestoration.cpp:370 (((1 << 20) + n^2 eps / 2) / (n^2 eps), n = 25 / 9 for
+// r = 2 / 1) and the divisions ((z << 8) + z / 2) / (z + 1) of :374-378 for z in 0..255.
+struct SgrTabs {
+    uint32_t s[16][2];
+    uint16_t xbyx1[256];
+};
+constexpr SgrTabs make_sgr_tabs()
+{
+    SgrTabs t{};
+    const int prm[16][4] = {{2, 12, 1, 4}, {2, 15, 1, 6}, {2, 18, 1, 8}, {2, 21, 1, 9}, {2, 24, 1, 10}, {2, 29, 1, 11},
+        {2, 36, 1, 12}, {2, 45, 1, 13}, {2, 56, 1, 14}, {2, 68, 1, 15}, {0, 0, 1, 5}, {0, 0, 1, 8}, {0, 0, 1, 11},
+        {0, 0, 1, 14}, {2, 30, 0, 0}, {2, 75, 0, 0}};  // Sgr_Params (Av1Common.h:206-211)
+    for (int set = 0; set < 16; set++)
+        for (int pass = 0; pass < 2; pass++) {
+            const int r = prm[set][pass * 2], eps = prm[set][pass * 2 + 1];
+            const int n = (2 * r + 1) * (2 * r + 1), n2e = n * n * eps;
+            t.s[set][pass] = r ? (uint32_t)(((1 << 20) + n2e / 2) / n2e) : 0u;
+        }
+    t.xbyx1[0] = 1;
+    for (int z = 1; z < 255; z++) t.xbyx1[z] = (uint16_t)(((z << 8) + (z / 2)) / (z + 1));
+    t.xbyx1[255] = 256;
+    return t;
+}
+__constant__ SgrTabs g_sgr = make_sgr_tabs();
+
 // a, b of the self-guided box at staged position (si, sj) = source (row, col) index of the
 // box centre (LoopRestoration.cpp:284-380, restated per position; 32-bit arithmetic as
 // the reference's)
 DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, int& A, int& B)
 {
-    const int eps = av1r_sgr_params[set][pass * 2 + 1];
-    const int n = (2 * r + 1) * (2 * r + 1);
-    const int n2e = n * n * eps;
-    const int s = ((1 << 20) + n2e / 2) / n2e;
+    const int n = r == 2 ? 25 : 9;  // (2r + 1)^2 (r is 1 or 2)
+    const uint32_t s = g_sgr.s[set][pass];
     int a = 0, b = 0;
     for (int dy = -r; dy <= r; dy++)
         for (int dx = -r; dx <= r; dx++) {
@@ -554,12 +578,11 @@ DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, in
             b += cv;
         }
     int p = imax(0, a * n - b * b);
-    int z = (int)((uint32_t)p * (uint32_t)s + (1u << 19)) >> 20;
+    int z = (int)((uint32_t)p * s + (1u << 19)) >> 20;
     int a2;
-    if (z >= 255) a2 = 256;
-    else if (z == 0) a2 = 1;
-    else a2 = ((z << 8) + (z / 2)) / (z + 1);
-    int oneOverN = ((1 << 12) + (n / 2)) / n;
+    if (z >= 0) a2 = g_sgr.xbyx1[imin(z, 255)];
+    else a2 = ((z << 8) + (z / 2)) / (z + 1);  // the 32-bit wrap-around case, as the reference
+    const int oneOverN = r == 2 ? 164 : 455;  // ((1 << 12) + n / 2) / n
     int b2 = ((1 << 8) - a2) * b * oneOverN;
     A = a2;
     B = r2(b2, 12);
@@ -605,10 +628,43 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
     const int nU = imin((x0 + tw - 1) / us, cols - 1) - uc0 + 1;
     if (t < nU) L.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
     const int y0 = imax(S.start, 0);  // forEachBlock's y: the stripe's first row
-    // stage the source rows ty0-3 .. ty1+2, cols x0-3 .. x0+tw+2
-    for (int q = t; q < (th + 6) * (tw + 6); q += 256) {
-        int i = q / (tw + 6), j = q - i * (tw + 6);
-        L.src[i][j] = (uint8_t)lr_src(S, x0 - 3 + j, ty0 - 3 + i);
+    // stage the source rows ty0-3 .. ty1+2, cols x0-4 .. x0+67 (L.src[i][j]: x = x0 - 4 + j):
+    // aligned dwords where no column needs clamping, else bytes; every lane's loads are
+    // issued before its LDS stores
+    if (x0 >= 4 && x0 + LR_SW - 4 <= C.w) {
+        constexpr int ND = LR_SW / 4, NQ = ((LR_TH + 6) * ND + 255) / 256;
+        uint32_t v[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / ND, d = q - i * ND;
+            if (i < th + 6) {
+                int y = ty0 - 3 + i;  // get_source_sample's row mapping
+                const bool pre = y < S.start || y >= S.end;
+                if (y < S.start) y = imax(S.start - 2, y);
+                else if (y >= S.end) y = imin(S.end + 1, y);
+                y = CLIP3(0, C.h - 1, y);
+                const uint8_t* row = (pre ? S.preP.p : C.p) + (size_t)y * (pre ? S.preP.stride : C.stride);
+                v[u] = *reinterpret_cast<const uint32_t*>(row + x0 - 4 + 4 * d);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / ND, d = q - i * ND;
+            if (i < th + 6) *reinterpret_cast<uint32_t*>(&L.src[i][4 * d]) = v[u];
+        }
+    } else {
+        constexpr int NQ = ((LR_TH + 6) * LR_SW + 255) / 256;
+        uint8_t v[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / LR_SW, j = q - i * LR_SW;
+            if (i < th + 6) v[u] = (uint8_t)lr_src(S, x0 - 4 + j, ty0 - 3 + i);
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / LR_SW, j = q - i * LR_SW;
+            if (i < th + 6) L.src[i][j] = v[u];
+        }
     }
     __syncthreads();
     int anyW = 0, anyS = 0;
@@ -625,7 +681,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
             const av1r_lr_unit& u = L.unit[unitOf(c)];
             if (u.type != AV1R_RESTORE_WIENER) continue;
             int hf3 = 128 - 2 * (u.wiener[1][0] + u.wiener[1][1] + u.wiener[1][2]);
-            const uint8_t* sp = &L.src[i][c];
+            const uint8_t* sp = &L.src[i][c + 1];
             int hs = u.wiener[1][0] * (sp[0] + sp[6]) + u.wiener[1][1] * (sp[1] + sp[5]) + u.wiener[1][2] * (sp[2] + sp[4]) + hf3 * sp[3];
             L.hw[i][c] = (int16_t)CLIP3(-offset, limit - offset, r2(hs, 3));
         }
@@ -642,7 +698,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
             if (!r) continue;
             if (pass == 0 && !((ty0 - 1 + ii - y0) & 1)) continue;  // pass 0 uses odd rows only
             int A, B;
-            sgr_ab_lds(L, ii + 2, cc + 2, r, u.sgr_set, pass, A, B);
+            sgr_ab_lds(L, ii + 2, cc + 3, r, u.sgr_set, pass, A, B);
             L.A[pass][ii][cc] = (int16_t)A;
             L.B[pass][ii][cc] = B;
         }
@@ -651,7 +707,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
     for (int q = t; q < tw * th; q += 256) {
         const int r = q / tw, c = q - r * tw;
         const int x = x0 + c, y = ty0 + r;
-        const int cdef = L.src[r + 3][c + 3];
+        const int cdef = L.src[r + 3][c + 4];
         int outv = cdef;
         const int ui = unitOf(c);
         const av1r_lr_unit& u = L.unit[ui];
@@ -687,7 +743,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
                                 A = L.A[pass][r + 1 + dy][c + 1 + dx];
                                 B = L.B[pass][r + 1 + dy][c + 1 + dx];
                             } else {  // neighbour column in another unit: this unit's parameters
-                                sgr_ab_lds(L, r + 3 + dy, c + 3 + dx, rad, set, pass, A, B);
+                                sgr_ab_lds(L, r + 3 + dy, c + 4 + dx, rad, set, pass, A, B);
                             }
                             a += wt * A;
                             b += wt * B;
