@@ -140,8 +140,10 @@ struct av1r_ctx {
     std::vector<uint8_t> fPal;
     // timing: one set of 5 stage-boundary events per frame since the last summary
     bool timing = false;
-    hipEvent_t ev[5] = {};
-    std::vector<std::array<hipEvent_t, 5>> evPool;
+    // [0] start, [1] recon end, [2] LF end, [3] CDEF end, [4] LR end; k_flow mode also
+    // [5] after k_inter, [6] after k_resid (zero-length spans in level mode)
+    hipEvent_t ev[7] = {};
+    std::vector<std::array<hipEvent_t, 7>> evPool;
     std::vector<int> evFrames;  // frames covered by each event set (batched launches)
     size_t evUsed = 0;
     int nLevelsLast = 0;
@@ -881,12 +883,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 
     if (lc->timing) {
         if (lc->evUsed == lc->evPool.size()) {
-            std::array<hipEvent_t, 5> e;
+            std::array<hipEvent_t, 7> e;
             for (auto& x : e) HIPCHK(hipEventCreate(&x));
             lc->evPool.push_back(e);
             lc->evFrames.push_back(0);
         }
-        for (int i = 0; i < 5; i++) lc->ev[i] = lc->evPool[lc->evUsed][i];
+        for (int i = 0; i < 7; i++) lc->ev[i] = lc->evPool[lc->evUsed][i];
         lc->evFrames[lc->evUsed] = n;
         lc->evUsed++;
         HIPCHK(hipEventRecord(lc->ev[0], st));
@@ -921,11 +923,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (flow) {
         // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
         if (total[0]) launch_k_level(0, slot, dtab, n, total[0], trace, ~0u, st);
+        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
         const uint32_t* hrt = reinterpret_cast<const uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
         if (hrt[n]) launch_k_resid(0, slot, drt, n, hrt[n], st);
         if (hrt[2 * n + 1]) launch_k_resid(1, slot, drt + n + 1, n, hrt[2 * n + 1], st);
+        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
         if (nGroups) {
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
@@ -942,6 +946,10 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             HIPCHK(hipEventRecord(lc->flowOut, fs));
             HIPCHK(hipStreamWaitEvent(st, lc->flowOut, 0));
         }
+    }
+    if (!flow && lc->timing) {
+        HIPCHK(hipEventRecord(lc->ev[5], st));
+        HIPCHK(hipEventRecord(lc->ev[6], st));
     }
     for (size_t l = 0; l < nLevels && !flow; l++) {
         const uint32_t nInter = total[l * 3], nLarge = total[l * 3 + 1], nSmall = total[l * 3 + 2];
@@ -1068,7 +1076,7 @@ int av1r_create(int device, av1r_ctx** out)
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->flowIn, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->flowOut, hipEventDisableTiming);
-    for (int i = 0; i < 5; i++) (void)hipEventCreate(&c->ev[i]);
+    for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
     *out = c;
@@ -1400,6 +1408,28 @@ int av1r_stage_times(av1r_ctx* c, float* totals, int* frames)
         *frames = nf;
     }
     c->evUsed = 0;
+    return AV1R_OK;
+}
+
+int av1r_recon_kernel_times(av1r_ctx* c, float* totals, int* frames)
+{
+    if (!c || !totals) return AV1R_E_INVALID;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 3; i++) totals[i] = 0.f;
+    for (size_t f = 0; f < c->evUsed; f++) {
+        const auto& e = c->evPool[f];
+        const hipEvent_t seq[4] = {e[0], e[5], e[6], e[1]};  // k_inter, k_resid, k_flow
+        for (int i = 0; i < 3; i++) {
+            float t = 0.f;
+            HIPCHK(hipEventElapsedTime(&t, seq[i], seq[i + 1]));
+            totals[i] += t;
+        }
+    }
+    if (frames) {
+        int nf = 0;
+        for (size_t f = 0; f < c->evUsed; f++) nf += c->evFrames[f];
+        *frames = nf;
+    }
     return AV1R_OK;
 }
 

@@ -112,6 +112,13 @@ class Decoder:
         self._check(self.l.av1r_last_frame_times(self.c, *[C.byref(x) for x in t]), "av1r_last_frame_times")
         return [x.value for x in t]
 
+    def recon_kernel_times(self):
+        """(totals_ms[k_inter, k_resid, k_flow], frames) of the frames stage_times() will report."""
+        t = (C.c_float * 3)()
+        n = C.c_int()
+        self._check(self.l.av1r_recon_kernel_times(self.c, t, C.byref(n)), "av1r_recon_kernel_times")
+        return list(t), n.value
+
     def stage_times(self):
         """(totals_ms[recon, lf, cdef, lr], frames) since the previous call (timing=True)."""
         t = (C.c_float * 4)()

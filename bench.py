@@ -175,6 +175,7 @@ def main():
     lead.l.av1r_set_timing(lead.c, 1)
     for t in range(args.warmup, args.warmup + args.steps):
         step(t)
+    ktot, _ = lead.recon_kernel_times()
     totals, nfr = lead.stage_times()
     lead.l.av1r_set_timing(lead.c, 0)
     names = ["recon", "lf", "cdef", "lr"]
@@ -250,6 +251,7 @@ def main():
                          "bytes_per_frame": int(sb[dominant]),
                          "ms_per_frame": round(per_frame_ms[dominant], 4)},
             "stage_ms_per_frame": {n: round(v, 4) for n, v in per_frame_ms.items()},
+            "recon_kernel_ms_per_frame": {n: round(v / max(nfr, 1), 4) for n, v in zip(("k_inter", "k_resid", "k_flow"), ktot)},
             "stage_algorithmic_GBps": {n: round(sb[n] / max(per_frame_ms[n], 1e-9) / 1e6, 2) for n in names},
             "single_stream_fps": round(single_fps, 3),
             "host_inclusive_fps": round(host_fps, 3),

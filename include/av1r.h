@@ -248,6 +248,10 @@ int av1r_set_timing(av1r_ctx* ctx, int enable);
 /* With timing on: synchronise, return the summed device time (ms) of the recon / LF /
  * CDEF / LR stages of every frame launched since the previous call, and reset. */
 int av1r_stage_times(av1r_ctx* ctx, float* totals4, int* frames);
+/* With timing on: the recon stage of the same frames split by kernel -- k_inter, k_resid
+ * (both residual launches), k_flow (incl. its stream hand-off) -- in k_flow mode; call
+ * BEFORE av1r_stage_times (which resets the record). */
+int av1r_recon_kernel_times(av1r_ctx* ctx, float* totals3, int* frames);
 /* Keep per-stage snapshots for av1r_read_stage (default on; costs 2 frame copies). */
 int av1r_set_keep_stages(av1r_ctx* ctx, int keep);
 /* Dependency levels (recon launches) and uploaded batch bytes of the last frame. */

@@ -13,7 +13,8 @@ import os
 import sys
 from collections import defaultdict
 
-STAGES = {"k_inter": "recon", "k_tb": "recon", "k_lf": "lf", "k_cdef": "cdef", "k_lr": "lr"}
+STAGES = {"k_inter": "recon", "k_tb": "recon", "k_resid_s": "recon", "k_resid_l": "recon", "k_flow": "recon",
+          "k_lf": "lf", "k_cdef": "cdef", "k_lr": "lr"}
 
 
 def fold(path, counter):

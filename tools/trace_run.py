@@ -157,7 +157,7 @@ def summarise_flow(path, lo=0, hi=None):
     f0 = t2[flow].min()
     print(f"k_flow: first entry {us(f0 - t0):.1f} us, last publish {us(t5[flow].max() - t0):.1f} us (span {us(t5[flow].max() - f0):.1f})")
     for name, m in (("TB intra", flow & (kind == 0) & (pred == 0)), ("TB palette", flow & (kind == 0) & (pred == 1)),
-                    ("TB inter", flow & (kind == 0) & (pred == 2)), ("ii blend", kind == 2)):
+                    ("TB inter", flow & (kind == 0) & (pred == 2)), ("ii blend", kind == 2), ("intra blk", kind == 3)):
         if not m.any():
             continue
         r = us(t3[m] - t2[m]); w = us(t4[m] - t3[m]); f = us(t5[m] - t4[m])
