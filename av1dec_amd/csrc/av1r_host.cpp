@@ -153,6 +153,7 @@ struct av1r_ctx {
     bool discardOutput = false;  // bench: shown frames are not queued for read-back
     Prepared streamP;
     std::vector<Prepared*> prepared;
+    int schedule = -1;  // av1r_set_schedule: -1 default (AV1R_FLOW), 0 level launches, 1 k_flow
     int16_t* resDev = nullptr;  // k_flow mode: the frame's residual tiles (k_resid)
     size_t resCap = 0;
 };
@@ -791,7 +792,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     const size_t tabBytes = align256(4 * tabW * std::max<size_t>(nLevels, 1));
     // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
     static const bool flowEnv = !getenv("AV1R_FLOW") || atoi(getenv("AV1R_FLOW")) != 0;
-    bool flow = flowEnv;
+    bool flow = lc->schedule >= 0 ? lc->schedule == 1 : flowEnv;
     size_t nGroups = 0;
     for (auto& j : jobs) {
         flow &= j.P->flowOk;
@@ -1408,6 +1409,13 @@ int av1r_stage_times(av1r_ctx* c, float* totals, int* frames)
         *frames = nf;
     }
     c->evUsed = 0;
+    return AV1R_OK;
+}
+
+int av1r_set_schedule(av1r_ctx* c, int mode)
+{
+    if (!c || mode < -1 || mode > 1) return AV1R_E_INVALID;
+    c->schedule = mode;
     return AV1R_OK;
 }
 

@@ -112,6 +112,10 @@ class Decoder:
         self._check(self.l.av1r_last_frame_times(self.c, *[C.byref(x) for x in t]), "av1r_last_frame_times")
         return [x.value for x in t]
 
+    def set_schedule(self, mode):
+        """1: dataflow kernel k_flow (default), 0: one launch per dependency level."""
+        self._check(self.l.av1r_set_schedule(self.c, int(mode)), "av1r_set_schedule")
+
     def recon_kernel_times(self):
         """(totals_ms[k_inter, k_resid, k_flow], frames) of the frames stage_times() will report."""
         t = (C.c_float * 3)()

@@ -95,6 +95,7 @@ def lib():
     l.av1r_last_error.restype = C.c_char_p
     l.av1r_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(i)]
     l.av1r_recon_kernel_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(i)]
+    l.av1r_set_schedule.argtypes = [vp, i]
     l.av1r_prepare.argtypes = [vp, vp, C.POINTER(i)]
     l.av1r_decode_prepared.argtypes = [vp, i]
     l.av1r_decode_prepared_batch.argtypes = [C.POINTER(vp), C.POINTER(i), i]
@@ -114,4 +115,5 @@ EXPORTS = [
     "av1r_set_keep_stages", "av1r_last_frame_stats", "av1r_last_error", "av1r_sizeof",
     "av1r_check_batch", "av1r_prepare", "av1r_decode_prepared", "av1r_release_prepared",
     "av1r_set_discard_output", "av1r_stage_times", "av1r_decode_prepared_batch", "av1r_recon_kernel_times",
+    "av1r_set_schedule",
 ]

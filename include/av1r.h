@@ -252,6 +252,11 @@ int av1r_stage_times(av1r_ctx* ctx, float* totals4, int* frames);
  * (both residual launches), k_flow (incl. its stream hand-off) -- in k_flow mode; call
  * BEFORE av1r_stage_times (which resets the record). */
 int av1r_recon_kernel_times(av1r_ctx* ctx, float* totals3, int* frames);
+/* Reconstruction schedule of the frames this context launches (a batch follows its first
+ * context): 1 = the dataflow kernel k_flow (default; frames with intra block copy still
+ * use level launches), 0 = one launch per dependency level, -1 = the default (environment
+ * AV1R_FLOW=0 selects level launches).  Both are bit-exact; level launches are slower. */
+int av1r_set_schedule(av1r_ctx* ctx, int mode);
 /* Keep per-stage snapshots for av1r_read_stage (default on; costs 2 frame copies). */
 int av1r_set_keep_stages(av1r_ctx* ctx, int keep);
 /* Dependency levels (recon launches) and uploaded batch bytes of the last frame. */

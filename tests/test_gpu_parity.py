@@ -19,10 +19,11 @@ def dev(native_lib):
     d.close()
 
 
-def run_stream(stream, check_stages=True):
+def run_stream(stream, check_stages=True, schedule=1):
     frames = batchfile.load(golden.batch_path(stream))
     rows, out_md5 = golden.stage_hashes(stream)
     d = Decoder(0, keep_stages=check_stages)
+    d.set_schedule(schedule)
     md = hashlib.md5()
     bad = []
     for i, fr in enumerate(frames):
@@ -47,6 +48,14 @@ def run_stream(stream, check_stages=True):
 def test_gpu_matches_reference(stream):
     bad, got, out_md5 = run_stream(stream)
     assert not bad, bad[:3]
+    assert got == out_md5 == BITS[stream]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", STREAMS)
+def test_gpu_level_schedule_matches_reference(stream):
+    # the level-launch schedule (the fallback for intra block copy frames) on every stream
+    bad, got, out_md5 = run_stream(stream, check_stages=False, schedule=0)
     assert got == out_md5 == BITS[stream]
 
 
