@@ -104,7 +104,6 @@ struct av1r_ctx {
     Upload meta[2];  // per-launch KParams + level tables
     int metaIdx = 0;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
-    hipEvent_t flowIn = nullptr, flowOut = nullptr;  // hand-off to / from the device's flow stream
     // debug timeline of every recon work item (env AV1R_TRACE_FILE): 8 x u64 per item
     FILE* traceFile = nullptr;
     unsigned long long* traceDev = nullptr;
@@ -750,20 +749,19 @@ static void job_end(FrameJob& j)
     c->lastUploadBytes = j.P->bytes;
 }
 
-// Every k_flow launch of a device runs on ONE stream.  Two k_flow grids resident at once
-// can starve each other: each one's progress needs a resident workgroup on every one of its
-// queues, and spinning workgroups of the other grid may hold the slots (measured: a
-// dependency wait timed out with four batches on four streams).  Other kernels always
-// finish, so they may overlap a k_flow freely.
-static hipStream_t flow_stream(int device)
-{
-    static std::mutex m;
-    static hipStream_t st[64] = {};
-    if (device < 0 || device >= 64) return nullptr;
-    std::lock_guard<std::mutex> lock(m);
-    if (!st[device] && hipStreamCreateWithFlags(&st[device], hipStreamNonBlocking) != hipSuccess) st[device] = nullptr;
-    return st[device];
-}
+// The k_flow launches of a device form ONE chain: each waits for the previous one,
+// whichever stream launched it.  Two k_flow grids resident at once can starve each other:
+// each one's progress needs a resident workgroup on every one of its queues, and spinning
+// workgroups of the other grid may hold the slots (measured: a dependency wait timed out
+// with four batches on four streams).  A launch from the same stream as the previous one
+// is ordered by the stream itself (no event wait: the batched bench case); other kernels
+// always finish, so they may overlap a k_flow freely.
+struct FlowChain {
+    std::mutex m;
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+};
+static FlowChain g_flowChain[64];
 
 static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 {
@@ -935,17 +933,18 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
             const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
-            hipStream_t fs = flow_stream(lc->device);
-            if (!fs) return fail(c, AV1R_E_DEVICE, "flow stream");
-            HIPCHK(hipEventRecord(lc->flowIn, st));
-            HIPCHK(hipStreamWaitEvent(fs, lc->flowIn, 0));
-            const int wslot = kpw_upload(lc->device, hk, n, fs);
+            if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
+            FlowChain& F = g_flowChain[lc->device];
+            std::lock_guard<std::mutex> lock(F.m);
+            if (!F.done) HIPCHK(hipEventCreateWithFlags(&F.done, hipEventDisableTiming));
+            if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
+            const int wslot = kpw_upload(lc->device, hk, n, st);
             if (wslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
-            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, trace, fs);
-            if (kpw_release(lc->device, wslot, fs)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
-            HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, fs));
-            HIPCHK(hipEventRecord(lc->flowOut, fs));
-            HIPCHK(hipStreamWaitEvent(st, lc->flowOut, 0));
+            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, trace, st);
+            HIPCHK(hipEventRecord(F.done, st));
+            F.last = st;
+            if (kpw_release(lc->device, wslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
+            HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, st));
         }
     }
     if (!flow && lc->timing) {
@@ -1075,8 +1074,6 @@ int av1r_create(int device, av1r_ctx** out)
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->meta[i].done, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&c->flowIn, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&c->flowOut, hipEventDisableTiming);
     for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
@@ -1103,8 +1100,6 @@ void av1r_destroy(av1r_ctx* c)
         }
     if (c->resDev) (void)hipFree(c->resDev);
     (void)hipEventDestroy(c->sync);
-    (void)hipEventDestroy(c->flowIn);
-    (void)hipEventDestroy(c->flowOut);
     if (c->traceDev) (void)hipFree(c->traceDev);
     if (c->traceFile) fclose(c->traceFile);
     for (auto& e : c->evPool)
