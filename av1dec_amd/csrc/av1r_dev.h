@@ -73,16 +73,24 @@ struct KParams {
     DevFrame ref[8];  // reference store slots
 };
 
-// launch batches: at most AV1R_MAX_BATCH frames per launch, AV1R_KP_SLOTS batches in
-// flight per device (recon.hip: g_kp)
+// launch batches: at most AV1R_MAX_BATCH frames per launch
 #define AV1R_MAX_BATCH 32
-#define AV1R_KP_SLOTS 8
+
+// The frames' parameters of a launch live at the start of its metadata buffer (uploaded
+// with one copy per batch) and are read through the constant address space: every field
+// is a scalar load the compiler may hoist anywhere (behind a plain global pointer the same
+// struct costs ~100 VGPRs of hoisted vector loads in k_inter, and the filters reload it
+// inside their pixel loops because the pixel stores might alias it).
+typedef const __attribute__((address_space(4))) KParams* KpConst;
+#define KP(kps, i) (*(const KParams*)(&((KpConst)(kps))[i]))
 
 // k_flow control block (recon.hip): FLOW_QUEUES queue heads, one 128-B line each, then
-// the error word; zeroed by the host before every launch
+// the error word and the address of the host's error word; written by the host before
+// every launch
 #define FLOW_QUEUES 8
 #define FLOW_LINE 32
 #define FLOW_ERR (FLOW_QUEUES * FLOW_LINE)
+#define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the host's pinned error word
 #define FLOW_CTL_BYTES 1280
 
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -28,22 +29,17 @@
 
 #include "av1r_dev.h"
 
-void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
+void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s);
-int kp_upload(int device, const KParams* host, int n, hipStream_t s);
-int kp_release(int device, int slot, hipStream_t s);
-void launch_k_lf(int slot, int n, int pass, int maxUnits, hipStream_t s);
-void launch_k_cdef(int slot, int n, int maxMiCols, int maxMiRows, hipStream_t s);
-void launch_k_lr(int slot, int n, int maxW, int maxH, hipStream_t s);
-int kpf_upload(int device, const KParams* host, int n, hipStream_t s);
-int kpf_release(int device, int slot, hipStream_t s);
+void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
+void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
+void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
+void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
 int flow_grid(int device);
-void launch_k_resid(int large, int slot, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
-int kpw_upload(int device, const KParams* host, int n, hipStream_t s);
-int kpw_release(int device, int slot, hipStream_t s);
-void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid,
-    unsigned long long* trace, hipStream_t s);
+void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
+    uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s);
 
 namespace {
 
@@ -59,8 +55,9 @@ struct Upload {
     uint8_t* dev = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;  // all work that reads this upload has finished
+    hipEvent_t ready = nullptr; // meta: the upload (on the context's copy stream) has landed
     bool pending = false;
-    uint32_t* err = nullptr;    // meta: pinned copy of the launch's k_flow error word
+    uint32_t* err = nullptr;    // meta: the launch's k_flow error word (pinned host memory the kernel writes)
 };
 
 struct Level {
@@ -101,9 +98,18 @@ struct av1r_ctx {
     bool keepStages = true;
     Upload up[2];
     int upIdx = 0;
-    Upload meta[2];  // per-launch KParams + level tables
+    // per-launch metadata (KParams, tables, flow groups): a ring, uploaded on a copy stream
+    // of its own so that the copy of batch N + 1 overlaps the kernels of batch N
+    static constexpr int kMetaRing = 3;
+    Upload meta[kMetaRing];
     int metaIdx = 0;
+    hipStream_t copyStream = nullptr;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
+    // this context's latest work was launched on joinLead's stream (a batch it was a member
+    // of) and nothing has been enqueued on its own stream since; ctx_join() orders its own
+    // stream after that work before anything else uses it
+    av1r_ctx* joinLead = nullptr;
+    hipEvent_t joinEv = nullptr;
     // debug timeline of every recon work item (env AV1R_TRACE_FILE): 8 x u64 per item
     FILE* traceFile = nullptr;
     unsigned long long* traceDev = nullptr;
@@ -157,6 +163,16 @@ struct av1r_ctx {
     size_t resCap = 0;
 };
 
+// Lazy cross-stream ordering of batch members (av1r_decode_prepared_batch): called before
+// anything enqueues on, or waits for, the context's own stream.
+static void ctx_join(av1r_ctx* c)
+{
+    if (!c || !c->joinLead) return;
+    (void)hipEventRecord(c->joinEv, c->joinLead->stream);
+    (void)hipStreamWaitEvent(c->stream, c->joinEv, 0);
+    c->joinLead = nullptr;
+}
+
 static int fail(av1r_ctx* c, int code, const char* fmt, ...)
 {
     char buf[512];
@@ -200,6 +216,7 @@ static FrameBuf* frame_get(av1r_ctx* c, int width, int height)
             delete f;
             return nullptr;
         }
+        ctx_join(c);
         (void)hipMemsetAsync(f->base, 0, need, c->stream);
         f->bytes = need;
         c->pool.push_back(f);
@@ -708,6 +725,7 @@ static int job_begin(FrameJob& j)
     j.k.cur = j.R->d;
     if (P.resElems > c->resCap) {
         if (c->resDev) {
+            ctx_join(c);
             HIPCHK(hipStreamSynchronize(c->stream));  // in-flight frames may still read it
             (void)hipFree(c->resDev);
             c->resDev = nullptr;
@@ -763,11 +781,26 @@ struct FlowChain {
 };
 static FlowChain g_flowChain[64];
 
+// AV1R_HOST_PROF: host time per phase of launch_jobs, printed when a context is destroyed
+struct HostProf {
+    double wait = 0, build = 0, launch = 0;
+    long calls = 0;
+};
+static HostProf g_hprof;
+static bool host_prof() { static const bool on = getenv("AV1R_HOST_PROF") != nullptr; return on; }
+static double now_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 {
+    const double tp0 = host_prof() ? now_us() : 0;
+    double tp1 = tp0, tp2 = tp0;
     av1r_ctx* c = lc;  // errors are reported on the launching context
     const int n = (int)jobs.size();
     if (n > AV1R_MAX_BATCH) return fail(c, AV1R_E_INVALID, "at most %d frames per batch", AV1R_MAX_BATCH);
+    ctx_join(lc);
     hipStream_t st = lc->stream;
     int rc;
     size_t nLevels = 0;
@@ -799,9 +832,10 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
     const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups + resTabBytes : 0);
     Upload& M = lc->meta[lc->metaIdx];
-    lc->metaIdx = (lc->metaIdx + 1) % 2;
+    lc->metaIdx = (lc->metaIdx + 1) % av1r_ctx::kMetaRing;
     if (M.pending) {
         HIPCHK(hipEventSynchronize(M.done));
+        if (host_prof()) tp1 = now_us();
         M.pending = false;
         if (M.err && *M.err) {
             *M.err = 0;
@@ -854,6 +888,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         // frames interleaved; {frame << 8 | n, first item}: n = 0 one large item, else
         // 1..4 small items
         memset(M.host + kBytes + tabBytes, 0, FLOW_CTL_BYTES);
+        *reinterpret_cast<uint32_t**>(M.host + kBytes + tabBytes + 4 * FLOW_HOSTERR) = M.err;
         uint32_t* g = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES);
         for (size_t l = 0; l < nLevels; l++)
             for (int i = 0; i < n; i++) {
@@ -877,7 +912,16 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             rt[n + 2 + i] = rt[n + 1 + i] + jobs[i].P->nResidL;
         }
     }
-    HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, st));
+    if (host_prof()) tp2 = now_us();
+    // AV1R_META_COPY=1: an SDMA copy on the context's copy stream instead of k_fetch
+    static const bool sdma = getenv("AV1R_META_COPY") && atoi(getenv("AV1R_META_COPY")) != 0;
+    if (sdma) {
+        HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, lc->copyStream));
+        HIPCHK(hipEventRecord(M.ready, lc->copyStream));
+        HIPCHK(hipStreamWaitEvent(st, M.ready, 0));
+    } else {
+        launch_k_fetch(M.dev, M.host, need, st);
+    }
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
 
     if (lc->timing) {
@@ -905,8 +949,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     };
 
     // ---- reconstruction, level by level (frame parameters in a constant-memory slot)
-    const int slot = kp_upload(lc->device, hk, n, st);
-    if (slot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
+    // the frames' KParams head the metadata buffer (read through the constant address space)
+    const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
     size_t allItems = 0;
     for (uint32_t v : total) allItems += v;
     allItems = std::max<size_t>(allItems, frameRows);
@@ -921,13 +965,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     static std::atomic<uint32_t> epochs{0};
     if (flow) {
         // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
-        if (total[0]) launch_k_level(0, slot, dtab, n, total[0], trace, ~0u, st);
+        if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
         const uint32_t* hrt = reinterpret_cast<const uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
-        if (hrt[n]) launch_k_resid(0, slot, drt, n, hrt[n], st);
-        if (hrt[2 * n + 1]) launch_k_resid(1, slot, drt + n + 1, n, hrt[2 * n + 1], st);
+        if (hrt[n]) launch_k_resid(0, dk, drt, n, hrt[n], st);
+        if (hrt[2 * n + 1]) launch_k_resid(1, dk, drt + n + 1, n, hrt[2 * n + 1], st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
         if (nGroups) {
             uint32_t epoch = ++epochs;
@@ -938,13 +982,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             std::lock_guard<std::mutex> lock(F.m);
             if (!F.done) HIPCHK(hipEventCreateWithFlags(&F.done, hipEventDisableTiming));
             if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
-            const int wslot = kpw_upload(lc->device, hk, n, st);
-            if (wslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
-            launch_k_flow(wslot, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, epoch, grid, trace, st);
+            launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, M.err, epoch, grid, trace, st);
             HIPCHK(hipEventRecord(F.done, st));
             F.last = st;
-            if (kpw_release(lc->device, wslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
-            HIPCHK(hipMemcpyAsync(M.err, ctl + FLOW_ERR, 4, hipMemcpyDeviceToHost, st));
         }
     }
     if (!flow && lc->timing) {
@@ -953,9 +993,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     for (size_t l = 0; l < nLevels && !flow; l++) {
         const uint32_t nInter = total[l * 3], nLarge = total[l * 3 + 1], nSmall = total[l * 3 + 2];
-        if (nInter) launch_k_level(0, slot, dtab + l * tabW, n, nInter, trace, traceBase, st);
+        if (nInter) launch_k_level(0, dk, dtab + l * tabW, n, nInter, trace, traceBase, st);
         traceBase += nInter;
-        if (nLarge + nSmall) launch_k_level(1, slot, dtab + l * tabW + tabI, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
+        if (nLarge + nSmall) launch_k_level(1, dk, dtab + l * tabW + tabI, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
         traceBase += nLarge + nSmall;
     }
     if (trace) {
@@ -980,19 +1020,16 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         fwrite(hv.data(), 8, hv.size(), lc->traceFile);
         fflush(lc->traceFile);
     }
-    if (kp_release(lc->device, slot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
     HIPCHK(hipGetLastError());
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
     // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place, 2 passes
-    const int fslot = kpf_upload(lc->device, hk, n, st);
-    if (fslot < 0) return fail(c, AV1R_E_DEVICE, "frame parameter upload");
-    launch_k_lf(fslot, n, 0, maxUnits, st);
-    launch_k_lf(fslot, n, 1, maxUnits, st);
+    launch_k_lf(dk, n, 0, maxUnits, st);
+    launch_k_lf(dk, n, 1, maxUnits, st);
     if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
     // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
-    launch_k_cdef(fslot, n, maxMiCols, maxMiRows, st);
+    launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
     if (snap) {
         frame_ref(jobs[0].C);
         frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
@@ -1000,13 +1037,19 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
     // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
-    if (anyLr) launch_k_lr(fslot, n, maxW, maxH, st);
-    if (kpf_release(lc->device, fslot, st)) return fail(c, AV1R_E_DEVICE, "frame parameter slot");
+    if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(M.done, st));
     M.pending = true;
     for (auto& j : jobs) job_end(j);
+    if (host_prof()) {
+        const double tp3 = now_us();
+        g_hprof.wait += (tp1 > tp0 ? tp1 : tp0) - tp0;
+        g_hprof.build += tp2 - (tp1 > tp0 ? tp1 : tp0);
+        g_hprof.launch += tp3 - tp2;
+        g_hprof.calls++;
+    }
     return AV1R_OK;
 }
 
@@ -1023,6 +1066,7 @@ static int launch_frame(av1r_ctx* c, const Prepared& P)
 // streaming path: one pinned staging buffer -> one async H2D copy (ring of 2)
 static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
 {
+    ctx_join(c);
     c->skipSlotCheck = true;  // slot presence is checked at launch time
     int rc = validate(c, b);
     c->skipSlotCheck = false;
@@ -1072,8 +1116,17 @@ int av1r_create(int device, av1r_ctx** out)
         return AV1R_E_DEVICE;
     }
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
-    for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->meta[i].done, hipEventDisableTiming);
+    for (auto& m : c->meta) {
+        (void)hipEventCreateWithFlags(&m.done, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&m.ready, hipEventDisableTiming);
+    }
+    if (hipStreamCreateWithFlags(&c->copyStream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return AV1R_E_DEVICE;
+    }
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->joinEv, hipEventDisableTiming);
     for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
@@ -1084,22 +1137,32 @@ int av1r_create(int device, av1r_ctx** out)
 void av1r_destroy(av1r_ctx* c)
 {
     if (!c) return;
+    ctx_join(c);
+    if (host_prof() && g_hprof.calls) {
+        fprintf(stderr, "av1r host: %ld launches, per launch wait %.1f us, build %.1f us, launch %.1f us\n", g_hprof.calls,
+            g_hprof.wait / g_hprof.calls, g_hprof.build / g_hprof.calls, g_hprof.launch / g_hprof.calls);
+        g_hprof = HostProf();
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (FrameBuf* f : c->pool) {
         (void)hipFree(f->base);
         delete f;
     }
-    for (auto* ring : {c->up, c->meta})
-        for (int i = 0; i < 2; i++) {
-            Upload& u = ring[i];
-            if (u.host) (void)hipHostFree(u.host);
-            if (u.dev) (void)hipFree(u.dev);
-            if (u.err) (void)hipHostFree(u.err);
-            (void)hipEventDestroy(u.done);
-        }
+    auto freeUpload = [](Upload& u) {
+        if (u.host) (void)hipHostFree(u.host);
+        if (u.dev) (void)hipFree(u.dev);
+        if (u.err) (void)hipHostFree(u.err);
+        (void)hipEventDestroy(u.done);
+        if (u.ready) (void)hipEventDestroy(u.ready);
+    };
+    for (auto& u : c->up) freeUpload(u);
+    for (auto& u : c->meta) freeUpload(u);
+    (void)hipStreamSynchronize(c->copyStream);
+    (void)hipStreamDestroy(c->copyStream);
     if (c->resDev) (void)hipFree(c->resDev);
     (void)hipEventDestroy(c->sync);
+    (void)hipEventDestroy(c->joinEv);
     if (c->traceDev) (void)hipFree(c->traceDev);
     if (c->traceFile) fclose(c->traceFile);
     for (auto& e : c->evPool)
@@ -1267,17 +1330,21 @@ int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n)
         std::vector<FrameJob> sub(jobs.begin() + part * jobs.size() / k, jobs.begin() + (part + 1) * jobs.size() / k);
         av1r_ctx* sl = sub[0].c;
         av1r_ctx* c = sl;
-        // the launch stream waits for every member's earlier work, and they for the batch
+        // the launch stream waits for every member's earlier work on its own stream (none
+        // if the member's latest work was a batch on this same stream); a member's own
+        // stream is ordered after the batch only when it is next used (ctx_join): no
+        // cross-queue signal between back-to-back batches
+        ctx_join(sl);
         for (auto& j : sub)
-            if (j.c != sl) {
+            if (j.c != sl && j.c->joinLead != sl) {
+                ctx_join(j.c);
                 HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
                 HIPCHK(hipStreamWaitEvent(sl->stream, j.c->sync, 0));
             }
         int rc = launch_jobs(sl, sub);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(sl->sync, sl->stream));
         for (auto& j : sub)
-            if (j.c != sl) HIPCHK(hipStreamWaitEvent(j.c->stream, sl->sync, 0));
+            if (j.c != sl) j.c->joinLead = sl;
     }
     return AV1R_OK;
 }
@@ -1285,6 +1352,7 @@ int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n)
 int av1r_release_prepared(av1r_ctx* c, int handle)
 {
     if (!c || handle < 0 || handle >= (int)c->prepared.size() || !c->prepared[handle]) return AV1R_E_INVALID;
+    ctx_join(c);
     (void)hipStreamSynchronize(c->stream);
     if (c->prepared[handle]->dev) (void)hipFree(c->prepared[handle]->dev);
     delete c->prepared[handle];
@@ -1302,6 +1370,7 @@ int av1r_set_discard_output(av1r_ctx* c, int discard)
 int av1r_show_existing(av1r_ctx* c, int slot, int refresh)
 {
     if (!c || slot < 0 || slot > 7 || !c->slots[slot]) return AV1R_E_INVALID;
+    ctx_join(c);
     FrameBuf* f = c->slots[slot];
     frame_ref(f);  // hold across the refresh
     frame_ref(f);
@@ -1329,6 +1398,7 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
 {
     if (!c) return AV1R_E_INVALID;
     if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
+    ctx_join(c);
     FrameBuf* f = c->outq.front();
     if (width) *width = f->d.width;
     if (height) *height = f->d.height;
@@ -1347,6 +1417,7 @@ int av1r_read_stage(av1r_ctx* c, int stage, int plane, uint8_t* dst, int ds)
 {
     if (!c || stage < 0 || stage > 3 || plane < 0 || plane > 2 || !c->stage[stage]) return AV1R_E_INVALID;
     (void)hipSetDevice(c->device);
+    ctx_join(c);
     int rc = copy_plane_d2h(c, c->stage[stage]->d.pl[plane], dst, ds);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1356,6 +1427,7 @@ int av1r_read_stage(av1r_ctx* c, int stage, int plane, uint8_t* dst, int ds)
 int av1r_synchronize(av1r_ctx* c)
 {
     if (!c) return AV1R_E_INVALID;
+    ctx_join(c);
     HIPCHK(hipStreamSynchronize(c->stream));
     return AV1R_OK;
 }
@@ -1390,6 +1462,7 @@ int av1r_last_frame_times(av1r_ctx* c, float* recon, float* lf, float* cdef, flo
 int av1r_stage_times(av1r_ctx* c, float* totals, int* frames)
 {
     if (!c || !totals) return AV1R_E_INVALID;
+    ctx_join(c);
     HIPCHK(hipStreamSynchronize(c->stream));
     for (int i = 0; i < 4; i++) totals[i] = 0.f;
     for (size_t f = 0; f < c->evUsed; f++)
@@ -1417,6 +1490,7 @@ int av1r_set_schedule(av1r_ctx* c, int mode)
 int av1r_recon_kernel_times(av1r_ctx* c, float* totals, int* frames)
 {
     if (!c || !totals) return AV1R_E_INVALID;
+    ctx_join(c);
     HIPCHK(hipStreamSynchronize(c->stream));
     for (int i = 0; i < 3; i++) totals[i] = 0.f;
     for (size_t f = 0; f < c->evUsed; f++) {

@@ -13,11 +13,10 @@
 //           LoopRestoration Wiener (LoopRestoration.cpp:247-277) and self-guided
 //           (:284-479) with the stripe/unit geometry of :33-189; the 3-pixel border
 //           extension (:196-198) is coordinate clamping.
-#include "av1r_dev.h"
-#include "kp_const.h"
+#include <algorithm>
 
-// Frame parameters of a launch: constant-address-space slots (kp_const.h).
-AV1R_KP_TABLE(g_kpf, kpf_upload, kpf_release)
+#include "av1r_dev.h"
+
 
 // ------------------------------------------------------------------------------------
 // Deblocking
@@ -117,9 +116,9 @@ DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int bl
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
-extern "C" __global__ __launch_bounds__(256) void k_lf(int slot, int pass)
+extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass)
 {
-    const KParams& k = g_kpf[slot][blockIdx.y];  // frame of this launch row
+    const KParams& k = KP(kps, blockIdx.y);  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
     if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
     const int planeMask = 1 | (hd.lf_level[2] ? 2 : 0) | (hd.lf_level[3] ? 4 : 0);
@@ -355,10 +354,10 @@ DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int 
 }
 
 // grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.cur, writes k.cdef
-extern "C" __global__ __launch_bounds__(256) void k_cdef(int slot)
+extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
 {
     __shared__ CdefLds L;
-    const KParams& k = g_kpf[slot][blockIdx.z];
+    const KParams& k = KP(kps, blockIdx.z);
     const int t = threadIdx.x;
     const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;  // mi units
     if (r0 >= k.mi_rows || c0 >= k.mi_cols) return;
@@ -590,11 +589,11 @@ DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, in
 
 // one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
 // frame (k.cdef) and the deblocked frame (k.cur, stripe rows), writes k.lrout.
-extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
+extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-    const KParams& k = g_kpf[slot][blockIdx.z / 3];
+    const KParams& k = KP(kps, blockIdx.z / 3);
     if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
     const int plane = blockIdx.z % 3, sub = plane ? 1 : 0;
     const DevPlane C = k.cdef.pl[plane];
@@ -758,6 +757,24 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(int slot)
     }
 }
 
+// The launch metadata, copied by the compute queue itself from pinned host memory (the
+// device reads it over the bus, bypassing the caches): no copy-engine hand-off between a
+// batch's last filter and the next batch's first kernel (an SDMA copy there started
+// ~75 us after the preceding kernel ended).
+extern "C" __global__ __launch_bounds__(256) void k_fetch(uint32_t* __restrict__ dst, uint32_t* src, size_t n4)
+{
+    // system-scope loads (sc0 sc1): never a stale cached copy of the host's rewritten ring slot
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s)
+{
+    const size_t n4 = (bytes + 3) / 4;
+    const unsigned grid = (unsigned)std::min<size_t>(1024, (n4 + 255) / 256);
+    hipLaunchKernelGGL(k_fetch, dim3(grid ? grid : 1), dim3(256), 0, s, reinterpret_cast<uint32_t*>(dst),
+        reinterpret_cast<uint32_t*>(const_cast<void*>(src)), n4);
+}
+
 // plain visible-region copy (stage snapshots)
 extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 {
@@ -768,19 +785,19 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 
 // ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
-void launch_k_lf(int slot, int n, int pass, int maxUnits, hipStream_t s)
+void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, slot, pass);
+    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
 }
-void launch_k_cdef(int slot, int n, int maxMiCols, int maxMiRows, hipStream_t s)
+void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, slot);
+    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
 }
-void launch_k_lr(int slot, int n, int maxW, int maxH, hipStream_t s)
+void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {
     // tile rows: luma stripes (64 rows from -8) in halves; chroma stripes whole
     const int tilesY = 2 * ((maxH + 8 + 63) / 64);
-    hipLaunchKernelGGL(k_lr, dim3((maxW + LR_TW - 1) / LR_TW, tilesY, 3 * n), dim3(256), 0, s, slot);
+    hipLaunchKernelGGL(k_lr, dim3((maxW + LR_TW - 1) / LR_TW, tilesY, 3 * n), dim3(256), 0, s, kps);
 }
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s)
 {

@@ -17,7 +17,6 @@
 // item reads was finalised by an earlier launch.
 #include "av1r_dev.h"
 #include "intra_dev.h"
-#include "kp_const.h"
 #include "txfm_dev.h"
 
 #define AV1R_TRACE_W 16  // u64 per item in the debug timeline
@@ -1131,25 +1130,18 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
 // One launch per dependency level: every work item of the level (inter tiles, inter-
 // intra blends, transform blocks) is one 64-lane workgroup.
 // ---------------------------------------------------------------------------------
-// Frame parameters of a launch: constant-address-space slots (kp_const.h).
 // recon.hip is compiled twice (native.py): the level kernels (k_inter, k_tb), and with
 // -DAV1R_FLOW_PART k_flow alone -- built without machine-level loop-invariant hoisting,
 // which in its persistent loop keeps ~50 constants in VGPRs (177 instead of 124 VGPRs:
 // half the occupancy) but which k_inter's pixel loops want.  Each object has its own
 // constant-memory parameter table.
 #define TB_SMALL 16  // the largest TB side handled one per wave (k_tb, k_flow)
-#ifndef AV1R_FLOW_PART
-AV1R_KP_TABLE(g_kp, kp_upload, kp_release)
-#else
-AV1R_KP_TABLE(g_kpw, kpw_upload, kpw_release)
-#define g_kp g_kpw
-#endif
 
 #ifndef AV1R_FLOW_PART
 // Level table of one launch over n frames (tab[0..n]: prefix sums of the frames' item
 // counts; tab[n + 1 + s]: offset of frame s's items in its item list).  `lane` indexes the
 // table (one lane per frame); item `b` of the launch.  Returns the frame's parameters.
-DEV const WorkItem& table_item(int slot, const uint32_t* __restrict__ tab, int n, uint32_t b, const KParams*& kp,
+DEV const WorkItem& table_item(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, const KParams*& kp,
     int& s)
 {
     // frame of item b: the number of frames whose items all precede it (one vector load
@@ -1157,7 +1149,7 @@ DEV const WorkItem& table_item(int slot, const uint32_t* __restrict__ tab, int n
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
-    kp = &g_kp[slot][s];
+    kp = &KP(kps, s);
     return kp->items[tab[n + 1 + s] + (b - tab[s])];
 }
 
@@ -1165,7 +1157,7 @@ DEV const WorkItem& table_item(int slot, const uint32_t* __restrict__ tab, int n
 // more, and the blends) take a whole 256-lane workgroup each; small TBs (up to 16x16) are
 // packed four per workgroup, one per wave, each wave with its own small LDS tiles.
 // tab: [big prefix (n + 1)][small prefix (n + 1)][big offsets (n)][small offsets (n)].
-extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t* __restrict__ tab, int n,
+extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
@@ -1180,7 +1172,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
         const int lane = threadIdx.x & 63;
         const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
         s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
-        kp = &g_kp[slot][s];
+        kp = &KP(kps, s);
         const WorkItem& wi = kp->items[tab[2 * n + 2 + s] + (b - tab[s])];
 #ifdef AV1R_TRACE
         unsigned long long* tr = trace ? trace + (size_t)(traceBase + b) * AV1R_TRACE_W : nullptr;
@@ -1206,7 +1198,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tabS[lane + 1] : 0xffffffffu;
     s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(i >= pre)));
-    kp = &g_kp[slot][s];
+    kp = &KP(kps, s);
     const WorkItem& wi = kp->items[tab[3 * n + 2 + s] + (i - tabS[s])];
 #ifdef AV1R_TRACE
     unsigned long long* tr = trace ? trace + (size_t)(traceBase + nBig + i) * AV1R_TRACE_W : nullptr;
@@ -1233,14 +1225,14 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(int slot, const uint32_t*
 #else
 #define K_INTER_BOUNDS __launch_bounds__(64, 4)
 #endif
-extern "C" __global__ K_INTER_BOUNDS void k_inter(int slot, const uint32_t* __restrict__ tab, int n,
+extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
 {
     __shared__ InterLds L;
     const unsigned long long tEntry = trace ? trace_now() : 0;
     const KParams* kp;
     int s;
-    const WorkItem& wi = table_item(slot, tab, n, blockIdx.x, kp, s);
+    const WorkItem& wi = table_item(kps, tab, n, blockIdx.x, kp, s);
     const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
 #ifdef AV1R_TRACE
     // traceBase ~0u (k_flow mode): frame-major rows, this frame's base + the item position
@@ -1302,7 +1294,12 @@ DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint
                 if (__all(ok)) break;
                 const bool dead = __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                 if (dead || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT) {
-                    if (lane == 0) __hip_atomic_store(ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) {
+                        __hip_atomic_store(ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        // the host's copy (pinned memory, checked when the launch's metadata is reused)
+                        __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(ctl + FLOW_HOSTERR)),
+                            1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     b = nd;
                     break;
                 }
@@ -1366,7 +1363,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
 // workgroup), n = 1..4 small items (one per wave)
-extern "C" __global__ __launch_bounds__(256, 4) void k_flow(int slot, const uint2* __restrict__ groups, uint32_t nGroups,
+extern "C" __global__ __launch_bounds__(256, 4) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
     uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
@@ -1387,7 +1384,7 @@ extern "C" __global__ __launch_bounds__(256, 4) void k_flow(int slot, const uint
         if (threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
         const uint2 gd = groups[g];
-        const KParams& k = g_kp[slot][gd.x >> 8];
+        const KParams& k = KP(kps, gd.x >> 8);
         const uint32_t n = gd.x & 0xff;
         if (n == 0) {
             flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8);
@@ -1423,10 +1420,11 @@ int flow_grid(int device)
     return cache[device];
 }
 
-void launch_k_flow(int slot, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t epoch, int grid,
-    unsigned long long* trace, hipStream_t s)
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
+    uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, slot, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
+    (void)hostErr;  // (its address travels in the control block: FLOW_HOSTERR)
+    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
         trace);
 }
 
@@ -1465,41 +1463,41 @@ DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
     }
 }
 
-extern "C" __global__ __launch_bounds__(256) void k_resid_s(int slot, const uint32_t* __restrict__ tab, int n)
+extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ __align__(16) int16_t res[16][16 * 18];
     const uint32_t b = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
-    const KParams& k = g_kp[slot][s];
+    const KParams& k = KP(kps, s);
     const int g = threadIdx.x >> 4;
     const uint32_t ti = k.resid_s[(b - tab[s]) * 16 + g];
     if (ti != ~0u) resid_one<16, 16>(k, ti, res[g]);
 }
 
-extern "C" __global__ __launch_bounds__(64) void k_resid_l(int slot, const uint32_t* __restrict__ tab, int n)
+extern "C" __global__ __launch_bounds__(64) void k_resid_l(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ __align__(16) int16_t res[64 * 66];
     const uint32_t b = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
-    const KParams& k = g_kp[slot][s];
+    const KParams& k = KP(kps, s);
     resid_one<64, 64>(k, k.resid_l[b - tab[s]], res);
 }
 
-void launch_k_resid(int large, int slot, const uint32_t* tab, int n, unsigned groups, hipStream_t s)
+void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s)
 {
-    if (large) hipLaunchKernelGGL(k_resid_l, dim3(groups), dim3(64), 0, s, slot, tab, n);
-    else hipLaunchKernelGGL(k_resid_s, dim3(groups), dim3(256), 0, s, slot, tab, n);
+    if (large) hipLaunchKernelGGL(k_resid_l, dim3(groups), dim3(64), 0, s, kps, tab, n);
+    else hipLaunchKernelGGL(k_resid_s, dim3(groups), dim3(256), 0, s, kps, tab, n);
 }
 
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4)
-void launch_k_level(int kind, int slot, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
+void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
 {
-    if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, slot, tab, n, trace, traceBase);
-    else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, slot, tab, n, trace, traceBase);
+    if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, kps, tab, n, trace, traceBase);
+    else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, kps, tab, n, trace, traceBase);
 }
 #endif  // !AV1R_FLOW_PART
