@@ -518,7 +518,7 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
 // Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the (rh + 7)
 // window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).  Four
 // outputs per lane from three LDS dwords when rw is a multiple of 4.
-DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0, int wcs = WC)
+DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0, int wcs = WC, int hstr = TS)
 {
     if ((rw & 3) == 0) {
         const int g4 = rw >> 2;
@@ -544,7 +544,7 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
             uint2 v;
             v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
             v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-            *reinterpret_cast<uint2*>(hb + i * TS + 4 * g) = v;
+            *reinterpret_cast<uint2*>(hb + i * hstr + 4 * g) = v;
         }
         return;
     }
@@ -554,7 +554,7 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
         int hs = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) hs += hf[u] * row[u];
-        hb[i * TS + j] = (int16_t)r2(hs, R0);
+        hb[i * hstr + j] = (int16_t)r2(hs, R0);
     }
 }
 
@@ -572,7 +572,7 @@ DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, 
 }
 // Four horizontally adjacent samples (cc a multiple of 4): 8 LDS reads of 4 int16.
 DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer, int* out,
-    int wcs = WC)
+    int wcs = WC, int hstr = TS)
 {
     if (integer) {
 #pragma unroll
@@ -582,7 +582,7 @@ DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0
     int s[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < 8; t++) {
-        const uint2 v = *reinterpret_cast<const uint2*>(hb + (rr + t) * TS + cc);
+        const uint2 v = *reinterpret_cast<const uint2*>(hb + (rr + t) * hstr + cc);
         s[0] += vf[t] * (int16_t)(v.x & 0xffff);
         s[1] += vf[t] * (int16_t)(v.x >> 16);
         s[2] += vf[t] * (int16_t)(v.y & 0xffff);
@@ -882,6 +882,112 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     }
 }
 
+// Both chroma planes of a single-PU, unwarped, unscaled block at once (the common case of
+// predict_pu for planes 1 and 2): the four reference windows (U, V x both references)
+// are fetched in one round trip and each pass runs for both planes between the same two
+// barriers, instead of one window round trip and three barriers per plane.  The tile
+// region is [rx0, rx0 + rw) x [ry0, ry0 + rh) of the block (rw a multiple of 4); plane p
+// lands in L.tile + p * C2_TILE.  Returns false, before touching LDS, when a reference is
+// warped or scaled (the caller then predicts plane by plane).
+#define C2_WS 24                   // chroma window row stride (<= 16 + 7 columns)
+#define C2_WIN (23 * C2_WS)        // one chroma window (<= 16 + 7 rows)
+#define C2_HS 16                   // chroma intermediate row stride
+#define C2_HB (23 * C2_HS)         // one chroma intermediate
+#define C2_TILE (16 * TS)          // chroma tile of plane 2 after plane 1's
+DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, int x, int y, int w, int h, int rx0,
+    int ry0, int rw, int rh)
+{
+    const int t = threadIdx.x;
+    const av1r_mi& info = mi_at(k, blk.mi_row, blk.mi_col);
+    RefSel R[2][2];
+    const int isCompound = setup_refs(k, blk, 1, x, y, w, h, blk.mi_row, blk.mi_col, R[0]);
+    if (!R[0][0].useWin || (isCompound && !R[0][1].useWin)) return false;
+    setup_refs(k, blk, 2, x, y, w, h, blk.mi_row, blk.mi_col, R[1]);
+    const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
+    int16_t hf[2][8], vf[2][8];
+    int integer[2] = {1, 1};
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+        if (l > isCompound) break;
+        const int hph = (R[0][l].startX >> 6) & 15, vph = (R[0][l].startY >> 6) & 15;
+        integer[l] = !hph && !vph;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            hf[l][u] = av1r_subpel_filters[(R[0][l].filtX * 16 + hph) * 8 + u];
+            vf[l][u] = av1r_subpel_filters[(R[0][l].filtY * 16 + vph) * 8 + u];
+        }
+    }
+    const int ct = blk.compound_type;
+    int mode;  // as predict_pu
+    if (!isCompound) mode = 0;
+    else if (ct == AV1R_COMPOUND_AVERAGE) mode = 1;
+    else if (ct == AV1R_COMPOUND_DISTANCE) mode = 2;
+    else mode = 3;
+    int fwd = 0, bck = 0;
+    if (mode == 2) distance_weights(k, info, fwd, bck);
+    WedgeSel ws = {0, 0, 0, 0};
+    if (mode == 3 && ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
+    uint8_t* win = &L.win[0][0];
+    int16_t* hb = &L.u.hbw[0][0];
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int l = 0; l < 2; l++)
+            if (l <= isCompound) load_window(R[p][l], win + (p * 2 + l) * C2_WIN, rx0, ry0, rw, rh, C2_WS);
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int l = 0; l < 2; l++)
+            if (l <= isCompound && !integer[l])
+                hpass(win + (p * 2 + l) * C2_WIN, hb + (p * 2 + l) * C2_HB, rw, rh, hf[l], R0, C2_WS, C2_HS);
+    __syncthreads();
+    const int g4 = rw >> 2;
+    for (int q = t; q < 2 * rh * g4; q += 64) {
+        const int p = q >= rh * g4, e = q - p * rh * g4;
+        const int rr = e / g4, cc = (e - rr * g4) * 4;
+        int p0[4], p1[4] = {0, 0, 0, 0};
+        pred_win4(win + (p * 2) * C2_WIN, hb + (p * 2) * C2_HB, rr, cc, R0, R1, vf[0], integer[0], p0, C2_WS, C2_HS);
+        if (isCompound)
+            pred_win4(win + (p * 2 + 1) * C2_WIN, hb + (p * 2 + 1) * C2_HB, rr, cc, R0, R1, vf[1], integer[1], p1, C2_WS, C2_HS);
+        uint8_t* tile = L.tile + p * C2_TILE;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const int r = ry0 + rr, c = rx0 + cc + m;  // block-relative
+            int v;
+            if (mode == 0) {
+                v = clip1(p0[m]);
+            } else if (mode == 1) {
+                v = clip1(r2(p0[m] + p1[m], 1 + PostRound));
+            } else if (mode == 2) {
+                v = clip1(r2(fwd * p0[m] + bck * p1[m], 4 + PostRound));
+            } else {
+                // 4:2:0 chroma mask: average of the 2x2 luma-resolution entries (maskBlend,
+                // InterPredict.cpp:584-609); the luma pass left the diff-weighted mask in L.mask
+                int s4 = 0;
+#pragma unroll
+                for (int dy = 0; dy < 2; dy++)
+#pragma unroll
+                    for (int dx = 0; dx < 2; dx++) {
+                        int mv;
+                        if (ct == AV1R_COMPOUND_WEDGE) {
+                            int mw = wedge_master(ws.dir, ws.yoff + 2 * r + dy, ws.xoff + 2 * c + dx);
+                            mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
+                        } else {
+                            mv = L.mask[(2 * rr + dy) * TS + 2 * (cc + m) + dx];
+                        }
+                        s4 += mv;
+                    }
+                const int mk = r2(s4, 2);
+                v = clip1(r2(mk * p0[m] + (64 - mk) * p1[m], 6 + PostRound));
+            }
+            tile[rr * TS + cc + m] = (uint8_t)v;
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
 // overlappedMotionCompensation (InterPredict.cpp:611-709) restricted to the tile
 // [TX0, TX0 + TW) x [TY0, TY0 + TH) (block-relative plane coordinates).
 DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int baseX, int baseY, int w, int h,
@@ -1007,6 +1113,19 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
     for (int plane = 0; plane < nPl; plane++) {
         const PlaneGeo G = plane_geo(k, blk, plane, tx, ty);
         if (plane == 0) trace_stamp(tr, 11);
+        if (plane == 1 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col &&
+            blk.motion_mode != AV1R_OBMC_CAUSAL && !(G.TW & 3) &&
+            predict_chroma2(k, blk, L, G.baseX, G.baseY, G.pw, G.ph, G.TX0, G.TY0, G.TW, G.TH)) {
+            for (int q = t; q < 2 * G.TW * G.TH; q += 64) {
+                const int p = q >= G.TW * G.TH, e = q - p * G.TW * G.TH;
+                const int i = e / G.TW, j = e - i * G.TW;
+                px(k.cur.pl[1 + p], G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[p * C2_TILE + i * TS + j];
+            }
+            __syncthreads();
+            trace_stamp(tr, 9);
+            trace_stamp(tr, 10);
+            break;
+        }
         {
             int r = 0;
             for (int yy = 0; yy < G.ph; yy += G.predH) {
