@@ -65,7 +65,9 @@ struct Level {
     // blends, TBs with a side >= 32: a workgroup each) and [2] small TBs (one per wave).
     // Within [1] and [2] the inter TBs come last: k_flow takes the first fcnt (inter TBs
     // are finished by k_resid there)
+    // The last sm0 inter tiles are small plain blocks (k_inter_s, four per wave; see build_schedule).
     uint32_t off[3] = {}, cnt[3] = {}, fcnt[3] = {};
+    uint32_t sm0 = 0;
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -515,6 +517,27 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             return av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
         };
         auto interTb = [&](uint32_t code) { return (b->blocks[b->tbs[AV1R_ITEM_INDEX(code)].block].flags & AV1R_BLK_INTER) != 0; };
+        // inter tiles: [the rest][small plain blocks].  Small plain = both luma sides <= 8,
+        // simple motion, no mask compound, no intra block copy, no global warp: what
+        // k_inter_s predicts (its frames' references must also be unscaled, checked per launch)
+        std::vector<uint32_t>& P = c->lvP[l];
+        auto smallTile = [&](uint32_t code) {
+            const av1r_block& blk = b->blocks[AV1R_ITEM_INDEX(code) >> 4];
+            const int bs = blk.mi_size;
+            if (av1r_num4x4w[bs] > 2 || av1r_num4x4h[bs] > 2) return false;
+            if (blk.motion_mode != AV1R_SIMPLE_TRANSLATION || (blk.flags & AV1R_BLK_INTRABC)) return false;
+            const av1r_mi& info = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col];
+            if (info.ref_frame[1] > AV1R_INTRA_FRAME && blk.compound_type != AV1R_COMPOUND_AVERAGE &&
+                blk.compound_type != AV1R_COMPOUND_DISTANCE)
+                return false;
+            if (blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV)
+                for (int r = 0; r < 2; r++)
+                    if (info.ref_frame[r] > AV1R_INTRA_FRAME && h->gm_type[info.ref_frame[r] & 7] > AV1R_GM_TRANSLATION)
+                        return false;
+            return true;
+        };
+        std::stable_partition(P.begin(), P.end(), [&](uint32_t code) { return !smallTile(code); });
+        c->levels[l].sm0 = (uint32_t)std::count_if(P.begin(), P.end(), smallTile);
         std::vector<uint32_t>& T = c->lvT[l];
         // [large intra][large inter][small intra][small inter]
         std::stable_sort(T.begin(), T.end(), [&](uint32_t a, uint32_t b2) {
@@ -700,6 +723,7 @@ struct FrameJob {
     const Prepared* P = nullptr;
     KParams k;
     FrameBuf *R = nullptr, *C = nullptr, *L = nullptr;
+    bool scaled = false;  // a reference differs in size from the frame (no k_inter_s tiles)
 };
 
 // resolve references, allocate the frame's buffers, fill its KParams
@@ -718,6 +742,12 @@ static int job_begin(FrameJob& j)
     j.k.items = P.dItems;
     for (int s = 0; s < 8; s++)
         if (c->slots[s]) j.k.ref[s] = c->slots[s]->d;
+    j.scaled = false;
+    for (int r = 1; r < 8; r++)
+        if (P.usedRef[r]) {
+            const DevFrame& f = c->slots[h->ref_frame_idx[r - 1]]->d;
+            j.scaled |= f.width != h->frame_width || f.height != h->frame_height;
+        }
     j.R = frame_get(c, h->frame_width, h->frame_height);
     j.C = frame_get(c, h->frame_width, h->frame_height);
     j.L = h->uses_lr ? frame_get(c, h->frame_width, h->frame_height) : nullptr;
@@ -817,8 +847,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         anyLr |= h->uses_lr != 0;
     }
     // launch metadata: [KParams x n][per level: k_inter table (n + 1 prefix counts, n item
-    // offsets), k_tb table (large prefix, small prefix, large offsets, small offsets)]
-    const size_t tabI = 2 * (size_t)n + 1, tabT = 4 * (size_t)n + 2, tabW = tabI + tabT;
+    // offsets), k_inter_s table (n + 1 group prefix, n offsets, n counts), k_tb table (large
+    // prefix, small prefix, large offsets, small offsets)]
+    const size_t tabI = 2 * (size_t)n + 1, tabS = 3 * (size_t)n + 1, tabT = 4 * (size_t)n + 2, tabW = tabI + tabS + tabT;
     const size_t kBytes = align256(sizeof(KParams) * n);
     const size_t tabBytes = align256(4 * tabW * std::max<size_t>(nLevels, 1));
     // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
@@ -862,25 +893,33 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         for (const Level& lv : jobs[i].P->levels) frameRows += lv.cnt[0] + lv.cnt[1] + lv.cnt[2];
     }
     uint32_t* tab = reinterpret_cast<uint32_t*>(M.host + kBytes);
-    // total[l * 3 + kind]: items of the level's inter / large / small lists
-    std::vector<uint32_t> total(nLevels * 3, 0);
+    // total[l * 4 + kind]: workgroups of the level's k_inter / k_inter_s launches, items of
+    // its large / small TB lists; totalS: its small inter tiles
+    std::vector<uint32_t> total(nLevels * 4, 0), totalS(nLevels, 0);
     for (size_t l = 0; l < nLevels; l++) {
         uint32_t* ti = tab + l * tabW;       // k_inter
-        uint32_t* tt = ti + tabI;            // k_tb
-        ti[0] = tt[0] = tt[n + 1] = 0;
+        uint32_t* ts = ti + tabI;            // k_inter_s
+        uint32_t* tt = ts + tabS;            // k_tb
+        ti[0] = ts[0] = tt[0] = tt[n + 1] = 0;
         for (int i = 0; i < n; i++) {
             const auto& lv = jobs[i].P->levels;
             const bool has = l < lv.size();
-            ti[i + 1] = ti[i] + (has ? lv[l].cnt[0] : 0);
+            const uint32_t sm = has && !jobs[i].scaled ? lv[l].sm0 : 0;
+            ti[i + 1] = ti[i] + (has ? lv[l].cnt[0] - sm : 0);
             ti[n + 1 + i] = has ? lv[l].off[0] : 0;
+            ts[i + 1] = ts[i] + (sm + 3) / 4;
+            ts[n + 1 + i] = has ? lv[l].off[0] + lv[l].cnt[0] - sm : 0;
+            ts[2 * n + 1 + i] = sm;
+            totalS[l] += sm;
             tt[i + 1] = tt[i] + (has ? lv[l].cnt[1] : 0);
             tt[n + 2 + i] = tt[n + 1 + i] + (has ? lv[l].cnt[2] : 0);
             tt[2 * n + 2 + i] = has ? lv[l].off[1] : 0;
             tt[3 * n + 2 + i] = has ? lv[l].off[2] : 0;
         }
-        total[l * 3 + 0] = ti[n];
-        total[l * 3 + 1] = tt[n];
-        total[l * 3 + 2] = tt[2 * n + 1];
+        total[l * 4 + 0] = ti[n];
+        total[l * 4 + 1] = ts[n];
+        total[l * 4 + 2] = tt[n];
+        total[l * 4 + 3] = tt[2 * n + 1];
     }
     uint32_t* ctl = reinterpret_cast<uint32_t*>(M.dev + kBytes + tabBytes);
     if (flow) {
@@ -966,6 +1005,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (flow) {
         // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
         if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
+        if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
@@ -992,10 +1032,11 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         HIPCHK(hipEventRecord(lc->ev[6], st));
     }
     for (size_t l = 0; l < nLevels && !flow; l++) {
-        const uint32_t nInter = total[l * 3], nLarge = total[l * 3 + 1], nSmall = total[l * 3 + 2];
+        const uint32_t nInter = total[l * 4], nInterS = total[l * 4 + 1], nLarge = total[l * 4 + 2], nSmall = total[l * 4 + 3];
         if (nInter) launch_k_level(0, dk, dtab + l * tabW, n, nInter, trace, traceBase, st);
-        traceBase += nInter;
-        if (nLarge + nSmall) launch_k_level(1, dk, dtab + l * tabW + tabI, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
+        if (nInterS) launch_k_level(2, dk, dtab + l * tabW + tabI, n, nInterS, trace, traceBase, st);
+        traceBase += nInter + totalS[l];  // (k_inter_s writes no timeline rows)
+        if (nLarge + nSmall) launch_k_level(1, dk, dtab + l * tabW + tabI + tabS, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
         traceBase += nLarge + nSmall;
     }
     if (trace) {
@@ -1014,8 +1055,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         } else {
             size_t q = 0;
             for (size_t l = 0; l < nLevels; l++)
-                for (int kk = 0; kk < 3; kk++)
-                    for (uint32_t i = 0; i < total[l * 3 + kk]; i++, q++) hv[q * 16 + 6] = l;
+                for (uint32_t i = 0; i < total[l * 4] + totalS[l] + total[l * 4 + 2] + total[l * 4 + 3]; i++, q++)
+                    hv[q * 16 + 6] = l;
         }
         fwrite(hv.data(), 8, hv.size(), lc->traceFile);
         fflush(lc->traceFile);

@@ -372,14 +372,32 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
 #define WARP_ROWS 16              // warped regions are predicted in chunks of 16 rows
 #define HBN ((TS + 7) * TS)       // horizontal rows; >= warp intermediates (TS * WARP_ROWS / 64 * 120)
 
-struct InterLds {
-    uint8_t tile[TS * TS];        // this plane's tile, assembled before the store
-    uint8_t mask[TS * TS];        // compute_prediction's Mask (luma, persists across planes)
-    uint8_t win[2][(TS + 7) * WC];  // reference windows (luma, or the current plane)
+// LDS of one tile of edge TSZ: TS for k_inter, 8 for k_inter_s (four tiles per wave)
+template <int TSZ>
+struct InterLdsT {
+    static constexpr int WCS = TSZ + 8;            // window row stride
+    static constexpr int HBS = (TSZ + 7) * TSZ;    // >= warp intermediates (TSZ * min(TSZ, WARP_ROWS) / 64 * 120)
+    uint8_t tile[TSZ * TSZ];      // this plane's tile, assembled before the store
+    uint8_t mask[TSZ * TSZ];      // compute_prediction's Mask (luma, persists across planes)
+    uint8_t win[2][(TSZ + 7) * WCS];  // reference windows (luma, or the current plane)
     struct {
-        int16_t hbw[2][HBN];      // horizontally filtered window rows / warp intermediates
+        int16_t hbw[2][HBS];      // horizontally filtered window rows / warp intermediates
     } u;
 };
+using InterLds = InterLdsT<TS>;
+static_assert(InterLdsT<TS>::HBS == HBN, "inter LDS");
+
+// NT lanes per tile: 64 (k_inter: one tile per single-wave workgroup, workgroup barriers)
+// or 16 (k_inter_s: four tiles per wave, wave-level ordering only -- the tiles of a wave
+// take different paths, and a one-wave workgroup needs no s_barrier)
+template <int NT>
+DEV int il_lane() { return NT == 64 ? (int)threadIdx.x : (int)(threadIdx.x & (NT - 1)); }
+template <int NT>
+DEV void il_sync()
+{
+    if (NT == 64) __syncthreads();
+    else coop_sync<NT>();
+}
 
 struct RefSel {
     DevPlane p;
@@ -492,6 +510,7 @@ DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1)
 // [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin).  Rows are
 // clamped per row; when no column needs clamping the row is moved as aligned dwords
 // (two loads funnel-shifted into one aligned LDS dword), otherwise byte by byte.
+template <int NT = 64>
 DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, int rh, int wcs = WC)
 {
     const int wx0 = (R.startX >> 10) - 3 + rx0, wy0 = (R.startY >> 10) - 3 + ry0;
@@ -499,7 +518,7 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
     if (wx0 >= 0 && wx0 + wc - 1 <= R.lastX) {
         const int ndw = (wc + 3) >> 2, sh = (wx0 & 3) * 8;
         const int ax0 = wx0 & ~3;
-        for (int q = threadIdx.x; q < ndw * wr; q += 64) {
+        for (int q = il_lane<NT>(); q < ndw * wr; q += NT) {
             const int i = q / ndw, d = q - i * ndw;
             const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, wy0 + i) * R.p.stride + ax0 + 4 * d;
             const uint32_t lo = *reinterpret_cast<const uint32_t*>(row);
@@ -508,7 +527,7 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
         }
         return;
     }
-    for (int q = threadIdx.x; q < wc * wr; q += 64) {
+    for (int q = il_lane<NT>(); q < wc * wr; q += NT) {
         int i = q / wc, j = q - i * wc;
         int yy = CLIP3(0, R.lastY, wy0 + i), xx = CLIP3(0, R.lastX, wx0 + j);
         win[i * wcs + j] = R.p.p[(size_t)yy * R.p.stride + xx];
@@ -518,11 +537,12 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
 // Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the (rh + 7)
 // window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).  Four
 // outputs per lane from three LDS dwords when rw is a multiple of 4.
+template <int NT = 64>
 DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0, int wcs = WC, int hstr = TS)
 {
     if ((rw & 3) == 0) {
         const int g4 = rw >> 2;
-        for (int q = threadIdx.x; q < (rh + 7) * g4; q += 64) {
+        for (int q = il_lane<NT>(); q < (rh + 7) * g4; q += NT) {
             const int i = q / g4, g = q - i * g4;
             const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + i * wcs) + g;
             const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2];
@@ -548,7 +568,7 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
         }
         return;
     }
-    for (int q = threadIdx.x; q < (rh + 7) * rw; q += 64) {
+    for (int q = il_lane<NT>(); q < (rh + 7) * rw; q += NT) {
         const int i = q / rw, j = q - i * rw;
         const uint8_t* row = win + i * wcs + j;
         int hs = 0;
@@ -561,13 +581,13 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
 // The same sample as pred_direct for an unscaled, unwarped reference: the vertical pass
 // over the staged intermediate rows (or the integer-position copy from the window).
 DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer,
-    int wcs = WC)
+    int wcs = WC, int hstr = TS)
 {
     if (integer) return (int16_t)(win[(rr + 3) * wcs + cc + 3] << (14 - R0 - R1));
-    const int16_t* col = hb + rr * TS + cc;
+    const int16_t* col = hb + rr * hstr + cc;
     int s = 0;
 #pragma unroll
-    for (int t = 0; t < 8; t++) s += vf[t] * col[t * TS];
+    for (int t = 0; t < 8; t++) s += vf[t] * col[t * hstr];
     return (int16_t)r2(s, R1);
 }
 // Four horizontally adjacent samples (cc a multiple of 4): 8 LDS reads of 4 int16.
@@ -608,10 +628,11 @@ DEV void warp_origin(const RefSel& R, int i8, int j8, int puX, int puY, int sub,
     iy4 = y4 >> 16;
     sy4 = y4 & 0xffff;
 }
+template <int NT = 64>
 DEV void warp_hpass(const RefSel& R, int16_t* hb, int rx0, int ry0, int rw, int rh, int puX, int puY, int sub, int R0)
 {
     const int w8 = rw >> 3, nb = (rh >> 3) * w8;
-    for (int q = threadIdx.x; q < nb * 120; q += 64) {
+    for (int q = il_lane<NT>(); q < nb * 120; q += NT) {
         const int b = q / 120, e = q - b * 120;
         const int bi = b / w8;
         const int i8 = (ry0 >> 3) + bi, j8 = (rx0 >> 3) + (b - bi * w8);
@@ -663,6 +684,7 @@ DEV int wedge_master(int dir, int i, int j)
 struct WedgeSel {
     int dir, xoff, yoff, flip;
 };
+template <int NT = 64>
 DEV WedgeSel wedge_select(int bs, int wedge)
 {
     int w = av1r_num4x4w[bs] * 4, h = av1r_num4x4h[bs] * 4;
@@ -673,12 +695,12 @@ DEV WedgeSel wedge_select(int bs, int wedge)
     s.xoff = 32 - ((cb[1] * w) >> 3);
     s.yoff = 32 - ((cb[2] * h) >> 3);
     // flipSign (initialise_wedge_mask_table, InterPredict.cpp:870-877)
-    // (the w + h - 1 edge samples summed across each wave; call with all 64 lanes active)
+    // (the w + h - 1 edge samples summed across the tile's NT lanes; call with all of them active)
     int sum = 0;
-    for (int i = threadIdx.x & 63; i < w + h - 1; i += 64)  // every wave sums all of them
+    for (int i = threadIdx.x & (NT - 1); i < w + h - 1; i += NT)
         sum += i < w ? wedge_master(s.dir, s.yoff, s.xoff + i) : wedge_master(s.dir, s.yoff + i - w + 1, s.xoff);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    for (int o = NT / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, NT);
     int avg = (sum + (w + h - 1) / 2) / (w + h - 1);
     s.flip = avg < 32;
     return s;
@@ -753,10 +775,11 @@ DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, in
 // predict_inter for the PU-relative region [rx0, rx0 + rw) x [ry0, ry0 + rh) of the
 // w x h prediction unit at plane position (x, y); sample (r, c) of the PU lands in
 // L.tile[(toy + r) * TS + tox + c].  Ends with a barrier.
-DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int x, int y,
+template <int NT, int TSZ>
+DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int plane, int x, int y,
     int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy)
 {
-    const int t = threadIdx.x;
+    const int t = il_lane<NT>();
     const av1r_mi& info = mi_at(k, candRow, candCol);
     const int sub = plane ? 1 : 0;
     RefSel R[2];
@@ -784,7 +807,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     int fwd = 0, bck = 0;
     if (mode == 2) distance_weights(k, info, fwd, bck);
     WedgeSel ws = {0, 0, 0, 0};
-    if (mode == 3 && ct == AV1R_COMPOUND_WEDGE) ws = wedge_select(blk.mi_size, blk.wedge_index);
+    if (mode == 3 && ct == AV1R_COMPOUND_WEDGE) ws = wedge_select<NT>(blk.mi_size, blk.wedge_index);
     const int diffwtdLuma = ct == AV1R_COMPOUND_DIFFWTD && plane == 0;
 
     // a warped region goes in chunks of WARP_ROWS rows (its 15 x 8 intermediates per 8x8
@@ -793,14 +816,14 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
     const int ryA = ry0, rhA = rh;
     for (int cy = 0; cy < rhA; cy += chunkH) {
     const int ry0 = ryA + cy, rh = imin(chunkH, rhA - cy);  // this chunk
-    if (R[0].useWin) load_window(R[0], L.win[0], rx0, ry0, rw, rh);
-    if (isCompound && R[1].useWin) load_window(R[1], L.win[1], rx0, ry0, rw, rh);
-    __syncthreads();
-    if (R[0].useWin && !integer[0]) hpass(L.win[0], L.u.hbw[0], rw, rh, hf[0], R0);
-    if (R[0].warp) warp_hpass(R[0], L.u.hbw[0], rx0, ry0, rw, rh, x, y, sub, R0);
-    if (isCompound && R[1].useWin && !integer[1]) hpass(L.win[1], L.u.hbw[1], rw, rh, hf[1], R0);
-    if (isCompound && R[1].warp) warp_hpass(R[1], L.u.hbw[1], rx0, ry0, rw, rh, x, y, sub, R0);
-    __syncthreads();
+    if (R[0].useWin) load_window<NT>(R[0], L.win[0], rx0, ry0, rw, rh, L.WCS);
+    if (isCompound && R[1].useWin) load_window<NT>(R[1], L.win[1], rx0, ry0, rw, rh, L.WCS);
+    il_sync<NT>();
+    if (R[0].useWin && !integer[0]) hpass<NT>(L.win[0], L.u.hbw[0], rw, rh, hf[0], R0, L.WCS, TSZ);
+    if (R[0].warp) warp_hpass<NT>(R[0], L.u.hbw[0], rx0, ry0, rw, rh, x, y, sub, R0);
+    if (isCompound && R[1].useWin && !integer[1]) hpass<NT>(L.win[1], L.u.hbw[1], rw, rh, hf[1], R0, L.WCS, TSZ);
+    if (isCompound && R[1].warp) warp_hpass<NT>(R[1], L.u.hbw[1], rx0, ry0, rw, rh, x, y, sub, R0);
+    il_sync<NT>();
     auto blend = [&](int p0, int p1, int r, int c) {
         int v;
         if (mode == 0) {
@@ -818,13 +841,13 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
                 diff = r2(diff, PostRound);
                 int mm = CLIP3(0, 64, 38 + diff / 16);
                 m = blk.mask_type ? 64 - mm : mm;
-                L.mask[(toy + r) * TS + tox + c] = (uint8_t)m;
+                L.mask[(toy + r) * TSZ + tox + c] = (uint8_t)m;
             } else if (!sub) {
                 if (ct == AV1R_COMPOUND_WEDGE) {
                     int mv = wedge_master(ws.dir, ws.yoff + r, ws.xoff + c);
                     m = blk.wedge_sign == ws.flip ? mv : 64 - mv;
                 } else {
-                    m = L.mask[(toy + r) * TS + tox + c];
+                    m = L.mask[(toy + r) * TSZ + tox + c];
                 }
             } else {
                 // 4:2:0 chroma: average of the 2x2 luma-resolution mask entries
@@ -838,7 +861,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
                             int mw = wedge_master(ws.dir, ws.yoff + 2 * r + dy, ws.xoff + 2 * c + dx);
                             mv = blk.wedge_sign == ws.flip ? mw : 64 - mw;
                         } else {
-                            mv = L.mask[(2 * (toy + r) + dy) * TS + 2 * (tox + c) + dx];
+                            mv = L.mask[(2 * (toy + r) + dy) * TSZ + 2 * (tox + c) + dx];
                         }
                         s4 += mv;
                     }
@@ -846,22 +869,22 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
             }
             v = clip1(r2(m * p0 + (64 - m) * p1, 6 + PostRound));
         }
-        L.tile[(toy + r) * TS + tox + c] = (uint8_t)v;
+        L.tile[(toy + r) * TSZ + tox + c] = (uint8_t)v;
     };
     auto sample = [&](int l, int rr, int cc) {
         const int r = ry0 + rr, c = rx0 + cc;
-        return R[l].useWin ? pred_win(L.win[l], L.u.hbw[l], rr, cc, R0, R1, vf[l], integer[l])
+        return R[l].useWin ? pred_win(L.win[l], L.u.hbw[l], rr, cc, R0, R1, vf[l], integer[l], L.WCS, TSZ)
              : R[l].warp   ? warp_v(R[l], L.u.hbw[l], rr, cc, r, c, rw, x, y, sub, R1)
                            : pred_direct(R[l], r, c, R0, R1);
     };
     if ((rw & 3) == 0 && R[0].useWin && (!isCompound || R[1].useWin)) {
         // four adjacent samples per lane (window references only)
         const int g4 = rw >> 2;
-        for (int q = t; q < rh * g4; q += 64) {
+        for (int q = t; q < rh * g4; q += NT) {
             const int rr = q / g4, cc = (q - rr * g4) * 4;
             int p0[4], p1[4] = {0, 0, 0, 0};
-            pred_win4(L.win[0], L.u.hbw[0], rr, cc, R0, R1, vf[0], integer[0], p0);
-            if (isCompound) pred_win4(L.win[1], L.u.hbw[1], rr, cc, R0, R1, vf[1], integer[1], p1);
+            pred_win4(L.win[0], L.u.hbw[0], rr, cc, R0, R1, vf[0], integer[0], p0, L.WCS, TSZ);
+            if (isCompound) pred_win4(L.win[1], L.u.hbw[1], rr, cc, R0, R1, vf[1], integer[1], p1, L.WCS, TSZ);
             // one blend body, the four samples rotated through it (no unrolled copies)
             int a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
             int b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
@@ -873,12 +896,12 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLds& L, int pl
             }
         }
     } else {
-        for (int q = t; q < rw * rh; q += 64) {
+        for (int q = t; q < rw * rh; q += NT) {
             const int rr = q / rw, cc = q - rr * rw;
             blend(sample(0, rr, cc), isCompound ? sample(1, rr, cc) : 0, ry0 + rr, rx0 + cc);
         }
     }
-    __syncthreads();
+    il_sync<NT>();
     }
 }
 
@@ -990,10 +1013,11 @@ DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, i
 
 // overlappedMotionCompensation (InterPredict.cpp:611-709) restricted to the tile
 // [TX0, TX0 + TW) x [TY0, TY0 + TH) (block-relative plane coordinates).
-DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, int baseX, int baseY, int w, int h,
+template <int NT, int TSZ>
+DEV void obmc(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int plane, int baseX, int baseY, int w, int h,
     int TX0, int TY0, int TW, int TH)
 {
-    const int t = threadIdx.x;
+    const int t = il_lane<NT>();
     const int sub = plane ? 1 : 0;
     const int bs = blk.mi_size;
     const av1r_frame_hdr& hd = *k.hdr;
@@ -1037,20 +1061,20 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLds& L, int plane, i
                         vf[u] = av1r_subpel_filters[(R.filtY * 16 + vph) * 8 + u];
                     }
                     if (R.useWin) {
-                        load_window(R, L.win[0], rx0, ry0, rw, rh);
-                        __syncthreads();
-                        if (!integer) hpass(L.win[0], L.u.hbw[0], rw, rh, hf, 3);
-                        __syncthreads();
+                        load_window<NT>(R, L.win[0], rx0, ry0, rw, rh, L.WCS);
+                        il_sync<NT>();
+                        if (!integer) hpass<NT>(L.win[0], L.u.hbw[0], rw, rh, hf, 3, L.WCS, TSZ);
+                        il_sync<NT>();
                     }
-                    for (int q = t; q < rw * rh; q += 64) {
+                    for (int q = t; q < rw * rh; q += NT) {
                         const int rr = q / rw, cc = q - rr * rw, i = ry0 + rr, j = rx0 + cc;
-                        int p = R.useWin ? pred_win(L.win[0], L.u.hbw[0], rr, cc, 3, 11, vf, integer)
+                        int p = R.useWin ? pred_win(L.win[0], L.u.hbw[0], rr, cc, 3, 11, vf, integer, L.WCS, TSZ)
                                          : pred_direct(R, i, j, 3, 11);
                         int m = pass ? mask[j] : mask[i];
-                        uint8_t& d = L.tile[(oy + i - TY0) * TS + ox + j - TX0];
+                        uint8_t& d = L.tile[(oy + i - TY0) * TSZ + ox + j - TX0];
                         d = (uint8_t)clip1(r2(m * d + (64 - m) * clip1(p), 6));
                     }
-                    __syncthreads();
+                    il_sync<NT>();
                 }
             }
             pos4 += step4;
@@ -1064,6 +1088,7 @@ struct PlaneGeo {
     int TX0, TY0, TW, TH;          // the tile, block-relative
     int candRow, candCol, predW, predH;  // prediction units (Block.cpp:146-174)
 };
+template <int TSZ>
 DEV PlaneGeo plane_geo(const KParams& k, const av1r_block& blk, int plane, int tx, int ty)
 {
     PlaneGeo G;
@@ -1075,10 +1100,10 @@ DEV PlaneGeo plane_geo(const KParams& k, const av1r_block& blk, int plane, int t
     G.baseY = (blk.mi_row >> sub) * 4;
     G.pw = n4w * 4;
     G.ph = n4h * 4;
-    G.TX0 = (tx * TS) >> sub;
-    G.TY0 = (ty * TS) >> sub;
-    G.TW = imin(TS >> sub, G.pw - G.TX0);
-    G.TH = imin(TS >> sub, G.ph - G.TY0);
+    G.TX0 = (tx * TSZ) >> sub;
+    G.TY0 = (ty * TSZ) >> sub;
+    G.TW = imin(TSZ >> sub, G.pw - G.TX0);
+    G.TH = imin(TSZ >> sub, G.ph - G.TY0);
     // sub-8x8 chroma may gather several prediction units
     G.candRow = (blk.mi_row >> sub) << sub;
     G.candCol = (blk.mi_col >> sub) << sub;
@@ -1101,9 +1126,10 @@ DEV PlaneGeo plane_geo(const KParams& k, const av1r_block& blk, int plane, int t
 }
 
 // One tile (tx, ty) of inter block `bi`: all planes.
-DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, unsigned long long* tr)
+template <int NT, int TSZ>
+DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ>& L, unsigned long long* tr)
 {
-    const int t = threadIdx.x;
+    const int t = il_lane<NT>();
     const av1r_block& blk = k.blocks[bi];
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
     // timeline (-DAV1R_TRACE): 1 = block size | motion mode << 8 | compound << 12, 8 + plane
@@ -1111,20 +1137,22 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
     trace_put(tr, 1, blk.mi_size | (blk.motion_mode << 8) |
         ((mi_at(k, blk.mi_row, blk.mi_col).ref_frame[1] > AV1R_INTRA_FRAME) << 12));
     for (int plane = 0; plane < nPl; plane++) {
-        const PlaneGeo G = plane_geo(k, blk, plane, tx, ty);
+        const PlaneGeo G = plane_geo<TSZ>(k, blk, plane, tx, ty);
         if (plane == 0) trace_stamp(tr, 11);
-        if (plane == 1 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col &&
-            blk.motion_mode != AV1R_OBMC_CAUSAL && !(G.TW & 3) &&
-            predict_chroma2(k, blk, L, G.baseX, G.baseY, G.pw, G.ph, G.TX0, G.TY0, G.TW, G.TH)) {
-            for (int q = t; q < 2 * G.TW * G.TH; q += 64) {
-                const int p = q >= G.TW * G.TH, e = q - p * G.TW * G.TH;
-                const int i = e / G.TW, j = e - i * G.TW;
-                px(k.cur.pl[1 + p], G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[p * C2_TILE + i * TS + j];
+        if constexpr (TSZ == TS) {
+            if (plane == 1 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col &&
+                blk.motion_mode != AV1R_OBMC_CAUSAL && !(G.TW & 3) &&
+                predict_chroma2(k, blk, L, G.baseX, G.baseY, G.pw, G.ph, G.TX0, G.TY0, G.TW, G.TH)) {
+                for (int q = t; q < 2 * G.TW * G.TH; q += NT) {
+                    const int p = q >= G.TW * G.TH, e = q - p * G.TW * G.TH;
+                    const int i = e / G.TW, j = e - i * G.TW;
+                    px(k.cur.pl[1 + p], G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[p * C2_TILE + i * TS + j];
+                }
+                il_sync<NT>();
+                trace_stamp(tr, 9);
+                trace_stamp(tr, 10);
+                break;
             }
-            __syncthreads();
-            trace_stamp(tr, 9);
-            trace_stamp(tr, 10);
-            break;
         }
         {
             int r = 0;
@@ -1134,7 +1162,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
                     const int ix0 = imax(xx, G.TX0), ix1 = imin(xx + G.predW, G.TX0 + G.TW);
                     const int iy0 = imax(yy, G.TY0), iy1 = imin(yy + G.predH, G.TY0 + G.TH);
                     if (ix0 < ix1 && iy0 < iy1)
-                        predict_pu(k, blk, L, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
+                        predict_pu<NT, TSZ>(k, blk, L, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
                             G.candCol + c, ix0 - xx, iy0 - yy, ix1 - ix0, iy1 - iy0, xx - G.TX0, yy - G.TY0);
                     c++;
                 }
@@ -1143,13 +1171,13 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLds& L, 
         }
         if (plane == 0) trace_stamp(tr, 12);
         if (blk.motion_mode == AV1R_OBMC_CAUSAL)
-            obmc(k, blk, L, plane, G.baseX, G.baseY, G.predW, G.predH, G.TX0, G.TY0, G.TW, G.TH);
+            obmc<NT, TSZ>(k, blk, L, plane, G.baseX, G.baseY, G.predW, G.predH, G.TX0, G.TY0, G.TW, G.TH);
         const DevPlane& dst = k.cur.pl[plane];
-        for (int q = t; q < G.TW * G.TH; q += 64) {
+        for (int q = t; q < G.TW * G.TH; q += NT) {
             int i = q / G.TW, j = q - i * G.TW;
-            px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[i * TS + j];
+            px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[i * TSZ + j];
         }
-        __syncthreads();
+        il_sync<NT>();
         trace_stamp(tr, 8 + plane);
     }
 }
@@ -1365,8 +1393,119 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint
     trace_put(tr, 2, tEntry);
     trace_put(tr, 0, wi.code);
     trace_stamp(tr, 3);
-    inter_tile(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
+    inter_tile<64, TS>(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
     trace_stamp(tr, 5);
+}
+
+// ---------------------------------------------------------------------------------
+// k_inter_s: small plain inter blocks, four per wave.
+//
+// Blocks with both luma sides <= 8 are most of an inter frame's tiles, and k_inter gives
+// each a whole wave (and its 128-VGPR register budget for every prediction mode) while
+// its 8x8 luma needs 16 lanes.  The plain ones (simple motion, single reference or
+// average / distance compound, unwarped, unscaled: classified by the host, build_schedule)
+// go here instead: 16 lanes per block, the unit's state per lane, ~1 KB of LDS each, the
+// samples stored straight to the frame -- many more blocks in flight per CU.
+// ---------------------------------------------------------------------------------
+struct SmallLds {
+    uint8_t win[2][15 * 16];  // reference windows: <= 8 + 7 rows, stride 16
+    int16_t hb[2][15 * 8];    // their horizontally filtered rows
+};
+
+// One prediction unit (predict_inter, InterPredict.cpp:962-1049; blockInterPrediction's
+// sub-pel filter, :319-383; the average / distance blend of :1022-1049) of w x h <= 8 x 8
+// at plane position (x, y).
+DEV void small_pu(const KParams& k, SmallLds& L, int ct, int plane, int x, int y, int w, int h, int candRow, int candCol)
+{
+    const int t = threadIdx.x & 15;
+    const av1r_mi& info = mi_at(k, candRow, candCol);
+    const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
+    int16_t hf[2][8], vf[2][8];
+    int integer[2] = {1, 1};
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+        if (l > isCompound) break;
+        RefSel R;
+        select_ref(k, R, k.hdr->ref_frame_idx[info.ref_frame[l] - 1], plane, x, y, info.mv[l]);
+        const int fx = filter_idx(info.filt, w, 1), fy = filter_idx(info.filt, h, 0);
+        const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
+        integer[l] = !hph && !vph;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            hf[l][u] = av1r_subpel_filters[(fx * 16 + hph) * 8 + u];
+            vf[l][u] = av1r_subpel_filters[(fy * 16 + vph) * 8 + u];
+        }
+        load_window<16>(R, L.win[l], 0, 0, w, h, 16);
+    }
+    coop_sync<16>();
+#pragma unroll
+    for (int l = 0; l < 2; l++)
+        if (l <= isCompound && !integer[l]) hpass<16>(L.win[l], L.hb[l], w, h, hf[l], 3, 16, 8);
+    coop_sync<16>();
+    const int R1 = isCompound ? 7 : 11, PostRound = 14 - (3 + R1);
+    int fwd = 0, bck = 0;
+    const int dist = isCompound && ct == AV1R_COMPOUND_DISTANCE;
+    if (dist) distance_weights(k, info, fwd, bck);
+    auto blend = [&](int p0, int p1) {
+        return !isCompound ? clip1(p0)
+             : dist        ? clip1(r2(fwd * p0 + bck * p1, 4 + PostRound))
+                           : clip1(r2(p0 + p1, 1 + PostRound));
+    };
+    const DevPlane& dst = k.cur.pl[plane];
+    if (!(w & 3)) {
+        const int g4 = w >> 2;
+        for (int q = t; q < h * g4; q += 16) {
+            const int rr = q / g4, cc = (q - rr * g4) * 4;
+            int p0[4], p1[4] = {0, 0, 0, 0};
+            pred_win4(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], p0, 16, 8);
+            if (isCompound) pred_win4(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], p1, 16, 8);
+            uint32_t v = 0;
+#pragma unroll
+            for (int m = 0; m < 4; m++) v |= (uint32_t)blend(p0[m], p1[m]) << (8 * m);
+            *reinterpret_cast<uint32_t*>(&px(dst, x + cc, y + rr)) = v;  // x, cc: multiples of 4
+        }
+    } else {
+        for (int q = t; q < h * w; q += 16) {
+            const int rr = q / w, cc = q - rr * w;
+            const int p0 = pred_win(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], 16, 8);
+            const int p1 = isCompound ? pred_win(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], 16, 8) : 0;
+            px(dst, x + cc, y + rr) = (uint8_t)blend(p0, p1);
+        }
+    }
+    coop_sync<16>();  // the next unit reuses the windows
+}
+
+// Frames' lists are dealt in groups of four (a frame's last group may be partial), so the
+// parameters of a workgroup stay uniform.  tab: [group prefix (n + 1)][offsets (n)][counts (n)].
+#ifdef AV1R_KIS_WAVES
+#define K_INTER_S_BOUNDS __launch_bounds__(64, AV1R_KIS_WAVES)
+#else
+#define K_INTER_S_BOUNDS __launch_bounds__(64)
+#endif
+extern "C" __global__ K_INTER_S_BOUNDS void k_inter_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ SmallLds L[4];
+    const int lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+    const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    const KParams& k = KP(kps, s);
+    const int g = threadIdx.x >> 4;
+    const uint32_t i = 4 * (b - tab[s]) + g;
+    if (i >= tab[2 * n + 1 + s]) return;  // (wave-level ordering only: no barrier follows)
+    const av1r_block& blk = k.blocks[AV1R_ITEM_INDEX(k.items[tab[n + 1 + s] + i].code) >> 4];
+    const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
+    for (int plane = 0; plane < nPl; plane++) {
+        // (sub-8x8 chroma may gather up to four units of neighbouring blocks)
+        const PlaneGeo G = plane_geo<8>(k, blk, plane, 0, 0);
+        int r = 0;
+        for (int yy = 0; yy < G.ph; yy += G.predH, r++) {
+            int c = 0;
+            for (int xx = 0; xx < G.pw; xx += G.predW, c++)
+                small_pu(k, L[g], blk.compound_type, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
+                    G.candCol + c);
+        }
+    }
 }
 
 #endif  // !AV1R_FLOW_PART
@@ -1612,11 +1751,13 @@ void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, u
     else hipLaunchKernelGGL(k_resid_s, dim3(groups), dim3(256), 0, s, kps, tab, n);
 }
 
-// kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4)
+// kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4);
+// kind 2: small inter tiles, `items` groups of four
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
 {
     if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, kps, tab, n, trace, traceBase);
+    else if (kind == 2) hipLaunchKernelGGL(k_inter_s, dim3(items), dim3(64), 0, s, kps, tab, n);
     else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, kps, tab, n, trace, traceBase);
 }
 #endif  // !AV1R_FLOW_PART
