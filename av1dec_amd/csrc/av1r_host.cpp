@@ -65,9 +65,10 @@ struct Level {
     // blends, TBs with a side >= 32: a workgroup each) and [2] small TBs (one per wave).
     // Within [1] and [2] the inter TBs come last: k_flow takes the first fcnt (inter TBs
     // are finished by k_resid there)
-    // The last sm0 inter tiles are small plain blocks (k_inter_s, four per wave; see build_schedule).
+    // List [0] ends with pl[0] medium then pl[1] small plain blocks (k_inter_m two per wave,
+    // k_inter_s four per wave; see build_schedule).
     uint32_t off[3] = {}, cnt[3] = {}, fcnt[3] = {};
-    uint32_t sm0 = 0;
+    uint32_t pl[2] = {};
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -517,27 +518,29 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             return av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
         };
         auto interTb = [&](uint32_t code) { return (b->blocks[b->tbs[AV1R_ITEM_INDEX(code)].block].flags & AV1R_BLK_INTER) != 0; };
-        // inter tiles: [the rest][small plain blocks].  Small plain = both luma sides <= 8,
-        // simple motion, no mask compound, no intra block copy, no global warp: what
-        // k_inter_s predicts (its frames' references must also be unscaled, checked per launch)
+        // inter tiles: [the rest][medium plain][small plain].  Plain = simple motion, no mask
+        // compound, no intra block copy, no global warp: what k_inter_m / k_inter_s predict
+        // (their frames' references must also be unscaled, checked per launch); small = both
+        // luma sides <= 8, medium = both <= 16
         std::vector<uint32_t>& P = c->lvP[l];
-        auto smallTile = [&](uint32_t code) {
+        auto plainClass = [&](uint32_t code) {  // 0 k_inter, 1 medium, 2 small
             const av1r_block& blk = b->blocks[AV1R_ITEM_INDEX(code) >> 4];
             const int bs = blk.mi_size;
-            if (av1r_num4x4w[bs] > 2 || av1r_num4x4h[bs] > 2) return false;
-            if (blk.motion_mode != AV1R_SIMPLE_TRANSLATION || (blk.flags & AV1R_BLK_INTRABC)) return false;
+            if (av1r_num4x4w[bs] > 4 || av1r_num4x4h[bs] > 4) return 0;
+            if (blk.motion_mode != AV1R_SIMPLE_TRANSLATION || (blk.flags & AV1R_BLK_INTRABC)) return 0;
             const av1r_mi& info = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col];
             if (info.ref_frame[1] > AV1R_INTRA_FRAME && blk.compound_type != AV1R_COMPOUND_AVERAGE &&
                 blk.compound_type != AV1R_COMPOUND_DISTANCE)
-                return false;
+                return 0;
             if (blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV)
                 for (int r = 0; r < 2; r++)
                     if (info.ref_frame[r] > AV1R_INTRA_FRAME && h->gm_type[info.ref_frame[r] & 7] > AV1R_GM_TRANSLATION)
-                        return false;
-            return true;
+                        return 0;
+            return av1r_num4x4w[bs] <= 2 && av1r_num4x4h[bs] <= 2 ? 2 : 1;
         };
-        std::stable_partition(P.begin(), P.end(), [&](uint32_t code) { return !smallTile(code); });
-        c->levels[l].sm0 = (uint32_t)std::count_if(P.begin(), P.end(), smallTile);
+        std::stable_sort(P.begin(), P.end(), [&](uint32_t a, uint32_t b2) { return plainClass(a) < plainClass(b2); });
+        for (int pc = 0; pc < 2; pc++)
+            c->levels[l].pl[pc] = (uint32_t)std::count_if(P.begin(), P.end(), [&](uint32_t code) { return plainClass(code) == pc + 1; });
         std::vector<uint32_t>& T = c->lvT[l];
         // [large intra][large inter][small intra][small inter]
         std::stable_sort(T.begin(), T.end(), [&](uint32_t a, uint32_t b2) {
@@ -847,9 +850,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         anyLr |= h->uses_lr != 0;
     }
     // launch metadata: [KParams x n][per level: k_inter table (n + 1 prefix counts, n item
-    // offsets), k_inter_s table (n + 1 group prefix, n offsets, n counts), k_tb table (large
-    // prefix, small prefix, large offsets, small offsets)]
-    const size_t tabI = 2 * (size_t)n + 1, tabS = 3 * (size_t)n + 1, tabT = 4 * (size_t)n + 2, tabW = tabI + tabS + tabT;
+    // offsets), k_inter_m and k_inter_s tables (n + 1 group prefix, n offsets, n counts),
+    // k_tb table (large prefix, small prefix, large offsets, small offsets)]
+    const size_t tabI = 2 * (size_t)n + 1, tabS = 3 * (size_t)n + 1, tabT = 4 * (size_t)n + 2, tabW = tabI + 2 * tabS + tabT;
     const size_t kBytes = align256(sizeof(KParams) * n);
     const size_t tabBytes = align256(4 * tabW * std::max<size_t>(nLevels, 1));
     // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
@@ -893,33 +896,40 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         for (const Level& lv : jobs[i].P->levels) frameRows += lv.cnt[0] + lv.cnt[1] + lv.cnt[2];
     }
     uint32_t* tab = reinterpret_cast<uint32_t*>(M.host + kBytes);
-    // total[l * 4 + kind]: workgroups of the level's k_inter / k_inter_s launches, items of
-    // its large / small TB lists; totalS: its small inter tiles
-    std::vector<uint32_t> total(nLevels * 4, 0), totalS(nLevels, 0);
+    // total[l * 5 + kind]: workgroups of the level's k_inter / k_inter_m / k_inter_s
+    // launches, items of its large / small TB lists; totalP: its plain inter tiles
+    std::vector<uint32_t> total(nLevels * 5, 0), totalP(nLevels, 0);
     for (size_t l = 0; l < nLevels; l++) {
         uint32_t* ti = tab + l * tabW;       // k_inter
-        uint32_t* ts = ti + tabI;            // k_inter_s
+        uint32_t* tm = ti + tabI;            // k_inter_m
+        uint32_t* ts = tm + tabS;            // k_inter_s
         uint32_t* tt = ts + tabS;            // k_tb
-        ti[0] = ts[0] = tt[0] = tt[n + 1] = 0;
+        ti[0] = tm[0] = ts[0] = tt[0] = tt[n + 1] = 0;
         for (int i = 0; i < n; i++) {
             const auto& lv = jobs[i].P->levels;
             const bool has = l < lv.size();
-            const uint32_t sm = has && !jobs[i].scaled ? lv[l].sm0 : 0;
-            ti[i + 1] = ti[i] + (has ? lv[l].cnt[0] - sm : 0);
+            const bool plain = has && !jobs[i].scaled;
+            const uint32_t md = plain ? lv[l].pl[0] : 0, sm = plain ? lv[l].pl[1] : 0;
+            const uint32_t rest = has ? lv[l].cnt[0] - md - sm : 0;
+            ti[i + 1] = ti[i] + rest;
             ti[n + 1 + i] = has ? lv[l].off[0] : 0;
+            tm[i + 1] = tm[i] + (md + 1) / 2;
+            tm[n + 1 + i] = has ? lv[l].off[0] + rest : 0;
+            tm[2 * n + 1 + i] = md;
             ts[i + 1] = ts[i] + (sm + 3) / 4;
-            ts[n + 1 + i] = has ? lv[l].off[0] + lv[l].cnt[0] - sm : 0;
+            ts[n + 1 + i] = has ? lv[l].off[0] + rest + md : 0;
             ts[2 * n + 1 + i] = sm;
-            totalS[l] += sm;
+            totalP[l] += md + sm;
             tt[i + 1] = tt[i] + (has ? lv[l].cnt[1] : 0);
             tt[n + 2 + i] = tt[n + 1 + i] + (has ? lv[l].cnt[2] : 0);
             tt[2 * n + 2 + i] = has ? lv[l].off[1] : 0;
             tt[3 * n + 2 + i] = has ? lv[l].off[2] : 0;
         }
-        total[l * 4 + 0] = ti[n];
-        total[l * 4 + 1] = ts[n];
-        total[l * 4 + 2] = tt[n];
-        total[l * 4 + 3] = tt[2 * n + 1];
+        total[l * 5 + 0] = ti[n];
+        total[l * 5 + 1] = tm[n];
+        total[l * 5 + 2] = ts[n];
+        total[l * 5 + 3] = tt[n];
+        total[l * 5 + 4] = tt[2 * n + 1];
     }
     uint32_t* ctl = reinterpret_cast<uint32_t*>(M.dev + kBytes + tabBytes);
     if (flow) {
@@ -1006,6 +1016,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
         if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
         if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, st);
+        if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
@@ -1032,11 +1043,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         HIPCHK(hipEventRecord(lc->ev[6], st));
     }
     for (size_t l = 0; l < nLevels && !flow; l++) {
-        const uint32_t nInter = total[l * 4], nInterS = total[l * 4 + 1], nLarge = total[l * 4 + 2], nSmall = total[l * 4 + 3];
-        if (nInter) launch_k_level(0, dk, dtab + l * tabW, n, nInter, trace, traceBase, st);
-        if (nInterS) launch_k_level(2, dk, dtab + l * tabW + tabI, n, nInterS, trace, traceBase, st);
-        traceBase += nInter + totalS[l];  // (k_inter_s writes no timeline rows)
-        if (nLarge + nSmall) launch_k_level(1, dk, dtab + l * tabW + tabI + tabS, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
+        const uint32_t* lt = dtab + l * tabW;
+        const uint32_t nInter = total[l * 5], nLarge = total[l * 5 + 3], nSmall = total[l * 5 + 4];
+        if (nInter) launch_k_level(0, dk, lt, n, nInter, trace, traceBase, st);
+        if (total[l * 5 + 1]) launch_k_level(2, dk, lt + tabI, n, total[l * 5 + 1], trace, traceBase, st);
+        if (total[l * 5 + 2]) launch_k_level(3, dk, lt + tabI + tabS, n, total[l * 5 + 2], trace, traceBase, st);
+        traceBase += nInter + totalP[l];  // (k_inter_m / k_inter_s write no timeline rows)
+        if (nLarge + nSmall) launch_k_level(1, dk, lt + tabI + 2 * tabS, n, nLarge + (nSmall + 3) / 4, trace, traceBase, st);
         traceBase += nLarge + nSmall;
     }
     if (trace) {
@@ -1055,7 +1068,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         } else {
             size_t q = 0;
             for (size_t l = 0; l < nLevels; l++)
-                for (uint32_t i = 0; i < total[l * 4] + totalS[l] + total[l * 4 + 2] + total[l * 4 + 3]; i++, q++)
+                for (uint32_t i = 0; i < total[l * 5] + totalP[l] + total[l * 5 + 3] + total[l * 5 + 4]; i++, q++)
                     hv[q * 16 + 6] = l;
         }
         fwrite(hv.data(), 8, hv.size(), lc->traceFile);

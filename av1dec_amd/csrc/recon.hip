@@ -1398,26 +1398,29 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint
 }
 
 // ---------------------------------------------------------------------------------
-// k_inter_s: small plain inter blocks, four per wave.
+// k_inter_s / k_inter_m: small / medium plain inter blocks, four / two per wave.
 //
 // Blocks with both luma sides <= 8 are most of an inter frame's tiles, and k_inter gives
 // each a whole wave (and its 128-VGPR register budget for every prediction mode) while
 // its 8x8 luma needs 16 lanes.  The plain ones (simple motion, single reference or
 // average / distance compound, unwarped, unscaled: classified by the host, build_schedule)
-// go here instead: 16 lanes per block, the unit's state per lane, ~1 KB of LDS each, the
-// samples stored straight to the frame -- many more blocks in flight per CU.
+// go to k_inter_s instead: 16 lanes per block, the unit's state per lane, ~1 KB of LDS
+// each, the samples stored straight to the frame -- many more blocks in flight per CU.
+// Plain blocks with both sides <= 16 go to k_inter_m the same way, 32 lanes each.
 // ---------------------------------------------------------------------------------
+template <int MS>
 struct SmallLds {
-    uint8_t win[2][15 * 16];  // reference windows: <= 8 + 7 rows, stride 16
-    int16_t hb[2][15 * 8];    // their horizontally filtered rows
+    uint8_t win[2][(MS + 7) * (MS + 8)];  // reference windows: <= MS + 7 rows, stride MS + 8
+    int16_t hb[2][(MS + 7) * MS];         // their horizontally filtered rows
 };
 
 // One prediction unit (predict_inter, InterPredict.cpp:962-1049; blockInterPrediction's
 // sub-pel filter, :319-383; the average / distance blend of :1022-1049) of w x h <= 8 x 8
-// at plane position (x, y).
-DEV void small_pu(const KParams& k, SmallLds& L, int ct, int plane, int x, int y, int w, int h, int candRow, int candCol)
+// at plane position (x, y), by NT lanes.
+template <int NT, int MS>
+DEV void small_pu(const KParams& k, SmallLds<MS>& L, int ct, int plane, int x, int y, int w, int h, int candRow, int candCol)
 {
-    const int t = threadIdx.x & 15;
+    const int t = threadIdx.x & (NT - 1);
     const av1r_mi& info = mi_at(k, candRow, candCol);
     const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
     int16_t hf[2][8], vf[2][8];
@@ -1435,13 +1438,13 @@ DEV void small_pu(const KParams& k, SmallLds& L, int ct, int plane, int x, int y
             hf[l][u] = av1r_subpel_filters[(fx * 16 + hph) * 8 + u];
             vf[l][u] = av1r_subpel_filters[(fy * 16 + vph) * 8 + u];
         }
-        load_window<16>(R, L.win[l], 0, 0, w, h, 16);
+        load_window<NT>(R, L.win[l], 0, 0, w, h, MS + 8);
     }
-    coop_sync<16>();
+    coop_sync<NT>();
 #pragma unroll
     for (int l = 0; l < 2; l++)
-        if (l <= isCompound && !integer[l]) hpass<16>(L.win[l], L.hb[l], w, h, hf[l], 3, 16, 8);
-    coop_sync<16>();
+        if (l <= isCompound && !integer[l]) hpass<NT>(L.win[l], L.hb[l], w, h, hf[l], 3, MS + 8, MS);
+    coop_sync<NT>();
     const int R1 = isCompound ? 7 : 11, PostRound = 14 - (3 + R1);
     int fwd = 0, bck = 0;
     const int dist = isCompound && ct == AV1R_COMPOUND_DISTANCE;
@@ -1454,58 +1457,63 @@ DEV void small_pu(const KParams& k, SmallLds& L, int ct, int plane, int x, int y
     const DevPlane& dst = k.cur.pl[plane];
     if (!(w & 3)) {
         const int g4 = w >> 2;
-        for (int q = t; q < h * g4; q += 16) {
+        for (int q = t; q < h * g4; q += NT) {
             const int rr = q / g4, cc = (q - rr * g4) * 4;
             int p0[4], p1[4] = {0, 0, 0, 0};
-            pred_win4(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], p0, 16, 8);
-            if (isCompound) pred_win4(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], p1, 16, 8);
+            pred_win4(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], p0, MS + 8, MS);
+            if (isCompound) pred_win4(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], p1, MS + 8, MS);
             uint32_t v = 0;
 #pragma unroll
             for (int m = 0; m < 4; m++) v |= (uint32_t)blend(p0[m], p1[m]) << (8 * m);
             *reinterpret_cast<uint32_t*>(&px(dst, x + cc, y + rr)) = v;  // x, cc: multiples of 4
         }
     } else {
-        for (int q = t; q < h * w; q += 16) {
+        for (int q = t; q < h * w; q += NT) {
             const int rr = q / w, cc = q - rr * w;
-            const int p0 = pred_win(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], 16, 8);
-            const int p1 = isCompound ? pred_win(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], 16, 8) : 0;
+            const int p0 = pred_win(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], MS + 8, MS);
+            const int p1 = isCompound ? pred_win(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], MS + 8, MS) : 0;
             px(dst, x + cc, y + rr) = (uint8_t)blend(p0, p1);
         }
     }
-    coop_sync<16>();  // the next unit reuses the windows
+    coop_sync<NT>();  // the next unit reuses the windows
 }
 
-// Frames' lists are dealt in groups of four (a frame's last group may be partial), so the
-// parameters of a workgroup stay uniform.  tab: [group prefix (n + 1)][offsets (n)][counts (n)].
-#ifdef AV1R_KIS_WAVES
-#define K_INTER_S_BOUNDS __launch_bounds__(64, AV1R_KIS_WAVES)
-#else
-#define K_INTER_S_BOUNDS __launch_bounds__(64)
-#endif
-extern "C" __global__ K_INTER_S_BOUNDS void k_inter_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+// Frames' lists are dealt in groups of 64 / NT (a frame's last group may be partial), so
+// the parameters of a workgroup stay uniform.  tab: [group prefix (n + 1)][offsets (n)][counts (n)].
+template <int NT, int MS>
+DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, SmallLds<MS>* L)
 {
-    __shared__ SmallLds L[4];
     const int lane = threadIdx.x & 63;
     const uint32_t b = blockIdx.x;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     const KParams& k = KP(kps, s);
-    const int g = threadIdx.x >> 4;
-    const uint32_t i = 4 * (b - tab[s]) + g;
+    const int g = threadIdx.x / NT;
+    const uint32_t i = (64 / NT) * (b - tab[s]) + g;
     if (i >= tab[2 * n + 1 + s]) return;  // (wave-level ordering only: no barrier follows)
     const av1r_block& blk = k.blocks[AV1R_ITEM_INDEX(k.items[tab[n + 1 + s] + i].code) >> 4];
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
     for (int plane = 0; plane < nPl; plane++) {
         // (sub-8x8 chroma may gather up to four units of neighbouring blocks)
-        const PlaneGeo G = plane_geo<8>(k, blk, plane, 0, 0);
+        const PlaneGeo G = plane_geo<MS>(k, blk, plane, 0, 0);
         int r = 0;
         for (int yy = 0; yy < G.ph; yy += G.predH, r++) {
             int c = 0;
             for (int xx = 0; xx < G.pw; xx += G.predW, c++)
-                small_pu(k, L[g], blk.compound_type, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
-                    G.candCol + c);
+                small_pu<NT, MS>(k, L[g], blk.compound_type, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH,
+                    G.candRow + r, G.candCol + c);
         }
     }
+}
+extern "C" __global__ __launch_bounds__(64) void k_inter_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ SmallLds<8> L[4];
+    inter_plain<16, 8>(kps, tab, n, L);
+}
+extern "C" __global__ __launch_bounds__(64) void k_inter_m(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ SmallLds<16> L[2];
+    inter_plain<32, 16>(kps, tab, n, L);
 }
 
 #endif  // !AV1R_FLOW_PART
@@ -1752,12 +1760,13 @@ void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, u
 }
 
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4);
-// kind 2: small inter tiles, `items` groups of four
+// kind 2 / 3: medium / small plain inter blocks, `items` groups of two / four
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
 {
     if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, kps, tab, n, trace, traceBase);
-    else if (kind == 2) hipLaunchKernelGGL(k_inter_s, dim3(items), dim3(64), 0, s, kps, tab, n);
+    else if (kind == 2) hipLaunchKernelGGL(k_inter_m, dim3(items), dim3(64), 0, s, kps, tab, n);
+    else if (kind == 3) hipLaunchKernelGGL(k_inter_s, dim3(items), dim3(64), 0, s, kps, tab, n);
     else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, kps, tab, n, trace, traceBase);
 }
 #endif  // !AV1R_FLOW_PART

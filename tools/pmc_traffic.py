@@ -13,7 +13,7 @@ import os
 import sys
 from collections import defaultdict
 
-STAGES = {"k_inter": "recon", "k_tb": "recon", "k_resid_s": "recon", "k_resid_l": "recon", "k_flow": "recon",
+STAGES = {"k_inter": "recon", "k_inter_m": "recon", "k_inter_s": "recon", "k_tb": "recon", "k_resid_s": "recon", "k_resid_l": "recon", "k_flow": "recon",
           "k_lf": "lf", "k_cdef": "cdef", "k_lr": "lr"}
 
 
