@@ -565,17 +565,10 @@ __constant__ SgrTabs g_sgr = make_sgr_tabs();
 // a, b of the self-guided box at staged position (si, sj) = source (row, col) index of the
 // box centre (LoopRestoration.cpp:284-380, restated per position; 32-bit arithmetic as
 // the reference's)
-DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, int& A, int& B)
+DEV void sgr_ab_fin(int a, int b, int r, int set, int pass, int& A, int& B)
 {
     const int n = r == 2 ? 25 : 9;  // (2r + 1)^2 (r is 1 or 2)
     const uint32_t s = g_sgr.s[set][pass];
-    int a = 0, b = 0;
-    for (int dy = -r; dy <= r; dy++)
-        for (int dx = -r; dx <= r; dx++) {
-            int cv = L.src[si + dy][sj + dx];
-            a += cv * cv;
-            b += cv;
-        }
     int p = imax(0, a * n - b * b);
     int z = (int)((uint32_t)p * s + (1u << 19)) >> 20;
     int a2;
@@ -585,6 +578,17 @@ DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, in
     int b2 = ((1 << 8) - a2) * b * oneOverN;
     A = a2;
     B = r2(b2, 12);
+}
+DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, int& A, int& B)
+{
+    int a = 0, b = 0;
+    for (int dy = -r; dy <= r; dy++)
+        for (int dx = -r; dx <= r; dx++) {
+            int cv = L.src[si + dy][sj + dx];
+            a += cv * cv;
+            b += cv;
+        }
+    sgr_ab_fin(a, b, r, set, pass, A, B);
 }
 
 // one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
@@ -686,20 +690,50 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
         }
     }
     if (anyS) {
-        // a, b of both passes at rows ty0-1 .. ty1, cols x0-1 .. x0+tw
-        for (int q = t; q < 2 * (th + 2) * (tw + 2); q += 256) {
-            const int pass = q >= (th + 2) * (tw + 2);
-            const int e = q - pass * (th + 2) * (tw + 2);
-            const int ii = e / (tw + 2), cc = e - ii * (tw + 2);
+        // a, b of both passes (box radius 2 / 1: Sgr_Params) at rows ty0-1 .. ty1 (ii), cols
+        // x0-1 .. x0+tw (cc).  The box sums are separable: each lane walks one column over a
+        // run of rows, keeping the last five rows' horizontal 5- and 3-sums in registers.
+        constexpr int RUNS = 3;
+        const int nr = th + 2, nc = tw + 2, runH = (nr + RUNS - 1) / RUNS;
+        for (int q = t; q < RUNS * nc; q += 256) {
+            const int cc = q % nc, i0 = (q / nc) * runH, i1 = imin(nr, i0 + runH);
             const av1r_lr_unit& u = L.unit[unitOf(cc - 1)];
-            if (u.type != AV1R_RESTORE_SGRPROJ) continue;
-            const int r = av1r_sgr_params[u.sgr_set][pass * 2];
-            if (!r) continue;
-            if (pass == 0 && !((ty0 - 1 + ii - y0) & 1)) continue;  // pass 0 uses odd rows only
-            int A, B;
-            sgr_ab_lds(L, ii + 2, cc + 3, r, u.sgr_set, pass, A, B);
-            L.A[pass][ii][cc] = (int16_t)A;
-            L.B[pass][ii][cc] = B;
+            if (u.type != AV1R_RESTORE_SGRPROJ || i0 >= i1) continue;
+            const int set = u.sgr_set;
+            const bool p0 = av1r_sgr_params[set][0] != 0, p1 = av1r_sgr_params[set][2] != 0;
+            // h5[k] / h3[k]: (squares, sums) of source row sr - k, columns cc+1..cc+5 / cc+2..cc+4
+            int a5[5] = {}, b5[5] = {}, a3[4] = {}, b3[4] = {};
+            for (int sr = i0; sr < i1 + 4; sr++) {
+#pragma unroll
+                for (int k = 4; k > 0; k--) {
+                    a5[k] = a5[k - 1];
+                    b5[k] = b5[k - 1];
+                }
+#pragma unroll
+                for (int k = 3; k > 0; k--) {
+                    a3[k] = a3[k - 1];
+                    b3[k] = b3[k - 1];
+                }
+                const uint8_t* row = &L.src[sr][cc + 1];
+                const int v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4];
+                b3[0] = v1 + v2 + v3;
+                a3[0] = v1 * v1 + v2 * v2 + v3 * v3;
+                b5[0] = b3[0] + v0 + v4;
+                a5[0] = a3[0] + v0 * v0 + v4 * v4;
+                const int ii = sr - 4;  // the box centre's row: source row ii + 2
+                if (ii < i0) continue;
+                int A, B;
+                if (p0 && ((ty0 - 1 + ii - y0) & 1)) {  // pass 0 uses odd rows only
+                    sgr_ab_fin(a5[0] + a5[1] + a5[2] + a5[3] + a5[4], b5[0] + b5[1] + b5[2] + b5[3] + b5[4], 2, set, 0, A, B);
+                    L.A[0][ii][cc] = (int16_t)A;
+                    L.B[0][ii][cc] = B;
+                }
+                if (p1) {  // rows ii + 1 .. ii + 3
+                    sgr_ab_fin(a3[1] + a3[2] + a3[3], b3[1] + b3[2] + b3[3], 1, set, 1, A, B);
+                    L.A[1][ii][cc] = (int16_t)A;
+                    L.B[1][ii][cc] = B;
+                }
+            }
         }
     }
     __syncthreads();
