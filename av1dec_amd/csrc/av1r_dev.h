@@ -62,6 +62,15 @@ struct KParams {
     int16_t* res;
     const uint32_t* resid_s;  // TBs with coefficients and sides <= 16 (16 per workgroup, ~0u pads)
     const uint32_t* resid_l;  // the larger ones
+    // k_flow edge granules (cdna_hip_programming.md §6 Guideline 16 R2: the data is the
+    // flag).  Per plane and 4x4 unit, the unit's bottom row (gran_h[row * gw + col]) and
+    // right column (gran_v[col * gh + row], top to bottom) as {4 pixels, epoch << 32},
+    // stored by the k_flow item that writes the unit.  gran = 0: edges through dependency
+    // flags instead (every edge owner in the item's list)
+    uint64_t* gran_h[3];
+    uint64_t* gran_v[3];
+    int gran_w[3], gran_hn[3];
+    int gran;
     uint32_t n_items;
     uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;

@@ -132,6 +132,15 @@ struct av1r_ctx {
     std::vector<int32_t> nodeDeps, nodeOfTb, nodeOfBlk, nodePos;
     std::vector<uint32_t> deps;
     bool flowOk = false;
+    // k_flow edge granules (KParams::gran_h / gran_v): per 4x4 unit whether it is on the
+    // bottom row / right column of its owner (the units whose granules the owner stores);
+    // per node 12 mask words (4 per plane: the above and left runs' units written by an
+    // item of the launch); granOk = every such unit a consumer reads has its granule
+    std::vector<uint8_t> emit[3];
+    std::vector<uint32_t> nodeMask;
+    bool granOk = false;
+    uint64_t* granDev = nullptr;
+    size_t granCap = 0;  // bytes
     // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
     // the small and large TB lists, the tiles' total size
     std::vector<uint32_t> tbRes, residS, residL;
@@ -343,7 +352,7 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
 // ------------------------------------------------------------------------------------
 // dependency levels
 // ------------------------------------------------------------------------------------
-static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
+static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true)
 {
     const av1r_frame_hdr* h = b->hdr;
     for (int p = 0; p < 3; p++) {
@@ -352,7 +361,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         c->mapH[p] = (((h->mi_rows_alloc * 4) >> sub) + 64) / 4;
         c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
         c->owner[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
+        c->emit[p].assign((size_t)c->mapW[p] * c->mapH[p], 0);
     }
+    static const bool granEnv = !getenv("AV1R_GRAN") || atoi(getenv("AV1R_GRAN")) != 0;
+    c->granOk = granEnv && allowGran;
+    c->nodeMask.clear();
+    uint32_t nm[12] = {};  // mask words of the node being built
     c->nodeDepStart.assign(1, 0);
     c->nodeDeps.clear();
     c->nodeOfTb.assign(b->n_tbs, -1);
@@ -370,15 +384,56 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
                 if (row[x] >= 0 && row[x] != last) dl.push_back(last = row[x]);
         }
     };
-    auto edge_owners = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL) {
-        if (hA) owners(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2);
-        if (hL) owners(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2);
+    // the owners of the pixels an intra prediction reads (coop_intra_edges): with granules,
+    // mask words nm[4 * slot ..] instead of dependencies (coop_intra_edges_gran's runs)
+    auto edge_owners = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int slot) {
+        if (!c->granOk) {
+            if (hA) owners(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2);
+            if (hL) owners(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2);
+            return;
+        }
+        uint32_t* m = nm + 4 * slot;
+        auto run = [&](int u0, int u1, bool horiz, uint32_t* mw) {  // units u0..u1 of row / column
+            if (u1 - u0 >= 32) c->granOk = false;
+            for (int u = u0; u <= u1 && u - u0 < 32; u++) {
+                const int ux = horiz ? u : (x - 1) >> 2, uy = horiz ? (y - 1) >> 2 : u;
+                if (ux < 0 || uy < 0 || ux >= c->mapW[p] || uy >= c->mapH[p]) continue;
+                const size_t i = (size_t)uy * c->mapW[p] + ux;
+                if (c->owner[p][i] < 0) continue;
+                *mw |= 1u << (u - u0);
+                if (!(c->emit[p][i] & (horiz ? 1 : 2))) {
+                    if (c->granOk && getenv("AV1R_GRAN_DEBUG"))
+                        fprintf(stderr, "no granule: plane %d unit %d,%d %s (consumer %d,%d %dx%d)\n", p, ux, uy, horiz ? "h" : "v", x, y, w, h);
+                    c->granOk = false;
+                }
+            }
+        };
+        // above run: row (y-1)/4 from x/4; left run: column (x-1)/4 from y/4; the corner
+        // pixel (x-1, y-1) separately (m[1]: bit 0 written in the launch, bit 1 its
+        // granule is its owner's right column instead of its bottom row)
+        if (hA) run(x >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, true, m);
+        if (hL) run(y >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2, false, m + 2);
+        if (hA && hL) {
+            const size_t i = (size_t)((y - 1) >> 2) * c->mapW[p] + ((x - 1) >> 2);
+            if (c->owner[p][i] >= 0) {
+                m[1] = (c->emit[p][i] & 1) ? 1u : 3u;
+                if (!c->emit[p][i]) c->granOk = false;
+            }
+        }
     };
     auto own_set = [&](int p, int x0, int y0, int w4, int h4, int32_t node) {
+        if (x0 + w4 > c->mapW[p] || y0 + h4 > c->mapH[p]) {  // its granules would not fit
+            if (c->granOk && getenv("AV1R_GRAN_DEBUG")) fprintf(stderr, "outside: plane %d %d,%d %dx%d\n", p, x0, y0, w4, h4);
+            c->granOk = false;
+        }
         int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
         for (int y = y0; y < y1; y++) {
             int32_t* row = &c->owner[p][(size_t)y * c->mapW[p]];
-            for (int x = x0; x < x1; x++) row[x] = node;
+            uint8_t* em = &c->emit[p][(size_t)y * c->mapW[p]];
+            for (int x = x0; x < x1; x++) {
+                row[x] = node;
+                em[x] = (y == y0 + h4 - 1 ? 1 : 0) | (x == x0 + w4 - 1 ? 2 : 0);
+            }
         }
     };
     auto end_node = [&]() {  // closes the node's dependency list; returns its id
@@ -386,6 +441,8 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
         dl.erase(std::unique(dl.begin(), dl.end()), dl.end());
         c->nodeDeps.insert(c->nodeDeps.end(), dl.begin(), dl.end());
         dl.clear();
+        c->nodeMask.insert(c->nodeMask.end(), nm, nm + 12);
+        memset(nm, 0, sizeof(nm));
         c->nodeDepStart.push_back((uint32_t)c->nodeDeps.size());
         return (int32_t)c->nodeDepStart.size() - 2;
     };
@@ -451,7 +508,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
                     const int ew = av1r_num4x4w[psz] * 4, eh = av1r_num4x4h[psz] * 4;
                     const bool hAR = (blk.ii_edge >> (2 * p)) & 1, hBL = (blk.ii_edge >> (2 * p + 1)) & 1;
                     dep = std::max(dep, edge_level(p, ex, ey, ew, eh, hL, hA, hAR, hBL));
-                    edge_owners(p, ex, ey, ew, eh, hL, hA, hAR, hBL);
+                    edge_owners(p, ex, ey, ew, eh, hL, hA, hAR, hBL, p);
                 }
                 blkLevel = dep + 1;
                 push(c->lvB, blkLevel, AV1R_ITEM(AV1R_ITEM_II, bi));
@@ -483,7 +540,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
                     const bool hL = t.flags & AV1R_TB_HAVE_LEFT, hA = t.flags & AV1R_TB_HAVE_ABOVE;
                     const bool hAR = t.flags & AV1R_TB_HAVE_AR, hBL = t.flags & AV1R_TB_HAVE_BL;
                     dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
-                    edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
+                    edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0);
                     if (p && blk.uv_mode == AV1R_UV_CFL_PRED) {  // the co-located luma (incl. sub-8x8 neighbours)
                         const int lx0 = t.x >> 1, ly0 = t.y >> 1, lx1 = (2 * (t.x + w) - 1) >> 2, ly1 = (2 * (t.y + hh) - 1) >> 2;
                         dep = std::max({dep, lumaMax, region_max(0, lx0, ly0, lx1, ly1)});
@@ -504,6 +561,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             // block is inter-intra, whose blend item adds the residuals
             if (!inter) own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, node);
         }
+    }
+    static const bool granDbg = getenv("AV1R_GRAN_DEBUG") != nullptr;
+    if (granDbg) fprintf(stderr, "av1r: granules %s (frame %dx%d)\n", c->granOk ? "on" : "off", h->frame_width, h->frame_height);
+    if (c->granOk != (granEnv && allowGran)) {  // a unit without its granule: dependency flags throughout
+        build_schedule(c, b, false);
+        return;
     }
     const size_t nl = (size_t)(globalMax + 1);
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
@@ -639,6 +702,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b)
             c->flowOk = false;
             break;
         }
+        if (c->granOk) {  // the mask words precede the list: 12 for a blend, 4 for a TB
+            const uint32_t* m = &c->nodeMask[(size_t)node * 12];
+            c->deps.insert(c->deps.end(), m, m + (AV1R_ITEM_KIND(code) == AV1R_ITEM_II ? 12 : 4));
+        }
         w.dep_off = (uint32_t)c->deps.size();
         w.dep_cnt = (uint16_t)(d1 - d0);
         for (uint32_t d = d0; d < d1; d++) {
@@ -698,6 +765,11 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.resid_s = (const uint32_t*)put(c->residS.data(), 4 * c->residS.size(), szResS);
     k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
     P.flowOk = c->flowOk;
+    k.gran = c->flowOk && c->granOk;
+    for (int p = 0; p < 3; p++) {
+        k.gran_w[p] = c->mapW[p];
+        k.gran_hn[p] = c->mapH[p];
+    }
     P.nResidS = (uint32_t)(c->residS.size() / 16);
     P.nResidL = (uint32_t)c->residL.size();
     P.resElems = c->resElems;
@@ -767,6 +839,31 @@ static int job_begin(FrameJob& j)
         HIPCHK(hipMalloc(&c->resDev, 2 * c->resCap));
     }
     j.k.res = c->resDev;
+    if (j.k.gran) {
+        size_t need = 0;
+        for (int p = 0; p < 3; p++) need += 2 * 8 * (size_t)j.k.gran_w[p] * j.k.gran_hn[p];
+        if (need > c->granCap) {
+            if (c->granDev) {
+                ctx_join(c);
+                HIPCHK(hipStreamSynchronize(c->stream));
+                (void)hipFree(c->granDev);
+                c->granDev = nullptr;
+            }
+            // zeroed (no launch's epoch: epochs start at 1) before any launch can use it:
+            // the context's streams are non-blocking, so not behind a null-stream memset
+            HIPCHK(hipMalloc(&c->granDev, need));
+            HIPCHK(hipMemsetAsync(c->granDev, 0, need, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            c->granCap = need;
+        }
+        uint64_t* g = c->granDev;
+        for (int p = 0; p < 3; p++) {
+            const size_t n = (size_t)j.k.gran_w[p] * j.k.gran_hn[p];
+            j.k.gran_h[p] = g;
+            j.k.gran_v[p] = g + n;
+            g += 2 * n;
+        }
+    }
     j.k.cdef = j.C->d;
     if (j.L) j.k.lrout = j.L->d;
     return AV1R_OK;
@@ -1215,6 +1312,7 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipStreamSynchronize(c->copyStream);
     (void)hipStreamDestroy(c->copyStream);
     if (c->resDev) (void)hipFree(c->resDev);
+    if (c->granDev) (void)hipFree(c->granDev);
     (void)hipEventDestroy(c->sync);
     (void)hipEventDestroy(c->joinEv);
     if (c->traceDev) (void)hipFree(c->traceDev);

@@ -173,6 +173,145 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
     }
 }
 
+// k_flow's edge gather through granules (KParams::gran_h / gran_v).  The above run is the
+// units of row (y-1)/4 from x/4 to aboveLimit/4, the left run the units of column (x-1)/4
+// from y/4 to leftLimit/4, plus the corner pixel (x-1, y-1): exactly the pixels
+// coop_intra_edges reads.  mask[0] (above) and mask[2] (left) flag, bit u = unit u of the
+// run, the units written by an item of this launch; mask[1] bit 0 the corner's, bit 1 its
+// granule (byte 3) is its owner's right column instead of its bottom row.  One lane per
+// such unit re-reads its granule (sc1) until the tag is the launch's epoch, so the pixels
+// arrive with the signal (no dependency flag, no second round trip).  The other units
+// were final before the launch and are read from the frame.  The runs are staged in
+// L.tmp / L.tmp2, then AboveRow / LeftCol are assembled as in coop_intra_edges.  Bounded:
+// a spin gives up after ~1 s (or once another wave has) and sets the launch's error word.
+struct GranEdges {
+    const uint32_t* mask;  // 4 words: above, corner, left, (unused)
+    const uint64_t* h;     // this plane's gran_h / gran_v, gw units per row / gh per column
+    const uint64_t* v;
+    int gw, gh;
+    uint32_t epoch;
+    uint32_t* ctl;         // k_flow control block (FLOW_ERR)
+};
+template <int NT>
+DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
+    int log2H, bool hL, bool hA, bool hAR, bool hBL, IntraLds& L, const GranEdges& G)
+{
+    const int t = coop_lane<NT>();
+    const int w = 1 << log2W, h = 1 << log2H;
+    const int sub = plane ? 1 : 0;
+    const int maxX = ((miCols * 4) >> sub) - 1;
+    const int maxY = ((miRows * 4) >> sub) - 1;
+    const int aboveLimit = imin(maxX, x + (hAR ? 2 * w : w) - 1);
+    const int leftLimit = imin(maxY, y + (hBL ? 2 * h : h) - 1);
+    const int na = hA ? (aboveLimit >> 2) - (x >> 2) + 1 : 0;
+    const int nl = hL ? (leftLimit >> 2) - (y >> 2) + 1 : 0;
+    const int nq = na + nl + (hA && hL ? 1 : 0);
+    uint32_t* stA = reinterpret_cast<uint32_t*>(L.tmp);
+    uint32_t* stL = reinterpret_cast<uint32_t*>(L.tmp2);  // [39]: the corner's unit
+    if ((NT == 64 || t < 64) && nq > 0) {
+        const int lane = t & 63;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool dead = false;
+        for (int base = 0; base < nq; base += 64) {
+            const int q = base + lane;
+            const bool act = q < nq;
+            const int kind = q < na ? 0 : q < na + nl ? 1 : 2;  // above, left, corner
+            const int u = kind == 0 ? q : q - na;
+            const uint32_t cm = G.mask[1];
+            const bool inl = act && (kind == 0 ? ((G.mask[0] >> (u & 31)) & 1)
+                                   : kind == 1 ? ((G.mask[2] >> (u & 31)) & 1) : (cm & 1));
+            const uint64_t* g = kind == 0 ? G.h + (size_t)((y - 1) >> 2) * G.gw + (x >> 2) + u
+                              : kind == 1 ? G.v + (size_t)((x - 1) >> 2) * G.gh + (y >> 2) + u
+                              : (cm & 2) ? G.v + (size_t)((x - 1) >> 2) * G.gh + ((y - 1) >> 2)
+                                         : G.h + (size_t)((y - 1) >> 2) * G.gw + ((x - 1) >> 2);
+            uint32_t val = 0;
+            if (act && !inl) {  // final before this launch
+                if (kind == 0) {
+                    val = ldp4<true>(src, x + 4 * u, y - 1);
+                } else if (kind == 1) {
+                    const int py = y + 4 * u;
+                    val = ldp<true>(src, x - 1, py) | (ldp<true>(src, x - 1, py + 1) << 8) |
+                          (ldp<true>(src, x - 1, py + 2) << 16) | ((uint32_t)ldp<true>(src, x - 1, py + 3) << 24);
+                } else {
+                    val = (uint32_t)ldp<true>(src, x - 1, y - 1) << 24;
+                }
+            }
+            for (;;) {
+                bool ok = true;
+                if (inl && !dead) {
+                    const uint64_t gv = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = (uint32_t)(gv >> 32) == G.epoch;
+                    val = (uint32_t)gv;
+                }
+                if (__all(ok)) break;
+                if (__hip_atomic_load(G.ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                    if (lane == 0) {
+                        __hip_atomic_store(G.ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(G.ctl + FLOW_HOSTERR)),
+                            1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    dead = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (act) (kind == 0 ? stA + u : kind == 1 ? stL + u : stL + 39)[0] = val;
+        }
+    }
+    coop_sync<NT>();
+    const uint8_t* sa = L.tmp - x;   // pixel (px, y - 1) at sa[px]
+    const uint8_t* sl = L.tmp2 - y;  // pixel (x - 1, py) at sl[py]
+    uint8_t* above = L.above + EDGE_OFF;
+    uint8_t* left = L.left + EDGE_OFF;
+    for (int i = t; i < w + h; i += NT) {
+        uint8_t a, l;
+        if (!hA && hL) a = sl[y];
+        else if (!hA && !hL) a = 127;
+        else a = sa[imin(aboveLimit, x + i)];
+        if (!hL && hA) l = sa[x];
+        else if (!hA && !hL) l = 129;
+        else l = sl[imin(leftLimit, y + i)];
+        above[i] = a;
+        left[i] = l;
+    }
+    if (t == 0) {
+        uint8_t c;
+        if (hA && hL) c = L.tmp2[4 * 39 + 3];
+        else if (hA) c = sa[x];
+        else if (hL) c = sl[y];
+        else c = 128;
+        above[-1] = c;
+        left[-1] = c;
+    }
+}
+
+// k_flow producer side of the granules: the bottom row and right column of a w x h region
+// at (x, y) whose final pixels are in `px` (row stride ps), one granule per 4x4 unit.
+// Follows the region's pixel stores; the caller's coop_sync must separate `px`'s writes.
+template <int NT>
+DEV void coop_publish_gran(const uint8_t* px, int ps, int x, int y, int w, int h, uint64_t* gh, uint64_t* gv, int gw,
+    int ghn, uint32_t epoch)
+{
+    const int t = coop_lane<NT>();
+    const int nw = w >> 2, nh = h >> 2;
+    const uint64_t tag = (uint64_t)epoch << 32;
+    for (int q = t; q < nw + nh; q += NT) {
+        uint32_t v;
+        uint64_t* g;
+        if (q < nw) {
+            v = *reinterpret_cast<const uint32_t*>(px + (h - 1) * ps + 4 * q);
+            g = gh + (size_t)((y + h - 1) >> 2) * gw + (x >> 2) + q;
+        } else {
+            const int r = 4 * (q - nw);
+            const uint8_t* c = px + r * ps + w - 1;
+            v = c[0] | (c[ps] << 8) | (c[2 * ps] << 16) | ((uint32_t)c[3 * ps] << 24);
+            g = gv + (size_t)((x + w - 1) >> 2) * ghn + (y >> 2) + (q - nw);
+        }
+        __hip_atomic_store(g, tag | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps) from edges already
 // gathered into L (coop_intra_edges + a barrier).  Ends with a coop_sync.
 template <int NT>

@@ -182,7 +182,7 @@ DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int1
 // IntraPredict::predict_intra with CFL (IntraPredict.cpp:563-667).  Inter TBs predict
 // nothing here (their prediction is already in the frame).  Ends with a coop_sync.
 template <int NT, int MAX, bool COH>
-DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L)
+DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, const GranEdges* G = nullptr)
 {
     constexpr int CM = TbLds<MAX>::CM;
     const int t = coop_lane<NT>();
@@ -202,9 +202,14 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             L.pred[i * MAX + j] = colors[map[(by + i) * mw + bx + j]];
         }
     } else if (tb.pred == AV1R_PRED_INTRA) {
-        coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
-            (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
-            (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
+        if (COH && G)
+            coop_intra_edges_gran<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+                (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
+                (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra, *G);
+        else
+            coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+                (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
+                (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
         const int isCfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
         IntraParams P;
         P.plane = plane;
@@ -321,20 +326,29 @@ DEV uint32_t add4(uint32_t p, uint2 r)
     return o;
 }
 template <int NT, int MAX>
-DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R)
+DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch)
 {
     const int t = coop_lane<NT>();
     const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;
     const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
     const DevPlane& dst = k.cur.pl[tb.plane];
+    const bool gran = k.gran;
 #pragma unroll
     for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
         const int q = t + u * NT;
         if (q < nq) {
             const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
-            const uint32_t p = *reinterpret_cast<const uint32_t*>(&L.pred[i * MAX + j]);
-            stp4<true>(dst, tb.x + j, tb.y + i, add4(p, R.r[u]));
+            uint32_t* pp = reinterpret_cast<uint32_t*>(&L.pred[i * MAX + j]);
+            const uint32_t o = add4(*pp, R.r[u]);
+            stp4<true>(dst, tb.x + j, tb.y + i, o);
+            if (gran) *pp = o;  // the final pixels, for the edge granules
         }
+    }
+    if (gran) {
+        coop_sync<NT>();
+        const int p = tb.plane;
+        coop_publish_gran<NT>(L.pred, MAX, tb.x, tb.y, av1r_tx_w[tb.tx_size], av1r_tx_h[tb.tx_size], k.gran_h[p], k.gran_v[p],
+            k.gran_w[p], k.gran_hn[p], epoch);
     }
 }
 
@@ -1186,7 +1200,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
 // the block's intra prediction (its edges are final when this item runs) blended with the
 // inter prediction inter_tile stored in the frame.
 template <int NT, bool COH>
-DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
+DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G = nullptr)
 {
     const int t = coop_lane<NT>();
     const av1r_block& blk = k.blocks[bi];
@@ -1219,7 +1233,20 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
         P.filterIntraMode = 0;
         P.smooth = 0;
         P.edgeFilter = k.hdr->enable_intra_edge_filter;
-        coop_intra_predict<NT, COH>(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
+        if (COH && G) {  // k_flow with edge granules: G holds plane 0's, 4 mask words per plane
+            GranEdges Gp = *G;
+            Gp.mask = G->mask + 4 * plane;
+            Gp.h = k.gran_h[plane];
+            Gp.v = k.gran_v[plane];
+            Gp.gw = k.gran_w[plane];
+            Gp.gh = k.gran_hn[plane];
+            coop_intra_edges_gran<NT>(k.mi_cols, k.mi_rows, dst, plane, P.x, P.y, P.log2W, P.log2H, P.haveLeft, P.haveAbove,
+                P.haveAR, P.haveBL, L.intra, Gp);
+            coop_sync<NT>();
+            coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, 64);
+        } else {
+            coop_intra_predict<NT, COH>(k.mi_cols, k.mi_rows, dst, P, L.intra, L.pred, 64);
+        }
         const int sizeScale = 128 / imax(ph, pw);
         const bool addRes = COH;  // k_flow: the block's residuals are added here (tiles)
         for (int q = t; q < pw * ph; q += NT) {
@@ -1268,6 +1295,9 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L)
                 const int i = q / pw, j = q - i * pw;
                 stp<COH>(dst, baseX + j, baseY + i, L.pred[i * 64 + j]);
             }
+            if (COH && G)
+                coop_publish_gran<NT>(L.pred, 64, baseX, baseY, pw, ph, k.gran_h[plane], k.gran_v[plane], k.gran_w[plane],
+                    k.gran_hn[plane], G->epoch);
             coop_sync<NT>();
         }
     }
@@ -1605,12 +1635,25 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     (void)trace;
     (void)s;
 #endif
+    // edge granules: the item's mask words precede its dependency list (4 per plane)
+    const bool gran = k.gran;
+    GranEdges G;
+    if (gran) {
+        const int p = AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 0 : wi.plane;
+        G.mask = k.deps + wi.dep_off - (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 12 : 4);
+        G.h = k.gran_h[p];
+        G.v = k.gran_v[p];
+        G.gw = k.gran_w[p];
+        G.gh = k.gran_hn[p];
+        G.epoch = epoch;
+        G.ctl = ctl;
+    }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
         if constexpr (MAX == 64) {  // blends are always large items
             trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
             trace_stamp(tr, 4);
-            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L);
+            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L, gran ? &G : nullptr);
         }
     } else {
         // intra / palette TB: its residual tile (k_resid) is fetched before the wait
@@ -1620,8 +1663,8 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         trace_stamp(tr, 3);
         flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
         trace_stamp(tr, 4);
-        tb_predict<NT, MAX, true>(k, wi, blk, L);
-        tb_store_flow<NT, MAX>(k, wi, L, R);
+        tb_predict<NT, MAX, true>(k, wi, blk, L, gran ? &G : nullptr);
+        tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
     }
     flow_publish<NT>(k.done + pos, epoch);
     trace_stamp(tr, 5);
