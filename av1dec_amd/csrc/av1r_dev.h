@@ -30,7 +30,7 @@ struct WorkItem {
     uint16_t coef_cnt;  // TB
     uint8_t plane, tx_size, tx_type, flags;  // TB (flags: AV1R_TB_*)
     uint8_t pred;       // TB prediction source: AV1R_PRED_INTRA / _PALETTE / _INTER
-    uint8_t pad0;
+    uint8_t pub;        // k_flow: 1 = a dependency list names this item (store sc1, drain, flag)
     uint16_t dep_cnt;   // k_flow: the items whose pixels this one reads ...
     uint16_t pad1;
     uint32_t dep_off;   // ... at KParams::deps[dep_off, dep_off + dep_cnt) (item positions)

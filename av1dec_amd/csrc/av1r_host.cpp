@@ -715,6 +715,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 break;
             }
             c->deps.push_back((uint32_t)pos);
+            c->items[pos].pub = 1;
         }
     }
 }

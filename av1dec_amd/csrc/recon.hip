@@ -328,6 +328,7 @@ DEV uint32_t add4(uint32_t p, uint2 r)
 template <int NT, int MAX>
 DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch)
 {
+
     const int t = coop_lane<NT>();
     const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;
     const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
@@ -1666,7 +1667,10 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         tb_predict<NT, MAX, true>(k, wi, blk, L, gran ? &G : nullptr);
         tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
     }
-    flow_publish<NT>(k.done + pos, epoch);
+    // the store drain and done flag only where a dependency list names the item (CFL's
+    // luma; every edge owner without granules): edges travel in granules, and later
+    // launches see every store anyway
+    if (wi.pub || !gran) flow_publish<NT>(k.done + pos, epoch);
     trace_stamp(tr, 5);
 }
 
