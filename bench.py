@@ -23,6 +23,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -213,6 +214,28 @@ def main():
     host_fps = n_host / (time.perf_counter() - t1)
     levels, _ = lead.last_frame_stats()
 
+    # the same with every stream fed by its own host thread (contexts are independent and
+    # may be driven concurrently: SURVEY.md §8b threading); frames/s over all streams
+    errs = []
+
+    def feed(d, fr):
+        try:
+            for i in range(n_host):
+                d.decode_frame(fr[i])
+            d.synchronize()
+        except Exception as e:  # re-raised below
+            errs.append(e)
+    sync()
+    th = [threading.Thread(target=feed, args=(d, fr)) for d, fr in zip(decs, streams)]
+    t1 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    host_mt_fps = S * n_host / (time.perf_counter() - t1)
+    if errs:
+        raise errs[0]
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cfps, cn, cdt = cpu_baseline(streams[0], args.cpu_budget)
@@ -255,6 +278,7 @@ def main():
             "stage_algorithmic_GBps": {n: round(sb[n] / max(per_frame_ms[n], 1e-9) / 1e6, 2) for n in names},
             "single_stream_fps": round(single_fps, 3),
             "host_inclusive_fps": round(host_fps, 3),
+            "host_inclusive_fps_threaded": round(host_mt_fps, 3),
             "recon_levels_last_frame": levels,
             "cpu_baseline": cpu,
         }

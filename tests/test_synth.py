@@ -145,6 +145,44 @@ def test_gpu_concurrent_contexts_match_oracle():
 
 
 @pytest.mark.gpu
+def test_gpu_threaded_contexts_match_oracle():
+    """One host thread per decoder (contexts are independent: validation, scheduling,
+    upload and launches run concurrently; k_flow launches share the device's flow chain):
+    every stream stays bit-exact."""
+    import threading
+    nfr = 3
+    dims = [(640, 360), (352, 288), (640, 360), (416, 240)]
+    streams = [pysynth.stream(w, h, nfr, 400 + i) for i, (w, h) in enumerate(dims)]
+    decs = [Decoder(0, keep_stages=False) for _ in streams]
+    errs = []
+
+    def feed(d, s):
+        try:
+            for f in s:
+                d.decode_frame(f)
+            d.synchronize()
+        except Exception as e:
+            errs.append(e)
+    th = [threading.Thread(target=feed, args=(d, s)) for d, s in zip(decs, streams)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for d, s in zip(decs, streams):
+        o = pyoracle.Oracle(keep_stages=False)
+        for f in s:
+            o.decode_frame(f)
+        n = 0
+        while o.output_pending():
+            for x, y in zip(d.get_output(), o.get_output()):
+                assert (x == y).all(), f"output {n}"
+            n += 1
+        assert n == nfr
+        d.close()
+
+
+@pytest.mark.gpu
 def test_gpu_level_schedule_synth_1080p():
     """The level-launch schedule on the bench's 1080p stream (stages checked)."""
     frames = pysynth.stream(1920, 1080, 3, 0x5EED0003)
