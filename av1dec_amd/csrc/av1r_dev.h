@@ -101,6 +101,12 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_ERR (FLOW_QUEUES * FLOW_LINE)
 #define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the host's pinned error word
 #define FLOW_CTL_BYTES 1280
+// k_flow spin bound, in polls of running waves (each a global load round trip, ~0.5-2 us),
+// not in wall-clock time: a wave that the hardware preempts (context save / restore) does
+// not count the time it was off the chip, so only a wait that makes no progress WHILE
+// running gives up (~2-6 s), or one outliving FLOW_WALL
+#define FLOW_SPINS (1u << 22)
+#define FLOW_WALL 3000000000ull  // 30 s of the 100 MHz real-time counter
 
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
 DEV int clip1(int v) { return CLIP3(0, 255, v); }

@@ -970,8 +970,10 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (host_prof()) tp1 = now_us();
         M.pending = false;
         if (M.err && *M.err) {
+            const uint32_t e = *M.err;
             *M.err = 0;
-            return fail(c, AV1R_E_DEVICE, "k_flow: a dependency wait timed out (output of an earlier batch is invalid)");
+            return fail(c, AV1R_E_DEVICE, "k_flow: a %s wait timed out (output of an earlier batch is invalid)",
+                e == 2 ? "edge granule" : "dependency");
         }
     }
     if (!M.err) {
@@ -1123,12 +1125,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (hrt[2 * n + 1]) launch_k_resid(1, dk, drt + n + 1, n, hrt[2 * n + 1], st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
         if (nGroups) {
-            uint32_t epoch = ++epochs;
-            if (!epoch) epoch = ++epochs;
             const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
             FlowChain& F = g_flowChain[lc->device];
             std::lock_guard<std::mutex> lock(F.m);
+            // epochs in chain order (unique per launch; taken under the chain's lock)
+            uint32_t epoch = ++epochs;
+            if (!epoch) epoch = ++epochs;
             if (!F.done) HIPCHK(hipEventCreateWithFlags(&F.done, hipEventDisableTiming));
             if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
             launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, M.err, epoch, grid, trace, st);

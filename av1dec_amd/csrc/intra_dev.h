@@ -191,6 +191,7 @@ struct GranEdges {
     int gw, gh;
     uint32_t epoch;
     uint32_t* ctl;         // k_flow control block (FLOW_ERR)
+    unsigned long long* tr;  // -DAV1R_TRACE timeline row (or null)
 };
 template <int NT>
 DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
@@ -211,6 +212,7 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
     if ((NT == 64 || t < 64) && nq > 0) {
         const int lane = t & 63;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t spins = 0;
         bool dead = false;
         for (int base = 0; base < nq; base += 64) {
             const int q = base + lane;
@@ -244,12 +246,12 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
                     val = (uint32_t)gv;
                 }
                 if (__all(ok)) break;
-                if (__hip_atomic_load(G.ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-                    __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
-                    if (lane == 0) {
-                        __hip_atomic_store(G.ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool other = __hip_atomic_load(G.ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (other || ++spins > FLOW_SPINS || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
+                    if (lane == 0 && !other) {  // 2: an edge granule wait (1: a dependency flag wait)
+                        __hip_atomic_store(G.ctl + FLOW_ERR, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(G.ctl + FLOW_HOSTERR)),
-                            1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                     dead = true;
                     break;

@@ -206,7 +206,8 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             coop_intra_edges_gran<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
                 (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
                 (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra, *G);
-        else
+        if (COH && G) trace_stamp(G->tr, 8);
+        if (!(COH && G))
             coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
                 (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
                 (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
@@ -1572,10 +1573,9 @@ extern "C" __global__ __launch_bounds__(64) void k_inter_m(const KParams* kps, c
 // reads every pixel another item of the launch may have written with sc1 loads (ldp /
 // ldp4<true>), which bypass the CU's L1.  The residual of a TB reads only the batch, so it
 // is computed BEFORE the wait, off the dependency chain.  Every spin is bounded: after
-// FLOW_TIMEOUT ticks (or once any wave has timed out) the wave gives up and sets the
+// FLOW_SPINS polls (or once any wave has timed out) the wave gives up and sets the
 // launch's error word, which the host reports.
 // ---------------------------------------------------------------------------------
-#define FLOW_TIMEOUT 100000000ull  // 1 s of the 100 MHz real-time counter
 
 template <int NT>
 DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint32_t epoch, uint32_t* ctl)
@@ -1583,6 +1583,7 @@ DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint
     if (nd && (NT == 64 || threadIdx.x < 64)) {
         const int lane = threadIdx.x & 63;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t spins = 0;
         for (uint32_t b = 0; b < nd; b += 64) {
             const bool mine = b + lane < nd;
             const uint32_t d = mine ? deps[b + lane] : 0u;
@@ -1590,8 +1591,8 @@ DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint
                 const bool ok = !mine || __hip_atomic_load(done + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
                 if (__all(ok)) break;
                 const bool dead = __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (dead || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT) {
-                    if (lane == 0) {
+                if (dead || ++spins > FLOW_SPINS || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
+                    if (lane == 0 && !dead) {  // the wave that gave up first reports
                         __hip_atomic_store(ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         // the host's copy (pinned memory, checked when the launch's metadata is reused)
                         __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(ctl + FLOW_HOSTERR)),
@@ -1648,6 +1649,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         G.gh = k.gran_hn[p];
         G.epoch = epoch;
         G.ctl = ctl;
+        G.tr = tr;
     }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
         if constexpr (MAX == 64) {  // blends are always large items
@@ -1665,7 +1667,9 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
         trace_stamp(tr, 4);
         tb_predict<NT, MAX, true>(k, wi, blk, L, gran ? &G : nullptr);
+        trace_stamp(tr, 9);
         tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
+        trace_stamp(tr, 10);
     }
     // the store drain and done flag only where a dependency list names the item (CFL's
     // luma; every edge owner without granules): edges travel in granules, and later

@@ -215,26 +215,34 @@ def main():
     levels, _ = lead.last_frame_stats()
 
     # the same with every stream fed by its own host thread (contexts are independent and
-    # may be driven concurrently: SURVEY.md §8b threading); frames/s over all streams
+    # may be driven concurrently: SURVEY.md §8b threading); frames/s over all streams.  Each
+    # context's first host-batch frame is issued serially first (known issue,
+    # a rare k_flow wait timeout when contexts' first frames come from concurrent threads);
+    # a failure here is reported in the line, never fatal to it
     errs = []
 
     def feed(d, fr):
         try:
-            for i in range(n_host):
-                d.decode_frame(fr[i])
+            for i in range(1, n_host + 1):
+                d.decode_frame(fr[i % len(fr)])
             d.synchronize()
-        except Exception as e:  # re-raised below
-            errs.append(e)
-    sync()
-    th = [threading.Thread(target=feed, args=(d, fr)) for d, fr in zip(decs, streams)]
-    t1 = time.perf_counter()
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
-    host_mt_fps = S * n_host / (time.perf_counter() - t1)
-    if errs:
-        raise errs[0]
+        except Exception as e:
+            errs.append(str(e))
+    host_mt_fps = None
+    try:
+        for d, fr in zip(decs, streams):
+            d.decode_frame(fr[0])
+        sync()
+        th = [threading.Thread(target=feed, args=(d, fr)) for d, fr in zip(decs, streams)]
+        t1 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if not errs:
+            host_mt_fps = round(S * n_host / (time.perf_counter() - t1), 3)
+    except Exception as e:
+        errs.append(str(e))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -278,7 +286,8 @@ def main():
             "stage_algorithmic_GBps": {n: round(sb[n] / max(per_frame_ms[n], 1e-9) / 1e6, 2) for n in names},
             "single_stream_fps": round(single_fps, 3),
             "host_inclusive_fps": round(host_fps, 3),
-            "host_inclusive_fps_threaded": round(host_mt_fps, 3),
+            "host_inclusive_fps_threaded": host_mt_fps,
+            **({"host_threaded_error": errs[0][:160]} if errs else {}),
             "recon_levels_last_frame": levels,
             "cpu_baseline": cpu,
         }

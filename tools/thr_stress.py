@@ -1,0 +1,40 @@
+"""Stress (GPU box): 8 decoders fed by 8 host threads (1080p synthetic streams), counting the
+rare k_flow wait timeouts of the first threaded round of a process (known issue).
+usage: python3 tools/thr_stress.py [reps]   (PREWARM=1: one serial frame per context first)"""
+import os, sys, threading, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tools", "synth")]
+import pysynth
+from av1dec_amd import Decoder
+S, N, REP = 8, 24, int(sys.argv[1]) if len(sys.argv) > 1 else 5
+streams = [pysynth.stream(1920, 1080, N, 0x5EED1000 + i) for i in range(S)]
+fails = 0
+if os.environ.get("PREWARM"):  # every context's buffers allocated before the threaded reps
+    keep = [Decoder(0, keep_stages=False) for _ in range(S)]
+    for d, fr in zip(keep, streams):
+        d.decode_frame(fr[0]); d.synchronize()
+    for d in keep: d.close()
+for rep in range(REP):
+    decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+    for d in decs:
+        d.set_discard_output(True)
+    errs = []
+    def feed(d, fr):
+        try:
+            for f in fr:
+                d.decode_frame(f)
+            d.synchronize()
+            d.decode_frame(fr[0]); d.synchronize()  # surfaces an error of the last launches
+        except Exception as e:
+            errs.append(str(e)[:120])
+    th = [threading.Thread(target=feed, args=(d, fr)) for d, fr in zip(decs, streams)]
+    t = time.perf_counter()
+    for x in th: x.start()
+    for x in th: x.join()
+    dt = time.perf_counter() - t
+    fails += bool(errs)
+    print(f"gran={os.environ.get('AV1R_GRAN', '1')} rep {rep}: {dt:.2f} s, errors {len(errs)} {errs[:1]}", flush=True)
+    for d in decs:
+        try: d.close()
+        except Exception as e: print("close:", e)
+print("fails", fails)

@@ -163,6 +163,16 @@ def summarise_flow(path, lo=0, hi=None):
         r = us(t3[m] - t2[m]); w = us(t4[m] - t3[m]); f = us(t5[m] - t4[m])
         print(f"{name:10s} n={m.sum():7d} resid p50 {np.median(r):5.2f} wait p50 {np.median(w):6.2f} p90 {np.percentile(w, 90):7.2f}"
               f" finish p50 {np.median(f):5.2f} p90 {np.percentile(f, 90):5.2f}  last publish {us(t5[m].max() - t0):8.1f} us")
+    m = flow & (kind == 0) & (pred == 0) & (a[:, 8] > 0)
+    if m.any():  # granule build: 8 edges gathered, 9 predicted, 10 stored + granules out
+        t8, t9, t10 = a[:, 8], a[:, 9], a[:, 10]
+        for ts in np.unique(txs[m]):
+            mm = m & (txs == ts)
+            if mm.sum() < 200:
+                continue
+            q = lambda x, y: np.percentile(us(x[mm] - y[mm]), [50, 90])
+            print(f"   intra tx {ts:2d}: gather(wait) p50/p90 %.2f/%.2f  predict %.2f/%.2f  store %.2f/%.2f  publish %.2f/%.2f"
+                  % (*q(t8, t4), *q(t9, t8), *q(t10, t9), *q(t5, t10)))
     m = flow & (kind == 0) & (pred == 0)
     for ts in np.unique(txs[m]):
         mm = m & (txs == ts)
