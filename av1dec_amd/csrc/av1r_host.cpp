@@ -1132,10 +1132,15 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
-            if (!F.done) HIPCHK(hipEventCreateWithFlags(&F.done, hipEventDisableTiming));
+            // a fresh event per k_flow: never re-recorded while another stream's wait may
+            // still refer to it (the previous one is released once waited for)
+            hipEvent_t ev = nullptr;
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
             launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, M.err, epoch, grid, trace, st);
-            HIPCHK(hipEventRecord(F.done, st));
+            HIPCHK(hipEventRecord(ev, st));
+            if (F.done) (void)hipEventDestroy(F.done);
+            F.done = ev;
             F.last = st;
         }
     }
