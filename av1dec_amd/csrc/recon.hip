@@ -1680,7 +1680,10 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
 // workgroup), n = 1..4 small items (one per wave)
-extern "C" __global__ __launch_bounds__(256, 4) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
+#ifndef AV1R_FLOW_WAVES
+#define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better)
+#endif
+extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
     uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
@@ -1731,6 +1734,8 @@ int flow_grid(int device)
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k_flow), 256, 0) != hipSuccess || per <= 0)
             per = 1;
         per = per > 8 ? 8 : per;
+        // AV1R_FLOW_PER_CU: fewer resident workgroups per CU (A/B of polling pressure)
+        if (const char* e = getenv("AV1R_FLOW_PER_CU")) per = per < atoi(e) ? per : (atoi(e) > 0 ? atoi(e) : per);
         cache[device] = ((cus * per) / FLOW_QUEUES) * FLOW_QUEUES;
         if (cache[device] < FLOW_QUEUES) cache[device] = FLOW_QUEUES;
     }
