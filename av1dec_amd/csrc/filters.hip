@@ -528,11 +528,18 @@ DEV int lr_src(const LrPix& S, int x, int y)
 #define LR_TW 64
 #define LR_TH 32
 #define LR_SW (LR_TW + 8)
+// The Wiener intermediates and the self-guided a/b planes share their LDS: a tile whose
+// units mix both types is filtered in two rounds (Wiener, then self-guided).  29.7 KB:
+// 5 workgroups per CU (34.5 KB and 4 without the union)
 struct LrLds {
-    uint8_t src[LR_TH + 6][LR_SW];        // get_source_sample over rows ty0-3.., cols x0-4..
-    int16_t hw[LR_TH + 6][LR_TW];         // Wiener horizontal pass
-    int16_t A[2][LR_TH + 2][LR_TW + 2];   // self-guided a per pass, rows ty0-1.., cols x0-1..
-    int32_t B[2][LR_TH + 2][LR_TW + 2];
+    uint8_t src[LR_TH + 6][LR_SW];            // get_source_sample over rows ty0-3.., cols x0-4..
+    union {
+        int16_t hw[LR_TH + 6][LR_TW];         // Wiener horizontal pass
+        struct {
+            int16_t A[2][LR_TH + 2][LR_TW + 2];  // self-guided a per pass, rows ty0-1.., cols x0-1..
+            int32_t B[2][LR_TH + 2][LR_TW + 2];
+        };
+    };
     av1r_lr_unit unit[3];
 };
 
@@ -676,118 +683,126 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
         anyS |= L.unit[u].type == AV1R_RESTORE_SGRPROJ;
     }
     auto unitOf = [&](int c) { return imin((x0 + CLIP3(0, tw - 1, c)) / us, cols - 1) - uc0; };
-    if (anyW) {
-        // wienerFilter horizontal pass (LoopRestoration.cpp:253-265)
-        const int offset = 1 << (8 + 7 - 3 - 1), limit = (1 << (8 + 1 + 7 - 3)) - 1;
-        for (int q = t; q < (th + 6) * tw; q += 256) {
-            int i = q / tw, c = q - i * tw;
-            const av1r_lr_unit& u = L.unit[unitOf(c)];
-            if (u.type != AV1R_RESTORE_WIENER) continue;
-            int hf3 = 128 - 2 * (u.wiener[1][0] + u.wiener[1][1] + u.wiener[1][2]);
-            const uint8_t* sp = &L.src[i][c + 1];
-            int hs = u.wiener[1][0] * (sp[0] + sp[6]) + u.wiener[1][1] * (sp[1] + sp[5]) + u.wiener[1][2] * (sp[2] + sp[4]) + hf3 * sp[3];
-            L.hw[i][c] = (int16_t)CLIP3(-offset, limit - offset, r2(hs, 3));
-        }
-    }
-    if (anyS) {
-        // a, b of both passes (box radius 2 / 1: Sgr_Params) at rows ty0-1 .. ty1 (ii), cols
-        // x0-1 .. x0+tw (cc).  The box sums are separable: each lane walks one column over a
-        // run of rows, keeping the last five rows' horizontal 5- and 3-sums in registers.
-        constexpr int RUNS = 3;
-        const int nr = th + 2, nc = tw + 2, runH = (nr + RUNS - 1) / RUNS;
-        for (int q = t; q < RUNS * nc; q += 256) {
-            const int cc = q % nc, i0 = (q / nc) * runH, i1 = imin(nr, i0 + runH);
-            const av1r_lr_unit& u = L.unit[unitOf(cc - 1)];
-            if (u.type != AV1R_RESTORE_SGRPROJ || i0 >= i1) continue;
-            const int set = u.sgr_set;
-            const bool p0 = av1r_sgr_params[set][0] != 0, p1 = av1r_sgr_params[set][2] != 0;
-            // h5[k] / h3[k]: (squares, sums) of source row sr - k, columns cc+1..cc+5 / cc+2..cc+4
-            int a5[5] = {}, b5[5] = {}, a3[4] = {}, b3[4] = {};
-            for (int sr = i0; sr < i1 + 4; sr++) {
-#pragma unroll
-                for (int k = 4; k > 0; k--) {
-                    a5[k] = a5[k - 1];
-                    b5[k] = b5[k - 1];
-                }
-#pragma unroll
-                for (int k = 3; k > 0; k--) {
-                    a3[k] = a3[k - 1];
-                    b3[k] = b3[k - 1];
-                }
-                const uint8_t* row = &L.src[sr][cc + 1];
-                const int v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4];
-                b3[0] = v1 + v2 + v3;
-                a3[0] = v1 * v1 + v2 * v2 + v3 * v3;
-                b5[0] = b3[0] + v0 + v4;
-                a5[0] = a3[0] + v0 * v0 + v4 * v4;
-                const int ii = sr - 4;  // the box centre's row: source row ii + 2
-                if (ii < i0) continue;
-                int A, B;
-                if (p0 && ((ty0 - 1 + ii - y0) & 1)) {  // pass 0 uses odd rows only
-                    sgr_ab_fin(a5[0] + a5[1] + a5[2] + a5[3] + a5[4], b5[0] + b5[1] + b5[2] + b5[3] + b5[4], 2, set, 0, A, B);
-                    L.A[0][ii][cc] = (int16_t)A;
-                    L.B[0][ii][cc] = B;
-                }
-                if (p1) {  // rows ii + 1 .. ii + 3
-                    sgr_ab_fin(a3[1] + a3[2] + a3[3], b3[1] + b3[2] + b3[3], 1, set, 1, A, B);
-                    L.A[1][ii][cc] = (int16_t)A;
-                    L.B[1][ii][cc] = B;
-                }
+    const int rounds = anyW && anyS ? 2 : 1;
+    for (int rd = 0; rd < rounds; rd++) {
+        const bool doW = anyW && (rounds == 1 || rd == 0), doS = anyS && (rounds == 1 || rd == 1);
+        if (rd) __syncthreads();  // round 0's reads of the shared LDS are done
+        if (doW) {
+            // wienerFilter horizontal pass (LoopRestoration.cpp:253-265)
+            const int offset = 1 << (8 + 7 - 3 - 1), limit = (1 << (8 + 1 + 7 - 3)) - 1;
+            for (int q = t; q < (th + 6) * tw; q += 256) {
+                int i = q / tw, c = q - i * tw;
+                const av1r_lr_unit& u = L.unit[unitOf(c)];
+                if (u.type != AV1R_RESTORE_WIENER) continue;
+                int hf3 = 128 - 2 * (u.wiener[1][0] + u.wiener[1][1] + u.wiener[1][2]);
+                const uint8_t* sp = &L.src[i][c + 1];
+                int hs = u.wiener[1][0] * (sp[0] + sp[6]) + u.wiener[1][1] * (sp[1] + sp[5]) + u.wiener[1][2] * (sp[2] + sp[4]) + hf3 * sp[3];
+                L.hw[i][c] = (int16_t)CLIP3(-offset, limit - offset, r2(hs, 3));
             }
         }
-    }
-    __syncthreads();
-    for (int q = t; q < tw * th; q += 256) {
-        const int r = q / tw, c = q - r * tw;
-        const int x = x0 + c, y = ty0 + r;
-        const int cdef = L.src[r + 3][c + 4];
-        int outv = cdef;
-        const int ui = unitOf(c);
-        const av1r_lr_unit& u = L.unit[ui];
-        if (x < planeEndX && y < planeEndY && u.type != AV1R_RESTORE_NONE) {
-            if (u.type == AV1R_RESTORE_WIENER) {
-                int vf3 = 128 - 2 * (u.wiener[0][0] + u.wiener[0][1] + u.wiener[0][2]);
-                int s = u.wiener[0][0] * (L.hw[r][c] + L.hw[r + 6][c]) + u.wiener[0][1] * (L.hw[r + 1][c] + L.hw[r + 5][c])
-                    + u.wiener[0][2] * (L.hw[r + 2][c] + L.hw[r + 4][c]) + vf3 * L.hw[r + 3][c];
-                outv = clip1(r2(s, 11));
-            } else {
-                // selfGuidedFilter (LoopRestoration.cpp:420-479)
+        if (doS) {
+            // a, b of both passes (box radius 2 / 1: Sgr_Params) at rows ty0-1 .. ty1 (ii), cols
+            // x0-1 .. x0+tw (cc).  The box sums are separable: each lane walks one column over a
+            // run of rows, keeping the last five rows' horizontal 5- and 3-sums in registers.
+            constexpr int RUNS = 3;
+            const int nr = th + 2, nc = tw + 2, runH = (nr + RUNS - 1) / RUNS;
+            for (int q = t; q < RUNS * nc; q += 256) {
+                const int cc = q % nc, i0 = (q / nc) * runH, i1 = imin(nr, i0 + runH);
+                const av1r_lr_unit& u = L.unit[unitOf(cc - 1)];
+                if (u.type != AV1R_RESTORE_SGRPROJ || i0 >= i1) continue;
                 const int set = u.sgr_set;
-                const int i = y - y0;
-                const int uu = cdef << 4;
-                const int w0 = u.sgr_xqd[0], w1 = u.sgr_xqd[1], w2 = (1 << 7) - w0 - w1;
-                int v = w1 * uu;
-#pragma unroll
-                for (int pass = 0; pass < 2; pass++) {
-                    const int rad = av1r_sgr_params[set][pass * 2];
-                    const int w = pass ? w2 : w0;
-                    if (!rad) {
-                        v += w * uu;
-                        continue;
+                const bool p0 = av1r_sgr_params[set][0] != 0, p1 = av1r_sgr_params[set][2] != 0;
+                // h5[k] / h3[k]: (squares, sums) of source row sr - k, columns cc+1..cc+5 / cc+2..cc+4
+                int a5[5] = {}, b5[5] = {}, a3[4] = {}, b3[4] = {};
+                for (int sr = i0; sr < i1 + 4; sr++) {
+    #pragma unroll
+                    for (int k = 4; k > 0; k--) {
+                        a5[k] = a5[k - 1];
+                        b5[k] = b5[k - 1];
                     }
-                    const int shift = (pass == 0 && (i & 1)) ? 4 : 5;
-                    int a = 0, b = 0;
-                    for (int dy = -1; dy <= 1; dy++) {
-                        if (pass == 0 && !((i + dy) & 1)) continue;
-                        for (int dx = -1; dx <= 1; dx++) {
-                            const int wt = pass == 0 ? (dx == 0 ? 6 : 5) : ((dx == 0 || dy == 0) ? 4 : 3);
-                            int A, B;
-                            if (unitOf(c + dx) == ui) {
-                                A = L.A[pass][r + 1 + dy][c + 1 + dx];
-                                B = L.B[pass][r + 1 + dy][c + 1 + dx];
-                            } else {  // neighbour column in another unit: this unit's parameters
-                                sgr_ab_lds(L, r + 3 + dy, c + 4 + dx, rad, set, pass, A, B);
-                            }
-                            a += wt * A;
-                            b += wt * B;
-                        }
+    #pragma unroll
+                    for (int k = 3; k > 0; k--) {
+                        a3[k] = a3[k - 1];
+                        b3[k] = b3[k - 1];
                     }
-                    v += w * r2(a * cdef + b, 8 + shift - 4);
+                    const uint8_t* row = &L.src[sr][cc + 1];
+                    const int v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4];
+                    b3[0] = v1 + v2 + v3;
+                    a3[0] = v1 * v1 + v2 * v2 + v3 * v3;
+                    b5[0] = b3[0] + v0 + v4;
+                    a5[0] = a3[0] + v0 * v0 + v4 * v4;
+                    const int ii = sr - 4;  // the box centre's row: source row ii + 2
+                    if (ii < i0) continue;
+                    int A, B;
+                    if (p0 && ((ty0 - 1 + ii - y0) & 1)) {  // pass 0 uses odd rows only
+                        sgr_ab_fin(a5[0] + a5[1] + a5[2] + a5[3] + a5[4], b5[0] + b5[1] + b5[2] + b5[3] + b5[4], 2, set, 0, A, B);
+                        L.A[0][ii][cc] = (int16_t)A;
+                        L.B[0][ii][cc] = B;
+                    }
+                    if (p1) {  // rows ii + 1 .. ii + 3
+                        sgr_ab_fin(a3[1] + a3[2] + a3[3], b3[1] + b3[2] + b3[3], 1, set, 1, A, B);
+                        L.A[1][ii][cc] = (int16_t)A;
+                        L.B[1][ii][cc] = B;
+                    }
                 }
-                outv = clip1(r2(v, 4 + 7));
             }
         }
-        O.p[(size_t)y * O.stride + x] = (uint8_t)outv;
+        __syncthreads();
+        for (int q = t; q < tw * th; q += 256) {
+            const int r = q / tw, c = q - r * tw;
+            const int x = x0 + c, y = ty0 + r;
+            const int cdef = L.src[r + 3][c + 4];
+            int outv = cdef;
+            const int ui = unitOf(c);
+            const av1r_lr_unit& u = L.unit[ui];
+            const bool filt = x < planeEndX && y < planeEndY && u.type != AV1R_RESTORE_NONE;
+            // this round's pixels: Wiener and unfiltered ones in round 0, self-guided in round 1
+            if (rounds == 2 && (rd == 1) != (filt && u.type == AV1R_RESTORE_SGRPROJ)) continue;
+            if (filt) {
+                if (u.type == AV1R_RESTORE_WIENER) {
+                    int vf3 = 128 - 2 * (u.wiener[0][0] + u.wiener[0][1] + u.wiener[0][2]);
+                    int s = u.wiener[0][0] * (L.hw[r][c] + L.hw[r + 6][c]) + u.wiener[0][1] * (L.hw[r + 1][c] + L.hw[r + 5][c])
+                        + u.wiener[0][2] * (L.hw[r + 2][c] + L.hw[r + 4][c]) + vf3 * L.hw[r + 3][c];
+                    outv = clip1(r2(s, 11));
+                } else {
+                    // selfGuidedFilter (LoopRestoration.cpp:420-479)
+                    const int set = u.sgr_set;
+                    const int i = y - y0;
+                    const int uu = cdef << 4;
+                    const int w0 = u.sgr_xqd[0], w1 = u.sgr_xqd[1], w2 = (1 << 7) - w0 - w1;
+                    int v = w1 * uu;
+    #pragma unroll
+                    for (int pass = 0; pass < 2; pass++) {
+                        const int rad = av1r_sgr_params[set][pass * 2];
+                        const int w = pass ? w2 : w0;
+                        if (!rad) {
+                            v += w * uu;
+                            continue;
+                        }
+                        const int shift = (pass == 0 && (i & 1)) ? 4 : 5;
+                        int a = 0, b = 0;
+                        for (int dy = -1; dy <= 1; dy++) {
+                            if (pass == 0 && !((i + dy) & 1)) continue;
+                            for (int dx = -1; dx <= 1; dx++) {
+                                const int wt = pass == 0 ? (dx == 0 ? 6 : 5) : ((dx == 0 || dy == 0) ? 4 : 3);
+                                int A, B;
+                                if (unitOf(c + dx) == ui) {
+                                    A = L.A[pass][r + 1 + dy][c + 1 + dx];
+                                    B = L.B[pass][r + 1 + dy][c + 1 + dx];
+                                } else {  // neighbour column in another unit: this unit's parameters
+                                    sgr_ab_lds(L, r + 3 + dy, c + 4 + dx, rad, set, pass, A, B);
+                                }
+                                a += wt * A;
+                                b += wt * B;
+                            }
+                        }
+                        v += w * r2(a * cdef + b, 8 + shift - 4);
+                    }
+                    outv = clip1(r2(v, 4 + 7));
+                }
+            }
+            O.p[(size_t)y * O.stride + x] = (uint8_t)outv;
+        }
     }
 }
 

@@ -187,6 +187,45 @@ def test_gpu_threaded_contexts_match_oracle():
         d.close()
 
 
+def _mixed_lr(frame):
+    """The frame with 32-px loop-restoration units on luma, alternating Wiener / self-guided
+    by column, so every 64-px k_lr tile mixes both types (its two-round path)."""
+    import numpy as np
+    from av1dec_amd import abi, batchfile
+    sec = dict(frame.sec)
+    h = abi.FrameHdr.from_buffer_copy(sec["hdr"].tobytes())
+    units = np.frombuffer(sec["lr"].tobytes(), dtype=abi.LR_DTYPE).copy()
+    wie = units[units["type"] == 1][0]
+    sgr = units[units["type"] == 2][0]
+    rows = max((h.frame_height + 16) // 32, 1)
+    cols = max((h.frame_width + 16) // 32, 1)
+    new = np.zeros(rows * cols, dtype=abi.LR_DTYPE)
+    for c in range(cols):
+        new[c::cols] = wie if c % 2 == 0 else sgr
+    h.lr_type[0] = 3  # switchable
+    h.lr_unit_size[0] = 32
+    h.lr_unit_rows[0], h.lr_unit_cols[0], h.lr_unit_off[0] = rows, cols, len(units)
+    sec["lr"] = np.concatenate([units, new]).view(np.uint8)
+    sec["hdr"] = np.frombuffer(bytes(h), dtype=np.uint8).copy()
+    return batchfile.Frame(sec)
+
+
+@pytest.mark.gpu
+def test_gpu_lr_mixed_unit_tiles():
+    """k_lr tiles whose units mix Wiener and self-guided (the LDS they share is used in two
+    rounds): every stage equals the oracle's."""
+    frames = [_mixed_lr(f) for f in pysynth.stream(640, 360, 2, 0x5EED0077)]
+    d = Decoder(0, keep_stages=True)
+    o = pyoracle.Oracle(keep_stages=True)
+    for i, f in enumerate(frames):
+        assert f.hdr.uses_lr
+        d.decode_frame(f)
+        o.decode_frame(f)
+        for p, (a, b) in enumerate(zip(d.read_stage(3), o.read_stage(3))):
+            assert (a == b).all(), f"frame {i} LR plane {p}"
+    d.close()
+
+
 @pytest.mark.gpu
 def test_gpu_level_schedule_synth_1080p():
     """The level-launch schedule on the bench's 1080p stream (stages checked)."""
