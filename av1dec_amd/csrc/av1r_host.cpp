@@ -36,7 +36,10 @@ void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipS
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
-int flow_grid(int device);
+#ifdef AV1R_FLOW_DEBUG
+uint32_t flow_debug_overlaps();
+#endif
+int flow_grid(int device, int maxPer);
 void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
 void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s);
@@ -1125,10 +1128,16 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (hrt[2 * n + 1]) launch_k_resid(1, dk, drt + n + 1, n, hrt[2 * n + 1], st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
         if (nGroups) {
-            const int grid = (int)std::min<size_t>(flow_grid(lc->device), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
             FlowChain& F = g_flowChain[lc->device];
             std::lock_guard<std::mutex> lock(F.m);
+            // Launches from several streams (contexts driven from concurrent threads) are
+            // chained by an event, but grids of different launches were measured resident
+            // together (-DAV1R_FLOW_DEBUG) and then starved each other now and then (a wait
+            // timed out).  Such a launch takes one workgroup per CU, so that several of them
+            // fit the chip side by side, each fully resident: progress whatever the overlap.
+            const bool shared = F.last && F.last != st;
+            const int grid = (int)std::min<size_t>(flow_grid(lc->device, shared ? 1 : 8), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
@@ -1322,6 +1331,9 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipStreamDestroy(c->copyStream);
     if (c->resDev) (void)hipFree(c->resDev);
     if (c->granDev) (void)hipFree(c->granDev);
+#ifdef AV1R_FLOW_DEBUG
+    fprintf(stderr, "av1r: k_flow co-resident entries so far: %u\n", flow_debug_overlaps());
+#endif
     (void)hipEventDestroy(c->sync);
     (void)hipEventDestroy(c->joinEv);
     if (c->traceDev) (void)hipFree(c->traceDev);

@@ -1683,6 +1683,11 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 #ifndef AV1R_FLOW_WAVES
 #define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better)
 #endif
+#ifdef AV1R_FLOW_DEBUG
+// -DAV1R_FLOW_DEBUG: counts workgroup entries that find another launch's k_flow
+// workgroups still running (co-resident grids, which the flow chain should exclude)
+__device__ uint32_t g_flow_active, g_flow_epoch, g_flow_overlap;
+#endif
 extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
     uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
@@ -1691,11 +1696,23 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     __shared__ uint32_t ticket[2];  // double-buffered: a slow wave may still read the old one
     const uint32_t q = blockIdx.x % FLOW_QUEUES;
     uint32_t* head = ctl + q * FLOW_LINE;
+#ifdef AV1R_FLOW_DEBUG
+    if (threadIdx.x == 0) {
+        const uint32_t prev = atomicExch(&g_flow_epoch, epoch);
+        const uint32_t act = atomicAdd(&g_flow_active, 1u);
+        if (prev != epoch && act > 0) atomicAdd(&g_flow_overlap, 1u);
+    }
+#endif
     if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     for (uint32_t it = 0;; it ^= 1) {
         const uint32_t g = __builtin_amdgcn_readfirstlane(ticket[it]) * FLOW_QUEUES + q;
-        if (g >= nGroups) return;
+        if (g >= nGroups) {
+#ifdef AV1R_FLOW_DEBUG
+            if (threadIdx.x == 0) atomicSub(&g_flow_active, 1u);
+#endif
+            return;
+        }
         // AV1R_TICKET_PREFETCH: take the next ticket before running this group (holding it
         // early keeps the progress argument: a held group waits only for earlier ones);
         // measured no faster, so off
@@ -1724,23 +1741,35 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 
 // persistent grid of k_flow on `device`: every CU's resident workgroups (capped at 8 per
 // CU), a multiple of FLOW_QUEUES
-int flow_grid(int device)
+int flow_grid(int device, int maxPer)
 {
-    static int cache[64] = {};
+    static int cache[64][2] = {};
     if (device < 0 || device >= 64) return FLOW_QUEUES;
-    if (!cache[device]) {
+    const int slot = maxPer < 8 ? 1 : 0;
+    if (!cache[device][slot]) {
         int cus = 0, per = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 32;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k_flow), 256, 0) != hipSuccess || per <= 0)
             per = 1;
         per = per > 8 ? 8 : per;
+        per = per > maxPer ? maxPer : per;
         // AV1R_FLOW_PER_CU: fewer resident workgroups per CU (A/B of polling pressure)
         if (const char* e = getenv("AV1R_FLOW_PER_CU")) per = per < atoi(e) ? per : (atoi(e) > 0 ? atoi(e) : per);
-        cache[device] = ((cus * per) / FLOW_QUEUES) * FLOW_QUEUES;
-        if (cache[device] < FLOW_QUEUES) cache[device] = FLOW_QUEUES;
+        int g = ((cus * per) / FLOW_QUEUES) * FLOW_QUEUES;
+        cache[device][slot] = g < FLOW_QUEUES ? FLOW_QUEUES : g;
     }
-    return cache[device];
+    return cache[device][slot];
 }
+
+#ifdef AV1R_FLOW_DEBUG
+uint32_t flow_debug_overlaps()
+{
+    uint32_t v = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_flow_overlap), sizeof(v));
+    return v;
+}
+#endif
 
 void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s)

@@ -216,9 +216,8 @@ def main():
 
     # the same with every stream fed by its own host thread (contexts are independent and
     # may be driven concurrently: SURVEY.md §8b threading); frames/s over all streams.  Each
-    # context's first host-batch frame is issued serially first (known issue,
-    # a rare k_flow wait timeout when contexts' first frames come from concurrent threads);
-    # a failure here is reported in the line, never fatal to it
+    # context's first host-batch frame is issued serially first (concurrent
+    # threads and the flow chain); a failure here is reported in the line, never fatal to it
     errs = []
 
     def feed(d, fr):

@@ -155,8 +155,8 @@ def test_gpu_threaded_contexts_match_oracle():
     streams = [pysynth.stream(w, h, nfr, 400 + i) for i, (w, h) in enumerate(dims)]
     decs = [Decoder(0, keep_stages=False) for _ in streams]
     errs = []
-    # each context's first frame serially (known issue, a rare k_flow wait
-    # timeout when contexts' FIRST frames come from concurrent threads at process start)
+    # each context's first frame serially (concurrent threads and the flow chain;
+    # a rare k_flow wait timeout there before multi-stream launches took small grids)
     for d, s in zip(decs, streams):
         d.decode_frame(s[0])
         d.synchronize()

@@ -1,5 +1,5 @@
 """Stress (GPU box): 8 decoders fed by 8 host threads (1080p synthetic streams), counting the
-rare k_flow wait timeouts of the first threaded round of a process (known issue).
+k_flow wait timeouts (concurrent threads and the flow chain).
 usage: python3 tools/thr_stress.py [reps]   (PREWARM=1: one serial frame per context first)"""
 import os, sys, threading, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
