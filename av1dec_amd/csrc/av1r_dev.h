@@ -94,12 +94,14 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define KP(kps, i) (*(const KParams*)(&((KpConst)(kps))[i]))
 
 // k_flow control block (recon.hip): FLOW_QUEUES queue heads, one 128-B line each, then
-// the error word and the address of the host's error word; written by the host before
-// every launch
+// the error word, the address of the host's error word and the spin bound (one line),
+// then the queue-assignment counter (its own line); written by the host before every launch
 #define FLOW_QUEUES 8
 #define FLOW_LINE 32
 #define FLOW_ERR (FLOW_QUEUES * FLOW_LINE)
-#define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the host's pinned error word
+#define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the launch's pinned host error word
+#define FLOW_SPINLIM (FLOW_ERR + 4)  // polls before a wait gives up (0: FLOW_SPINS)
+#define FLOW_ASSIGN (FLOW_ERR + FLOW_LINE)  // workgroup entries: entry k serves queue k % FLOW_QUEUES
 #define FLOW_CTL_BYTES 1280
 // k_flow spin bound, in polls of running waves (each a global load round trip, ~0.5-2 us),
 // not in wall-clock time: a wave that the hardware preempts (context save / restore) does
@@ -107,6 +109,12 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 // running gives up (~2-6 s), or one outliving FLOW_WALL
 #define FLOW_SPINS (1u << 22)
 #define FLOW_WALL 3000000000ull  // 30 s of the 100 MHz real-time counter
+// the launch's spin bound (av1r_set_flow_spins: a test forces the timeout path with 1)
+DEV uint32_t flow_spin_limit(const uint32_t* ctl)
+{
+    const uint32_t v = __hip_atomic_load(ctl + FLOW_SPINLIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v ? v : FLOW_SPINS;
+}
 
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
 DEV int clip1(int v) { return CLIP3(0, 255, v); }

@@ -37,7 +37,7 @@ void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
 #ifdef AV1R_FLOW_DEBUG
-uint32_t flow_debug_overlaps();
+uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset);
 #endif
 int flow_grid(int device, int maxPer);
 void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
@@ -50,6 +50,7 @@ struct FrameBuf {
     uint8_t* base = nullptr;
     size_t bytes = 0;
     int refcnt = 0;
+    uint64_t seq = 0;  // the owning context's frame sequence number of the launch that wrote it
     DevFrame d;
 };
 
@@ -60,7 +61,6 @@ struct Upload {
     hipEvent_t done = nullptr;  // all work that reads this upload has finished
     hipEvent_t ready = nullptr; // meta: the upload (on the context's copy stream) has landed
     bool pending = false;
-    uint32_t* err = nullptr;    // meta: the launch's k_flow error word (pinned host memory the kernel writes)
 };
 
 struct Level {
@@ -176,7 +176,66 @@ struct av1r_ctx {
     int schedule = -1;  // av1r_set_schedule: -1 default (AV1R_FLOW), 0 level launches, 1 k_flow
     int16_t* resDev = nullptr;  // k_flow mode: the frame's residual tiles (k_resid)
     size_t resCap = 0;
+    uint32_t flowSpins = 0;     // av1r_set_flow_spins (0: FLOW_SPINS)
+    // device-error bookkeeping (under g_recMu): frame sequence numbers of this context's
+    // frames whose launch reported a k_flow timeout, those not yet returned by
+    // av1r_synchronize, and the sequence numbers of key frames refreshing every slot (a
+    // failure taints every later frame of the stream up to the next such key frame)
+    uint64_t seq = 0, lastSeq = 0;
+    std::vector<uint64_t> failed, keySeqs;
+    size_t failedReported = 0;
 };
+
+// A launch that ran k_flow: its pinned error word (the kernel writes it when a wait
+// times out), an event after the launch's last kernel, and the frames it produced as
+// (context, frame sequence number).  When the event has completed the record is
+// harvested: a set error word marks those frames failed in EVERY member context.
+struct LaunchRec {
+    uint32_t* err = nullptr;
+    hipEvent_t done = nullptr;
+    std::vector<std::pair<av1r_ctx*, uint64_t>> members;
+};
+static std::mutex g_recMu;
+static std::vector<LaunchRec*> g_recPending, g_recFree;
+
+// collect completed launch records (wait: block on each pending one first)
+static void harvest(bool wait)
+{
+    std::lock_guard<std::mutex> lock(g_recMu);
+    for (size_t i = 0; i < g_recPending.size();) {
+        LaunchRec* r = g_recPending[i];
+        if (wait) (void)hipEventSynchronize(r->done);
+        if (hipEventQuery(r->done) != hipSuccess) {
+            i++;
+            continue;
+        }
+        if (const uint32_t e = *r->err) {
+            for (auto& m : r->members) {
+                m.first->failed.push_back(m.second);
+                m.first->err = e == 2 ? "k_flow: an edge granule wait timed out (frame output invalid)"
+                                      : "k_flow: a dependency wait timed out (frame output invalid)";
+            }
+            *r->err = 0;
+        }
+        r->members.clear();
+        g_recFree.push_back(r);
+        g_recPending[i] = g_recPending.back();
+        g_recPending.pop_back();
+    }
+}
+
+// whether frame `seq` of context c is corrupt: some failed frame b <= seq of its stream
+// with no key frame refreshing every slot in (b, seq]  (caller holds g_recMu)
+static bool frame_failed(const av1r_ctx* c, uint64_t seq)
+{
+    for (uint64_t b : c->failed) {
+        if (b > seq) continue;
+        bool healed = false;
+        for (uint64_t k : c->keySeqs) healed |= k > b && k <= seq;
+        if (!healed) return true;
+    }
+    return false;
+}
 
 // Lazy cross-stream ordering of batch members (av1r_decode_prepared_batch): called before
 // anything enqueues on, or waits for, the context's own stream.
@@ -576,51 +635,55 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         if (v->size() < nl) v->resize(nl);
     c->items.clear();
     c->levels.assign(nl, Level());
+    size_t nItems = 0;
+    for (size_t l = 0; l < nl; l++) nItems += c->lvP[l].size() + c->lvB[l].size() + c->lvT[l].size();
+    c->items.reserve(nItems);
+    // stable partition of a level's list by a small class key (counting sort, one pass)
+    std::vector<uint32_t> bk[4];
+    auto partition = [&](std::vector<uint32_t>& v, int nk, uint32_t* counts, auto key) {
+        for (int q = 0; q < nk; q++) bk[q].clear();
+        for (uint32_t x : v) bk[key(x)].push_back(x);
+        size_t o = 0;
+        for (int q = 0; q < nk; q++) {
+            counts[q] = (uint32_t)bk[q].size();
+            std::copy(bk[q].begin(), bk[q].end(), v.begin() + o);
+            o += bk[q].size();
+        }
+    };
+    // inter tiles: [the rest][medium plain][small plain].  Plain = simple motion, no mask
+    // compound, no intra block copy, no global warp: what k_inter_m / k_inter_s predict
+    // (their frames' references must also be unscaled, checked per launch); small = both
+    // luma sides <= 8, medium = both <= 16
+    auto plainClass = [&](uint32_t code) {  // 0 k_inter, 1 medium, 2 small
+        const av1r_block& blk = b->blocks[AV1R_ITEM_INDEX(code) >> 4];
+        const int bs = blk.mi_size;
+        if (av1r_num4x4w[bs] > 4 || av1r_num4x4h[bs] > 4) return 0;
+        if (blk.motion_mode != AV1R_SIMPLE_TRANSLATION || (blk.flags & AV1R_BLK_INTRABC)) return 0;
+        const av1r_mi& info = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col];
+        if (info.ref_frame[1] > AV1R_INTRA_FRAME && blk.compound_type != AV1R_COMPOUND_AVERAGE &&
+            blk.compound_type != AV1R_COMPOUND_DISTANCE)
+            return 0;
+        if (blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV)
+            for (int r = 0; r < 2; r++)
+                if (info.ref_frame[r] > AV1R_INTRA_FRAME && h->gm_type[info.ref_frame[r] & 7] > AV1R_GM_TRANSLATION)
+                    return 0;
+        return av1r_num4x4w[bs] <= 2 && av1r_num4x4h[bs] <= 2 ? 2 : 1;
+    };
+    // TB lists: [large intra][large inter][small intra][small inter]; large = a side > 16
+    auto tbClass = [&](uint32_t code) {
+        const av1r_tb& t = b->tbs[AV1R_ITEM_INDEX(code)];
+        const bool large = av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
+        return (large ? 0 : 2) + ((b->blocks[t.block].flags & AV1R_BLK_INTER) ? 1 : 0);
+    };
     for (size_t l = 0; l < nl; l++) {
         // order: inter tiles, then k_tb's large items, then its small ones
-        auto large = [&](uint32_t code) {
-            if (AV1R_ITEM_KIND(code) != AV1R_ITEM_TB) return true;
-            const av1r_tb& t = b->tbs[AV1R_ITEM_INDEX(code)];
-            return av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
-        };
-        auto interTb = [&](uint32_t code) { return (b->blocks[b->tbs[AV1R_ITEM_INDEX(code)].block].flags & AV1R_BLK_INTER) != 0; };
-        // inter tiles: [the rest][medium plain][small plain].  Plain = simple motion, no mask
-        // compound, no intra block copy, no global warp: what k_inter_m / k_inter_s predict
-        // (their frames' references must also be unscaled, checked per launch); small = both
-        // luma sides <= 8, medium = both <= 16
-        std::vector<uint32_t>& P = c->lvP[l];
-        auto plainClass = [&](uint32_t code) {  // 0 k_inter, 1 medium, 2 small
-            const av1r_block& blk = b->blocks[AV1R_ITEM_INDEX(code) >> 4];
-            const int bs = blk.mi_size;
-            if (av1r_num4x4w[bs] > 4 || av1r_num4x4h[bs] > 4) return 0;
-            if (blk.motion_mode != AV1R_SIMPLE_TRANSLATION || (blk.flags & AV1R_BLK_INTRABC)) return 0;
-            const av1r_mi& info = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col];
-            if (info.ref_frame[1] > AV1R_INTRA_FRAME && blk.compound_type != AV1R_COMPOUND_AVERAGE &&
-                blk.compound_type != AV1R_COMPOUND_DISTANCE)
-                return 0;
-            if (blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV)
-                for (int r = 0; r < 2; r++)
-                    if (info.ref_frame[r] > AV1R_INTRA_FRAME && h->gm_type[info.ref_frame[r] & 7] > AV1R_GM_TRANSLATION)
-                        return 0;
-            return av1r_num4x4w[bs] <= 2 && av1r_num4x4h[bs] <= 2 ? 2 : 1;
-        };
-        std::stable_sort(P.begin(), P.end(), [&](uint32_t a, uint32_t b2) { return plainClass(a) < plainClass(b2); });
-        for (int pc = 0; pc < 2; pc++)
-            c->levels[l].pl[pc] = (uint32_t)std::count_if(P.begin(), P.end(), [&](uint32_t code) { return plainClass(code) == pc + 1; });
+        uint32_t pc[4] = {}, tc[4] = {};
+        partition(c->lvP[l], 3, pc, plainClass);
+        c->levels[l].pl[0] = pc[1];
+        c->levels[l].pl[1] = pc[2];
         std::vector<uint32_t>& T = c->lvT[l];
-        // [large intra][large inter][small intra][small inter]
-        std::stable_sort(T.begin(), T.end(), [&](uint32_t a, uint32_t b2) {
-            return (large(a) ? 0 : 2) + interTb(a) < (large(b2) ? 0 : 2) + interTb(b2);
-        });
-        uint32_t nLargeT = 0, nLargeIntra = 0, nSmallIntra = 0;
-        for (uint32_t code : T) {
-            if (large(code)) {
-                nLargeT++;
-                nLargeIntra += !interTb(code);
-            } else {
-                nSmallIntra += !interTb(code);
-            }
-        }
+        partition(T, 4, tc, tbClass);
+        const uint32_t nLargeT = tc[0] + tc[1], nLargeIntra = tc[0], nSmallIntra = tc[2];
         c->levels[l].off[0] = (uint32_t)c->items.size();
         c->levels[l].cnt[0] = (uint32_t)c->lvP[l].size();
         c->levels[l].off[1] = c->levels[l].off[0] + c->levels[l].cnt[0];
@@ -803,6 +866,7 @@ struct FrameJob {
     KParams k;
     FrameBuf *R = nullptr, *C = nullptr, *L = nullptr;
     bool scaled = false;  // a reference differs in size from the frame (no k_inter_s tiles)
+    uint64_t seq = 0;     // the context's frame sequence number
 };
 
 // resolve references, allocate the frame's buffers, fill its KParams
@@ -870,6 +934,7 @@ static int job_begin(FrameJob& j)
     }
     j.k.cdef = j.C->d;
     if (j.L) j.k.lrout = j.L->d;
+    j.seq = ++c->seq;
     return AV1R_OK;
 }
 
@@ -879,6 +944,13 @@ static void job_end(FrameJob& j)
     av1r_ctx* c = j.c;
     const av1r_frame_hdr* h = &j.P->hdr;
     FrameBuf* out = j.L ? j.L : j.C;
+    out->seq = j.seq;
+    c->lastSeq = j.seq;
+    if (h->frame_type == 0 && h->refresh_frame_flags == 0xff) {  // KEY_FRAME refreshing every slot
+        std::lock_guard<std::mutex> lock(g_recMu);
+        if (c->failed.empty()) c->keySeqs.clear();
+        c->keySeqs.push_back(j.seq);
+    }
     if (j.L) frame_unref(c, j.C);
     frame_unref(c, j.R);
     if (c->keepStages) {
@@ -914,6 +986,20 @@ struct FlowChain {
     hipEvent_t done = nullptr;
 };
 static FlowChain g_flowChain[64];
+
+// -DAV1R_FLOW_DEBUG: the stream that launched each epoch (av1r_flow_debug classifies the
+// overlapping pairs the kernel records as same-stream or cross-stream)
+#ifdef AV1R_FLOW_DEBUG
+static std::mutex g_epochMu;
+static std::vector<std::pair<uint32_t, hipStream_t>> g_epochLog;
+static void flow_debug_note(uint32_t epoch, hipStream_t st)
+{
+    std::lock_guard<std::mutex> lock(g_epochMu);
+    g_epochLog.emplace_back(epoch, st);
+}
+#else
+static void flow_debug_note(uint32_t, hipStream_t) {}
+#endif
 
 // AV1R_HOST_PROF: host time per phase of launch_jobs, printed when a context is destroyed
 struct HostProf {
@@ -972,16 +1058,24 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         HIPCHK(hipEventSynchronize(M.done));
         if (host_prof()) tp1 = now_us();
         M.pending = false;
-        if (M.err && *M.err) {
-            const uint32_t e = *M.err;
-            *M.err = 0;
-            return fail(c, AV1R_E_DEVICE, "k_flow: a %s wait timed out (output of an earlier batch is invalid)",
-                e == 2 ? "edge granule" : "dependency");
+        harvest(false);  // device errors reach their frames (av1r_get_output / av1r_synchronize)
+    }
+    // the launch's status record (k_flow launches only)
+    LaunchRec* rec = nullptr;
+    if (flow && nGroups) {
+        std::lock_guard<std::mutex> lock(g_recMu);
+        if (!g_recFree.empty()) {
+            rec = g_recFree.back();
+            g_recFree.pop_back();
         }
     }
-    if (!M.err) {
-        HIPCHK(hipHostMalloc(&M.err, 256));
-        *M.err = 0;
+    if (flow && nGroups && !rec) {
+        rec = new LaunchRec;
+        if (hipHostMalloc(&rec->err, 64) != hipSuccess || hipEventCreateWithFlags(&rec->done, hipEventDisableTiming) != hipSuccess) {
+            delete rec;
+            return fail(c, AV1R_E_NOMEM, "launch record");
+        }
+        *rec->err = 0;
     }
     if (M.cap < need) {
         if (M.host) (void)hipHostFree(M.host);
@@ -1040,7 +1134,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         // frames interleaved; {frame << 8 | n, first item}: n = 0 one large item, else
         // 1..4 small items
         memset(M.host + kBytes + tabBytes, 0, FLOW_CTL_BYTES);
-        *reinterpret_cast<uint32_t**>(M.host + kBytes + tabBytes + 4 * FLOW_HOSTERR) = M.err;
+        uint32_t* hctl = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes);
+        *reinterpret_cast<uint32_t**>(hctl + FLOW_HOSTERR) = rec ? rec->err : nullptr;
+        hctl[FLOW_SPINLIM] = lc->flowSpins;
         uint32_t* g = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES);
         for (size_t l = 0; l < nLevels; l++)
             for (int i = 0; i < n; i++) {
@@ -1131,13 +1227,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
             FlowChain& F = g_flowChain[lc->device];
             std::lock_guard<std::mutex> lock(F.m);
-            // Launches from several streams (contexts driven from concurrent threads) are
-            // chained by an event, but grids of different launches were measured resident
-            // together (-DAV1R_FLOW_DEBUG) and then starved each other now and then (a wait
-            // timed out).  Such a launch takes one workgroup per CU, so that several of them
-            // fit the chip side by side, each fully resident: progress whatever the overlap.
-            const bool shared = F.last && F.last != st;
-            const int grid = (int)std::min<size_t>(flow_grid(lc->device, shared ? 1 : 8), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            // Full persistent grid always: k_flow's workgroups take their queues in entry
+            // order, so overlapping grids cannot starve each other (recon.hip, k_flow).
+            const int grid = (int)std::min<size_t>(flow_grid(lc->device, 8), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
@@ -1146,7 +1238,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             hipEvent_t ev = nullptr;
             HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
-            launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, M.err, epoch, grid, trace, st);
+            launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
+            flow_debug_note(epoch, st);
             HIPCHK(hipEventRecord(ev, st));
             if (F.done) (void)hipEventDestroy(F.done);
             F.done = ev;
@@ -1212,6 +1305,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     HIPCHK(hipEventRecord(M.done, st));
     M.pending = true;
     for (auto& j : jobs) job_end(j);
+    if (rec) {
+        HIPCHK(hipEventRecord(rec->done, st));
+        std::lock_guard<std::mutex> lock(g_recMu);
+        for (auto& j : jobs) rec->members.emplace_back(j.c, j.seq);
+        g_recPending.push_back(rec);
+    }
     if (host_prof()) {
         const double tp3 = now_us();
         g_hprof.wait += (tp1 > tp0 ? tp1 : tp0) - tp0;
@@ -1321,7 +1420,6 @@ void av1r_destroy(av1r_ctx* c)
     auto freeUpload = [](Upload& u) {
         if (u.host) (void)hipHostFree(u.host);
         if (u.dev) (void)hipFree(u.dev);
-        if (u.err) (void)hipHostFree(u.err);
         (void)hipEventDestroy(u.done);
         if (u.ready) (void)hipEventDestroy(u.ready);
     };
@@ -1331,9 +1429,13 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipStreamDestroy(c->copyStream);
     if (c->resDev) (void)hipFree(c->resDev);
     if (c->granDev) (void)hipFree(c->granDev);
-#ifdef AV1R_FLOW_DEBUG
-    fprintf(stderr, "av1r: k_flow co-resident entries so far: %u\n", flow_debug_overlaps());
-#endif
+    {  // the context leaves every launch record still pending
+        std::lock_guard<std::mutex> lock(g_recMu);
+        for (LaunchRec* r : g_recPending)
+            r->members.erase(std::remove_if(r->members.begin(), r->members.end(),
+                                 [&](const std::pair<av1r_ctx*, uint64_t>& m) { return m.first == c; }),
+                r->members.end());
+    }
     (void)hipEventDestroy(c->sync);
     (void)hipEventDestroy(c->joinEv);
     if (c->traceDev) (void)hipFree(c->traceDev);
@@ -1583,6 +1685,9 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
     HIPCHK(hipStreamSynchronize(c->stream));
     c->outq.pop_front();
     frame_unref(c, f);
+    harvest(false);
+    std::lock_guard<std::mutex> lock(g_recMu);
+    if (frame_failed(c, f->seq)) return fail(c, AV1R_E_DEVICE, "frame %llu: %s", (unsigned long long)f->seq, c->err.c_str());
     return AV1R_OK;
 }
 
@@ -1594,15 +1699,66 @@ int av1r_read_stage(av1r_ctx* c, int stage, int plane, uint8_t* dst, int ds)
     int rc = copy_plane_d2h(c, c->stage[stage]->d.pl[plane], dst, ds);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
+    harvest(false);
+    std::lock_guard<std::mutex> lock(g_recMu);
+    if (frame_failed(c, c->lastSeq)) return fail(c, AV1R_E_DEVICE, "stage read: %s", c->err.c_str());
     return AV1R_OK;
 }
 
+// Waits for the context's work; AV1R_E_DEVICE once for every failure (a k_flow wait that
+// timed out in a launch holding one of its frames) not reported by an earlier call.
 int av1r_synchronize(av1r_ctx* c)
 {
     if (!c) return AV1R_E_INVALID;
     ctx_join(c);
     HIPCHK(hipStreamSynchronize(c->stream));
+    harvest(false);
+    std::lock_guard<std::mutex> lock(g_recMu);
+    if (c->failed.size() > c->failedReported) {
+        c->failedReported = c->failed.size();
+        return fail(c, AV1R_E_DEVICE, "%s", c->err.c_str());
+    }
     return AV1R_OK;
+}
+
+int av1r_set_flow_spins(av1r_ctx* c, uint32_t spins)
+{
+    if (!c) return AV1R_E_INVALID;
+    c->flowSpins = spins;
+    return AV1R_OK;
+}
+
+int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream)
+{
+#ifdef AV1R_FLOW_DEBUG
+    std::vector<uint32_t> pr(256);
+    const int cnt = (int)flow_debug_overlaps(pr.data(), 256, reset);
+    int cross = 0;
+    std::lock_guard<std::mutex> lock(g_epochMu);
+    auto streamOf = [&](uint32_t slot, uint32_t entering) {  // latest epoch < entering in that slot
+        hipStream_t s = nullptr, es = nullptr;
+        for (auto& e : g_epochLog) {
+            if ((e.first & 0xffff) == (entering & 0xffff)) es = e.second;
+            if ((e.first & 63) == slot && (e.first & 0xffff) != (entering & 0xffff)) s = e.second;
+        }
+        return std::make_pair(s, es);
+    };
+    for (int i = 0; i < std::min(cnt, 256); i++) {
+        auto se = streamOf(pr[i] >> 16, pr[i] & 0xffff);
+        cross += se.first != se.second;
+    }
+    if (pairs)
+        for (int i = 0; i < n && i < 256; i++) pairs[i] = pr[i];
+    if (cross_stream) *cross_stream = cross;
+    if (reset) g_epochLog.clear();
+    return cnt;
+#else
+    (void)pairs;
+    (void)n;
+    (void)reset;
+    (void)cross_stream;
+    return -1;
+#endif
 }
 
 int av1r_set_timing(av1r_ctx* c, int enable)

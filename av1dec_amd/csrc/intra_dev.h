@@ -212,7 +212,7 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
     if ((NT == 64 || t < 64) && nq > 0) {
         const int lane = t & 63;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t spins = 0;
+        uint32_t spins = 0, lim = 0;
         bool dead = false;
         for (int base = 0; base < nq; base += 64) {
             const int q = base + lane;
@@ -247,7 +247,8 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
                 }
                 if (__all(ok)) break;
                 const bool other = __hip_atomic_load(G.ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (other || ++spins > FLOW_SPINS || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
+                if (!lim) lim = flow_spin_limit(G.ctl);
+                if (other || ++spins > lim || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
                     if (lane == 0 && !other) {  // 2: an edge granule wait (1: a dependency flag wait)
                         __hip_atomic_store(G.ctl + FLOW_ERR, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(G.ctl + FLOW_HOSTERR)),

@@ -1557,14 +1557,18 @@ extern "C" __global__ __launch_bounds__(64) void k_inter_m(const KParams* kps, c
 //
 // The host lists the items' groups (one large item, or up to four small ones: the same
 // packing as k_tb) in a topological order: level by level, frames interleaved.  Group g
-// belongs to queue g % 8; workgroup b pulls queue b % 8's next group with one atomic add,
-// so a queue's groups are taken in order.  Every item waits only for items of EARLIER
-// groups (its dependency list, built by the host from the 4x4 units whose pixels it reads:
-// intra edges, CFL luma, the inter-intra prediction), so the earliest unfinished group is
-// either held by a running workgroup whose dependencies are all complete, or is the next
-// group of a queue whose workgroups are all free: the launch always progresses, whatever
-// the residency, as long as each queue has one resident workgroup (grid >= 8, dealt
-// round-robin).
+// belongs to queue g % 8; the k-th workgroup to START serves queue k % 8 and pulls its
+// next group with one atomic add, so a queue's groups are taken in order.  Every item
+// waits only for items of EARLIER groups (its dependency list, built by the host from the
+// 4x4 units whose pixels it reads: intra edges, CFL luma, the inter-intra prediction), so
+// the earliest unfinished group is either held by a running workgroup whose dependencies
+// are all complete, or is the next group of a queue whose workgroups are all free.  A
+// workgroup leaves only when its queue has no group left to hand out, so once 8 of the
+// grid's workgroups have started every queue with work has a resident server: the launch
+// progresses whatever the residency or placement.  Several overlapping k_flow grids (from
+// different streams) cannot starve each other either: they never wait on one another, so
+// while the chip holds >= 8 workgroups of some grid that grid finishes and frees its
+// slots (1280 slots at 5 per CU: up to 160 overlapping grids).
 //
 // Hand-off between items (cdna_hip_programming.md §6 Guideline 16, R1): a producer stores
 // its pixels write-through (stp/stp4<true>: sc1), every storing wave drains them
@@ -1583,7 +1587,7 @@ DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint
     if (nd && (NT == 64 || threadIdx.x < 64)) {
         const int lane = threadIdx.x & 63;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t spins = 0;
+        uint32_t spins = 0, lim = 0;
         for (uint32_t b = 0; b < nd; b += 64) {
             const bool mine = b + lane < nd;
             const uint32_t d = mine ? deps[b + lane] : 0u;
@@ -1591,7 +1595,8 @@ DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint
                 const bool ok = !mine || __hip_atomic_load(done + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
                 if (__all(ok)) break;
                 const bool dead = __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (dead || ++spins > FLOW_SPINS || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
+                if (!lim) lim = flow_spin_limit(ctl);
+                if (dead || ++spins > lim || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
                     if (lane == 0 && !dead) {  // the wave that gave up first reports
                         __hip_atomic_store(ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         // the host's copy (pinned memory, checked when the launch's metadata is reused)
@@ -1685,8 +1690,12 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 #endif
 #ifdef AV1R_FLOW_DEBUG
 // -DAV1R_FLOW_DEBUG: counts workgroup entries that find another launch's k_flow
-// workgroups still running (co-resident grids, which the flow chain should exclude)
-__device__ uint32_t g_flow_active, g_flow_epoch, g_flow_overlap;
+// workgroups still running (co-resident grids, which the flow chain should exclude), and
+// records the first FLOW_DBG_PAIRS (earlier epoch, entering epoch) pairs.  g_flow_active
+// holds, per epoch slot (epoch % 64), that launch's running workgroups, so an entry is an
+// overlap exactly when another slot is non-zero (one atomic per slot, no cross-word race).
+#define FLOW_DBG_PAIRS 256
+__device__ uint32_t g_flow_active[64], g_flow_overlap, g_flow_pairs[FLOW_DBG_PAIRS];
 #endif
 extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
     uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
@@ -1694,22 +1703,37 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
     __shared__ __align__(16) uint8_t smem[kLds];
     __shared__ uint32_t ticket[2];  // double-buffered: a slow wave may still read the old one
-    const uint32_t q = blockIdx.x % FLOW_QUEUES;
-    uint32_t* head = ctl + q * FLOW_LINE;
-#ifdef AV1R_FLOW_DEBUG
+    // The queue a workgroup serves is its ENTRY order, not its blockIdx: the first
+    // FLOW_QUEUES workgroups to start cover every queue wherever the dispatcher put them.
+    // (blockIdx % 8 is also the XCD a workgroup lands on: with queue = blockIdx % 8 every
+    // queue lived on one XCD, and two overlapping grids could each fill an XCD the other
+    // needed -- grid A's queue-q groups waiting for a slot on XCD q held by grid B's spinning
+    // workgroups, and B's the other way round: the cross-stream timeout of round 1.)
+    __shared__ uint32_t qsh;
     if (threadIdx.x == 0) {
-        const uint32_t prev = atomicExch(&g_flow_epoch, epoch);
-        const uint32_t act = atomicAdd(&g_flow_active, 1u);
-        if (prev != epoch && act > 0) atomicAdd(&g_flow_overlap, 1u);
-    }
+        qsh = __hip_atomic_fetch_add(ctl + FLOW_ASSIGN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % FLOW_QUEUES;
+#ifdef AV1R_FLOW_DEBUG
+        atomicAdd(&g_flow_active[epoch & 63], 1u);
+        for (uint32_t e = 1; e < 64; e++) {
+            const uint32_t o = (epoch + e) & 63;
+            if (__hip_atomic_load(&g_flow_active[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                const uint32_t k = atomicAdd(&g_flow_overlap, 1u);
+                if (k < FLOW_DBG_PAIRS) g_flow_pairs[k] = (o << 16) | (epoch & 0xffff);
+                break;
+            }
+        }
 #endif
+    }
+    __syncthreads();
+    const uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
+    uint32_t* head = ctl + q * FLOW_LINE;
     if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     for (uint32_t it = 0;; it ^= 1) {
         const uint32_t g = __builtin_amdgcn_readfirstlane(ticket[it]) * FLOW_QUEUES + q;
         if (g >= nGroups) {
 #ifdef AV1R_FLOW_DEBUG
-            if (threadIdx.x == 0) atomicSub(&g_flow_active, 1u);
+            if (threadIdx.x == 0) atomicSub(&g_flow_active[epoch & 63], 1u);
 #endif
             return;
         }
@@ -1762,11 +1786,20 @@ int flow_grid(int device, int maxPer)
 }
 
 #ifdef AV1R_FLOW_DEBUG
-uint32_t flow_debug_overlaps()
+// overlap count since the last reset; pairs[] (up to n) the (earlier epoch slot << 16 |
+// entering epoch) of the first overlaps; reset = 1 zeroes the counters afterwards
+uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset)
 {
     uint32_t v = 0;
     (void)hipDeviceSynchronize();
     (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_flow_overlap), sizeof(v));
+    if (pairs && n > 0) (void)hipMemcpyFromSymbol(pairs, HIP_SYMBOL(g_flow_pairs), 4 * (n < FLOW_DBG_PAIRS ? n : FLOW_DBG_PAIRS));
+    if (reset) {
+        const uint32_t z[64] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_flow_overlap), z, 4);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_flow_active), z, sizeof(z));
+        (void)hipDeviceSynchronize();
+    }
     return v;
 }
 #endif

@@ -112,6 +112,10 @@ class Decoder:
         self._check(self.l.av1r_last_frame_times(self.c, *[C.byref(x) for x in t]), "av1r_last_frame_times")
         return [x.value for x in t]
 
+    def set_flow_spins(self, spins):
+        """Test hook: polls before a k_flow wait gives up (0 = default; 1 forces timeouts)."""
+        self._check(self.l.av1r_set_flow_spins(self.c, int(spins)), "av1r_set_flow_spins")
+
     def set_schedule(self, mode):
         """1: dataflow kernel k_flow (default), 0: one launch per dependency level."""
         self._check(self.l.av1r_set_schedule(self.c, int(mode)), "av1r_set_schedule")

@@ -104,6 +104,8 @@ def lib():
     l.av1r_check_batch.argtypes = [vp, C.POINTER(i), C.c_char_p, i]
     l.av1r_sizeof.argtypes = [i]
     l.av1r_sizeof.restype = C.c_size_t
+    l.av1r_set_flow_spins.argtypes = [vp, C.c_uint32]
+    l.av1r_flow_debug.argtypes = [C.POINTER(C.c_uint32), i, i, C.POINTER(i)]
     _lib = l
     return l
 
@@ -115,5 +117,5 @@ EXPORTS = [
     "av1r_set_keep_stages", "av1r_last_frame_stats", "av1r_last_error", "av1r_sizeof",
     "av1r_check_batch", "av1r_prepare", "av1r_decode_prepared", "av1r_release_prepared",
     "av1r_set_discard_output", "av1r_stage_times", "av1r_decode_prepared_batch", "av1r_recon_kernel_times",
-    "av1r_set_schedule",
+    "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug",
 ]

@@ -85,6 +85,40 @@ def aggregate_fps(world, steps, elapsed):
     return world * steps / elapsed
 
 
+def gop_offsets(S, F):
+    """Stream j starts j*F/S frames into its GOP: independent streams are not in phase, so
+    any window of steps holds its share of key frames (S/F per step)."""
+    return [j * F // S for j in range(S)]
+
+
+class StreamSet:
+    """S streams of prepared (HBM-resident) frames, each cycling its own GOP from its own
+    phase.  One step = the next frame of every stream in shared launches
+    (av1r_decode_prepared_batch).  A stream always decodes its frames in order from its key
+    frame (frame 0 refreshes every slot, so cycling the GOP is a valid stream)."""
+
+    def __init__(self, decs, handles, F):
+        self.decs, self.handles, self.F = decs, handles, F
+        self.pos = [0] * len(decs)
+
+    def stagger(self):
+        """Bring stream j alone to frame j*F/S (untimed setup)."""
+        from av1dec_amd import Decoder  # noqa: F401
+        for j, off in enumerate(gop_offsets(len(self.decs), self.F)):
+            while self.pos[j] < off:
+                self.decs[j].decode_prepared(self.handles[j][self.pos[j] % self.F])
+                self.pos[j] += 1
+
+    def frames(self):
+        """(stream, frame index) decoded by the next step."""
+        return [(j, p % self.F) for j, p in enumerate(self.pos)]
+
+    def step(self):
+        from av1dec_amd import Decoder
+        Decoder.decode_prepared_batch(self.decs, [hs[p % self.F] for hs, p in zip(self.handles, self.pos)])
+        self.pos = [p + 1 for p in self.pos]
+
+
 def cpu_baseline(frames, budget_s):
     """The C oracle (reference algorithm restated, single-threaded) on the first frames."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -141,51 +175,54 @@ def main():
         d.set_discard_output(True)
     handles = [[d.prepare(f) for f in fr] for d, fr in zip(decs, streams)]
     F = args.frames
-
-    def step(t):
-        Decoder.decode_prepared_batch(decs, [hs[t % F] for hs in handles])
+    ss = StreamSet(decs, handles, F)
 
     def sync():
         for d in decs:
             d.synchronize()
 
-    # priming pass (setup, untimed): every prepared frame once, so that the timed region
-    # does not see first-touch / clock ramp effects of a freshly started process
-    t_prime = time.perf_counter()
-    for t in range(F):
-        step(t)
+    # setup (untimed): stream j is brought to its own GOP phase, then a priming pass of
+    # whole GOPs (first-touch / clock ramp), then the warmup steps
+    ss.stagger()
     sync()
-    while time.perf_counter() - t_prime < 1.0:
-        for t in range(F):
-            step(t)
+    t_prime = time.perf_counter()
+    while True:
+        for _ in range(F):
+            ss.step()
         sync()
-    for t in range(args.warmup):
-        step(t)
+        if time.perf_counter() - t_prime >= 1.0:
+            break
+    for _ in range(args.warmup):
+        ss.step()
     sync()
     if dist:
         dist.barrier()
+    timed = []  # (stream, frame) of every frame in the timed region
     t0 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
-        step(t)
+    for _ in range(args.steps):
+        timed += ss.frames()
+        ss.step()
     sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     fps = aggregate_fps(world, args.steps * S, elapsed)
+    n_key = sum(1 for j, t in timed if streams[j][t].hdr.frame_type == 0)
 
     # per-stage device time over the same batches (HIP events on the launch stream)
     lead = decs[0]
     lead.l.av1r_set_timing(lead.c, 1)
-    for t in range(args.warmup, args.warmup + args.steps):
-        step(t)
+    timed2 = []
+    for _ in range(args.steps):
+        timed2 += ss.frames()
+        ss.step()
     ktot, _ = lead.recon_kernel_times()
     totals, nfr = lead.stage_times()
     lead.l.av1r_set_timing(lead.c, 0)
     names = ["recon", "lf", "cdef", "lr"]
     per_frame_ms = {n: totals[k] / max(nfr, 1) for k, n in enumerate(names)}
     sb = {n: 0.0 for n in names}
-    for t in range(args.warmup, args.warmup + args.steps):
-        for fr in streams:
-            for n, v in stage_bytes(fr[t % F]).items():
-                sb[n] += v / (args.steps * S)
+    for j, t in timed2:
+        for n, v in stage_bytes(streams[j][t]).items():
+            sb[n] += v / len(timed2)
     dominant = max(names, key=lambda n: per_frame_ms[n])
     achieved = sb[dominant] / (per_frame_ms[dominant] * 1e-3) / 1e9
     traffic = None
@@ -200,7 +237,8 @@ def main():
     # one stream alone (latency-bound) on the same frames
     sync()
     t1 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
+    p0 = ss.pos[0]
+    for t in range(p0, p0 + args.steps):
         lead.decode_prepared(handles[0][t % F])
     lead.synchronize()
     single_fps = args.steps / (time.perf_counter() - t1)
@@ -215,23 +253,19 @@ def main():
     levels, _ = lead.last_frame_stats()
 
     # the same with every stream fed by its own host thread (contexts are independent and
-    # may be driven concurrently: SURVEY.md §8b threading); frames/s over all streams.  Each
-    # context's first host-batch frame is issued serially first (concurrent
-    # threads and the flow chain); a failure here is reported in the line, never fatal to it
+    # may be driven concurrently: SURVEY.md §8b threading); frames/s over all streams.  A
+    # failure here is reported in the line, never fatal to it
     errs = []
 
     def feed(d, fr):
         try:
-            for i in range(1, n_host + 1):
+            for i in range(n_host):
                 d.decode_frame(fr[i % len(fr)])
             d.synchronize()
         except Exception as e:
             errs.append(str(e))
     host_mt_fps = None
     try:
-        for d, fr in zip(decs, streams):
-            d.decode_frame(fr[0])
-        sync()
         th = [threading.Thread(target=feed, args=(d, fr)) for d, fr in zip(decs, streams)]
         t1 = time.perf_counter()
         for x in th:
@@ -270,9 +304,11 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": f"{S} independent synthetic {W}x{H} 8-bit 4:2:0 inter streams per GPU "
-                                   f"(BASELINE configs[4] share; each {F} frames: 1 key + {F - 1} inter, cycled; "
-                                   f"tiles {tiles[0]}x{tiles[1]}; seeds {seed:#x}+stream), one frame of every "
-                                   f"stream per step in shared launches",
+                                   f"(BASELINE configs[4] share; each {F} frames: 1 key + {F - 1} inter, cycled, "
+                                   f"stream j offset by j*{F}/{S} frames; tiles {tiles[0]}x{tiles[1]}; seeds "
+                                   f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
+                                   f"timed frames: {args.steps * S} of which {n_key} key",
+                       "timed_key_frames": n_key,
                        "streams_per_gpu": S, "frames_per_step": S,
                        "parallelism": f"stream-per-GPU x{world}"},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),

@@ -262,6 +262,15 @@ int av1r_set_keep_stages(av1r_ctx* ctx, int keep);
 /* Dependency levels (recon launches) and uploaded batch bytes of the last frame. */
 int av1r_last_frame_stats(av1r_ctx* ctx, int* levels, uint64_t* upload_bytes);
 const char* av1r_last_error(av1r_ctx* ctx);
+/* Test / diagnosis hooks.  av1r_set_flow_spins: polls after which a k_flow wait of this
+ * context's launches gives up (0 = the default bound); 1 forces the timeout path, whose
+ * frames must then surface as AV1R_E_DEVICE from av1r_get_output / av1r_synchronize.
+ * av1r_flow_debug: in a -DAV1R_FLOW_DEBUG build, the number of k_flow workgroup entries
+ * that found another launch's k_flow still running, the first n recorded pairs
+ * (earlier epoch slot << 16 | entering epoch) and how many of those pairs were launched
+ * from different streams; -1 in a normal build. */
+int av1r_set_flow_spins(av1r_ctx* ctx, uint32_t spins);
+int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);

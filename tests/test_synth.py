@@ -75,8 +75,11 @@ def test_gpu_synth_1080p():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)
 def test_gpu_synth_4k_tiles():
-    assert compare_gpu_oracle(pysynth.stream(3840, 2160, 2, 0x5EED0002, tiles=(4, 2)), stages=False) == 2
+    """BASELINE configs[3]: 3840x2160, 4x2 uniform tiles, every stage of 4 frames (key + 3
+    inter) bit-exact with the oracle."""
+    assert compare_gpu_oracle(pysynth.stream(3840, 2160, 4, 0x5EED0002, tiles=(4, 2)), stages=True) == 4
 
 
 @pytest.mark.gpu
@@ -150,20 +153,15 @@ def test_gpu_threaded_contexts_match_oracle():
     upload and launches run concurrently; k_flow launches share the device's flow chain):
     every stream stays bit-exact."""
     import threading
-    nfr = 3
-    dims = [(640, 360), (352, 288), (640, 360), (416, 240)]
+    nfr = 4
+    dims = [(640, 360), (352, 288), (640, 360), (416, 240), (1280, 720), (640, 360), (352, 288), (704, 576)]
     streams = [pysynth.stream(w, h, nfr, 400 + i) for i, (w, h) in enumerate(dims)]
     decs = [Decoder(0, keep_stages=False) for _ in streams]
     errs = []
-    # each context's first frame serially (DESIGN.md §7: concurrent threads and the flow chain;
-    # a rare k_flow wait timeout there before multi-stream launches took small grids)
-    for d, s in zip(decs, streams):
-        d.decode_frame(s[0])
-        d.synchronize()
 
-    def feed(d, s):
+    def feed(d, s):  # from the very first frame: key frames of all threads overlap
         try:
-            for f in s[1:]:
+            for f in s:
                 d.decode_frame(f)
             d.synchronize()
         except Exception as e:
@@ -240,3 +238,91 @@ def test_gpu_level_schedule_synth_1080p():
             for p, (a, b) in enumerate(zip(d.read_stage(st), o.read_stage(st))):
                 assert (a == b).all(), f"frame {i} stage {st} plane {p}"
     d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_flow_timeout_surfaces_as_device_error():
+    """A k_flow wait that gives up (forced: one poll allowed) must never hand out its frame
+    as AV1R_OK: get_output / synchronize report AV1R_E_DEVICE for every frame of the stream
+    from the failed launch on (they may reference it), for every context of the batch."""
+    from av1dec_amd.decoder import BackendError
+    frames = [pysynth.stream(640, 360, 3, 0x5EED0099 + i) for i in range(2)]
+    decs = [Decoder(0, keep_stages=False) for _ in frames]
+    decs[0].set_flow_spins(1)  # the batch launches on decs[0]: its bound applies to both
+    handles = [[d.prepare(f) for f in s] for d, s in zip(decs, frames)]
+    for t in range(3):
+        Decoder.decode_prepared_batch(decs, [h[t] for h in handles])
+    for d in decs:
+        with pytest.raises(BackendError, match=r"\(-3\)"):
+            d.synchronize()
+        d.synchronize()  # reported once
+        n = 0
+        while d.output_pending():
+            with pytest.raises(BackendError, match=r"\(-3\)"):
+                d.get_output()
+            n += 1
+        assert n == 3
+    # the same stream with the default bound decodes bit-exact again from its key frame
+    decs[0].set_flow_spins(0)
+    for t in range(3):
+        Decoder.decode_prepared_batch(decs, [h[t] for h in handles])
+    o = pyoracle.Oracle(keep_stages=False)
+    for f in frames[0]:
+        o.decode_frame(f)
+    while o.output_pending():
+        for x, y in zip(decs[0].get_output(), o.get_output()):
+            assert (x == y).all()
+    for d, hs in zip(decs, handles):
+        for hd in hs:
+            d.release_prepared(hd)
+        d.close()
+
+
+def _oracle_md5s(frames):
+    o = pyoracle.Oracle(keep_stages=False)
+    out = []
+    for f in frames:
+        o.decode_frame(f)
+        while o.output_pending():
+            out.append(b"".join(hashlib.md5(p.tobytes()).digest() for p in o.get_output()))
+    o.close()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gpu_bench_workload_matches_oracle():
+    """The exact workload bench.py times: 8 synthetic 1080p streams with the bench's seeds
+    through av1r_decode_prepared_batch, each stream offset to its own GOP phase, one whole
+    GOP (key frame included) per stream -- every output frame bit-exact with the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    import bench
+    S, F = 8, 60
+    W, H, tiles, seed = bench.CONFIGS["1080p"]
+    with ThreadPoolExecutor(8) as ex:
+        streams = list(ex.map(lambda j: pysynth.stream(W, H, F, bench.stream_seed(seed, j), sb128=True, tiles=tiles),
+                              range(S)))
+        ref = ex.submit(lambda: list(ex.map(_oracle_md5s, streams)))
+        decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+        handles = [[d.prepare(f) for f in fr] for d, fr in zip(decs, streams)]
+        ss = bench.StreamSet(decs, handles, F)
+        ss.stagger()
+        got = [[] for _ in range(S)]
+        keys = 0
+        for _ in range(F):
+            keys += sum(1 for j, t in ss.frames() if t == 0)
+            ss.step()
+            for j, d in enumerate(decs):
+                while d.output_pending():
+                    got[j].append(b"".join(hashlib.md5(p.tobytes()).digest() for p in d.get_output()))
+        ref = ref.result()
+    assert keys >= S - 1  # the timed-style window holds key frames
+    for j in range(S):
+        off = bench.gop_offsets(S, F)[j]
+        assert len(got[j]) == off + F
+        for k, m in enumerate(got[j]):
+            assert m == ref[j][k % F], f"stream {j} output {k} (frame {k % F})"
+    for d, hs in zip(decs, handles):
+        for hd in hs:
+            d.release_prepared(hd)
+        d.close()

@@ -9,7 +9,7 @@ from av1dec_amd import Decoder
 S, N, REP = 8, 24, int(sys.argv[1]) if len(sys.argv) > 1 else 5
 streams = [pysynth.stream(1920, 1080, N, 0x5EED1000 + i) for i in range(S)]
 fails = 0
-if os.environ.get("PREWARM"):  # every context's buffers allocated before the threaded reps
+if os.environ.get("PREWARM"):  # (round 1 workaround probe; no longer needed)  # every context's buffers allocated before the threaded reps
     keep = [Decoder(0, keep_stages=False) for _ in range(S)]
     for d, fr in zip(keep, streams):
         d.decode_frame(fr[0]); d.synchronize()
@@ -33,7 +33,12 @@ for rep in range(REP):
     for x in th: x.join()
     dt = time.perf_counter() - t
     fails += bool(errs)
-    print(f"gran={os.environ.get('AV1R_GRAN', '1')} rep {rep}: {dt:.2f} s, errors {len(errs)} {errs[:1]}", flush=True)
+    import ctypes as C
+    from av1dec_amd import native
+    pairs, cross = (C.c_uint32 * 8)(), C.c_int()
+    ov = native.lib().av1r_flow_debug(pairs, 8, 1, C.byref(cross))  # -1: not a -DAV1R_FLOW_DEBUG build
+    print(f"gran={os.environ.get('AV1R_GRAN', '1')} rep {rep}: {dt:.2f} s, errors {len(errs)} {errs[:1]}; "
+          f"k_flow overlapping entries {ov} (cross-stream pairs {cross.value}) {[hex(x) for x in pairs][:4]}", flush=True)
     for d in decs:
         try: d.close()
         except Exception as e: print("close:", e)
