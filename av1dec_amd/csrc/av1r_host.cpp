@@ -88,10 +88,23 @@ struct Prepared {
     const WorkItem* dItems = nullptr;
     std::vector<Level> levels;
     bool flowOk = false;  // k_flow can run it: no inter tile after level 0 (intra block copy)
+    bool levelsOk = true; // the level launches can run it (false: a flow-only schedule)
     uint32_t nResidS = 0, nResidL = 0;  // k_resid workgroups (16 TBs / 1 TB each)
     size_t resElems = 0;                // int16 residual tiles of the frame
     bool usedRef[8] = {};
     uint64_t bytes = 0;
+    bool offsets = false;  // packed in host memory: base pointers are offsets into the upload
+};
+
+// A frame validated, scheduled and packed into (pinned) host memory by av1r_pack, on any
+// thread, ahead of its launch; av1r_decode_packed_batch uploads and decodes it.
+struct av1r_packed {
+    Prepared P;
+    uint8_t* host = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    hipEvent_t copied = nullptr;  // the upload of this buffer (its host memory is in use until then)
+    bool copyPending = false;
 };
 
 struct av1r_ctx {
@@ -104,6 +117,10 @@ struct av1r_ctx {
     bool keepStages = true;
     Upload up[2];
     int upIdx = 0;
+    static constexpr int kPackRing = 3;  // device slots of packed uploads (av1r_decode_packed_batch)
+    Upload pk[kPackRing];
+    int pkIdx = 0;
+    hipEvent_t pkReady = nullptr;  // the packed uploads of a batch (lead's copy stream) have landed
     // per-launch metadata (KParams, tables, flow groups): a ring, uploaded on a copy stream
     // of its own so that the copy of batch N + 1 overlaps the kernels of batch N
     static constexpr int kMetaRing = 3;
@@ -135,6 +152,8 @@ struct av1r_ctx {
     std::vector<int32_t> nodeDeps, nodeOfTb, nodeOfBlk, nodePos;
     std::vector<uint32_t> deps;
     bool flowOk = false;
+    bool levelsOk = true;  // the level schedule was built too (not a flow-only schedule)
+    bool usedRef[8] = {};  // validate(): references the mode-info grid uses
     // k_flow edge granules (KParams::gran_h / gran_v): per 4x4 unit whether it is on the
     // bottom row / right column of its owner (the units whose granules the owner stores);
     // per node 12 mask words (4 per plane: the above and left runs' units written by an
@@ -237,6 +256,10 @@ static bool frame_failed(const av1r_ctx* c, uint64_t seq)
     return false;
 }
 
+// live contexts (a destroyed batch lead must not stay another context's joinLead)
+static std::mutex g_ctxMu;
+static std::vector<av1r_ctx*> g_ctxs;
+
 // Lazy cross-stream ordering of batch members (av1r_decode_prepared_batch): called before
 // anything enqueues on, or waits for, the context's own stream.
 static void ctx_join(av1r_ctx* c)
@@ -328,19 +351,28 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
     for (int i = 0; i < h->cdef_rows * h->cdef_cols; i++)
         if (b->cdef_idx[i] < -1 || b->cdef_idx[i] > 7) return fail(c, AV1R_E_INVALID, "cdef_idx out of range");
     const int aw4 = h->mi_stride, ah4 = h->mi_rows_alloc;
-    // mode info: sizes, tx sizes, refs (and the slots they resolve to)
-    bool usedRef[8] = {};
+    // mode info: sizes, tx sizes, refs (and the slots they resolve to).  One branch-free
+    // pass accumulating the violations; the slow pass names the first one
+    bool* usedRef = c->usedRef;
+    memset(c->usedRef, 0, sizeof(c->usedRef));
+    uint32_t bad = 0, refs = 0;
     for (int i = 0; i < aw4 * ah4; i++) {
+        const av1r_mi& m = b->mi[i];
+        bad |= (m.mi_size >= AV1R_BLOCK_SIZES) | (m.lf_tx[0] >= AV1R_TX_SIZES) | (m.lf_tx[1] >= AV1R_TX_SIZES) |
+               (m.lf_tx[2] >= AV1R_TX_SIZES) | ((uint8_t)(m.ref_frame[0] + 1) > 8) | ((uint8_t)(m.ref_frame[1] + 1) > 8) |
+               ((m.filt & 15) > 3) | ((m.filt >> 4) > 3);
+        refs |= (1u << ((m.ref_frame[0] + 1) & 15)) | (1u << ((m.ref_frame[1] + 1) & 15));
+    }
+    for (int i = 0; bad && i < aw4 * ah4; i++) {
         const av1r_mi& m = b->mi[i];
         if (m.mi_size >= AV1R_BLOCK_SIZES) return fail(c, AV1R_E_INVALID, "mi_size");
         for (int p = 0; p < 3; p++)
             if (m.lf_tx[p] >= AV1R_TX_SIZES) return fail(c, AV1R_E_INVALID, "lf tx size");
-        for (int l = 0; l < 2; l++) {
+        for (int l = 0; l < 2; l++)
             if (m.ref_frame[l] < -1 || m.ref_frame[l] > 7) return fail(c, AV1R_E_INVALID, "ref_frame");
-            if (m.ref_frame[l] > 0) usedRef[m.ref_frame[l]] = true;
-        }
         if ((m.filt & 15) > 3 || (m.filt >> 4) > 3) return fail(c, AV1R_E_INVALID, "interp filter");
     }
+    for (int r = 1; r < 8; r++) usedRef[r] = (refs >> (r + 1)) & 1;
     for (int r = 1; r < 8 && !c->skipSlotCheck; r++) {
         if (!usedRef[r]) continue;
         int slot = h->ref_frame_idx[r - 1];
@@ -384,9 +416,11 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
         if (t.x + av1r_tx_w[t.tx_size] > ((aw4 * 4) >> sub) + 64 || t.y + av1r_tx_h[t.tx_size] > ((ah4 * 4) >> sub) + 64)
             return fail(c, AV1R_E_INVALID, "tb %u outside the frame", i);
         if ((uint64_t)t.coef_off + t.coef_cnt > b->n_coefs) return fail(c, AV1R_E_INVALID, "tb %u coefficients", i);
-        int tw = std::min<int>(av1r_tx_w[t.tx_size], 32), th = std::min<int>(av1r_tx_h[t.tx_size], 32);
-        for (int q = 0; q < t.coef_cnt; q++)
-            if (AV1R_COEF_POS(b->coefs[t.coef_off + q]) >= tw * th) return fail(c, AV1R_E_INVALID, "tb %u coefficient position", i);
+        const uint32_t area = (uint32_t)std::min<int>(av1r_tx_w[t.tx_size], 32) * std::min<int>(av1r_tx_h[t.tx_size], 32);
+        uint32_t posBad = 0;
+        const uint32_t* cf = b->coefs + t.coef_off;
+        for (int q = 0; q < t.coef_cnt; q++) posBad |= AV1R_COEF_POS(cf[q]) >= (int)area;
+        if (posBad) return fail(c, AV1R_E_INVALID, "tb %u coefficient position", i);
         const av1r_block& k = b->blocks[t.block];
         if (!(k.flags & AV1R_BLK_INTER) && (t.plane ? k.palette_size_uv : k.palette_size_y)) {
             const uint8_t* ph = b->palette + k.palette_off;
@@ -414,9 +448,16 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
 // ------------------------------------------------------------------------------------
 // dependency levels
 // ------------------------------------------------------------------------------------
-static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true)
+// flowOnly: the frame will run on k_flow (av1r_pack; no intra block copy), so inter TBs
+// outside inter-intra blocks -- finished by k_resid before k_flow -- get no node, item or
+// level: only the level launches need them.  c->levelsOk says whether the level schedule
+// was built too.
+static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
 {
     const av1r_frame_hdr* h = b->hdr;
+    if (flowOnly)
+        for (uint32_t i = 0; i < b->n_blocks && flowOnly; i++) flowOnly = !(b->blocks[i].flags & AV1R_BLK_INTRABC);
+    c->levelsOk = !flowOnly;
     for (int p = 0; p < 3; p++) {
         int sub = p ? 1 : 0;
         c->mapW[p] = (((h->mi_stride * 4) >> sub) + 64) / 4;
@@ -591,7 +632,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             const int w = av1r_tx_w[t.tx_size], hh = av1r_tx_h[t.tx_size];
             int lv;
             if (inter) {
-                if (!t.coef_cnt) continue;  // prediction only: nothing to add
+                if (!t.coef_cnt || flowOnly) continue;  // prediction only: nothing to add
                 lv = blkLevel + 1;
                 // the prediction it adds to: the inter tile (preceding launch) or the blend
                 if (c->nodeOfBlk[bi] >= 0) dl.push_back(c->nodeOfBlk[bi]);
@@ -627,7 +668,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     static const bool granDbg = getenv("AV1R_GRAN_DEBUG") != nullptr;
     if (granDbg) fprintf(stderr, "av1r: granules %s (frame %dx%d)\n", c->granOk ? "on" : "off", h->frame_width, h->frame_height);
     if (c->granOk != (granEnv && allowGran)) {  // a unit without its granule: dependency flags throughout
-        build_schedule(c, b, false);
+        build_schedule(c, b, false, flowOnly);
         return;
     }
     const size_t nl = (size_t)(globalMax + 1);
@@ -784,6 +825,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->items[pos].pub = 1;
         }
     }
+    if (flowOnly && !c->flowOk) build_schedule(c, b, allowGran, false);  // k_flow cannot take it: levels too
 }
 
 // ------------------------------------------------------------------------------------
@@ -848,10 +890,8 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     P.hdr = *h;
     P.levels = c->levels;
     P.bytes = off;
-    memset(P.usedRef, 0, sizeof(P.usedRef));
-    for (int i = 0; i < h->mi_stride * h->mi_rows_alloc; i++)
-        for (int l = 0; l < 2; l++)
-            if (b->mi[i].ref_frame[l] > 0) P.usedRef[b->mi[i].ref_frame[l]] = true;
+    memcpy(P.usedRef, c->usedRef, sizeof(P.usedRef));
+    P.levelsOk = c->levelsOk;
     return AV1R_OK;
 }
 
@@ -867,6 +907,7 @@ struct FrameJob {
     FrameBuf *R = nullptr, *C = nullptr, *L = nullptr;
     bool scaled = false;  // a reference differs in size from the frame (no k_inter_s tiles)
     uint64_t seq = 0;     // the context's frame sequence number
+    uint8_t* dev = nullptr;  // P->offsets: the device copy of the packed buffer
 };
 
 // resolve references, allocate the frame's buffers, fill its KParams
@@ -883,6 +924,13 @@ static int job_begin(FrameJob& j)
     }
     j.k = P.base;
     j.k.items = P.dItems;
+    if (P.offsets) {  // a packed frame: its pointers are offsets into the uploaded buffer
+        auto rb = [&](auto& ptr) {
+            ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
+        };
+        rb(j.k.hdr), rb(j.k.mi), rb(j.k.blocks), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
+        rb(j.k.lr), rb(j.k.items), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
+    }
     for (int s = 0; s < 8; s++)
         if (c->slots[s]) j.k.ref[s] = c->slots[s]->d;
     j.scaled = false;
@@ -1023,6 +1071,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     ctx_join(lc);
     hipStream_t st = lc->stream;
     int rc;
+    // the thread's sticky HIP error may hold the status of an unrelated earlier call (an
+    // event query of another launch's record): only this launch's kernels are checked below
+    (void)hipGetLastError();
     size_t nLevels = 0;
     int maxUnits = 0, maxMiCols = 0, maxMiRows = 0, maxW = 0, maxH = 0;
     bool anyLr = false;
@@ -1045,9 +1096,15 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
     static const bool flowEnv = !getenv("AV1R_FLOW") || atoi(getenv("AV1R_FLOW")) != 0;
     bool flow = lc->schedule >= 0 ? lc->schedule == 1 : flowEnv;
+    bool allFlow = true, mustFlow = false;  // flow-only schedules (av1r_pack) run on k_flow
+    for (auto& j : jobs) {
+        allFlow &= j.P->flowOk;
+        mustFlow |= !j.P->levelsOk;
+    }
+    if (mustFlow && !allFlow) return fail(c, AV1R_E_INVALID, "a flow-only frame batched with a level-schedule frame");
+    flow = (flow || mustFlow) && allFlow;
     size_t nGroups = 0;
     for (auto& j : jobs) {
-        flow &= j.P->flowOk;
         for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
     }
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
@@ -1384,6 +1441,8 @@ int av1r_create(int device, av1r_ctx** out)
         return AV1R_E_DEVICE;
     }
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
+    for (auto& u : c->pk) (void)hipEventCreateWithFlags(&u.done, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->pkReady, hipEventDisableTiming);
     for (auto& m : c->meta) {
         (void)hipEventCreateWithFlags(&m.done, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&m.ready, hipEventDisableTiming);
@@ -1398,6 +1457,10 @@ int av1r_create(int device, av1r_ctx** out)
     for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
+    {
+        std::lock_guard<std::mutex> lock(g_ctxMu);
+        g_ctxs.push_back(c);
+    }
     *out = c;
     return AV1R_OK;
 }
@@ -1413,6 +1476,12 @@ void av1r_destroy(av1r_ctx* c)
     }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    {  // members of its batches: their pending join on its (now drained) stream is satisfied
+        std::lock_guard<std::mutex> lock(g_ctxMu);
+        for (av1r_ctx* m : g_ctxs)
+            if (m->joinLead == c) m->joinLead = nullptr;
+        g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), c), g_ctxs.end());
+    }
     for (FrameBuf* f : c->pool) {
         (void)hipFree(f->base);
         delete f;
@@ -1424,11 +1493,22 @@ void av1r_destroy(av1r_ctx* c)
         if (u.ready) (void)hipEventDestroy(u.ready);
     };
     for (auto& u : c->up) freeUpload(u);
+    for (auto& u : c->pk) freeUpload(u);
     for (auto& u : c->meta) freeUpload(u);
     (void)hipStreamSynchronize(c->copyStream);
     (void)hipStreamDestroy(c->copyStream);
     if (c->resDev) (void)hipFree(c->resDev);
     if (c->granDev) (void)hipFree(c->granDev);
+    {  // its stream leaves the device's k_flow chain (no later wait refers to it)
+        FlowChain& F = g_flowChain[c->device & 63];
+        std::lock_guard<std::mutex> lock(F.m);
+        if (F.last == c->stream) {
+            if (F.done) (void)hipEventDestroy(F.done);
+            F.done = nullptr;
+            F.last = nullptr;
+        }
+    }
+    harvest(false);  // records of launches on its (now idle) stream are complete
     {  // the context leaves every launch record still pending
         std::lock_guard<std::mutex> lock(g_recMu);
         for (LaunchRec* r : g_recPending)
@@ -1438,6 +1518,7 @@ void av1r_destroy(av1r_ctx* c)
     }
     (void)hipEventDestroy(c->sync);
     (void)hipEventDestroy(c->joinEv);
+    (void)hipEventDestroy(c->pkReady);
     if (c->traceDev) (void)hipFree(c->traceDev);
     if (c->traceFile) fclose(c->traceFile);
     for (auto& e : c->evPool)
@@ -1632,6 +1713,159 @@ int av1r_release_prepared(av1r_ctx* c, int handle)
     if (c->prepared[handle]->dev) (void)hipFree(c->prepared[handle]->dev);
     delete c->prepared[handle];
     c->prepared[handle] = nullptr;
+    return AV1R_OK;
+}
+
+// ---- packed frames: host work off the launching thread ----
+static std::mutex g_packMu;
+static std::vector<av1r_packed*> g_packFree;
+static thread_local av1r_ctx t_packScratch;
+
+const char* av1r_pack_last_error(void) { return t_packScratch.err.c_str(); }
+
+int av1r_pack(const av1r_frame_batch* b, av1r_packed** out)
+{
+    if (!b || !b->hdr || !out) return AV1R_E_INVALID;
+    *out = nullptr;
+    av1r_ctx* c = &t_packScratch;  // per-thread schedule scratch: av1r_pack is thread-safe
+    if (b->hdr->version != AV1R_VERSION) return fail(c, AV1R_E_INVALID, "batch version %u", b->hdr->version);
+    av1r_packed* pk = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_packMu);
+        if (!g_packFree.empty()) {
+            pk = g_packFree.back();
+            g_packFree.pop_back();
+        }
+    }
+    if (!pk) pk = new av1r_packed;
+    if (pk->copyPending) {  // its previous upload may still read the host buffer
+        (void)hipEventSynchronize(pk->copied);
+        pk->copyPending = false;
+    }
+    Prepared& P = pk->P;
+    P = Prepared();
+    P.hdr = *b->hdr;
+    if (!b->hdr->show_existing_frame) {
+        c->skipSlotCheck = true;
+        int rc = validate(c, b);
+        c->skipSlotCheck = false;
+        if (rc) {
+            av1r_packed_free(pk);
+            return rc;
+        }
+        build_schedule(c, b, true, true);
+        size_t need = 0;
+        pack_frame(c, b, P, nullptr, nullptr, &need);
+        if (pk->cap < need) {
+            if (pk->host) pk->pinned ? (void)hipHostFree(pk->host) : free(pk->host);
+            const size_t cap = need + need / 4 + 65536;
+            pk->pinned = hipHostMalloc(&pk->host, cap, hipHostMallocDefault) == hipSuccess;
+            if (!pk->pinned) pk->host = static_cast<uint8_t*>(malloc(cap));  // no device here (host-only use)
+            pk->cap = pk->host ? cap : 0;
+            if (!pk->host) {
+                delete pk;
+                return AV1R_E_NOMEM;
+            }
+        }
+        pack_frame(c, b, P, pk->host, nullptr, &need);
+        P.cap = need;
+        P.offsets = true;
+    }
+    *out = pk;
+    return AV1R_OK;
+}
+
+void av1r_packed_free(av1r_packed* pk)
+{
+    if (!pk) return;
+    std::lock_guard<std::mutex> lock(g_packMu);
+    g_packFree.push_back(pk);
+}
+
+size_t av1r_packed_bytes(const av1r_packed* pk) { return pk ? pk->P.bytes : 0; }
+
+int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int n)
+{
+    if (!ctxs || !pks || n <= 0 || !ctxs[0]) return AV1R_E_INVALID;
+    av1r_ctx* lc = ctxs[0];
+    av1r_ctx* c = lc;
+    for (int i = 0; i < n; i++) {
+        if (!ctxs[i] || ctxs[i]->device != lc->device || !pks[i]) return fail(lc, AV1R_E_INVALID, "bad batch member %d", i);
+        for (int j = 0; j < i; j++)
+            if (ctxs[j] == ctxs[i]) return fail(lc, AV1R_E_INVALID, "a context appears twice in one batch");
+    }
+    (void)hipSetDevice(lc->device);
+    ctx_join(lc);
+    // uploads on the lead's copy stream (they overlap the previous batch's kernels), then
+    // the launch stream waits for them once
+    std::vector<FrameJob> jobs;
+    jobs.reserve(n);
+    bool copies = false;
+    for (int i = 0; i < n; i++) {
+        av1r_ctx* m = ctxs[i];
+        av1r_packed* pk = pks[i];
+        if (pk->P.hdr.show_existing_frame) {
+            int rc = av1r_show_existing(m, pk->P.hdr.frame_to_show, pk->P.hdr.refresh_frame_flags);
+            if (rc) return rc;
+            continue;
+        }
+        Upload& U = m->pk[m->pkIdx];
+        m->pkIdx = (m->pkIdx + 1) % av1r_ctx::kPackRing;
+        if (U.pending) {  // a launch three batches back may still read this slot
+            HIPCHK(hipEventSynchronize(U.done));
+            U.pending = false;
+        }
+        if (U.cap < pk->P.cap) {
+            if (U.dev) (void)hipFree(U.dev);
+            U.cap = pk->P.cap + pk->P.cap / 4 + 65536;
+            HIPCHK(hipMalloc(&U.dev, U.cap));
+        }
+        HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.cap, hipMemcpyHostToDevice, lc->copyStream));
+        if (!pk->copied) HIPCHK(hipEventCreateWithFlags(&pk->copied, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(pk->copied, lc->copyStream));
+        pk->copyPending = true;
+        copies = true;
+        FrameJob j;
+        j.c = m;
+        j.P = &pk->P;
+        j.dev = U.dev;
+        int rc = job_begin(j);
+        if (rc) return rc;
+        jobs.push_back(j);
+    }
+    if (jobs.empty()) return AV1R_OK;
+    // members' own earlier work first (as av1r_decode_prepared_batch)
+    for (auto& j : jobs)
+        if (j.c != lc && j.c->joinLead != lc) {
+            ctx_join(j.c);
+            HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
+            HIPCHK(hipStreamWaitEvent(lc->stream, j.c->sync, 0));
+        }
+    if (copies) {
+        HIPCHK(hipEventRecord(lc->pkReady, lc->copyStream));
+        HIPCHK(hipStreamWaitEvent(lc->stream, lc->pkReady, 0));
+    }
+    // a flow-only frame and a level-schedule frame (intra block copy) cannot share launches
+    std::vector<FrameJob> lv;
+    for (size_t i = 0; i < jobs.size();)
+        if (!jobs[i].P->flowOk) {
+            lv.push_back(jobs[i]);
+            jobs.erase(jobs.begin() + i);
+        } else {
+            i++;
+        }
+    int rc = jobs.empty() ? AV1R_OK : launch_jobs(lc, jobs);
+    if (!rc && !lv.empty()) rc = launch_jobs(lc, lv);
+    if (rc) return rc;
+    for (int i = 0, q = 0; i < n; i++) {
+        if (pks[i]->P.hdr.show_existing_frame) continue;
+        av1r_ctx* m = ctxs[i];
+        Upload& U = m->pk[(m->pkIdx + av1r_ctx::kPackRing - 1) % av1r_ctx::kPackRing];
+        HIPCHK(hipEventRecord(U.done, lc->stream));
+        U.pending = true;
+        if (m != lc) m->joinLead = lc;
+        q++;
+    }
     return AV1R_OK;
 }
 

@@ -73,6 +73,33 @@ class Decoder:
         hs = (C.c_int * n)(*handles)
         decoders[0]._check(decoders[0].l.av1r_decode_prepared_batch(ctxs, hs, n), "av1r_decode_prepared_batch")
 
+    @staticmethod
+    def pack(frame):
+        """Validate, schedule and pack a frame batch into pinned host memory (av1r_pack:
+        no context needed, safe from any thread).  Returns a handle for
+        decode_packed_batch; free it with free_packed once that call has returned."""
+        l = native.lib()
+        p = C.c_void_p()
+        rc = l.av1r_pack(C.cast(frame.byref(), C.c_void_p), C.byref(p))
+        if rc != 0:
+            raise BackendError(f"av1r_pack failed ({rc}): {l.av1r_pack_last_error().decode()}")
+        return p
+
+    @staticmethod
+    def free_packed(p):
+        native.lib().av1r_packed_free(p)
+
+    @staticmethod
+    def decode_packed_batch(decoders, packed):
+        """Frame packed[i] of decoders[i] (independent streams, one device): uploaded from
+        pinned memory and decoded in shared launches on decoders[0]'s stream."""
+        n = len(decoders)
+        if n == 0 or n != len(packed):
+            raise ValueError("need one packed frame per decoder")
+        ctxs = (C.c_void_p * n)(*[d.c.value for d in decoders])
+        ps = (C.c_void_p * n)(*[p.value for p in packed])
+        decoders[0]._check(decoders[0].l.av1r_decode_packed_batch(ctxs, ps, n), "av1r_decode_packed_batch")
+
     def release_prepared(self, handle):
         self._check(self.l.av1r_release_prepared(self.c, handle), "av1r_release_prepared")
 

@@ -106,6 +106,14 @@ def lib():
     l.av1r_sizeof.restype = C.c_size_t
     l.av1r_set_flow_spins.argtypes = [vp, C.c_uint32]
     l.av1r_flow_debug.argtypes = [C.POINTER(C.c_uint32), i, i, C.POINTER(i)]
+    l.av1r_pack.argtypes = [vp, C.POINTER(vp)]
+    l.av1r_packed_free.argtypes = [vp]
+    l.av1r_packed_free.restype = None
+    l.av1r_packed_bytes.argtypes = [vp]
+    l.av1r_packed_bytes.restype = C.c_size_t
+    l.av1r_pack_last_error.argtypes = []
+    l.av1r_pack_last_error.restype = C.c_char_p
+    l.av1r_decode_packed_batch.argtypes = [C.POINTER(vp), C.POINTER(vp), i]
     _lib = l
     return l
 
@@ -117,5 +125,6 @@ EXPORTS = [
     "av1r_set_keep_stages", "av1r_last_frame_stats", "av1r_last_error", "av1r_sizeof",
     "av1r_check_batch", "av1r_prepare", "av1r_decode_prepared", "av1r_release_prepared",
     "av1r_set_discard_output", "av1r_stage_times", "av1r_decode_prepared_batch", "av1r_recon_kernel_times",
-    "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug",
+    "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug", "av1r_pack", "av1r_packed_free",
+    "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch",
 ]

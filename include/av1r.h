@@ -224,6 +224,21 @@ int av1r_decode_prepared(av1r_ctx* ctx, int handle);
  * av1r_decode_prepared calls. */
 int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n);
 int av1r_release_prepared(av1r_ctx* ctx, int handle);
+
+/* Host-pipelined decoding (the parse -> schedule -> GPU pipeline of SURVEY.md 8f rank 4).
+ * av1r_pack validates, schedules and packs one frame batch into pinned host memory: it
+ * needs no context and is thread-safe, so worker threads pack frames t+1, t+2, ... while
+ * the GPU decodes frame t.  av1r_decode_packed_batch uploads each packed frame (async, on
+ * the lead context's copy stream, overlapping the previous batch's kernels) and decodes
+ * frame i of context ctxs[i] in shared launches, as av1r_decode_prepared_batch.  A packed
+ * frame may be freed (returned to the library's pool) as soon as the call returns;
+ * av1r_pack_last_error describes the calling thread's last av1r_pack failure. */
+typedef struct av1r_packed av1r_packed;
+int av1r_pack(const av1r_frame_batch* batch, av1r_packed** out);
+void av1r_packed_free(av1r_packed* p);
+size_t av1r_packed_bytes(const av1r_packed* p);
+const char* av1r_pack_last_error(void);
+int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* frames, int n);
 /* Do not queue shown frames for read-back (they still refresh the reference store). */
 int av1r_set_discard_output(av1r_ctx* ctx, int discard);
 

@@ -79,3 +79,34 @@ def test_validation_rejects_bad_batches(native_lib):
     secs = dict(fr.sec)
     secs["hdr"] = np.frombuffer(bytes(hdr), np.uint8).copy()
     assert native_lib.av1r_check_batch(C.cast(batchfile.Frame(secs).byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_UNSUPPORTED
+
+
+def test_pack_is_host_only_and_thread_safe(native_lib):
+    """av1r_pack (validation + flow-only schedule + packing, no context, no device) on
+    every frame of several fixture streams from concurrent threads: every frame packs, the
+    packed size is stable across threads, and a malformed batch fails with its message."""
+    import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from av1dec_amd import Decoder
+    frames = []
+    for s in ("av1-1-b8-06-mfmv", "av1-1-b8-04-cdfupdate", "Halo_426x240_1frames_intrabc", "64x64"):
+        frames += batchfile.load(golden.batch_path(s))
+
+    def size(fr):
+        p = Decoder.pack(fr)
+        n = native_lib.av1r_packed_bytes(p)
+        Decoder.free_packed(p)
+        return n
+    serial = [size(f) for f in frames]
+    with ThreadPoolExecutor(4) as ex:
+        assert list(ex.map(size, frames * 2)) == serial * 2
+    assert all(n > 0 for f, n in zip(frames, serial) if not f.show_existing)
+    fr = batchfile.load(golden.batch_path("av1-1-b8-06-mfmv"))[1]
+    tb = np.frombuffer(fr.sec["tbs"].tobytes(), abi.TB_DTYPE).copy()
+    tb["tx_size"][0] = 99
+    secs = dict(fr.sec)
+    secs["tbs"] = tb.view(np.uint8).ravel()
+    p = C.c_void_p()
+    assert native_lib.av1r_pack(C.cast(batchfile.Frame(secs).byref(), C.c_void_p), C.byref(p)) == abi.AV1R_E_INVALID
+    assert b"tb 0" in native_lib.av1r_pack_last_error()

@@ -326,3 +326,53 @@ def test_gpu_bench_workload_matches_oracle():
         for hd in hs:
             d.release_prepared(hd)
         d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_packed_batches_match_oracle():
+    """av1r_pack + av1r_decode_packed_batch (flow-only schedules, uploads from pinned memory
+    on the copy stream), with an intra-block-copy frame (level schedule) in the same batch as
+    flow-only frames: every output bit-exact with the oracle."""
+    import golden
+    from av1dec_amd import batchfile
+    streams = [pysynth.stream(w, h, 4, 500 + i) for i, (w, h) in enumerate([(640, 360), (352, 288), (416, 240)])]
+    streams.append(batchfile.load(golden.batch_path("Halo_426x240_1frames_intrabc")))
+    decs = [Decoder(0, keep_stages=False) for _ in streams]
+    for t in range(4):
+        members = [i for i, s in enumerate(streams) if t < len(s)]
+        packs = [Decoder.pack(streams[i][t]) for i in members]
+        Decoder.decode_packed_batch([decs[i] for i in members], packs)
+        for p in packs:
+            Decoder.free_packed(p)
+    for d, s in zip(decs, streams):
+        ref = _oracle_md5s(s)
+        n = 0
+        while d.output_pending():
+            assert b"".join(hashlib.md5(p.tobytes()).digest() for p in d.get_output()) == ref[n], f"output {n}"
+            n += 1
+        assert n == len(ref)
+        d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pack_pipeline_matches_oracle():
+    """bench.py's headline path (PackPipeline: packing threads ahead of the launches, stream
+    GOP phases staggered) on 4 small streams over two GOPs: bit-exact with the oracle."""
+    import bench
+    S, F = 4, 6
+    streams = [pysynth.stream(640, 360, F, 600 + j) for j in range(S)]
+    decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+    pp = bench.PackPipeline(decs, streams, F, workers=3)
+    pp.stagger()
+    for _ in range(2 * F):
+        pp.step()
+    pp.close()
+    for j, (d, s) in enumerate(zip(decs, streams)):
+        ref = _oracle_md5s(s)
+        got = []
+        while d.output_pending():
+            got.append(b"".join(hashlib.md5(p.tobytes()).digest() for p in d.get_output()))
+        assert len(got) == bench.gop_offsets(S, F)[j] + 2 * F
+        for k, m in enumerate(got):
+            assert m == ref[k % F], f"stream {j} output {k}"
+        d.close()
