@@ -190,6 +190,13 @@ def host_workers():
     return max(1, min(share, 32) - 1)
 
 
+def cpu_model():
+    try:
+        return next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return "unknown"
+
+
 def cpu_baseline(frames, budget_s):
     """The C oracle (reference algorithm restated, single-threaded) on the first frames."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -372,7 +379,18 @@ def main():
         cfps, cn, cdt = cpu_baseline(streams[0], args.cpu_budget)
         cpu = {"value": round(cfps, 4), "unit": "frames/s", "cores": 1, "kind": "port",
                "sample": f"frames 0..{cn - 1} of synthetic {args.config} stream 0 "
-                         f"({cn} frames, {cdt:.1f} s): oracle/av1r_oracle.c, -O2, 1 thread"}
+                         f"({cn} frames, {cdt:.1f} s): oracle/av1r_oracle.c, -O2, 1 thread",
+               "cpu_model": cpu_model(), "host_cores": os.cpu_count()}
+        cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+        if os.path.exists(cal):
+            # the reference cannot travel; k = reference fps / oracle fps on the
+            # same conformance frames, measured in the build container (tools/calibrate_k.py)
+            cj = json.load(open(cal))
+            ref_eq = cfps * cj["k"]
+            cpu.update({"k": cj["k"], "k_source": "profiles/cpu_calibration.json (" + cj["cpu_model"] + ", "
+                        + str(cj["frames"]) + " conformance frames; reference -O1 incl. its parse)",
+                        "reference_equivalent_fps": round(ref_eq, 4),
+                        "speedup_vs_reference_equivalent": round(fps / max(ref_eq, 1e-9), 1)})
     for d, hs in zip(decs, handles):
         for hd in hs:
             d.release_prepared(hd)

@@ -467,7 +467,7 @@ static void predict_cfl(const oracle_ctx* c, const IntraArgs* a, uint8_t* pred)
     int w = 1 << a->log2W, hh = 1 << a->log2H;
     int alpha = a->plane == 1 ? a->blk->cfl_alpha_u : a->blk->cfl_alpha_v;
     int maxLW = a->blk->max_luma_w, maxLH = a->blk->max_luma_h;
-    static int L[64 * 64];
+    static _Thread_local int L[64 * 64];
     int avg = 0;
     for (int i = 0; i < hh; i++) {
         int ly = MIN((a->y + i) << subY, maxLH - (1 << subY));
@@ -705,7 +705,7 @@ static void reconstruct(const oracle_ctx* c, const av1r_tb* tb, const av1r_block
     int acDelta = tb->plane == 0 ? 0 : tb->plane == 1 ? h->delta_q_u_ac : h->delta_q_v_ac;
     int dcQ = av1r_dc_qlookup[CLIP3(0, 255, blk->qindex + dcDelta)];
     int acQ = av1r_ac_qlookup[CLIP3(0, 255, blk->qindex + acDelta)];
-    static int dq[32 * 32];
+    static _Thread_local int dq[32 * 32];
     memset(dq, 0, sizeof(dq));
     const uint32_t* cf = c->b->coefs + tb->coef_off;
     for (int k = 0; k < tb->coef_cnt; k++) {
@@ -757,8 +757,8 @@ static void decode_tb(oracle_ctx* c, const av1r_tb* tb)
     int w = av1r_tx_w[txSz], hh = av1r_tx_h[txSz];
     int isInter = (blk->flags & AV1R_BLK_INTER) != 0;
     int palSize = plane ? blk->palette_size_uv : blk->palette_size_y;
-    static uint8_t pred[64 * 64];
-    static int res[64 * 64];
+    static _Thread_local uint8_t pred[64 * 64];
+    static _Thread_local int res[64 * 64];
     if (!isInter) {
         if (palSize) {
             /* Block::Palette::predict_palette (Block.cpp:2279-2298) */
@@ -900,7 +900,7 @@ static void block_inter_pred(Inter* I, int refIdx, int refList, int w, int h, in
     }
     const av1r_mi* info = mi_at(c, candRow, candCol);
     int ih = (((h - 1) * I->yStep + (1 << 10) - 1) >> 10) + 8;
-    static int inter[136][128];
+    static _Thread_local int inter[136][128];
     int fidx = filter_idx(info, w, 1);
     for (int r = 0; r < ih; r++) {
         int y = CLIP3(0, lastY, (I->startY >> 10) + r - 3);
@@ -966,9 +966,10 @@ static void block_warp(Inter* I, const int32_t* wp, int refIdx, int refList, int
 }
 
 /* initialise_wedge_mask_table (InterPredict.cpp:835-886): built once. */
-static uint8_t g_master[6][64][64];
-static uint8_t g_wedge_flip[AV1R_BLOCK_SIZES][16];
-static int g_wedge_init;
+/* per thread: oracle instances may run concurrently (tests drive one per stream) */
+static _Thread_local uint8_t g_master[6][64][64];
+static _Thread_local uint8_t g_wedge_flip[AV1R_BLOCK_SIZES][16];
+static _Thread_local int g_wedge_init;
 static void wedge_init(void)
 {
     if (g_wedge_init) return;
@@ -1245,7 +1246,7 @@ static void compute_prediction(oracle_ctx* c, const av1r_block* blk)
             int im = blk->interintra_mode;
             int mode = im == AV1R_II_DC_PRED ? AV1R_DC_PRED : im == AV1R_II_V_PRED ? AV1R_V_PRED
                 : im == AV1R_II_H_PRED ? AV1R_H_PRED : AV1R_SMOOTH_PRED;
-            static uint8_t pred[64 * 64];
+            static _Thread_local uint8_t pred[64 * 64];
             IntraArgs a = {plane, baseX, baseY, log2W, log2H, blk};
             int haveL = plane == 0 ? (blk->flags & AV1R_BLK_AVAIL_L) != 0 : (blk->flags & AV1R_BLK_AVAIL_L_UV) != 0;
             int haveA = plane == 0 ? (blk->flags & AV1R_BLK_AVAIL_U) != 0 : (blk->flags & AV1R_BLK_AVAIL_U_UV) != 0;
@@ -1603,7 +1604,7 @@ static void lr_wiener(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w
     const int R0 = 3, R1 = 11;
     int offset = 1 << (8 + 7 - R0 - 1);
     int limit = (1 << (8 + 1 + 7 - R0)) - 1;
-    static int inter[64 + 6][256];
+    static _Thread_local int inter[64 + 6][256];
     for (int r = 0; r < h + 6; r++)
         for (int cc = 0; cc < w; cc++) {
             int s = 0;
@@ -1624,7 +1625,7 @@ static void lr_wiener(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w
  * evaluated directly (the reference's own #if 0 branch asserts they are equal). */
 static void lr_box(const LrCtx* L, int x, int y, int w, int h, int set, int pass, int r, int* F /* [h][w] stride 256 */)
 {
-    static int A[66][258], Bv[66][258];
+    static _Thread_local int A[66][258], Bv[66][258];
     int eps = av1r_sgr_params[set][pass * 2 + 1];
     int n = (2 * r + 1) * (2 * r + 1);
     int n2e = n * n * eps;
@@ -1670,7 +1671,7 @@ static void lr_box(const LrCtx* L, int x, int y, int w, int h, int set, int pass
 /* selfGuidedFilter (LoopRestoration.cpp:444-479) */
 static void lr_sgr(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w, int h)
 {
-    static int flt0[64 * 256], flt1[64 * 256];
+    static _Thread_local int flt0[64 * 256], flt1[64 * 256];
     int set = u->sgr_set;
     int r0 = av1r_sgr_params[set][0], r1 = av1r_sgr_params[set][2];
     if (r0) lr_box(L, x, y, w, h, set, 0, r0, flt0);
