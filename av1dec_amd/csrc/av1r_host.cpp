@@ -196,6 +196,11 @@ struct av1r_ctx {
     int16_t* resDev = nullptr;  // k_flow mode: the frame's residual tiles (k_resid)
     size_t resCap = 0;
     uint32_t flowSpins = 0;     // av1r_set_flow_spins (0: FLOW_SPINS)
+    int flowPerCU = 8;          // k_flow workgroups per CU of this context's launches (capped by occupancy)
+    // a deep frame launched alone on this context's own stream (batched entry points): its
+    // completion; av1r_busy reports whether it is still running
+    hipEvent_t soloDone = nullptr;
+    bool soloPending = false;
     // device-error bookkeeping (under g_recMu): frame sequence numbers of this context's
     // frames whose launch reported a k_flow timeout, those not yet returned by
     // av1r_synchronize, and the sequence numbers of key frames refreshing every slot (a
@@ -1021,13 +1026,12 @@ static void job_end(FrameJob& j)
     c->lastUploadBytes = j.P->bytes;
 }
 
-// The k_flow launches of a device form ONE chain: each waits for the previous one,
-// whichever stream launched it.  Two k_flow grids resident at once can starve each other:
-// each one's progress needs a resident workgroup on every one of its queues, and spinning
-// workgroups of the other grid may hold the slots (measured: a dependency wait timed out
-// with four batches on four streams).  A launch from the same stream as the previous one
-// is ordered by the stream itself (no event wait: the batched bench case); other kernels
-// always finish, so they may overlap a k_flow freely.
+// AV1R_FLOW_CHAIN=1: the k_flow launches of a device form ONE chain (each waits for the
+// previous one, whichever stream launched it).  Round 1 needed it; since k_flow's
+// workgroups take their queues in entry order, overlapping grids cannot starve each other
+// (recon.hip, k_flow), so by default k_flow grids of different streams may run together:
+// a deep frame (a key frame's long intra chain) launched alone on its own stream overlaps
+// the other streams' batches.
 struct FlowChain {
     std::mutex m;
     hipStream_t last = nullptr;
@@ -1282,25 +1286,31 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
         if (nGroups) {
             if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
+            static const bool chain = getenv("AV1R_FLOW_CHAIN") && atoi(getenv("AV1R_FLOW_CHAIN")) != 0;
             FlowChain& F = g_flowChain[lc->device];
-            std::lock_guard<std::mutex> lock(F.m);
-            // Full persistent grid always: k_flow's workgroups take their queues in entry
-            // order, so overlapping grids cannot starve each other (recon.hip, k_flow).
-            const int grid = (int)std::min<size_t>(flow_grid(lc->device, 8), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            std::unique_lock<std::mutex> lock(F.m, std::defer_lock);
+            if (chain) lock.lock();
+            // the persistent grid: every resident slot (lc->flowPerCU workgroups per CU; a
+            // solo deep frame takes one per CU and leaves the rest to concurrent batches)
+            const int grid = (int)std::min<size_t>(flow_grid(lc->device, lc->flowPerCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
-            // a fresh event per k_flow: never re-recorded while another stream's wait may
-            // still refer to it (the previous one is released once waited for)
-            hipEvent_t ev = nullptr;
-            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
-            launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
+            if (chain) {
+                // a fresh event per k_flow: never re-recorded while another stream's wait may
+                // still refer to it (the previous one is released once waited for)
+                hipEvent_t ev = nullptr;
+                HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
+                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
+                HIPCHK(hipEventRecord(ev, st));
+                if (F.done) (void)hipEventDestroy(F.done);
+                F.done = ev;
+                F.last = st;
+            } else {
+                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
+            }
             flow_debug_note(epoch, st);
-            HIPCHK(hipEventRecord(ev, st));
-            if (F.done) (void)hipEventDestroy(F.done);
-            F.done = ev;
-            F.last = st;
         }
     }
     if (!flow && lc->timing) {
@@ -1378,6 +1388,32 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     return AV1R_OK;
 }
 
+// A frame whose dependency chain is long -- a key frame's intra wavefront: ~2 000 levels
+// at 1080p against ~80 for an inter frame -- holds a shared batch for its whole chain.  The
+// batched entry points launch it alone on its own context's stream instead (k_flow on one
+// workgroup per CU), where it overlaps the other streams' batches (AV1R_SOLO_LEVELS: the
+// level count above which a frame goes alone, 0 = never).
+static bool deep_frame(const Prepared& P)
+{
+    static const int lim = getenv("AV1R_SOLO_LEVELS") ? atoi(getenv("AV1R_SOLO_LEVELS")) : 400;
+    return lim > 0 && P.flowOk && (int)P.levels.size() > lim;
+}
+
+static int launch_solo(FrameJob& j)
+{
+    av1r_ctx* m = j.c;
+    av1r_ctx* c = m;
+    std::vector<FrameJob> one(1, j);
+    const int per = m->flowPerCU;
+    m->flowPerCU = 1;
+    int rc = launch_jobs(m, one);
+    m->flowPerCU = per;
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(m->soloDone, m->stream));
+    m->soloPending = true;
+    return AV1R_OK;
+}
+
 static int launch_frame(av1r_ctx* c, const Prepared& P)
 {
     std::vector<FrameJob> jobs(1);
@@ -1443,6 +1479,7 @@ int av1r_create(int device, av1r_ctx** out)
     for (int i = 0; i < 2; i++) (void)hipEventCreateWithFlags(&c->up[i].done, hipEventDisableTiming);
     for (auto& u : c->pk) (void)hipEventCreateWithFlags(&u.done, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->pkReady, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->soloDone, hipEventDisableTiming);
     for (auto& m : c->meta) {
         (void)hipEventCreateWithFlags(&m.done, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&m.ready, hipEventDisableTiming);
@@ -1519,6 +1556,7 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipEventDestroy(c->sync);
     (void)hipEventDestroy(c->joinEv);
     (void)hipEventDestroy(c->pkReady);
+    (void)hipEventDestroy(c->soloDone);
     if (c->traceDev) (void)hipFree(c->traceDev);
     if (c->traceFile) fclose(c->traceFile);
     for (auto& e : c->evPool)
@@ -1675,6 +1713,10 @@ int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n)
         j.P = &P;
         int rc = job_begin(j);
         if (rc) return rc;
+        if (n > 1 && deep_frame(P)) {  // alone on its own stream, overlapping the batch
+            if ((rc = launch_solo(j))) return rc;
+            continue;
+        }
         jobs.push_back(j);
     }
     if (jobs.empty()) return AV1R_OK;
@@ -1795,11 +1837,14 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             if (ctxs[j] == ctxs[i]) return fail(lc, AV1R_E_INVALID, "a context appears twice in one batch");
     }
     (void)hipSetDevice(lc->device);
-    ctx_join(lc);
-    // uploads on the lead's copy stream (they overlap the previous batch's kernels), then
-    // the launch stream waits for them once
-    std::vector<FrameJob> jobs;
-    jobs.reserve(n);
+    // deep frames go alone on their own context's stream; the rest share launches on the
+    // first shallow member's stream
+    av1r_ctx* bl = nullptr;
+    for (int i = 0; i < n && !bl; i++)
+        if (!pks[i]->P.hdr.show_existing_frame && !(n > 1 && deep_frame(pks[i]->P))) bl = ctxs[i];
+    if (bl) ctx_join(bl);
+    std::vector<FrameJob> jobs, solo;
+    std::vector<Upload*> slots(n, nullptr);
     bool copies = false;
     for (int i = 0; i < n; i++) {
         av1r_ctx* m = ctxs[i];
@@ -1809,9 +1854,12 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             if (rc) return rc;
             continue;
         }
+        const bool alone = n > 1 && deep_frame(pk->P);
+        av1r_ctx* up = alone ? m : bl;  // whose copy stream carries the upload
         Upload& U = m->pk[m->pkIdx];
+        slots[i] = &U;
         m->pkIdx = (m->pkIdx + 1) % av1r_ctx::kPackRing;
-        if (U.pending) {  // a launch three batches back may still read this slot
+        if (U.pending) {  // a launch three frames back may still read this slot
             HIPCHK(hipEventSynchronize(U.done));
             U.pending = false;
         }
@@ -1820,53 +1868,75 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             U.cap = pk->P.cap + pk->P.cap / 4 + 65536;
             HIPCHK(hipMalloc(&U.dev, U.cap));
         }
-        HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.cap, hipMemcpyHostToDevice, lc->copyStream));
+        HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.cap, hipMemcpyHostToDevice, up->copyStream));
         if (!pk->copied) HIPCHK(hipEventCreateWithFlags(&pk->copied, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(pk->copied, lc->copyStream));
+        HIPCHK(hipEventRecord(pk->copied, up->copyStream));
         pk->copyPending = true;
-        copies = true;
+        if (alone) {
+            ctx_join(m);
+            HIPCHK(hipStreamWaitEvent(m->stream, pk->copied, 0));
+        } else {
+            copies = true;
+        }
         FrameJob j;
         j.c = m;
         j.P = &pk->P;
         j.dev = U.dev;
         int rc = job_begin(j);
         if (rc) return rc;
-        jobs.push_back(j);
+        (alone ? solo : jobs).push_back(j);
     }
-    if (jobs.empty()) return AV1R_OK;
-    // members' own earlier work first (as av1r_decode_prepared_batch)
-    for (auto& j : jobs)
-        if (j.c != lc && j.c->joinLead != lc) {
-            ctx_join(j.c);
-            HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
-            HIPCHK(hipStreamWaitEvent(lc->stream, j.c->sync, 0));
-        }
-    if (copies) {
-        HIPCHK(hipEventRecord(lc->pkReady, lc->copyStream));
-        HIPCHK(hipStreamWaitEvent(lc->stream, lc->pkReady, 0));
+    for (auto& j : solo) {  // first, so that their long chains start at once
+        int rc = launch_solo(j);
+        if (rc) return rc;
     }
-    // a flow-only frame and a level-schedule frame (intra block copy) cannot share launches
-    std::vector<FrameJob> lv;
-    for (size_t i = 0; i < jobs.size();)
-        if (!jobs[i].P->flowOk) {
-            lv.push_back(jobs[i]);
-            jobs.erase(jobs.begin() + i);
-        } else {
-            i++;
+    if (!jobs.empty()) {
+        // members' own earlier work first (as av1r_decode_prepared_batch)
+        for (auto& j : jobs)
+            if (j.c != bl && j.c->joinLead != bl) {
+                ctx_join(j.c);
+                HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
+                HIPCHK(hipStreamWaitEvent(bl->stream, j.c->sync, 0));
+            }
+        if (copies) {
+            HIPCHK(hipEventRecord(bl->pkReady, bl->copyStream));
+            HIPCHK(hipStreamWaitEvent(bl->stream, bl->pkReady, 0));
         }
-    int rc = jobs.empty() ? AV1R_OK : launch_jobs(lc, jobs);
-    if (!rc && !lv.empty()) rc = launch_jobs(lc, lv);
-    if (rc) return rc;
-    for (int i = 0, q = 0; i < n; i++) {
-        if (pks[i]->P.hdr.show_existing_frame) continue;
+        // a flow-only frame and a level-schedule frame (intra block copy) cannot share launches
+        std::vector<FrameJob> lv;
+        for (size_t i = 0; i < jobs.size();)
+            if (!jobs[i].P->flowOk) {
+                lv.push_back(jobs[i]);
+                jobs.erase(jobs.begin() + i);
+            } else {
+                i++;
+            }
+        int rc = jobs.empty() ? AV1R_OK : launch_jobs(bl, jobs);
+        if (!rc && !lv.empty()) rc = launch_jobs(bl, lv);
+        if (rc) return rc;
+        for (auto& j : jobs)
+            if (j.c != bl) j.c->joinLead = bl;
+        for (auto& j : lv)
+            if (j.c != bl) j.c->joinLead = bl;
+    }
+    for (int i = 0; i < n; i++) {  // the upload slots are free again after their launch
+        if (!slots[i]) continue;
         av1r_ctx* m = ctxs[i];
-        Upload& U = m->pk[(m->pkIdx + av1r_ctx::kPackRing - 1) % av1r_ctx::kPackRing];
-        HIPCHK(hipEventRecord(U.done, lc->stream));
-        U.pending = true;
-        if (m != lc) m->joinLead = lc;
-        q++;
+        const bool alone = std::any_of(solo.begin(), solo.end(), [&](const FrameJob& j) { return j.c == m; });
+        HIPCHK(hipEventRecord(slots[i]->done, alone ? m->stream : bl->stream));
+        slots[i]->pending = true;
     }
     return AV1R_OK;
+}
+
+// 1 while a deep frame this context launched alone (batched entry points) is running
+int av1r_busy(av1r_ctx* c)
+{
+    if (!c) return AV1R_E_INVALID;
+    if (!c->soloPending) return 0;
+    if (hipEventQuery(c->soloDone) == hipErrorNotReady) return 1;
+    c->soloPending = false;
+    return 0;
 }
 
 int av1r_set_discard_output(av1r_ctx* c, int discard)

@@ -100,6 +100,10 @@ class Decoder:
         ps = (C.c_void_p * n)(*[p.value for p in packed])
         decoders[0]._check(decoders[0].l.av1r_decode_packed_batch(ctxs, ps, n), "av1r_decode_packed_batch")
 
+    def busy(self):
+        """True while a deep frame (key frame) of this decoder launched alone is running."""
+        return self.l.av1r_busy(self.c) == 1
+
     def release_prepared(self, handle):
         self._check(self.l.av1r_release_prepared(self.c, handle), "av1r_release_prepared")
 

@@ -97,90 +97,88 @@ def gop_offsets(S, F):
     return [j * F // S for j in range(S)]
 
 
-class StreamSet:
-    """S streams of prepared (HBM-resident) frames, each cycling its own GOP from its own
-    phase.  One step = the next frame of every stream in shared launches
-    (av1r_decode_prepared_batch).  A stream always decodes its frames in order from its key
-    frame (frame 0 refreshes every slot, so cycling the GOP is a valid stream)."""
+class StreamScheduler:
+    """S independent streams, each cycling its own F-frame GOP from its own phase (stream j
+    starts j*F/S frames in), decoded in shared launches.  Each round batches the next frame
+    of every stream that is ready: a stream whose key frame is still running alone on its
+    own HIP stream (av1r_busy: the library launches deep frames solo so that they overlap
+    the batches) sits out until it is done.  A stream always decodes its frames in order
+    from its key frame (frame 0 refreshes every slot, so cycling the GOP is a valid stream).
 
-    def __init__(self, decs, handles, F):
-        self.decs, self.handles, self.F = decs, handles, F
+    packed: the host-inclusive pipeline -- worker threads validate, schedule and pack
+    (av1r_pack) each stream's next `depth` frames while the GPU decodes, and every round
+    uploads and decodes the packed frames (av1r_decode_packed_batch); the frame batches
+    (the host parser's output) sit in host memory.  Otherwise frames come from
+    per-stream lists of prepared handles (av1r_prepare: scheduled and resident in HBM)."""
+
+    def __init__(self, decs, F, streams=None, handles=None, workers=1, depth=3):
+        from concurrent.futures import ThreadPoolExecutor
+        self.decs, self.F, self.streams, self.handles, self.depth = decs, F, streams, handles, depth
+        self.packed = handles is None
+        self.ex = ThreadPoolExecutor(max(1, workers)) if self.packed else None
         self.pos = [0] * len(decs)
+        self.q = [[] for _ in decs]  # packed: per stream, futures of its next frames
+
+    def _item(self, j):
+        from av1dec_amd import Decoder
+        if not self.packed:
+            return self.handles[j][self.pos[j] % self.F]
+        while len(self.q[j]) < self.depth:
+            t = (self.pos[j] + len(self.q[j])) % self.F
+            self.q[j].append(self.ex.submit(Decoder.pack, self.streams[j][t]))
+        return self.q[j].pop(0).result()
+
+    def _launch(self, js):
+        from av1dec_amd import Decoder
+        items = [self._item(j) for j in js]
+        decs = [self.decs[j] for j in js]
+        if self.packed:
+            Decoder.decode_packed_batch(decs, items)
+            for p in items:
+                Decoder.free_packed(p)
+            for j in js:  # keep the packers `depth` frames ahead
+                self._top_up(j)
+        else:
+            Decoder.decode_prepared_batch(decs, items)
+        out = [(j, self.pos[j] % self.F) for j in js]
+        for j in js:
+            self.pos[j] += 1
+        return out
+
+    def _top_up(self, j):
+        from av1dec_amd import Decoder
+        while len(self.q[j]) < self.depth:
+            t = (self.pos[j] + 1 + len(self.q[j])) % self.F
+            self.q[j].append(self.ex.submit(Decoder.pack, self.streams[j][t]))
 
     def stagger(self):
         """Bring stream j alone to frame j*F/S (untimed setup)."""
-        from av1dec_amd import Decoder  # noqa: F401
         for j, off in enumerate(gop_offsets(len(self.decs), self.F)):
             while self.pos[j] < off:
-                self.decs[j].decode_prepared(self.handles[j][self.pos[j] % self.F])
-                self.pos[j] += 1
+                self._launch([j])
 
-    def frames(self):
-        """(stream, frame index) decoded by the next step."""
-        return [(j, p % self.F) for j, p in enumerate(self.pos)]
-
-    def step(self):
-        from av1dec_amd import Decoder
-        Decoder.decode_prepared_batch(self.decs, [hs[p % self.F] for hs, p in zip(self.handles, self.pos)])
-        self.pos = [p + 1 for p in self.pos]
-
-
-class PackPipeline:
-    """The host-inclusive decode pipeline: worker threads validate, schedule and pack (into
-    pinned memory) the frames of step t+1 .. t+depth while the GPU decodes step t; the
-    launching thread uploads each step's packed frames (async, copy stream) and decodes them
-    in shared launches (av1r_pack / av1r_decode_packed_batch).  Streams keep their own GOP
-    phases as in StreamSet; the batches are the host parser's output, held in host memory."""
-
-    def __init__(self, decs, streams, F, workers, depth=3):
-        from concurrent.futures import ThreadPoolExecutor
-        self.decs, self.streams, self.F, self.depth = decs, streams, F, depth
-        self.ex = ThreadPoolExecutor(max(1, workers))
-        self.pos = [0] * len(decs)
-        self.ahead = [0] * len(decs)  # next frame to pack, per stream
-        self.q = []
-
-    def stagger(self):
-        """Bring stream j alone to frame j*F/S, from its key frame (untimed setup)."""
-        from av1dec_amd import Decoder
-        for j, off in enumerate(gop_offsets(len(self.decs), self.F)):
-            for t in range(off):
-                p = Decoder.pack(self.streams[j][t % self.F])
-                Decoder.decode_packed_batch([self.decs[j]], [p])
-                Decoder.free_packed(p)
-            self.pos[j] = self.ahead[j] = off
-
-    def _submit(self):
-        from av1dec_amd import Decoder
-        futs = [self.ex.submit(Decoder.pack, self.streams[j][a % self.F]) for j, a in enumerate(self.ahead)]
-        self.q.append(([(j, a % self.F) for j, a in enumerate(self.ahead)], futs))
-        self.ahead = [a + 1 for a in self.ahead]
-
-    def step(self):
-        """Decode the next frame of every stream; returns their (stream, frame) pairs."""
-        from av1dec_amd import Decoder
-        while len(self.q) < self.depth:
-            self._submit()
-        frames, futs = self.q.pop(0)
-        packs = [f.result() for f in futs]
-        Decoder.decode_packed_batch(self.decs, packs)
-        for p in packs:
-            Decoder.free_packed(p)
-        self.pos = [p + 1 for p in self.pos]
-        self._submit()
-        return frames
-
-    def drain(self):
-        from av1dec_amd import Decoder
-        for _, futs in self.q:
-            for f in futs:
-                Decoder.free_packed(f.result())
-        self.q = []
-        self.ahead = list(self.pos)
+    def run(self, k):
+        """Decode the next k frames of every stream; returns the (stream, frame) pairs."""
+        target = [p + k for p in self.pos]
+        done = []
+        while True:
+            left = [j for j in range(len(self.decs)) if self.pos[j] < target[j]]
+            if not left:
+                return done
+            ready = [j for j in left if not self.decs[j].busy()]
+            if not ready:
+                time.sleep(50e-6)
+                continue
+            done += self._launch(ready)
 
     def close(self):
-        self.drain()
-        self.ex.shutdown()
+        from av1dec_amd import Decoder
+        if self.ex:
+            for q in self.q:
+                for f in q:
+                    Decoder.free_packed(f.result())
+            self.q = [[] for _ in self.decs]
+            self.ex.shutdown()
 
 
 def host_workers():
@@ -262,23 +260,19 @@ def main():
     # GPU).  Setup (untimed): stream j brought to its own GOP phase, a priming pass of ~1 s,
     # then the warmup steps.
     workers = host_workers()
-    pp = PackPipeline(decs, streams, F, workers)
+    pp = StreamScheduler(decs, F, streams=streams, workers=workers)
     pp.stagger()
     sync()
     t_prime = time.perf_counter()
     while time.perf_counter() - t_prime < 1.0:
-        for _ in range(F):
-            pp.step()
+        pp.run(F)
         sync()
-    for _ in range(args.warmup):
-        pp.step()
+    pp.run(args.warmup)
     sync()
     if dist:
         dist.barrier()
-    timed = []  # (stream, frame) of every frame in the timed region
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        timed += pp.step()
+    timed = pp.run(args.steps)  # (stream, frame) of every frame in the timed region
     sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     fps = aggregate_fps(world, args.steps * S, elapsed)
@@ -288,32 +282,32 @@ def main():
     # ---- device-only rate: the same streams with every batch already validated, scheduled
     # and resident in HBM (av1r_prepare), the same staggered GOP phases
     handles = [[d.prepare(f) for f in fr] for d, fr in zip(decs, streams)]
-    ss = StreamSet(decs, handles, F)
+    ss = StreamScheduler(decs, F, handles=handles)
     ss.stagger()
-    for _ in range(F):
-        ss.step()
-    for _ in range(args.warmup):
-        ss.step()
+    ss.run(F + args.warmup)
     sync()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ss.step()
+    ss.run(args.steps)
     sync()
     elapsed_dev = max_over_ranks(time.perf_counter() - t0, dist)
     device_fps = aggregate_fps(world, args.steps * S, elapsed_dev)
 
     # per-stage device time over the same batches (HIP events on the launch stream)
     lead = decs[0]
-    lead.l.av1r_set_timing(lead.c, 1)
-    timed2 = []
-    for _ in range(args.steps):
-        timed2 += ss.frames()
-        ss.step()
-    ktot, _ = lead.recon_kernel_times()
-    totals, nfr = lead.stage_times()
-    lead.l.av1r_set_timing(lead.c, 0)
+    for d in decs:  # every context records the launches it leads (batches and solo frames)
+        d.l.av1r_set_timing(d.c, 1)
+    timed2 = ss.run(args.steps)
+    sync()
+    ktot, totals, nfr = [0.0] * 3, [0.0] * 4, 0
+    for d in decs:
+        kt, _ = d.recon_kernel_times()
+        st, nf = d.stage_times()
+        ktot = [a + b for a, b in zip(ktot, kt)]
+        totals = [a + b for a, b in zip(totals, st)]
+        nfr += nf
+        d.l.av1r_set_timing(d.c, 0)
     names = ["recon", "lf", "cdef", "lr"]
     per_frame_ms = {n: totals[k] / max(nfr, 1) for k, n in enumerate(names)}
     sb = {n: 0.0 for n in names}
@@ -416,8 +410,9 @@ def main():
                                    f"stream j offset by j*{F}/{S} frames; tiles {tiles[0]}x{tiles[1]}; seeds "
                                    f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
                                    f"host-inclusive: each frame validated, scheduled, packed and uploaded from "
-                                   f"host memory inside the timed region ({workers} packing threads, 3 steps "
-                                   f"ahead of the GPU); timed frames: {args.steps * S} of which {n_key} key",
+                                   f"host memory inside the timed region ({workers} packing threads, 3 frames "
+                                   f"ahead per stream; key frames run alone on their stream, overlapping "
+                                   f"the other streams' batches); timed frames: {args.steps * S} of which {n_key} key",
                        "host_threads": workers + 1,
                        "timed_key_frames": n_key,
                        "streams_per_gpu": S, "frames_per_step": S,

@@ -239,6 +239,11 @@ void av1r_packed_free(av1r_packed* p);
 size_t av1r_packed_bytes(const av1r_packed* p);
 const char* av1r_pack_last_error(void);
 int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* frames, int n);
+/* In both batched entry points a frame with a deep dependency chain (a key frame) is
+ * launched alone on its own context's stream, overlapping the batch.  av1r_busy returns 1
+ * while such a frame is still running: a scheduler leaves that stream out of the next
+ * batches until then, so they never wait for the chain. */
+int av1r_busy(av1r_ctx* ctx);
 /* Do not queue shown frames for read-back (they still refresh the reference store). */
 int av1r_set_discard_output(av1r_ctx* ctx, int discard);
 

@@ -305,18 +305,17 @@ def test_gpu_bench_workload_matches_oracle():
         ref = ex.submit(lambda: list(ex.map(_oracle_md5s, streams)))
         decs = [Decoder(0, keep_stages=False) for _ in range(S)]
         handles = [[d.prepare(f) for f in fr] for d, fr in zip(decs, streams)]
-        ss = bench.StreamSet(decs, handles, F)
+        ss = bench.StreamScheduler(decs, F, handles=handles)
         ss.stagger()
         got = [[] for _ in range(S)]
         keys = 0
-        for _ in range(F):
-            keys += sum(1 for j, t in ss.frames() if t == 0)
-            ss.step()
+        for _ in range(F // 4):
+            keys += sum(1 for j, t in ss.run(4) if t == 0)
             for j, d in enumerate(decs):
                 while d.output_pending():
                     got[j].append(b"".join(hashlib.md5(p.tobytes()).digest() for p in d.get_output()))
         ref = ref.result()
-    assert keys >= S - 1  # the timed-style window holds key frames
+    assert keys >= S - 1  # the timed-style window holds key frames (each launched alone)
     for j in range(S):
         off = bench.gop_offsets(S, F)[j]
         assert len(got[j]) == off + F
@@ -356,16 +355,16 @@ def test_gpu_packed_batches_match_oracle():
 
 @pytest.mark.gpu
 def test_gpu_pack_pipeline_matches_oracle():
-    """bench.py's headline path (PackPipeline: packing threads ahead of the launches, stream
-    GOP phases staggered) on 4 small streams over two GOPs: bit-exact with the oracle."""
+    """bench.py's headline path (StreamScheduler: packing threads ahead of the launches,
+    stream GOP phases staggered, key frames launched alone while the other streams' batches
+    go on) on 4 small streams over two GOPs: bit-exact with the oracle."""
     import bench
     S, F = 4, 6
     streams = [pysynth.stream(640, 360, F, 600 + j) for j in range(S)]
     decs = [Decoder(0, keep_stages=False) for _ in range(S)]
-    pp = bench.PackPipeline(decs, streams, F, workers=3)
+    pp = bench.StreamScheduler(decs, F, streams=streams, workers=3)
     pp.stagger()
-    for _ in range(2 * F):
-        pp.step()
+    pp.run(2 * F)
     pp.close()
     for j, (d, s) in enumerate(zip(decs, streams)):
         ref = _oracle_md5s(s)
