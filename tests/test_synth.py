@@ -248,7 +248,8 @@ def test_gpu_flow_timeout_surfaces_as_device_error():
     from av1dec_amd.decoder import BackendError
     frames = [pysynth.stream(640, 360, 3, 0x5EED0099 + i) for i in range(2)]
     decs = [Decoder(0, keep_stages=False) for _ in frames]
-    decs[0].set_flow_spins(1)  # the batch launches on decs[0]: its bound applies to both
+    for d in decs:  # the bound of the launching context applies (batch lead, or a key frame's own)
+        d.set_flow_spins(1)
     handles = [[d.prepare(f) for f in s] for d, s in zip(decs, frames)]
     for t in range(3):
         Decoder.decode_prepared_batch(decs, [h[t] for h in handles])
@@ -263,7 +264,8 @@ def test_gpu_flow_timeout_surfaces_as_device_error():
             n += 1
         assert n == 3
     # the same stream with the default bound decodes bit-exact again from its key frame
-    decs[0].set_flow_spins(0)
+    for d in decs:
+        d.set_flow_spins(0)
     for t in range(3):
         Decoder.decode_prepared_batch(decs, [h[t] for h in handles])
     o = pyoracle.Oracle(keep_stages=False)
