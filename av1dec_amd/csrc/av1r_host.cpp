@@ -1845,6 +1845,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
     if (bl) ctx_join(bl);
     std::vector<FrameJob> jobs, solo;
     std::vector<Upload*> slots(n, nullptr);
+    std::vector<hipEvent_t> waits;  // uploads on member copy streams the batch waits for
     bool copies = false;
     for (int i = 0; i < n; i++) {
         av1r_ctx* m = ctxs[i];
@@ -1855,7 +1856,10 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             continue;
         }
         const bool alone = n > 1 && deep_frame(pk->P);
-        av1r_ctx* up = alone ? m : bl;  // whose copy stream carries the upload
+        // whose copy stream carries the upload: by default every member's own (the copies of
+        // a batch spread over the copy engines); AV1R_COPY_SPREAD=0: the batch lead's
+        static const bool spread = !getenv("AV1R_COPY_SPREAD") || atoi(getenv("AV1R_COPY_SPREAD")) != 0;
+        av1r_ctx* up = alone || spread ? m : bl;
         Upload& U = m->pk[m->pkIdx];
         slots[i] = &U;
         m->pkIdx = (m->pkIdx + 1) % av1r_ctx::kPackRing;
@@ -1875,6 +1879,8 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         if (alone) {
             ctx_join(m);
             HIPCHK(hipStreamWaitEvent(m->stream, pk->copied, 0));
+        } else if (up != bl) {
+            waits.push_back(pk->copied);
         } else {
             copies = true;
         }
@@ -1902,6 +1908,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             HIPCHK(hipEventRecord(bl->pkReady, bl->copyStream));
             HIPCHK(hipStreamWaitEvent(bl->stream, bl->pkReady, 0));
         }
+        for (hipEvent_t e : waits) HIPCHK(hipStreamWaitEvent(bl->stream, e, 0));
         // a flow-only frame and a level-schedule frame (intra block copy) cannot share launches
         std::vector<FrameJob> lv;
         for (size_t i = 0; i < jobs.size();)
