@@ -1,0 +1,70 @@
+// api.cpp -- C-ABI of the host parser (include/av1p.h).
+#include "parser.h"
+
+#include <new>
+
+#include "av1p.h"
+
+struct av1p_ctx {
+    av1p::Parser parser;
+    std::vector<av1p::Frame*> frames;
+    std::string err;
+    void release()
+    {
+        for (auto* f : frames) delete f;
+        frames.clear();
+    }
+    ~av1p_ctx() { release(); }
+};
+
+extern "C" {
+
+int av1p_create(av1p_ctx** out)
+{
+    if (!out) return AV1R_E_INVALID;
+    *out = new (std::nothrow) av1p_ctx;
+    return *out ? AV1R_OK : AV1R_E_NOMEM;
+}
+
+void av1p_destroy(av1p_ctx* ctx)
+{
+    if (!ctx) return;
+    delete ctx->parser.cur;
+    ctx->parser.cur = nullptr;
+    for (auto* f : ctx->parser.done) delete f;
+    ctx->parser.done.clear();
+    delete ctx;
+}
+
+int av1p_decode_tu(av1p_ctx* ctx, const uint8_t* data, size_t size, int* n_frames)
+{
+    if (!ctx || (!data && size)) return AV1R_E_INVALID;
+    ctx->release();
+    ctx->parser.err.clear();
+    int rc;
+    try {
+        rc = ctx->parser.decode_tu(data, size);
+    } catch (const std::bad_alloc&) {
+        ctx->parser.err = "out of memory";
+        rc = AV1R_E_NOMEM;
+    }
+    ctx->frames.swap(ctx->parser.done);
+    if (rc) {
+        // a frame whose tile data failed is not handed out
+        delete ctx->parser.cur;
+        ctx->parser.cur = nullptr;
+        ctx->parser.seen_frame_header = false;
+    }
+    if (n_frames) *n_frames = (int)ctx->frames.size();
+    return rc;
+}
+
+const av1r_frame_batch* av1p_frame(av1p_ctx* ctx, int i)
+{
+    if (!ctx || i < 0 || i >= (int)ctx->frames.size()) return nullptr;
+    return &ctx->frames[i]->batch;
+}
+
+const char* av1p_last_error(av1p_ctx* ctx) { return ctx ? ctx->parser.err.c_str() : "null context"; }
+
+}  // extern "C"

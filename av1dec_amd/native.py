@@ -62,6 +62,57 @@ def build(force=False, jobs=3, out=None, defines=(), src_flags=None):
     return lib_path
 
 
+PARSE_LIB = os.path.join(BUILD, "libav1p.so")
+PARSE_SRCS = ("obu.cpp", "block.cpp", "api.cpp")
+CXX = os.environ.get("CXX", "g++")
+
+
+def build_parser(force=False, out=None, extra=()):
+    """Host parser (include/av1p.h): plain C++, no device code -- libav1p.so in-tree."""
+    lib_path = out or PARSE_LIB
+    pdir = os.path.join(PKG, "csrc", "parse")
+    if out is None and not force and not extra and os.path.exists(lib_path):
+        t = os.path.getmtime(lib_path)
+        deps = [os.path.join(pdir, f) for f in os.listdir(pdir)] + [os.path.join(ROOT, "include", f)
+                                                                   for f in os.listdir(os.path.join(ROOT, "include"))]
+        if all(os.path.getmtime(d) <= t for d in deps):
+            return lib_path
+    os.makedirs(BUILD, exist_ok=True)
+    tmp = lib_path + ".tmp"
+    subprocess.check_call([CXX, "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wno-class-memaccess",
+                           "-I" + os.path.join(ROOT, "include"), "-I" + pdir, *extra, "-o", tmp]
+                          + [os.path.join(pdir, s) for s in PARSE_SRCS])
+    os.replace(tmp, lib_path)
+    return lib_path
+
+
+_plib = None
+
+
+def parser_lib():
+    global _plib
+    if _plib is not None:
+        return _plib
+    path = os.environ.get("AV1P_LIB", PARSE_LIB)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run av1dec_amd.native.build_parser()")
+    l = C.CDLL(path)
+    vp = C.c_void_p
+    l.av1p_create.argtypes = [C.POINTER(vp)]
+    l.av1p_destroy.argtypes = [vp]
+    l.av1p_destroy.restype = None
+    l.av1p_decode_tu.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
+    l.av1p_frame.argtypes = [vp, C.c_int]
+    l.av1p_frame.restype = vp
+    l.av1p_last_error.argtypes = [vp]
+    l.av1p_last_error.restype = C.c_char_p
+    _plib = l
+    return l
+
+
+PARSE_EXPORTS = ["av1p_create", "av1p_destroy", "av1p_decode_tu", "av1p_frame", "av1p_last_error"]
+
+
 _lib = None
 
 

@@ -35,3 +35,17 @@ def bits_md5():
             if len(p) == 2:
                 m[p[1].replace(".ivf", "").replace(".mkv", "")] = p[0]
     return m
+
+
+REF_BITS = os.path.join(os.environ.get("AV1DEC_REF", "/root/reference"), "bits")
+
+
+def ivf_path(stream):
+    """The conformance bitstream itself: the reference checkout's bits/<stream>.ivf.  Only in
+    the build container -- the bitstreams are not part of this repository, so tests that
+    parse them are CPU tests that skip where the checkout is absent."""
+    return os.path.join(REF_BITS, stream + ".ivf")
+
+
+def have_ivf():
+    return os.path.isdir(REF_BITS)
