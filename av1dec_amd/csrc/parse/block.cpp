@@ -544,7 +544,7 @@ void BlockParser::read_delta_qindex(Blk& b)
     if (abs) {
         const int sign = (int)L(1);
         const int reduced = sign ? -abs : abs;
-        P.current_q = clip3(1, 255, P.current_q + (reduced << fh.delta_q_res));
+        P.current_q = clip3(1, 255, P.current_q + reduced * (1 << fh.delta_q_res));
         b.qindex = P.current_q;
     }
 }
@@ -564,7 +564,7 @@ void BlockParser::read_delta_lf(Blk& b)
         if (abs) {
             const int sign = (int)L(1);
             const int reduced = sign ? -abs : abs;
-            P.delta_lf[i] = clip3(-63, 63, P.delta_lf[i] + (reduced << fh.delta_lf_res));
+            P.delta_lf[i] = clip3(-63, 63, P.delta_lf[i] + reduced * (1 << fh.delta_lf_res));
         }
     }
 }
@@ -1623,7 +1623,7 @@ void BlockParser::warp_estimation(Blk& b)  // warpEstimation + setupShear
     resolve_divisor(det, divShift, divFactor);
     divShift -= kWarpPrecBits;
     if (divShift < 0) {
-        divFactor = divFactor << (-divShift);
+        divFactor = divFactor * (1 << (-divShift));
         divShift = 0;
     }
     const int kClamp = 1 << 13;
@@ -1647,7 +1647,7 @@ void BlockParser::warp_estimation(Blk& b)  // warpEstimation + setupShear
     const int alpha0 = clip3(-32768, 32767, p[2] - (1 << kWarpPrecBits));
     const int beta0 = clip3(-32768, 32767, p[3]);
     resolve_divisor(p[2], divShift, divFactor);
-    const int64_t v = (int64_t)p[4] << kWarpPrecBits;
+    const int64_t v = (int64_t)p[4] * (1 << kWarpPrecBits);
     const int gamma0 = (int)std::max<int64_t>(-32768, std::min<int64_t>(32767, round2signed_64(v * divFactor, divShift)));
     const int64_t w = (int64_t)p[3] * p[4];
     const int delta0 = (int)std::max<int64_t>(

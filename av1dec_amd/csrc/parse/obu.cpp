@@ -440,7 +440,7 @@ int Parser::global_motion_params(BitReader& br)
             const int sub = (idx % 3) == 2 ? (1 << precBits) : 0;
             const int mx = 1 << absBits;
             const int r = (fh.prev_gm[ref][idx] >> precDiff) - sub;
-            fh.gm_params[ref][idx] = (decode_signed_subexp_with_ref(br, -mx, mx + 1, r) << precDiff) + round;
+            fh.gm_params[ref][idx] = decode_signed_subexp_with_ref(br, -mx, mx + 1, r) * (1 << precDiff) + round;
         };
         if (type >= AV1R_GM_ROTZOOM) {
             param(2);
@@ -873,6 +873,10 @@ int Parser::parse_uncompressed_header(BitReader& br)
     CHK(film_grain_params(br));
     if (br.over) return fail(AV1R_E_INVALID, "truncated frame header");
     if (fh.frame_width & 1 || fh.frame_height & 1) return fail(AV1R_E_UNSUPPORTED, "odd frame size %dx%d", fh.frame_width, fh.frame_height);
+    if (fh.frame_width > seq.max_frame_width || fh.frame_height > seq.max_frame_height ||
+        (int64_t)fh.frame_width * fh.frame_height > (int64_t)8192 * 4352)
+        return fail(AV1R_E_UNSUPPORTED, "frame size %dx%d (sequence maximum %dx%d, library limit 8192x4352 pixels)",
+                    fh.frame_width, fh.frame_height, seq.max_frame_width, seq.max_frame_height);
     return AV1R_OK;
 }
 
@@ -1147,6 +1151,9 @@ int Parser::tile_group(BitReader& br, const uint8_t* data, size_t size)
     br.byte_align();
     size_t off = br.byte_pos();
     (void)start;
+    if (tgStart > tgEnd || tgEnd >= numTiles || tgStart != tile_num || !cur)
+        return fail(AV1R_E_INVALID, "tile group %d..%d does not continue the frame (next tile %d of %d)", tgStart, tgEnd,
+                    tile_num, numTiles);
     for (int tn = tgStart; tn <= tgEnd; tn++) {
         const int tileRow = tn / fh.tile_cols, tileCol = tn % fh.tile_cols;
         size_t tileSize;

@@ -123,12 +123,16 @@ struct Dumper {
         r.mi_size = b.MiSize;
         r.qindex = (uint8_t)b.m_frame.get_qindex(b.CurrentQIndex, b.segment_id);
         r.y_mode = b.YMode;
-        r.uv_mode = b.HasChroma ? b.UVMode : 0;
+        // only the fields the reference reads for this kind of block: UVMode, use_filter_intra
+        // and CflAlpha* are uninitialised members of Block otherwise
+        r.uv_mode = (b.HasChroma && !b.is_inter) ? b.UVMode : 0;
         r.angle_delta_y = b.AngleDeltaY;
         r.angle_delta_uv = b.AngleDeltaUV;
-        r.filter_intra_mode = b.use_filter_intra ? b.filter_intra_mode : 0;
-        r.cfl_alpha_u = b.CflAlphaU;
-        r.cfl_alpha_v = b.CflAlphaV;
+        r.filter_intra_mode = (!b.is_inter && b.use_filter_intra) ? b.filter_intra_mode : 0;
+        if (!b.is_inter && b.HasChroma && b.UVMode == UV_CFL_PRED) {
+            r.cfl_alpha_u = b.CflAlphaU;
+            r.cfl_alpha_v = b.CflAlphaV;
+        }
         r.palette_size_y = b.PaletteSizeY;
         r.palette_size_uv = b.PaletteSizeUV;
         uint32_t f = 0;
@@ -359,7 +363,7 @@ struct Dumper {
         const CdefParams& cd = h.m_cdef;
         o.cdef_damping = cd.CdefDamping;
         o.cdef_bits = cd.cdef_bits;
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < (1 << cd.cdef_bits); i++) {  // the rest is never written
             o.cdef_y_pri[i] = cd.cdef_y_pri_strength[i];
             o.cdef_y_sec[i] = cd.cdef_y_sec_strength[i];
             o.cdef_uv_pri[i] = cd.cdef_uv_pri_strength[i];

@@ -1,0 +1,114 @@
+"""Host parser (include/av1p.h, libav1p.so) against the reference's parse trees.
+
+The fixtures tests/golden/batches/*.av1b.gz are the reference decoder's own parse of each
+conformance stream, serialised by oracle/harness/refdump; the parser must reproduce every
+byte of every frame batch from the bitstream alone.  The bitstreams are read from the
+reference checkout (not part of this repository), so these tests run in the build
+container and skip elsewhere.  CPU only: the parser is host code."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import golden  # noqa: E402
+from av1dec_amd import abi, batchfile, native  # noqa: E402
+
+needs_bits = pytest.mark.skipif(not golden.have_ivf(), reason="conformance bitstreams (reference checkout) absent")
+
+
+@pytest.fixture(scope="module")
+def parser_mod():
+    native.build_parser()
+    from av1dec_amd import parser
+    return parser
+
+
+def _frames(parser_mod, stream):
+    with open(golden.ivf_path(stream), "rb") as f:
+        return parser_mod.Parser().decode_ivf(f.read())
+
+
+SHOW_EXISTING_FIELDS = ("show_existing_frame", "frame_to_show", "refresh_frame_flags", "frame_type")
+
+
+def _same(f, g):
+    if f.show_existing or g.show_existing:
+        return all(getattr(f.hdr, n) == getattr(g.hdr, n) for n in SHOW_EXISTING_FIELDS)
+    return all(np.array_equal(f.sec[s], g.sec[s]) for s in batchfile.SECTIONS)
+
+
+@needs_bits
+@pytest.mark.parametrize("stream", golden.streams())
+def test_parser_matches_reference_parse(parser_mod, stream):
+    frames = _frames(parser_mod, stream)
+    gold = batchfile.load(golden.batch_path(stream))
+    assert len(frames) == len(gold)
+    for k, (f, g) in enumerate(zip(frames, gold)):
+        assert _same(f, g), f"{stream}: frame {k} differs from the reference's parse"
+
+
+def test_parser_exports_and_structs():
+    native.build_parser()
+    lib = native.parser_lib()
+    for name in native.PARSE_EXPORTS:
+        assert hasattr(lib, name)
+
+
+@needs_bits
+def test_parser_rejects_damage_without_crashing(parser_mod):
+    with open(golden.ivf_path("av1-1-b8-01-size-16x16"), "rb") as f:
+        tus = list(parser_mod.ivf_frames(f.read()))
+    # truncated temporal units, and random bytes: a status, never a crash
+    p = parser_mod.Parser()
+    with pytest.raises(parser_mod.ParseError):
+        p.decode_tu(tus[0][: len(tus[0]) // 3])
+    rng = np.random.default_rng(7)
+    for _ in range(20):
+        p = parser_mod.Parser()
+        try:
+            p.decode_tu(rng.integers(0, 256, 200, dtype=np.uint8).tobytes())
+        except parser_mod.ParseError:
+            pass
+    # tile data corrupted after a valid header: parse completes or fails cleanly
+    bad = bytearray(tus[0])
+    for i in range(len(bad) // 2, len(bad)):
+        bad[i] ^= 0x5A
+    p = parser_mod.Parser()
+    try:
+        p.decode_tu(bytes(bad))
+    except parser_mod.ParseError:
+        pass
+
+
+def test_parser_empty_and_delimiter_only(parser_mod):
+    p = parser_mod.Parser()
+    assert p.decode_tu(b"") == []
+    assert p.decode_tu(bytes([0x12, 0x00])) == []  # temporal delimiter OBU
+    with pytest.raises(parser_mod.ParseError):  # a frame header before any sequence header
+        p.decode_tu(bytes([0x1A, 0x01, 0x00]))
+
+
+@needs_bits
+def test_parser_streams_are_independent(parser_mod):
+    """Two contexts interleaved give the same batches as each alone (no shared state)."""
+    a, b = "av1-1-b8-06-mfmv", "av1-1-b8-04-cdfupdate"
+    with open(golden.ivf_path(a), "rb") as f:
+        ta = list(parser_mod.ivf_frames(f.read()))
+    with open(golden.ivf_path(b), "rb") as f:
+        tb = list(parser_mod.ivf_frames(f.read()))
+    pa, pb = parser_mod.Parser(), parser_mod.Parser()
+    fa, fb = [], []
+    for i in range(max(len(ta), len(tb))):
+        if i < len(ta):
+            fa += pa.decode_tu(ta[i])
+        if i < len(tb):
+            fb += pb.decode_tu(tb[i])
+    for stream, frames in ((a, fa), (b, fb)):
+        gold = batchfile.load(golden.batch_path(stream))
+        assert len(frames) == len(gold)
+        assert all(_same(f, g) for f, g in zip(frames, gold))

@@ -37,7 +37,9 @@ def one(stream):
         r = subprocess.run([REFDUMP, src, b, h], capture_output=True, text=True)
         if r.returncode != 0:
             return stream, False, r.stderr.strip()[-200:]
-        with open(b, "rb") as f, gzip.open(os.path.join(GOLD, "batches", stream + ".av1b.gz"), "wb", 9) as g:
+        # mtime=0: the same batches give byte-identical fixtures (regeneration is checkable)
+        with open(b, "rb") as f, open(os.path.join(GOLD, "batches", stream + ".av1b.gz"), "wb") as raw, \
+                gzip.GzipFile(fileobj=raw, mode="wb", compresslevel=9, mtime=0) as g:
             shutil.copyfileobj(f, g)
         shutil.copy(h, os.path.join(GOLD, "hashes", stream + ".txt"))
     return stream, True, ""

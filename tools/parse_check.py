@@ -55,19 +55,6 @@ def rec_diff(name, a, b, dtype, limit=3):
     return out
 
 
-def sanitize_blocks(raw):
-    """Zero the block fields the reference leaves uninitialised for this kind of block (the
-    fixtures written before refdump cleared them hold heap garbage there)."""
-    r = raw.view(abi.BLOCK_DTYPE).copy()
-    inter = (r["flags"] & 1) != 0
-    r["uv_mode"][inter] = 0
-    r["filter_intra_mode"][(r["flags"] & (1 << 4)) == 0] = 0
-    nocfl = inter | (r["uv_mode"] != 13) | ((r["flags"] & (1 << 3)) == 0)
-    r["cfl_alpha_u"][nocfl] = 0
-    r["cfl_alpha_v"][nocfl] = 0
-    return r.view(np.uint8)
-
-
 def compare(frames, gold):
     problems = []
     if len(frames) != len(gold):
@@ -76,7 +63,7 @@ def compare(frames, gold):
         d = hdr_diff(f.hdr, g.hdr)
         if not f.show_existing:
             d += rec_diff("mi", f.sec["mi"], g.sec["mi"], abi.MI_DTYPE)
-            d += rec_diff("blocks", sanitize_blocks(f.sec["blocks"]), sanitize_blocks(g.sec["blocks"]), abi.BLOCK_DTYPE)
+            d += rec_diff("blocks", f.sec["blocks"], g.sec["blocks"], abi.BLOCK_DTYPE)
             d += rec_diff("tbs", f.sec["tbs"], g.sec["tbs"], abi.TB_DTYPE)
             for s in ("coefs", "palette", "cdef", "lr"):
                 if not np.array_equal(f.sec[s], g.sec[s]):
