@@ -1,0 +1,174 @@
+// decoder.cpp -- the whole decoder behind the reference's API: YamiAv1::Decoder
+// (include/YamiAv1/Av1Decoder.h) and its C-ABI (include/av1dec.h).
+//
+// Decoder::decode (oddstone/av1dec decoder/Av1Decoder.cpp:49-109) parses a temporal unit and,
+// per frame, walks the tile trees (decodeFrame, 128-156) or shows a stored frame
+// (showExistingFrame, 158-169).  Here the parse is the host parser (av1p_decode_tu) and each
+// parsed frame goes to the MI355X backend as one batch (av1r_decode_frame) -- asynchronous:
+// the host parses frame t+1 while the GPU reconstructs frame t.  getOutput copies the oldest
+// shown frame back (av1r_get_output, which waits for that frame only).
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "YamiAv1/Av1Decoder.h"
+#include "av1dec.h"
+#include "av1p.h"
+#include "av1r.h"
+
+struct av1d_ctx {
+    av1p_ctx* parser = nullptr;
+    av1r_ctx* recon = nullptr;
+    std::string err;
+    int fail(int rc, const char* what, const char* detail)
+    {
+        err = std::string(what) + ": " + (detail ? detail : "");
+        return rc;
+    }
+};
+
+extern "C" {
+
+int av1d_create(int device, av1d_ctx** out)
+{
+    if (!out) return AV1R_E_INVALID;
+    *out = nullptr;
+    av1d_ctx* c = new (std::nothrow) av1d_ctx;
+    if (!c) return AV1R_E_NOMEM;
+    int rc = av1p_create(&c->parser);
+    if (!rc) rc = av1r_create(device, &c->recon);
+    if (rc) {
+        av1d_destroy(c);
+        return rc;
+    }
+    av1r_set_keep_stages(c->recon, 0);  // no per-stage snapshots: output only
+    *out = c;
+    return AV1R_OK;
+}
+
+void av1d_destroy(av1d_ctx* c)
+{
+    if (!c) return;
+    if (c->recon) av1r_destroy(c->recon);
+    if (c->parser) av1p_destroy(c->parser);
+    delete c;
+}
+
+int av1d_decode(av1d_ctx* c, const uint8_t* data, size_t size)
+{
+    if (!c) return AV1R_E_INVALID;
+    if (!data || !size) return AV1R_OK;  // end of stream: nothing buffered to flush
+    int n = 0;
+    int rc = av1p_decode_tu(c->parser, data, size, &n);
+    // frames the unit completed before a failure are still reconstructed, as the reference
+    // decodes each frame as soon as its last tile group is parsed
+    for (int i = 0; i < n; i++) {
+        const av1r_frame_batch* b = av1p_frame(c->parser, i);
+        const av1r_frame_hdr* h = b->hdr;
+        int r = h->show_existing_frame ? av1r_show_existing(c->recon, h->frame_to_show, h->refresh_frame_flags)
+                                       : av1r_decode_frame(c->recon, b);
+        if (r) return c->fail(r, "reconstruction", av1r_last_error(c->recon));
+    }
+    if (rc) return c->fail(rc, "parse", av1p_last_error(c->parser));
+    return AV1R_OK;
+}
+
+int av1d_output_size(av1d_ctx* c, int* width, int* height)
+{
+    if (!c) return AV1R_E_INVALID;
+    if (!av1r_output_pending(c->recon)) return AV1R_E_NO_OUTPUT;
+    return av1r_get_output(c->recon, nullptr, 0, nullptr, 0, nullptr, 0, width, height);
+}
+
+int av1d_get_output(av1d_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height)
+{
+    if (!c) return AV1R_E_INVALID;
+    if (!av1r_output_pending(c->recon)) return AV1R_E_NO_OUTPUT;
+    const int rc = av1r_get_output(c->recon, y, ys, u, us, v, vs, width, height);
+    if (rc) return c->fail(rc, "output", av1r_last_error(c->recon));
+    return AV1R_OK;
+}
+
+const char* av1d_last_error(av1d_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+}  // extern "C"
+
+// ---- C++ facade ----
+namespace Yami {
+
+std::shared_ptr<YuvFrame> YuvFrame::create(int width, int height)
+{
+    std::shared_ptr<YuvFrame> f(new YuvFrame);
+    const int cw = (width + 1) >> 1, ch = (height + 1) >> 1;
+    const size_t ySize = (size_t)width * height, cSize = (size_t)cw * ch;
+    f->m_buffer = (uint8_t*)malloc(ySize + 2 * cSize);
+    if (!f->m_buffer) return nullptr;
+    f->width = width;
+    f->height = height;
+    f->data[0] = f->m_buffer;
+    f->data[1] = f->m_buffer + ySize;
+    f->data[2] = f->m_buffer + ySize + cSize;
+    f->strides[0] = f->widths[0] = width;
+    f->heights[0] = height;
+    for (int p = 1; p < 3; p++) {
+        f->strides[p] = f->widths[p] = cw;
+        f->heights[p] = ch;
+    }
+    return f;
+}
+
+YuvFrame::~YuvFrame() { free(m_buffer); }
+
+}  // namespace Yami
+
+namespace YamiAv1 {
+
+struct Decoder::Impl {
+    av1d_ctx* ctx = nullptr;
+    int64_t pts = 0;
+    std::string err;
+};
+
+Decoder::Decoder(int device) : m_impl(new Impl)
+{
+    const int rc = av1d_create(device, &m_impl->ctx);
+    if (rc) m_impl->err = "av1d_create failed with status " + std::to_string(rc);
+}
+
+Decoder::~Decoder()
+{
+    av1d_destroy(m_impl->ctx);
+    delete m_impl;
+}
+
+bool Decoder::decode(uint8_t* data, size_t size)
+{
+    if (!m_impl->ctx) return false;
+    if (av1d_decode(m_impl->ctx, data, size)) {
+        m_impl->err = av1d_last_error(m_impl->ctx);
+        return false;
+    }
+    return true;
+}
+
+std::shared_ptr<Yami::YuvFrame> Decoder::getOutput()
+{
+    if (!m_impl->ctx) return nullptr;
+    int w = 0, h = 0;
+    if (av1d_output_size(m_impl->ctx, &w, &h)) return nullptr;
+    std::shared_ptr<Yami::YuvFrame> f = Yami::YuvFrame::create(w, h);
+    if (!f) return nullptr;
+    if (av1d_get_output(m_impl->ctx, f->data[0], f->strides[0], f->data[1], f->strides[1], f->data[2], f->strides[2], &w,
+                        &h)) {
+        m_impl->err = av1d_last_error(m_impl->ctx);
+        return nullptr;
+    }
+    f->pts = m_impl->pts++;
+    return f;
+}
+
+const std::string& Decoder::lastError() const { return m_impl->err; }
+
+}  // namespace YamiAv1

@@ -467,7 +467,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         int sub = p ? 1 : 0;
         c->mapW[p] = (((h->mi_stride * 4) >> sub) + 64) / 4;
         c->mapH[p] = (((h->mi_rows_alloc * 4) >> sub) + 64) / 4;
-        c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
+        // k_flow only (flowOnly): the levels just order the items, dependencies carry the
+        // hand-offs, so the inter predictions' level 0 is the map's initial value and the
+        // plain inter blocks need not be painted (below)
+        c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], flowOnly ? 0 : -1);
         c->owner[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
         c->emit[p].assign((size_t)c->mapW[p] * c->mapH[p], 0);
     }
@@ -623,12 +626,15 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 iiNode = c->nodeOfBlk[bi] = end_node();
             }
             globalMax = std::max(globalMax, blkLevel);
-            for (int p = 0; p < nPlanes; p++) {
-                int sub = p ? 1 : 0;
-                int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
-                region_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], blkLevel);
-                own_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], iiNode);
-            }
+            // (flowOnly: a plain inter block is level 0 and owns nothing -- the maps' initial
+            // values -- so it is not painted; blocks never overlap)
+            if (!flowOnly || isII)
+                for (int p = 0; p < nPlanes; p++) {
+                    int sub = p ? 1 : 0;
+                    int psz = p ? av1r_ss420[blk.mi_size] : blk.mi_size;
+                    region_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], blkLevel);
+                    own_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], iiNode);
+                }
         }
         int lumaMax = -1;  // CFL reads this block's reconstructed luma
         for (uint32_t ti = blk.first_tb; ti < blk.first_tb + blk.n_tbs; ti++) {

@@ -22,11 +22,26 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(ROOT, "include")]
 
 
+# host-only C++ linked into the same library: the parser (include/av1p.h) and the
+# whole-decoder facade (include/av1dec.h, include/YamiAv1/Av1Decoder.h)
+HOST_SRCS = [("parse/obu.cpp", "p_obu"), ("parse/block.cpp", "p_block"), ("parse/api.cpp", "p_api"),
+             ("app/decoder.cpp", "app_decoder")]
+CLI = os.path.join(BUILD, "av1dec")
+
+
+def _host_cmd(src, obj):
+    return [os.environ.get("CXX", "g++"), "-std=c++17", "-O2", "-fPIC", "-Wall", "-Wno-class-memaccess",
+            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc", "parse"), "-c",
+            os.path.join(PKG, "csrc", src), "-o", obj]
+
+
 def _stale():
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(CLI):
         return True
-    t = os.path.getmtime(LIB)
+    t = min(os.path.getmtime(LIB), os.path.getmtime(CLI))
     deps = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc"))]
+    for sub in ("parse", "app"):
+        deps += [os.path.join(PKG, "csrc", sub, f) for f in os.listdir(os.path.join(PKG, "csrc", sub))]
     deps += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
     return any(os.path.getmtime(d) > t for d in deps)
 
@@ -53,12 +68,23 @@ def build(force=False, jobs=3, out=None, defines=(), src_flags=None):
         if len(procs) >= jobs:
             if procs.pop(0).wait() != 0:
                 raise RuntimeError("hipcc failed")
+    for src, name in HOST_SRCS:
+        obj = os.path.join(BUILD, name + tag + ".o")
+        procs.append(subprocess.Popen(_host_cmd(src, obj)))
+        objs.append(obj)
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
     tmp = lib_path + ".tmp"
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
     os.replace(tmp, lib_path)
+    if out is None:
+        # the command-line decoder (tests/Av1Dec.cpp's counterpart), linked to this library
+        tmp = CLI + ".tmp"
+        subprocess.check_call([os.environ.get("CXX", "g++"), "-std=c++17", "-O2", "-I" + os.path.join(ROOT, "include"),
+                               "-o", tmp, os.path.join(PKG, "csrc", "app", "av1dec.cpp"), "-L" + BUILD, "-lav1r",
+                               "-Wl,-rpath,$ORIGIN"])
+        os.replace(tmp, CLI)
     return lib_path
 
 

@@ -118,6 +118,24 @@ class StreamScheduler:
         self.ex = ThreadPoolExecutor(max(1, workers)) if self.packed else None
         self.pos = [0] * len(decs)
         self.q = [[] for _ in decs]  # packed: per stream, futures of its next frames
+        # host profile of the packed pipeline: worker seconds in av1r_pack, launching-thread
+        # seconds waiting for packed frames and inside av1r_decode_packed_batch
+        self.prof = {"pack_s": 0.0, "packs": 0, "wait_s": 0.0, "launch_s": 0.0, "launches": 0}
+        self._plock = __import__("threading").Lock()
+
+    def _pack(self, frame):
+        from av1dec_amd import Decoder
+        t = time.perf_counter()
+        p = Decoder.pack(frame)
+        dt = time.perf_counter() - t
+        with self._plock:
+            self.prof["pack_s"] += dt
+            self.prof["packs"] += 1
+        return p
+
+    def reset_prof(self):
+        for k in self.prof:
+            self.prof[k] = 0 if k in ("packs", "launches") else 0.0
 
     def _item(self, j):
         from av1dec_amd import Decoder
@@ -125,15 +143,21 @@ class StreamScheduler:
             return self.handles[j][self.pos[j] % self.F]
         while len(self.q[j]) < self.depth:
             t = (self.pos[j] + len(self.q[j])) % self.F
-            self.q[j].append(self.ex.submit(Decoder.pack, self.streams[j][t]))
-        return self.q[j].pop(0).result()
+            self.q[j].append(self.ex.submit(self._pack, self.streams[j][t]))
+        t0 = time.perf_counter()
+        r = self.q[j].pop(0).result()
+        self.prof["wait_s"] += time.perf_counter() - t0
+        return r
 
     def _launch(self, js):
         from av1dec_amd import Decoder
         items = [self._item(j) for j in js]
         decs = [self.decs[j] for j in js]
         if self.packed:
+            t0 = time.perf_counter()
             Decoder.decode_packed_batch(decs, items)
+            self.prof["launch_s"] += time.perf_counter() - t0
+            self.prof["launches"] += 1
             for p in items:
                 Decoder.free_packed(p)
             for j in js:  # keep the packers `depth` frames ahead
@@ -149,7 +173,7 @@ class StreamScheduler:
         from av1dec_amd import Decoder
         while len(self.q[j]) < self.depth:
             t = (self.pos[j] + 1 + len(self.q[j])) % self.F
-            self.q[j].append(self.ex.submit(Decoder.pack, self.streams[j][t]))
+            self.q[j].append(self.ex.submit(self._pack, self.streams[j][t]))
 
     def stagger(self):
         """Bring stream j alone to frame j*F/S (untimed setup)."""
@@ -271,12 +295,23 @@ def main():
     sync()
     if dist:
         dist.barrier()
+    pp.reset_prof()
     t0 = time.perf_counter()
     timed = pp.run(args.steps)  # (stream, frame) of every frame in the timed region
     sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     fps = aggregate_fps(world, args.steps * S, elapsed)
     n_key = sum(1 for j, t in timed if streams[j][t].hdr.frame_type == 0)
+    pr = pp.prof
+    host_profile = {  # where the host-inclusive pipeline spends its time (rank 0)
+        "workers": workers,
+        "pack_ms_per_frame": round(1e3 * pr["pack_s"] / max(pr["packs"], 1), 3),
+        "pack_worker_utilisation": round(pr["pack_s"] / (workers * elapsed), 3),
+        "launch_thread_ms_per_step": round(1e3 * (pr["launch_s"] + pr["wait_s"]) / max(args.steps, 1), 3),
+        "launch_call_ms_per_batch": round(1e3 * pr["launch_s"] / max(pr["launches"], 1), 3),
+        "wait_packed_ms_per_step": round(1e3 * pr["wait_s"] / max(args.steps, 1), 3),
+        "batches": pr["launches"],
+    }
     pp.close()
 
     # ---- device-only rate: the same streams with every batch already validated, scheduled
@@ -317,11 +352,13 @@ def main():
     dominant = max(names, key=lambda n: per_frame_ms[n])
     achieved = sb[dominant] / (per_frame_ms[dominant] * 1e-3) / 1e9
     traffic = None
+    traffic_src = None  # which PMC measurement (and at which commit) the traffic figure is
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
             if tj.get("config") == args.config and tj.get("streams", 1) == S and dominant in tj.get("stages", {}):
                 traffic = tj["stages"][dominant]
+                traffic_src = {"file": os.path.relpath(args.traffic, ROOT), "git_head": tj.get("git_head")}
         except Exception:
             traffic = None
 
@@ -420,12 +457,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "bytes_per_frame": int(sb[dominant]),
                          "ms_per_frame": round(per_frame_ms[dominant], 4)},
             "stage_ms_per_frame": {n: round(v, 4) for n, v in per_frame_ms.items()},
             "recon_kernel_ms_per_frame": {n: round(v / max(nfr, 1), 4) for n, v in zip(("k_inter", "k_resid", "k_flow"), ktot)},
             "stage_algorithmic_GBps": {n: round(sb[n] / max(per_frame_ms[n], 1e-9) / 1e6, 2) for n in names},
             "device_only_fps": round(device_fps, 3),
+            "host_profile": host_profile,
             "single_stream_fps": round(single_fps, 3),
             "decode_frame_fps_1thread": round(host_fps, 3),
             "decode_frame_fps_threads": host_mt_fps,

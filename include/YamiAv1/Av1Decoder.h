@@ -1,0 +1,68 @@
+// Av1Decoder.h -- drop-in for the reference decoder's public class (oddstone/av1dec,
+// decoder/Av1Decoder.h:47-70 and decoder/VideoFrame.h:34-48): the same names, signatures and
+// semantics, backed by the host parser (include/av1p.h) and the MI355X reconstruction
+// backend (include/av1r.h).  An application written against YamiAv1::Decoder -- like the
+// reference's own tests/Av1Dec.cpp -- rebuilds against this header and libav1r.so unchanged.
+//
+//   YamiAv1::Decoder decoder;                    // Decoder::Decoder (Av1Decoder.cpp:40-43)
+//   decoder.decode(data, size);                  // one temporal unit (Av1Decoder.cpp:49-109)
+//   while (auto f = decoder.getOutput()) ...     // shown frames in order (Av1Decoder.cpp:203-211)
+//
+// Differences, by design: decode() runs reconstruction and filtering on the GPU
+// asynchronously and getOutput() waits for the frame it returns; device errors surface as
+// decode() == false or a null getOutput(), with lastError() describing them.
+#ifndef YAMIAV1_AV1DECODER_H
+#define YAMIAV1_AV1DECODER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+
+namespace Yami {
+
+// decoder/VideoFrame.h:34-48 -- an 8-bit I420 frame in host memory
+struct YuvFrame {
+    static const int MAX_PLANES = 3;
+    int64_t pts = 0;
+    int width = 0;
+    int height = 0;
+    uint8_t* data[MAX_PLANES] = {};
+    int strides[MAX_PLANES] = {};
+    int widths[MAX_PLANES] = {};
+    int heights[MAX_PLANES] = {};
+    static std::shared_ptr<YuvFrame> create(int width, int height);
+    ~YuvFrame();
+
+private:
+    uint8_t* m_buffer = nullptr;
+};
+
+}  // namespace Yami
+
+namespace YamiAv1 {
+
+class Decoder {
+public:
+    // device: HIP device ordinal (the reference has no device; 0 by default)
+    explicit Decoder(int device = 0);
+    ~Decoder();
+    Decoder(const Decoder&) = delete;
+    Decoder& operator=(const Decoder&) = delete;
+    // Parse one temporal unit and queue its frames for reconstruction (returns false on a
+    // parse error, an unsupported stream or a device error).
+    bool decode(uint8_t* data, size_t size);
+    // The oldest shown frame not yet returned, or nullptr if none is pending.
+    std::shared_ptr<Yami::YuvFrame> getOutput();
+    // Not in the reference: the message of the last failure.
+    const std::string& lastError() const;
+
+private:
+    struct Impl;
+    Impl* m_impl;
+};
+
+}  // namespace YamiAv1
+
+#endif
