@@ -4,7 +4,7 @@ Only the structs Python needs to build or inspect are mirrored; sizes are checke
 against the C library's av1r_sizeof() at load time (see native.py) and in tests."""
 import ctypes as C
 
-AV1R_VERSION = 1
+AV1R_VERSION = 2
 
 AV1R_OK = 0
 AV1R_E_INVALID = -1
@@ -63,7 +63,7 @@ class FrameBatch(C.Structure):
 
 # record sizes (bytes) of the array element structs in av1r.h
 SIZEOF_MI = 24
-SIZEOF_BLOCK = 68
+SIZEOF_BLOCK = 84
 SIZEOF_TB = 20
 SIZEOF_LR_UNIT = 12
 
@@ -82,7 +82,8 @@ BLOCK_DTYPE = _np.dtype([
     ("motion_mode", "u1"), ("compound_type", "u1"), ("interintra_mode", "u1"), ("wedge_index", "u1"),
     ("wedge_sign", "u1"), ("mask_type", "u1"), ("ii_edge", "u1"), ("pad0", "u1", (2,)), ("flags", "<u4"),
     ("max_luma_w", "<u2"), ("max_luma_h", "<u2"), ("local_warp", "<i4", (6,)), ("palette_off", "<u4"),
-    ("first_tb", "<u4"), ("n_tbs", "<u4")])
+    ("first_tb", "<u4"), ("n_tbs", "<u4"), ("mv", "<i2", (2, 2)), ("ref_frame", "i1", (2,)), ("filt", "u1"),
+    ("pad1", "u1"), ("delta_lf", "i1", (4,))])
 TB_DTYPE = _np.dtype([
     ("block", "<u4"), ("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("coef_cnt", "<u2"),
     ("plane", "u1"), ("tx_size", "u1"), ("tx_type", "u1"), ("flags", "u1"), ("pad", "u1", (2,))])

@@ -75,6 +75,8 @@ struct KParams {
     uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;
     int mi_cols, mi_rows;
+    int mi_rows_alloc;
+    uint32_t n_blocks, n_tbs;  // k_mi: the records the mode-info grid is derived from
     int frame_w, frame_h;
     DevFrame cur;     // frame under reconstruction, deblocked in place
     DevFrame cdef;    // CDEF output (Cdef::filter's copy, Cdef.cpp:43)

@@ -36,6 +36,7 @@ void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipS
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
+void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s);
 #ifdef AV1R_FLOW_DEBUG
 uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset);
 #endif
@@ -92,7 +93,8 @@ struct Prepared {
     uint32_t nResidS = 0, nResidL = 0;  // k_resid workgroups (16 TBs / 1 TB each)
     size_t resElems = 0;                // int16 residual tiles of the frame
     bool usedRef[8] = {};
-    uint64_t bytes = 0;
+    uint64_t bytes = 0;    // the packed layout (incl. the device-filled mode-info grid)
+    size_t upBytes = 0;    // its uploaded prefix
     bool offsets = false;  // packed in host memory: base pointers are offsets into the upload
 };
 
@@ -350,32 +352,28 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
     int sb4 = h->sb128 ? 32 : 16;
     if (h->mi_stride < ((h->mi_cols + sb4 - 1) / sb4) * sb4 || h->mi_rows_alloc < ((h->mi_rows + sb4 - 1) / sb4) * sb4)
         return fail(c, AV1R_E_INVALID, "mode-info grid smaller than the SB-aligned frame");
-    if (!b->mi || !b->cdef_idx) return fail(c, AV1R_E_INVALID, "missing mode-info or cdef grid");
+    if (!b->cdef_idx) return fail(c, AV1R_E_INVALID, "missing cdef grid");
     if (h->cdef_rows != (h->mi_rows + 15) / 16 || h->cdef_cols != (h->mi_cols + 15) / 16)
         return fail(c, AV1R_E_INVALID, "cdef grid dims");
     for (int i = 0; i < h->cdef_rows * h->cdef_cols; i++)
         if (b->cdef_idx[i] < -1 || b->cdef_idx[i] > 7) return fail(c, AV1R_E_INVALID, "cdef_idx out of range");
     const int aw4 = h->mi_stride, ah4 = h->mi_rows_alloc;
-    // mode info: sizes, tx sizes, refs (and the slots they resolve to).  One branch-free
-    // pass accumulating the violations; the slow pass names the first one
+    // the blocks' reference frames (and the slots they resolve to): one branch-free pass
+    // accumulating the violations; the block loop below names the first one.  (The mode-info
+    // grid is not read: the device derives it from the blocks and transform blocks.)
     bool* usedRef = c->usedRef;
     memset(c->usedRef, 0, sizeof(c->usedRef));
     uint32_t bad = 0, refs = 0;
-    for (int i = 0; i < aw4 * ah4; i++) {
-        const av1r_mi& m = b->mi[i];
-        bad |= (m.mi_size >= AV1R_BLOCK_SIZES) | (m.lf_tx[0] >= AV1R_TX_SIZES) | (m.lf_tx[1] >= AV1R_TX_SIZES) |
-               (m.lf_tx[2] >= AV1R_TX_SIZES) | ((uint8_t)(m.ref_frame[0] + 1) > 8) | ((uint8_t)(m.ref_frame[1] + 1) > 8) |
-               ((m.filt & 15) > 3) | ((m.filt >> 4) > 3);
-        refs |= (1u << ((m.ref_frame[0] + 1) & 15)) | (1u << ((m.ref_frame[1] + 1) & 15));
+    for (uint32_t i = 0; i < b->n_blocks; i++) {
+        const av1r_block& k = b->blocks[i];
+        bad |= ((uint8_t)(k.ref_frame[0] + 1) > 8) | ((uint8_t)(k.ref_frame[1] + 1) > 8) | ((k.filt & 15) > 3) | ((k.filt >> 4) > 3);
+        refs |= (1u << ((k.ref_frame[0] + 1) & 15)) | (1u << ((k.ref_frame[1] + 1) & 15));
     }
-    for (int i = 0; bad && i < aw4 * ah4; i++) {
-        const av1r_mi& m = b->mi[i];
-        if (m.mi_size >= AV1R_BLOCK_SIZES) return fail(c, AV1R_E_INVALID, "mi_size");
-        for (int p = 0; p < 3; p++)
-            if (m.lf_tx[p] >= AV1R_TX_SIZES) return fail(c, AV1R_E_INVALID, "lf tx size");
+    for (uint32_t i = 0; bad && i < b->n_blocks; i++) {
+        const av1r_block& k = b->blocks[i];
         for (int l = 0; l < 2; l++)
-            if (m.ref_frame[l] < -1 || m.ref_frame[l] > 7) return fail(c, AV1R_E_INVALID, "ref_frame");
-        if ((m.filt & 15) > 3 || (m.filt >> 4) > 3) return fail(c, AV1R_E_INVALID, "interp filter");
+            if (k.ref_frame[l] < -1 || k.ref_frame[l] > 7) return fail(c, AV1R_E_INVALID, "block %u ref_frame", i);
+        if ((k.filt & 15) > 3 || (k.filt >> 4) > 3) return fail(c, AV1R_E_INVALID, "block %u interp filter", i);
     }
     for (int r = 1; r < 8; r++) usedRef[r] = (refs >> (r + 1)) & 1;
     for (int r = 1; r < 8 && !c->skipSlotCheck; r++) {
@@ -421,11 +419,13 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
         if (t.x + av1r_tx_w[t.tx_size] > ((aw4 * 4) >> sub) + 64 || t.y + av1r_tx_h[t.tx_size] > ((ah4 * 4) >> sub) + 64)
             return fail(c, AV1R_E_INVALID, "tb %u outside the frame", i);
         if ((uint64_t)t.coef_off + t.coef_cnt > b->n_coefs) return fail(c, AV1R_E_INVALID, "tb %u coefficients", i);
-        const uint32_t area = (uint32_t)std::min<int>(av1r_tx_w[t.tx_size], 32) * std::min<int>(av1r_tx_h[t.tx_size], 32);
-        uint32_t posBad = 0;
+        // positions < area = min(w,32) * min(h,32), a power of two: no position has a bit at
+        // or above log2(area) set, so one OR over the TB's coefficients decides (vectorised)
+        const int log2Area = std::min<int>(av1r_tx_w_log2[t.tx_size], 5) + std::min<int>(av1r_tx_h_log2[t.tx_size], 5);
+        uint32_t acc = 0;
         const uint32_t* cf = b->coefs + t.coef_off;
-        for (int q = 0; q < t.coef_cnt; q++) posBad |= AV1R_COEF_POS(cf[q]) >= (int)area;
-        if (posBad) return fail(c, AV1R_E_INVALID, "tb %u coefficient position", i);
+        for (int q = 0; q < t.coef_cnt; q++) acc |= cf[q];
+        if ((acc & 1023u) >> log2Area) return fail(c, AV1R_E_INVALID, "tb %u coefficient position", i);
         const av1r_block& k = b->blocks[t.block];
         if (!(k.flags & AV1R_BLK_INTER) && (t.plane ? k.palette_size_uv : k.palette_size_y)) {
             const uint8_t* ph = b->palette + k.palette_off;
@@ -451,6 +451,23 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
 }
 
 // ------------------------------------------------------------------------------------
+// av1r_pack profile (AV1R_PACK_PROF=1): nanoseconds per phase, summed over every thread
+// ------------------------------------------------------------------------------------
+enum { PP_VALIDATE, PP_SCHED_INIT, PP_SCHED_BLOCKS, PP_SCHED_ITEMS, PP_SCHED_DEPS, PP_COPY, PP_N };
+static std::atomic<uint64_t> g_packNs[PP_N + 1];  // [PP_N]: packed frames
+static const bool g_packProf = getenv("AV1R_PACK_PROF") && atoi(getenv("AV1R_PACK_PROF")) != 0;
+struct PackClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(int phase)
+    {
+        if (!g_packProf) return;
+        const auto n = std::chrono::steady_clock::now();
+        g_packNs[phase] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count();
+        t = n;
+    }
+};
+
+// ------------------------------------------------------------------------------------
 // dependency levels
 // ------------------------------------------------------------------------------------
 // flowOnly: the frame will run on k_flow (av1r_pack; no intra block copy), so inter TBs
@@ -460,6 +477,7 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
 static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
 {
     const av1r_frame_hdr* h = b->hdr;
+    PackClock clk;
     if (flowOnly)
         for (uint32_t i = 0; i < b->n_blocks && flowOnly; i++) flowOnly = !(b->blocks[i].flags & AV1R_BLK_INTRABC);
     c->levelsOk = !flowOnly;
@@ -593,13 +611,14 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         v[lv].push_back(item);
     };
     int globalMax = -1;
+    clk.lap(PP_SCHED_INIT);
     for (uint32_t bi = 0; bi < b->n_blocks; bi++) {
         const av1r_block& blk = b->blocks[bi];
         const bool inter = blk.flags & AV1R_BLK_INTER;
         const int nPlanes = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
         int blkLevel = -1;  // level after which the block's prediction is complete
         if (inter) {
-            const bool isII = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col].ref_frame[1] == AV1R_INTRA_FRAME;
+            const bool isII = blk.ref_frame[1] == AV1R_INTRA_FRAME;
             // intra block copy reads already-decoded pixels of the current frame
             const int pLevel = (blk.flags & AV1R_BLK_INTRABC) ? globalMax + 1 : 0;
             const int bw = av1r_num4x4w[blk.mi_size] * 4, bh = av1r_num4x4h[blk.mi_size] * 4;
@@ -683,6 +702,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         return;
     }
     const size_t nl = (size_t)(globalMax + 1);
+    clk.lap(PP_SCHED_BLOCKS);
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
         if (v->size() < nl) v->resize(nl);
     c->items.clear();
@@ -711,7 +731,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         const int bs = blk.mi_size;
         if (av1r_num4x4w[bs] > 4 || av1r_num4x4h[bs] > 4) return 0;
         if (blk.motion_mode != AV1R_SIMPLE_TRANSLATION || (blk.flags & AV1R_BLK_INTRABC)) return 0;
-        const av1r_mi& info = b->mi[(size_t)blk.mi_row * h->mi_stride + blk.mi_col];
+        const av1r_block& info = blk;  // (its mode info)
         if (info.ref_frame[1] > AV1R_INTRA_FRAME && blk.compound_type != AV1R_COMPOUND_AVERAGE &&
             blk.compound_type != AV1R_COMPOUND_DISTANCE)
             return 0;
@@ -776,6 +796,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         }
     }
     c->nLevelsLast = (int)nl;
+    clk.lap(PP_SCHED_ITEMS);
     // k_resid: residual tiles for intra TBs and the TBs of inter-intra blocks; the other
     // inter TBs are added in place
     c->tbRes.assign(b->n_tbs, ~0u);
@@ -836,6 +857,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->items[pos].pub = 1;
         }
     }
+    clk.lap(PP_SCHED_DEPS);
     if (flowOnly && !c->flowOk) build_schedule(c, b, allowGran, false);  // k_flow cannot take it: levels too
 }
 
@@ -858,7 +880,8 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szTbRes = align256(4 * c->tbRes.size() + 4);
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
-    *need = szHdr + szMi + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL;
+    // the mode-info grid goes last and is not uploaded: k_mi derives it in place
+    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi;
     if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {
@@ -870,7 +893,6 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     KParams& k = P.base;
     memset(&k, 0, sizeof(k));
     k.hdr = (const av1r_frame_hdr*)put(h, sizeof(av1r_frame_hdr), szHdr);
-    k.mi = (const av1r_mi*)put(b->mi, sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc, szMi);
     k.blocks = (const av1r_block*)put(b->blocks, sizeof(av1r_block) * (size_t)b->n_blocks, szBlk);
     k.tbs = (const av1r_tb*)put(b->tbs, sizeof(av1r_tb) * (size_t)b->n_tbs, szTb);
     k.coefs = (const uint32_t*)put(b->coefs, 4 * (size_t)b->n_coefs, szCoef);
@@ -884,6 +906,8 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.tb_res = (const uint32_t*)put(c->tbRes.data(), 4 * c->tbRes.size(), szTbRes);
     k.resid_s = (const uint32_t*)put(c->residS.data(), 4 * c->residS.size(), szResS);
     k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
+    P.upBytes = off;  // everything up to here travels; the grid below is filled on the device
+    k.mi = (const av1r_mi*)put(nullptr, 0, szMi);
     P.flowOk = c->flowOk;
     k.gran = c->flowOk && c->granOk;
     for (int p = 0; p < 3; p++) {
@@ -896,6 +920,9 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.mi_stride = h->mi_stride;
     k.mi_cols = h->mi_cols;
     k.mi_rows = h->mi_rows;
+    k.mi_rows_alloc = h->mi_rows_alloc;
+    k.n_blocks = b->n_blocks;
+    k.n_tbs = b->n_tbs;
     k.frame_w = h->frame_width;
     k.frame_h = h->frame_height;
     P.hdr = *h;
@@ -1029,7 +1056,7 @@ static void job_end(FrameJob& j)
         }
     frame_unref(c, out);
     c->nLevelsLast = (int)j.P->levels.size();
-    c->lastUploadBytes = j.P->bytes;
+    c->lastUploadBytes = j.P->upBytes;
 }
 
 // AV1R_FLOW_CHAIN=1: the k_flow launches of a device form ONE chain (each waits for the
@@ -1266,6 +1293,15 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // ---- reconstruction, level by level (frame parameters in a constant-memory slot)
     // the frames' KParams head the metadata buffer (read through the constant address space)
     const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
+    {  // the frames' mode-info grids, derived on the device from their blocks and TBs
+        uint32_t maxUnits = 0, maxBlocks = 0, maxTbs = 0;
+        for (auto& j : jobs) {
+            maxUnits = std::max(maxUnits, (uint32_t)(j.k.mi_stride * j.k.mi_rows_alloc));
+            maxBlocks = std::max(maxBlocks, j.k.n_blocks);
+            maxTbs = std::max(maxTbs, j.k.n_tbs);
+        }
+        launch_k_mi(dk, n, maxUnits, maxBlocks, maxTbs, st);
+    }
     size_t allItems = 0;
     for (uint32_t v : total) allItems += v;
     allItems = std::max<size_t>(allItems, frameRows);
@@ -1457,7 +1493,7 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
         U.cap = cap;
     }
     pack_frame(c, b, P, U.host, U.dev, &need);
-    HIPCHK(hipMemcpyAsync(U.dev, U.host, need, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(U.dev, U.host, P.upBytes, hipMemcpyHostToDevice, c->stream));
     rc = launch_frame(c, P);
     if (rc) return rc;
     HIPCHK(hipEventRecord(U.done, c->stream));
@@ -1671,7 +1707,7 @@ int av1r_prepare(av1r_ctx* c, const av1r_frame_batch* b, int* handle)
         P->owned = true;
         P->cap = need;
         pack_frame(c, b, *P, host.data(), P->dev, &need);
-        if (hipMemcpy(P->dev, host.data(), need, hipMemcpyHostToDevice) != hipSuccess) {
+        if (hipMemcpy(P->dev, host.data(), P->upBytes, hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(P->dev);
             delete P;
             return fail(c, AV1R_E_DEVICE, "prepared batch upload");
@@ -1795,13 +1831,16 @@ int av1r_pack(const av1r_frame_batch* b, av1r_packed** out)
     P.hdr = *b->hdr;
     if (!b->hdr->show_existing_frame) {
         c->skipSlotCheck = true;
+        PackClock clk;
         int rc = validate(c, b);
+        clk.lap(PP_VALIDATE);
         c->skipSlotCheck = false;
         if (rc) {
             av1r_packed_free(pk);
             return rc;
         }
         build_schedule(c, b, true, true);
+        clk = PackClock();
         size_t need = 0;
         pack_frame(c, b, P, nullptr, nullptr, &need);
         if (pk->cap < need) {
@@ -1816,11 +1855,22 @@ int av1r_pack(const av1r_frame_batch* b, av1r_packed** out)
             }
         }
         pack_frame(c, b, P, pk->host, nullptr, &need);
+        clk.lap(PP_COPY);
+        if (g_packProf) g_packNs[PP_N]++;
         P.cap = need;
         P.offsets = true;
     }
     *out = pk;
     return AV1R_OK;
+}
+
+int av1r_pack_profile(uint64_t* ns, int n, int reset)
+{
+    const int m = n < PP_N + 1 ? n : PP_N + 1;
+    for (int i = 0; i < m && ns; i++) ns[i] = g_packNs[i].load();
+    if (reset)
+        for (auto& v : g_packNs) v = 0;
+    return g_packProf ? PP_N : 0;
 }
 
 void av1r_packed_free(av1r_packed* pk)
@@ -1830,7 +1880,7 @@ void av1r_packed_free(av1r_packed* pk)
     g_packFree.push_back(pk);
 }
 
-size_t av1r_packed_bytes(const av1r_packed* pk) { return pk ? pk->P.bytes : 0; }
+size_t av1r_packed_bytes(const av1r_packed* pk) { return pk ? pk->P.upBytes : 0; }
 
 int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int n)
 {
@@ -1879,7 +1929,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             U.cap = pk->P.cap + pk->P.cap / 4 + 65536;
             HIPCHK(hipMalloc(&U.dev, U.cap));
         }
-        HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.cap, hipMemcpyHostToDevice, up->copyStream));
+        HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.upBytes, hipMemcpyHostToDevice, up->copyStream));
         if (!pk->copied) HIPCHK(hipEventCreateWithFlags(&pk->copied, hipEventDisableTiming));
         HIPCHK(hipEventRecord(pk->copied, up->copyStream));
         pk->copyPending = true;

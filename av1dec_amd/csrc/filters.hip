@@ -824,6 +824,82 @@ void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s)
         reinterpret_cast<uint32_t*>(const_cast<void*>(src)), n4);
 }
 
+// ------------------------------------------------------------------------------------
+// k_mi: the mode-info grid of each frame of the launch, derived from its records instead of
+// uploaded (24 B per 4x4 unit: 3.1 MB of a 1080p frame's ~7.6 MB batch).  What the parser
+// stores per 4x4 (Block::parse, Block.cpp:322-362) is the block's mode info over its units;
+// LoopfilterTxSizes is the transform size over the units each transform block covers, the
+// luma units under a chroma one included (TransformBlock::decode, TransformBlock.cpp:
+// 2444-2454); units outside the frame that no block reaches stay zero.  Three launches (one
+// frame per grid row): zero the out-of-frame units, write the blocks' units (16 lanes per
+// block), then the transform blocks' lf_tx bytes.
+// ------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void k_mi_zero(const KParams* kps)
+{
+    const KParams& k = KP(kps, blockIdx.y);
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const int r = (int)(i / (uint32_t)k.mi_stride), c = (int)(i - (uint32_t)r * k.mi_stride);
+    if (r >= k.mi_rows_alloc || (r < k.mi_rows && c < k.mi_cols)) return;
+    uint32_t* d = reinterpret_cast<uint32_t*>(const_cast<av1r_mi*>(k.mi) + i);
+#pragma unroll
+    for (int w = 0; w < 6; w++) d[w] = 0;
+}
+extern "C" __global__ __launch_bounds__(256) void k_mi_blocks(const KParams* kps)
+{
+    const KParams& k = KP(kps, blockIdx.y);
+    const uint32_t bi = blockIdx.x * 16 + (threadIdx.x >> 4);
+    if (bi >= k.n_blocks) return;
+    const av1r_block& b = k.blocks[bi];
+    av1r_mi m;
+    memset(&m, 0, sizeof(m));
+    for (int l = 0; l < 2; l++) {
+        m.mv[l][0] = b.mv[l][0];
+        m.mv[l][1] = b.mv[l][1];
+        m.ref_frame[l] = b.ref_frame[l];
+    }
+    m.mi_size = b.mi_size;
+    m.y_mode = b.y_mode;
+    m.filt = b.filt;
+    m.flags = (uint8_t)(((b.flags & AV1R_BLK_SKIP) ? AV1R_MI_SKIP : 0) | ((b.flags & AV1R_BLK_INTER) ? AV1R_MI_INTER : 0));
+    for (int i = 0; i < 4; i++) m.delta_lf[i] = b.delta_lf[i];
+    m.uv_mode = b.uv_mode;
+    uint32_t w[6];
+    memcpy(w, &m, sizeof(w));
+    const int bw4 = av1r_num4x4w[b.mi_size], bh4 = av1r_num4x4h[b.mi_size], n = bw4 * bh4;
+    for (int q = threadIdx.x & 15; q < n; q += 16) {
+        const int r = b.mi_row + q / bw4, c = b.mi_col + q % bw4;
+        uint32_t* d = reinterpret_cast<uint32_t*>(const_cast<av1r_mi*>(k.mi) + (size_t)r * k.mi_stride + c);
+#pragma unroll
+        for (int i = 0; i < 6; i++) d[i] = w[i];
+    }
+}
+extern "C" __global__ __launch_bounds__(256) void k_mi_tbs(const KParams* kps)
+{
+    const KParams& k = KP(kps, blockIdx.y);
+    const uint32_t ti = blockIdx.x * 256 + threadIdx.x;
+    if (ti >= k.n_tbs) return;
+    const av1r_tb& t = k.tbs[ti];
+    const int sub = t.plane ? 1 : 0;
+    const int row = (t.y << sub) >> 2, col = (t.x << sub) >> 2;
+    const int stepX = av1r_tx_w[t.tx_size] >> 2, stepY = av1r_tx_h[t.tx_size] >> 2;
+    uint8_t* base = reinterpret_cast<uint8_t*>(const_cast<av1r_mi*>(k.mi));
+    for (int i = 0; i < (stepY << sub); i++) {
+        const int r = row + i;
+        if (r >= k.mi_rows_alloc) break;
+        for (int j = 0; j < (stepX << sub); j++) {
+            const int c = col + j;
+            if (c >= k.mi_stride) break;
+            base[((size_t)r * k.mi_stride + c) * sizeof(av1r_mi) + offsetof(av1r_mi, lf_tx) + t.plane] = t.tx_size;
+        }
+    }
+}
+void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mi_zero, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps);
+    if (maxBlocks) hipLaunchKernelGGL(k_mi_blocks, dim3((maxBlocks + 15) / 16, n), dim3(256), 0, s, kps);
+    if (maxTbs) hipLaunchKernelGGL(k_mi_tbs, dim3((maxTbs + 255) / 256, n), dim3(256), 0, s, kps);
+}
+
 // plain visible-region copy (stage snapshots)
 extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 {

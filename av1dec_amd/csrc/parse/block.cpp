@@ -2308,6 +2308,16 @@ void BlockParser::emit(Blk& b)
     }
     rec.palette_size_y = (uint8_t)b.pal_y;
     rec.palette_size_uv = (uint8_t)b.pal_uv;
+    {  // the block's mode info as stored over its 4x4 units (decode_block above)
+        const MiInfo& m = mi(b.r, b.c);
+        for (int l = 0; l < 2; l++) {
+            rec.mv[l][0] = m.mv[l].r;
+            rec.mv[l][1] = m.mv[l].c;
+            rec.ref_frame[l] = m.ref[l];
+        }
+        rec.filt = (uint8_t)((m.interp[0] & 15) | (m.interp[1] << 4));
+        for (int i = 0; i < 4; i++) rec.delta_lf[i] = m.delta_lf[i];
+    }
     uint32_t f = 0;
     const bool ii = b.is_inter && b.interintra && !b.use_intrabc;
     if (b.is_inter) {

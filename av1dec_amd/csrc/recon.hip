@@ -182,7 +182,8 @@ DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int1
 // IntraPredict::predict_intra with CFL (IntraPredict.cpp:563-667).  Inter TBs predict
 // nothing here (their prediction is already in the frame).  Ends with a coop_sync.
 template <int NT, int MAX, bool COH>
-DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, const GranEdges* G = nullptr)
+DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, const GranEdges* G = nullptr,
+    bool gran = false)
 {
     constexpr int CM = TbLds<MAX>::CM;
     const int t = coop_lane<NT>();
@@ -202,12 +203,12 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             L.pred[i * MAX + j] = colors[map[(by + i) * mw + bx + j]];
         }
     } else if (tb.pred == AV1R_PRED_INTRA) {
-        if (COH && G)
+        if (COH && gran)
             coop_intra_edges_gran<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
                 (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
                 (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra, *G);
-        if (COH && G) trace_stamp(G->tr, 8);
-        if (!(COH && G))
+        if (COH && gran) trace_stamp(G->tr, 8);
+        if (!(COH && gran))
             coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
                 (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
                 (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
@@ -1202,7 +1203,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
 // the block's intra prediction (its edges are final when this item runs) blended with the
 // inter prediction inter_tile stored in the frame.
 template <int NT, bool COH>
-DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G = nullptr)
+DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G = nullptr, bool gran = false)
 {
     const int t = coop_lane<NT>();
     const av1r_block& blk = k.blocks[bi];
@@ -1235,7 +1236,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
         P.filterIntraMode = 0;
         P.smooth = 0;
         P.edgeFilter = k.hdr->enable_intra_edge_filter;
-        if (COH && G) {  // k_flow with edge granules: G holds plane 0's, 4 mask words per plane
+        if (COH && gran) {  // k_flow with edge granules: G holds plane 0's, 4 mask words per plane
             GranEdges Gp = *G;
             Gp.mask = G->mask + 4 * plane;
             Gp.h = k.gran_h[plane];
@@ -1297,7 +1298,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
                 const int i = q / pw, j = q - i * pw;
                 stp<COH>(dst, baseX + j, baseY + i, L.pred[i * 64 + j]);
             }
-            if (COH && G)
+            if (COH && gran)
                 coop_publish_gran<NT>(L.pred, 64, baseX, baseY, pw, ph, k.gran_h[plane], k.gran_v[plane], k.gran_w[plane],
                     k.gran_hn[plane], G->epoch);
             coop_sync<NT>();
@@ -1399,10 +1400,13 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const
 
 // 4 waves/SIMD (128 VGPRs, 64 B/lane of spills; LDS 10160 B: 16 workgroups/CU); the
 // -DAV1R_TRACE build keeps its registers (with the stamps it would spill ~1.9 KB/lane)
-#ifdef AV1R_TRACE
+#ifndef AV1R_INTER_WAVES
+#define AV1R_INTER_WAVES 4
+#endif
+#if defined(AV1R_TRACE) || AV1R_INTER_WAVES == 0
 #define K_INTER_BOUNDS __launch_bounds__(64)
 #else
-#define K_INTER_BOUNDS __launch_bounds__(64, 4)
+#define K_INTER_BOUNDS __launch_bounds__(64, AV1R_INTER_WAVES)
 #endif
 extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
@@ -1643,8 +1647,10 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     (void)s;
 #endif
     // edge granules: the item's mask words precede its dependency list (4 per plane)
+    // (G goes to the predictors by address whatever `gran` says: a pointer that is either
+    // &G or null made G a 64 B/lane stack object -- scratch traffic on every item)
     const bool gran = k.gran;
-    GranEdges G;
+    GranEdges G = {};
     if (gran) {
         const int p = AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 0 : wi.plane;
         G.mask = k.deps + wi.dep_off - (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 12 : 4);
@@ -1661,7 +1667,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
             trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
             trace_stamp(tr, 4);
-            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L, gran ? &G : nullptr);
+            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L, &G, gran);
         }
     } else {
         // intra / palette TB: its residual tile (k_resid) is fetched before the wait
@@ -1671,7 +1677,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         trace_stamp(tr, 3);
         flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
         trace_stamp(tr, 4);
-        tb_predict<NT, MAX, true>(k, wi, blk, L, gran ? &G : nullptr);
+        tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran);
         trace_stamp(tr, 9);
         tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
         trace_stamp(tr, 10);

@@ -192,6 +192,7 @@ def lib():
     l.av1r_pack_last_error.restype = C.c_char_p
     l.av1r_decode_packed_batch.argtypes = [C.POINTER(vp), C.POINTER(vp), i]
     l.av1r_busy.argtypes = [vp]
+    l.av1r_pack_profile.argtypes = [C.POINTER(C.c_uint64), i, i]
     _lib = l
     return l
 
@@ -204,5 +205,5 @@ EXPORTS = [
     "av1r_check_batch", "av1r_prepare", "av1r_decode_prepared", "av1r_release_prepared",
     "av1r_set_discard_output", "av1r_stage_times", "av1r_decode_prepared_batch", "av1r_recon_kernel_times",
     "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug", "av1r_pack", "av1r_packed_free",
-    "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy",
+    "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy", "av1r_pack_profile",
 ]

@@ -75,6 +75,20 @@ def stream_seed(config_seed, rank):
     return config_seed + rank
 
 
+def rank_stream_ids(rank, S):
+    """The global stream ids rank `rank` decodes (S per GPU, contiguous): stream i of the job
+    is synthetic seed stream_seed(config_seed, i) -- disjoint shards, no data-path exchange."""
+    return [rank * S + j for j in range(S)]
+
+
+def rank_streams(config, rank, S, frames, width=None, height=None):
+    """Rank `rank`'s shard: its S synthetic streams (frame batches), as the bench decodes them."""
+    import pysynth
+    W, H, tiles, seed = CONFIGS[config]
+    W, H = width or W, height or H
+    return [pysynth.stream(W, H, frames, stream_seed(seed, i), sb128=True, tiles=tiles) for i in rank_stream_ids(rank, S)]
+
+
 def max_over_ranks(elapsed, dist=None):
     """The timed region's MAX over ranks (barrier after, so no rank races ahead)."""
     if dist is None:
@@ -268,8 +282,7 @@ def main():
     W, H, tiles, seed = CONFIGS[args.config]
     S = max(1, args.streams)
     # stream i of the job = rank * S + j (independent streams, one GPU each)
-    streams = [pysynth.stream(W, H, args.frames, stream_seed(seed, rank * S + j), sb128=True, tiles=tiles)
-               for j in range(S)]
+    streams = rank_streams(args.config, rank, S, args.frames)
     decs = [Decoder(local, keep_stages=False, timing=False) for _ in range(S)]
     for d in decs:
         d.set_discard_output(True)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define AV1R_VERSION 1u
+#define AV1R_VERSION 2u
 
 /* ---- status codes (map onto YamiStatus, interface/VideoCommonDefs.h:130-164) ---- */
 #define AV1R_OK 0
@@ -88,6 +88,14 @@ typedef struct av1r_block {
     int32_t local_warp[6];     /* LocalWarpParams (Block.cpp:1116-1169) when AV1R_BLK_LOCAL_VALID */
     uint32_t palette_off;      /* byte offset of this block's av1r_palette record     */
     uint32_t first_tb, n_tbs;  /* this block's transform blocks in the tb array       */
+    /* the block's own mode-info values (ModeInfoBlock, Parser.h:432-455; v2): with the
+     * fields above and the transform blocks they determine the whole mode-info grid, which
+     * the library derives on the device instead of uploading it (see av1r_frame_batch.mi) */
+    int16_t mv[2][2];          /* Mvs[refList] (inter blocks; [1] zero unless compound)  */
+    int8_t ref_frame[2];       /* RefFrame[] (intra: 0, -1; inter-intra: ref, 0)         */
+    uint8_t filt;              /* InterpFilters[0] | InterpFilters[1] << 4 (inter only)  */
+    uint8_t pad1;
+    int8_t delta_lf[4];        /* DeltaLF[] at the block                                 */
 } av1r_block;
 #define AV1R_BLK_INTER (1u << 0)
 #define AV1R_BLK_INTRABC (1u << 1)
@@ -177,7 +185,11 @@ typedef struct av1r_frame_hdr {
 /* ---- one frame's (or one tile's) payload ---- */
 typedef struct av1r_frame_batch {
     const av1r_frame_hdr* hdr;
-    const av1r_mi* mi;             /* mi_rows_alloc * mi_stride records               */
+    /* mi_rows_alloc * mi_stride records, or NULL.  The grid is a function of the blocks
+     * (their mode info over their 4x4 units) and transform blocks (lf_tx over the units each
+     * covers, TransformBlock.cpp:2444-2454), zero elsewhere: the library derives it on the
+     * device (k_mi) and never reads this array -- host consumers (the CPU oracle) may. */
+    const av1r_mi* mi;
     const av1r_block* blocks;
     uint32_t n_blocks;
     const av1r_tb* tbs;
@@ -239,6 +251,11 @@ void av1r_packed_free(av1r_packed* p);
 size_t av1r_packed_bytes(const av1r_packed* p);
 const char* av1r_pack_last_error(void);
 int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* frames, int n);
+/* Profiling hook (environment AV1R_PACK_PROF=1): ns[0..5] = nanoseconds all threads spent
+ * in av1r_pack's phases (validation, schedule set-up, per-block dependencies, item lists,
+ * dependency lists, packing copy), ns[6] = frames packed; returns the phase count (6), or 0
+ * when profiling is off.  reset = 1 zeroes the counters afterwards. */
+int av1r_pack_profile(uint64_t* ns, int n, int reset);
 /* In both batched entry points a frame with a deep dependency chain (a key frame) is
  * launched alone on its own context's stream, overlapping the batch.  av1r_busy returns 1
  * while such a frame is still running: a scheduler leaves that stream out of the next

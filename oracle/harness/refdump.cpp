@@ -226,6 +226,17 @@ struct Dumper {
             while (cur.palette.size() & 3)
                 cur.palette.push_back(0);
         }
+        {  // v2: the block's mode info, as stored over its 4x4 units
+            const ModeInfoBlock& m = b.m_frame.m_modeInfo[b.MiRow][b.MiCol];
+            for (int l = 0; l < 2; l++) {
+                r.mv[l][0] = m.Mvs[l].mv[0];
+                r.mv[l][1] = m.Mvs[l].mv[1];
+                r.ref_frame[l] = (int8_t)m.RefFrames[l];
+            }
+            r.filt = (uint8_t)((m.InterpFilters[0] & 15) | (m.InterpFilters[1] << 4));
+            for (int i = 0; i < 4; i++)
+                r.delta_lf[i] = m.DeltaLFs[i];
+        }
         r.first_tb = (uint32_t)cur.tbs.size();
         uint32_t blockIdx = (uint32_t)cur.blocks.size();
         cur.blocks.push_back(r);

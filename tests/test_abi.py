@@ -110,3 +110,38 @@ def test_pack_is_host_only_and_thread_safe(native_lib):
     p = C.c_void_p()
     assert native_lib.av1r_pack(C.cast(batchfile.Frame(secs).byref(), C.c_void_p), C.byref(p)) == abi.AV1R_E_INVALID
     assert b"tb 0" in native_lib.av1r_pack_last_error()
+
+
+def _declared(header, prefix):
+    src = open(os.path.join(native.ROOT, "include", header)).read()
+    return sorted(set(re.findall(r"\b(%s_\w+)\s*\(" % prefix, src)) - {prefix + "_ctx"})
+
+
+def test_parser_and_decoder_entry_points_exported(native_lib):
+    """libav1r.so carries the host parser (include/av1p.h) and the whole-decoder C-ABI
+    (include/av1dec.h) too, so one library is the drop-in; libav1p.so is the parser alone."""
+    for header, prefix in (("av1p.h", "av1p"), ("av1dec.h", "av1d")):
+        names = _declared(header, prefix)
+        assert names, header
+        for n in names:
+            assert hasattr(native_lib, n), n
+    assert sorted(native.PARSE_EXPORTS) == _declared("av1p.h", "av1p")
+    plib = C.CDLL(native.build_parser())
+    for n in native.PARSE_EXPORTS:
+        assert hasattr(plib, n), n
+    # the C++ facade (YamiAv1::Decoder, Yami::YuvFrame) is exported with C++ linkage
+    import subprocess
+    syms = subprocess.run(["nm", "-DC", native.LIB], capture_output=True, text=True).stdout
+    for s in ("YamiAv1::Decoder::decode(unsigned char*, unsigned long)", "YamiAv1::Decoder::getOutput()",
+              "Yami::YuvFrame::create(int, int)"):
+        assert s in syms, s
+
+
+def test_cli_usage_without_device():
+    """The av1dec CLI (tests/Av1Dec.cpp's counterpart) is built next to the library and
+    rejects a bad command line before touching any device."""
+    import subprocess
+    r = subprocess.run([native.CLI], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "usage" in r.stderr
+    r = subprocess.run([native.CLI, "-i", "/nonexistent.ivf"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "can't open" in r.stderr

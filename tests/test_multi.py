@@ -51,3 +51,76 @@ def test_two_rank_timing_and_sharding():
 def test_single_rank_passthrough():
     assert bench.max_over_ranks(1.5, None) == 1.5
     assert bench.aggregate_fps(1, 60, 2.0) == 30.0
+
+
+def _shard_worker(rank, world, port, q):
+    """One rank of the bench's N>1 path on real data: it builds ITS shard with the bench's
+    own selection (bench.rank_streams), decodes it with the CPU oracle, and reports the
+    per-stream output digests.  The only collective is the test's own check that the shards
+    are disjoint (the bench itself exchanges nothing but the timing MAX)."""
+    import hashlib
+    import sys
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, os.path.join(bench.ROOT, "oracle"))
+        import pyoracle
+        import torch
+        S = 2
+        ids = bench.rank_stream_ids(rank, S)
+        shard = bench.rank_streams("1080p", rank, S, 2, width=128, height=96)
+        digests = []
+        for frames in shard:
+            o = pyoracle.Oracle(keep_stages=False)
+            h = hashlib.md5()
+            for fr in frames:
+                o.decode_frame(fr)
+                while o.output_pending():
+                    for plane in o.get_output():
+                        h.update(plane.tobytes())
+            o.close()
+            digests.append(h.hexdigest())
+        gathered = [torch.zeros(S, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, torch.tensor(ids, dtype=torch.int64))
+        q.put((rank, ids, digests, [g.tolist() for g in gathered]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_real_shards():
+    """world_size 2: rank r decodes streams r*S .. r*S+S-1 (disjoint, covering 0..2S-1) and
+    gets exactly what one process decoding those streams gets."""
+    import hashlib
+    import sys
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    all_ids = [i for _, ids, _, _ in res for i in ids]
+    assert sorted(all_ids) == list(range(2 * world)) and len(set(all_ids)) == len(all_ids)
+    assert res[0][3] == res[1][3] == [r[1] for r in res]
+    # single-process reference of the same global streams
+    sys.path.insert(0, os.path.join(bench.ROOT, "oracle"))
+    import pyoracle
+    W, H, tiles, seed = bench.CONFIGS["1080p"]
+    import pysynth
+    for rank, ids, digests, _ in res:
+        for i, d in zip(ids, digests):
+            frames = pysynth.stream(128, 96, 2, bench.stream_seed(seed, i), sb128=True, tiles=tiles)
+            o = pyoracle.Oracle(keep_stages=False)
+            h = hashlib.md5()
+            for fr in frames:
+                o.decode_frame(fr)
+                while o.output_pending():
+                    for plane in o.get_output():
+                        h.update(plane.tobytes())
+            o.close()
+            assert h.hexdigest() == d, f"rank {rank} stream {i}"
+    assert len({d for _, _, ds, _ in res for d in ds}) == 2 * world  # the shards differ

@@ -112,3 +112,24 @@ def test_parser_streams_are_independent(parser_mod):
         gold = batchfile.load(golden.batch_path(stream))
         assert len(frames) == len(gold)
         assert all(_same(f, g) for f, g in zip(frames, gold))
+
+
+@needs_bits
+@pytest.mark.parametrize("stream", ["av1-1-b8-01-size-16x18", "av1-1-b8-04-cdfupdate", "av1-1-b8-06-mfmv",
+                                    "Halo_426x240_1frames_intrabc"])
+def test_bitstream_to_pixels_matches_conformance_md5(parser_mod, stream):
+    """Bitstream -> host parser -> CPU oracle restatement -> the conformance MD5 (bits.md5):
+    the whole decode with nothing from the reference in the loop."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    expect = golden.bits_md5()[stream]
+    o = pyoracle.Oracle(keep_stages=False)
+    h = hashlib.md5()
+    for fr in _frames(parser_mod, stream):
+        o.decode_frame(fr)
+        while o.output_pending():
+            for plane in o.get_output():
+                h.update(plane.tobytes())
+    o.close()
+    assert h.hexdigest() == expect

@@ -55,7 +55,7 @@ def stream(width, height, nframes, seed, sb128=True, tiles=(1, 1)):
             if l.av1r_synth_next(h, C.byref(p), C.byref(n)) != 0:
                 raise RuntimeError("synth failed")
             rec = bytes(np.ctypeslib.as_array(p, shape=(n.value,)))
-            out.extend(batchfile.parse(b"AV1B" + struct.pack("<I", 1) + rec))
+            out.extend(batchfile.parse(b"AV1B" + struct.pack("<I", batchfile.abi.AV1R_VERSION) + rec))
     finally:
         l.av1r_synth_close(h)
     return out

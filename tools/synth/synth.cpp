@@ -420,7 +420,7 @@ struct Gen {
         }
         if (inter && (B.flags & AV1R_BLK_INTERINTRA)) ymode = AV1R_NEWMV;
         B.y_mode = (uint8_t)ymode;
-        B.uv_mode = (uint8_t)(hasChroma ? uvmode : 0);
+        B.uv_mode = (uint8_t)(hasChroma && !inter ? uvmode : 0);  // as the parser: intra blocks only
         B.flags = f;
         // smooth-neighbour luma check of the reference reads YMode regardless of inter-ness
         if (!inter) {
@@ -442,6 +442,14 @@ struct Gen {
                 m.mi_size = (uint8_t)bs;
                 m.flags = (uint8_t)((skip ? AV1R_MI_SKIP : 0) | (inter ? AV1R_MI_INTER : 0));
             }
+        {  // v2: the block's mode info (what it wrote over its units above)
+            const av1r_mi& m = M(r, c);
+            memcpy(B.mv, m.mv, sizeof(B.mv));
+            B.ref_frame[0] = m.ref_frame[0];
+            B.ref_frame[1] = m.ref_frame[1];
+            B.filt = m.filt;
+            memcpy(B.delta_lf, m.delta_lf, sizeof(B.delta_lf));
+        }
         uint32_t bi = (uint32_t)blocks.size();
         blocks.push_back(B);
         emit_tbs(rng, bi, lumaTx, inter, skip);
