@@ -1401,7 +1401,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const
 // 4 waves/SIMD (128 VGPRs, 64 B/lane of spills; LDS 10160 B: 16 workgroups/CU); the
 // -DAV1R_TRACE build keeps its registers (with the stamps it would spill ~1.9 KB/lane)
 #ifndef AV1R_INTER_WAVES
-#define AV1R_INTER_WAVES 4
+#define AV1R_INTER_WAVES 3  // 3 waves/SIMD: 163 VGPRs, no spills (4: 128 VGPRs + 88 B/lane scratch, no faster, 2x the HBM writes)
 #endif
 #if defined(AV1R_TRACE) || AV1R_INTER_WAVES == 0
 #define K_INTER_BOUNDS __launch_bounds__(64)
