@@ -1058,6 +1058,9 @@ void BlockParser::read_mv(Blk& b, const Mv* pred, int ref)
 {
     const int ctx = b.use_intrabc ? 1 : 0;
     int diff[2] = {0, 0};
+#ifdef AV1P_WRITER
+    if (sd.hook) sd.hook->mv_pred(pred[ref], ctx);
+#endif
     const int joint = S(cdf.mv[ctx].joints, 4);
     if (joint == 2 || joint == 3) diff[0] = read_mv_component(ctx, 0);
     if (joint == 1 || joint == 3) diff[1] = read_mv_component(ctx, 1);
@@ -2111,7 +2114,14 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         for (int i = 0; i < w4; i++)
             for (int j = 0; j < h4; j++) P.mi[(size_t)(y4 + j) * P.mi_stride + x4 + i].tx_type = (uint8_t)type;
     };
-    const bool allZero = S(cdf.coef.txb_skip[txSzCtx][all_zero_ctx(b, plane, txSz, x4, y4, w, h)], 2) != 0;
+    const int azCtx = all_zero_ctx(b, plane, txSz, x4, y4, w, h);
+#ifdef AV1P_TRACE
+    {
+        static FILE* tf = fopen("/tmp/av1p_az.txt", "w");
+        fprintf(tf, "p%d x4 %d y4 %d tx %d ctx %d\n", plane, x4, y4, txSz, azCtx);
+    }
+#endif
+    const bool allZero = S(cdf.coef.txb_skip[txSzCtx][azCtx], 2) != 0;
     if (allZero) {
         if (plane == 0) set_luma_type(DCT_DCT);
     } else {
@@ -2244,6 +2254,9 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 uint32_t bit;
                 do {
                     length++;
+#ifdef AV1P_WRITER
+                    if (sd.hook) sd.hook->golomb_prefix(length);
+#endif
                     bit = L(1);
                     if (length > 32) {
                         P.fail(AV1R_E_INVALID, "invalid Golomb code");
@@ -2252,12 +2265,19 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 } while (!bit);
                 uint32_t x = 1;
                 for (int i = length - 2; i >= 0; i--) x = (x << 1) | L(1);
-                quant[pos] = (int16_t)x + kCoeffBaseRange + kNumBaseLevels;
+                // int16 twice, as the reference's getLevel (TransformBlock.cpp:1620-1635)
+                quant[pos] = (int16_t)((int16_t)x + kCoeffBaseRange + kNumBaseLevels);
             }
             if (pos == 0 && quant[pos] > 0) dcCategory = sign ? 1 : 2;
             culLevel += quant[pos];
             if (sign) quant[pos] = -quant[pos];
         }
+#ifdef AV1P_TRACE
+        {
+            static FILE* tf = fopen("/tmp/av1p_cul.txt", "w");
+            fprintf(tf, "p%d x4 %d y4 %d eob %d cul %d\n", plane, x4, y4, eob, culLevel);
+        }
+#endif
         culLevel = std::min(63, culLevel);
         // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j
         std::vector<uint32_t>& out = P.cur->coefs;
@@ -2277,9 +2297,9 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             return 0;
         }
     }
-    std::fill_n(&P.above_level[plane][x4], w4, (uint8_t)culLevel);
+    std::fill_n(&P.above_level[plane][x4], w4, (int16_t)culLevel);
     std::fill_n(&P.above_dc[plane][x4], w4, (uint8_t)dcCategory);
-    std::fill_n(&P.left_level[plane][y4], h4, (uint8_t)culLevel);
+    std::fill_n(&P.left_level[plane][y4], h4, (int16_t)culLevel);
     std::fill_n(&P.left_dc[plane][y4], h4, (uint8_t)dcCategory);
     return eob;
 }

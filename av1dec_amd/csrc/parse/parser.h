@@ -119,6 +119,17 @@ struct BitReader {
     size_t byte_pos() const { return pos >> 3; }
 };
 
+#ifdef AV1P_WRITER
+// Bitstream-writer build only (tools/bsw): the symbol reads of the syntax walk are answered by
+// a chooser that also arithmetic-codes the chosen symbol, so the same walk writes a stream.
+struct WriterHook {
+    virtual int symbol(uint16_t* cdf, int nsym) = 0;  // choose a value and encode it
+    virtual void mv_pred(const Mv& pred, int ctx) = 0;  // read_mv: the predictor of the next vector
+    virtual void golomb_prefix(int length) = 0;         // the next literal bit is Golomb prefix bit `length`
+    virtual ~WriterHook() {}
+};
+#endif
+
 // ---- arithmetic decoder (AV1 spec 8.2: init_symbol / read_symbol / exit_symbol) with
 // CDFs in libaom's inverted form (32768 - cumulative, then the adaptation counter) ----
 struct SymbolDecoder {
@@ -158,8 +169,23 @@ struct SymbolDecoder {
         maxBits = 8 * (int64_t)sz - 15;
         noUpdate = disableCdfUpdate;
     }
+#ifdef AV1P_WRITER
+    WriterHook* hook = nullptr;
+#endif
     int read(uint16_t* cdf, int nsym)
     {
+#ifdef AV1P_TRACE
+        const uint32_t range0 = range;
+        uint16_t cdf0[16];
+        for (int q = 0; q < nsym; q++) cdf0[q] = cdf[q];
+#endif
+#ifdef AV1P_WRITER
+        if (hook) {
+            const int s = hook->symbol(cdf, nsym);
+            if (!noUpdate) adapt(cdf, s, nsym);
+            return s;
+        }
+#endif
         uint32_t cur = range, prev;
         int sym = -1;
         do {
@@ -179,6 +205,14 @@ struct SymbolDecoder {
         value = padded ^ (((value + 1) << b) - 1);
         maxBits -= b;
         if (!noUpdate) adapt(cdf, sym, nsym);
+#ifdef AV1P_TRACE  // debug aid: the symbol sequence, for diffing against another decoder
+        {
+            static FILE* tf = fopen("/tmp/av1p_sym.txt", "w");
+            fprintf(tf, "%d %d %u", nsym, sym, range0);
+            for (int q = 0; q < nsym; q++) fprintf(tf, " %u", cdf0[q]);
+            fprintf(tf, "\n");
+        }
+#endif
         return sym;
     }
     static void adapt(uint16_t* cdf, int sym, int nsym)
@@ -375,7 +409,10 @@ public:
     int mi_row_start = 0, mi_row_end = 0, mi_col_start = 0, mi_col_end = 0;
     SymbolDecoder sd;
     Cdfs tcdf;  // the tile's CDFs
-    std::vector<uint8_t> above_level[3], above_dc[3], left_level[3], left_dc[3];
+    // level contexts are int16 as the reference's BlockContext::LevelContext: a Golomb level
+    // past int16 wraps negative and stays so in the context (TransformBlock.cpp:1620-1702)
+    std::vector<int16_t> above_level[3], left_level[3];
+    std::vector<uint8_t> above_dc[3], left_dc[3];
     int delta_lf[4] = {};
     int current_q = 0;
     bool read_deltas = false;

@@ -1576,6 +1576,9 @@ typedef struct LrCtx {
 } LrCtx;
 
 /* get_source_sample (LoopRestoration.cpp:234-246) */
+/* the widest unit: the last one of a row spans up to 1.5 unit sizes - 1 (count_units_in_frame
+ * rounds, LoopRestoration.cpp:32-35), i.e. 383 px at 256 */
+#define LR_MAXW 384
 static inline int lr_src(const LrCtx* L, int x, int y)
 {
     if (y < L->st.start) {
@@ -1604,7 +1607,7 @@ static void lr_wiener(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w
     const int R0 = 3, R1 = 11;
     int offset = 1 << (8 + 7 - R0 - 1);
     int limit = (1 << (8 + 1 + 7 - R0)) - 1;
-    static _Thread_local int inter[64 + 6][256];
+    static _Thread_local int inter[64 + 6][LR_MAXW];
     for (int r = 0; r < h + 6; r++)
         for (int cc = 0; cc < w; cc++) {
             int s = 0;
@@ -1623,9 +1626,9 @@ static void lr_wiener(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w
 }
 /* boxFilter with boxsum1/boxsum2 (LoopRestoration.cpp:284-430); the box sums are
  * evaluated directly (the reference's own #if 0 branch asserts they are equal). */
-static void lr_box(const LrCtx* L, int x, int y, int w, int h, int set, int pass, int r, int* F /* [h][w] stride 256 */)
+static void lr_box(const LrCtx* L, int x, int y, int w, int h, int set, int pass, int r, int* F /* [h][w] stride LR_MAXW */)
 {
-    static _Thread_local int A[66][258], Bv[66][258];
+    static _Thread_local int A[66][LR_MAXW + 2], Bv[66][LR_MAXW + 2];
     int eps = av1r_sgr_params[set][pass * 2 + 1];
     int n = (2 * r + 1) * (2 * r + 1);
     int n2e = n * n * eps;
@@ -1664,14 +1667,14 @@ static void lr_box(const LrCtx* L, int x, int y, int w, int h, int set, int pass
                     b += wt * Bv[i + dy + 1][j + dx + 1];
                 }
             int v = a * PIX(L->cdefF, L->plane, x + j, y + i) + b;
-            F[i * 256 + j] = r2(v, 8 + shift - 4);
+            F[i * LR_MAXW + j] = r2(v, 8 + shift - 4);
         }
     }
 }
 /* selfGuidedFilter (LoopRestoration.cpp:444-479) */
 static void lr_sgr(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w, int h)
 {
-    static _Thread_local int flt0[64 * 256], flt1[64 * 256];
+    static _Thread_local int flt0[64 * LR_MAXW], flt1[64 * LR_MAXW];
     int set = u->sgr_set;
     int r0 = av1r_sgr_params[set][0], r1 = av1r_sgr_params[set][2];
     if (r0) lr_box(L, x, y, w, h, set, 0, r0, flt0);
@@ -1681,8 +1684,8 @@ static void lr_sgr(const LrCtx* L, const av1r_lr_unit* u, int x, int y, int w, i
         for (int j = 0; j < w; j++) {
             int uu = PIX(L->cdefF, L->plane, x + j, y + i) << 4;
             int v = w1 * uu;
-            v += r0 ? w0 * flt0[i * 256 + j] : w0 * uu;
-            v += r1 ? w2 * flt1[i * 256 + j] : w2 * uu;
+            v += r0 ? w0 * flt0[i * LR_MAXW + j] : w0 * uu;
+            v += r1 ? w2 * flt1[i * LR_MAXW + j] : w2 * uu;
             int s = r2(v, 4 + 7);
             PIX(L->out, L->plane, x + j, y + i) = (uint8_t)CLIP1(s);
         }

@@ -495,17 +495,32 @@ struct Dumper {
             };
             dump(*frame, "recon");
         }
+        const char* planeDir = getenv("REFDUMP_PLANES");
+        auto dumpStage = [&](const YuvFrame& f, const char* tag) {
+            if (!planeDir) return;
+            char path[512];
+            snprintf(path, sizeof(path), "%s/f%d_%s.yuv", planeDir, frameNo, tag);
+            FILE* fp = fopen(path, "wb");
+            for (int p = 0; p < 3; p++) {
+                int w = p ? f.width >> 1 : f.width, hh = p ? f.height >> 1 : f.height;
+                for (int y = 0; y < hh; y++) fwrite(f.data[p] + y * f.strides[p], 1, w, fp);
+            }
+            fclose(fp);
+        };
         LoopFilter lf(dec.m_frame);
         lf.filter(frame);
         std::string hLf = md5_planes(*frame);
+        dumpStage(*frame, "lf");
         Cdef cdef(dec.m_frame);
         std::shared_ptr<YuvFrame> cdefFrame = cdef.filter(frame);
         std::string hCdef = md5_planes(*cdefFrame);
+        dumpStage(*cdefFrame, "cdef");
         std::shared_ptr<YuvFrame> upCdef = dec.upscaling(cdefFrame);
         std::shared_ptr<YuvFrame> upCur = dec.upscaling(frame);
         LoopRestoration lr(dec.m_frame, upCdef, upCur);
         std::shared_ptr<YuvFrame> lrFrame = lr.filter();
         std::string hLr = md5_planes(*lrFrame);
+        dumpStage(*lrFrame, "lr");
         dec.m_frame->motionVectorStorage();
         write_batch(out, cur);
         fprintf(hashes, "%d %d %d %d %s %s %s %s %zu %zu %zu\n", frameNo, (int)h.frame_type,
