@@ -1,0 +1,130 @@
+"""Many independent AV1 streams decoded end to end on one GPU.
+
+Each stream gets a host thread that parses its temporal units in order (av1p_decode_tu, the
+host parser linked into libav1r.so) and packs every completed frame (av1r_pack: validation,
+dependency schedule, pinned copy) into that stream's queue, a few frames ahead.  One launching
+thread takes the next packed frame of every stream that has one and is not running a key frame
+alone (av1r_busy), and decodes them in shared launches (av1r_decode_packed_batch).  Parse of
+frame N+1 therefore overlaps the GPU work of frame N (legal: parsing needs only the previous
+frames' parse state, never their pixels -- SURVEY K4), and the streams' parses run in parallel.
+
+This is the reference's Decoder::decode loop (decoder/Av1Decoder.cpp:49-109) per stream, with
+the per-frame reconstruction (Av1Decoder.cpp:128-192) batched across streams."""
+import ctypes as C
+import queue
+import threading
+import time
+
+from . import native
+from .decoder import BackendError, Decoder
+from .parser import ivf_frames
+
+
+def _plib():
+    l = native.lib()  # libav1r.so carries the parser too (include/av1p.h)
+    vp = C.c_void_p
+    l.av1p_create.argtypes = [C.POINTER(vp)]
+    l.av1p_destroy.argtypes = [vp]
+    l.av1p_destroy.restype = None
+    l.av1p_decode_tu.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
+    l.av1p_frame.argtypes = [vp, C.c_int]
+    l.av1p_frame.restype = vp
+    l.av1p_last_error.argtypes = [vp]
+    l.av1p_last_error.restype = C.c_char_p
+    return l
+
+
+class IvfPipeline:
+    """streams: IVF file contents (bytes), one per stream; decoders: one Decoder each (same
+    device).  run() decodes every frame of every stream once and returns the elapsed seconds."""
+
+    def __init__(self, decoders, streams, depth=3):
+        if len(decoders) != len(streams):
+            raise ValueError("one decoder per stream")
+        self.decs, self.depth = decoders, depth
+        self.tus = [list(ivf_frames(s)) for s in streams]
+        self.l = _plib()
+        self.parse_s = [0.0] * len(streams)
+        self.pack_s = [0.0] * len(streams)
+        self.frames = [0] * len(streams)
+        self.batches = 0
+
+    def _producer(self, j, q, err):
+        l = self.l
+        p = C.c_void_p()
+        if l.av1p_create(C.byref(p)):
+            err.append("av1p_create failed")
+            q.put(None)
+            return
+        n = C.c_int()
+        try:
+            for tu in self.tus[j]:
+                t0 = time.perf_counter()
+                rc = l.av1p_decode_tu(p, tu, len(tu), C.byref(n))
+                t1 = time.perf_counter()
+                self.parse_s[j] += t1 - t0
+                if rc:
+                    err.append(f"stream {j}: parse failed ({rc}): {l.av1p_last_error(p).decode()}")
+                    return
+                for i in range(n.value):
+                    ptr = l.av1p_frame(p, i)
+                    pk = C.c_void_p()
+                    t2 = time.perf_counter()
+                    rc = l.av1r_pack(ptr, C.byref(pk))
+                    self.pack_s[j] += time.perf_counter() - t2
+                    if rc:
+                        err.append(f"stream {j}: av1r_pack failed ({rc}): {l.av1r_pack_last_error().decode()}")
+                        return
+                    q.put(pk)
+                    self.frames[j] += 1
+        finally:
+            l.av1p_destroy(p)
+            q.put(None)  # end of stream
+
+    def run(self):
+        S = len(self.decs)
+        qs = [queue.Queue(maxsize=self.depth) for _ in range(S)]
+        err = []
+        th = [threading.Thread(target=self._producer, args=(j, qs[j], err), daemon=True) for j in range(S)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        live = set(range(S))
+        head = [None] * S  # a packed frame taken from the queue, not yet launched
+        try:
+            while live and not err:
+                for j in list(live):
+                    if head[j] is None:
+                        try:
+                            head[j] = qs[j].get_nowait()
+                        except queue.Empty:
+                            continue
+                        if head[j] is None:  # end of stream
+                            live.discard(j)
+                ready = [j for j in live if head[j] is not None and not self.decs[j].busy()]
+                if not ready:
+                    time.sleep(50e-6)
+                    continue
+                Decoder.decode_packed_batch([self.decs[j] for j in ready], [head[j] for j in ready])
+                self.batches += 1
+                for j in ready:
+                    Decoder.free_packed(head[j])
+                    head[j] = None
+            for d in self.decs:
+                d.synchronize()
+        finally:
+            for j in range(S):  # drain the producers (an error ends the run early)
+                if head[j] is not None:
+                    Decoder.free_packed(head[j])
+                while th[j].is_alive() or not qs[j].empty():
+                    try:
+                        pk = qs[j].get(timeout=0.05)
+                    except queue.Empty:
+                        continue
+                    if pk is not None:
+                        Decoder.free_packed(pk)
+            for t in th:
+                t.join()
+        if err:
+            raise BackendError(err[0])
+        return time.perf_counter() - t0

@@ -219,6 +219,39 @@ class StreamScheduler:
             self.ex.shutdown()
 
 
+def ivf_streams(rank, S, frames):
+    """Rank `rank`'s shard of configs[4] as real bitstreams: S synthetic 1080p IVF streams from
+    the bitstream writer (tools/bsw, configuration 1080p_s1; stream i of the job has seed
+    0x5EED1000 + i, so stream 0 is the one tests/golden/bsw.json pins to the reference's MD5),
+    written in parallel (untimed)."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "tools", "bsw"))
+    import pybsw
+    ids = rank_stream_ids(rank, S)
+    with ThreadPoolExecutor(min(S, 16)) as ex:
+        return list(ex.map(lambda i: pybsw.stream_ivf("1080p_s1", seed=0x5EED1000 + i, frames=frames), ids))
+
+
+def ivf_leg(decs, streams, frames):
+    """configs[4] end to end: every stream's IVF parsed on its own host thread and packed
+    while the GPU decodes, one frame of every ready stream per shared launch
+    (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one."""
+    from av1dec_amd.pipeline import IvfPipeline
+    IvfPipeline(decs, streams).run()
+    pl = IvfPipeline(decs, streams)
+    dt = pl.run()
+    n = sum(pl.frames)
+    return {"fps": round(n / dt, 3), "streams": len(streams), "frames_per_stream": frames,
+            "frames": n, "elapsed_s": round(dt, 3),
+            "parse_ms_per_frame": round(1e3 * sum(pl.parse_s) / n, 3),
+            "pack_ms_per_frame": round(1e3 * sum(pl.pack_s) / n, 3),
+            "stream_bytes_per_frame": int(sum(len(s) for s in streams) / n),
+            "batches": pl.batches,
+            "workload": f"{len(streams)} synthetic 1920x1080 IVF streams from tools/bsw (1080p_s1: 1 key + "
+                        f"{frames - 1} inter, seeds 0x5eed1000+stream), each parsed by the host parser on "
+                        f"its own thread, packed and decoded in shared launches; parse inside the timed region"}
+
+
 def host_workers():
     """Packing threads: the box's CPU share (OMP_NUM_THREADS is set to it there) less the
     launching thread."""
@@ -263,6 +296,7 @@ def main():
     ap.add_argument("--frames", type=int, default=60, help="stream length (1 key + inter)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ivf-frames", type=int, default=24, help="frames per stream of the IVF end-to-end leg (0: skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per frame (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -418,6 +452,13 @@ def main():
     except Exception as e:
         errs.append(str(e))
 
+    # ---- configs[4] end to end from IVF bitstreams (parse on the host inside the timed region)
+    ivf = None
+    if args.ivf_frames > 0 and args.config == "1080p":
+        ivf = ivf_leg(decs, ivf_streams(rank, S, args.ivf_frames), args.ivf_frames)
+        if dist:
+            ivf["fps_all_ranks"] = round(world * ivf["frames"] / max_over_ranks(ivf["elapsed_s"], dist), 3)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cfps, cn, cdt = cpu_baseline(streams[0], args.cpu_budget)
@@ -435,6 +476,14 @@ def main():
                         + str(cj["frames"]) + " conformance frames; reference -O1 incl. its parse)",
                         "reference_equivalent_fps": round(ref_eq, 4),
                         "speedup_vs_reference_equivalent": round(fps / max(ref_eq, 1e-9), 1)})
+        bg = os.path.join(ROOT, "tests", "golden", "bsw.json")
+        if os.path.exists(bg) and args.config == "1080p":
+            # the reference decoder itself on a 1080p bitstream (tools/bsw_golden.py, build
+            # container, 1 core, -O1): measured, not extrapolated
+            g = json.load(open(bg))["1080p_s1"]
+            cpu["reference_measured_fps_1080p"] = {"value": g["ref_decode_fps"], "stream": "tools/bsw 1080p_s1 "
+                                                   f"({g['frames']} frames, {g['bytes']} B)",
+                                                   "where": "build container (profiles/cpu_calibration.json CPU), 1 core"}
     for d, hs in zip(decs, handles):
         for hd in hs:
             d.release_prepared(hd)
@@ -483,6 +532,7 @@ def main():
             "decode_frame_fps_threads": host_mt_fps,
             **({"host_threaded_error": errs[0][:160]} if errs else {}),
             "recon_levels_last_frame": levels,
+            "ivf_end_to_end": ivf,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

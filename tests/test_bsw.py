@@ -101,3 +101,30 @@ def test_gpu_cli_matches_reference_md5(native_lib, name, tmp_path):
     r = subprocess.run([native.CLI, "-i", str(f), "-md5"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-500:]
     assert re.search(r"md5=([0-9a-f]{32})", r.stdout + r.stderr).group(1) == GOLD[name]["md5"]
+
+
+@pytest.mark.gpu
+def test_gpu_ivf_pipeline_matches_reference_md5(native_lib):
+    """The bench's configs[4] path (av1dec_amd.pipeline: a parse+pack thread per stream,
+    shared launches) on streams of three sizes at once, outputs kept: every stream's MD5
+    equals the reference's."""
+    from av1dec_amd import Decoder
+    from av1dec_amd.pipeline import IvfPipeline
+    names = ["1080p_s1", "cif_s1", "640x360_tiles2x2_sb64", "odd_416x234_key3"]
+    decs = [Decoder(0) for _ in names]
+    try:
+        outs = [[] for _ in names]
+        pl = IvfPipeline(decs, [stream(n) for n in names])
+        pl.run()
+        for d, o in zip(decs, outs):
+            while d.output_pending():
+                o.append(d.get_output())
+        for n, o in zip(names, outs):
+            md = hashlib.md5()
+            for planes in o:
+                for p in planes:
+                    md.update(p.tobytes())
+            assert md.hexdigest() == GOLD[n]["md5"], n
+    finally:
+        for d in decs:
+            d.close()
