@@ -12,6 +12,7 @@
 
 #include <new>
 #include <string>
+#include <vector>
 
 #include "YamiAv1/Av1Decoder.h"
 #include "av1dec.h"
@@ -89,6 +90,21 @@ int av1d_get_output(av1d_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
     const int rc = av1r_get_output(c->recon, y, ys, u, us, v, vs, width, height);
     if (rc) return c->fail(rc, "output", av1r_last_error(c->recon));
     return AV1R_OK;
+}
+
+int av1d_flush(av1d_ctx* c)
+{
+    if (!c) return AV1R_E_INVALID;
+    std::vector<uint8_t> scratch;
+    int w = 0, h = 0, rc = AV1R_OK;
+    while (av1d_output_size(c, &w, &h) == AV1R_OK) {
+        const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+        scratch.resize((size_t)w * h + 2 * (size_t)cw * ch);
+        uint8_t* y = scratch.data();
+        uint8_t* u = y + (size_t)w * h;
+        if ((rc = av1d_get_output(c, y, w, u, cw, u + (size_t)cw * ch, cw, &w, &h))) break;
+    }
+    return rc;
 }
 
 const char* av1d_last_error(av1d_ctx* c) { return c ? c->err.c_str() : "null context"; }

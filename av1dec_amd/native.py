@@ -25,8 +25,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.j
 # host-only C++ linked into the same library: the parser (include/av1p.h) and the
 # whole-decoder facade (include/av1dec.h, include/YamiAv1/Av1Decoder.h)
 HOST_SRCS = [("parse/obu.cpp", "p_obu"), ("parse/block.cpp", "p_block"), ("parse/api.cpp", "p_api"),
-             ("app/decoder.cpp", "app_decoder")]
+             ("app/decoder.cpp", "app_decoder"), ("app/yami.cpp", "app_yami")]
 CLI = os.path.join(BUILD, "av1dec")
+YAMI_APP = os.path.join(BUILD, "yami_decode")
 
 
 def _host_cmd(src, obj):
@@ -36,13 +37,14 @@ def _host_cmd(src, obj):
 
 
 def _stale():
-    if not os.path.exists(LIB) or not os.path.exists(CLI):
+    if not all(os.path.exists(p) for p in (LIB, CLI, YAMI_APP)):
         return True
-    t = min(os.path.getmtime(LIB), os.path.getmtime(CLI))
+    t = min(os.path.getmtime(p) for p in (LIB, CLI, YAMI_APP))
     deps = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc"))]
     for sub in ("parse", "app"):
         deps += [os.path.join(PKG, "csrc", sub, f) for f in os.listdir(os.path.join(PKG, "csrc", sub))]
-    deps += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+    for dp, _, fs in os.walk(os.path.join(ROOT, "include")):
+        deps += [os.path.join(dp, f) for f in fs]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -85,6 +87,12 @@ def build(force=False, jobs=3, out=None, defines=(), src_flags=None):
                                "-o", tmp, os.path.join(PKG, "csrc", "app", "av1dec.cpp"), "-L" + BUILD, "-lav1r",
                                "-Wl,-rpath,$ORIGIN"])
         os.replace(tmp, CLI)
+        # an application of the Yami decoder API (include/yami/yami_av1.h, createVideoDecoder)
+        tmp = YAMI_APP + ".tmp"
+        subprocess.check_call([os.environ.get("CXX", "g++"), "-std=c++17", "-O2", "-I" + os.path.join(ROOT, "include"),
+                               "-o", tmp, os.path.join(PKG, "csrc", "app", "yami_decode.cpp"), "-L" + BUILD, "-lav1r",
+                               "-Wl,-rpath,$ORIGIN"])
+        os.replace(tmp, YAMI_APP)
     return lib_path
 
 

@@ -32,6 +32,9 @@ int av1d_output_size(av1d_ctx* ctx, int* width, int* height);
 /* Copy the next shown frame's visible I420 planes and pop it (AV1R_E_NO_OUTPUT if none). */
 int av1d_get_output(av1d_ctx* ctx, uint8_t* y, int y_stride, uint8_t* u, int u_stride, uint8_t* v,
                     int v_stride, int* width, int* height);
+/* Drop every decoded frame not yet returned (IVideoDecoder::flush, a seek): the next unit
+ * should start at a key frame. */
+int av1d_flush(av1d_ctx* ctx);
 const char* av1d_last_error(av1d_ctx* ctx);
 
 #ifdef __cplusplus

