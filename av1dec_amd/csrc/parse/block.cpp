@@ -258,6 +258,7 @@ private:
     Cdfs& cdf;
     std::vector<Tb> tbs;
     std::vector<int> quant;  // Quant[] of the transform block being parsed
+    uint8_t lvl[36 * 36] = {};  // coefficient levels while parsing them, padded (coeffs())
 
     int S(uint16_t* c, int n) { return sd.read(c, n); }
     uint32_t L(int n) { return sd.literal(n); }
@@ -2105,9 +2106,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz], w4 = w >> 2, h4 = h >> 2;
     const int sqr = kTxSizeSqr[txSz], sqrUp = kTxSizeSqrUp[txSz];
     const int txSzCtx = (sqr + sqrUp + 1) >> 1;
-    const int tw = std::min(w, 32), th = std::min(h, 32);
+    const int tw = std::min(w, 32);
     const int segEob = (txSz == TX_16X64 || txSz == TX_64X16) ? 512 : std::min(1024, w * h);
-    quant.assign(1024, 0);
+    // quant[] is all zero between transform blocks: each block clears what it set
+    if (quant.size() != 1024) quant.assign(1024, 0);
     (void)segEob;
     int eob = 0, culLevel = 0, dcCategory = 0;
     auto set_luma_type = [&](int type) {
@@ -2173,10 +2175,14 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         const int adj = kAdjustedTxSize[txSz];
         const int bwl = av1r_tx_w_log2[adj];
         const int width = 1 << bwl, height = av1r_tx_h[adj];
+        // levels so far, padded by 4 zero rows / columns below and right (every context offset
+        // is non-negative): the neighbour sums need no bounds checks
+        const int ps = width + 4;
         for (int c = eob - 1; c >= 0; c--) {
             const int pos = scan[c];
             int level;
             const int row = pos >> bwl, col = pos - (row << bwl);
+            const uint8_t* lp = &lvl[row * ps + col];
             if (c == eob - 1) {
                 int ctx;
                 if (c == 0) ctx = kSigCoefContexts - 4;
@@ -2187,10 +2193,8 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 level = S(cdf.coef.coeff_base_eob[txSzCtx][ptype][ctx], 3) + 1;
             } else {
                 int mag = 0;
-                for (int k = 0; k < 5; k++) {
-                    const int rr = row + kSigRefDiffOffset[cls][k][0], cc = col + kSigRefDiffOffset[cls][k][1];
-                    if (rr >= 0 && cc >= 0 && rr < height && cc < width) mag += std::min(abs(quant[(rr << bwl) + cc]), 3);
-                }
+                for (int k = 0; k < 5; k++)
+                    mag += std::min((int)lp[kSigRefDiffOffset[cls][k][0] * ps + kSigRefDiffOffset[cls][k][1]], 3);
                 int ctx = std::min((mag + 1) >> 1, 4);
                 if (cls == TX_CLASS_2D) {
                     ctx = (row == 0 && col == 0) ? 0 : ctx + kCoeffBaseCtxOffset[txSz][std::min(row, 4)][std::min(col, 4)];
@@ -2202,12 +2206,8 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             }
             if (level > kNumBaseLevels) {
                 for (int idx = 0; idx < kCoeffBaseRange / (kBrCdfSize - 1); idx++) {
-                    int mag = 0;
-                    for (int k = 0; k < 3; k++) {
-                        const int rr = row + kMagRefOffset[cls][k][0], cc = col + kMagRefOffset[cls][k][1];
-                        if (rr >= 0 && cc >= 0 && rr < height && cc < width)
-                            mag += std::min(quant[rr * width + cc], kCoeffBaseRange + kNumBaseLevels + 1);
-                    }
+                    int mag = 0;  // levels here are at most 15 = COEFF_BASE_RANGE + NUM_BASE_LEVELS + 1
+                    for (int k = 0; k < 3; k++) mag += lp[kMagRefOffset[cls][k][0] * ps + kMagRefOffset[cls][k][1]];
                     mag = std::min((mag + 1) >> 1, 6);
                     int ctx;
                     if (pos == 0) ctx = mag;
@@ -2220,7 +2220,13 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 }
             }
             quant[pos] = level;
+            lvl[row * ps + col] = (uint8_t)level;
         }
+        for (int c = 0; c < eob; c++) {  // back to all zero for the next transform block
+            const int pos = scan[c];
+            lvl[(pos >> bwl) * ps + (pos & (width - 1))] = 0;
+        }
+        (void)height;
         // signs and Golomb remainders, in scan order
         for (int c = 0; c < eob; c++) {
             const int pos = scan[c];
@@ -2279,18 +2285,28 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         }
 #endif
         culLevel = std::min(63, culLevel);
-        // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j
+        // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j, in
+        // raster order over the bounding box of the scanned positions, which is cleared again
         std::vector<uint32_t>& out = P.cur->coefs;
-        for (int i = 0; i < th; i++)
-            for (int j = 0; j < tw; j++) {
-                const int v = quant[i * tw + j];
+        int maxI = 0, maxJ = 0;
+        for (int c = 0; c < eob; c++) {
+            const int pos = scan[c];
+            maxI = std::max(maxI, pos / tw);
+            maxJ = std::max(maxJ, pos % tw);
+        }
+        for (int i = 0; i <= maxI; i++) {
+            int* row = &quant[i * tw];
+            for (int j = 0; j <= maxJ; j++) {
+                const int v = row[j];
                 if (!v) continue;
+                row[j] = 0;
                 if (v >= (1 << 21) || v < -(1 << 21)) {
                     P.fail(AV1R_E_UNSUPPORTED, "coefficient out of packable range");
                     return 0;
                 }
                 out.push_back(((uint32_t)v << 10) | (uint32_t)(i * tw + j));
             }
+        }
         t.coef_cnt = (uint32_t)out.size() - t.coef_off;
         if (!t.coef_cnt) {
             P.fail(AV1R_E_INVALID, "transform block with eob %d and no non-zero coefficient", eob);

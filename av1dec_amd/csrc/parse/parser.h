@@ -195,15 +195,7 @@ struct SymbolDecoder {
         } while (value < cur);
         range = prev - cur;
         value -= cur;
-        int b = 0;
-        for (uint32_t r = range; r < (1u << 15); r <<= 1) b++;  // 15 - FloorLog2(range)
-        range <<= b;
-        int nb = b;
-        if (nb > maxBits) nb = maxBits > 0 ? (int)maxBits : 0;
-        const uint32_t newData = bits(nb);
-        const uint32_t padded = newData << (b - nb);
-        value = padded ^ (((value + 1) << b) - 1);
-        maxBits -= b;
+        renorm();
         if (!noUpdate) adapt(cdf, sym, nsym);
 #ifdef AV1P_TRACE  // debug aid: the symbol sequence, for diffing against another decoder
         {
@@ -214,6 +206,17 @@ struct SymbolDecoder {
         }
 #endif
         return sym;
+    }
+    void renorm()
+    {
+        const int b = __builtin_clz(range) - 16;  // 15 - FloorLog2(range)
+        range <<= b;
+        int nb = b;
+        if (nb > maxBits) nb = maxBits > 0 ? (int)maxBits : 0;
+        const uint32_t newData = bits(nb);
+        const uint32_t padded = newData << (b - nb);
+        value = padded ^ (((value + 1) << b) - 1);
+        maxBits -= b;
     }
     static void adapt(uint16_t* cdf, int sym, int nsym)
     {
@@ -229,6 +232,21 @@ struct SymbolDecoder {
     }
     int boolean()  // read_literal bit: probability 1/2, never adapted
     {
+#if !defined(AV1P_WRITER) && !defined(AV1P_TRACE)
+        // read() over the CDF {16384, 0}: the first interval boundary, then the same renormalisation
+        const uint32_t v0 = ((range >> 8) << 7) + 4;
+        int sym;
+        if (value >= v0) {
+            sym = 0;
+            range -= v0;
+            value -= v0;
+        } else {
+            sym = 1;
+            range = v0;
+        }
+        renorm();
+        return sym;
+#endif
         uint16_t c[3] = {16384, 0, 0};
         const bool nu = noUpdate;
         noUpdate = true;
