@@ -25,7 +25,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.j
 # host-only C++ linked into the same library: the parser (include/av1p.h) and the
 # whole-decoder facade (include/av1dec.h, include/YamiAv1/Av1Decoder.h)
 HOST_SRCS = [("parse/obu.cpp", "p_obu"), ("parse/block.cpp", "p_block"), ("parse/api.cpp", "p_api"),
-             ("app/decoder.cpp", "app_decoder"), ("app/yami.cpp", "app_yami")]
+             ("app/decoder.cpp", "app_decoder"), ("app/yami.cpp", "app_yami"), ("av1r_pipeline.cpp", "av1r_pipeline")]
 CLI = os.path.join(BUILD, "av1dec")
 YAMI_APP = os.path.join(BUILD, "yami_decode")
 
@@ -78,7 +78,7 @@ def build(force=False, jobs=3, out=None, defines=(), src_flags=None):
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
     tmp = lib_path + ".tmp"
-    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", tmp] + objs)
     os.replace(tmp, lib_path)
     if out is None:
         # the command-line decoder (tests/Av1Dec.cpp's counterpart), linked to this library
@@ -201,8 +201,26 @@ def lib():
     l.av1r_decode_packed_batch.argtypes = [C.POINTER(vp), C.POINTER(vp), i]
     l.av1r_busy.argtypes = [vp]
     l.av1r_pack_profile.argtypes = [C.POINTER(C.c_uint64), i, i]
+    l.av1r_pipeline_run.argtypes = [C.POINTER(vp), i, C.POINTER(StreamSource), C.c_int64, i, C.POINTER(PipelineStats)]
+    l.av1r_cycle_next.argtypes = [vp, i, C.POINTER(vp)]
+    l.av1r_ivf_source_create.argtypes = [C.POINTER(vp), C.POINTER(C.c_size_t), i, C.POINTER(StreamSource)]
+    l.av1r_ivf_source_destroy.argtypes = [C.POINTER(StreamSource)]
+    l.av1r_ivf_source_destroy.restype = None
     _lib = l
     return l
+
+
+class StreamSource(C.Structure):  # av1r_stream_source
+    _fields_ = [("next", C.c_void_p), ("user", C.c_void_p)]
+
+
+class PipelineStats(C.Structure):  # av1r_pipeline_stats
+    _fields_ = [("frames", C.c_uint64), ("batches", C.c_uint64), ("elapsed_s", C.c_double),
+                ("produce_s", C.c_double), ("pack_s", C.c_double), ("wait_s", C.c_double)]
+
+
+class Cycle(C.Structure):  # av1r_cycle
+    _fields_ = [("batches", C.c_void_p), ("count", C.POINTER(C.c_int)), ("pos", C.POINTER(C.c_int64))]
 
 
 EXPORTS = [
@@ -214,4 +232,5 @@ EXPORTS = [
     "av1r_set_discard_output", "av1r_stage_times", "av1r_decode_prepared_batch", "av1r_recon_kernel_times",
     "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug", "av1r_pack", "av1r_packed_free",
     "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy", "av1r_pack_profile",
+    "av1r_pipeline_run", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
 ]

@@ -128,3 +128,50 @@ class IvfPipeline:
         if err:
             raise BackendError(err[0])
         return time.perf_counter() - t0
+
+
+def run_native(decoders, source="cycle", streams=None, positions=None, max_frames=0, depth=3):
+    """The same pipeline in native threads (av1r_pipeline_run, include/av1r.h): no
+    interpreter on the path.  source "cycle": streams = per-stream lists of batchfile.Frame;
+    stream j continues at frame positions[j] (mod its length), and positions is advanced in
+    place by the frames decoded; "ivf": streams = IVF file contents.  Returns the
+    av1r_pipeline_stats as a dict."""
+    l = native.lib()
+    n = len(decoders)
+    ctxs = (C.c_void_p * n)(*[d.c.value for d in decoders])
+    src = native.StreamSource()
+    keep = []  # buffers the native side points into, alive for the call
+    if source == "cycle":
+        rows = []
+        for fr in streams:
+            arr = (C.c_void_p * len(fr))(*[C.cast(f.byref(), C.c_void_p).value for f in fr])
+            rows.append(arr)
+        table = (C.c_void_p * n)(*[C.cast(r, C.c_void_p).value for r in rows])
+        count = (C.c_int * n)(*[len(fr) for fr in streams])
+        pos = (C.c_int64 * n)(*(positions or [0] * n))
+        cyc = native.Cycle(C.cast(table, C.c_void_p).value, count, pos)
+        keep += [rows, table, count, pos, cyc, streams]
+        src.next = C.cast(l.av1r_cycle_next, C.c_void_p).value
+        src.user = C.cast(C.pointer(cyc), C.c_void_p).value
+    elif source == "ivf":
+        bufs = [C.create_string_buffer(bytes(s), len(s)) for s in streams]
+        files = (C.c_void_p * n)(*[C.cast(b, C.c_void_p).value for b in bufs])
+        sizes = (C.c_size_t * n)(*[len(s) for s in streams])
+        keep += [bufs, files, sizes]
+        rc = l.av1r_ivf_source_create(files, sizes, n, C.byref(src))
+        if rc:
+            raise BackendError(f"av1r_ivf_source_create failed ({rc})")
+    else:
+        raise ValueError(source)
+    st = native.PipelineStats()
+    try:
+        rc = l.av1r_pipeline_run(ctxs, n, C.byref(src), int(max_frames), int(depth), C.byref(st))
+    finally:
+        if source == "ivf":
+            l.av1r_ivf_source_destroy(C.byref(src))
+    if rc:
+        raise BackendError(f"av1r_pipeline_run failed ({rc}): {decoders[0].l.av1r_last_error(decoders[0].c).decode()}")
+    if source == "cycle" and positions is not None:
+        # every producer fetched exactly the frames that were decoded (max_frames each)
+        positions[:] = list(pos)
+    return {k: getattr(st, k) for k, _ in native.PipelineStats._fields_}

@@ -236,20 +236,22 @@ def ivf_leg(decs, streams, frames):
     """configs[4] end to end: every stream's IVF parsed on its own host thread and packed
     while the GPU decodes, one frame of every ready stream per shared launch
     (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one."""
-    from av1dec_amd.pipeline import IvfPipeline
-    IvfPipeline(decs, streams).run()
-    pl = IvfPipeline(decs, streams)
-    dt = pl.run()
-    n = sum(pl.frames)
+    from av1dec_amd.pipeline import run_native
+    run_native(decs, "ivf", streams)
+    t0 = time.perf_counter()
+    st = run_native(decs, "ivf", streams)
+    dt = time.perf_counter() - t0
+    n = int(st["frames"])
     return {"fps": round(n / dt, 3), "streams": len(streams), "frames_per_stream": frames,
             "frames": n, "elapsed_s": round(dt, 3),
-            "parse_ms_per_frame": round(1e3 * sum(pl.parse_s) / n, 3),
-            "pack_ms_per_frame": round(1e3 * sum(pl.pack_s) / n, 3),
+            "parse_ms_per_frame": round(1e3 * st["produce_s"] / n, 3),
+            "pack_ms_per_frame": round(1e3 * st["pack_s"] / n, 3),
             "stream_bytes_per_frame": int(sum(len(s) for s in streams) / n),
-            "batches": pl.batches,
+            "batches": int(st["batches"]),
             "workload": f"{len(streams)} synthetic 1920x1080 IVF streams from tools/bsw (1080p_s1: 1 key + "
-                        f"{frames - 1} inter, seeds 0x5eed1000+stream), each parsed by the host parser on "
-                        f"its own thread, packed and decoded in shared launches; parse inside the timed region"}
+                        f"{frames - 1} inter, seeds 0x5eed1000+stream), each parsed by the host parser and packed on "
+                        f"its own native thread (av1r_pipeline_run), decoded in shared launches; parse inside "
+                        f"the timed region"}
 
 
 def host_workers():
@@ -330,36 +332,36 @@ def main():
     # and PCIe upload of the parser's batches inside the timed region, overlapped with the
     # GPU).  Setup (untimed): stream j brought to its own GOP phase, a priming pass of ~1 s,
     # then the warmup steps.
-    workers = host_workers()
-    pp = StreamScheduler(decs, F, streams=streams, workers=workers)
+    # (the native pipeline, av1r_pipeline_run: one producer thread per stream packs its frames
+    # up to 3 ahead, the calling thread launches one frame of every ready stream per batch)
+    from av1dec_amd.pipeline import run_native
+    workers = S
+    pp = StreamScheduler(decs, F, streams=streams, workers=1)
     pp.stagger()
+    pp.close()
     sync()
+    pos = list(pp.pos)
     t_prime = time.perf_counter()
     while time.perf_counter() - t_prime < 1.0:
-        pp.run(F)
-        sync()
-    pp.run(args.warmup)
-    sync()
+        run_native(decs, "cycle", streams, pos, max_frames=F)
+    run_native(decs, "cycle", streams, pos, max_frames=args.warmup)
     if dist:
         dist.barrier()
-    pp.reset_prof()
+    pos0 = list(pos)
     t0 = time.perf_counter()
-    timed = pp.run(args.steps)  # (stream, frame) of every frame in the timed region
-    sync()
+    pr = run_native(decs, "cycle", streams, pos, max_frames=args.steps)  # synchronizes every context
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     fps = aggregate_fps(world, args.steps * S, elapsed)
+    timed = [(j, t % F) for j in range(S) for t in range(pos0[j], pos0[j] + args.steps)]
     n_key = sum(1 for j, t in timed if streams[j][t].hdr.frame_type == 0)
-    pr = pp.prof
     host_profile = {  # where the host-inclusive pipeline spends its time (rank 0)
-        "workers": workers,
-        "pack_ms_per_frame": round(1e3 * pr["pack_s"] / max(pr["packs"], 1), 3),
-        "pack_worker_utilisation": round(pr["pack_s"] / (workers * elapsed), 3),
-        "launch_thread_ms_per_step": round(1e3 * (pr["launch_s"] + pr["wait_s"]) / max(args.steps, 1), 3),
-        "launch_call_ms_per_batch": round(1e3 * pr["launch_s"] / max(pr["launches"], 1), 3),
-        "wait_packed_ms_per_step": round(1e3 * pr["wait_s"] / max(args.steps, 1), 3),
-        "batches": pr["launches"],
+        "producer_threads": workers,
+        "pack_ms_per_frame": round(1e3 * pr["pack_s"] / max(pr["frames"], 1), 3),
+        "producer_utilisation": round(pr["pack_s"] / (workers * elapsed), 3),
+        "launcher_idle_ms_per_step": round(1e3 * pr["wait_s"] / max(args.steps, 1), 3),
+        "batches": int(pr["batches"]),
     }
-    pp.close()
+    pp.pos = list(pos)
 
     # ---- device-only rate: the same streams with every batch already validated, scheduled
     # and resident in HBM (av1r_prepare), the same staggered GOP phases
@@ -509,8 +511,8 @@ def main():
                                    f"stream j offset by j*{F}/{S} frames; tiles {tiles[0]}x{tiles[1]}; seeds "
                                    f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
                                    f"host-inclusive: each frame validated, scheduled, packed and uploaded from "
-                                   f"host memory inside the timed region ({workers} packing threads, 3 frames "
-                                   f"ahead per stream; key frames run alone on their stream, overlapping "
+                                   f"host memory inside the timed region (native pipeline: a packing thread per "
+                                   f"stream, 3 frames ahead; key frames run alone on their stream, overlapping "
                                    f"the other streams' batches); timed frames: {args.steps * S} of which {n_key} key",
                        "host_threads": workers + 1,
                        "timed_key_frames": n_key,

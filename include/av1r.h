@@ -314,6 +314,45 @@ int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int 
 /* sizeof of the ABI structs: 0 hdr, 1 mi, 2 block, 3 tb, 4 lr_unit, 5 frame_batch. */
 size_t av1r_sizeof(int which);
 
+/* ---- multi-stream pipeline (av1r_pipeline.cpp; SURVEY.md 8e + 8f rank 4) ----
+ * n independent streams (contexts on one device) decoded end to end in native threads: one
+ * producer thread per stream pulls its frames in decode order from `src` and packs them
+ * (av1r_pack) up to `depth` ahead; the calling thread launches one frame of every ready
+ * stream per shared launch (av1r_decode_packed_batch), applies show-existing frames in
+ * order (av1r_show_existing), and finally synchronizes every context.  Stops after
+ * max_frames frames per stream (<= 0: at each source's end).  The reference's per-stream
+ * Decoder::decode loop (decoder/Av1Decoder.cpp:49-109), reconstruction batched across
+ * streams. */
+typedef struct av1r_stream_source {
+    /* Frame k of stream `stream` (k = 0, 1, ... per stream, only ever called from that
+     * stream's producer): *batch stays valid until the next call for the same stream.
+     * Returns 0 (a frame), 1 (end of stream) or a negative status. */
+    int (*next)(void* user, int stream, const av1r_frame_batch** batch);
+    void* user;
+} av1r_stream_source;
+typedef struct av1r_pipeline_stats {
+    uint64_t frames;   /* frames decoded (shown-existing included), all streams          */
+    uint64_t batches;  /* shared launches                                                  */
+    double elapsed_s;  /* wall time of the run, synchronisation included                  */
+    double produce_s;  /* producer time in src->next (e.g. parsing), summed over streams  */
+    double pack_s;     /* producer time in av1r_pack, summed over streams                 */
+    double wait_s;     /* launcher time with no stream ready                               */
+} av1r_pipeline_stats;
+int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
+                      av1r_pipeline_stats* stats);
+/* Source over in-memory batches: stream s yields batches[s][pos[s] % count[s]], then
+ * advances pos[s] (use av1r_cycle_next as `next` and an av1r_cycle as `user`). */
+typedef struct av1r_cycle {
+    const av1r_frame_batch* const* const* batches;
+    const int* count;
+    int64_t* pos;
+} av1r_cycle;
+int av1r_cycle_next(void* user, int stream, const av1r_frame_batch** batch);
+/* Source over IVF files (one per stream, caller-owned while the source lives): temporal
+ * units parsed by the host parser (include/av1p.h) on the producer threads. */
+int av1r_ivf_source_create(const uint8_t* const* files, const size_t* sizes, int n, av1r_stream_source* out);
+void av1r_ivf_source_destroy(av1r_stream_source* src);
+
 #ifdef __cplusplus
 }
 #endif

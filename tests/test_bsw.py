@@ -128,3 +128,25 @@ def test_gpu_ivf_pipeline_matches_reference_md5(native_lib):
     finally:
         for d in decs:
             d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_native_pipeline_ivf_matches_reference_md5(native_lib):
+    """av1r_pipeline_run over the IVF source (native producer threads, the bench's
+    ivf_end_to_end path) on four streams of different sizes, outputs kept."""
+    from av1dec_amd import Decoder
+    from av1dec_amd.pipeline import run_native
+    names = ["1080p_s1", "cif_gm_rotzoom", "640x360_tiles2x2_sb64", "odd_416x234_key3"]
+    decs = [Decoder(0) for _ in names]
+    try:
+        st = run_native(decs, "ivf", [stream(n) for n in names])
+        assert st["frames"] == sum(GOLD[n]["frames"] for n in names)
+        for n, d in zip(names, decs):
+            md = hashlib.md5()
+            while d.output_pending():
+                for p in d.get_output():
+                    md.update(p.tobytes())
+            assert md.hexdigest() == GOLD[n]["md5"], n
+    finally:
+        for d in decs:
+            d.close()

@@ -377,3 +377,31 @@ def test_gpu_pack_pipeline_matches_oracle():
         for k, m in enumerate(got):
             assert m == ref[k % F], f"stream {j} output {k}"
         d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_native_pipeline_matches_oracle():
+    """bench.py's headline path since round 2 (av1r_pipeline_run over in-memory batches: a
+    native packing thread per stream, GOP phases staggered, key frames alone) on 4 small
+    streams over two GOPs, in three runs that continue each other: bit-exact with the oracle."""
+    import bench
+    from av1dec_amd.pipeline import run_native
+    S, F = 4, 6
+    streams = [pysynth.stream(640, 360, F, 700 + j) for j in range(S)]
+    decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+    pp = bench.StreamScheduler(decs, F, streams=streams, workers=1)
+    pp.stagger()
+    pp.close()
+    pos = list(pp.pos)
+    for k in (F, 1, F - 1):
+        st = run_native(decs, "cycle", streams, pos, max_frames=k)
+        assert st["frames"] == S * k
+    for j, (d, s) in enumerate(zip(decs, streams)):
+        ref = _oracle_md5s(s)
+        got = []
+        while d.output_pending():
+            got.append(b"".join(hashlib.md5(p.tobytes()).digest() for p in d.get_output()))
+        assert len(got) == bench.gop_offsets(S, F)[j] + 2 * F
+        for k, m in enumerate(got):
+            assert m == ref[k % F], f"stream {j} output {k}"
+        d.close()
