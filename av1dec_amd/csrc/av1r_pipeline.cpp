@@ -1,10 +1,11 @@
 // av1r_pipeline.cpp -- many independent streams on one GPU, in native threads (include/av1r.h,
 // "multi-stream pipeline"; SURVEY.md §8e batching + §8f rank 4 parse || GPU).
 //
-// One producer thread per stream pulls the stream's frames in decode order from a source
-// (in-memory batches, or IVF temporal units parsed by the host parser) and packs each
-// (av1r_pack: validation, dependency schedule, pinned copy) into the stream's queue, up to
-// `depth` frames ahead.  The calling thread is the launcher: each round it takes the head of
+// A pool of worker threads pulls every stream's frames in decode order from a source
+// (in-memory batches, or IVF temporal units parsed by the host parser; one fetch per stream
+// at a time) and packs them (av1r_pack: validation, dependency schedule, pinned copy), up to
+// `depth` frames ahead per stream -- frames of one stream pack concurrently when the
+// source's batches outlive the next fetch (`stable`).  The calling thread is the launcher: each round it takes the head of
 // every stream that has one and is not running a key frame alone (av1r_busy), and decodes
 // them in shared launches (av1r_decode_packed_batch); a show-existing frame is applied on its
 // stream in order (av1r_show_existing).  This is the reference's per-stream Decoder::decode
@@ -16,7 +17,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
-#include <deque>
+#include <algorithm>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -38,81 +40,109 @@ struct Entry {
     int status = 0;
 };
 
+// Per stream: frames are fetched from the source in order (one fetch at a time: seq numbers
+// nextFetch), packed by any worker, and re-ordered by seq for the launcher (nextLaunch).
 struct StreamQ {
-    std::mutex m;
-    std::condition_variable space;
-    std::deque<Entry> q;
+    std::map<int64_t, Entry> ready;
+    int64_t nextFetch = 0, nextLaunch = 0;
+    bool pulling = false;  // a worker is inside src->next (or, unstable source, its pack)
+    bool ended = false;    // the end / error entry has been queued
     double produce_s = 0, pack_s = 0;
     std::string err;
 };
 
 struct Run {
     std::vector<StreamQ> qs;
-    std::atomic<bool> stop{false};
-    std::mutex wm;  // launcher wake-up
-    std::condition_variable ready;
+    const av1r_stream_source* src = nullptr;
+    int64_t maxFrames = 0;
     int depth = 3;
+    bool stable = false;
+    std::atomic<bool> stop{false};
+    std::mutex m;  // guards every StreamQ's bookkeeping (operations are tiny)
+    std::condition_variable work, ready;
+    int rr = 0;  // round-robin start of the workers' stream search
     explicit Run(int n) : qs(n) {}
 
-    void push(int s, const Entry& e)
+    // a stream with room that nobody is fetching from, or -1
+    int pick()
     {
-        StreamQ& Q = qs[s];
-        {
-            std::unique_lock<std::mutex> l(Q.m);
-            Q.space.wait(l, [&] { return (int)Q.q.size() < depth || stop.load(); });
-            if (stop.load() && e.p) {
-                av1r_packed_free(e.p);
-                return;
-            }
-            Q.q.push_back(e);
+        const int n = (int)qs.size();
+        for (int k = 0; k < n; k++) {
+            const int s = (rr + k) % n;
+            StreamQ& Q = qs[s];
+            if (Q.pulling || Q.ended || Q.nextFetch - Q.nextLaunch >= depth) continue;
+            rr = (s + 1) % n;
+            return s;
         }
-        std::lock_guard<std::mutex> l(wm);
-        ready.notify_one();
+        return -1;
     }
 };
 
-void producer(Run* R, int s, const av1r_stream_source* src, int64_t maxFrames)
+void worker(Run* R)
 {
-    StreamQ& Q = R->qs[s];
-    int64_t made = 0;
-    Entry e;
-    while (!R->stop.load() && (maxFrames <= 0 || made < maxFrames)) {
+    std::unique_lock<std::mutex> l(R->m);
+    while (!R->stop.load()) {
+        const int s = R->pick();
+        if (s < 0) {
+            R->work.wait(l);
+            continue;
+        }
+        StreamQ& Q = R->qs[s];
+        const int64_t seq = Q.nextFetch++;
+        Entry e;
+        if (R->maxFrames > 0 && seq >= R->maxFrames) {  // this stream's share is done
+            e.kind = 2;
+            Q.ended = true;
+            Q.ready[seq] = e;
+            R->ready.notify_one();
+            continue;
+        }
+        Q.pulling = true;
+        l.unlock();
         const av1r_frame_batch* b = nullptr;
         const auto t0 = Clock::now();
-        const int rc = src->next(src->user, s, &b);
+        const int rc = R->src->next(R->src->user, s, &b);
         const auto t1 = Clock::now();
-        Q.produce_s += secs(t1 - t0);
-        if (rc == 1) break;
-        if (rc < 0 || !b || !b->hdr) {
-            e = Entry();
-            e.kind = 3;
-            e.status = rc < 0 ? rc : AV1R_E_INVALID;
-            Q.err = "stream " + std::to_string(s) + ": source failed";
-            R->push(s, e);
-            return;
-        }
-        e = Entry();
-        if (b->hdr->show_existing_frame) {
-            e.kind = 1;
-            e.show = b->hdr->frame_to_show;
-            e.refresh = b->hdr->refresh_frame_flags;
-        } else {
+        double packS = 0;
+        bool released = false;
+        if (rc == 0 && b && b->hdr && !b->hdr->show_existing_frame) {
+            if (R->stable) {  // the batch outlives the next fetch: let another worker fetch
+                l.lock();
+                Q.pulling = false;
+                R->work.notify_one();
+                l.unlock();
+                released = true;
+            }
             const int pr = av1r_pack(b, &e.p);
-            Q.pack_s += secs(Clock::now() - t1);
+            packS = secs(Clock::now() - t1);
             if (pr) {
                 e.kind = 3;
                 e.status = pr;
+                e.p = nullptr;
+                l.lock();
                 Q.err = "stream " + std::to_string(s) + ": av1r_pack: " + av1r_pack_last_error();
-                R->push(s, e);
-                return;
+                l.unlock();
             }
+        } else if (rc == 0 && b && b->hdr) {
+            e.kind = 1;
+            e.show = b->hdr->frame_to_show;
+            e.refresh = b->hdr->refresh_frame_flags;
+        } else if (rc == 1) {
+            e.kind = 2;
+        } else {
+            e.kind = 3;
+            e.status = rc < 0 ? rc : AV1R_E_INVALID;
         }
-        R->push(s, e);
-        made++;
+        l.lock();
+        if (!released) Q.pulling = false;
+        if (e.kind == 3 && Q.err.empty()) Q.err = "stream " + std::to_string(s) + ": source failed";
+        if (e.kind >= 2) Q.ended = true;
+        Q.produce_s += secs(t1 - t0);
+        Q.pack_s += packS;
+        Q.ready[seq] = e;
+        R->ready.notify_one();
+        R->work.notify_one();
     }
-    e = Entry();
-    e.kind = 2;
-    R->push(s, e);
 }
 
 // ---- built-in sources ----
@@ -179,6 +209,7 @@ int av1r_ivf_source_create(const uint8_t* const* files, const size_t* sizes, int
     }
     out->next = ivf_next;
     out->user = S;
+    out->stable = 0;  // a unit's batches live until the parser's next unit
     return AV1R_OK;
 }
 
@@ -193,15 +224,19 @@ void av1r_ivf_source_destroy(av1r_stream_source* src)
 }
 
 int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
-                      av1r_pipeline_stats* stats)
+                      int workers, av1r_pipeline_stats* stats)
 {
     if (!ctxs || n <= 0 || n > 32 || !src || !src->next) return AV1R_E_INVALID;
     Run R(n);
+    R.src = src;
+    R.maxFrames = max_frames;
     R.depth = depth > 0 ? depth : 3;
+    R.stable = src->stable != 0;
+    const int W = std::max(1, std::min(workers > 0 ? workers : n, 64));
     const auto t0 = Clock::now();
     std::vector<std::thread> th;
-    th.reserve(n);
-    for (int s = 0; s < n; s++) th.emplace_back(producer, &R, s, src, max_frames);
+    th.reserve(W);
+    for (int w = 0; w < W; w++) th.emplace_back(worker, &R);
     std::vector<bool> done(n, false);
     int live = n, rc = AV1R_OK;
     uint64_t frames = 0, batches = 0;
@@ -219,12 +254,15 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
             for (;;) {
                 Entry e;
                 {
-                    std::lock_guard<std::mutex> l(Q.m);
-                    if (Q.q.empty()) break;
-                    e = Q.q.front();
-                    Q.q.pop_front();
+                    std::lock_guard<std::mutex> l(R.m);
+                    auto it = Q.ready.find(Q.nextLaunch);
+                    if (it == Q.ready.end()) break;
+                    e = it->second;
+                    Q.ready.erase(it);
+                    Q.nextLaunch++;
+                    if (e.kind == 3) err = Q.err;
+                    R.work.notify_one();  // room for this stream again
                 }
-                Q.space.notify_one();
                 if (e.kind == 0) {
                     bc.push_back(ctxs[s]);
                     bp.push_back(e.p);
@@ -236,11 +274,7 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
                     if (rc) break;
                     continue;
                 }
-                if (e.kind == 3) {
-                    rc = e.status;
-                    std::lock_guard<std::mutex> l(Q.m);
-                    err = Q.err;
-                }
+                if (e.kind == 3) rc = e.status;
                 done[s] = true;
                 live--;
                 break;
@@ -256,25 +290,25 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
             frames += bc.size();
             batches++;
         } else if (live > 0 && rc == AV1R_OK) {
-            // nothing ready: a producer's push wakes us; a key frame running alone does not,
+            // nothing ready: a worker's push wakes us; a key frame running alone does not,
             // hence the short bound
             const auto w0 = Clock::now();
-            std::unique_lock<std::mutex> l(R.wm);
+            std::unique_lock<std::mutex> l(R.m);
             R.ready.wait_for(l, std::chrono::microseconds(50));
             wait_s += secs(Clock::now() - w0);
         }
     }
-    // stop and drain the producers (an error ends the run early)
-    R.stop.store(true);
-    for (auto& Q : R.qs) {
-        std::lock_guard<std::mutex> l(Q.m);
-        Q.space.notify_all();
+    // stop and drain the workers (an error ends the run early)
+    {
+        std::lock_guard<std::mutex> l(R.m);
+        R.stop.store(true);
+        R.work.notify_all();
     }
     for (auto& t : th) t.join();
     double produce_s = 0, pack_s = 0;
     for (auto& Q : R.qs) {
-        for (auto& e : Q.q)
-            if (e.p) av1r_packed_free(e.p);
+        for (auto& kv : Q.ready)
+            if (kv.second.p) av1r_packed_free(kv.second.p);
         produce_s += Q.produce_s;
         pack_s += Q.pack_s;
     }

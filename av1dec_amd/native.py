@@ -201,7 +201,7 @@ def lib():
     l.av1r_decode_packed_batch.argtypes = [C.POINTER(vp), C.POINTER(vp), i]
     l.av1r_busy.argtypes = [vp]
     l.av1r_pack_profile.argtypes = [C.POINTER(C.c_uint64), i, i]
-    l.av1r_pipeline_run.argtypes = [C.POINTER(vp), i, C.POINTER(StreamSource), C.c_int64, i, C.POINTER(PipelineStats)]
+    l.av1r_pipeline_run.argtypes = [C.POINTER(vp), i, C.POINTER(StreamSource), C.c_int64, i, i, C.POINTER(PipelineStats)]
     l.av1r_cycle_next.argtypes = [vp, i, C.POINTER(vp)]
     l.av1r_ivf_source_create.argtypes = [C.POINTER(vp), C.POINTER(C.c_size_t), i, C.POINTER(StreamSource)]
     l.av1r_ivf_source_destroy.argtypes = [C.POINTER(StreamSource)]
@@ -211,7 +211,7 @@ def lib():
 
 
 class StreamSource(C.Structure):  # av1r_stream_source
-    _fields_ = [("next", C.c_void_p), ("user", C.c_void_p)]
+    _fields_ = [("next", C.c_void_p), ("user", C.c_void_p), ("stable", C.c_int)]
 
 
 class PipelineStats(C.Structure):  # av1r_pipeline_stats

@@ -130,9 +130,9 @@ class IvfPipeline:
         return time.perf_counter() - t0
 
 
-def run_native(decoders, source="cycle", streams=None, positions=None, max_frames=0, depth=3):
+def run_native(decoders, source="cycle", streams=None, positions=None, max_frames=0, depth=3, workers=0):
     """The same pipeline in native threads (av1r_pipeline_run, include/av1r.h): no
-    interpreter on the path.  source "cycle": streams = per-stream lists of batchfile.Frame;
+    interpreter on the path (`workers` packing threads, 0: one per stream).  source "cycle": streams = per-stream lists of batchfile.Frame;
     stream j continues at frame positions[j] (mod its length), and positions is advanced in
     place by the frames decoded; "ivf": streams = IVF file contents.  Returns the
     av1r_pipeline_stats as a dict."""
@@ -153,6 +153,7 @@ def run_native(decoders, source="cycle", streams=None, positions=None, max_frame
         keep += [rows, table, count, pos, cyc, streams]
         src.next = C.cast(l.av1r_cycle_next, C.c_void_p).value
         src.user = C.cast(C.pointer(cyc), C.c_void_p).value
+        src.stable = 1
     elif source == "ivf":
         bufs = [C.create_string_buffer(bytes(s), len(s)) for s in streams]
         files = (C.c_void_p * n)(*[C.cast(b, C.c_void_p).value for b in bufs])
@@ -165,7 +166,7 @@ def run_native(decoders, source="cycle", streams=None, positions=None, max_frame
         raise ValueError(source)
     st = native.PipelineStats()
     try:
-        rc = l.av1r_pipeline_run(ctxs, n, C.byref(src), int(max_frames), int(depth), C.byref(st))
+        rc = l.av1r_pipeline_run(ctxs, n, C.byref(src), int(max_frames), int(depth), int(workers), C.byref(st))
     finally:
         if source == "ivf":
             l.av1r_ivf_source_destroy(C.byref(src))

@@ -335,7 +335,7 @@ def main():
     # (the native pipeline, av1r_pipeline_run: one producer thread per stream packs its frames
     # up to 3 ahead, the calling thread launches one frame of every ready stream per batch)
     from av1dec_amd.pipeline import run_native
-    workers = S
+    workers = host_workers()
     pp = StreamScheduler(decs, F, streams=streams, workers=1)
     pp.stagger()
     pp.close()
@@ -343,19 +343,19 @@ def main():
     pos = list(pp.pos)
     t_prime = time.perf_counter()
     while time.perf_counter() - t_prime < 1.0:
-        run_native(decs, "cycle", streams, pos, max_frames=F)
-    run_native(decs, "cycle", streams, pos, max_frames=args.warmup)
+        run_native(decs, "cycle", streams, pos, max_frames=F, workers=workers)
+    run_native(decs, "cycle", streams, pos, max_frames=args.warmup, workers=workers)
     if dist:
         dist.barrier()
     pos0 = list(pos)
     t0 = time.perf_counter()
-    pr = run_native(decs, "cycle", streams, pos, max_frames=args.steps)  # synchronizes every context
+    pr = run_native(decs, "cycle", streams, pos, max_frames=args.steps, workers=workers)  # synchronizes every context
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     fps = aggregate_fps(world, args.steps * S, elapsed)
     timed = [(j, t % F) for j in range(S) for t in range(pos0[j], pos0[j] + args.steps)]
     n_key = sum(1 for j, t in timed if streams[j][t].hdr.frame_type == 0)
     host_profile = {  # where the host-inclusive pipeline spends its time (rank 0)
-        "producer_threads": workers,
+        "packing_threads": workers,
         "pack_ms_per_frame": round(1e3 * pr["pack_s"] / max(pr["frames"], 1), 3),
         "producer_utilisation": round(pr["pack_s"] / (workers * elapsed), 3),
         "launcher_idle_ms_per_step": round(1e3 * pr["wait_s"] / max(args.steps, 1), 3),
@@ -511,8 +511,8 @@ def main():
                                    f"stream j offset by j*{F}/{S} frames; tiles {tiles[0]}x{tiles[1]}; seeds "
                                    f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
                                    f"host-inclusive: each frame validated, scheduled, packed and uploaded from "
-                                   f"host memory inside the timed region (native pipeline: a packing thread per "
-                                   f"stream, 3 frames ahead; key frames run alone on their stream, overlapping "
+                                   f"host memory inside the timed region (native pipeline: {workers} packing "
+                                   f"threads, 3 frames ahead per stream; key frames run alone on their stream, overlapping "
                                    f"the other streams' batches); timed frames: {args.steps * S} of which {n_key} key",
                        "host_threads": workers + 1,
                        "timed_key_frames": n_key,

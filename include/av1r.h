@@ -315,9 +315,9 @@ int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int 
 size_t av1r_sizeof(int which);
 
 /* ---- multi-stream pipeline (av1r_pipeline.cpp; SURVEY.md 8e + 8f rank 4) ----
- * n independent streams (contexts on one device) decoded end to end in native threads: one
- * producer thread per stream pulls its frames in decode order from `src` and packs them
- * (av1r_pack) up to `depth` ahead; the calling thread launches one frame of every ready
+ * n independent streams (contexts on one device) decoded end to end in native threads:
+ * `workers` threads pull each stream's frames in decode order from `src` and pack them
+ * (av1r_pack) up to `depth` ahead per stream; the calling thread launches one frame of every ready
  * stream per shared launch (av1r_decode_packed_batch), applies show-existing frames in
  * order (av1r_show_existing), and finally synchronizes every context.  Stops after
  * max_frames frames per stream (<= 0: at each source's end).  The reference's per-stream
@@ -329,6 +329,9 @@ typedef struct av1r_stream_source {
      * Returns 0 (a frame), 1 (end of stream) or a negative status. */
     int (*next)(void* user, int stream, const av1r_frame_batch** batch);
     void* user;
+    /* 1: a returned batch stays valid until the run ends (then several frames of a stream
+     * are packed concurrently); 0: only until the next call for that stream */
+    int stable;
 } av1r_stream_source;
 typedef struct av1r_pipeline_stats {
     uint64_t frames;   /* frames decoded (shown-existing included), all streams          */
@@ -339,7 +342,7 @@ typedef struct av1r_pipeline_stats {
     double wait_s;     /* launcher time with no stream ready                               */
 } av1r_pipeline_stats;
 int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
-                      av1r_pipeline_stats* stats);
+                      int workers, av1r_pipeline_stats* stats);
 /* Source over in-memory batches: stream s yields batches[s][pos[s] % count[s]], then
  * advances pos[s] (use av1r_cycle_next as `next` and an av1r_cycle as `user`). */
 typedef struct av1r_cycle {
