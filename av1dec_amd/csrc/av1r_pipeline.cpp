@@ -12,6 +12,7 @@
 // loop (decoder/Av1Decoder.cpp:49-109) with reconstruction batched across streams, and with
 // no interpreter anywhere on the path.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -244,10 +245,18 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
     std::vector<av1r_ctx*> bc;
     std::vector<av1r_packed*> bp;
     std::string err;
+    // AV1R_PIPE_GROUPS=g: the streams form g groups whose batches go to g different HIP
+    // streams (each batch runs on its first member's stream), so one group's latency-bound
+    // k_flow overlaps the other groups' kernels
+    static const int groups = std::max(1, getenv("AV1R_PIPE_GROUPS") ? atoi(getenv("AV1R_PIPE_GROUPS")) : 1);
+    const int G = std::min(groups, n);
+    int g = 0;
     while (live > 0 && rc == AV1R_OK) {
         bc.clear();
         bp.clear();
-        for (int s = 0; s < n && rc == AV1R_OK; s++) {
+        const int sBeg = g * n / G, sEnd = (g + 1) * n / G;
+        g = (g + 1) % G;
+        for (int s = sBeg; s < sEnd && rc == AV1R_OK; s++) {
             if (done[s] || av1r_busy(ctxs[s]) == 1) continue;
             StreamQ& Q = R.qs[s];
             // show-existing frames of this stream apply in order ahead of its next frame
@@ -289,8 +298,8 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
             }
             frames += bc.size();
             batches++;
-        } else if (live > 0 && rc == AV1R_OK) {
-            // nothing ready: a worker's push wakes us; a key frame running alone does not,
+        } else if (live > 0 && rc == AV1R_OK && g == 0) {
+            // nothing ready in any group: a worker's push wakes us; a key frame running alone does not,
             // hence the short bound
             const auto w0 = Clock::now();
             std::unique_lock<std::mutex> l(R.m);

@@ -873,31 +873,31 @@ extern "C" __global__ __launch_bounds__(256) void k_mi_blocks(const KParams* kps
         for (int i = 0; i < 6; i++) d[i] = w[i];
     }
 }
+// 16 lanes per transform block, one 4x4 unit each in turn (a 64x64 TB covers 256 units: one
+// lane per TB serialised them behind its largest TB)
 extern "C" __global__ __launch_bounds__(256) void k_mi_tbs(const KParams* kps)
 {
     const KParams& k = KP(kps, blockIdx.y);
-    const uint32_t ti = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t ti = blockIdx.x * 16 + (threadIdx.x >> 4);
     if (ti >= k.n_tbs) return;
     const av1r_tb& t = k.tbs[ti];
     const int sub = t.plane ? 1 : 0;
     const int row = (t.y << sub) >> 2, col = (t.x << sub) >> 2;
-    const int stepX = av1r_tx_w[t.tx_size] >> 2, stepY = av1r_tx_h[t.tx_size] >> 2;
-    uint8_t* base = reinterpret_cast<uint8_t*>(const_cast<av1r_mi*>(k.mi));
-    for (int i = 0; i < (stepY << sub); i++) {
-        const int r = row + i;
-        if (r >= k.mi_rows_alloc) break;
-        for (int j = 0; j < (stepX << sub); j++) {
-            const int c = col + j;
-            if (c >= k.mi_stride) break;
-            base[((size_t)r * k.mi_stride + c) * sizeof(av1r_mi) + offsetof(av1r_mi, lf_tx) + t.plane] = t.tx_size;
-        }
+    const int w4 = (av1r_tx_w[t.tx_size] >> 2) << sub, h4 = (av1r_tx_h[t.tx_size] >> 2) << sub;
+    const int wIn = min(w4, k.mi_stride - col), hIn = min(h4, k.mi_rows_alloc - row);
+    if (wIn <= 0 || hIn <= 0) return;
+    uint8_t* base = reinterpret_cast<uint8_t*>(const_cast<av1r_mi*>(k.mi)) + offsetof(av1r_mi, lf_tx) + t.plane;
+    const uint8_t v = t.tx_size;
+    for (int q = threadIdx.x & 15; q < wIn * hIn; q += 16) {
+        const int r = row + q / wIn, c = col + q % wIn;
+        base[((size_t)r * k.mi_stride + c) * sizeof(av1r_mi)] = v;
     }
 }
 void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s)
 {
     hipLaunchKernelGGL(k_mi_zero, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps);
     if (maxBlocks) hipLaunchKernelGGL(k_mi_blocks, dim3((maxBlocks + 15) / 16, n), dim3(256), 0, s, kps);
-    if (maxTbs) hipLaunchKernelGGL(k_mi_tbs, dim3((maxTbs + 255) / 256, n), dim3(256), 0, s, kps);
+    if (maxTbs) hipLaunchKernelGGL(k_mi_tbs, dim3((maxTbs + 15) / 16, n), dim3(256), 0, s, kps);
 }
 
 // plain visible-region copy (stage snapshots)
