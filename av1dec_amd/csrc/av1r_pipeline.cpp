@@ -241,7 +241,7 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
     std::vector<bool> done(n, false);
     int live = n, rc = AV1R_OK;
     uint64_t frames = 0, batches = 0;
-    double wait_s = 0;
+    double wait_s = 0, launch_s = 0;
     std::vector<av1r_ctx*> bc;
     std::vector<av1r_packed*> bp;
     std::string err;
@@ -290,7 +290,9 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
             }
         }
         if (!bc.empty()) {
+            const auto l0 = Clock::now();
             const int r = av1r_decode_packed_batch(bc.data(), bp.data(), (int)bc.size());
+            launch_s += secs(Clock::now() - l0);
             for (auto* p : bp) av1r_packed_free(p);
             if (r && rc == AV1R_OK) {
                 rc = r;
@@ -335,6 +337,7 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
         stats->produce_s = produce_s;
         stats->pack_s = pack_s;
         stats->wait_s = wait_s;
+        stats->launch_s = launch_s;
     }
     if (rc) fprintf(stderr, "av1r_pipeline_run: %s\n", err.c_str());
     return rc;

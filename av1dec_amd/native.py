@@ -216,7 +216,8 @@ class StreamSource(C.Structure):  # av1r_stream_source
 
 class PipelineStats(C.Structure):  # av1r_pipeline_stats
     _fields_ = [("frames", C.c_uint64), ("batches", C.c_uint64), ("elapsed_s", C.c_double),
-                ("produce_s", C.c_double), ("pack_s", C.c_double), ("wait_s", C.c_double)]
+                ("produce_s", C.c_double), ("pack_s", C.c_double), ("wait_s", C.c_double),
+                ("launch_s", C.c_double)]
 
 
 class Cycle(C.Structure):  # av1r_cycle

@@ -256,7 +256,9 @@ def ivf_leg(decs, streams, frames):
 
 def host_workers():
     """Packing threads: the box's CPU share (OMP_NUM_THREADS is set to it there) less the
-    launching thread."""
+    launching thread (AV1R_BENCH_WORKERS overrides, A/B)."""
+    if os.environ.get("AV1R_BENCH_WORKERS"):
+        return int(os.environ["AV1R_BENCH_WORKERS"])
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     return max(1, min(share, 32) - 1)
 
@@ -359,6 +361,7 @@ def main():
         "pack_ms_per_frame": round(1e3 * pr["pack_s"] / max(pr["frames"], 1), 3),
         "producer_utilisation": round(pr["pack_s"] / (workers * elapsed), 3),
         "launcher_idle_ms_per_step": round(1e3 * pr["wait_s"] / max(args.steps, 1), 3),
+        "launcher_submit_ms_per_step": round(1e3 * pr["launch_s"] / max(args.steps, 1), 3),
         "batches": int(pr["batches"]),
     }
     pp.pos = list(pos)

@@ -340,6 +340,7 @@ typedef struct av1r_pipeline_stats {
     double produce_s;  /* producer time in src->next (e.g. parsing), summed over streams  */
     double pack_s;     /* producer time in av1r_pack, summed over streams                 */
     double wait_s;     /* launcher time with no stream ready                               */
+    double launch_s;   /* launcher time inside av1r_decode_packed_batch                    */
 } av1r_pipeline_stats;
 int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
                       int workers, av1r_pipeline_stats* stats);
