@@ -119,13 +119,16 @@ struct av1r_ctx {
     bool keepStages = true;
     Upload up[2];
     int upIdx = 0;
-    static constexpr int kPackRing = 3;  // device slots of packed uploads (av1r_decode_packed_batch)
+#ifndef AV1R_RING
+#define AV1R_RING 3
+#endif
+    static constexpr int kPackRing = AV1R_RING;  // device slots of packed uploads (av1r_decode_packed_batch)
     Upload pk[kPackRing];
     int pkIdx = 0;
     hipEvent_t pkReady = nullptr;  // the packed uploads of a batch (lead's copy stream) have landed
     // per-launch metadata (KParams, tables, flow groups): a ring, uploaded on a copy stream
     // of its own so that the copy of batch N + 1 overlaps the kernels of batch N
-    static constexpr int kMetaRing = 3;
+    static constexpr int kMetaRing = AV1R_RING;
     Upload meta[kMetaRing];
     int metaIdx = 0;
     hipStream_t copyStream = nullptr;

@@ -250,12 +250,29 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
     // k_flow overlaps the other groups' kernels
     static const int groups = std::max(1, getenv("AV1R_PIPE_GROUPS") ? atoi(getenv("AV1R_PIPE_GROUPS")) : 1);
     const int G = std::min(groups, n);
+    static const double fillUs = getenv("AV1R_PIPE_WAIT_US") ? atof(getenv("AV1R_PIPE_WAIT_US")) : 300.0;
     int g = 0;
     while (live > 0 && rc == AV1R_OK) {
         bc.clear();
         bp.clear();
         const int sBeg = g * n / G, sEnd = (g + 1) * n / G;
         g = (g + 1) % G;
+        // full batches: while a stream that could join (live, not running a key frame alone)
+        // has nothing packed yet, wait for it up to AV1R_PIPE_WAIT_US (bigger launches keep
+        // the GPU busier than a partial batch launched early)
+        if (fillUs > 0) {
+            const auto f0 = Clock::now();
+            std::unique_lock<std::mutex> l(R.m);
+            for (;;) {
+                int missing = 0;
+                for (int s = sBeg; s < sEnd; s++)
+                    if (!done[s] && R.qs[s].ready.find(R.qs[s].nextLaunch) == R.qs[s].ready.end() && av1r_busy(ctxs[s]) != 1)
+                        missing++;
+                if (!missing || secs(Clock::now() - f0) * 1e6 >= fillUs) break;
+                R.ready.wait_for(l, std::chrono::microseconds(20));
+            }
+            wait_s += secs(Clock::now() - f0);
+        }
         for (int s = sBeg; s < sEnd && rc == AV1R_OK; s++) {
             if (done[s] || av1r_busy(ctxs[s]) == 1) continue;
             StreamQ& Q = R.qs[s];

@@ -338,6 +338,7 @@ def main():
     # up to 3 ahead, the calling thread launches one frame of every ready stream per batch)
     from av1dec_amd.pipeline import run_native
     workers = host_workers()
+    depth = int(os.environ.get("AV1R_BENCH_DEPTH", "3"))  # frames packed ahead per stream
     pp = StreamScheduler(decs, F, streams=streams, workers=1)
     pp.stagger()
     pp.close()
@@ -345,13 +346,13 @@ def main():
     pos = list(pp.pos)
     t_prime = time.perf_counter()
     while time.perf_counter() - t_prime < 1.0:
-        run_native(decs, "cycle", streams, pos, max_frames=F, workers=workers)
-    run_native(decs, "cycle", streams, pos, max_frames=args.warmup, workers=workers)
+        run_native(decs, "cycle", streams, pos, max_frames=F, workers=workers, depth=depth)
+    run_native(decs, "cycle", streams, pos, max_frames=args.warmup, workers=workers, depth=depth)
     if dist:
         dist.barrier()
     pos0 = list(pos)
     t0 = time.perf_counter()
-    pr = run_native(decs, "cycle", streams, pos, max_frames=args.steps, workers=workers)  # synchronizes every context
+    pr = run_native(decs, "cycle", streams, pos, max_frames=args.steps, workers=workers, depth=depth)  # synchronizes every context
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     fps = aggregate_fps(world, args.steps * S, elapsed)
     timed = [(j, t % F) for j in range(S) for t in range(pos0[j], pos0[j] + args.steps)]
@@ -515,7 +516,7 @@ def main():
                                    f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
                                    f"host-inclusive: each frame validated, scheduled, packed and uploaded from "
                                    f"host memory inside the timed region (native pipeline: {workers} packing "
-                                   f"threads, 3 frames ahead per stream; key frames run alone on their stream, overlapping "
+                                   f"threads, {depth} frames ahead per stream; key frames run alone on their stream, overlapping "
                                    f"the other streams' batches); timed frames: {args.steps * S} of which {n_key} key",
                        "host_threads": workers + 1,
                        "timed_key_frames": n_key,
