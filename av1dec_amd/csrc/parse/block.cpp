@@ -438,6 +438,24 @@ void BlockParser::decode_partition(int r, int c, int bsize)
 // ------------------------------------------------------------------------------------
 // block (Block::Block + Block::parse, Block.cpp:46-88, 313-363)
 // ------------------------------------------------------------------------------------
+#ifdef AV1P_PROF  // debug aid: cycles per phase of the block walk, printed at exit
+#include <x86intrin.h>
+struct ProfAcc {
+    uint64_t t[10] = {};
+    ~ProfAcc()
+    {
+        fprintf(stderr, "av1p prof (Mcycles): mode %.1f residual %.1f mi %.1f emit %.1f | coef: head %.1f eob %.1f levels %.1f signs %.1f pack %.1f\n",
+                t[0] / 1e6, t[1] / 1e6, t[2] / 1e6, t[3] / 1e6, t[4] / 1e6, t[5] / 1e6, t[6] / 1e6, t[7] / 1e6, t[8] / 1e6);
+    }
+};
+static ProfAcc g_prof;
+#define PROF_T(v) const uint64_t v = __rdtsc()
+#define PROF_ADD(i, a, b) g_prof.t[i] += (b) - (a)
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, a, b)
+#endif
+
 void BlockParser::decode_block(int r, int c, int bsize)
 {
     if (!P.err.empty()) return;
@@ -463,12 +481,15 @@ void BlockParser::decode_block(int r, int c, int bsize)
     b.qindex = P.current_q;
     tbs.clear();
 
+    PROF_T(t0);
     if (fh.frame_is_intra) intra_frame_mode_info(b);
     else inter_frame_mode_info(b);
     palette_tokens(b);
     read_block_tx_size(b);
     if (b.skip) reset_block_context(b);
     const bool isCompound = b.ref[1] > INTRA_FRAME;
+    PROF_T(t1);
+    PROF_ADD(0, t0, t1);
     for (int y = 0; y < b.bh4; y++)
         for (int x = 0; x < b.bw4; x++) {
             MiInfo& m = mi(r + y, c + x);
@@ -486,7 +507,11 @@ void BlockParser::decode_block(int r, int c, int bsize)
                 for (int l = 0; l < 1 + isCompound; l++) m.mv[l] = b.mv[l];
             }
         }
+    PROF_T(t2);
     residual(b);
+    PROF_T(t3);
+    PROF_ADD(2, t1, t2);
+    PROF_ADD(1, t2, t3);
     if (!P.err.empty()) return;
     uint32_t palIdx = ~0u;
     if (b.pal_y || b.pal_uv) {
@@ -508,7 +533,11 @@ void BlockParser::decode_block(int r, int c, int bsize)
             m.pal_idx = palIdx;
             for (int i = 0; i < 4; i++) m.delta_lf[i] = (int8_t)P.delta_lf[i];
         }
+    PROF_T(t4);
     emit(b);
+    PROF_T(t5);
+    PROF_ADD(2, t3, t4);
+    PROF_ADD(3, t4, t5);
 }
 
 bool BlockParser::read_skip(Blk& b)
@@ -2116,6 +2145,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         for (int i = 0; i < w4; i++)
             for (int j = 0; j < h4; j++) P.mi[(size_t)(y4 + j) * P.mi_stride + x4 + i].tx_type = (uint8_t)type;
     };
+    PROF_T(c0);
     const int azCtx = all_zero_ctx(b, plane, txSz, x4, y4, w, h);
 #ifdef AV1P_TRACE
     {
@@ -2171,6 +2201,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 if (L(1)) eob += 1 << eobShift;
             }
         }
+        PROF_T(c2);
         // levels, in reverse scan order
         const int adj = kAdjustedTxSize[txSz];
         const int bwl = av1r_tx_w_log2[adj];
@@ -2227,6 +2258,8 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             lvl[(pos >> bwl) * ps + (pos & (width - 1))] = 0;
         }
         (void)height;
+        PROF_T(c3);
+        PROF_ADD(6, c2, c3);
         // signs and Golomb remainders, in scan order
         for (int c = 0; c < eob; c++) {
             const int pos = scan[c];
@@ -2285,6 +2318,8 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         }
 #endif
         culLevel = std::min(63, culLevel);
+        PROF_T(c4);
+        PROF_ADD(7, c3, c4);
         // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j, in
         // raster order over the bounding box of the scanned positions, which is cleared again
         std::vector<uint32_t>& out = P.cur->coefs;
@@ -2313,6 +2348,12 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             return 0;
         }
     }
+#ifdef AV1P_PROF
+    {
+        PROF_T(c5);
+        PROF_ADD(8, c0, c5);  // (head, eob: below)
+    }
+#endif
     std::fill_n(&P.above_level[plane][x4], w4, (int16_t)culLevel);
     std::fill_n(&P.above_dc[plane][x4], w4, (uint8_t)dcCategory);
     std::fill_n(&P.left_level[plane][y4], h4, (int16_t)culLevel);
