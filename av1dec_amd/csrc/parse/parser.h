@@ -222,12 +222,10 @@ struct SymbolDecoder {
     {
         const int cnt = cdf[nsym];
         const int rate = 3 + (cnt > 15) + (cnt > 31) + (nsym >= 4 ? 2 : nsym >= 2 ? 1 : 0);
-        uint32_t tmp = 1u << 15;
-        for (int i = 0; i < nsym - 1; i++) {
-            if (i == sym) tmp = 0;
-            if (tmp < cdf[i]) cdf[i] -= (uint16_t)((cdf[i] - tmp) >> rate);
-            else cdf[i] += (uint16_t)((tmp - cdf[i]) >> rate);
-        }
+        // below the symbol the (inverted) CDF moves up toward 32768, from it on down toward 0
+        // (the spec's single loop with tmp = 32768 / 0, as two branch-free runs)
+        for (int i = 0; i < sym; i++) cdf[i] += (uint16_t)((32768u - cdf[i]) >> rate);
+        for (int i = sym; i < nsym - 1; i++) cdf[i] -= (uint16_t)(cdf[i] >> rate);
         cdf[nsym] += cdf[nsym] < 32;
     }
     int boolean()  // read_literal bit: probability 1/2, never adapted
