@@ -143,8 +143,16 @@ struct av1r_ctx {
     unsigned long long* traceDev = nullptr;
     size_t traceCap = 0;
     std::string err;
-    // schedule scratch
-    std::vector<int16_t> lvlmap[3];
+    // schedule scratch: per 4x4 unit and plane, its level (the item that last wrote it), its
+    // owner node and whether it is on its owner's bottom row / right column (one 8-byte
+    // record per unit: the three lookups of a unit share a cache line)
+    struct MapUnit {
+        int32_t owner;
+        int16_t lvl;
+        uint8_t emit;
+        uint8_t pad;
+    };
+    std::vector<MapUnit> umap[3];
     int mapW[3] = {}, mapH[3] = {};
     std::vector<std::vector<uint32_t>> lvP, lvB, lvT;  // inter tiles, inter-intra blends, TBs per level
     std::vector<WorkItem> items;
@@ -152,7 +160,6 @@ struct av1r_ctx {
     // k_flow dependencies: per 4x4 unit the node (TB / inter-intra item, decode order) that
     // last wrote it (-1: nothing, or an inter tile of the preceding launch); per node its
     // dependency nodes (CSR); then, in item order, the dependencies' item positions
-    std::vector<int32_t> owner[3];
     std::vector<uint32_t> nodeDepStart;
     std::vector<int32_t> nodeDeps, nodeOfTb, nodeOfBlk, nodePos;
     std::vector<uint32_t> deps;
@@ -163,7 +170,6 @@ struct av1r_ctx {
     // bottom row / right column of its owner (the units whose granules the owner stores);
     // per node 12 mask words (4 per plane: the above and left runs' units written by an
     // item of the launch); granOk = every such unit a consumer reads has its granule
-    std::vector<uint8_t> emit[3];
     std::vector<uint32_t> nodeMask;
     bool granOk = false;
     uint64_t* granDev = nullptr;
@@ -491,9 +497,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         // k_flow only (flowOnly): the levels just order the items, dependencies carry the
         // hand-offs, so the inter predictions' level 0 is the map's initial value and the
         // plain inter blocks need not be painted (below)
-        c->lvlmap[p].assign((size_t)c->mapW[p] * c->mapH[p], flowOnly ? 0 : -1);
-        c->owner[p].assign((size_t)c->mapW[p] * c->mapH[p], -1);
-        c->emit[p].assign((size_t)c->mapW[p] * c->mapH[p], 0);
+        c->umap[p].assign((size_t)c->mapW[p] * c->mapH[p], av1r_ctx::MapUnit{-1, (int16_t)(flowOnly ? 0 : -1), 0, 0});
     }
     static const bool granEnv = !getenv("AV1R_GRAN") || atoi(getenv("AV1R_GRAN")) != 0;
     c->granOk = granEnv && allowGran;
@@ -510,10 +514,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         x1 = std::min(x1, c->mapW[p] - 1);
         y1 = std::min(y1, c->mapH[p] - 1);
         for (int y = y0; y <= y1; y++) {
-            const int32_t* row = &c->owner[p][(size_t)y * c->mapW[p]];
+            const av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
             int32_t last = -1;
             for (int x = x0; x <= x1; x++)
-                if (row[x] >= 0 && row[x] != last) dl.push_back(last = row[x]);
+                if (row[x].owner >= 0 && row[x].owner != last) dl.push_back(last = row[x].owner);
         }
     };
     // the owners of the pixels an intra prediction reads (coop_intra_edges): with granules,
@@ -531,9 +535,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 const int ux = horiz ? u : (x - 1) >> 2, uy = horiz ? (y - 1) >> 2 : u;
                 if (ux < 0 || uy < 0 || ux >= c->mapW[p] || uy >= c->mapH[p]) continue;
                 const size_t i = (size_t)uy * c->mapW[p] + ux;
-                if (c->owner[p][i] < 0) continue;
+                const av1r_ctx::MapUnit& mu = c->umap[p][i];
+                if (mu.owner < 0) continue;
                 *mw |= 1u << (u - u0);
-                if (!(c->emit[p][i] & (horiz ? 1 : 2))) {
+                if (!(mu.emit & (horiz ? 1 : 2))) {
                     if (c->granOk && getenv("AV1R_GRAN_DEBUG"))
                         fprintf(stderr, "no granule: plane %d unit %d,%d %s (consumer %d,%d %dx%d)\n", p, ux, uy, horiz ? "h" : "v", x, y, w, h);
                     c->granOk = false;
@@ -547,9 +552,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         if (hL) run(y >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2, false, m + 2);
         if (hA && hL) {
             const size_t i = (size_t)((y - 1) >> 2) * c->mapW[p] + ((x - 1) >> 2);
-            if (c->owner[p][i] >= 0) {
-                m[1] = (c->emit[p][i] & 1) ? 1u : 3u;
-                if (!c->emit[p][i]) c->granOk = false;
+            const av1r_ctx::MapUnit& mu = c->umap[p][i];
+            if (mu.owner >= 0) {
+                m[1] = (mu.emit & 1) ? 1u : 3u;
+                if (!mu.emit) c->granOk = false;
             }
         }
     };
@@ -560,11 +566,11 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         }
         int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
         for (int y = y0; y < y1; y++) {
-            int32_t* row = &c->owner[p][(size_t)y * c->mapW[p]];
-            uint8_t* em = &c->emit[p][(size_t)y * c->mapW[p]];
+            av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
+            const uint8_t last = y == y0 + h4 - 1 ? 1 : 0;
             for (int x = x0; x < x1; x++) {
-                row[x] = node;
-                em[x] = (y == y0 + h4 - 1 ? 1 : 0) | (x == x0 + w4 - 1 ? 2 : 0);
+                row[x].owner = node;
+                row[x].emit = last | (x == x0 + w4 - 1 ? 2 : 0);
             }
         }
     };
@@ -587,16 +593,16 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         y1 = std::min(y1, c->mapH[p] - 1);
         int m = -1;
         for (int y = y0; y <= y1; y++) {
-            const int16_t* row = &c->lvlmap[p][(size_t)y * c->mapW[p]];
-            for (int x = x0; x <= x1; x++) m = std::max<int>(m, row[x]);
+            const av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
+            for (int x = x0; x <= x1; x++) m = std::max<int>(m, row[x].lvl);
         }
         return m;
     };
     auto region_set = [&](int p, int x0, int y0, int w4, int h4, int lv) {
         int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
         for (int y = y0; y < y1; y++) {
-            int16_t* row = &c->lvlmap[p][(size_t)y * c->mapW[p]];
-            for (int x = x0; x < x1; x++) row[x] = (int16_t)lv;
+            av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
+            for (int x = x0; x < x1; x++) row[x].lvl = (int16_t)lv;
         }
     };
     // Latest level among the pixels coop_intra_predict reads for a w x h prediction at
