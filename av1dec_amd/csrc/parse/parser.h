@@ -133,41 +133,44 @@ struct WriterHook {
 // ---- arithmetic decoder (AV1 spec 8.2: init_symbol / read_symbol / exit_symbol) with
 // CDFs in libaom's inverted form (32768 - cumulative, then the adaptation counter) ----
 struct SymbolDecoder {
+    // The decoder state in the windowed form (the spec's SymbolValue with the following bits
+    // of the tile already shifted in, complemented: libaom's od_ec_dec, which the reference's
+    // SymbolDecoder also uses): the top 16 bits of `dif` compare against the interval
+    // boundaries; bytes are XORed in 8 at a time when `cnt` runs out, so a symbol costs no
+    // per-bit refill.  Past the end of the tile the data reads as zero bits (spec 8.2.2).
     const uint8_t* p = nullptr;
     const uint8_t* end = nullptr;
-    uint64_t win = 0;   // bit window, MSB aligned
-    int winBits = 0;
-    uint32_t value = 0; // SymbolValue
-    uint32_t range = 0; // SymbolRange
-    int64_t maxBits = 0;
+    uint64_t dif = 0;
+    uint32_t range = 0;  // SymbolRange
+    int cnt = 0;
     bool noUpdate = false;
 
-    uint32_t bits(int nb)  // nb <= 24; zeros past the end
+    void refill()
     {
-        if (nb == 0) return 0;
-        while (winBits < nb) {
-            const uint64_t byte = p < end ? *p++ : 0;
-            win |= byte << (56 - winBits);
-            winBits += 8;
+        int sh = 64 - 9 - (cnt + 15);
+        for (; sh >= 0 && p < end; sh -= 8, p++) {
+            dif ^= (uint64_t)*p << sh;
+            cnt += 8;
         }
-        const uint32_t v = (uint32_t)(win >> (64 - nb));
-        win <<= nb;
-        winBits -= nb;
-        return v;
+        if (p >= end) cnt = 0x4000;  // zeros (ones in dif) from here on: never refill again
     }
     void init(const uint8_t* data, size_t sz, bool disableCdfUpdate)
     {
         p = data;
         end = data + sz;
-        win = 0;
-        winBits = 0;
-        const int numBits = sz * 8 < 15 ? (int)(sz * 8) : 15;
-        const uint32_t buf = bits(numBits);
-        const uint32_t padded = buf << (15 - numBits);
-        value = ((1u << 15) - 1) ^ padded;
-        range = 1u << 15;
-        maxBits = 8 * (int64_t)sz - 15;
+        dif = ((uint64_t)1 << 63) - 1;
+        range = 0x8000;
+        cnt = -15;
+        refill();
         noUpdate = disableCdfUpdate;
+    }
+    void renorm(uint64_t d64)
+    {
+        const int d = __builtin_clz(range) - 16;  // 15 - FloorLog2(range)
+        cnt -= d;
+        dif = ((d64 + 1) << d) - 1;
+        range <<= d;
+        if (cnt < 0) refill();
     }
 #ifdef AV1P_WRITER
     WriterHook* hook = nullptr;
@@ -186,16 +189,16 @@ struct SymbolDecoder {
             return s;
         }
 #endif
+        const uint32_t c = (uint32_t)(dif >> 48);
         uint32_t cur = range, prev;
         int sym = -1;
         do {
             sym++;
             prev = cur;
             cur = ((range >> 8) * (uint32_t)(cdf[sym] >> 6) >> 1) + 4u * (uint32_t)(nsym - sym - 1);
-        } while (value < cur);
+        } while (c < cur);
         range = prev - cur;
-        value -= cur;
-        renorm();
+        renorm(dif - ((uint64_t)cur << 48));
         if (!noUpdate) adapt(cdf, sym, nsym);
 #ifdef AV1P_TRACE  // debug aid: the symbol sequence, for diffing against another decoder
         {
@@ -206,17 +209,6 @@ struct SymbolDecoder {
         }
 #endif
         return sym;
-    }
-    void renorm()
-    {
-        const int b = __builtin_clz(range) - 16;  // 15 - FloorLog2(range)
-        range <<= b;
-        int nb = b;
-        if (nb > maxBits) nb = maxBits > 0 ? (int)maxBits : 0;
-        const uint32_t newData = bits(nb);
-        const uint32_t padded = newData << (b - nb);
-        value = padded ^ (((value + 1) << b) - 1);
-        maxBits -= b;
     }
     static void adapt(uint16_t* cdf, int sym, int nsym)
     {
@@ -233,17 +225,14 @@ struct SymbolDecoder {
 #if !defined(AV1P_WRITER) && !defined(AV1P_TRACE)
         // read() over the CDF {16384, 0}: the first interval boundary, then the same renormalisation
         const uint32_t v0 = ((range >> 8) << 7) + 4;
-        int sym;
-        if (value >= v0) {
-            sym = 0;
+        if ((uint32_t)(dif >> 48) >= v0) {
             range -= v0;
-            value -= v0;
-        } else {
-            sym = 1;
-            range = v0;
+            renorm(dif - ((uint64_t)v0 << 48));
+            return 0;
         }
-        renorm();
-        return sym;
+        range = v0;
+        renorm(dif);
+        return 1;
 #endif
         uint16_t c[3] = {16384, 0, 0};
         const bool nu = noUpdate;
