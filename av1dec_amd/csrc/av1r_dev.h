@@ -8,6 +8,38 @@
 
 #define DEV __device__ __forceinline__
 
+// XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"):
+// workgroups are dealt round-robin over the 8 XCDs, so b and b + 8 share one XCD's L2.
+// Renumbering gives each XCD a contiguous eighth of the grid's logical order instead of
+// every eighth tile: neighbouring tiles (reference windows around the same motion, filter
+// halos) and, in a batched launch, one frame's tiles stay in one L2.  Speed only: it is a
+// bijection on [0, g), so any placement stays correct.
+#ifndef AV1R_XCD_ORDER
+#define AV1R_XCD_ORDER 1
+#endif
+DEV uint32_t xcd_order(uint32_t b, uint32_t g)
+{
+#if AV1R_XCD_ORDER
+    const uint32_t x = b & 7, q = g >> 3, r = g & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+#else
+    (void)g;
+    return b;
+#endif
+}
+// This workgroup's logical (x, y, z) in XCD order (x fastest, as the hardware deals them).
+DEV uint3 xcd_block()
+{
+    const uint32_t gxy = gridDim.x * gridDim.y;
+    uint32_t L = xcd_order(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gxy * gridDim.z);
+    uint3 r;
+    r.z = L / gxy;
+    L -= r.z * gxy;
+    r.y = L / gridDim.x;
+    r.x = L - r.y * gridDim.x;
+    return r;
+}
+
 // One plane of a device frame.  Frames are SB-aligned + 64 px margin, origin at (0,0);
 // w/h are the VISIBLE plane dims (YuvFrame::widths/heights, VideoFrame.cpp:49-51).
 struct DevPlane {

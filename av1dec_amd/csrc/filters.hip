@@ -118,13 +118,14 @@ DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int bl
 // one lane per (plane, 4x4 unit) edge of pass `pass`
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass)
 {
-    const KParams& k = KP(kps, blockIdx.y);  // frame of this launch row
+    const uint3 wg = xcd_block();
+    const KParams& k = KP(kps, wg.y);  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
     if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
     const int planeMask = 1 | (hd.lf_level[2] ? 2 : 0) | (hd.lf_level[3] ? 4 : 0);
     const int nY = k.mi_rows * k.mi_cols;
     const int cCols = (k.mi_cols + 1) / 2, nC = ((k.mi_rows + 1) / 2) * cCols;
-    int id = blockIdx.x * blockDim.x + threadIdx.x;
+    int id = wg.x * blockDim.x + threadIdx.x;
     int plane, row0, col0;
     if (id < nY) {
         plane = 0;
@@ -357,9 +358,10 @@ DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int 
 extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
 {
     __shared__ CdefLds L;
-    const KParams& k = KP(kps, blockIdx.z);
+    const uint3 wg = xcd_block();
+    const KParams& k = KP(kps, wg.z);
     const int t = threadIdx.x;
-    const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;  // mi units
+    const int r0 = wg.y * 16, c0 = wg.x * 16;  // mi units
     if (r0 >= k.mi_rows || c0 >= k.mi_cols) return;
     const av1r_frame_hdr& h = *k.hdr;
     const int idx = k.cdef_idx[(r0 >> 4) * h.cdef_cols + (c0 >> 4)];
@@ -604,16 +606,17 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-    const KParams& k = KP(kps, blockIdx.z / 3);
+    const uint3 wg = xcd_block();
+    const KParams& k = KP(kps, wg.z / 3);
     if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
-    const int plane = blockIdx.z % 3, sub = plane ? 1 : 0;
+    const int plane = wg.z % 3, sub = plane ? 1 : 0;
     const DevPlane C = k.cdef.pl[plane];
     const DevPlane O = k.lrout.pl[plane];
-    const int x0 = blockIdx.x * LR_TW;
+    const int x0 = wg.x * LR_TW;
     if (x0 >= C.w) return;
     const int stripeH = 64 >> sub, off = 8 >> sub;
     const int perStripe = stripeH / LR_TH;
-    const int sNum = blockIdx.y / perStripe, half = blockIdx.y - sNum * perStripe;
+    const int sNum = wg.y / perStripe, half = wg.y - sNum * perStripe;
     LrPix S;
     S.cdefP = C;
     S.preP = k.cur.pl[plane];

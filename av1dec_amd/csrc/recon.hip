@@ -1344,7 +1344,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const
     __shared__ __align__(16) uint8_t smem[kLds];
     const uint32_t* tabS = tab + n + 1;  // small prefix
     const uint32_t nBig = tab[n], nSmall = tabS[n];
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const KParams* kp;
     int s;
     if (b < nBig) {
@@ -1415,11 +1415,12 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint
     const unsigned long long tEntry = trace ? trace_now() : 0;
     const KParams* kp;
     int s;
-    const WorkItem& wi = table_item(kps, tab, n, blockIdx.x, kp, s);
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
+    const WorkItem& wi = table_item(kps, tab, n, b, kp, s);
     const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
 #ifdef AV1R_TRACE
     // traceBase ~0u (k_flow mode): frame-major rows, this frame's base + the item position
-    const size_t row = traceBase == ~0u ? kp->trace_base + (size_t)(&wi - kp->items) : (size_t)traceBase + blockIdx.x;
+    const size_t row = traceBase == ~0u ? kp->trace_base + (size_t)(&wi - kp->items) : (size_t)traceBase + b;
     unsigned long long* tr = trace ? trace + row * AV1R_TRACE_W : nullptr;
 #else
     unsigned long long* tr = nullptr;
@@ -1520,7 +1521,7 @@ template <int NT, int MS>
 DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, SmallLds<MS>* L)
 {
     const int lane = threadIdx.x & 63;
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     const KParams& k = KP(kps, s);
@@ -1856,7 +1857,7 @@ DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
 extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ __align__(16) int16_t res[16][16 * 18];
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
@@ -1869,7 +1870,7 @@ extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, 
 extern "C" __global__ __launch_bounds__(64) void k_resid_l(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ __align__(16) int16_t res[64 * 66];
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));

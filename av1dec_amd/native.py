@@ -112,7 +112,7 @@ def build_parser(force=False, out=None, extra=()):
         if all(os.path.getmtime(d) <= t for d in deps):
             return lib_path
     os.makedirs(BUILD, exist_ok=True)
-    tmp = lib_path + ".tmp"
+    tmp = f"{lib_path}.{os.getpid()}.tmp"  # (concurrent test workers may build at once)
     subprocess.check_call([CXX, "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wno-class-memaccess",
                            "-I" + os.path.join(ROOT, "include"), "-I" + pdir, *extra, "-o", tmp]
                           + [os.path.join(pdir, s) for s in PARSE_SRCS])

@@ -8,7 +8,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc/$c -o run -- \
         python3 bench.py --steps 8 --warmup 2 --frames 12 --no-cpu > gpurun_out/pmc/$c.json 2> gpurun_out/pmc/$c.err || exit $?
 done
-python3 tools/pmc_traffic.py gpurun_out/pmc gpurun_out/traffic.json 8 > /dev/null || exit $?
+python3 tools/pmc_traffic.py gpurun_out/pmc gpurun_out/traffic.json 8 > /dev/null || exit $?  # (AV1R_GIT_HEAD: set by the caller)
 timeout -k 10 600 python3 bench.py --traffic gpurun_out/traffic.json > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
 cat gpurun_out/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \

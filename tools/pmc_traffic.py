@@ -22,6 +22,7 @@ def fold(path, counter):
     if not files:
         raise SystemExit(f"no counter_collection csv under {path}")
     tot = defaultdict(float)
+    per_kernel = defaultdict(float)
     rows = []
     for f in files:
         for r in csv.DictReader(open(f)):
@@ -31,20 +32,22 @@ def fold(path, counter):
             st = STAGES.get(name)
             if st is None:
                 continue
-            tot[st] += float(r["Counter_Value"]) * (1024 if counter.endswith("_SIZE") else 1)
+            v = float(r["Counter_Value"]) * (1024 if counter.endswith("_SIZE") else 1)
+            tot[st] += v
+            per_kernel[name] += v
             if st == "cdef":
                 rows.append(int(r["Grid_Size"]))
     # one k_cdef launch covers every frame of its batch: frames = grid / one frame's grid
     one = min(rows) if rows else 1
     frames = sum(round(g / one) for g in rows)
-    return tot, frames
+    return tot, frames, per_kernel
 
 
 def main():
     base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
-    fetch, nf = fold(os.path.join(base, "FETCH_SIZE"), "FETCH_SIZE")
-    write, nw = fold(os.path.join(base, "WRITE_SIZE"), "WRITE_SIZE")
+    fetch, nf, fk = fold(os.path.join(base, "FETCH_SIZE"), "FETCH_SIZE")
+    write, nw, wk = fold(os.path.join(base, "WRITE_SIZE"), "WRITE_SIZE")
     stages = {}
     for st in dict.fromkeys(STAGES.values()):
         f = fetch.get(st, 0.0) / max(nf, 1)
@@ -53,8 +56,11 @@ def main():
                       "traffic_bytes": round(2 * f + w)}
     res = {"config": "1080p", "streams": int(sys.argv[3]) if len(sys.argv) > 3 else 8,
            "frames_fetch": nf, "frames_write": nw,
+           "git_head": os.environ.get("AV1R_GIT_HEAD"),  # the commit the counters were collected at (no .git on the box)
            "unit": "bytes per frame (per stage, all launches of the frame)",
-           "stages": {k: v["traffic_bytes"] for k, v in stages.items()}, "detail": stages}
+           "stages": {k: v["traffic_bytes"] for k, v in stages.items()}, "detail": stages,
+           "kernels": {k: {"fetch_bytes_x2": round(2 * fk.get(k, 0.0) / max(nf, 1)), "write_bytes": round(wk.get(k, 0.0) / max(nw, 1))}
+                       for k in sorted(set(fk) | set(wk))}}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
