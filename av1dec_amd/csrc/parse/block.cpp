@@ -261,6 +261,8 @@ private:
     uint8_t lvl[36 * 36] = {};  // coefficient levels while parsing them, padded (coeffs())
 
     int S(uint16_t* c, int n) { return sd.read(c, n); }
+    template <int N>
+    int SN(uint16_t* c) { return sd.readN<N>(c); }
     uint32_t L(int n) { return sd.literal(n); }
     MiInfo& mi(int r, int c) { return P.mi_at(r, c); }
     bool inside(int r, int c) const { return P.is_inside(r, c); }
@@ -2153,7 +2155,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         fprintf(tf, "p%d x4 %d y4 %d tx %d ctx %d\n", plane, x4, y4, txSz, azCtx);
     }
 #endif
-    const bool allZero = S(cdf.coef.txb_skip[txSzCtx][azCtx], 2) != 0;
+    const bool allZero = SN<2>(cdf.coef.txb_skip[txSzCtx][azCtx]) != 0;
     if (allZero) {
         if (plane == 0) set_luma_type(DCT_DCT);
     } else {
@@ -2195,7 +2197,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         eob = eobPt < 2 ? eobPt : (1 << (eobPt - 2)) + 1;
         int eobShift = std::max(-1, eobPt - 3);
         if (eobShift >= 0) {
-            if (S(cdf.coef.eob_extra[txSzCtx][ptype][eobPt - 3], 2)) eob += 1 << eobShift;
+            if (SN<2>(cdf.coef.eob_extra[txSzCtx][ptype][eobPt - 3])) eob += 1 << eobShift;
             for (int i = 1; i < std::max(0, eobPt - 2); i++) {
                 eobShift = std::max(0, eobPt - 2) - 1 - i;
                 if (L(1)) eob += 1 << eobShift;
@@ -2221,7 +2223,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 else if (c <= (height << bwl) / 4) ctx = kSigCoefContexts - 2;
                 else ctx = kSigCoefContexts - 1;
                 ctx = ctx - kSigCoefContexts + kSigCoefContextsEob;
-                level = S(cdf.coef.coeff_base_eob[txSzCtx][ptype][ctx], 3) + 1;
+                level = SN<3>(cdf.coef.coeff_base_eob[txSzCtx][ptype][ctx]) + 1;
             } else {
                 int mag = 0;
                 for (int k = 0; k < 5; k++)
@@ -2233,7 +2235,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                     const int idx = cls == TX_CLASS_VERT ? row : col;
                     ctx += kCoeffBasePosCtxOffset[std::min(idx, 2)];
                 }
-                level = S(cdf.coef.coeff_base[txSzCtx][ptype][ctx], 4);
+                level = SN<4>(cdf.coef.coeff_base[txSzCtx][ptype][ctx]);
             }
             if (level > kNumBaseLevels) {
                 for (int idx = 0; idx < kCoeffBaseRange / (kBrCdfSize - 1); idx++) {
@@ -2245,7 +2247,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                     else if (cls == TX_CLASS_2D) ctx = (row < 2 && col < 2) ? mag + 7 : mag + 14;
                     else if (cls == TX_CLASS_HORIZ) ctx = col == 0 ? mag + 7 : mag + 14;
                     else ctx = row == 0 ? mag + 7 : mag + 14;
-                    const int br = S(cdf.coef.coeff_br[std::min(txSzCtx, 3)][ptype][ctx], 4);
+                    const int br = SN<4>(cdf.coef.coeff_br[std::min(txSzCtx, 3)][ptype][ctx]);
                     level += br;
                     if (br < kBrCdfSize - 1) break;
                 }
@@ -2283,7 +2285,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                             dcSign += s == 1 ? -1 : s == 2 ? 1 : 0;
                         }
                     const int ctx = dcSign < 0 ? 1 : dcSign > 0 ? 2 : 0;
-                    sign = S(cdf.coef.dc_sign[ptype][ctx], 2) != 0;
+                    sign = SN<2>(cdf.coef.dc_sign[ptype][ctx]) != 0;
                 } else {
                     sign = L(1) != 0;
                 }
