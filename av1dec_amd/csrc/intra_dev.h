@@ -186,6 +186,7 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
 // a spin gives up after ~1 s (or once another wave has) and sets the launch's error word.
 struct GranEdges {
     const uint32_t* mask;  // 4 words: above, corner, left, (unused)
+    uint32_t mA, mC, mL;   // mask[0..2], loaded by the caller (k_flow: before its dependency wait)
     const uint64_t* h;     // this plane's gran_h / gran_v, gw units per row / gh per column
     const uint64_t* v;
     int gw, gh;
@@ -219,9 +220,9 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
             const bool act = q < nq;
             const int kind = q < na ? 0 : q < na + nl ? 1 : 2;  // above, left, corner
             const int u = kind == 0 ? q : q - na;
-            const uint32_t cm = G.mask[1];
-            const bool inl = act && (kind == 0 ? ((G.mask[0] >> (u & 31)) & 1)
-                                   : kind == 1 ? ((G.mask[2] >> (u & 31)) & 1) : (cm & 1));
+            const uint32_t cm = G.mC;
+            const bool inl = act && (kind == 0 ? ((G.mA >> (u & 31)) & 1)
+                                   : kind == 1 ? ((G.mL >> (u & 31)) & 1) : (cm & 1));
             const uint64_t* g = kind == 0 ? G.h + (size_t)((y - 1) >> 2) * G.gw + (x >> 2) + u
                               : kind == 1 ? G.v + (size_t)((x - 1) >> 2) * G.gh + (y >> 2) + u
                               : (cm & 2) ? G.v + (size_t)((x - 1) >> 2) * G.gh + ((y - 1) >> 2)

@@ -183,7 +183,7 @@ DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int1
 // nothing here (their prediction is already in the frame).  Ends with a coop_sync.
 template <int NT, int MAX, bool COH>
 DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, const GranEdges* G = nullptr,
-    bool gran = false)
+    bool gran = false, int edgeFilter = -1)
 {
     constexpr int CM = TbLds<MAX>::CM;
     const int t = coop_lane<NT>();
@@ -229,7 +229,7 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
         P.filterIntraMode = blk.filter_intra_mode;
         P.smooth = plane ? ((bflags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
                          : ((bflags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
-        P.edgeFilter = k.hdr->enable_intra_edge_filter;
+        P.edgeFilter = edgeFilter >= 0 ? edgeFilter : k.hdr->enable_intra_edge_filter;
         int s = 0;
         if (isCfl) {
             // predict_chroma_from_luma (IntraPredict.cpp:632-667): the luma loads go out
@@ -1239,6 +1239,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
         if (COH && gran) {  // k_flow with edge granules: G holds plane 0's, 4 mask words per plane
             GranEdges Gp = *G;
             Gp.mask = G->mask + 4 * plane;
+            Gp.mA = Gp.mask[0], Gp.mC = Gp.mask[1], Gp.mL = Gp.mask[2];
             Gp.h = k.gran_h[plane];
             Gp.v = k.gran_v[plane];
             Gp.gw = k.gran_w[plane];
@@ -1542,12 +1543,20 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
         }
     }
 }
-extern "C" __global__ __launch_bounds__(64) void k_inter_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+#ifndef AV1R_PLAIN_WAVES
+#define AV1R_PLAIN_WAVES 0  // minimum waves/SIMD for k_inter_s / k_inter_m (0: the compiler's choice, 153 VGPRs = 3)
+#endif
+#if AV1R_PLAIN_WAVES
+#define K_PLAIN_BOUNDS __launch_bounds__(64, AV1R_PLAIN_WAVES)
+#else
+#define K_PLAIN_BOUNDS __launch_bounds__(64)
+#endif
+extern "C" __global__ K_PLAIN_BOUNDS void k_inter_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ SmallLds<8> L[4];
     inter_plain<16, 8>(kps, tab, n, L);
 }
-extern "C" __global__ __launch_bounds__(64) void k_inter_m(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+extern "C" __global__ K_PLAIN_BOUNDS void k_inter_m(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ SmallLds<16> L[2];
     inter_plain<32, 16>(kps, tab, n, L);
@@ -1635,7 +1644,18 @@ template <int NT, int MAX>
 DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl,
     unsigned long long* trace, uint32_t s)
 {
+    // What the item reads from the batch after its wait -- its edge mask words, its block's
+    // prediction fields, the edge-filter flag (and with AV1R_FLOW_ITEM_COPY its own record)
+    // -- is loaded into registers BEFORE the wait: after it (the wait's memory clobber
+    // forces a reload) each was one more dependent round trip on every hop of the chain.
+#ifndef AV1R_FLOW_ITEM_COPY
+#define AV1R_FLOW_ITEM_COPY 1  // k_flow -9 %, device-only +5 % (A/B on one box; costs 16 B/lane of scratch)
+#endif
+#if AV1R_FLOW_ITEM_COPY
+    const WorkItem wi = k.items[pos];  // (16 B/lane of scratch: the record stays live across the wait)
+#else
     const WorkItem& wi = k.items[pos];
+#endif
 #ifdef AV1R_TRACE
     unsigned long long* tr = trace ? trace + (size_t)(k.trace_base + pos) * AV1R_TRACE_W : nullptr;
     trace_stamp(tr, 2);
@@ -1655,6 +1675,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     if (gran) {
         const int p = AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 0 : wi.plane;
         G.mask = k.deps + wi.dep_off - (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 12 : 4);
+        G.mA = G.mask[0], G.mC = G.mask[1], G.mL = G.mask[2];
         G.h = k.gran_h[p];
         G.v = k.gran_v[p];
         G.gw = k.gran_w[p];
@@ -1674,11 +1695,12 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         // intra / palette TB: its residual tile (k_resid) is fetched before the wait
         ResQuads<NT, MAX> R;
         res_prefetch<NT, MAX>(k, wi, R);
-        const av1r_block& blk = k.blocks[wi.block];
+        const av1r_block blk = k.blocks[wi.block];  // (a copy: only the fields predict reads are loaded)
+        const int edgeFilter = k.hdr->enable_intra_edge_filter;
         trace_stamp(tr, 3);
         flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
         trace_stamp(tr, 4);
-        tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran);
+        tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran, edgeFilter);
         trace_stamp(tr, 9);
         tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
         trace_stamp(tr, 10);
