@@ -40,6 +40,21 @@ DEV uint3 xcd_block()
     return r;
 }
 
+// The same within each z slice only (z = blockIdx.z): every XCD takes a contiguous eighth of
+// every slice.  For grids whose slices carry unequal work (k_lr: z = frame x plane, chroma
+// slices half empty) a contiguous eighth of the whole grid would leave the XCDs holding
+// luma slices with most of the work.
+DEV uint3 xcd_block_xy()
+{
+    const uint32_t gxy = gridDim.x * gridDim.y;
+    const uint32_t L = xcd_order(blockIdx.x + gridDim.x * blockIdx.y, gxy);
+    uint3 r;
+    r.z = blockIdx.z;
+    r.y = L / gridDim.x;
+    r.x = L - r.y * gridDim.x;
+    return r;
+}
+
 // One plane of a device frame.  Frames are SB-aligned + 64 px margin, origin at (0,0);
 // w/h are the VISIBLE plane dims (YuvFrame::widths/heights, VideoFrame.cpp:49-51).
 struct DevPlane {

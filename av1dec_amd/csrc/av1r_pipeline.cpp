@@ -231,9 +231,12 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
     Run R(n);
     R.src = src;
     R.maxFrames = max_frames;
-    R.depth = depth > 0 ? depth : 3;
     R.stable = src->stable != 0;
     const int W = std::max(1, std::min(workers > 0 ? workers : n, 64));
+    // default look-ahead: enough packed frames per stream to keep every worker busy twice
+    // over, at least 8 (measured on the box: 4K x 2 streams 410-445 frames/s at depth 3,
+    // 530-600 at 5, 680-685 at 8; 1080p x 8 streams 3 370-3 450 / 3 470 / 3 610-3 670)
+    R.depth = depth > 0 ? depth : std::max(8, 2 * ((W + n - 1) / n));
     const auto t0 = Clock::now();
     std::vector<std::thread> th;
     th.reserve(W);

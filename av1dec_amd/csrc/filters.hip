@@ -606,7 +606,14 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-    const uint3 wg = xcd_block();
+#ifndef AV1R_LR_XCD
+#define AV1R_LR_XCD 1
+#endif
+#if AV1R_LR_XCD
+    const uint3 wg = xcd_block_xy();  // (per slice: chroma slices are half empty)
+#else
+    const uint3 wg = make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
+#endif
     const KParams& k = KP(kps, wg.z / 3);
     if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
     const int plane = wg.z % 3, sub = plane ? 1 : 0;

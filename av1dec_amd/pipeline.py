@@ -130,7 +130,7 @@ class IvfPipeline:
         return time.perf_counter() - t0
 
 
-def run_native(decoders, source="cycle", streams=None, positions=None, max_frames=0, depth=3, workers=0):
+def run_native(decoders, source="cycle", streams=None, positions=None, max_frames=0, depth=0, workers=0):
     """The same pipeline in native threads (av1r_pipeline_run, include/av1r.h): no
     interpreter on the path (`workers` packing threads, 0: one per stream).  source "cycle": streams = per-stream lists of batchfile.Frame;
     stream j continues at frame positions[j] (mod its length), and positions is advanced in

@@ -335,10 +335,13 @@ def main():
     # GPU).  Setup (untimed): stream j brought to its own GOP phase, a priming pass of ~1 s,
     # then the warmup steps.
     # (the native pipeline, av1r_pipeline_run: one producer thread per stream packs its frames
-    # up to 3 ahead, the calling thread launches one frame of every ready stream per batch)
+    # ahead, the calling thread launches one frame of every ready stream per batch)
     from av1dec_amd.pipeline import run_native
     workers = host_workers()
-    depth = int(os.environ.get("AV1R_BENCH_DEPTH", "3"))  # frames packed ahead per stream
+    # frames packed ahead per stream (AV1R_BENCH_DEPTH; 0: the pipeline's default,
+    # max(8, 2 * ceil(workers / streams)) -- 8 at 1080p x 8 streams, 16 at 4K x 2)
+    depth = int(os.environ.get("AV1R_BENCH_DEPTH", "0"))
+    depth_eff = depth if depth > 0 else max(8, 2 * -(-max(1, workers) // len(streams)))
     pp = StreamScheduler(decs, F, streams=streams, workers=1)
     pp.stagger()
     pp.close()
@@ -516,7 +519,7 @@ def main():
                                    f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
                                    f"host-inclusive: each frame validated, scheduled, packed and uploaded from "
                                    f"host memory inside the timed region (native pipeline: {workers} packing "
-                                   f"threads, {depth} frames ahead per stream; key frames run alone on their stream, overlapping "
+                                   f"threads, {depth_eff} frames ahead per stream; key frames run alone on their stream, overlapping "
                                    f"the other streams' batches); timed frames: {args.steps * S} of which {n_key} key",
                        "host_threads": workers + 1,
                        "timed_key_frames": n_key,

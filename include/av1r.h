@@ -317,7 +317,8 @@ size_t av1r_sizeof(int which);
 /* ---- multi-stream pipeline (av1r_pipeline.cpp; SURVEY.md 8e + 8f rank 4) ----
  * n independent streams (contexts on one device) decoded end to end in native threads:
  * `workers` threads pull each stream's frames in decode order from `src` and pack them
- * (av1r_pack) up to `depth` ahead per stream; the calling thread launches one frame of every ready
+ * (av1r_pack) up to `depth` ahead per stream (<= 0: max(8, 2 * ceil(workers / n))); the calling
+ * thread launches one frame of every ready
  * stream per shared launch (av1r_decode_packed_batch), applies show-existing frames in
  * order (av1r_show_existing), and finally synchronizes every context.  Stops after
  * max_frames frames per stream (<= 0: at each source's end).  The reference's per-stream

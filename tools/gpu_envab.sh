@@ -6,7 +6,7 @@ for i in 1 2; do
     v=0
     for e in "$@"; do
         env $e timeout -k 10 300 python3 bench.py --no-cpu > gpurun_out/envab/v$v.$i.json 2> gpurun_out/envab/v$v.$i.err || exit $?
-        python3 -c "import json,sys; d=json.load(open('gpurun_out/envab/v$v.$i.json')); print('$e', d['value'], d['stage_ms_per_frame'], d['single_stream_fps'])"
+        python3 -c "import json,sys; d=json.load(open('gpurun_out/envab/v$v.$i.json')); print('$e', d['value'], d.get('device_only_fps'), d['stage_ms_per_frame'], d['single_stream_fps'])"
         v=$((v + 1))
     done
 done
