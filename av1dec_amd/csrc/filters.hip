@@ -606,8 +606,8 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-#ifndef AV1R_LR_XCD
-#define AV1R_LR_XCD 1
+#ifndef AV1R_LR_XCD  // XCD order for k_lr: 4K LR 0.080 -> 0.108 ms/frame (1080p unchanged), though
+#define AV1R_LR_XCD 0   // its fabric traffic fell 16.7 -> 6.7 MB/frame: measured, so off
 #endif
 #if AV1R_LR_XCD
     const uint3 wg = xcd_block_xy();  // (per slice: chroma slices are half empty)
