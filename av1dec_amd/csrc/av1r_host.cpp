@@ -1455,8 +1455,10 @@ static int launch_solo(FrameJob& j)
     av1r_ctx* m = j.c;
     av1r_ctx* c = m;
     std::vector<FrameJob> one(1, j);
+    // AV1R_SOLO_PER_CU: k_flow workgroups per CU of a solo deep frame (A/B)
+    static const int soloPer = getenv("AV1R_SOLO_PER_CU") ? std::max(1, atoi(getenv("AV1R_SOLO_PER_CU"))) : 1;
     const int per = m->flowPerCU;
-    m->flowPerCU = 1;
+    m->flowPerCU = soloPer;
     int rc = launch_jobs(m, one);
     m->flowPerCU = per;
     if (rc) return rc;
