@@ -1203,10 +1203,11 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
 // the block's intra prediction (its edges are final when this item runs) blended with the
 // inter prediction inter_tile stored in the frame.
 template <int NT, bool COH>
-DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G = nullptr, bool gran = false)
+DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G = nullptr, bool gran = false,
+    const av1r_block* pre = nullptr)
 {
     const int t = coop_lane<NT>();
-    const av1r_block& blk = k.blocks[bi];
+    const av1r_block& blk = pre ? *pre : k.blocks[bi];  // (k_flow: loaded before the wait)
     const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
     const int bs = blk.mi_size;
     const int im = blk.interintra_mode;
@@ -1686,10 +1687,11 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
         if constexpr (MAX == 64) {  // blends are always large items
+            const av1r_block blk = k.blocks[AV1R_ITEM_INDEX(wi.code)];
             trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
             trace_stamp(tr, 4);
-            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L, &G, gran);
+            ii_item<NT, true>(k, AV1R_ITEM_INDEX(wi.code), L, &G, gran, &blk);
         }
     } else {
         // intra / palette TB: its residual tile (k_resid) is fetched before the wait
