@@ -118,6 +118,9 @@ struct KParams {
     uint64_t* gran_v[3];
     int gran_w[3], gran_hn[3];
     int gran;
+    // k_strip (build_strips): this frame's items run one strip per workgroup, same-strip
+    // pixels read from the strip's LDS ring, the frame stored plainly
+    int strip;
     uint32_t n_items;
     uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;
@@ -152,6 +155,12 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_SPINLIM (FLOW_ERR + 4)  // polls before a wait gives up (0: FLOW_SPINS)
 #define FLOW_ASSIGN (FLOW_ERR + FLOW_LINE)  // workgroup entries: entry k serves queue k % FLOW_QUEUES
 #define FLOW_CTL_BYTES 1280
+// k_strip: luma rows per strip (one workgroup each; chroma strips are the same rows at 4:2:0).
+// 64 = the largest transform side, so no transform block spans two strips
+#define AV1R_STRIP_H 64
+// k_strip: columns of a strip kept in its LDS ring (luma; chroma half): 64 x 512 + 2 x 32 x 256
+// = 48 KB.  The host checks that no ring cell is overwritten before its last read
+#define AV1R_RING_W 512
 // k_flow spin bound, in polls of running waves (each a global load round trip, ~0.5-2 us),
 // not in wall-clock time: a wave that the hardware preempts (context save / restore) does
 // not count the time it was off the chip, so only a wait that makes no progress WHILE
@@ -242,6 +251,29 @@ DEV void stp4(const DevPlane& p, int x, int y, uint32_t v)
     if constexpr (COH) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *a = v;
 }
+
+// runtime choice between the two forms (a uniform branch): coh = sc1, else plain
+DEV uint8_t ldp_c(const DevPlane& p, int x, int y, bool coh) { return coh ? ldp<true>(p, x, y) : ldp<false>(p, x, y); }
+DEV uint32_t ldp4_c(const DevPlane& p, int x, int y, bool coh) { return coh ? ldp4<true>(p, x, y) : ldp4<false>(p, x, y); }
+DEV void stp4_c(const DevPlane& p, int x, int y, uint32_t v, bool coh)
+{
+    if (coh) stp4<true>(p, x, y, v);
+    else stp4<false>(p, x, y, v);
+}
+DEV void stp_c(const DevPlane& p, int x, int y, uint8_t v, bool coh)
+{
+    if (coh) stp<true>(p, x, y, v);
+    else stp<false>(p, x, y, v);
+}
+// THE INVARIANT of the dataflow kernels.  k_flow: every read of a pixel that another item
+// of the same launch may have written goes through the sc1 accessors (ldp<true> /
+// ldp4<true>) or a granule, and every such pixel is stored sc1 -- a plain load could return
+// a stale line from this CU's L1 (cdna_hip_programming.md §6 Guideline 16).  k_strip
+// (KParams::strip): such a pixel is either another strip's, read as a granule, or this
+// strip's, read from the workgroup's LDS ring behind the barrier that ended its writer's
+// group; the frame itself is then only written in the launch (plain stores), never read
+// for an in-launch pixel.  -DAV1R_FLOW_DEBUG checks both at run time (flow_check_read).
+DEV bool strip_plain(int kstrip, bool gran) { return kstrip && gran; }  // (k_strip runs only with granules)
 
 // Work-item encoding of the per-level item lists (host schedule -> k_level):
 // bits 31..30 kind, 29..0 index (TB index; block index for inter-intra blends;

@@ -44,6 +44,8 @@ int flow_grid(int device, int maxPer);
 void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
 void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s);
+void launch_k_strip(const KParams* kps, const void* groups, const uint32_t* stripStart, uint32_t nStrips, uint32_t* ctl,
+    uint32_t epoch, unsigned long long* trace, hipStream_t s);
 
 namespace {
 
@@ -96,6 +98,9 @@ struct Prepared {
     uint64_t bytes = 0;    // the packed layout (incl. the device-filled mode-info grid)
     size_t upBytes = 0;    // its uploaded prefix
     bool offsets = false;  // packed in host memory: base pointers are offsets into the upload
+    // k_strip schedule (deep frames; empty: k_flow): {n, first item} pairs per group and the
+    // strips' group ranges (av1r_ctx::stripGroups / stripStart)
+    std::vector<uint32_t> stripGroups, stripStart;
 };
 
 // A frame validated, scheduled and packed into (pinned) host memory by av1r_pack, on any
@@ -172,6 +177,12 @@ struct av1r_ctx {
     // item of the launch); granOk = every such unit a consumer reads has its granule
     std::vector<uint32_t> nodeMask;
     bool granOk = false;
+    // k_strip (deep frames, build_strips): one workgroup per 64-row strip runs the strip's
+    // groups in level order; stripGroups = {n, first item} pairs, strip s's groups at
+    // [stripStart[s], stripStart[s + 1]); itemStrip per item position
+    bool stripMode = false;
+    std::vector<uint32_t> stripGroups, stripStart;
+    std::vector<uint16_t> itemStrip;
     uint64_t* granDev = nullptr;
     size_t granCap = 0;  // bytes
     // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
@@ -477,6 +488,181 @@ struct PackClock {
 };
 
 // ------------------------------------------------------------------------------------
+// k_strip schedule of a deep frame (recon.hip, k_strip)
+// ------------------------------------------------------------------------------------
+// A key frame's intra TBs form a wavefront ~2 000 levels deep at 1080p.  On k_flow every
+// hop of that chain is a hand-off between workgroups on arbitrary CUs (a granule or flag
+// round trip through the device coherence point, ~3.4 us per level measured).  k_strip
+// instead gives each 64-row strip of the frame (AV1R_STRIP_H luma rows, the same rows of
+// chroma at 4:2:0) to ONE workgroup, which runs the strip's groups (one large item or up to
+// four small ones, as k_flow's) in level order, separated by its barrier, and keeps the
+// strip's reconstructed pixels in an LDS ring of AV1R_RING_W columns: an edge or CFL read
+// inside the strip is an LDS read of a pixel an earlier group wrote.  Only what crosses a
+// strip boundary -- the row above the strip's first row, below-left columns reaching into
+// the next strip -- keeps k_flow's granule hand-off.  Built after the k_flow schedule; the
+// frame keeps k_flow unless every condition holds:
+//   - granules (c->granOk) and nothing but intra / palette TBs (an intra frame: no inter
+//     tile, blend or inter TB, whose pixels the ring would not hold);
+//   - no dependency-list entry across strips (an intra frame's lists hold only CFL's luma,
+//     the same block's, hence the same strip's);
+//   - the ring never loses a pixel still to be read: simulated group by group, every ring
+//     cell read holds the column the reader wants (AV1R_RING_W columns of the strip are
+//     live at once; a strip's level order keeps its rows within a few hundred columns).
+// Then every item's edge mask words lose their same-strip units (read from the ring), the
+// owners of the units still masked -- read by the next or previous strip -- get pub bit 1
+// (they publish granules; the others skip it), and the frame's groups are listed per strip.
+// (default 0 = off until k_strip beats k_flow: 12.8 vs 6.9 ms per 1080p key frame, r03)
+static std::atomic<int> g_stripLevels{getenv("AV1R_STRIP_LEVELS") ? atoi(getenv("AV1R_STRIP_LEVELS")) : 0};
+
+static void build_strips(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    c->stripMode = false;
+    const size_t ni = c->items.size();
+    const av1r_frame_hdr* h = b->hdr;
+    static const bool dbg = getenv("AV1R_STRIP_DEBUG") != nullptr;
+    auto bail = [&](const char* why) {
+        if (dbg) fprintf(stderr, "av1r strips: off (%s)\n", why);
+    };
+    if (!c->granOk) return bail("no granules");
+    for (const WorkItem& w : c->items)
+        if (AV1R_ITEM_KIND(w.code) != AV1R_ITEM_TB || w.pred == AV1R_PRED_INTER) return bail("not an intra frame");
+    const uint32_t nStrips = (uint32_t)(h->mi_rows * 4 + AV1R_STRIP_H - 1) / AV1R_STRIP_H;
+    std::vector<uint16_t>& st = c->itemStrip;
+    st.assign(ni, 0);
+    for (size_t i = 0; i < ni; i++) {
+        const WorkItem& w = c->items[i];
+        st[i] = (uint16_t)std::min<uint32_t>(((uint32_t)w.y << (w.plane ? 1 : 0)) / AV1R_STRIP_H, nStrips - 1);
+    }
+    // groups, strip by strip, each strip's in level order: a large item alone, small items of
+    // one level and strip by four (adjacent: build_schedule sorted them by strip)
+    std::vector<uint32_t> cnt(nStrips + 1, 0);
+    auto walk = [&](auto&& emit) {
+        for (const Level& L : c->levels) {
+            for (uint32_t q = 0; q < L.fcnt[1]; q++) emit(st[L.off[1] + q], 0u, L.off[1] + q);
+            for (uint32_t q = 0; q < L.fcnt[2];) {
+                const uint32_t pos = L.off[2] + q, s = st[pos];
+                uint32_t n = 1;
+                while (n < 4 && q + n < L.fcnt[2] && st[pos + n] == s) n++;
+                emit(s, n, pos);
+                q += n;
+            }
+        }
+    };
+    walk([&](uint32_t s, uint32_t, uint32_t) { cnt[s + 1]++; });
+    for (uint32_t s = 0; s < nStrips; s++) cnt[s + 1] += cnt[s];
+    std::vector<uint32_t> start = cnt, groups(2 * (size_t)cnt[nStrips], 0);
+    walk([&](uint32_t s, uint32_t n, uint32_t pos) {
+        const uint32_t g = cnt[s]++;
+        groups[2 * g] = n;
+        groups[2 * g + 1] = pos;
+    });
+    // the ring simulation: per strip and plane, cell (unit row in the strip, unit column mod
+    // the ring) = the unit column it holds (-1: none yet)
+    const int ringU[3] = {AV1R_RING_W / 4, AV1R_RING_W / 8, AV1R_RING_W / 8};
+    const int rowsU[3] = {AV1R_STRIP_H / 4, AV1R_STRIP_H / 8, AV1R_STRIP_H / 8};
+    std::vector<int32_t> cell[3];
+    bool ringOk = true;
+    for (uint32_t s = 0; s < nStrips && ringOk; s++) {
+        for (int p = 0; p < 3; p++) cell[p].assign((size_t)ringU[p] * rowsU[p], -1);
+        auto inStrip = [&](int p, int uy) { return uy >= (int)s * rowsU[p] && uy < ((int)s + 1) * rowsU[p]; };
+        auto rd = [&](int p, int ux, int uy) {
+            if (!inStrip(p, uy)) return;
+            if (cell[p][(size_t)(uy - s * rowsU[p]) * ringU[p] + (ux & (ringU[p] - 1))] != ux) ringOk = false;
+        };
+        for (uint32_t g = start[s]; g < start[s + 1] && ringOk; g++) {
+            const uint32_t n = std::max<uint32_t>(groups[2 * g], 1), pos0 = groups[2 * g + 1];
+            for (uint32_t q = 0; q < n; q++) {  // every read of the group, then its writes
+                const WorkItem& w = c->items[pos0 + q];
+                if (w.pred != AV1R_PRED_INTRA) continue;
+                const int p = w.plane, sub = p ? 1 : 0, x = w.x, y = w.y;
+                const int tw = av1r_tx_w[w.tx_size], th = av1r_tx_h[w.tx_size];
+                const bool hL = w.flags & AV1R_TB_HAVE_LEFT, hA = w.flags & AV1R_TB_HAVE_ABOVE;
+                const bool hAR = w.flags & AV1R_TB_HAVE_AR, hBL = w.flags & AV1R_TB_HAVE_BL;
+                const int maxX = ((h->mi_cols * 4) >> sub) - 1, maxY = ((h->mi_rows * 4) >> sub) - 1;
+                if (hA)
+                    for (int ux = x >> 2; ux <= std::min(maxX, x + (hAR ? 2 * tw : tw) - 1) >> 2; ux++) rd(p, ux, (y - 1) >> 2);
+                if (hL)
+                    for (int uy = y >> 2; uy <= std::min(maxY, y + (hBL ? 2 * th : th) - 1) >> 2; uy++) rd(p, (x - 1) >> 2, uy);
+                if (hA && hL) rd(p, (x - 1) >> 2, (y - 1) >> 2);
+                const av1r_block& blk = b->blocks[w.block];
+                if (p && blk.uv_mode == AV1R_UV_CFL_PRED) {  // tb_predict's co-located luma
+                    const int lx1 = std::min(2 * (x + tw) - 1, blk.max_luma_w - 1), ly1 = std::min(2 * (y + th) - 1, blk.max_luma_h - 1);
+                    for (int uy = (2 * y) >> 2; uy <= ly1 >> 2; uy++)
+                        for (int ux = (2 * x) >> 2; ux <= lx1 >> 2; ux++) rd(0, ux, uy);
+                }
+            }
+            for (uint32_t q = 0; q < n; q++) {
+                const WorkItem& w = c->items[pos0 + q];
+                const int p = w.plane;
+                const int tw = av1r_tx_w[w.tx_size], th = av1r_tx_h[w.tx_size];
+                for (int uy = w.y >> 2; uy < (w.y + th) >> 2; uy++)
+                    for (int ux = w.x >> 2; ux < (w.x + tw) >> 2; ux++)
+                        if (inStrip(p, uy)) cell[p][(size_t)(uy - s * rowsU[p]) * ringU[p] + (ux & (ringU[p] - 1))] = ux;
+            }
+        }
+    }
+    if (!ringOk) return bail("ring overrun");
+    // the masks and lists without their same-strip entries (into scratch; committed below)
+    auto ownerStrip = [&](int p, int ux, int uy, int32_t* pos) -> int {  // -1: not written in the launch
+        const int32_t node = c->umap[p][(size_t)uy * c->mapW[p] + ux].owner;
+        *pos = node < 0 ? -1 : c->nodePos[node];
+        return *pos < 0 ? -1 : st[*pos];
+    };
+    std::vector<uint32_t> nd;
+    nd.reserve(c->deps.size());
+    std::vector<uint32_t> off(ni), dcnt(ni);
+    std::vector<uint8_t> pub(ni, 0);
+    for (size_t i = 0; i < ni; i++) {
+        const WorkItem& w = c->items[i];
+        const int s = st[i];
+        uint32_t m[4];
+        for (int q = 0; q < 4; q++) m[q] = c->deps[w.dep_off - 4 + q];
+        const int p = w.plane, x = w.x, y = w.y;
+        int32_t o;
+        for (int u = 0; u < 32; u++) {
+            if ((m[0] >> u) & 1) {
+                if (ownerStrip(p, (x >> 2) + u, (y - 1) >> 2, &o) == s) m[0] &= ~(1u << u);
+                else if (o >= 0) pub[o] |= 2;
+            }
+            if ((m[2] >> u) & 1) {
+                if (ownerStrip(p, (x - 1) >> 2, (y >> 2) + u, &o) == s) m[2] &= ~(1u << u);
+                else if (o >= 0) pub[o] |= 2;
+            }
+        }
+        if (m[1] & 1) {
+            if (ownerStrip(p, (x - 1) >> 2, (y - 1) >> 2, &o) == s) m[1] = 0;
+            else if (o >= 0) pub[o] |= 2;
+        }
+        nd.insert(nd.end(), m, m + 4);
+        off[i] = (uint32_t)nd.size();
+        for (uint32_t d = w.dep_off; d < w.dep_off + w.dep_cnt; d++) {
+            const uint32_t pos = c->deps[d];
+            if (st[pos] != s) return bail("a dependency list crosses strips");
+        }
+        dcnt[i] = 0;
+    }
+    for (size_t i = 0; i < ni; i++) {
+        c->items[i].dep_off = off[i];
+        c->items[i].dep_cnt = (uint16_t)dcnt[i];
+        c->items[i].pub = pub[i];
+    }
+    c->deps.swap(nd);
+    c->stripStart.swap(start);
+    c->stripGroups.swap(groups);
+    c->stripMode = true;
+    if (dbg) {
+        uint32_t mx = 0, crossG = 0, pubs = 0;
+        for (uint32_t s = 0; s < nStrips; s++) mx = std::max(mx, c->stripStart[s + 1] - c->stripStart[s]);
+        for (size_t i = 0; i < ni; i++) {
+            for (int q = 0; q < 4; q++) crossG += __builtin_popcount(c->deps[c->items[i].dep_off - 4 + q]);
+            pubs += c->items[i].pub != 0;
+        }
+        fprintf(stderr, "av1r strips: %u strips, %u groups (max %u per strip), %zu levels, %u cross-strip granule units, %u publishing items\n",
+            nStrips, c->stripStart[nStrips], mx, c->levels.size(), crossG, pubs);
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // dependency levels
 // ------------------------------------------------------------------------------------
 // flowOnly: the frame will run on k_flow (av1r_pack; no intra block copy), so inter TBs
@@ -711,6 +897,14 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         return;
     }
     const size_t nl = (size_t)(globalMax + 1);
+    // a deep frame (a key frame's intra wavefront) runs on k_strip: its items are ordered
+    // by strip within each level so that a strip's small items of one level are adjacent
+    const int stripLv = g_stripLevels.load(std::memory_order_relaxed);
+    c->stripMode = stripLv > 0 && (int)nl > stripLv;
+    auto stripOf = [&](const WorkItem& w) -> uint32_t {
+        if (AV1R_ITEM_KIND(w.code) == AV1R_ITEM_II) return (uint32_t)(b->blocks[w.block].mi_row * 4) / AV1R_STRIP_H;
+        return ((uint32_t)w.y << (w.plane ? 1 : 0)) / AV1R_STRIP_H;
+    };
     clk.lap(PP_SCHED_BLOCKS);
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
         if (v->size() < nl) v->resize(nl);
@@ -803,6 +997,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 c->items.push_back(w);
             }
         }
+        if (c->stripMode) {
+            auto byStrip = [&](const WorkItem& a, const WorkItem& q) { return stripOf(a) < stripOf(q); };
+            const Level& L = c->levels[l];
+            std::stable_sort(c->items.begin() + L.off[1], c->items.begin() + L.off[1] + L.fcnt[1], byStrip);
+            std::stable_sort(c->items.begin() + L.off[2], c->items.begin() + L.off[2] + L.fcnt[2], byStrip);
+        }
     }
     c->nLevelsLast = (int)nl;
     clk.lap(PP_SCHED_ITEMS);
@@ -865,6 +1065,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->deps.push_back((uint32_t)pos);
             c->items[pos].pub = 1;
         }
+    }
+    if (c->stripMode && c->flowOk) build_strips(c, b);  // (clears stripMode where k_flow stays)
+    else c->stripMode = false;
+    if (!c->stripMode) {
+        c->stripGroups.clear();
+        c->stripStart.clear();
     }
     clk.lap(PP_SCHED_DEPS);
     if (flowOnly && !c->flowOk) build_schedule(c, b, allowGran, false);  // k_flow cannot take it: levels too
@@ -936,6 +1142,8 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.frame_h = h->frame_height;
     P.hdr = *h;
     P.levels = c->levels;
+    P.stripGroups = c->stripGroups;
+    P.stripStart = c->stripStart;
     P.bytes = off;
     memcpy(P.usedRef, c->usedRef, sizeof(P.usedRef));
     P.levelsOk = c->levelsOk;
@@ -1149,12 +1357,22 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     if (mustFlow && !allFlow) return fail(c, AV1R_E_INVALID, "a flow-only frame batched with a level-schedule frame");
     flow = (flow || mustFlow) && allFlow;
-    size_t nGroups = 0;
+    // k_flow groups of the frames without a strip schedule; k_strip strips and groups of the
+    // others (deep frames, build_strips)
+    size_t nGroups = 0, nStripG = 0, nStripS = 0;
     for (auto& j : jobs) {
+        if (flow && !j.P->stripGroups.empty()) {
+            nStripG += j.P->stripGroups.size() / 2;
+            nStripS += j.P->stripStart.size() - 1;
+            continue;
+        }
         for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
     }
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
-    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups + resTabBytes : 0);
+    const size_t stripTabBytes = nStripS ? align256(4 * (2 * nStripS + 2)) : 0;
+    const size_t stripBytes = nStripS ? stripTabBytes + 8 * nStripG : 0;
+    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups + resTabBytes + stripBytes : 0);
+    const bool anyFlow = flow && (nGroups || nStripG);
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % av1r_ctx::kMetaRing;
     if (M.pending) {
@@ -1165,14 +1383,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     // the launch's status record (k_flow launches only)
     LaunchRec* rec = nullptr;
-    if (flow && nGroups) {
+    if (anyFlow) {
         std::lock_guard<std::mutex> lock(g_recMu);
         if (!g_recFree.empty()) {
             rec = g_recFree.back();
             g_recFree.pop_back();
         }
     }
-    if (flow && nGroups && !rec) {
+    if (anyFlow && !rec) {
         rec = new LaunchRec;
         if (hipHostMalloc(&rec->err, 64) != hipSuccess || hipEventCreateWithFlags(&rec->done, hipEventDisableTiming) != hipSuccess) {
             delete rec;
@@ -1192,6 +1410,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     uint32_t frameRows = 0;  // k_flow-mode timeline: frame-major rows
     for (int i = 0; i < n; i++) {
         hk[i] = jobs[i].k;
+        hk[i].strip = flow && !jobs[i].P->stripGroups.empty();
         hk[i].trace_base = frameRows;
         for (const Level& lv : jobs[i].P->levels) frameRows += lv.cnt[0] + lv.cnt[1] + lv.cnt[2];
     }
@@ -1244,7 +1463,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         for (size_t l = 0; l < nLevels; l++)
             for (int i = 0; i < n; i++) {
                 const auto& lvs = jobs[i].P->levels;
-                if (l >= lvs.size()) continue;
+                if (l >= lvs.size() || !jobs[i].P->stripGroups.empty()) continue;
                 const Level& lv = lvs[l];
                 for (uint32_t q = 0; q < lv.fcnt[1]; q++, g += 2) {
                     g[0] = (uint32_t)i << 8;
@@ -1261,6 +1480,28 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         for (int i = 0; i < n; i++) {
             rt[i + 1] = rt[i] + jobs[i].P->nResidS;
             rt[n + 2 + i] = rt[n + 1 + i] + jobs[i].P->nResidL;
+        }
+        if (nStripS) {
+            // k_strip: [the strips' first groups (nStripS + 1)] [the strips' indices in their
+            // frames (nStripS)] [groups {frame << 8 | n, first item}]
+            uint32_t* ss = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups + resTabBytes);
+            uint32_t* sg = ss + stripTabBytes / 4;
+            uint32_t gb = 0, si = 0;
+            for (int i = 0; i < n; i++) {
+                const Prepared& P = *jobs[i].P;
+                if (P.stripGroups.empty()) continue;
+                for (size_t s = 0; s + 1 < P.stripStart.size(); s++) {
+                    ss[nStripS + 1 + si] = (uint32_t)s;
+                    ss[si++] = gb + P.stripStart[s];
+                }
+                const size_t ng = P.stripGroups.size() / 2;
+                for (size_t q = 0; q < ng; q++) {
+                    sg[2 * (gb + q)] = ((uint32_t)i << 8) | P.stripGroups[2 * q];
+                    sg[2 * (gb + q) + 1] = P.stripGroups[2 * q + 1];
+                }
+                gb += (uint32_t)ng;
+            }
+            ss[si] = gb;
         }
     }
     if (host_prof()) tp2 = now_us();
@@ -1362,6 +1603,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                 launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
             }
             flow_debug_note(epoch, st);
+        }
+        if (nStripS) {  // deep frames: one workgroup per strip (build_strips)
+            uint32_t epoch = ++epochs;
+            if (!epoch) epoch = ++epochs;
+            const uint8_t* sb = M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups + resTabBytes;
+            launch_k_strip(dk, sb + stripTabBytes, reinterpret_cast<const uint32_t*>(sb), (uint32_t)nStripS, ctl, epoch, trace, st);
         }
     }
     if (!flow && lc->timing) {
@@ -2106,6 +2353,8 @@ int av1r_set_flow_spins(av1r_ctx* c, uint32_t spins)
     c->flowSpins = spins;
     return AV1R_OK;
 }
+
+int av1r_set_strip_levels(int levels) { return g_stripLevels.exchange(levels < 0 ? 0 : levels); }
 
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream)
 {

@@ -184,6 +184,23 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
 // were final before the launch and are read from the frame.  The runs are staged in
 // L.tmp / L.tmp2, then AboveRow / LeftCol are assembled as in coop_intra_edges.  Bounded:
 // a spin gives up after ~1 s (or once another wave has) and sets the launch's error word.
+// k_strip: the strip's reconstructed pixels in LDS (av1r_host.cpp build_strips).  Plane p
+// holds rows [top[p], top[p] + (AV1R_STRIP_H >> sub)), column c at c mod (AV1R_RING_W >> sub).
+// (LDS address-space pointers: through a generic pointer every ring access would be a
+// flat_ instruction, which also waits for the wave's outstanding global stores)
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+struct RingView {
+    lds_u8* base[3];
+    int top[3];
+};
+DEV bool ring_has(const RingView& R, int p, int y) { return y >= R.top[p] && y < R.top[p] + (AV1R_STRIP_H >> (p ? 1 : 0)); }
+DEV lds_u8* ring_px(const RingView& R, int p, int x, int y)
+{
+    const int w = AV1R_RING_W >> (p ? 1 : 0);
+    return R.base[p] + (y - R.top[p]) * w + (x & (w - 1));
+}
+
 struct GranEdges {
     const uint32_t* mask;  // 4 words: above, corner, left, (unused)
     uint32_t mA, mC, mL;   // mask[0..2], loaded by the caller (k_flow: before its dependency wait)
@@ -193,6 +210,8 @@ struct GranEdges {
     uint32_t epoch;
     uint32_t* ctl;         // k_flow control block (FLOW_ERR)
     unsigned long long* tr;  // -DAV1R_TRACE timeline row (or null)
+    bool coh;              // units read from the frame: sc1 (k_flow) or plain (k_strip: strip_plain)
+    const RingView* ring;  // k_strip: this strip's pixels (units of the strip's rows come from here)
 };
 template <int NT>
 DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
@@ -228,15 +247,28 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
                               : (cm & 2) ? G.v + (size_t)((x - 1) >> 2) * G.gh + ((y - 1) >> 2)
                                          : G.h + (size_t)((y - 1) >> 2) * G.gw + ((x - 1) >> 2);
             uint32_t val = 0;
-            if (act && !inl) {  // final before this launch
+            if (act && !inl && G.ring && ring_has(*G.ring, plane, kind == 1 ? y + 4 * u : y - 1)) {
+                // k_strip: a unit of this strip, written by an earlier group (the LDS ring)
+                const RingView& R = *G.ring;
                 if (kind == 0) {
-                    val = ldp4<true>(src, x + 4 * u, y - 1);
+                    val = *reinterpret_cast<lds_u32*>(ring_px(R, plane, x + 4 * u, y - 1));
                 } else if (kind == 1) {
                     const int py = y + 4 * u;
-                    val = ldp<true>(src, x - 1, py) | (ldp<true>(src, x - 1, py + 1) << 8) |
-                          (ldp<true>(src, x - 1, py + 2) << 16) | ((uint32_t)ldp<true>(src, x - 1, py + 3) << 24);
+                    val = *ring_px(R, plane, x - 1, py) | (*ring_px(R, plane, x - 1, py + 1) << 8) |
+                          (*ring_px(R, plane, x - 1, py + 2) << 16) | ((uint32_t)*ring_px(R, plane, x - 1, py + 3) << 24);
                 } else {
-                    val = (uint32_t)ldp<true>(src, x - 1, y - 1) << 24;
+                    val = (uint32_t)*ring_px(R, plane, x - 1, y - 1) << 24;
+                }
+            } else if (act && !inl) {  // final before this launch
+                const bool c = G.coh;
+                if (kind == 0) {
+                    val = ldp4_c(src, x + 4 * u, y - 1, c);
+                } else if (kind == 1) {
+                    const int py = y + 4 * u;
+                    val = ldp_c(src, x - 1, py, c) | (ldp_c(src, x - 1, py + 1, c) << 8) |
+                          (ldp_c(src, x - 1, py + 2, c) << 16) | ((uint32_t)ldp_c(src, x - 1, py + 3, c) << 24);
+                } else {
+                    val = (uint32_t)ldp_c(src, x - 1, y - 1, c) << 24;
                 }
             }
             for (;;) {

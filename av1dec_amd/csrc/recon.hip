@@ -42,9 +42,21 @@ DEV unsigned long long trace_now()
     return 0;
 #endif
 }
+// -DAV1R_TRACE_LITE (with AV1R_TRACE): the stamps wait for nothing and go to an LDS row per
+// wave, copied to the timeline by trace_flush at the item's end -- the time a wave reaches
+// each point of its instruction stream, without the drains of the full build
+#ifdef AV1R_TRACE_LITE
+DEV unsigned long long* lite_slots()
+{
+    __shared__ unsigned long long rows[4][AV1R_TRACE_W];
+    return rows[(threadIdx.x >> 6) & 3];
+}
+#endif
 DEV void trace_stamp(unsigned long long* tr, int slot)
 {
-#ifdef AV1R_TRACE
+#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
+    if (tr && (threadIdx.x & 63) == 0) lite_slots()[slot] = __builtin_amdgcn_s_memrealtime();
+#elif defined(AV1R_TRACE)
     if (tr && (threadIdx.x & 63) == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         tr[slot] = __builtin_amdgcn_s_memrealtime();
@@ -52,6 +64,19 @@ DEV void trace_stamp(unsigned long long* tr, int slot)
 #else
     (void)tr;
     (void)slot;
+#endif
+}
+DEV void trace_flush(unsigned long long* tr)
+{
+#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
+    if (tr && (threadIdx.x & 63) == 0)
+        for (int q = 2; q < 14; q++)
+            if (q != 6 && q != 7) {
+                tr[q] = lite_slots()[q];
+                lite_slots()[q] = 0;
+            }
+#else
+    (void)tr;
 #endif
 }
 
@@ -236,10 +261,17 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             // together with the edge loads
             const DevPlane& luma = k.cur.pl[0];
             const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
+            // (k_strip: the same block's luma, in this strip's LDS ring)
+            const RingView* ring = COH && gran ? G->ring : nullptr;
             for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
                 int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
-                int v = (ldp<COH>(luma, lx, ly) + ldp<COH>(luma, lx + 1, ly) + ldp<COH>(luma, lx, ly + 1) +
+                int v;
+                if (ring)
+                    v = (*ring_px(*ring, 0, lx, ly) + *ring_px(*ring, 0, lx + 1, ly) + *ring_px(*ring, 0, lx, ly + 1) +
+                            *ring_px(*ring, 0, lx + 1, ly + 1)) << 1;
+                else
+                    v = (ldp<COH>(luma, lx, ly) + ldp<COH>(luma, lx + 1, ly) + ldp<COH>(luma, lx, ly + 1) +
                             ldp<COH>(luma, lx + 1, ly + 1)) << 1;
                 L.cfl[i * CM + j] = (int16_t)v;
                 s += v;
@@ -327,8 +359,11 @@ DEV uint32_t add4(uint32_t p, uint2 r)
     for (int b = 0; b < 4; b++) o |= (uint32_t)clip1((int)((p >> (8 * b)) & 0xff) + v[b]) << (8 * b);
     return o;
 }
+// k_strip (ring): the pixels also go to the strip's LDS ring, and the granules only where
+// another strip reads them (pub bit 1)
 template <int NT, int MAX>
-DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch)
+DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch,
+    const RingView* ring = nullptr)
 {
 
     const int t = coop_lane<NT>();
@@ -336,6 +371,7 @@ DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, cons
     const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
     const DevPlane& dst = k.cur.pl[tb.plane];
     const bool gran = k.gran;
+    const bool coh = !strip_plain(k.strip, gran);
 #pragma unroll
     for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
         const int q = t + u * NT;
@@ -343,11 +379,12 @@ DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, cons
             const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
             uint32_t* pp = reinterpret_cast<uint32_t*>(&L.pred[i * MAX + j]);
             const uint32_t o = add4(*pp, R.r[u]);
-            stp4<true>(dst, tb.x + j, tb.y + i, o);
+            stp4_c(dst, tb.x + j, tb.y + i, o, coh);
+            if (ring) *reinterpret_cast<lds_u32*>(ring_px(*ring, tb.plane, tb.x + j, tb.y + i)) = o;
             if (gran) *pp = o;  // the final pixels, for the edge granules
         }
     }
-    if (gran) {
+    if (gran && (!ring || (tb.pub & 2))) {
         coop_sync<NT>();
         const int p = tb.plane;
         coop_publish_gran<NT>(L.pred, MAX, tb.x, tb.y, av1r_tx_w[tb.tx_size], av1r_tx_h[tb.tx_size], k.gran_h[p], k.gran_v[p],
@@ -1296,9 +1333,10 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
                 }
                 coop_sync<NT>();
             }
+            const bool coh = COH && !strip_plain(k.strip, gran);
             for (int q = t; q < pw * ph; q += NT) {
                 const int i = q / pw, j = q - i * pw;
-                stp<COH>(dst, baseX + j, baseY + i, L.pred[i * 64 + j]);
+                stp_c(dst, baseX + j, baseY + i, L.pred[i * 64 + j], coh);
             }
             if (COH && gran)
                 coop_publish_gran<NT>(L.pred, 64, baseX, baseY, pw, ph, k.gran_h[plane], k.gran_v[plane], k.gran_w[plane],
@@ -1643,7 +1681,7 @@ DEV void flow_publish(uint32_t* flag, uint32_t epoch)
 // 7 XCC id << 16 | dependency count
 template <int NT, int MAX>
 DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl,
-    unsigned long long* trace, uint32_t s)
+    unsigned long long* trace, uint32_t s, const RingView* ring = nullptr)
 {
     // What the item reads from the batch after its wait -- its edge mask words, its block's
     // prediction fields, the edge-filter flag (and with AV1R_FLOW_ITEM_COPY its own record)
@@ -1683,6 +1721,8 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         G.gh = k.gran_hn[p];
         G.epoch = epoch;
         G.ctl = ctl;
+        G.coh = !strip_plain(k.strip, gran);
+        G.ring = ring;
         G.tr = tr;
     }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
@@ -1704,14 +1744,15 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         trace_stamp(tr, 4);
         tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran, edgeFilter);
         trace_stamp(tr, 9);
-        tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
+        tb_store_flow<NT, MAX>(k, wi, L, R, epoch, ring);
         trace_stamp(tr, 10);
     }
     // the store drain and done flag only where a dependency list names the item (CFL's
     // luma; every edge owner without granules): edges travel in granules, and later
     // launches see every store anyway
-    if (wi.pub || !gran) flow_publish<NT>(k.done + pos, epoch);
+    if ((wi.pub & 1) || !gran) flow_publish<NT>(k.done + pos, epoch);
     trace_stamp(tr, 5);
+    trace_flush(tr);
 }
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
@@ -1841,6 +1882,74 @@ void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uin
     (void)hostErr;  // (its address travels in the control block: FLOW_HOSTERR)
     hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
         trace);
+}
+
+// ---------------------------------------------------------------------------------
+// k_strip: the items of deep intra frames (a key frame's ~2 000-level wavefront), one
+// workgroup per 64-row strip of a frame (av1r_host.cpp build_strips).  The workgroup runs
+// its strip's groups -- k_flow's groups: one large item, or up to four small ones, one per
+// wave -- in level order, and keeps the strip's reconstructed pixels in an LDS ring
+// (AV1R_RING_W columns, RingView): an item reads the edge and CFL pixels of its own strip
+// from the ring, written by an earlier group before the barrier that ends every group, so
+// a same-strip hand-off costs an LDS round trip instead of a trip through the device
+// coherence point.  The frame is written with plain stores and never read for a pixel of
+// this launch; what crosses a strip boundary (the row above a strip, below-left columns
+// reaching into the next strip) travels as k_flow's granules, published only by the items
+// whose units another strip reads.  Progress: an item waits only for granules of items of
+// lower levels; every strip runs its groups in level order, so a wait chain strictly
+// descends in level and ends at an item whose strip is running it, once every strip's
+// workgroup is resident (a few dozen per frame; nothing else on the chip waits for them).
+// tab: [first group of each strip (nStrips + 1)] [each strip's index in its frame (nStrips)].
+// ---------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void k_strip(const KParams* kps, const uint2* __restrict__ groups,
+    const uint32_t* __restrict__ tab, uint32_t nStrips, uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
+{
+    constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
+    constexpr int kRingY = AV1R_STRIP_H * AV1R_RING_W, kRingC = (AV1R_STRIP_H / 2) * (AV1R_RING_W / 2);
+    __shared__ __align__(16) uint8_t smem[kLds];
+    __shared__ __align__(16) uint8_t ringMem[kRingY + 2 * kRingC];
+    const uint32_t s = blockIdx.x;
+    const uint32_t sid = tab[nStrips + 1 + s];
+    RingView R;
+    R.base[0] = (lds_u8*)ringMem;
+    R.base[1] = (lds_u8*)ringMem + kRingY;
+    R.base[2] = (lds_u8*)ringMem + kRingY + kRingC;
+    R.top[0] = (int)sid * AV1R_STRIP_H;
+    R.top[1] = R.top[2] = (int)sid * (AV1R_STRIP_H / 2);
+    const uint32_t g1 = tab[s + 1];
+    for (uint32_t g = tab[s]; g < g1; g++) {
+        const uint2 gd = groups[g];
+        const KParams& k = KP(kps, gd.x >> 8);
+        const uint32_t n = gd.x & 0xff;
+        if (n == 0) {
+            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8, &R);
+        } else {
+            const uint32_t wave = threadIdx.x >> 6;
+            if (wave < n)
+                flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
+                    gd.x >> 8, &R);
+        }
+        // the group's ring writes are visible to every later group; its frame stores and
+        // granules need no drain (nothing in the strip reads them back)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifdef AV1R_TRACE
+        if (trace && threadIdx.x == 0) {  // row slots 14: strip << 32 | group, 15: group end
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t w = 0; w < (n ? n : 1); w++) {
+                unsigned long long* tr = trace + (size_t)(k.trace_base + gd.y + w) * AV1R_TRACE_W;
+                tr[14] = ((unsigned long long)s << 32) | g;
+                tr[15] = now;
+            }
+        }
+#endif
+    }
+}
+
+void launch_k_strip(const KParams* kps, const void* groups, const uint32_t* tab, uint32_t nStrips, uint32_t* ctl,
+    uint32_t epoch, unsigned long long* trace, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_strip, dim3(nStrips), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), tab, nStrips, ctl,
+        epoch, trace);
 }
 
 #endif  // AV1R_FLOW_PART

@@ -308,6 +308,11 @@ const char* av1r_last_error(av1r_ctx* ctx);
  * from different streams; -1 in a normal build. */
 int av1r_set_flow_spins(av1r_ctx* ctx, uint32_t spins);
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream);
+/* Process-wide: frames scheduled from now on with more than `levels` dependency levels
+ * (a key frame's intra wavefront) run on k_strip, one workgroup per 64-row strip, instead
+ * of k_flow; 0 = never.  Default 0 (environment AV1R_STRIP_LEVELS).  Returns the previous
+ * value.  Both kernels are bit-exact; tests lower it to run every stream on k_strip. */
+int av1r_set_strip_levels(int levels);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);

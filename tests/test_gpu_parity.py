@@ -51,6 +51,24 @@ def test_gpu_matches_reference(stream):
     assert got == out_md5 == BITS[stream]
 
 
+@pytest.fixture
+def strip_everywhere(native_lib):
+    # every frame with more than one dependency level on k_strip (one workgroup per 64-row
+    # strip; by default only deep frames -- > 400 levels -- take it)
+    prev = native_lib.av1r_set_strip_levels(1)
+    yield
+    native_lib.av1r_set_strip_levels(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", STREAMS)
+def test_gpu_strip_schedule_matches_reference(stream, strip_everywhere):
+    # k_strip (av1r_host.cpp build_strips): every stage of every frame, all 172 streams
+    bad, got, out_md5 = run_stream(stream)
+    assert not bad, bad[:3]
+    assert got == out_md5 == BITS[stream]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream", STREAMS)
 def test_gpu_level_schedule_matches_reference(stream):
