@@ -11,6 +11,7 @@
 
 #include <deque>
 #include <new>
+#include <vector>
 
 #include "av1dec.h"
 #include "av1r.h"
@@ -72,6 +73,7 @@ public:
         if (m_ctx) av1d_destroy(m_ctx);
         m_ctx = nullptr;
         m_pts.clear();
+        m_changed.clear();
     }
 
     void flush() override
@@ -79,12 +81,23 @@ public:
         if (!m_ctx) return;
         av1d_flush(m_ctx);
         m_pts.clear();
+        m_changed.clear();
     }
 
     YamiStatus decode(VideoDecodeBuffer* buffer) override
     {
         if (!m_ctx) return YAMI_NO_CONFIG;
         if (!buffer || !buffer->data || !buffer->size) return YAMI_SUCCESS;  // end of stream
+        // A libyami client answers YAMI_DECODE_FORMAT_CHANGE by reconfiguring and sending the
+        // same buffer again.  This decoder has already decoded that unit (its frames are
+        // queued), so the resend is acknowledged without decoding it twice (which would
+        // duplicate its output, refresh the reference slots again and shift the pts queue).
+        if (!m_changed.empty()) {
+            const bool resend = buffer->size == m_changed.size() && buffer->timeStamp == m_changedTs &&
+                                memcmp(buffer->data, m_changed.data(), buffer->size) == 0;
+            m_changed.clear();
+            if (resend) return YAMI_SUCCESS;
+        }
         const int rc = av1d_decode(m_ctx, buffer->data, buffer->size);
         const bool parse = strncmp(av1d_last_error(m_ctx), "parse", 5) == 0;
         if (rc) return to_yami(rc, parse);
@@ -102,6 +115,8 @@ public:
             if ((m_wantW && m_wantW != (uint32_t)w) || (m_wantH && m_wantH != (uint32_t)h)) {
                 m_wantW = (uint32_t)w;
                 m_wantH = (uint32_t)h;
+                m_changed.assign(buffer->data, buffer->data + buffer->size);
+                m_changedTs = buffer->timeStamp;
                 return YAMI_DECODE_FORMAT_CHANGE;
             }
         }
@@ -160,6 +175,8 @@ private:
     VideoFormatInfo m_info = {};
     uint32_t m_wantW = 0, m_wantH = 0;
     std::deque<int64_t> m_pts;
+    std::vector<uint8_t> m_changed;  // the unit that reported YAMI_DECODE_FORMAT_CHANGE (a resend is a no-op)
+    int64_t m_changedTs = 0;
     char m_mime[32] = YAMI_MIME_AV1;
 };
 

@@ -5,7 +5,8 @@
 //   yami_decode <in.ivf> <out.yuv> [--size WxH] [--flush-at N]
 //
 // --size passes the expected dimensions to start() (a stream of another size reports
-// YAMI_DECODE_FORMAT_CHANGE once); --flush-at N calls flush() after unit N and skips to the
+// YAMI_DECODE_FORMAT_CHANGE once, and the buffer is sent again, as libyami clients do);
+// --flush-at N calls flush() after unit N and skips to the
 // next key frame (seek).  Exit status 0 on success; the status of a failing call otherwise.
 #include <stdio.h>
 #include <stdlib.h>
@@ -118,7 +119,9 @@ int main(int argc, char** argv)
             const VideoFormatInfo* fi = dec->getFormatInfo();
             fprintf(stderr, "format change: %ux%u\n", fi ? fi->width : 0, fi ? fi->height : 0);
             formatChanges++;
-        } else if (st != YAMI_SUCCESS) {
+            st = dec->decode(&buf);  // as libyami clients do: reconfigure, then send the buffer again
+        }
+        if (st != YAMI_SUCCESS) {
             fprintf(stderr, "decode unit %d: status %d\n", unit, st);
             releaseVideoDecoder(dec);
             return 5;

@@ -1097,6 +1097,10 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
     *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi;
+    static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
+    if (sizeDbg && host)
+        fprintf(stderr, "av1r pack: blocks %zu tbs %zu coefs %zu items %zu (%zu) deps %zu done %zu tbres %zu resid %zu lr %zu\n", szBlk,
+            szTb, szCoef, szItems, c->items.size(), szDeps, szDone, szTbRes, szResS + szResL, szLr);
     if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {

@@ -183,7 +183,7 @@ extern "C" {
 int av1r_cycle_next(void* user, int stream, const av1r_frame_batch** batch)
 {
     av1r_cycle* c = (av1r_cycle*)user;
-    if (!c || !batch || stream < 0 || c->count[stream] <= 0) return AV1R_E_INVALID;
+    if (!c || !batch || stream < 0 || stream >= c->n_streams || c->count[stream] <= 0) return AV1R_E_INVALID;
     *batch = c->batches[stream][c->pos[stream] % c->count[stream]];
     c->pos[stream]++;
     return 0;
@@ -228,6 +228,10 @@ int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* sr
                       int workers, av1r_pipeline_stats* stats)
 {
     if (!ctxs || n <= 0 || n > 32 || !src || !src->next) return AV1R_E_INVALID;
+    // a cycling source never ends: it needs a frame budget, and one batch list per stream
+    if (src->next == av1r_cycle_next &&
+        (max_frames <= 0 || !src->user || static_cast<const av1r_cycle*>(src->user)->n_streams < n))
+        return AV1R_E_INVALID;
     Run R(n);
     R.src = src;
     R.maxFrames = max_frames;

@@ -222,7 +222,8 @@ class PipelineStats(C.Structure):  # av1r_pipeline_stats
 
 
 class Cycle(C.Structure):  # av1r_cycle
-    _fields_ = [("batches", C.c_void_p), ("count", C.POINTER(C.c_int)), ("pos", C.POINTER(C.c_int64))]
+    _fields_ = [("batches", C.c_void_p), ("count", C.POINTER(C.c_int)), ("pos", C.POINTER(C.c_int64)),
+                ("n_streams", C.c_int)]
 
 
 EXPORTS = [

@@ -134,7 +134,8 @@ def run_native(decoders, source="cycle", streams=None, positions=None, max_frame
     """The same pipeline in native threads (av1r_pipeline_run, include/av1r.h): no
     interpreter on the path (`workers` packing threads, 0: one per stream).  source "cycle": streams = per-stream lists of batchfile.Frame;
     stream j continues at frame positions[j] (mod its length), and positions is advanced in
-    place by the frames decoded; "ivf": streams = IVF file contents.  Returns the
+    place by the frames decoded (it never ends: max_frames > 0 is required); "ivf": streams =
+    IVF file contents.  Returns the
     av1r_pipeline_stats as a dict."""
     l = native.lib()
     n = len(decoders)
@@ -149,7 +150,9 @@ def run_native(decoders, source="cycle", streams=None, positions=None, max_frame
         table = (C.c_void_p * n)(*[C.cast(r, C.c_void_p).value for r in rows])
         count = (C.c_int * n)(*[len(fr) for fr in streams])
         pos = (C.c_int64 * n)(*(positions or [0] * n))
-        cyc = native.Cycle(C.cast(table, C.c_void_p).value, count, pos)
+        if max_frames <= 0:
+            raise ValueError("the cycle source never ends: max_frames must be > 0")
+        cyc = native.Cycle(C.cast(table, C.c_void_p).value, count, pos, n)
         keep += [rows, table, count, pos, cyc, streams]
         src.next = C.cast(l.av1r_cycle_next, C.c_void_p).value
         src.user = C.cast(C.pointer(cyc), C.c_void_p).value

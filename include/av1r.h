@@ -350,12 +350,15 @@ typedef struct av1r_pipeline_stats {
 } av1r_pipeline_stats;
 int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
                       int workers, av1r_pipeline_stats* stats);
-/* Source over in-memory batches: stream s yields batches[s][pos[s] % count[s]], then
- * advances pos[s] (use av1r_cycle_next as `next` and an av1r_cycle as `user`). */
+/* Source over in-memory batches: stream s (< n_streams) yields batches[s][pos[s] % count[s]],
+ * then advances pos[s] (use av1r_cycle_next as `next` and an av1r_cycle as `user`).  It
+ * never ends, so av1r_pipeline_run rejects it (AV1R_E_INVALID) without max_frames > 0 or
+ * with fewer than n streams. */
 typedef struct av1r_cycle {
     const av1r_frame_batch* const* const* batches;
     const int* count;
     int64_t* pos;
+    int n_streams;
 } av1r_cycle;
 int av1r_cycle_next(void* user, int stream, const av1r_frame_batch** batch);
 /* Source over IVF files (one per stream, caller-owned while the source lives): temporal

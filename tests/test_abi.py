@@ -145,3 +145,26 @@ def test_cli_usage_without_device():
     assert r.returncode != 0 and "usage" in r.stderr
     r = subprocess.run([native.CLI, "-i", "/nonexistent.ivf"], capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "can't open" in r.stderr
+
+
+def test_cycle_source_bounds(native_lib):
+    """The in-memory cycling source (av1r_cycle_next) checks its stream index, and the
+    pipeline refuses it without a frame budget (it never ends) -- both before any device use."""
+    frames = batchfile.load(golden.batch_path("64x64"))
+    row = (C.c_void_p * 1)(C.cast(frames[0].byref(), C.c_void_p).value)
+    table = (C.c_void_p * 1)(C.cast(row, C.c_void_p).value)
+    count = (C.c_int * 1)(1)
+    pos = (C.c_int64 * 1)(0)
+    cyc = native.Cycle(C.cast(table, C.c_void_p).value, count, pos, 1)
+    out = C.c_void_p()
+    assert native_lib.av1r_cycle_next(C.byref(cyc), 0, C.byref(out)) == 0 and out.value == row[0]
+    assert pos[0] == 1
+    assert native_lib.av1r_cycle_next(C.byref(cyc), 1, C.byref(out)) == abi.AV1R_E_INVALID
+    assert native_lib.av1r_cycle_next(C.byref(cyc), -1, C.byref(out)) == abi.AV1R_E_INVALID
+    src = native.StreamSource(C.cast(native_lib.av1r_cycle_next, C.c_void_p).value,
+                              C.cast(C.pointer(cyc), C.c_void_p).value, 1)
+    ctxs = (C.c_void_p * 1)(1)  # never dereferenced: rejected first
+    st = native.PipelineStats()
+    assert native_lib.av1r_pipeline_run(ctxs, 1, C.byref(src), 0, 0, 1, C.byref(st)) == abi.AV1R_E_INVALID
+    ctxs2 = (C.c_void_p * 2)(1, 1)
+    assert native_lib.av1r_pipeline_run(ctxs2, 2, C.byref(src), 5, 0, 1, C.byref(st)) == abi.AV1R_E_INVALID

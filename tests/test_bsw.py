@@ -40,6 +40,18 @@ def test_golden_covers_every_config():
     assert set(GOLD) == set(pybsw.CONFIGS)
 
 
+def test_hidden_and_show_existing_units():
+    """cif_hidden's units carry hidden frames (show_frame = 0) and show_existing_frame units:
+    the parser yields one more frame batch per hidden frame and one show-existing entry per
+    such unit, and exactly one shown frame per unit."""
+    from av1dec_amd import parser
+    frames = parser.Parser().decode_ivf(stream("cif_hidden"))
+    hidden = [f for f in frames if not f.show_existing and not f.hdr.show_frame]
+    shown_existing = [f for f in frames if f.show_existing]
+    assert len(hidden) == len(shown_existing) == 3
+    assert len(frames) - len(hidden) == GOLD["cif_hidden"]["frames"]
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_writer_is_exact(name):
     """Every unit re-parsed by a second parser gives the writer's own frame batches."""
@@ -70,7 +82,7 @@ def test_oracle_matches_reference_md5(name):
     import pyoracle
     from av1dec_amd import parser
     frames = parser.Parser().decode_ivf(stream(name))
-    assert len(frames) == GOLD[name]["frames"]
+    assert sum(1 for f in frames if f.show_existing or f.hdr.show_frame) == GOLD[name]["frames"]  # shown frames
     o = pyoracle.Oracle(keep_stages=False)
     try:
         assert _md5_of(frames, o) == GOLD[name]["md5"]
@@ -110,7 +122,7 @@ def test_gpu_ivf_pipeline_matches_reference_md5(native_lib):
     equals the reference's."""
     from av1dec_amd import Decoder
     from av1dec_amd.pipeline import IvfPipeline
-    names = ["1080p_s1", "cif_s1", "640x360_tiles2x2_sb64", "odd_416x234_key3"]
+    names = ["1080p_s1", "cif_s1", "640x360_tiles2x2_sb64", "odd_416x234_key3", "cif_hidden"]
     decs = [Decoder(0) for _ in names]
     try:
         outs = [[] for _ in names]
@@ -133,14 +145,17 @@ def test_gpu_ivf_pipeline_matches_reference_md5(native_lib):
 @pytest.mark.gpu
 def test_gpu_native_pipeline_ivf_matches_reference_md5(native_lib):
     """av1r_pipeline_run over the IVF source (native producer threads, the bench's
-    ivf_end_to_end path) on four streams of different sizes, outputs kept."""
+    ivf_end_to_end path) on five streams of different sizes, outputs kept.  cif_hidden carries
+    hidden frames and show_existing_frame units: the pipeline's show-existing entries
+    (av1r_show_existing, ordered by sequence number across the workers) in output order."""
     from av1dec_amd import Decoder
     from av1dec_amd.pipeline import run_native
-    names = ["1080p_s1", "cif_gm_rotzoom", "640x360_tiles2x2_sb64", "odd_416x234_key3"]
+    names = ["1080p_s1", "cif_gm_rotzoom", "640x360_tiles2x2_sb64", "odd_416x234_key3", "cif_hidden"]
     decs = [Decoder(0) for _ in names]
     try:
         st = run_native(decs, "ivf", [stream(n) for n in names])
-        assert st["frames"] == sum(GOLD[n]["frames"] for n in names)
+        from av1dec_amd import parser  # decoded frames: shown, hidden and show-existing entries
+        assert st["frames"] == sum(len(parser.Parser().decode_ivf(stream(n))) for n in names)
         for n, d in zip(names, decs):
             md = hashlib.md5()
             while d.output_pending():

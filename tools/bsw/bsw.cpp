@@ -52,6 +52,9 @@ typedef struct av1bsw_params {
     int lr;                // 0 none, 1 Wiener luma + self-guided chroma, 2 switchable on all planes
     int verify;            // re-parse every temporal unit and compare the batches
     int intra_only;        // every frame a key frame (intra)
+    int hidden;            // hidden frames: every 4th unit after a key frame codes an ALTREF-style frame
+                           // (show_frame = 0, two frames ahead, slot 7) before its shown frame, and
+                           // two units later a show_existing_frame unit shows it
 } av1bsw_params;
 }
 
@@ -270,6 +273,8 @@ public:
     Rng rng;
     Cdfs defaults;  // the distributions the chooser samples from
     int t = 0, since_key = 0;
+    int coded_since_key = 0;  // coded shown frames since the key frame (the slot cycle)
+    bool hidden_pending = false;  // slot 7 holds a hidden frame not yet shown
     int slot_of_age[8] = {};  // slot holding the frame `age` frames back (age 1..7)
     std::vector<uint8_t> tu;
     std::string err;
@@ -451,16 +456,18 @@ public:
 
     // the frame header; `key` frames refresh every slot, inter frames one slot, referencing
     // the seven most recent frames (the key frame in slot 0 as GOLDEN)
-    void frame_header(BitWriter& w, bool key, int refresh, const int* ref_idx)
+    // (show = false: a hidden, showable frame whose order hint is `hint_ahead` units ahead)
+    void frame_header(BitWriter& w, bool key, int refresh, const int* ref_idx, bool show = true, int hint_ahead = 0)
     {
         const SeqHdr& seq = P.seq;
         w.f(1, 0);  // show_existing_frame
         w.f(2, key ? KEY_FRAME : INTER_FRAME);
-        w.f(1, 1);  // show_frame
+        w.f(1, show);  // show_frame
+        if (!show) w.f(1, 1);  // showable_frame
         if (!key) w.f(1, 0);  // error_resilient_mode
         w.f(1, 0);  // disable_cdf_update
         w.f(1, 0);  // frame_size_override_flag
-        const int hint = t & ((1 << seq.order_hint_bits) - 1);
+        const int hint = (t + hint_ahead) & ((1 << seq.order_hint_bits) - 1);
         w.f(seq.order_hint_bits, (uint32_t)hint);
         if (!key) w.f(3, 0);  // primary_ref_frame = LAST
         if (!key) w.f(8, (uint32_t)refresh);
@@ -578,15 +585,30 @@ public:
         w.f(1, 1);  // tx_mode_select
         if (!key) {
             w.f(1, 1);  // reference_select
-            // skip_mode_present: allowed when the (all forward) references carry two hints
-            int h0 = -1;
-            bool two = false;
+            // skip_mode_present when skipModeAllowed (spec 5.9.22): a forward reference and a
+            // backward one, or two forward references with different hints
+            const int bits = seq.order_hint_bits, cur = hint;
+            auto dist = [&](int a, int b) {
+                const int m = 1 << (bits - 1);
+                int d = a - b;
+                return (d & (m - 1)) - (d & m);
+            };
+            int fwd = -1, bwd = -1, fwdHint = 0, bwdHint = 0;
             for (int i = 0; i < kRefsPerFrame; i++) {
                 const int h = P.slots[ref_idx[i]].order_hint;
-                if (h0 < 0) h0 = h;
-                else if (h != h0) two = true;
+                if (dist(h, cur) < 0) {
+                    if (fwd < 0 || dist(h, fwdHint) > 0) fwd = i, fwdHint = h;
+                } else if (dist(h, cur) > 0) {
+                    if (bwd < 0 || dist(h, bwdHint) < 0) bwd = i, bwdHint = h;
+                }
             }
-            if (two) w.f(1, rng.bern(0.5));
+            bool allowed = fwd >= 0 && bwd >= 0;
+            if (fwd >= 0 && bwd < 0)
+                for (int i = 0; i < kRefsPerFrame && !allowed; i++) {
+                    const int h = P.slots[ref_idx[i]].order_hint;
+                    if (dist(h, fwdHint) < 0) allowed = true;
+                }
+            if (allowed) w.f(1, rng.bern(0.5));
             w.f(1, 1);  // allow_warped_motion
         }
         w.f(1, 0);  // reduced_tx_set
@@ -660,22 +682,57 @@ public:
             if (P.parse_sequence_header(br)) return fail("sequence header: %s", P.err.c_str());
         }
         int refIdx[7] = {}, refresh = 0xff;
+        const bool hid = prm.hidden && !key;
         if (key) {
             since_key = 0;
+            coded_since_key = 0;
+            hidden_pending = false;
             for (int a = 0; a < 8; a++) slot_of_age[a] = 0;
         } else {
             since_key++;
-            // this frame's slot: cycle 1..7 (slot 0 keeps the key frame as GOLDEN)
-            const int slot = 1 + (since_key - 1) % 7;
+            if (hid && since_key % 4 == 3 && hidden_pending) {
+                // a show_existing_frame unit: the hidden frame of two units back (its order hint
+                // is this unit's), spec 5.9.2 / 7.21 (Av1Decoder.cpp:158-169)
+                BitWriter sw;
+                sw.f(1, 1);  // show_existing_frame
+                sw.f(3, 7);  // frame_to_show_map_idx
+                sw.trailing();
+                BitReader br(sw.b.data(), sw.b.size());
+                P.seen_frame_header = false;
+                if (P.parse_frame_header(br)) return fail("unit %d: show_existing header: %s", t, P.err.c_str());
+                obu(tu, OBU_FRAME_HEADER, sw.b);
+                hidden_pending = false;
+                return end_unit();
+            }
+            coded_since_key++;
+            // this frame's slot: cycle 1..7 (slot 0 keeps the key frame as GOLDEN); with hidden
+            // frames 1..6, and ALTREF is slot 7 (the latest hidden frame, or the key frame)
+            const int nslots = hid ? 6 : 7;
+            const int slot = 1 + (coded_since_key - 1) % nslots;
             refresh = 1 << slot;
             const int ages[7] = {1, 2, 3, 0, 4, 5, 6};  // LAST, LAST2, LAST3, GOLDEN(key), BWDREF, ALTREF2, ALTREF
             for (int i = 0; i < 7; i++) refIdx[i] = ages[i] == 0 ? 0 : slot_of_age[ages[i]];
+            if (hid) refIdx[6] = 7;
             for (int a = 7; a > 1; a--) slot_of_age[a] = slot_of_age[a - 1];
             slot_of_age[1] = slot;
+            if (hid && since_key % 4 == 1) {
+                // a hidden frame first (two units ahead, into slot 7), shown two units later
+                BitWriter hh;
+                frame_header(hh, false, 1 << 7, refIdx, false, 2);
+                if (int rc = code_frame(hh)) return rc;
+                hidden_pending = true;
+            }
         }
         if (key) slot_of_age[1] = 0;
         BitWriter hw;
         frame_header(hw, key, refresh, refIdx);
+        if (int rc = code_frame(hw)) return rc;
+        return end_unit();
+    }
+
+    // the frame whose uncompressed header is in hw: header check, tiles, one OBU_FRAME
+    int code_frame(BitWriter& hw)
+    {
         const size_t hdrBits = hw.pos;
         {
             std::vector<uint8_t> hb = hw.b;
@@ -719,6 +776,12 @@ public:
         if (P.finish_frame()) return fail("frame %d: %s", t, P.err.c_str());
         P.seen_frame_header = false;
         obu(tu, OBU_FRAME, payload);
+        return 0;
+    }
+
+    // verify the unit (every frame it carries re-parsed and compared) and advance
+    int end_unit()
+    {
         int rc = 0;
         if (prm.verify) {
             if (V.decode_tu(tu.data(), tu.size())) {
@@ -771,7 +834,7 @@ void av1bsw_close(void* h) { delete (Writer*)h; }
 
 #ifdef AV1BSW_MAIN
 // av1bsw -o out.ivf [-w 1920] [-h 1080] [-n 60] [-s seed] [--tiles C R] [--sb64] [-q 96]
-//        [--sharp N] [--lf-deltas] [--delta-q N] [--gm N] [--cdef N] [--lr N] [--key N] [--verify]
+//        [--sharp N] [--lf-deltas] [--delta-q N] [--gm N] [--cdef N] [--lr N] [--key N] [--hidden] [--verify]
 int main(int argc, char** argv)
 {
     av1bsw_params p = {};
@@ -804,6 +867,7 @@ int main(int argc, char** argv)
         else if (a == "--lr") p.lr = atoi(arg());
         else if (a == "--key") p.key_interval = atoi(arg());
         else if (a == "--intra") p.intra_only = 1;
+        else if (a == "--hidden") p.hidden = 1;
         else if (a == "--verify") p.verify = 1;
         else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }

@@ -24,7 +24,7 @@ SRCS = [os.path.join(HERE, "bsw.cpp"), os.path.join(PARSE, "obu.cpp"), os.path.j
 # global motion) against the reference decoder.
 BASE = dict(width=1920, height=1080, seed=0x5EED0001, sb128=1, tile_cols_log2=0, tile_rows_log2=0, base_q_idx=96,
             key_interval=0, lf_level=(32, 32, 16, 16), lf_sharpness=0, lf_delta_update=0, delta_q=0, gm=0, cdef=4,
-            lr=1, intra_only=0)
+            lr=1, intra_only=0, hidden=0)
 CONFIGS = {
     "cif_s1": dict(width=352, height=288, frames=10, seed=0x5EED0101),
     "cif_intra": dict(width=352, height=288, frames=3, seed=0x5EED0102, intra_only=1, base_q_idx=40),
@@ -39,6 +39,9 @@ CONFIGS = {
                                   tile_rows_log2=1),
     "odd_416x234_key3": dict(width=416, height=234, frames=7, seed=0x5EED010A, key_interval=3, base_q_idx=180),
     "1080p_s1": dict(width=1920, height=1080, frames=6, seed=0x5EED1000),
+    # hidden (show_frame = 0) ALTREF-style frames with future order hints, shown two units
+    # later by show_existing_frame units: output order != decode order, backward references
+    "cif_hidden": dict(width=352, height=288, frames=12, seed=0x5EED010B, hidden=1),
     "4k_s2_tiles4x2": dict(width=3840, height=2160, frames=3, seed=0x5EED0002, tile_cols_log2=2, tile_rows_log2=1),
 }
 
@@ -48,7 +51,7 @@ class Params(C.Structure):
                 ("tile_cols_log2", C.c_int), ("tile_rows_log2", C.c_int), ("base_q_idx", C.c_int),
                 ("key_interval", C.c_int), ("lf_level", C.c_int * 4), ("lf_sharpness", C.c_int),
                 ("lf_delta_update", C.c_int), ("delta_q", C.c_int), ("gm", C.c_int), ("cdef", C.c_int),
-                ("lr", C.c_int), ("verify", C.c_int), ("intra_only", C.c_int)]
+                ("lr", C.c_int), ("verify", C.c_int), ("intra_only", C.c_int), ("hidden", C.c_int)]
 
 
 def _stale(target):
