@@ -114,28 +114,64 @@ const char* av1d_last_error(av1d_ctx* c) { return c ? c->err.c_str() : "null con
 // ---- C++ facade ----
 namespace Yami {
 
+// VideoFrame.cpp:41-65: rows padded to 128 + 2 x 16 luma pixels, 16 (luma) / 8 (chroma)
+// pixels of margin around every plane, so extendBorder() stays inside the allocation
 std::shared_ptr<YuvFrame> YuvFrame::create(int width, int height)
 {
-    std::shared_ptr<YuvFrame> f(new YuvFrame);
-    const int cw = (width + 1) >> 1, ch = (height + 1) >> 1;
-    const size_t ySize = (size_t)width * height, cSize = (size_t)cw * ch;
-    f->m_buffer = (uint8_t*)malloc(ySize + 2 * cSize);
-    if (!f->m_buffer) return nullptr;
+    if (width <= 0 || height <= 0) return nullptr;
+    std::shared_ptr<YuvFrame> f(new (std::nothrow) YuvFrame);
+    if (!f) return nullptr;
+    const int pad = 16;
+    const size_t aw = (size_t)((width + 127) & ~127) + 2 * pad, ah = (size_t)((height + 127) & ~127) + 2 * pad;
+    try {
+        f->m_storage.resize(aw * ah * 3 / 2);
+    } catch (const std::bad_alloc&) {
+        return nullptr;
+    }
     f->width = width;
     f->height = height;
-    f->data[0] = f->m_buffer;
-    f->data[1] = f->m_buffer + ySize;
-    f->data[2] = f->m_buffer + ySize + cSize;
-    f->strides[0] = f->widths[0] = width;
-    f->heights[0] = height;
-    for (int p = 1; p < 3; p++) {
-        f->strides[p] = f->widths[p] = cw;
-        f->heights[p] = ch;
+    size_t base = 0;
+    for (int p = 0; p < MAX_PLANES; p++) {
+        const int sub = p ? 2 : 1;
+        f->widths[p] = width / sub;
+        f->heights[p] = height / sub;
+        f->strides[p] = (int)(aw / sub);
+        f->data[p] = f->m_storage.data() + base + (size_t)(pad / sub) * f->strides[p] + pad / sub;
+        base += (aw / sub) * (ah / sub);
     }
     return f;
 }
 
-YuvFrame::~YuvFrame() { free(m_buffer); }
+std::shared_ptr<YuvFrame> YuvFrame::create(const std::shared_ptr<YuvFrame>& other)
+{
+    if (!other) return nullptr;
+    std::shared_ptr<YuvFrame> f = create(other->width, other->height);
+    if (!f) return nullptr;
+    f->pts = other->pts;
+    for (int p = 0; p < MAX_PLANES; p++)
+        for (int y = 0; y < other->heights[p]; y++)
+            memcpy(f->data[p] + (size_t)y * f->strides[p], other->data[p] + (size_t)y * other->strides[p], other->widths[p]);
+    return f;
+}
+
+void YuvFrame::extendBorder(int borders)
+{
+    if (borders <= 0 || borders >= 8) return;  // the margin is 8 chroma pixels
+    for (int p = 0; p < MAX_PLANES; p++) {
+        const int w = widths[p], h = heights[p], s = strides[p];
+        for (int y = 0; y < h; y++) {
+            uint8_t* row = data[p] + (size_t)y * s;
+            memset(row - borders, row[0], borders);
+            memset(row + w, row[w - 1], borders);
+        }
+        const uint8_t* top = data[p] - borders;
+        const uint8_t* bottom = top + (size_t)(h - 1) * s;
+        for (int i = 1; i <= borders; i++) {
+            memcpy(data[p] - borders - (size_t)i * s, top, w + 2 * borders);
+            memcpy(data[p] - borders + (size_t)(h - 1 + i) * s, bottom, w + 2 * borders);
+        }
+    }
+}
 
 }  // namespace Yami
 

@@ -1,8 +1,9 @@
 // Av1Decoder.h -- drop-in for the reference decoder's public class (oddstone/av1dec,
-// decoder/Av1Decoder.h:47-70 and decoder/VideoFrame.h:34-48): the same names, signatures and
+// decoder/Av1Decoder.h:47-70; the frame type is VideoFrame.h's): the same names, signatures and
 // semantics, backed by the host parser (include/av1p.h) and the MI355X reconstruction
 // backend (include/av1r.h).  An application written against YamiAv1::Decoder -- like the
-// reference's own tests/Av1Dec.cpp -- rebuilds against this header and libav1r.so unchanged.
+// reference's own tests/Av1Dec.cpp -- rebuilds against this directory and libav1r.so unchanged
+// (tests/test_yami.py compiles and links it).
 //
 //   YamiAv1::Decoder decoder;                    // Decoder::Decoder (Av1Decoder.cpp:40-43)
 //   decoder.decode(data, size);                  // one temporal unit (Av1Decoder.cpp:49-109)
@@ -20,26 +21,7 @@
 #include <memory>
 #include <string>
 
-namespace Yami {
-
-// decoder/VideoFrame.h:34-48 -- an 8-bit I420 frame in host memory
-struct YuvFrame {
-    static const int MAX_PLANES = 3;
-    int64_t pts = 0;
-    int width = 0;
-    int height = 0;
-    uint8_t* data[MAX_PLANES] = {};
-    int strides[MAX_PLANES] = {};
-    int widths[MAX_PLANES] = {};
-    int heights[MAX_PLANES] = {};
-    static std::shared_ptr<YuvFrame> create(int width, int height);
-    ~YuvFrame();
-
-private:
-    uint8_t* m_buffer = nullptr;
-};
-
-}  // namespace Yami
+#include "VideoFrame.h"  // Yami::YuvFrame (decoder/VideoFrame.h:34-58)
 
 namespace YamiAv1 {
 

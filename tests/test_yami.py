@@ -12,6 +12,7 @@ VideoDecoderInterface.h:40-66, declared there and never implemented).
   the remainder of a stream exactly."""
 import hashlib
 import json
+import re
 import os
 import subprocess
 import sys
@@ -123,3 +124,36 @@ def test_gpu_yami_flush_and_seek(native_lib, tmp_path):
     # units 0 and 1 were returned before the flush (getOutput after every unit), 2 skipped
     assert len(data) == fsz * 6
     assert data[:2 * fsz] == full[:2 * fsz] and data[2 * fsz:] == full[3 * fsz:]
+
+
+REF_TREE = os.environ.get("AV1DEC_REF", "/root/reference")
+CLIENT = os.path.join(ROOT, "oracle", "_ref", "av1dec_client")
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_TREE, "tests")), reason="needs the reference tree (build container)")
+def test_reference_client_builds_unchanged(native_lib):
+    """the reference's OWN application -- tests/Av1Dec.cpp, DecodeInput.cpp,
+    DecodeOutput.cpp, md5.c, unchanged -- compiles against include/YamiAv1 (Av1Decoder.h,
+    VideoFrame.h) and links to libav1r.so (oracle/Makefile `client`, outputs in oracle/_ref)."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "client"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    syms = subprocess.run(["nm", "-C", CLIENT], capture_output=True, text=True).stdout
+    for s in ("YamiAv1::Decoder::decode(unsigned char*, unsigned long)", "YamiAv1::Decoder::getOutput()"):
+        assert s in syms, s  # resolved from libav1r.so, not from the reference's decoder
+    assert "Parser" not in syms.replace("DecodeOutput", "")  # none of the reference's decoder is linked in
+    r = subprocess.run([CLIENT], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "usage" in r.stdout  # its own command line, no device touched
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(CLIENT), reason="the reference's client is built in the build container")
+@pytest.mark.parametrize("name", ["cif_hidden", "1080p_s1"])
+def test_gpu_reference_client_matches_reference_md5(native_lib, tmp_path, name):
+    """The reference's own application, rebuilt against the drop-in, decodes a writer stream
+    to the reference decoder's MD5 (its -md5 output)."""
+    ivf = tmp_path / f"{name}.ivf"
+    ivf.write_bytes(pybsw.stream_ivf(name, seed=GOLD[name]["seed"]))
+    r = subprocess.run([CLIENT, "-i", str(ivf), "-md5"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout[-500:], r.stderr[-500:])
+    assert re.search(r"md5=([0-9a-f]{32})", r.stdout).group(1) == GOLD[name]["md5"]
