@@ -34,6 +34,7 @@ void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, un
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
+void launch_k_post(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
 void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s);
@@ -486,6 +487,9 @@ struct PackClock {
         t = n;
     }
 };
+
+// the filters fused into one kernel (av1r_set_filter_fusion; AV1R_FUSED=1)
+static std::atomic<int> g_fusedFilters{getenv("AV1R_FUSED") ? atoi(getenv("AV1R_FUSED")) : 0};
 
 // ------------------------------------------------------------------------------------
 // k_strip schedule of a deep frame (recon.hip, k_strip)
@@ -1654,22 +1658,32 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     HIPCHK(hipGetLastError());
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
-    // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place, 2 passes
-    launch_k_lf(dk, n, 0, maxUnits, st);
-    launch_k_lf(dk, n, 1, maxUnits, st);
-    if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
-    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
-    // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
-    launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
-    if (snap) {
-        frame_ref(jobs[0].C);
-        frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
-        lc->stage[AV1R_STAGE_CDEF] = jobs[0].C;
+    // ---- the in-loop filters: the three stage kernels, or fused (av1r_set_filter_fusion /
+    // AV1R_FUSED=1: k_post, deblocking -> CDEF -> loop restoration per stripe tile in LDS,
+    // straight into the output frame; measured 1.9x slower) unless the stages
+    // are kept for av1r_read_stage
+    if (g_fusedFilters.load(std::memory_order_relaxed) && !snap) {
+        launch_k_post(dk, n, maxW, maxH, st);
+        if (lc->timing)  // (the whole fused time is reported as the deblocking stage's)
+            for (int e = 2; e <= 4; e++) HIPCHK(hipEventRecord(lc->ev[e], st));
+    } else {
+        // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place, 2 passes
+        launch_k_lf(dk, n, 0, maxUnits, st);
+        launch_k_lf(dk, n, 1, maxUnits, st);
+        if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
+        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
+        // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
+        launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
+        if (snap) {
+            frame_ref(jobs[0].C);
+            frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
+            lc->stage[AV1R_STAGE_CDEF] = jobs[0].C;
+        }
+        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
+        // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
+        if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
+        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     }
-    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
-    // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
-    if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
-    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(M.done, st));
     M.pending = true;
@@ -2359,6 +2373,8 @@ int av1r_set_flow_spins(av1r_ctx* c, uint32_t spins)
 }
 
 int av1r_set_strip_levels(int levels) { return g_stripLevels.exchange(levels < 0 ? 0 : levels); }
+
+int av1r_set_filter_fusion(int on) { return g_fusedFilters.exchange(on ? 1 : 0); }
 
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream)
 {

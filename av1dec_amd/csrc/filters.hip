@@ -44,8 +44,8 @@ DEV int lf_level(const KParams& k, int row, int col, int plane, int pass)
 
 // wideFilter (LoopFilter.cpp:246-289): F[i] = Round2(sum_j tap(j) * clamp(i + j), log2Size)
 // over the 2n samples around the edge; taps are 2 for |j| <= n2, else 1.
-template <int n, int log2Size, int n2>
-DEV void lf_wide(uint8_t* c, int step)
+template <int n, int log2Size, int n2, class PX>
+DEV void lf_wide(PX* c, int step)
 {
     int v[2 * n + 2];  // v[p + n + 1] = pixel at offset p, p in [-(n + 1), n]
 #pragma unroll
@@ -65,10 +65,11 @@ DEV void lf_wide(uint8_t* c, int step)
     for (int i = -n; i < n; i++) c[step * i] = (uint8_t)F[i + n];
 }
 
-DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int blimit, int thresh, int dx, int dy, int filterSize)
+// sampleFilter (LoopFilter.cpp:145-289) at the edge pixel c (the first q sample), samples
+// `step` apart across the edge: the frame (k_lf) or an LDS tile (k_post)
+template <class PX>
+DEV void lf_filter(PX* c, int step, int plane, int limit, int blimit, int thresh, int filterSize)
 {
-    uint8_t* c = P.p + (size_t)y * P.stride + x;
-    const int step = dx + dy * P.stride;
 #define PP(k) c[-step * ((k) + 1)]
 #define QQ(k) c[step * (k)]
     int q0 = QQ(0), q1 = QQ(1), q2 = QQ(2), q3 = QQ(3);
@@ -115,6 +116,47 @@ DEV void lf_sample(const DevPlane& P, int x, int y, int plane, int limit, int bl
 #undef QQ
 }
 
+// The edge of pass `pass` (0: vertical edges, 1: horizontal) at plane position (xP, yP), a
+// multiple of 4, of plane `plane` (LoopFilter::loop_filter_edge, LoopFilter.cpp:85-126, and
+// the level / limit derivation, :301-359): false if no filter runs there, else its size
+// and limits.  Reads only the mode-info grid.
+struct LfEdge {
+    int filterSize, limit, blimit, thresh;
+};
+DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& e)
+{
+    const av1r_frame_hdr& hd = *k.hdr;
+    const int sub = plane ? 1 : 0;
+    if (plane && !hd.lf_level[plane + 1]) return false;
+    const int x = xP << sub, y = yP << sub;
+    if (x < 0 || y < 0 || x >= k.frame_w || y >= k.frame_h) return false;
+    if (!pass && !x) return false;
+    if (pass && !y) return false;
+    const int dx = pass == 0, dy = pass == 1;
+    const int row = (y >> 2) | sub, col = (x >> 2) | sub;
+    const int prevRow = row - (dy << sub), prevCol = col - (dx << sub);
+    const av1r_mi& info = mi_at(k, row, col);
+    const int txSz = info.lf_tx[plane];
+    const int psz = plane_bsize(info.mi_size, plane);
+    const int skip = info.flags & AV1R_MI_SKIP;
+    const int isIntra = info.ref_frame[0] <= AV1R_INTRA_FRAME;
+    const int prevTx = mi_at(k, prevRow, prevCol).lf_tx[plane];
+    const int isBlockEdge = !pass ? !(xP % (av1r_num4x4w[psz] * 4)) : !(yP % (av1r_num4x4h[psz] * 4));
+    const int isTxEdge = !pass ? !(xP % av1r_tx_w[txSz]) : !(yP % av1r_tx_h[txSz]);
+    if (!(isTxEdge && (isBlockEdge || !skip || isIntra))) return false;
+    const int base = !pass ? imin(av1r_tx_w[prevTx], av1r_tx_w[txSz]) : imin(av1r_tx_h[prevTx], av1r_tx_h[txSz]);
+    e.filterSize = !plane ? imin(16, base) : imin(8, base);
+    int lvl = lf_level(k, row, col, plane, pass);
+    if (!lvl) lvl = lf_level(k, prevRow, prevCol, plane, pass);
+    if (lvl <= 0) return false;
+    const int sharp = hd.lf_sharpness;
+    const int shift = sharp > 4 ? 2 : (sharp > 0 ? 1 : 0);
+    e.limit = sharp > 0 ? CLIP3(1, 9 - sharp, lvl >> shift) : imax(1, lvl >> shift);
+    e.blimit = 2 * (lvl + 2) + e.limit;
+    e.thresh = lvl >> 4;
+    return true;
+}
+
 // one lane per (plane, 4x4 unit) edge of pass `pass`
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass)
 {
@@ -122,7 +164,6 @@ extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int p
     const KParams& k = KP(kps, wg.y);  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
     if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
-    const int planeMask = 1 | (hd.lf_level[2] ? 2 : 0) | (hd.lf_level[3] ? 4 : 0);
     const int nY = k.mi_rows * k.mi_cols;
     const int cCols = (k.mi_cols + 1) / 2, nC = ((k.mi_rows + 1) / 2) * cCols;
     int id = wg.x * blockDim.x + threadIdx.x;
@@ -141,37 +182,15 @@ extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int p
     } else {
         return;
     }
-    if (!((planeMask >> plane) & 1)) return;
     const int sub = plane ? 1 : 0;
-    const int dx = pass == 0, dy = pass == 1;
-    const int x = col0 * 4, y = row0 * 4;
-    const int row = row0 | sub, col = col0 | sub;
-    if (x >= k.frame_w || y >= k.frame_h) return;
-    if (!pass && !x) return;
-    if (pass && !y) return;
-    const int xP = x >> sub, yP = y >> sub;
-    const int prevRow = row - (dy << sub), prevCol = col - (dx << sub);
-    const av1r_mi& info = mi_at(k, row, col);
-    const int txSz = info.lf_tx[plane];
-    const int psz = plane_bsize(info.mi_size, plane);
-    const int skip = info.flags & AV1R_MI_SKIP;
-    const int isIntra = info.ref_frame[0] <= AV1R_INTRA_FRAME;
-    const int prevTx = mi_at(k, prevRow, prevCol).lf_tx[plane];
-    const int isBlockEdge = !pass ? !(xP % (av1r_num4x4w[psz] * 4)) : !(yP % (av1r_num4x4h[psz] * 4));
-    const int isTxEdge = !pass ? !(xP % av1r_tx_w[txSz]) : !(yP % av1r_tx_h[txSz]);
-    if (!(isTxEdge && (isBlockEdge || !skip || isIntra))) return;
-    const int base = !pass ? imin(av1r_tx_w[prevTx], av1r_tx_w[txSz]) : imin(av1r_tx_h[prevTx], av1r_tx_h[txSz]);
-    const int filterSize = !plane ? imin(16, base) : imin(8, base);
-    int lvl = lf_level(k, row, col, plane, pass);
-    if (!lvl) lvl = lf_level(k, prevRow, prevCol, plane, pass);
-    if (lvl <= 0) return;
-    const int sharp = k.hdr->lf_sharpness;
-    const int shift = sharp > 4 ? 2 : (sharp > 0 ? 1 : 0);
-    const int limit = sharp > 0 ? CLIP3(1, 9 - sharp, lvl >> shift) : imax(1, lvl >> shift);
-    const int blimit = 2 * (lvl + 2) + limit;
-    const int thresh = lvl >> 4;
+    const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
+    LfEdge e;
+    if (!lf_edge(k, plane, pass, xP, yP, e)) return;
     const DevPlane& P = k.cur.pl[plane];
-    for (int i = 0; i < 4; i++) lf_sample(P, xP + dy * i, yP + dx * i, plane, limit, blimit, thresh, dx, dy, filterSize);
+    const int dx = pass == 0, dy = pass == 1;
+    const int step = dx + dy * P.stride;
+    for (int i = 0; i < 4; i++)
+        lf_filter(P.p + (size_t)(yP + dx * i) * P.stride + xP + dy * i, step, plane, e.limit, e.blimit, e.thresh, e.filterSize);
 }
 
 // ------------------------------------------------------------------------------------
@@ -209,10 +228,10 @@ struct CdefLds {
 
 // partial[d][k] of cdefDirection (Cdef.cpp:203-261) for one line k of direction d, summed
 // over the 8x8 block at (bx, by) of the staged luma tile
-template <int d>
-DEV int cdef_cost(const CdefLds& L, int bx, int by)
+template <int d, class PX>
+DEV int cdef_cost(const PX* blk, int ts)  // blk: the block's top-left pixel in a tile of row stride ts
 {
-    auto px8 = [&](int i, int j) { return (int)L.y[CD_H + by + i][CD_X + bx + j] - 128; };
+    auto px8 = [&](int i, int j) { return (int)blk[i * ts + j] - 128; };
     int cost = 0;
     if (d == 2 || d == 6) {
 #pragma unroll
@@ -408,14 +427,14 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
             const int bx = (b & 7) * 8, by = (b >> 3) * 8;
             int c;
             switch (d) {
-            case 0: c = cdef_cost<0>(L, bx, by); break;
-            case 1: c = cdef_cost<1>(L, bx, by); break;
-            case 2: c = cdef_cost<2>(L, bx, by); break;
-            case 3: c = cdef_cost<3>(L, bx, by); break;
-            case 4: c = cdef_cost<4>(L, bx, by); break;
-            case 5: c = cdef_cost<5>(L, bx, by); break;
-            case 6: c = cdef_cost<6>(L, bx, by); break;
-            default: c = cdef_cost<7>(L, bx, by); break;
+            case 0: c = cdef_cost<0>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            case 1: c = cdef_cost<1>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            case 2: c = cdef_cost<2>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            case 3: c = cdef_cost<3>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            case 4: c = cdef_cost<4>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            case 5: c = cdef_cost<5>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            case 6: c = cdef_cost<6>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            default: c = cdef_cost<7>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
             }
             L.cost[b][d] = c;
         }
@@ -600,93 +619,15 @@ DEV void sgr_ab_lds(const LrLds& L, int si, int sj, int r, int set, int pass, in
     sgr_ab_fin(a, b, r, set, pass, A, B);
 }
 
-// one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
-// frame (k.cdef) and the deblocked frame (k.cur, stripe rows), writes k.lrout.
-extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
+// LoopRestoration's filters over one staged tile (L.src, L.unit ready; the caller's
+// barrier after staging): Wiener (LoopRestoration.cpp:247-277) and self-guided (:284-479),
+// rows [ty0, ty0 + th) x columns [x0, x0 + tw) of plane `plane`, written to O.  y0: the
+// stripe's first row (forEachBlock's y); us / cols / uc0 / nU: unit size, unit columns of the
+// plane, the tile's first unit column and its unit count.
+DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, int tw, int ty0, int th, int y0, int us,
+    int cols, int uc0, int nU, int planeEndX, int planeEndY, const DevPlane& O)
 {
-    __shared__ LrLds L;
     const int t = threadIdx.x;
-#ifndef AV1R_LR_XCD  // XCD order for k_lr: 4K LR 0.080 -> 0.108 ms/frame (1080p unchanged), though
-#define AV1R_LR_XCD 0   // its fabric traffic fell 16.7 -> 6.7 MB/frame: measured, so off
-#endif
-#if AV1R_LR_XCD
-    const uint3 wg = xcd_block_xy();  // (per slice: chroma slices are half empty)
-#else
-    const uint3 wg = make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
-#endif
-    const KParams& k = KP(kps, wg.z / 3);
-    if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
-    const int plane = wg.z % 3, sub = plane ? 1 : 0;
-    const DevPlane C = k.cdef.pl[plane];
-    const DevPlane O = k.lrout.pl[plane];
-    const int x0 = wg.x * LR_TW;
-    if (x0 >= C.w) return;
-    const int stripeH = 64 >> sub, off = 8 >> sub;
-    const int perStripe = stripeH / LR_TH;
-    const int sNum = wg.y / perStripe, half = wg.y - sNum * perStripe;
-    LrPix S;
-    S.cdefP = C;
-    S.preP = k.cur.pl[plane];
-    S.start = sNum * stripeH - off;
-    S.end = S.start + stripeH;
-    const int ty0 = imax(0, S.start + half * LR_TH), ty1 = imin(S.start + (half + 1) * LR_TH, C.h);
-    if (ty0 >= ty1) return;
-    const int tw = imin(LR_TW, C.w - x0), th = ty1 - ty0;
-    const av1r_frame_hdr& h = *k.hdr;
-    if (h.lr_type[plane] == AV1R_RESTORE_NONE) {
-        for (int q = t; q < tw * th; q += 256) {
-            int r = q / tw, c = q - r * tw;
-            O.p[(size_t)(ty0 + r) * O.stride + x0 + c] = C.p[(size_t)(ty0 + r) * C.stride + x0 + c];
-        }
-        return;
-    }
-    const int us = h.lr_unit_size[plane];
-    const int rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
-    const int planeEndX = r2(k.frame_w, sub), planeEndY = r2(k.frame_h, sub);
-    const int ur = imin((ty0 + off) / us, rows - 1);  // one unit row per stripe
-    const int uc0 = imin(x0 / us, cols - 1);
-    const int nU = imin((x0 + tw - 1) / us, cols - 1) - uc0 + 1;
-    if (t < nU) L.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
-    const int y0 = imax(S.start, 0);  // forEachBlock's y: the stripe's first row
-    // stage the source rows ty0-3 .. ty1+2, cols x0-4 .. x0+67 (L.src[i][j]: x = x0 - 4 + j):
-    // aligned dwords where no column needs clamping, else bytes; every lane's loads are
-    // issued before its LDS stores
-    if (x0 >= 4 && x0 + LR_SW - 4 <= C.w) {
-        constexpr int ND = LR_SW / 4, NQ = ((LR_TH + 6) * ND + 255) / 256;
-        uint32_t v[NQ];
-#pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int q = t + 256 * u, i = q / ND, d = q - i * ND;
-            if (i < th + 6) {
-                int y = ty0 - 3 + i;  // get_source_sample's row mapping
-                const bool pre = y < S.start || y >= S.end;
-                if (y < S.start) y = imax(S.start - 2, y);
-                else if (y >= S.end) y = imin(S.end + 1, y);
-                y = CLIP3(0, C.h - 1, y);
-                const uint8_t* row = (pre ? S.preP.p : C.p) + (size_t)y * (pre ? S.preP.stride : C.stride);
-                v[u] = *reinterpret_cast<const uint32_t*>(row + x0 - 4 + 4 * d);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int q = t + 256 * u, i = q / ND, d = q - i * ND;
-            if (i < th + 6) *reinterpret_cast<uint32_t*>(&L.src[i][4 * d]) = v[u];
-        }
-    } else {
-        constexpr int NQ = ((LR_TH + 6) * LR_SW + 255) / 256;
-        uint8_t v[NQ];
-#pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int q = t + 256 * u, i = q / LR_SW, j = q - i * LR_SW;
-            if (i < th + 6) v[u] = (uint8_t)lr_src(S, x0 - 4 + j, ty0 - 3 + i);
-        }
-#pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int q = t + 256 * u, i = q / LR_SW, j = q - i * LR_SW;
-            if (i < th + 6) L.src[i][j] = v[u];
-        }
-    }
-    __syncthreads();
     int anyW = 0, anyS = 0;
     for (int u = 0; u < nU; u++) {
         anyW |= L.unit[u].type == AV1R_RESTORE_WIENER;
@@ -814,6 +755,383 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
             O.p[(size_t)y * O.stride + x] = (uint8_t)outv;
         }
     }
+}
+
+// one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
+// frame (k.cdef) and the deblocked frame (k.cur, stripe rows), writes k.lrout.
+extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
+{
+    __shared__ LrLds L;
+    const int t = threadIdx.x;
+#ifndef AV1R_LR_XCD  // XCD order for k_lr: 4K LR 0.080 -> 0.108 ms/frame (1080p unchanged), though
+#define AV1R_LR_XCD 0   // its fabric traffic fell 16.7 -> 6.7 MB/frame: measured, so off
+#endif
+#if AV1R_LR_XCD
+    const uint3 wg = xcd_block_xy();  // (per slice: chroma slices are half empty)
+#else
+    const uint3 wg = make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
+#endif
+    const KParams& k = KP(kps, wg.z / 3);
+    if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
+    const int plane = wg.z % 3, sub = plane ? 1 : 0;
+    const DevPlane C = k.cdef.pl[plane];
+    const DevPlane O = k.lrout.pl[plane];
+    const int x0 = wg.x * LR_TW;
+    if (x0 >= C.w) return;
+    const int stripeH = 64 >> sub, off = 8 >> sub;
+    const int perStripe = stripeH / LR_TH;
+    const int sNum = wg.y / perStripe, half = wg.y - sNum * perStripe;
+    LrPix S;
+    S.cdefP = C;
+    S.preP = k.cur.pl[plane];
+    S.start = sNum * stripeH - off;
+    S.end = S.start + stripeH;
+    const int ty0 = imax(0, S.start + half * LR_TH), ty1 = imin(S.start + (half + 1) * LR_TH, C.h);
+    if (ty0 >= ty1) return;
+    const int tw = imin(LR_TW, C.w - x0), th = ty1 - ty0;
+    const av1r_frame_hdr& h = *k.hdr;
+    if (h.lr_type[plane] == AV1R_RESTORE_NONE) {
+        for (int q = t; q < tw * th; q += 256) {
+            int r = q / tw, c = q - r * tw;
+            O.p[(size_t)(ty0 + r) * O.stride + x0 + c] = C.p[(size_t)(ty0 + r) * C.stride + x0 + c];
+        }
+        return;
+    }
+    const int us = h.lr_unit_size[plane];
+    const int rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
+    const int planeEndX = r2(k.frame_w, sub), planeEndY = r2(k.frame_h, sub);
+    const int ur = imin((ty0 + off) / us, rows - 1);  // one unit row per stripe
+    const int uc0 = imin(x0 / us, cols - 1);
+    const int nU = imin((x0 + tw - 1) / us, cols - 1) - uc0 + 1;
+    if (t < nU) L.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
+    const int y0 = imax(S.start, 0);  // forEachBlock's y: the stripe's first row
+    // stage the source rows ty0-3 .. ty1+2, cols x0-4 .. x0+67 (L.src[i][j]: x = x0 - 4 + j):
+    // aligned dwords where no column needs clamping, else bytes; every lane's loads are
+    // issued before its LDS stores
+    if (x0 >= 4 && x0 + LR_SW - 4 <= C.w) {
+        constexpr int ND = LR_SW / 4, NQ = ((LR_TH + 6) * ND + 255) / 256;
+        uint32_t v[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / ND, d = q - i * ND;
+            if (i < th + 6) {
+                int y = ty0 - 3 + i;  // get_source_sample's row mapping
+                const bool pre = y < S.start || y >= S.end;
+                if (y < S.start) y = imax(S.start - 2, y);
+                else if (y >= S.end) y = imin(S.end + 1, y);
+                y = CLIP3(0, C.h - 1, y);
+                const uint8_t* row = (pre ? S.preP.p : C.p) + (size_t)y * (pre ? S.preP.stride : C.stride);
+                v[u] = *reinterpret_cast<const uint32_t*>(row + x0 - 4 + 4 * d);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / ND, d = q - i * ND;
+            if (i < th + 6) *reinterpret_cast<uint32_t*>(&L.src[i][4 * d]) = v[u];
+        }
+    } else {
+        constexpr int NQ = ((LR_TH + 6) * LR_SW + 255) / 256;
+        uint8_t v[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / LR_SW, j = q - i * LR_SW;
+            if (i < th + 6) v[u] = (uint8_t)lr_src(S, x0 - 4 + j, ty0 - 3 + i);
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int q = t + 256 * u, i = q / LR_SW, j = q - i * LR_SW;
+            if (i < th + 6) L.src[i][j] = v[u];
+        }
+    }
+    __syncthreads();
+    lr_filter_tile(L, h, plane, x0, tw, ty0, th, y0, us, cols, uc0, nU, planeEndX, planeEndY, O);
+}
+
+// ------------------------------------------------------------------------------------
+// k_post: deblocking -> CDEF -> loop restoration fused, one workgroup per (frame, 64-row
+// loop-restoration stripe, 64 luma columns) with its two chroma tiles.  The reference runs
+// the three filters frame after frame (Av1Decoder.cpp:171-192: LoopFilter::filter, then
+// Cdef::filter into a new frame, Cdef.cpp:43, then LoopRestoration::filter into another,
+// LoopRestoration.cpp:191-219); here the reconstructed pixels the tile needs are read once
+// into LDS, deblocked there (both passes, LoopFilter.cpp:40-126), CDEF'd into LDS
+// (Cdef.cpp:72-198) and restored (LoopRestoration.cpp:136-479) straight to the output
+// frame: neither the deblocked nor the CDEF frame exists in memory.
+//
+// Geometry (luma; chroma the same at half size, with its shorter filters).  Stripe k covers
+// rows [s0, s0 + 64), s0 = 64k - 8 (LoopRestoration.cpp:136-189).  Loop restoration of the
+// tile reads the source 3 pixels around it: CDEF output inside the stripe, deblocked rows
+// s0 - 2, s0 - 1, s0 + 64, s0 + 65 outside it (get_source_sample, :234-246).  CDEF of the
+// 4-pixel groups x0 - 4 .. x0 + 67 over the stripe's rows works on the 8x8 blocks x0 - 8 ..
+// x0 + 71 (direction search per block) and reads deblocked pixels 2 around them.  Those are
+// the output of the horizontal-edge pass at edges s0 - 4 .. s0 + 68 (a 16-wide filter
+// writes 6 and reads 7 rows on each side), which reads the vertical-edge pass's output over
+// rows s0 - 11 .. s0 + 74; the vertical edges x0 - 8 .. x0 + 72 that write the columns
+// needed read x0 - 15 .. x0 + 78.  So the tile stages reconstructed rows [s0 - 12, s0 + 76)
+// x columns [x0 - 16, x0 + 80) (chroma: [cs0 - 4, cs0 + 36) x [cx0 - 8, cx0 + 40)) and runs
+// every edge of each pass that touches them; a pass's edges never overlap (the filter lengths
+// are bounded by the transform sizes on both sides), exactly as on the whole frame.
+// Recomputed halo: 1.9x the tile's deblocking, 1.25x its CDEF; no frame round trips.
+// ------------------------------------------------------------------------------------
+#define PY_R 88   // luma: rows s0 - 12 .. s0 + 75
+#define PY_C 96   // luma: columns x0 - 16 .. x0 + 79
+#define PY_OY 12
+#define PY_OX 16
+#define PC_R 40   // chroma: rows cs0 - 4 .. cs0 + 35
+#define PC_C 48   // chroma: columns cx0 - 8 .. cx0 + 39
+#define PC_OY 4
+#define PC_OX 8
+#define PO_YC 72  // CDEF output, luma: columns x0 - 4 .. x0 + 67, rows s0 .. s0 + 63
+#define PO_CC 40  // chroma: columns cx0 - 4 .. cx0 + 35, rows cs0 .. cs0 + 31
+#define PB_X 10   // 8x8 luma blocks: columns x0 - 8 .. x0 + 71
+#define PB (PB_X * 8)
+struct PostLds {
+    uint8_t y[PY_R][PY_C];
+    uint8_t uv[2][PC_R][PC_C];
+    uint8_t oy[64][PO_YC];
+    uint8_t ouv[2][32][PO_CC];
+    int cost[PB][8];
+    int16_t pri[PB];
+    int8_t idx[PB];
+    uint8_t filt[PB];
+    int16_t offY[PB][6], offC[PB][6];
+    LrLds lr;
+};
+
+// stage rows [y0, y0 + nr) x columns [x0, x0 + nc) (nc a multiple of 4, x0 of 4) of plane P
+// into t (row stride ts): dwords where the row and columns lie inside [0, mx] x [0, my] (the
+// mi grid), else bytes with clamped coordinates (never read by a filter that runs)
+DEV void post_stage(uint8_t* t, int ts, int nr, int nc, const DevPlane& P, int x0, int y0, int mx, int my)
+{
+    const int nd = nc / 4;
+    for (int q = threadIdx.x; q < nr * nd; q += 256) {
+        const int i = q / nd, d = q - i * nd;
+        const int y = y0 + i, x = x0 + 4 * d;
+        uint32_t v;
+        if (y >= 0 && y <= my && x >= 0 && x + 3 <= mx) {
+            v = *reinterpret_cast<const uint32_t*>(P.p + (size_t)y * P.stride + x);
+        } else {
+            const int yy = CLIP3(0, my, y);
+            v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) v |= (uint32_t)px(P, CLIP3(0, mx, x + b), yy) << (8 * b);
+        }
+        *reinterpret_cast<uint32_t*>(t + i * ts + 4 * d) = v;
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_post(const KParams* kps)
+{
+    __shared__ PostLds L;
+    const int t = threadIdx.x;
+    const uint3 wg = xcd_block();  // x: 64-column tile, y: stripe, z: frame
+    const KParams& k = KP(kps, wg.z);
+    const av1r_frame_hdr& h = *k.hdr;
+    const int x0 = (int)wg.x * 64, s0 = (int)wg.y * 64 - 8;
+    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
+    if (x0 >= k.frame_w || imax(s0, 0) >= k.frame_h) return;
+    const int cx0 = x0 >> 1, cs0 = s0 >> 1, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
+    // ---- the reconstructed pixels
+    post_stage(&L.y[0][0], PY_C, PY_R, PY_C, k.cur.pl[0], x0 - PY_OX, s0 - PY_OY, limX - 1, limY - 1);
+    for (int pl = 0; pl < 2; pl++)
+        post_stage(&L.uv[pl][0][0], PC_C, PC_R, PC_C, k.cur.pl[1 + pl], cx0 - PC_OX, cs0 - PC_OY, climX - 1, climY - 1);
+    // ---- CDEF's per-block parameters (mode info only: overlaps the staging loads)
+    if (t < PB) {
+        const int bx = x0 - 8 + 8 * (t % PB_X), by = s0 + 8 * (t / PB_X);
+        int idx = -1, f = 0;
+        if (bx >= 0 && by >= 0 && bx < limX && by < limY) {
+            idx = k.cdef_idx[(by >> 6) * h.cdef_cols + (bx >> 6)];
+            const int br = by >> 2, bc = bx >> 2;
+            // cdef_block's skip test (Cdef.cpp:79-82)
+            f = idx != -1 && !((mi_at(k, br, bc).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc).flags & AV1R_MI_SKIP)
+                && (mi_at(k, br, bc + 1).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc + 1).flags & AV1R_MI_SKIP));
+        }
+        L.idx[t] = (int8_t)idx;
+        L.filt[t] = (uint8_t)f;
+    }
+    __syncthreads();
+    // ---- deblocking, both passes over the staged tiles (LoopFilter::filter, LoopFilter.cpp:40-58)
+    if (h.lf_level[0] || h.lf_level[1]) {
+        for (int pass = 0; pass < 2; pass++) {
+            // pass 0: luma edge columns x0 - 8 .. x0 + 72 (21) x 4-row units s0 - 12 .. s0 + 72 (22);
+            //         chroma edge columns cx0 - 4 .. cx0 + 36 (11) x 4-row units cs0 - 4 .. cs0 + 32 (10)
+            // pass 1: luma edge rows s0 - 4 .. s0 + 68 (19) x 4-column units x0 - 8 .. x0 + 68 (20);
+            //         chroma edge rows cs0 .. cs0 + 32 (9) x 4-column units cx0 - 8 .. cx0 + 36 (12)
+            const int nEy = pass ? 19 : 21, nUy = pass ? 20 : 22;
+            const int nEc = pass ? 9 : 11, nUc = pass ? 12 : 10;
+            const int nY = nEy * nUy, nT = nY + 2 * nEc * nUc;
+            for (int q = t; q < nT; q += 256) {
+                int plane, e, u;
+                if (q < nY) {
+                    plane = 0;
+                    e = q / nUy;
+                    u = q - e * nUy;
+                } else {
+                    const int r = q - nY;
+                    plane = 1 + (r >= nEc * nUc);
+                    const int r2 = r - (plane - 1) * nEc * nUc;
+                    e = r2 / nUc;
+                    u = r2 - e * nUc;
+                }
+                int xP, yP;
+                if (!plane) {
+                    xP = pass ? x0 - 8 + 4 * u : x0 - 8 + 4 * e;
+                    yP = pass ? s0 - 4 + 4 * e : s0 - 12 + 4 * u;
+                } else {
+                    xP = pass ? cx0 - 8 + 4 * u : cx0 - 4 + 4 * e;
+                    yP = pass ? cs0 + 4 * e : cs0 - 4 + 4 * u;
+                }
+                LfEdge ed;
+                if (!lf_edge(k, plane, pass, xP, yP, ed)) continue;
+                uint8_t* tile = plane ? &L.uv[plane - 1][0][0] : &L.y[0][0];
+                const int ts = plane ? PC_C : PY_C;
+                uint8_t* c = plane ? tile + (yP - cs0 + PC_OY) * ts + (xP - cx0 + PC_OX)
+                                   : tile + (yP - s0 + PY_OY) * ts + (xP - x0 + PY_OX);
+                const int step = pass ? ts : 1, along = pass ? 1 : ts;
+                for (int i = 0; i < 4; i++) lf_filter(c + along * i, step, plane, ed.limit, ed.blimit, ed.thresh, ed.filterSize);
+            }
+            __syncthreads();
+        }
+    }
+    // ---- CDEF direction search (cdefDirection, Cdef.cpp:203-261): one lane per (block, direction)
+    for (int q = t; q < PB * 8; q += 256) {
+        const int b = q >> 3, d = q & 7;
+        if (!L.filt[b]) continue;
+        const uint8_t* blk = &L.y[PY_OY + 8 * (b / PB_X)][PY_OX - 8 + 8 * (b % PB_X)];
+        int c;
+        switch (d) {
+        case 0: c = cdef_cost<0>(blk, PY_C); break;
+        case 1: c = cdef_cost<1>(blk, PY_C); break;
+        case 2: c = cdef_cost<2>(blk, PY_C); break;
+        case 3: c = cdef_cost<3>(blk, PY_C); break;
+        case 4: c = cdef_cost<4>(blk, PY_C); break;
+        case 5: c = cdef_cost<5>(blk, PY_C); break;
+        case 6: c = cdef_cost<6>(blk, PY_C); break;
+        default: c = cdef_cost<7>(blk, PY_C); break;
+        }
+        L.cost[b][d] = c;
+    }
+    __syncthreads();
+    if (t < PB && L.filt[t]) {
+        int best = 0, yDir = 0;
+        for (int d = 0; d < 8; d++)
+            if (L.cost[t][d] > best) {
+                best = L.cost[t][d];
+                yDir = d;
+            }
+        const int idx = L.idx[t];
+        const int var = (best - L.cost[t][(yDir + 4) & 7]) >> 10;
+        const int priStr = h.cdef_y_pri[idx];
+        const int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
+        L.pri[t] = (int16_t)(var ? (priStr * (4 + varStr) + 8) >> 4 : 0);
+        const int dy0 = priStr == 0 ? 0 : yDir, dc0 = h.cdef_uv_pri[idx] == 0 ? 0 : av1r_cdef_uv_dir420[yDir];
+#pragma unroll
+        for (int s = 0; s < 3; s++)
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                const int dl = s == 0 ? dy0 : ((dy0 + (s == 1 ? -2 : 2)) & 7);
+                const int dc = s == 0 ? dc0 : ((dc0 + (s == 1 ? -2 : 2)) & 7);
+                L.offY[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dl][kk][0] * PY_C + av1r_cdef_directions[dl][kk][1]);
+                L.offC[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dc][kk][0] * PC_C + av1r_cdef_directions[dc][kk][1]);
+            }
+    }
+    __syncthreads();
+    // ---- CDEF filter (cdefFilter, Cdef.cpp:158-198): luma 4-pixel groups x0 - 4 .. x0 + 64
+    // over the stripe's rows, chroma groups cx0 - 4 .. cx0 + 32 (unfiltered blocks: copied)
+    for (int q = t; q < 64 * 18 + 2 * 32 * 10; q += 256) {
+        int plane, r, x, y;
+        if (q < 64 * 18) {
+            plane = 0;
+            r = q / 18;
+            x = x0 - 4 + 4 * (q - r * 18);
+            y = s0 + r;
+            if (x < 0 || x >= limX || y < 0 || y >= limY) continue;
+        } else {
+            const int e = q - 64 * 18;
+            plane = 1 + (e >= 320);
+            const int e2 = e - (plane - 1) * 320;
+            r = e2 / 10;
+            x = cx0 - 4 + 4 * (e2 - r * 10);
+            y = cs0 + r;
+            if (x < 0 || x >= climX || y < 0 || y >= climY) continue;
+        }
+        const int sub = plane ? 1 : 0;
+        const int b = (r >> (3 - sub)) * PB_X + ((x - ((x0 - 8) >> sub)) >> (3 - sub));
+        const uint8_t* tile = plane ? &L.uv[plane - 1][0][0] : &L.y[0][0];
+        const int ts = plane ? PC_C : PY_C;
+        const int p = plane ? (y - cs0 + PC_OY) * ts + (x - cx0 + PC_OX) : (y - s0 + PY_OY) * ts + (x - x0 + PY_OX);
+        const int mx = plane ? climX : limX, my = plane ? climY : limY;
+        uint32_t o;
+        if (!L.filt[b]) {
+            o = *reinterpret_cast<const uint32_t*>(tile + p);
+        } else {
+            const int idx = L.idx[b];
+            const int pri = plane ? h.cdef_uv_pri[idx] : L.pri[b];
+            const int sec = plane ? h.cdef_uv_sec[idx] : h.cdef_y_sec[idx];
+            const int damping = h.cdef_damping - sub;
+            const int16_t* off = plane ? L.offC[b] : L.offY[b];
+            if (x < CD_H || y < CD_H || x + 4 + CD_H > mx || y + CD_H >= my)
+                o = cdef_quad<true>(tile, p, off, pri, sec, damping, x, y, ts, mx, my);
+            else
+                o = cdef_quad<false>(tile, p, off, pri, sec, damping, 0, 0, ts, 0, 0);
+        }
+        uint8_t* dst = plane ? &L.ouv[plane - 1][r][x - cx0 + 4] : &L.oy[r][x - x0 + 4];
+        *reinterpret_cast<uint32_t*>(dst) = o;
+    }
+    __syncthreads();
+    // ---- loop restoration (or the CDEF output itself) into the output frame
+    for (int plane = 0; plane < 3; plane++) {
+        const int sub = plane ? 1 : 0;
+        const DevPlane O = h.uses_lr ? k.lrout.pl[plane] : k.cdef.pl[plane];
+        const int Wp = O.w, Hp = O.h;
+        const int px0 = x0 >> sub, start = s0 >> sub, stripeH = 64 >> sub;
+        const int tw = imin(64 >> sub, Wp - px0);
+        if (tw <= 0) continue;
+        const uint8_t* cd = plane ? &L.ouv[plane - 1][0][0] : &L.oy[0][0];  // CDEF output, rows from start
+        const int cs = plane ? PO_CC : PO_YC;
+        if (!h.uses_lr || h.lr_type[plane] == AV1R_RESTORE_NONE) {
+            const int r0 = imax(start, 0), r1 = imin(start + stripeH, Hp);
+            for (int q = t; q < (r1 - r0) * tw; q += 256) {
+                const int i = q / tw, c = q - i * tw;
+                O.p[(size_t)(r0 + i) * O.stride + px0 + c] = cd[(r0 + i - start) * cs + c + 4];
+            }
+            continue;
+        }
+        const uint8_t* db = plane ? &L.uv[plane - 1][0][0] : &L.y[0][0];  // deblocked
+        const int dbs = plane ? PC_C : PY_C, dby = plane ? cs0 - PC_OY : s0 - PY_OY, dbx = plane ? cx0 - PC_OX : x0 - PY_OX;
+        const int us = h.lr_unit_size[plane];
+        const int rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
+        const int planeEndX = r2(k.frame_w, sub), planeEndY = r2(k.frame_h, sub);
+        const int off = 8 >> sub, end = start + stripeH;
+        for (int half = 0; half < stripeH / LR_TH; half++) {
+            const int ty0 = imax(0, start + half * LR_TH), ty1 = imin(start + (half + 1) * LR_TH, Hp);
+            if (ty0 >= ty1) continue;
+            const int th = ty1 - ty0;
+            const int ur = imin((ty0 + off) / us, rows - 1);
+            const int uc0 = imin(px0 / us, cols - 1);
+            const int nU = imin((px0 + tw - 1) / us, cols - 1) - uc0 + 1;
+            if (t < nU) L.lr.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
+            // the source (get_source_sample, LoopRestoration.cpp:234-246, with extendBorder(3)
+            // as clamping): CDEF output inside the stripe, deblocked rows outside it
+            for (int q = t; q < (th + 6) * (tw + 8); q += 256) {
+                const int i = q / (tw + 8), j = q - i * (tw + 8);
+                int y = ty0 - 3 + i;
+                const bool pre = y < start || y >= end;
+                if (y < start) y = imax(start - 2, y);
+                else if (y >= end) y = imin(end + 1, y);
+                y = CLIP3(0, Hp - 1, y);
+                const int x = CLIP3(0, Wp - 1, px0 - 4 + j);
+                L.lr.src[i][j] = pre ? db[(y - dby) * dbs + (x - dbx)] : cd[(y - start) * cs + (x - px0 + 4)];
+            }
+            __syncthreads();
+            lr_filter_tile(L.lr, h, plane, px0, tw, ty0, th, imax(start, 0), us, cols, uc0, nU, planeEndX, planeEndY, O);
+            __syncthreads();  // L.lr is staged again by the next half / plane
+        }
+    }
+}
+
+void launch_k_post(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_post, dim3((maxW + 63) / 64, (maxH + 8 + 63) / 64, n), dim3(256), 0, s, kps);
 }
 
 // The launch metadata, copied by the compute queue itself from pinned host memory (the

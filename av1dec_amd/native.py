@@ -192,6 +192,7 @@ def lib():
     l.av1r_set_flow_spins.argtypes = [vp, C.c_uint32]
     l.av1r_flow_debug.argtypes = [C.POINTER(C.c_uint32), i, i, C.POINTER(i)]
     l.av1r_set_strip_levels.argtypes = [i]
+    l.av1r_set_filter_fusion.argtypes = [i]
     l.av1r_pack.argtypes = [vp, C.POINTER(vp)]
     l.av1r_packed_free.argtypes = [vp]
     l.av1r_packed_free.restype = None
@@ -236,5 +237,79 @@ EXPORTS = [
     "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug", "av1r_pack", "av1r_packed_free",
     "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy", "av1r_pack_profile",
     "av1r_pipeline_run", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
-    "av1r_set_strip_levels",
+    "av1r_set_strip_levels", "av1r_set_filter_fusion",
 ]
+
+
+_hip = None
+
+
+def hip():
+    """The HIP runtime libav1r.so itself is linked to (ctypes), for the measurement helpers
+    below: torch carries its own runtime, which cannot share a process with this one."""
+    global _hip
+    if _hip is None:
+        lib()  # loads libamdhip64 as a dependency of libav1r.so
+        h = C.CDLL("libamdhip64.so.7")
+        vp = C.c_void_p
+        h.hipHostMalloc.argtypes = [C.POINTER(vp), C.c_size_t, C.c_uint]
+        h.hipHostFree.argtypes = [vp]
+        h.hipMalloc.argtypes = [C.POINTER(vp), C.c_size_t]
+        h.hipFree.argtypes = [vp]
+        h.hipMemcpy.argtypes = [vp, vp, C.c_size_t, C.c_int]
+        h.hipEventCreate.argtypes = [C.POINTER(vp)]
+        h.hipEventRecord.argtypes = [vp, vp]
+        h.hipEventSynchronize.argtypes = [vp]
+        h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), vp, vp]
+        h.hipEventDestroy.argtypes = [vp]
+        h.hipMemcpyAsync.argtypes = [vp, vp, C.c_size_t, C.c_int, vp]
+        h.hipSetDevice.argtypes = [C.c_int]
+        h.hipDeviceSynchronize.argtypes = []
+        _hip = h
+    return _hip
+
+
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc) of `n` bytes."""
+
+    def __init__(self, n):
+        self.n = n
+        self.ptr = C.c_void_p()
+        if hip().hipHostMalloc(C.byref(self.ptr), n, 0) != 0:
+            raise MemoryError(f"hipHostMalloc({n})")
+
+    def close(self):
+        if self.ptr:
+            hip().hipHostFree(self.ptr)
+            self.ptr = C.c_void_p()
+
+
+def copy_peak_gbps(device=0, nbytes=1 << 30, reps=10):
+    """Device-to-device copy rate (read + write bytes / s, best of `reps`, HIP events)."""
+    h = hip()
+    h.hipSetDevice(device)
+    a, b = C.c_void_p(), C.c_void_p()
+    if h.hipMalloc(C.byref(a), nbytes) or h.hipMalloc(C.byref(b), nbytes):
+        raise MemoryError("hipMalloc")
+    e0, e1 = C.c_void_p(), C.c_void_p()
+    h.hipEventCreate(C.byref(e0))
+    h.hipEventCreate(C.byref(e1))
+    try:
+        h.hipMemcpyAsync(b, a, nbytes, 3, None)  # hipMemcpyDeviceToDevice
+        h.hipDeviceSynchronize()
+        best = None
+        for _ in range(reps):
+            h.hipEventRecord(e0, None)
+            h.hipMemcpyAsync(b, a, nbytes, 3, None)
+            h.hipEventRecord(e1, None)
+            h.hipEventSynchronize(e1)
+            ms = C.c_float()
+            h.hipEventElapsedTime(C.byref(ms), e0, e1)
+            best = ms.value if best is None else min(best, ms.value)
+    finally:
+        h.hipEventDestroy(e0)
+        h.hipEventDestroy(e1)
+        h.hipFree(a)
+        h.hipFree(b)
+    return 2 * nbytes / (best * 1e-3) / 1e9
+

@@ -263,27 +263,12 @@ def host_workers():
     return max(1, min(share, 32) - 1)
 
 
-def copy_peak_gbps(local, nbytes=1 << 30, reps=10):
-    """The device's measured STREAM-copy rate (report the roofline fraction
-    against it as well as against the 8 TB/s spec): a 1 GiB device-to-device copy, read +
-    write bytes per second, best of `reps`."""
-    import torch
-    dev = torch.device("cuda", local)
-    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize(dev)
-    best = None
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1)
-        best = ms if best is None else min(best, ms)
-    del a, b
-    return 2 * nbytes / (best * 1e-3) / 1e9
+def copy_peak_gbps(local):
+    """The device's measured copy rate (report the roofline fraction against
+    it as well as against the 8 TB/s spec): a 1 GiB device-to-device hipMemcpy, read +
+    write bytes per second, best of 10 (av1dec_amd.native.copy_peak_gbps)."""
+    from av1dec_amd import native
+    return native.copy_peak_gbps(local)
 
 
 def output_leg(decs, streams, pos, steps, workers):
@@ -292,14 +277,14 @@ def output_leg(decs, streams, pos, steps, workers):
     buffers (av1r_get_output) -- decode + delivery over the total time.  The read-back runs
     after the decode (a context is driven by one thread at a time), so this is a lower bound
     of a server that overlaps the two."""
-    import torch
+    from av1dec_amd import native
     from av1dec_amd.pipeline import run_native
     for d in decs:
         d.set_discard_output(False)
     W, H = streams[0][0].hdr.frame_width, streams[0][0].hdr.frame_height
     n = len(decs) * steps
-    pin = torch.empty(n * W * H * 3 // 2, dtype=torch.uint8).pin_memory()
-    base = pin.data_ptr()
+    pin = native.PinnedBuffer(n * W * H * 3 // 2)
+    base = pin.ptr.value
     t0 = time.perf_counter()
     st = run_native(decs, "cycle", streams, pos, max_frames=steps, workers=workers)
     t1 = time.perf_counter()
@@ -311,6 +296,7 @@ def output_leg(decs, streams, pos, steps, workers):
                      "av1r_get_output")
             k += 1
     t2 = time.perf_counter()
+    pin.close()
     for d in decs:
         d.set_discard_output(True)
     return {"fps": round(k / (t2 - t0), 3), "frames": k, "decoded": int(st["frames"]),

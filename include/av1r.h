@@ -313,6 +313,11 @@ int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream);
  * of k_flow; 0 = never.  Default 0 (environment AV1R_STRIP_LEVELS).  Returns the previous
  * value.  Both kernels are bit-exact; tests lower it to run every stream on k_strip. */
 int av1r_set_strip_levels(int levels);
+/* Process-wide: 1 = the in-loop filters of frames launched from now on run fused (k_post:
+ * deblocking -> CDEF -> loop restoration per 64-row stripe tile in LDS, straight into the
+ * output frame; not for frames whose stage snapshots are kept), 0 = the three stage kernels
+ * (default; environment AV1R_FUSED).  Both are bit-exact.  Returns the previous value. */
+int av1r_set_filter_fusion(int on);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);
