@@ -272,7 +272,15 @@ DEV void stp_c(const DevPlane& p, int x, int y, uint8_t v, bool coh)
 // (KParams::strip): such a pixel is either another strip's, read as a granule, or this
 // strip's, read from the workgroup's LDS ring behind the barrier that ended its writer's
 // group; the frame itself is then only written in the launch (plain stores), never read
-// for an in-launch pixel.  -DAV1R_FLOW_DEBUG checks both at run time (flow_check_read).
+// for an in-launch pixel.  Checklist for a new read site in recon.hip's AV1R_FLOW_PART code
+// (k_flow, k_strip): (1) can another item of this launch have written the pixel?  If not
+// (batch data, reference frames, pixels final before the launch), any load will do.  (2) If
+// so: in k_flow it is read through ldp<true>/ldp4<true> (or ldp_c/ldp4_c with coh = true) or
+// arrives in a granule, after the wait that orders it; in k_strip it is a granule (another
+// strip's) or a ring read (this strip's).  (3) Its writer stores it sc1 in k_flow (stp4<true>,
+// stp_c with coh), and publishes a granule or a done flag if a consumer's wait names it.
+// The read sites today: coop_intra_edges_gran (intra_dev.h), tb_predict's CFL luma and
+// ii_item's edges and inter prediction (recon.hip); each is marked "(flow read site)".
 DEV bool strip_plain(int kstrip, bool gran) { return kstrip && gran; }  // (k_strip runs only with granules)
 
 // Work-item encoding of the per-level item lists (host schedule -> k_level):

@@ -151,6 +151,7 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
     const int n = w + h;
     const int aboveLimit = imin(maxX, x + (hAR ? 2 * w : w) - 1);
     const int leftLimit = imin(maxY, y + (hBL ? 2 * h : h) - 1);
+    // (flow read site, COH = true in k_flow: sc1 loads after the dependency-flag wait)
     for (int i = t; i < n; i += nt) {
         uint8_t a, l;
         if (!hA && hL) a = ldp<COH>(src, x - 1, y);
@@ -247,6 +248,8 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
                               : (cm & 2) ? G.v + (size_t)((x - 1) >> 2) * G.gh + ((y - 1) >> 2)
                                          : G.h + (size_t)((y - 1) >> 2) * G.gw + ((x - 1) >> 2);
             uint32_t val = 0;
+            // (flow read site: in-launch units of other items are granules (inl), this strip's
+            // come from the ring; the frame is read only for pixels final before the launch)
             if (act && !inl && G.ring && ring_has(*G.ring, plane, kind == 1 ? y + 4 * u : y - 1)) {
                 // k_strip: a unit of this strip, written by an earlier group (the LDS ring)
                 const RingView& R = *G.ring;

@@ -261,7 +261,8 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             // together with the edge loads
             const DevPlane& luma = k.cur.pl[0];
             const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
-            // (k_strip: the same block's luma, in this strip's LDS ring)
+            // (flow read site: the same block's luma, written by earlier items of the launch:
+            // sc1 loads after the done-flag wait in k_flow, this strip's LDS ring in k_strip)
             const RingView* ring = COH && gran ? G->ring : nullptr;
             for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
@@ -1312,7 +1313,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
                     }
                 m = r2(s4, 2);
             }
-            const int d = ldp<COH>(dst, baseX + j, baseY + i);
+            const int d = ldp<COH>(dst, baseX + j, baseY + i);  // (flow read site: k_inter's output, final before the launch)
             const uint8_t v = (uint8_t)clip1(r2(m * L.pred[i * 64 + j] + (64 - m) * d, 6));
             if (addRes) L.pred[i * 64 + j] = v;
             else stp<COH>(dst, baseX + j, baseY + i, v);
