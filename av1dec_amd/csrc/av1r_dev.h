@@ -211,6 +211,53 @@ DEV void coop_sync()
     }
 }
 
+// Wave-uniform reads of data no kernel of the launch writes (the batch's records, the
+// spec tables) through the scalar cache.  A global_load of a uniform value is a VECTOR
+// memory op: its s_waitcnt vmcnt counts every store the wave issued before it (gfx9 keeps
+// loads and stores in one in-order counter), so in k_flow / k_strip each record or table
+// read after an item's pixel stores waited for those stores to reach L2.  s_load (address
+// space 4, lgkmcnt) does not.  Only for data final before the launch: the scalar cache is
+// not coherent with vector stores (a dispatch's acquire invalidates it).
+typedef __attribute__((address_space(4))) const uint32_t sc_u32;
+DEV uintptr_t uniform_addr(const void* p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    // (readfirstlane returns int: through uint32_t, or a low word >= 2^31 sign-extends)
+    return (uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
+           ((uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
+}
+template <class T>
+DEV T sload(const T* p)  // a record (size and address multiples of 4)
+{
+    static_assert(sizeof(T) % 4 == 0, "sload: dword records");
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) T*)uniform_addr(p);
+#else
+    return *p;  // (the host pass of the single-source compile; never run)
+#endif
+}
+template <class T>
+DEV int sfield(const T* p)  // a byte / halfword at a uniform address (the dword holding it)
+{
+    static_assert(sizeof(T) <= 2, "sfield: byte / halfword fields");
+    const uintptr_t a = uniform_addr(p);
+    const uint32_t w = *(sc_u32*)(a & ~(uintptr_t)3) >> (8 * (a & 3));
+    return (int)(T)w;
+}
+// tab[i], the index clamped to the table: a scalar load also runs in a branch no lane
+// takes (exec = 0), with whatever the index register holds there
+template <class T, int N>
+DEV int stab(const T (&tab)[N], int i)
+{
+    return sfield(tab + (i < 0 ? 0 : i >= N ? N - 1 : i));
+}
+template <int NT, class T, int N>
+DEV int ctab(const T (&tab)[N], int i)  // tab[i] for an item of NT lanes: scalar when i is wave-uniform
+{
+    if constexpr (NT >= 64) return stab(tab, i);
+    else return tab[i];
+}
+
 DEV const av1r_mi& mi_at(const KParams& k, int row, int col) { return k.mi[(size_t)row * k.mi_stride + col]; }
 DEV int plane_bsize(int bs, int plane) { return plane ? av1r_ss420[bs] : bs; }
 DEV uint8_t& px(const DevPlane& p, int x, int y) { return p.p[(size_t)y * p.stride + x]; }
@@ -292,3 +339,67 @@ DEV bool strip_plain(int kstrip, bool gran) { return kstrip && gran; }  // (k_st
 #define AV1R_ITEM(kind, idx) (((uint32_t)(kind) << 30) | (uint32_t)(idx))
 #define AV1R_ITEM_KIND(v) ((v) >> 30)
 #define AV1R_ITEM_INDEX(v) ((v) & 0x3fffffffu)
+
+// ---- debug timeline of the recon kernels (-DAV1R_TRACE; recon.hip) ----
+#define AV1R_TRACE_W 16  // u64 per item in the debug timeline
+// Debug timeline (AV1R_TRACE_FILE): lane 0 of each item stamps the 100 MHz real-time
+// counter at entry, once the item record is in, after the prediction and at the end.
+// Compiled in only with -DAV1R_TRACE (the stamps' waits constrain scheduling).
+DEV void trace_put(unsigned long long* tr, int slot, unsigned long long v)
+{
+#ifdef AV1R_TRACE
+    if (tr && (threadIdx.x & 63) == 0) tr[slot] = v;
+#else
+    (void)tr;
+    (void)slot;
+    (void)v;
+#endif
+}
+DEV unsigned long long trace_now()
+{
+#ifdef AV1R_TRACE
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memrealtime();
+#else
+    return 0;
+#endif
+}
+// -DAV1R_TRACE_LITE (with AV1R_TRACE): the stamps wait for nothing and go to an LDS row per
+// wave, copied to the timeline by trace_flush at the item's end -- the time a wave reaches
+// each point of its instruction stream, without the drains of the full build
+#ifdef AV1R_TRACE_LITE
+DEV unsigned long long* lite_slots()
+{
+    __shared__ unsigned long long rows[4][AV1R_TRACE_W];
+    return rows[(threadIdx.x >> 6) & 3];
+}
+#endif
+DEV void trace_stamp(unsigned long long* tr, int slot)
+{
+#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
+    if (tr && (threadIdx.x & 63) == 0) lite_slots()[slot] = __builtin_amdgcn_s_memrealtime();
+#elif defined(AV1R_TRACE)
+    if (tr && (threadIdx.x & 63) == 0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        tr[slot] = __builtin_amdgcn_s_memrealtime();
+    }
+#else
+    (void)tr;
+    (void)slot;
+#endif
+}
+DEV void trace_flush(unsigned long long* tr)
+{
+#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
+    if (tr && (threadIdx.x & 63) == 0)
+        for (int q = 2; q < 14; q++)
+            if (q != 6 && q != 7) {
+                tr[q] = lite_slots()[q];
+                lite_slots()[q] = 0;
+            }
+#else
+    (void)tr;
+#endif
+}
+
+

@@ -82,27 +82,34 @@ DEV int edge_upsample_used(int w, int h, int filterType, int delta)
 // nUA / nUL: upsampled lengths (0: no upsampling).
 template <int NT>
 DEV void coop_edge_prepare(uint8_t* above, uint8_t* left, IntraLds& L, bool corner, int strA, int nA, int strL,
-    int nL, int nUA, int nUL)
+    int nL, int nUA, int nUL, unsigned long long* tr = nullptr)
 {
     const int t = coop_lane<NT>(), nt = NT;
     const int cs = corner ? r2(left[0] * 5 + above[-1] * 6 + above[0] * 5, 4) : above[-1];
+    int kA[5], kL[5];  // the two filters' taps (uniform: scalar loads)
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        kA[j] = strA ? ctab<NT>(av1r_edge_kernel[strA - 1], j) : 0;
+        kL[j] = strL ? ctab<NT>(av1r_edge_kernel[strL - 1], j) : 0;
+    }
     if (strA)
         for (int i = t; i < nA; i += nt) L.tmp[i] = i == 0 ? (uint8_t)cs : above[i - 1];
     if (strL)
         for (int i = t; i < nL; i += nt) L.tmp2[i] = i == 0 ? (uint8_t)cs : left[i - 1];
     if (strA || strL || corner) coop_sync<NT>();
+    trace_stamp(tr, 13);
     if (strA)
         for (int i = 1 + t; i < nA; i += nt) {
             int s = 0;
 #pragma unroll
-            for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strA - 1][j] * L.tmp[CLIP3(0, nA - 1, i - 2 + j)];
+            for (int j = 0; j < 5; j++) s += kA[j] * L.tmp[CLIP3(0, nA - 1, i - 2 + j)];
             above[i - 1] = (uint8_t)((s + 8) >> 4);
         }
     if (strL)
         for (int i = 1 + t; i < nL; i += nt) {
             int s = 0;
 #pragma unroll
-            for (int j = 0; j < 5; j++) s += av1r_edge_kernel[strL - 1][j] * L.tmp2[CLIP3(0, nL - 1, i - 2 + j)];
+            for (int j = 0; j < 5; j++) s += kL[j] * L.tmp2[CLIP3(0, nL - 1, i - 2 + j)];
             left[i - 1] = (uint8_t)((s + 8) >> 4);
         }
     if (corner && t == 0) {
@@ -298,6 +305,7 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
             if (act) (kind == 0 ? stA + u : kind == 1 ? stL + u : stL + 39)[0] = val;
         }
     }
+    trace_stamp(G.tr, 11);
     coop_sync<NT>();
     const uint8_t* sa = L.tmp - x;   // pixel (px, y - 1) at sa[px]
     const uint8_t* sl = L.tmp2 - y;  // pixel (x - 1, py) at sl[py]
@@ -354,7 +362,8 @@ DEV void coop_publish_gran(const uint8_t* px, int ps, int x, int y, int w, int h
 // Predicts the (1<<log2W) x (1<<log2H) block into pred (row stride ps) from edges already
 // gathered into L (coop_intra_edges + a barrier).  Ends with a coop_sync.
 template <int NT>
-DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, IntraLds& L, uint8_t* pred, int ps)
+DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, IntraLds& L, uint8_t* pred, int ps,
+    unsigned long long* tr = nullptr)
 {
     const int t = coop_lane<NT>(), nt = NT;
     const int w = 1 << P.log2W, h = 1 << P.log2H;
@@ -407,7 +416,7 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
         // directionalIntraPredict (IntraPredict.cpp:379-483)
         const int maxXd = (miCols * 4) >> sub;
         const int maxYd = (miRows * 4) >> sub;  // subsampling_y == subsampling_x (4:2:0)
-        int pAngle = av1r_mode_to_angle[mode] + P.angleDelta * 3;
+        int pAngle = ctab<NT>(av1r_mode_to_angle, mode) + P.angleDelta * 3;
         int upA = 0, upL = 0;
         const uint8_t* A = above;
         const uint8_t* Lc = left;
@@ -420,15 +429,16 @@ DEV void coop_intra_from_edges(int miCols, int miRows, const IntraParams& P, Int
             upA = edge_upsample_used(w, h, P.smooth, pAngle - 90);
             upL = edge_upsample_used(w, h, P.smooth, pAngle - 180);
             coop_edge_prepare<NT>(above, left, L, corner, strA, nA, strL, nL, upA ? w + (pAngle < 90 ? h : 0) : 0,
-                upL ? h + (pAngle > 180 ? w : 0) : 0);
+                upL ? h + (pAngle > 180 ? w : 0) : 0, tr);
             if (upA) A = L.upA + EDGE_OFF;
             if (upL) Lc = L.upL + EDGE_OFF;
         }
+        trace_stamp(tr, 12);
         int dx = 0, dy = 0;
-        if (pAngle < 90) dx = av1r_dr_intra_derivative[pAngle];
-        else if (pAngle > 90 && pAngle < 180) dx = av1r_dr_intra_derivative[180 - pAngle];
-        if (pAngle > 90 && pAngle < 180) dy = av1r_dr_intra_derivative[pAngle - 90];
-        else if (pAngle > 180) dy = av1r_dr_intra_derivative[270 - pAngle];
+        if (pAngle < 90) dx = ctab<NT>(av1r_dr_intra_derivative, pAngle);
+        else if (pAngle > 90 && pAngle < 180) dx = ctab<NT>(av1r_dr_intra_derivative, 180 - pAngle);
+        if (pAngle > 90 && pAngle < 180) dy = ctab<NT>(av1r_dr_intra_derivative, pAngle - 90);
+        else if (pAngle > 180) dy = ctab<NT>(av1r_dr_intra_derivative, 270 - pAngle);
         for (int q = t; q < w * h; q += nt) {
             int i = q >> P.log2W, j = q & (w - 1);
             int v;

@@ -19,67 +19,6 @@
 #include "intra_dev.h"
 #include "txfm_dev.h"
 
-#define AV1R_TRACE_W 16  // u64 per item in the debug timeline
-// Debug timeline (AV1R_TRACE_FILE): lane 0 of each item stamps the 100 MHz real-time
-// counter at entry, once the item record is in, after the prediction and at the end.
-// Compiled in only with -DAV1R_TRACE (the stamps' waits constrain scheduling).
-DEV void trace_put(unsigned long long* tr, int slot, unsigned long long v)
-{
-#ifdef AV1R_TRACE
-    if (tr && (threadIdx.x & 63) == 0) tr[slot] = v;
-#else
-    (void)tr;
-    (void)slot;
-    (void)v;
-#endif
-}
-DEV unsigned long long trace_now()
-{
-#ifdef AV1R_TRACE
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    return __builtin_amdgcn_s_memrealtime();
-#else
-    return 0;
-#endif
-}
-// -DAV1R_TRACE_LITE (with AV1R_TRACE): the stamps wait for nothing and go to an LDS row per
-// wave, copied to the timeline by trace_flush at the item's end -- the time a wave reaches
-// each point of its instruction stream, without the drains of the full build
-#ifdef AV1R_TRACE_LITE
-DEV unsigned long long* lite_slots()
-{
-    __shared__ unsigned long long rows[4][AV1R_TRACE_W];
-    return rows[(threadIdx.x >> 6) & 3];
-}
-#endif
-DEV void trace_stamp(unsigned long long* tr, int slot)
-{
-#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
-    if (tr && (threadIdx.x & 63) == 0) lite_slots()[slot] = __builtin_amdgcn_s_memrealtime();
-#elif defined(AV1R_TRACE)
-    if (tr && (threadIdx.x & 63) == 0) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        tr[slot] = __builtin_amdgcn_s_memrealtime();
-    }
-#else
-    (void)tr;
-    (void)slot;
-#endif
-}
-DEV void trace_flush(unsigned long long* tr)
-{
-#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
-    if (tr && (threadIdx.x & 63) == 0)
-        for (int q = 2; q < 14; q++)
-            if (q != 6 && q != 7) {
-                tr[q] = lite_slots()[q];
-                lite_slots()[q] = 0;
-            }
-#else
-    (void)tr;
-#endif
-}
-
 // ---------------------------------------------------------------------------------
 // Transform blocks
 // ---------------------------------------------------------------------------------
@@ -213,8 +152,8 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
     constexpr int CM = TbLds<MAX>::CM;
     const int t = coop_lane<NT>();
     const int plane = tb.plane, x = tb.x, y = tb.y, txSz = tb.tx_size;
-    const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
-    const int log2W = av1r_tx_w_log2[txSz];
+    const int w = ctab<NT>(av1r_tx_w, txSz), h = ctab<NT>(av1r_tx_h, txSz);
+    const int log2W = ctab<NT>(av1r_tx_w_log2, txSz), log2H = ctab<NT>(av1r_tx_h_log2, txSz);
     const DevPlane& dst = k.cur.pl[plane];
     const uint32_t bflags = blk.flags;
     if (tb.pred == AV1R_PRED_PALETTE) {
@@ -229,12 +168,12 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
         }
     } else if (tb.pred == AV1R_PRED_INTRA) {
         if (COH && gran)
-            coop_intra_edges_gran<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+            coop_intra_edges_gran<NT>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, log2H,
                 (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
                 (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra, *G);
         if (COH && gran) trace_stamp(G->tr, 8);
         if (!(COH && gran))
-            coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, av1r_tx_h_log2[txSz],
+            coop_intra_edges<NT, COH>(k.mi_cols, k.mi_rows, dst, plane, x, y, log2W, log2H,
                 (tb.flags & AV1R_TB_HAVE_LEFT) != 0, (tb.flags & AV1R_TB_HAVE_ABOVE) != 0,
                 (tb.flags & AV1R_TB_HAVE_AR) != 0, (tb.flags & AV1R_TB_HAVE_BL) != 0, L.intra);
         const int isCfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
@@ -243,7 +182,7 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
         P.x = x;
         P.y = y;
         P.log2W = log2W;
-        P.log2H = av1r_tx_h_log2[txSz];
+        P.log2H = log2H;
         P.haveLeft = (tb.flags & AV1R_TB_HAVE_LEFT) != 0;
         P.haveAbove = (tb.flags & AV1R_TB_HAVE_ABOVE) != 0;
         P.haveAR = (tb.flags & AV1R_TB_HAVE_AR) != 0;
@@ -279,7 +218,7 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             }
         }
         coop_sync<NT>();  // edges gathered
-        coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, MAX);
+        coop_intra_from_edges<NT>(k.mi_cols, k.mi_rows, P, L.intra, L.pred, MAX, COH && gran ? G->tr : nullptr);
         if (isCfl) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -343,8 +282,8 @@ template <int NT, int MAX>
 DEV void res_prefetch(const KParams& k, const WorkItem& tb, ResQuads<NT, MAX>& R)
 {
     const int t = coop_lane<NT>();
-    const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
-    const uint32_t ro = tb.coef_cnt ? k.tb_res[AV1R_ITEM_INDEX(tb.code)] : ~0u;
+    const int nq = (ctab<NT>(av1r_tx_w, tb.tx_size) * ctab<NT>(av1r_tx_h, tb.tx_size)) >> 2;
+    const uint32_t ro = tb.coef_cnt ? (NT >= 64 ? sload(k.tb_res + AV1R_ITEM_INDEX(tb.code)) : k.tb_res[AV1R_ITEM_INDEX(tb.code)]) : ~0u;
     const uint2* q4 = reinterpret_cast<const uint2*>(k.res + ro);
 #pragma unroll
     for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
@@ -368,8 +307,9 @@ DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, cons
 {
 
     const int t = coop_lane<NT>();
-    const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;
-    const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
+    const int l2q = ctab<NT>(av1r_tx_w_log2, tb.tx_size) - 2;
+    const int tw = ctab<NT>(av1r_tx_w, tb.tx_size), th = ctab<NT>(av1r_tx_h, tb.tx_size);
+    const int nq = (tw * th) >> 2;
     const DevPlane& dst = k.cur.pl[tb.plane];
     const bool gran = k.gran;
     const bool coh = !strip_plain(k.strip, gran);
@@ -388,7 +328,7 @@ DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, cons
     if (gran && (!ring || (tb.pub & 2))) {
         coop_sync<NT>();
         const int p = tb.plane;
-        coop_publish_gran<NT>(L.pred, MAX, tb.x, tb.y, av1r_tx_w[tb.tx_size], av1r_tx_h[tb.tx_size], k.gran_h[p], k.gran_v[p],
+        coop_publish_gran<NT>(L.pred, MAX, tb.x, tb.y, tw, th, k.gran_h[p], k.gran_v[p],
             k.gran_w[p], k.gran_hn[p], epoch);
     }
 }
@@ -1413,7 +1353,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const
         return;
     }
     // small: item i of the small list, one per wave
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: a wave past the list returns as a whole)
     const uint32_t i = (b - nBig) * 4 + wave;
     if (i >= nSmall) return;  // (no workgroup barrier in this mode)
     const int lane = threadIdx.x & 63;
@@ -1692,7 +1632,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 #define AV1R_FLOW_ITEM_COPY 1  // k_flow -9 %, device-only +5 % (A/B on one box; costs 16 B/lane of scratch)
 #endif
 #if AV1R_FLOW_ITEM_COPY
-    const WorkItem wi = k.items[pos];  // (16 B/lane of scratch: the record stays live across the wait)
+    const WorkItem wi = sload(k.items + pos);  // (scalar registers, live across the wait)
 #else
     const WorkItem& wi = k.items[pos];
 #endif
@@ -1715,7 +1655,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     if (gran) {
         const int p = AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 0 : wi.plane;
         G.mask = k.deps + wi.dep_off - (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 12 : 4);
-        G.mA = G.mask[0], G.mC = G.mask[1], G.mL = G.mask[2];
+        G.mA = sload(G.mask), G.mC = sload(G.mask + 1), G.mL = sload(G.mask + 2);
         G.h = k.gran_h[p];
         G.v = k.gran_v[p];
         G.gw = k.gran_w[p];
@@ -1728,7 +1668,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
         if constexpr (MAX == 64) {  // blends are always large items
-            const av1r_block blk = k.blocks[AV1R_ITEM_INDEX(wi.code)];
+            const av1r_block blk = sload(k.blocks + AV1R_ITEM_INDEX(wi.code));
             trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
             trace_stamp(tr, 4);
@@ -1738,8 +1678,8 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         // intra / palette TB: its residual tile (k_resid) is fetched before the wait
         ResQuads<NT, MAX> R;
         res_prefetch<NT, MAX>(k, wi, R);
-        const av1r_block blk = k.blocks[wi.block];  // (a copy: only the fields predict reads are loaded)
-        const int edgeFilter = k.hdr->enable_intra_edge_filter;
+        const av1r_block blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
+        const int edgeFilter = sfield(&k.hdr->enable_intra_edge_filter);
         trace_stamp(tr, 3);
         flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
         trace_stamp(tr, 4);
@@ -1823,7 +1763,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
         if (n == 0) {
             flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8);
         } else {
-            const uint32_t wave = threadIdx.x >> 6;
+            const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (a scalar branch: no item code runs with exec = 0)
             if (wave < n)
                 flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
                     gd.x >> 8);
@@ -1925,7 +1865,7 @@ extern "C" __global__ __launch_bounds__(256) void k_strip(const KParams* kps, co
         if (n == 0) {
             flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8, &R);
         } else {
-            const uint32_t wave = threadIdx.x >> 6;
+            const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
             if (wave < n)
                 flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
                     gd.x >> 8, &R);

@@ -14,7 +14,7 @@ def main():
         print(f"{name}: {body.count(chr(10))} lines")
         for pat in ["flat_load", "flat_store", "global_load", "global_store", "global_atomic", "ds_read", "ds_write",
                     "s_waitcnt vmcnt(0)", "scratch_", "buffer_", "s_barrier"]:
-            print(f"  {pat:20s} {len(re.findall(pat, body))}")
+            print(f"  {pat:20s} {body.count(pat)}")
         k = s.find(f".name:           {name}\n")
         blk = s[s.rfind("- .args:", 0, k):k + 800]
         for key in [".vgpr_count", ".sgpr_count", ".group_segment_fixed_size", ".private_segment_fixed_size"]:

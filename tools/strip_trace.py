@@ -77,6 +77,18 @@ def main():
     ph = ok & (t8 > 0)
     print("phase p50 (us): entry->resid %.2f resid->wait %.2f wait->edges %.2f edges->pred %.2f pred->store %.2f store->pub %.2f pub->groupend %.2f"
           % tuple(np.median(us(x[ph] - y[ph])) for x, y in ((t3, t2), (t4, t3), (t8, t4), (t9, t8), (t10, t9), (t5, t10), (gend, t5))))
+    t11, t12 = a[:, 11], a[:, 12]
+    for ts in (0, 1, 5, 6):
+        m = ok & (t8 > 0) & (t11 > 0) & (txs == ts)
+        md = m & (t12 > 0)  # directional modes (edge preparation stamped)
+        if not m.any():
+            continue
+        q = lambda x, y, mm: np.median(us(x[mm] - y[mm])) if mm.any() else float("nan")
+        print(f"  tx {ts:2d}: edge loads {q(t11, t4, m):.2f} edge assembly {q(t8, t11, m):.2f} | directional n={md.sum()}: "
+              f"edge prep {q(t12, t8, md):.2f} predict loop {q(t9, t12, md):.2f} | other modes predict {q(t9, t8, m & ~md):.2f}")
+        t13 = a[:, 13]
+        me = md & (t13 > 0)
+        print(f"        edge prep split: params + corner copy {q(t13, t8, me):.2f}, filter + upsample {q(t12, t13, me):.2f}")
 
 
 if __name__ == "__main__":
