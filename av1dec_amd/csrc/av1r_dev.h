@@ -121,6 +121,7 @@ struct KParams {
     // k_strip (build_strips): this frame's items run one strip per workgroup, same-strip
     // pixels read from the strip's LDS ring, the frame stored plainly
     int strip;
+    int fi;  // k_flow / k_strip: small intra TBs take the lean path (intra_fast.h; AV1R_FI=0: off)
     uint32_t n_items;
     uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;

@@ -489,6 +489,9 @@ struct PackClock {
 };
 
 // the filters fused into one kernel (av1r_set_filter_fusion; AV1R_FUSED=1)
+// the lean small-intra path of k_flow / k_strip (intra_fast.h); AV1R_FI=0 or
+// av1r_set_fast_intra(0): the generic path (A/B)
+static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) : 1};
 static std::atomic<int> g_fusedFilters{getenv("AV1R_FUSED") ? atoi(getenv("AV1R_FUSED")) : 0};
 
 // ------------------------------------------------------------------------------------
@@ -1419,6 +1422,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     for (int i = 0; i < n; i++) {
         hk[i] = jobs[i].k;
         hk[i].strip = flow && !jobs[i].P->stripGroups.empty();
+        hk[i].fi = g_fastIntra.load(std::memory_order_relaxed);
         hk[i].trace_base = frameRows;
         for (const Level& lv : jobs[i].P->levels) frameRows += lv.cnt[0] + lv.cnt[1] + lv.cnt[2];
     }
@@ -2375,6 +2379,8 @@ int av1r_set_flow_spins(av1r_ctx* c, uint32_t spins)
 int av1r_set_strip_levels(int levels) { return g_stripLevels.exchange(levels < 0 ? 0 : levels); }
 
 int av1r_set_filter_fusion(int on) { return g_fusedFilters.exchange(on ? 1 : 0); }
+
+int av1r_set_fast_intra(int on) { return g_fastIntra.exchange(on ? 1 : 0); }
 
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream)
 {

@@ -198,15 +198,22 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
 // flat_ instruction, which also waits for the wave's outstanding global stores)
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-struct RingView {
-    lds_u8* base[3];
-    int top[3];
+struct RingView {  // (passed by value: a pointer to it made it a scratch object, and every
+                  // scratch reload waited for the wave's outstanding pixel stores)
+    lds_u8* base;  // luma [AV1R_STRIP_H][AV1R_RING_W], then U and V [AV1R_STRIP_H / 2][AV1R_RING_W / 2]
+    int top;       // the strip's first luma row
+    bool on;       // k_strip (false: k_flow, no ring)
 };
-DEV bool ring_has(const RingView& R, int p, int y) { return y >= R.top[p] && y < R.top[p] + (AV1R_STRIP_H >> (p ? 1 : 0)); }
+DEV bool ring_has(const RingView& R, int p, int y)
+{
+    const int t = p ? R.top >> 1 : R.top;
+    return R.on && y >= t && y < t + (AV1R_STRIP_H >> (p ? 1 : 0));
+}
 DEV lds_u8* ring_px(const RingView& R, int p, int x, int y)
 {
     const int w = AV1R_RING_W >> (p ? 1 : 0);
-    return R.base[p] + (y - R.top[p]) * w + (x & (w - 1));
+    const int off = p ? AV1R_STRIP_H * AV1R_RING_W + (p - 1) * (AV1R_STRIP_H / 2) * (AV1R_RING_W / 2) : 0;
+    return R.base + off + (y - (p ? R.top >> 1 : R.top)) * w + (x & (w - 1));
 }
 
 struct GranEdges {
@@ -219,19 +226,16 @@ struct GranEdges {
     uint32_t* ctl;         // k_flow control block (FLOW_ERR)
     unsigned long long* tr;  // -DAV1R_TRACE timeline row (or null)
     bool coh;              // units read from the frame: sc1 (k_flow) or plain (k_strip: strip_plain)
-    const RingView* ring;  // k_strip: this strip's pixels (units of the strip's rows come from here)
+    RingView ring;         // k_strip: this strip's pixels (units of the strip's rows come from here)
 };
+// The gather half: the above run's units into L.tmp (pixel (x + i, y - 1) at byte i), the
+// left run's into L.tmp2 (pixel (x - 1, y + i) at byte i), the corner's unit at L.tmp2
+// word 39 (the pixel in its byte 3).  aboveLimit / leftLimit: as coop_intra_edges.
 template <int NT>
-DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
-    int log2H, bool hL, bool hA, bool hAR, bool hBL, IntraLds& L, const GranEdges& G)
+DEV void gran_gather(const DevPlane& src, int plane, int x, int y, bool hL, bool hA, int aboveLimit, int leftLimit,
+    IntraLds& L, const GranEdges& G)
 {
     const int t = coop_lane<NT>();
-    const int w = 1 << log2W, h = 1 << log2H;
-    const int sub = plane ? 1 : 0;
-    const int maxX = ((miCols * 4) >> sub) - 1;
-    const int maxY = ((miRows * 4) >> sub) - 1;
-    const int aboveLimit = imin(maxX, x + (hAR ? 2 * w : w) - 1);
-    const int leftLimit = imin(maxY, y + (hBL ? 2 * h : h) - 1);
     const int na = hA ? (aboveLimit >> 2) - (x >> 2) + 1 : 0;
     const int nl = hL ? (leftLimit >> 2) - (y >> 2) + 1 : 0;
     const int nq = na + nl + (hA && hL ? 1 : 0);
@@ -257,9 +261,9 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
             uint32_t val = 0;
             // (flow read site: in-launch units of other items are granules (inl), this strip's
             // come from the ring; the frame is read only for pixels final before the launch)
-            if (act && !inl && G.ring && ring_has(*G.ring, plane, kind == 1 ? y + 4 * u : y - 1)) {
+            if (act && !inl && ring_has(G.ring, plane, kind == 1 ? y + 4 * u : y - 1)) {
                 // k_strip: a unit of this strip, written by an earlier group (the LDS ring)
-                const RingView& R = *G.ring;
+                const RingView& R = G.ring;
                 if (kind == 0) {
                     val = *reinterpret_cast<lds_u32*>(ring_px(R, plane, x + 4 * u, y - 1));
                 } else if (kind == 1) {
@@ -306,6 +310,19 @@ DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int 
         }
     }
     trace_stamp(G.tr, 11);
+}
+template <int NT>
+DEV void coop_intra_edges_gran(int miCols, int miRows, const DevPlane& src, int plane, int x, int y, int log2W,
+    int log2H, bool hL, bool hA, bool hAR, bool hBL, IntraLds& L, const GranEdges& G)
+{
+    const int t = coop_lane<NT>();
+    const int w = 1 << log2W, h = 1 << log2H;
+    const int sub = plane ? 1 : 0;
+    const int maxX = ((miCols * 4) >> sub) - 1;
+    const int maxY = ((miRows * 4) >> sub) - 1;
+    const int aboveLimit = imin(maxX, x + (hAR ? 2 * w : w) - 1);
+    const int leftLimit = imin(maxY, y + (hBL ? 2 * h : h) - 1);
+    gran_gather<NT>(src, plane, x, y, hL, hA, aboveLimit, leftLimit, L, G);
     coop_sync<NT>();
     const uint8_t* sa = L.tmp - x;   // pixel (px, y - 1) at sa[px]
     const uint8_t* sl = L.tmp2 - y;  // pixel (x - 1, py) at sl[py]

@@ -202,14 +202,14 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
             // (flow read site: the same block's luma, written by earlier items of the launch:
             // sc1 loads after the done-flag wait in k_flow, this strip's LDS ring in k_strip)
-            const RingView* ring = COH && gran ? G->ring : nullptr;
+            const bool ring = COH && gran && G->ring.on;
             for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
                 int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
                 int v;
                 if (ring)
-                    v = (*ring_px(*ring, 0, lx, ly) + *ring_px(*ring, 0, lx + 1, ly) + *ring_px(*ring, 0, lx, ly + 1) +
-                            *ring_px(*ring, 0, lx + 1, ly + 1)) << 1;
+                    v = (*ring_px(G->ring, 0, lx, ly) + *ring_px(G->ring, 0, lx + 1, ly) + *ring_px(G->ring, 0, lx, ly + 1) +
+                            *ring_px(G->ring, 0, lx + 1, ly + 1)) << 1;
                 else
                     v = (ldp<COH>(luma, lx, ly) + ldp<COH>(luma, lx + 1, ly) + ldp<COH>(luma, lx, ly + 1) +
                             ldp<COH>(luma, lx + 1, ly + 1)) << 1;
@@ -303,7 +303,7 @@ DEV uint32_t add4(uint32_t p, uint2 r)
 // another strip reads them (pub bit 1)
 template <int NT, int MAX>
 DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch,
-    const RingView* ring = nullptr)
+    RingView ring = {})
 {
 
     const int t = coop_lane<NT>();
@@ -321,11 +321,11 @@ DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, cons
             uint32_t* pp = reinterpret_cast<uint32_t*>(&L.pred[i * MAX + j]);
             const uint32_t o = add4(*pp, R.r[u]);
             stp4_c(dst, tb.x + j, tb.y + i, o, coh);
-            if (ring) *reinterpret_cast<lds_u32*>(ring_px(*ring, tb.plane, tb.x + j, tb.y + i)) = o;
+            if (ring.on) *reinterpret_cast<lds_u32*>(ring_px(ring, tb.plane, tb.x + j, tb.y + i)) = o;
             if (gran) *pp = o;  // the final pixels, for the edge granules
         }
     }
-    if (gran && (!ring || (tb.pub & 2))) {
+    if (gran && (!ring.on || (tb.pub & 2))) {
         coop_sync<NT>();
         const int p = tb.plane;
         coop_publish_gran<NT>(L.pred, MAX, tb.x, tb.y, tw, th, k.gran_h[p], k.gran_v[p],
@@ -1575,6 +1575,8 @@ extern "C" __global__ K_PLAIN_BOUNDS void k_inter_m(const KParams* kps, const ui
 // launch's error word, which the host reports.
 // ---------------------------------------------------------------------------------
 
+#include "intra_fast.h"
+
 template <int NT>
 DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint32_t epoch, uint32_t* ctl)
 {
@@ -1622,7 +1624,7 @@ DEV void flow_publish(uint32_t* flag, uint32_t epoch)
 // 7 XCC id << 16 | dependency count
 template <int NT, int MAX>
 DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl,
-    unsigned long long* trace, uint32_t s, const RingView* ring = nullptr)
+    unsigned long long* trace, uint32_t s, RingView ring = {})
 {
     // What the item reads from the batch after its wait -- its edge mask words, its block's
     // prediction fields, the edge-filter flag (and with AV1R_FLOW_ITEM_COPY its own record)
@@ -1680,13 +1682,28 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         res_prefetch<NT, MAX>(k, wi, R);
         const av1r_block blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
         const int edgeFilter = sfield(&k.hdr->enable_intra_edge_filter);
-        trace_stamp(tr, 3);
-        flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
-        trace_stamp(tr, 4);
-        tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran, edgeFilter);
-        trace_stamp(tr, 9);
-        tb_store_flow<NT, MAX>(k, wi, L, R, epoch, ring);
-        trace_stamp(tr, 10);
+        bool lean = false;
+        if constexpr (NT == 64 && MAX == TB_SMALL) {
+            // small intra TBs: the lean path (intra_fast.h), its parameters set up before the wait
+            if (gran && k.fi && fi_ok(wi, blk)) {
+                lean = true;
+                const FiParams F = fi_setup(k, wi, blk, edgeFilter);
+                trace_stamp(tr, 3);
+                flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+                trace_stamp(tr, 4);
+                fi_run<MAX>(k, wi, F, L, G, R.r[0], epoch, ring, gran);
+                trace_stamp(tr, 10);
+            }
+        }
+        if (!lean) {
+            trace_stamp(tr, 3);
+            flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+            trace_stamp(tr, 4);
+            tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran, edgeFilter);
+            trace_stamp(tr, 9);
+            tb_store_flow<NT, MAX>(k, wi, L, R, epoch, ring);
+            trace_stamp(tr, 10);
+        }
     }
     // the store drain and done flag only where a dependency list names the item (CFL's
     // luma; every edge owner without granules): edges travel in granules, and later
@@ -1852,23 +1869,21 @@ extern "C" __global__ __launch_bounds__(256) void k_strip(const KParams* kps, co
     const uint32_t s = blockIdx.x;
     const uint32_t sid = tab[nStrips + 1 + s];
     RingView R;
-    R.base[0] = (lds_u8*)ringMem;
-    R.base[1] = (lds_u8*)ringMem + kRingY;
-    R.base[2] = (lds_u8*)ringMem + kRingY + kRingC;
-    R.top[0] = (int)sid * AV1R_STRIP_H;
-    R.top[1] = R.top[2] = (int)sid * (AV1R_STRIP_H / 2);
+    R.base = (lds_u8*)ringMem;
+    R.top = (int)sid * AV1R_STRIP_H;
+    R.on = true;
     const uint32_t g1 = tab[s + 1];
     for (uint32_t g = tab[s]; g < g1; g++) {
         const uint2 gd = groups[g];
         const KParams& k = KP(kps, gd.x >> 8);
         const uint32_t n = gd.x & 0xff;
         if (n == 0) {
-            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8, &R);
+            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8, R);
         } else {
             const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
             if (wave < n)
                 flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
-                    gd.x >> 8, &R);
+                    gd.x >> 8, R);
         }
         // the group's ring writes are visible to every later group; its frame stores and
         // granules need no drain (nothing in the strip reads them back)

@@ -193,6 +193,7 @@ def lib():
     l.av1r_flow_debug.argtypes = [C.POINTER(C.c_uint32), i, i, C.POINTER(i)]
     l.av1r_set_strip_levels.argtypes = [i]
     l.av1r_set_filter_fusion.argtypes = [i]
+    l.av1r_set_fast_intra.argtypes = [i]
     l.av1r_pack.argtypes = [vp, C.POINTER(vp)]
     l.av1r_packed_free.argtypes = [vp]
     l.av1r_packed_free.restype = None
@@ -237,7 +238,7 @@ EXPORTS = [
     "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug", "av1r_pack", "av1r_packed_free",
     "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy", "av1r_pack_profile",
     "av1r_pipeline_run", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
-    "av1r_set_strip_levels", "av1r_set_filter_fusion",
+    "av1r_set_strip_levels", "av1r_set_filter_fusion", "av1r_set_fast_intra",
 ]
 
 

@@ -318,6 +318,10 @@ int av1r_set_strip_levels(int levels);
  * output frame; not for frames whose stage snapshots are kept), 0 = the three stage kernels
  * (default; environment AV1R_FUSED).  Both are bit-exact.  Returns the previous value. */
 int av1r_set_filter_fusion(int on);
+/* Process-wide: 1 = small intra transform blocks of the dataflow kernels take the lean path
+ * (default; environment AV1R_FI), 0 = the generic one.  Both are bit-exact (A/B).  Returns
+ * the previous value. */
+int av1r_set_fast_intra(int on);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);

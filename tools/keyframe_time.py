@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Device time of one synthetic 1080p key frame alone on the chip, k_flow against k_strip
 (av1r_set_strip_levels), and a check that both reconstruct it identically.
-usage (GPU box): python3 tools/keyframe_time.py [reps]"""
+usage (GPU box): python3 tools/keyframe_time.py [reps] [k_flow|k_strip]  (one kernel only: PMC passes)"""
 import hashlib
 import os
 import sys
@@ -18,7 +18,10 @@ def main():
     L = native.lib()
     frames = pysynth.stream(1920, 1080, 2, 0x5EED1000, sb128=True)
     out = {}
+    only = sys.argv[2] if len(sys.argv) > 2 else None
     for name, lv in (("k_flow", 0), ("k_strip", 400)):
+        if only and name != only:
+            continue
         L.av1r_set_strip_levels(lv)
         d = Decoder(0, keep_stages=True, timing=True)
         h = d.prepare(frames[0])
