@@ -189,6 +189,7 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F, TbLds<M
         EL[t - 1] = (uint8_t)l;
     }
     coop_sync<64>();
+    trace_stamp(G.tr, 12);
     // upsampling: buf[2i - 1], buf[2i] from the edge (index -2 .. 2n - 2)
     const uint8_t* A = EA;
     const uint8_t* Lc = EL;
@@ -221,6 +222,7 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F, TbLds<M
         else if (F.hL) dc = clip1((s + (h >> 1)) >> log2H);
         else if (F.hA) dc = clip1((s + (w >> 1)) >> log2W);
     }
+    trace_stamp(G.tr, 13);
     // the prediction of this lane's quad
     uint32_t p = 0;
     if (t < nq) {

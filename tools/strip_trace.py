@@ -41,6 +41,17 @@ def main():
     t2, t3, t4, t5, t8, t9, t10 = (a[:, i] for i in (2, 3, 4, 5, 8, 9, 10))
     f0 = t2.min()
     print(f"{len(a)} items; span {us(t5.max() - f0):.1f} us")
+    # lean small-intra items (intra_fast.h): 4 wait done, 8 edges in LDS, 12 edge pass, 13
+    # upsampling + DC, 9 predicted, 10 stored
+    t12, t13 = a[:, 12], a[:, 13]
+    ml = (kind == 0) & (t8 > 0) & (t12 > 0) & (t13 > 0) & (t9 > 0)
+    for ts in np.unique(txs[ml]):
+        mm = ml & (txs == ts)
+        if mm.sum() < 100:
+            continue
+        q = lambda x, y: np.percentile(us(x[mm] - y[mm]), 50)
+        print(f"  lean tx {ts:2d} n={mm.sum():6d} gather {q(t8, t4):.2f} edge pass {q(t12, t8):.2f} up+dc {q(t13, t12):.2f} "
+              f"predict {q(t9, t13):.2f} store {q(t10, t9):.2f} publish {q(t5, t10):.2f}")
     m = (kind == 0) & (t8 > 0)
     for ts in np.unique(txs[m]):
         mm = m & (txs == ts)
