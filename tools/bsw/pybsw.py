@@ -7,6 +7,7 @@ to the reference decoder's MD5 of the decoded output."""
 import ctypes as C
 import hashlib
 import os
+import threading
 import struct
 import subprocess
 
@@ -69,16 +70,23 @@ def build(force=False):
               "-I" + os.path.join(ROOT, "include"), "-I" + PARSE]
     for target, extra in ((LIB, ["-shared", "-fPIC"]), (CLI, ["-DAV1BSW_MAIN"])):
         if force or _stale(target):
-            tmp = f"{target}.{os.getpid()}.tmp"
+            tmp = f"{target}.{os.getpid()}.{threading.get_ident()}.tmp"
             subprocess.check_call(common + extra + SRCS + ["-o", tmp])
             os.replace(tmp, target)
     return LIB
 
 
 _lib = None
+_lib_lock = threading.Lock()  # threads of one process (bench's IVF writers) build once
 
 
 def lib():
+    global _lib
+    with _lib_lock:
+        return _lib_locked()
+
+
+def _lib_locked():
     global _lib
     if _lib is None:
         if _stale(LIB):

@@ -1,6 +1,7 @@
 """Python binding of the synthetic frame-batch generator (tools/synth/synth.cpp)."""
 import ctypes as C
 import os
+import threading
 import subprocess
 
 import numpy as np
@@ -15,7 +16,7 @@ def build(force=False):
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
             os.path.getmtime(src), os.path.getmtime(os.path.join(ROOT, "include", "av1r.h"))):
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        tmp = f"{LIB}.{os.getpid()}.tmp"  # build aside, then rename: concurrent test workers never see a partial file
+        tmp = f"{LIB}.{os.getpid()}.{threading.get_ident()}.tmp"  # build aside, then rename: concurrent test workers never see a partial file
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"),
                                src, "-o", tmp])
         os.replace(tmp, LIB)
@@ -23,9 +24,16 @@ def build(force=False):
 
 
 _lib = None
+_lib_lock = threading.Lock()  # threads of one process (bench's IVF writers) build once
 
 
 def lib():
+    global _lib
+    with _lib_lock:
+        return _lib_locked()
+
+
+def _lib_locked():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB):
