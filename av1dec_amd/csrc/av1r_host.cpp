@@ -2162,8 +2162,37 @@ void av1r_packed_free(av1r_packed* pk)
 
 size_t av1r_packed_bytes(const av1r_packed* pk) { return pk ? pk->P.upBytes : 0; }
 
+// AV1R_PIPE_PROF=1: where av1r_decode_packed_batch spends the launcher's time (seconds,
+// summed; printed by av1r_pipeline_run): waiting for an upload slot (the GPU three frames
+// behind on that stream), the solo launches, the shared launches, the rest
+struct PipeProf {
+    double slotWait = 0, solo = 0, shared = 0, total = 0;
+    long batches = 0, frames = 0, soloFrames = 0;
+};
+static PipeProf g_pprof;
+static const bool g_pipeProf = getenv("AV1R_PIPE_PROF") && atoi(getenv("AV1R_PIPE_PROF")) != 0;
+static double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+extern "C" void av1r_pipe_prof_dump(double elapsed)
+{
+    if (!g_pipeProf) return;
+    const PipeProf& P = g_pprof;
+    fprintf(stderr, "av1r pipe: %.1f ms elapsed, %ld batches (%.2f frames each, %ld solo), launcher: slot wait %.1f ms, "
+            "solo launches %.1f ms, shared launches %.1f ms, other %.1f ms\n", 1e3 * elapsed, P.batches,
+            P.batches ? (double)P.frames / P.batches : 0.0, P.soloFrames, 1e3 * P.slotWait, 1e3 * P.solo, 1e3 * P.shared,
+            1e3 * (P.total - P.slotWait - P.solo - P.shared));
+    g_pprof = PipeProf();
+}
+
 int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int n)
 {
+    const double tIn = g_pipeProf ? now_s() : 0;
+    struct Tot {
+        double t;
+        ~Tot() { if (g_pipeProf) g_pprof.total += now_s() - t; }
+    } tot{tIn};
     if (!ctxs || !pks || n <= 0 || !ctxs[0]) return AV1R_E_INVALID;
     av1r_ctx* lc = ctxs[0];
     av1r_ctx* c = lc;
@@ -2201,7 +2230,9 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         slots[i] = &U;
         m->pkIdx = (m->pkIdx + 1) % av1r_ctx::kPackRing;
         if (U.pending) {  // a launch three frames back may still read this slot
+            const double w0 = g_pipeProf ? now_s() : 0;
             HIPCHK(hipEventSynchronize(U.done));
+            if (g_pipeProf) g_pprof.slotWait += now_s() - w0;
             U.pending = false;
         }
         if (U.cap < pk->P.cap) {
@@ -2229,9 +2260,17 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         if (rc) return rc;
         (alone ? solo : jobs).push_back(j);
     }
+    const double s0 = g_pipeProf ? now_s() : 0;
     for (auto& j : solo) {  // first, so that their long chains start at once
         int rc = launch_solo(j);
         if (rc) return rc;
+    }
+    const double s1 = g_pipeProf ? now_s() : 0;
+    if (g_pipeProf) {
+        g_pprof.solo += s1 - s0;
+        g_pprof.batches++;
+        g_pprof.frames += n;
+        g_pprof.soloFrames += (long)solo.size();
     }
     if (!jobs.empty()) {
         // members' own earlier work first (as av1r_decode_prepared_batch)
@@ -2262,6 +2301,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             if (j.c != bl) j.c->joinLead = bl;
         for (auto& j : lv)
             if (j.c != bl) j.c->joinLead = bl;
+        if (g_pipeProf) g_pprof.shared += now_s() - s1;
     }
     for (int i = 0; i < n; i++) {  // the upload slots are free again after their launch
         if (!slots[i]) continue;

@@ -205,6 +205,11 @@ def lib():
     l.av1r_busy.argtypes = [vp]
     l.av1r_pack_profile.argtypes = [C.POINTER(C.c_uint64), i, i]
     l.av1r_pipeline_run.argtypes = [C.POINTER(vp), i, C.POINTER(StreamSource), C.c_int64, i, i, C.POINTER(PipelineStats)]
+    l.av1r_pipeline_open.argtypes = [C.POINTER(vp), i, C.POINTER(StreamSource), i, i, C.POINTER(vp)]
+    l.av1r_pipeline_step.argtypes = [vp, C.c_int64, C.POINTER(PipelineStats)]
+    l.av1r_pipeline_launched.argtypes = [vp, C.POINTER(C.c_int64), i]
+    l.av1r_pipeline_close.argtypes = [vp]
+    l.av1r_pipeline_close.restype = None
     l.av1r_cycle_next.argtypes = [vp, i, C.POINTER(vp)]
     l.av1r_ivf_source_create.argtypes = [C.POINTER(vp), C.POINTER(C.c_size_t), i, C.POINTER(StreamSource)]
     l.av1r_ivf_source_destroy.argtypes = [C.POINTER(StreamSource)]
@@ -237,7 +242,8 @@ EXPORTS = [
     "av1r_set_discard_output", "av1r_stage_times", "av1r_decode_prepared_batch", "av1r_recon_kernel_times",
     "av1r_set_schedule", "av1r_set_flow_spins", "av1r_flow_debug", "av1r_pack", "av1r_packed_free",
     "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy", "av1r_pack_profile",
-    "av1r_pipeline_run", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
+    "av1r_pipeline_run", "av1r_pipeline_open", "av1r_pipeline_step", "av1r_pipeline_launched",
+    "av1r_pipeline_close", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
     "av1r_set_strip_levels", "av1r_set_filter_fusion", "av1r_set_fast_intra",
 ]
 

@@ -130,6 +130,65 @@ class IvfPipeline:
         return time.perf_counter() - t0
 
 
+def _cycle_source(l, streams, positions, keep):
+    n = len(streams)
+    rows = []
+    for fr in streams:
+        arr = (C.c_void_p * len(fr))(*[C.cast(f.byref(), C.c_void_p).value for f in fr])
+        rows.append(arr)
+    table = (C.c_void_p * n)(*[C.cast(r, C.c_void_p).value for r in rows])
+    count = (C.c_int * n)(*[len(fr) for fr in streams])
+    pos = (C.c_int64 * n)(*(positions or [0] * n))
+    cyc = native.Cycle(C.cast(table, C.c_void_p).value, count, pos, n)
+    keep += [rows, table, count, pos, cyc, streams]
+    src = native.StreamSource()
+    src.next = C.cast(l.av1r_cycle_next, C.c_void_p).value
+    src.user = C.cast(C.pointer(cyc), C.c_void_p).value
+    src.stable = 1
+    return src
+
+
+class NativePipeline:
+    """av1r_pipeline_open / _step / _close over a cycling source: the packing workers stay
+    up between steps, `depth` frames ahead of every stream, so each step after the first
+    runs in steady state (bench.py's headline).  positions: each stream's starting frame;
+    positions() reports where every stream's launches have reached."""
+
+    def __init__(self, decoders, streams, positions=None, depth=0, workers=0):
+        self.l = l = native.lib()
+        self.decs = decoders
+        n = len(decoders)
+        self.n = n
+        self.pos0 = list(positions or [0] * n)
+        self.keep = []
+        self.src = _cycle_source(l, streams, self.pos0, self.keep)
+        ctxs = (C.c_void_p * n)(*[d.c.value for d in decoders])
+        self.keep.append(ctxs)
+        self.p = C.c_void_p()
+        rc = l.av1r_pipeline_open(ctxs, n, C.byref(self.src), int(depth), int(workers), C.byref(self.p))
+        if rc:
+            raise BackendError(f"av1r_pipeline_open failed ({rc})")
+
+    def step(self, frames):
+        """Launch `frames` more frames of every stream and synchronize; the step's stats."""
+        st = native.PipelineStats()
+        rc = self.l.av1r_pipeline_step(self.p, int(frames), C.byref(st))
+        if rc:
+            raise BackendError(f"av1r_pipeline_step failed ({rc}): {self.decs[0].l.av1r_last_error(self.decs[0].c).decode()}")
+        return {k: getattr(st, k) for k, _ in native.PipelineStats._fields_}
+
+    def positions(self):
+        c = (C.c_int64 * self.n)()
+        if self.l.av1r_pipeline_launched(self.p, c, self.n):
+            raise BackendError("av1r_pipeline_launched failed")
+        return [p0 + int(v) for p0, v in zip(self.pos0, c)]
+
+    def close(self):
+        if self.p:
+            self.l.av1r_pipeline_close(self.p)
+            self.p = C.c_void_p()
+
+
 def run_native(decoders, source="cycle", streams=None, positions=None, max_frames=0, depth=0, workers=0):
     """The same pipeline in native threads (av1r_pipeline_run, include/av1r.h): no
     interpreter on the path (`workers` packing threads, 0: one per stream).  source "cycle": streams = per-stream lists of batchfile.Frame;

@@ -369,16 +369,27 @@ def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, p
     pp.close()
     sync()
     pos = list(pp.pos)
-    t_prime = time.perf_counter()
-    while time.perf_counter() - t_prime < prime_s:
-        run_native(decs, "cycle", streams, pos, max_frames=F, workers=workers, depth=depth)
-    run_native(decs, "cycle", streams, pos, max_frames=warmup, workers=workers, depth=depth)
-    if dist:
-        dist.barrier()
-    pos0 = list(pos)
-    t0 = time.perf_counter()
-    pr = run_native(decs, "cycle", streams, pos, max_frames=steps, workers=workers, depth=depth)  # synchronizes every context
-    elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+    # one pipeline for the priming pass, the warmup and the timed window: its packing
+    # workers run continuously, `depth` frames ahead of every stream, so the window holds a
+    # running decoder's steady-state work (every frame it launches was packed by the same
+    # workers, which meanwhile pack the frames after the window) rather than a cold start
+    # and a drain (av1r_pipeline_open / _step, include/av1r.h)
+    from av1dec_amd.pipeline import NativePipeline
+    pl = NativePipeline(decs, streams, pos, depth=depth, workers=workers)
+    try:
+        t_prime = time.perf_counter()
+        while time.perf_counter() - t_prime < prime_s:
+            pl.step(F)
+        pl.step(warmup)
+        if dist:
+            dist.barrier()
+        pos0 = pl.positions()
+        t0 = time.perf_counter()
+        pr = pl.step(steps)  # synchronizes every context
+        elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+        pos = pl.positions()
+    finally:
+        pl.close()
     fps = aggregate_fps(world, steps * S, elapsed)
     timed = [(j, t % F) for j in range(S) for t in range(pos0[j], pos0[j] + steps)]
     n_key = sum(1 for j, t in timed if streams[j][t].hdr.frame_type == 0)
@@ -676,8 +687,9 @@ def main():
                                    f"stream j offset by j*{F}/{S} frames; tiles {tiles[0]}x{tiles[1]}; seeds "
                                    f"{seed:#x}+stream), one frame of every stream per step in shared launches; "
                                    f"host-inclusive: each frame validated, scheduled, packed and uploaded from "
-                                   f"host memory inside the timed region (native pipeline: {workers} packing "
-                                   f"threads, {depth_eff} frames ahead per stream; key frames run alone on their stream, overlapping "
+                                   f"host memory inside the timed region (native pipeline kept running across priming, warmup and "
+                                   f"the timed window: {workers} packing threads, {depth_eff} frames ahead per stream, packing the "
+                                   f"frames after the window while it runs; key frames run alone on their stream, overlapping "
                                    f"the other streams' batches); timed frames: {args.steps * S} of which {r['n_key']} key",
                        "host_threads": workers + 1,
                        "timed_key_frames": r["n_key"],

@@ -359,6 +359,21 @@ typedef struct av1r_pipeline_stats {
 } av1r_pipeline_stats;
 int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
                       int workers, av1r_pipeline_stats* stats);
+/* The same pipeline kept open between runs: av1r_pipeline_open starts the workers, which
+ * from then on keep every stream `depth` frames ahead (no frame budget: a cycling source
+ * is fetched for as long as the pipeline is open); each av1r_pipeline_step launches
+ * `frames` more entries of every stream (frames and show-existing units; 0: to every
+ * stream's end) and returns once every context is synchronized -- so consecutive steps see
+ * the steady state of a decoder that never stops (av1r_pipeline_run = open + one step +
+ * close, with the workers stopping at max_frames).  av1r_pipeline_launched: the entries
+ * launched per stream so far (counts[n], n = the pipeline's stream count).
+ * av1r_pipeline_close stops the workers and frees what they packed ahead. */
+typedef struct av1r_pipeline av1r_pipeline;
+int av1r_pipeline_open(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int depth, int workers,
+                       av1r_pipeline** out);
+int av1r_pipeline_step(av1r_pipeline* p, int64_t frames, av1r_pipeline_stats* stats);
+int av1r_pipeline_launched(const av1r_pipeline* p, int64_t* counts, int n);
+void av1r_pipeline_close(av1r_pipeline* p);
 /* Source over in-memory batches: stream s (< n_streams) yields batches[s][pos[s] % count[s]],
  * then advances pos[s] (use av1r_cycle_next as `next` and an av1r_cycle as `user`).  It
  * never ends, so av1r_pipeline_run rejects it (AV1R_E_INVALID) without max_frames > 0 or

@@ -168,3 +168,13 @@ def test_cycle_source_bounds(native_lib):
     assert native_lib.av1r_pipeline_run(ctxs, 1, C.byref(src), 0, 0, 1, C.byref(st)) == abi.AV1R_E_INVALID
     ctxs2 = (C.c_void_p * 2)(1, 1)
     assert native_lib.av1r_pipeline_run(ctxs2, 2, C.byref(src), 5, 0, 1, C.byref(st)) == abi.AV1R_E_INVALID
+    # the persistent pipeline: a cycle source with fewer streams than contexts, null
+    # arguments, a step without a pipeline -- all refused before any thread or device use
+    p = C.c_void_p()
+    assert native_lib.av1r_pipeline_open(ctxs2, 2, C.byref(src), 0, 1, C.byref(p)) == abi.AV1R_E_INVALID
+    assert native_lib.av1r_pipeline_open(ctxs, 1, C.byref(src), 0, 1, None) == abi.AV1R_E_INVALID
+    assert native_lib.av1r_pipeline_open(None, 1, C.byref(src), 0, 1, C.byref(p)) == abi.AV1R_E_INVALID
+    assert native_lib.av1r_pipeline_step(None, 5, C.byref(st)) == abi.AV1R_E_INVALID
+    counts = (C.c_int64 * 1)()
+    assert native_lib.av1r_pipeline_launched(None, counts, 1) == abi.AV1R_E_INVALID
+    native_lib.av1r_pipeline_close(None)  # a no-op

@@ -1,6 +1,7 @@
 """The exact paths bench.py times, at the headline configuration, checked frame by frame.
 
-* cycle: bench.py's headline -- av1r_pipeline_run over the in-memory batches of the bench's
+* cycle: bench.py's headline -- the native pipeline (av1r_pipeline_open, then steps, as the
+  bench keeps it open across priming, warmup and the timed window) over the in-memory batches of the bench's
   own 8 synthetic 1080p streams (bench.rank_streams seeds), GOP phases staggered as the bench
   staggers them, bench.host_workers() packing threads, the pipeline's default look-ahead,
   deep (key) frames launched alone, batch re-ordering -- for one whole GOP per stream (every
@@ -58,7 +59,7 @@ def test_headline_helpers_are_the_bench_ones():
 def test_gpu_headline_cycle_path_matches_oracle():
     import bench
     from av1dec_amd import Decoder
-    from av1dec_amd.pipeline import run_native
+    from av1dec_amd.pipeline import NativePipeline
     S, F = 8, 60
     streams = bench.rank_streams("1080p", 0, S, F)
     with ThreadPoolExecutor(min(S, 16)) as ex:
@@ -71,8 +72,16 @@ def test_gpu_headline_cycle_path_matches_oracle():
             pp.close()
             pos = list(pp.pos)
             pos0 = list(pos)
-            st = run_native(decs, "cycle", streams, pos, max_frames=F, workers=bench.host_workers(), depth=0)
-            assert st["frames"] == S * F
+            # bench.py's pipeline: kept open across the priming pass, the warmup and the timed
+            # window (here: three steps covering one GOP), workers packing ahead throughout
+            pl = NativePipeline(decs, streams, pos, depth=0, workers=bench.host_workers())
+            try:
+                frames = sum(pl.step(k)["frames"] for k in (5, 20, F - 25))
+                pos = pl.positions()
+            finally:
+                pl.close()
+            assert frames == S * F
+            assert pos == [p + F for p in pos0]
             keys = sum(1 for j in range(S) for t in range(pos0[j], pos0[j] + F) if streams[j][t % F].hdr.frame_type == 0)
             assert keys == S  # one whole GOP per stream: every key frame ran in the pipeline
             got = [[] for _ in range(S)]
