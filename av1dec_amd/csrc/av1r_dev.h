@@ -169,6 +169,9 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_SPINS (1u << 22)
 #define FLOW_WALL 3000000000ull  // 30 s of the 100 MHz real-time counter
 // the launch's spin bound (av1r_set_flow_spins: a test forces the timeout path with 1)
+#ifndef AV1R_ERR_POLL_MASK
+#define AV1R_ERR_POLL_MASK 31  // spinning waves read the launch's error word every 32nd poll
+#endif
 DEV uint32_t flow_spin_limit(const uint32_t* ctl)
 {
     const uint32_t v = __hip_atomic_load(ctl + FLOW_SPINLIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -293,10 +293,10 @@ DEV void gran_gather(const DevPlane& src, int plane, int x, int y, bool hL, bool
                     val = (uint32_t)gv;
                 }
                 if (__all(ok)) break;
-                // (the launch's error word every 32nd spin: every spinning wave of the chip
-                // polls this one line)
+                // (the launch's error word every AV1R_ERR_POLL_MASK + 1 spins: every spinning
+                // wave of the chip polls this one line)
                 const bool other =
-                    (spins & 31) == 0 && __hip_atomic_load(G.ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    (spins & AV1R_ERR_POLL_MASK) == 0 && __hip_atomic_load(G.ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                 if (!lim) lim = flow_spin_limit(G.ctl);
                 if (other || ++spins > lim || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
                     if (lane == 0 && !other) {  // 2: an edge granule wait (1: a dependency flag wait)

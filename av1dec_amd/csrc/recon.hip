@@ -1591,7 +1591,7 @@ DEV void flow_wait(const uint32_t* deps, uint32_t nd, const uint32_t* done, uint
                 const bool ok = !mine || __hip_atomic_load(done + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
                 if (__all(ok)) break;
                 const bool dead =
-                    (spins & 31) == 0 && __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    (spins & AV1R_ERR_POLL_MASK) == 0 && __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                 if (!lim) lim = flow_spin_limit(ctl);
                 if (dead || ++spins > lim || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
                     if (lane == 0 && !dead) {  // the wave that gave up first reports
