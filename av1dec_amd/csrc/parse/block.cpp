@@ -2211,6 +2211,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         // levels so far, padded by 4 zero rows / columns below and right (every context offset
         // is non-negative): the neighbour sums need no bounds checks
         const int ps = width + 4;
+        // the context neighbours as offsets into lvl[] (per transform block, not per level)
+        int sigOff[5], magOff[3];
+        for (int k = 0; k < 5; k++) sigOff[k] = kSigRefDiffOffset[cls][k][0] * ps + kSigRefDiffOffset[cls][k][1];
+        for (int k = 0; k < 3; k++) magOff[k] = kMagRefOffset[cls][k][0] * ps + kMagRefOffset[cls][k][1];
         for (int c = eob - 1; c >= 0; c--) {
             const int pos = scan[c];
             int level;
@@ -2226,8 +2230,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 level = SN<3>(cdf.coef.coeff_base_eob[txSzCtx][ptype][ctx]) + 1;
             } else {
                 int mag = 0;
-                for (int k = 0; k < 5; k++)
-                    mag += std::min((int)lp[kSigRefDiffOffset[cls][k][0] * ps + kSigRefDiffOffset[cls][k][1]], 3);
+                for (int k = 0; k < 5; k++) mag += std::min((int)lp[sigOff[k]], 3);
                 int ctx = std::min((mag + 1) >> 1, 4);
                 if (cls == TX_CLASS_2D) {
                     ctx = (row == 0 && col == 0) ? 0 : ctx + kCoeffBaseCtxOffset[txSz][std::min(row, 4)][std::min(col, 4)];
@@ -2240,7 +2243,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             if (level > kNumBaseLevels) {
                 for (int idx = 0; idx < kCoeffBaseRange / (kBrCdfSize - 1); idx++) {
                     int mag = 0;  // levels here are at most 15 = COEFF_BASE_RANGE + NUM_BASE_LEVELS + 1
-                    for (int k = 0; k < 3; k++) mag += lp[kMagRefOffset[cls][k][0] * ps + kMagRefOffset[cls][k][1]];
+                    for (int k = 0; k < 3; k++) mag += lp[magOff[k]];
                     mag = std::min((mag + 1) >> 1, 6);
                     int ctx;
                     if (pos == 0) ctx = mag;
@@ -2326,10 +2329,11 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         // raster order over the bounding box of the scanned positions, which is cleared again
         std::vector<uint32_t>& out = P.cur->coefs;
         int maxI = 0, maxJ = 0;
+        const int twl = av1r_tx_w_log2[txSz] < 5 ? av1r_tx_w_log2[txSz] : 5;  // log2(tw)
         for (int c = 0; c < eob; c++) {
             const int pos = scan[c];
-            maxI = std::max(maxI, pos / tw);
-            maxJ = std::max(maxJ, pos % tw);
+            maxI = std::max(maxI, pos >> twl);
+            maxJ = std::max(maxJ, pos & (tw - 1));
         }
         for (int i = 0; i <= maxI; i++) {
             int* row = &quant[i * tw];
