@@ -106,10 +106,41 @@ DEV int fi_row_sum(int v)
 
 // After the dependency wait: gather, predict, add, store, publish (see the file comment).
 // R: the residual quad of this lane (res_prefetch<64, 16>).  Ends with the stores issued.
+// the wave-uniform value in a scalar register (the parameters cross the dependency wait,
+// after which the compiler no longer knows them uniform: every table read or branch on them
+// became a readfirstlane + scalar load of its own)
+DEV int fi_uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// Intra_Edge_Kernel[strength - 1][j] (spec 7.11.2.12, av1r_edge_kernel): {0,4,8,4,0},
+// {0,5,6,5,0}, {2,4,4,4,2} -- symmetric, as selects instead of table reads
+DEV int fi_ek0(int str) { return str == 3 ? 2 : 0; }
+DEV int fi_ek1(int str) { return str == 2 ? 5 : 4; }
+DEV int fi_ek2(int str) { return str == 1 ? 8 : str == 2 ? 6 : 4; }
+
 template <int MAX>
-DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F, TbLds<MAX>& L, const GranEdges& G, uint2 res,
+DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<MAX>& L, const GranEdges& G, uint2 res,
     uint32_t epoch, RingView ring, bool gran)
 {
+    FiParams F;
+    F.cls = fi_uni(F0.cls);
+    F.log2W = fi_uni(F0.log2W);
+    F.log2H = fi_uni(F0.log2H);
+    F.hA = fi_uni(F0.hA) != 0;
+    F.hL = fi_uni(F0.hL) != 0;
+    F.cfl = fi_uni(F0.cfl) != 0;
+    F.aboveLimit = fi_uni(F0.aboveLimit);
+    F.leftLimit = fi_uni(F0.leftLimit);
+    F.strA = fi_uni(F0.strA);
+    F.strL = fi_uni(F0.strL);
+    F.nA = fi_uni(F0.nA);
+    F.nL = fi_uni(F0.nL);
+    F.nUA = fi_uni(F0.nUA);
+    F.nUL = fi_uni(F0.nUL);
+    F.corner = fi_uni(F0.corner);
+    F.dx = fi_uni(F0.dx);
+    F.dy = fi_uni(F0.dy);
+    F.alpha = fi_uni(F0.alpha);
+    F.maxLW = fi_uni(F0.maxLW);
+    F.maxLH = fi_uni(F0.maxLH);
     const int t = coop_lane<64>();
     const int plane = tb.plane, x = tb.x, y = tb.y;
     const int log2W = F.log2W, log2H = F.log2H, w = 1 << log2W, h = 1 << log2H;
@@ -155,38 +186,32 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F, TbLds<M
     const int cs = F.corner ? r2(rawL(0) * 5 + corner0 * 6 + rawA(0) * 5, 4) : corner0;
     uint8_t* EA = I.above + EDGE_OFF;
     uint8_t* EL = I.left + EDGE_OFF;
-    // one pass: lane l writes AboveRow[l - 1] and LeftCol[l - 1] (edge-filtered where the
-    // filter reaches; index -1 is the (filtered) corner)
+    // AboveRow / LeftCol in two passes with no per-tap branching: lane l writes the filter
+    // input e[l] (e[0] the corner or its filtered value, e[k] = raw [k - 1]); where a side is
+    // filtered, a second pass runs the 5-tap filter over e[] (clamped indices, plain LDS
+    // reads) into AboveRow / LeftCol; where no side is, e[] already is them (EA = eA + 1)
+    const bool filt = (F.strA | F.strL) != 0;
+    uint8_t* eA = filt ? I.upA : EA - 1;
+    uint8_t* eL = filt ? I.upL : EL - 1;
     if (t <= w + h) {
-        int a, l;
-        if (t == 0) {
-            a = l = cs;
-        } else {
-            if (F.strA && t < F.nA) {
-                int s = 0;
-#pragma unroll
-                for (int j = 0; j < 5; j++) {
-                    const int m = CLIP3(0, F.nA - 1, t - 2 + j);
-                    s += stab(av1r_edge_kernel[F.strA - 1], j) * (m == 0 ? cs : rawA(m - 1));
-                }
-                a = (s + 8) >> 4;
-            } else {
-                a = rawA(t - 1);
+        eA[t] = (uint8_t)(t == 0 ? cs : rawA(t - 1));
+        eL[t] = (uint8_t)(t == 0 ? cs : rawL(t - 1));
+    }
+    if (filt) {
+        coop_sync<64>();
+        if (t <= w + h) {
+            int a = eA[t], l = eL[t];
+            if (F.strA && t >= 1 && t < F.nA) {
+                const int n1 = F.nA - 1, k0 = fi_ek0(F.strA), k1 = fi_ek1(F.strA), k2 = fi_ek2(F.strA);
+                a = (k0 * (eA[imax(t - 2, 0)] + eA[imin(t + 2, n1)]) + k1 * (eA[t - 1] + eA[imin(t + 1, n1)]) + k2 * a + 8) >> 4;
             }
-            if (F.strL && t < F.nL) {
-                int s = 0;
-#pragma unroll
-                for (int j = 0; j < 5; j++) {
-                    const int m = CLIP3(0, F.nL - 1, t - 2 + j);
-                    s += stab(av1r_edge_kernel[F.strL - 1], j) * (m == 0 ? cs : rawL(m - 1));
-                }
-                l = (s + 8) >> 4;
-            } else {
-                l = rawL(t - 1);
+            if (F.strL && t >= 1 && t < F.nL) {
+                const int n1 = F.nL - 1, k0 = fi_ek0(F.strL), k1 = fi_ek1(F.strL), k2 = fi_ek2(F.strL);
+                l = (k0 * (eL[imax(t - 2, 0)] + eL[imin(t + 2, n1)]) + k1 * (eL[t - 1] + eL[imin(t + 1, n1)]) + k2 * l + 8) >> 4;
             }
+            EA[t - 1] = (uint8_t)a;
+            EL[t - 1] = (uint8_t)l;
         }
-        EA[t - 1] = (uint8_t)a;
-        EL[t - 1] = (uint8_t)l;
     }
     coop_sync<64>();
     trace_stamp(G.tr, 12);

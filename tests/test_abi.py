@@ -178,3 +178,37 @@ def test_cycle_source_bounds(native_lib):
     counts = (C.c_int64 * 1)()
     assert native_lib.av1r_pipeline_launched(None, counts, 1) == abi.AV1R_E_INVALID
     native_lib.av1r_pipeline_close(None)  # a no-op
+
+
+def test_lean_intra_constants_match_the_tables():
+    """intra_fast.h restates two spec tables as immediates (the smooth weights of sides 4,
+    8, 16 and the intra edge kernel): they must equal av1r_tables.h / av1r_consts.h."""
+    root = native.ROOT
+    src = open(os.path.join(root, "av1dec_amd", "csrc", "intra_fast.h")).read()
+    tab = open(os.path.join(root, "include", "av1r_tables.h")).read()
+    body = tab[tab.index("av1r_sm_weights[124]"):]
+    sm = [int(v) for v in re.findall(r"\d+", body[body.index("{"):body.index("}")])][:28]
+    fn = src[src.index("DEV uint32_t fi_smw"):]
+    fn = fn[:fn.index("\n}")]
+    words = [int(h, 16) for h in re.findall(r"0x([0-9a-f]{8})u", fn)]
+    got = [(w >> (8 * b)) & 0xff for w in words for b in range(4)]
+    assert got == sm  # 4: words[0]; 8: words[1..2]; 16: words[3..6]
+    cst = open(os.path.join(root, "include", "av1r_consts.h")).read()
+    ek = cst[cst.index("av1r_edge_kernel[3][5]"):]
+    ek = [int(v) for v in re.findall(r"\d+", ek[ek.index("{"):ek.index(";")])]
+    kern = [ek[5 * i:5 * i + 5] for i in range(3)]
+
+    def sel(name, s):  # evaluate fi_ek0/1/2 of intra_fast.h for strength s
+        f = src[src.index(f"DEV int {name}(int str)"):]
+        expr = f[f.index("return") + 6:f.index(";")].strip()
+        def tern(e):  # C's right-associative  c ? a : rest
+            if "?" not in e:
+                return int(e)
+            c, rest = e.split("?", 1)
+            a, rest = rest.split(":", 1)
+            return int(a) if eval(c.replace("str", str(s)), {}) else tern(rest.strip())
+        return tern(expr)
+    for s in (1, 2, 3):
+        k = kern[s - 1]
+        assert k == k[::-1]
+        assert [sel("fi_ek0", s), sel("fi_ek1", s), sel("fi_ek2", s)] == k[:3], s
