@@ -676,6 +676,8 @@ static void build_strips(av1r_ctx* c, const av1r_frame_batch* b)
 // outside inter-intra blocks -- finished by k_resid before k_flow -- get no node, item or
 // level: only the level launches need them.  c->levelsOk says whether the level schedule
 // was built too.
+// AV1R_PACK_FUSED=0: the map walks one by one (the fused walks must pack identical bytes)
+static const bool g_packFused = !getenv("AV1R_PACK_FUSED") || atoi(getenv("AV1R_PACK_FUSED")) != 0;
 static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
 {
     const av1r_frame_hdr* h = b->hdr;
@@ -798,6 +800,18 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             for (int x = x0; x < x1; x++) row[x].lvl = (int16_t)lv;
         }
     };
+    auto region_own_set = [&](int p, int x0, int y0, int w4, int h4, int lv, int32_t node) {  // both at once
+        if (x0 + w4 > c->mapW[p] || y0 + h4 > c->mapH[p]) {
+            if (c->granOk && getenv("AV1R_GRAN_DEBUG")) fprintf(stderr, "outside: plane %d %d,%d %dx%d\n", p, x0, y0, w4, h4);
+            c->granOk = false;
+        }
+        int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
+        for (int y = y0; y < y1; y++) {
+            av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
+            const uint8_t last = y == y0 + h4 - 1 ? 1 : 0;
+            for (int x = x0; x < x1; x++) row[x] = av1r_ctx::MapUnit{node, (int16_t)lv, (uint8_t)(last | (x == x0 + w4 - 1 ? 2 : 0)), 0};
+        }
+    };
     // Latest level among the pixels coop_intra_predict reads for a w x h prediction at
     // pixel (x, y) of plane p with the given edge availability (IntraPredict.cpp:563-631):
     // row y-1 over [x-1 | x, x + (AR ? 2w : w) - 1], column x-1 over [y-1 | y, y + (BL ? 2h : h) - 1];
@@ -806,6 +820,44 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         int m = -1;
         if (hA) m = std::max(m, region_max(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2));
         if (hL) m = std::max(m, region_max(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2));
+        return m;
+    };
+    // granule mode: edge_level and edge_owners in one walk over the same units (the above
+    // run, the left run, the corner); returns the latest level
+    auto edge_scan = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int slot) {
+        int m = -1;
+        uint32_t* mw = nm + 4 * slot;
+        const int W = c->mapW[p], H = c->mapH[p];
+        const av1r_ctx::MapUnit* map = c->umap[p].data();
+        auto unit = [&](int ux, int uy, int bit, uint32_t* word, uint8_t need) {
+            if (ux < 0 || uy < 0 || ux >= W || uy >= H) return;
+            const av1r_ctx::MapUnit& mu = map[(size_t)uy * W + ux];
+            m = std::max<int>(m, mu.lvl);
+            if (mu.owner < 0) return;
+            *word |= 1u << bit;
+            if (!(mu.emit & need)) c->granOk = false;
+        };
+        if (hA) {
+            const int u0 = x >> 2, u1 = (x + (hAR ? 2 * w : w) - 1) >> 2, uy = (y - 1) >> 2;
+            if (u1 - u0 >= 32) c->granOk = false;
+            for (int u = u0; u <= u1 && u - u0 < 32; u++) unit(u, uy, u - u0, mw, 1);
+        }
+        if (hL) {
+            const int u0 = y >> 2, u1 = (y + (hBL ? 2 * h : h) - 1) >> 2, ux = (x - 1) >> 2;
+            if (u1 - u0 >= 32) c->granOk = false;
+            for (int u = u0; u <= u1 && u - u0 < 32; u++) unit(ux, u, u - u0, mw + 2, 2);
+        }
+        if (hA && hL) {
+            const int ux = (x - 1) >> 2, uy = (y - 1) >> 2;
+            if (ux >= 0 && uy >= 0 && ux < W && uy < H) {
+                const av1r_ctx::MapUnit& mu = map[(size_t)uy * W + ux];
+                m = std::max<int>(m, mu.lvl);
+                if (mu.owner >= 0) {
+                    mw[1] = (mu.emit & 1) ? 1u : 3u;
+                    if (!mu.emit) c->granOk = false;
+                }
+            }
+        }
         return m;
     };
     auto push = [&](std::vector<std::vector<uint32_t>>& v, int lv, uint32_t item) {
@@ -874,8 +926,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 if (!pal) {
                     const bool hL = t.flags & AV1R_TB_HAVE_LEFT, hA = t.flags & AV1R_TB_HAVE_ABOVE;
                     const bool hAR = t.flags & AV1R_TB_HAVE_AR, hBL = t.flags & AV1R_TB_HAVE_BL;
-                    dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
-                    edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0);
+                    if (c->granOk && g_packFused) {
+                        dep = edge_scan(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0);
+                    } else {
+                        dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
+                        edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0);
+                    }
                     if (p && blk.uv_mode == AV1R_UV_CFL_PRED) {  // the co-located luma (incl. sub-8x8 neighbours)
                         const int lx0 = t.x >> 1, ly0 = t.y >> 1, lx1 = (2 * (t.x + w) - 1) >> 2, ly1 = (2 * (t.y + hh) - 1) >> 2;
                         dep = std::max({dep, lumaMax, region_max(0, lx0, ly0, lx1, ly1)});
@@ -890,11 +946,15 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             if (p == 0) lumaMax = std::max(lumaMax, lv);
             push(c->lvT, lv, AV1R_ITEM(AV1R_ITEM_TB, ti));
             globalMax = std::max(globalMax, lv);
-            region_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv);
             const int32_t node = c->nodeOfTb[ti] = end_node();
             // an inter TB's pixels are final before k_flow (k_inter + k_resid) unless the
             // block is inter-intra, whose blend item adds the residuals
-            if (!inter) own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, node);
+            if (!inter && g_packFused) {
+                region_own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv, node);
+            } else {
+                region_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv);
+                if (!inter) own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, node);
+            }
         }
     }
     static const bool granDbg = getenv("AV1R_GRAN_DEBUG") != nullptr;
@@ -2161,6 +2221,13 @@ void av1r_packed_free(av1r_packed* pk)
 }
 
 size_t av1r_packed_bytes(const av1r_packed* pk) { return pk ? pk->P.upBytes : 0; }
+
+const void* av1r_packed_data(const av1r_packed* pk, size_t* bytes)
+{
+    if (!pk) return nullptr;
+    if (bytes) *bytes = pk->P.upBytes;
+    return pk->host;
+}
 
 // AV1R_PIPE_PROF=1: where av1r_decode_packed_batch spends the launcher's time (seconds,
 // summed; printed by av1r_pipeline_run): waiting for an upload slot (the GPU three frames

@@ -249,6 +249,9 @@ typedef struct av1r_packed av1r_packed;
 int av1r_pack(const av1r_frame_batch* batch, av1r_packed** out);
 void av1r_packed_free(av1r_packed* p);
 size_t av1r_packed_bytes(const av1r_packed* p);
+/* The packed frame's host bytes that travel to the device (*bytes: their count): for
+ * inspection and tests (e.g. that packing is deterministic). */
+const void* av1r_packed_data(const av1r_packed* p, size_t* bytes);
 const char* av1r_pack_last_error(void);
 int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* frames, int n);
 /* Profiling hook (environment AV1R_PACK_PROF=1): ns[0..5] = nanoseconds all threads spent

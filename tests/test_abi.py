@@ -212,3 +212,14 @@ def test_lean_intra_constants_match_the_tables():
         k = kern[s - 1]
         assert k == k[::-1]
         assert [sel("fi_ek0", s), sel("fi_ek1", s), sel("fi_ek2", s)] == k[:3], s
+
+
+def test_pack_walks_fused_and_separate_pack_the_same_bytes():
+    """build_schedule's fused map walks (edge level + owners in one pass, level + owner
+    painting in one pass) pack byte-identical batches to the separate walks."""
+    import subprocess
+    import sys
+    tool = os.path.join(native.ROOT, "tools", "pack_digest.py")
+    out = [subprocess.run([sys.executable, tool, "40"], capture_output=True, text=True, timeout=600,
+                          env=dict(os.environ, AV1R_PACK_FUSED=v)).stdout.split() for v in ("1", "0")]
+    assert out[0] and out[0] == out[1]
