@@ -180,9 +180,17 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     const uint8_t* ta = I.tmp;
     const uint8_t* tl = I.tmp2;
     const int aLim = F.aboveLimit - x, lLim = F.leftLimit - y;
-    const int corner0 = F.hA && F.hL ? tl[4 * 39 + 3] : F.hA ? ta[0] : F.hL ? tl[0] : 128;
-    auto rawA = [&](int i) -> int { return F.hA ? ta[imin(aLim, i)] : F.hL ? tl[0] : 127; };
-    auto rawL = [&](int i) -> int { return F.hL ? tl[imin(lLim, i)] : F.hA ? ta[0] : 129; };
+    // each edge value is one LDS byte at a uniformly chosen base and clamp, or a constant:
+    // no branches, so every read of the pass goes out before the one wait
+    const uint8_t* bA = F.hA ? ta : tl;  // (!hA: the left neighbour (x - 1, y) stands in)
+    const uint8_t* bL = F.hL ? tl : ta;
+    const int cA = F.hA ? aLim : 0, cL = F.hL ? lLim : 0;
+    const int kA = F.hA || F.hL ? -1 : 127, kL = F.hA || F.hL ? -1 : 129;  // neither edge: constants
+    auto rawA = [&](int i) -> int { const int v = bA[imin(cA, i)]; return kA >= 0 ? kA : v; };
+    auto rawL = [&](int i) -> int { const int v = bL[imin(cL, i)]; return kL >= 0 ? kL : v; };
+    const uint8_t* bC = F.hA && F.hL ? tl + 4 * 39 + 3 : F.hA ? ta : tl;
+    const int c0 = *bC;
+    const int corner0 = F.hA || F.hL ? c0 : 128;
     const int cs = F.corner ? r2(rawL(0) * 5 + corner0 * 6 + rawA(0) * 5, 4) : corner0;
     uint8_t* EA = I.above + EDGE_OFF;
     uint8_t* EL = I.left + EDGE_OFF;
@@ -350,8 +358,22 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
         // granules from the registers: the bottom row's units are the last row's quads; a
         // right-column unit is byte 3 of four vertically adjacent quads
         const uint64_t tag = (uint64_t)epoch << 32;
-        const int src = imin(t + w4, 63), src2 = imin(t + 2 * w4, 63), src3 = imin(t + 3 * w4, 63);
-        const uint32_t o1 = __shfl(o, src, 64), o2 = __shfl(o, src2, 64), o3 = __shfl(o, src3, 64);
+        // the quads below in the same 16-lane DPP row (a publishing lane is the row's
+        // lane w4 - 1 + 4 * w4 * k, so its three partners t + w4, + 2 w4, + 3 w4 stay in the row)
+        uint32_t o1, o2, o3;
+        if (w4 == 1) {
+            o1 = __builtin_amdgcn_update_dpp(0, (int)o, 0x101, 0xf, 0xf, true);  // row_shl:1
+            o2 = __builtin_amdgcn_update_dpp(0, (int)o, 0x102, 0xf, 0xf, true);
+            o3 = __builtin_amdgcn_update_dpp(0, (int)o, 0x103, 0xf, 0xf, true);
+        } else if (w4 == 2) {
+            o1 = __builtin_amdgcn_update_dpp(0, (int)o, 0x102, 0xf, 0xf, true);
+            o2 = __builtin_amdgcn_update_dpp(0, (int)o, 0x104, 0xf, 0xf, true);
+            o3 = __builtin_amdgcn_update_dpp(0, (int)o, 0x106, 0xf, 0xf, true);
+        } else {
+            o1 = __builtin_amdgcn_update_dpp(0, (int)o, 0x104, 0xf, 0xf, true);
+            o2 = __builtin_amdgcn_update_dpp(0, (int)o, 0x108, 0xf, 0xf, true);
+            o3 = __builtin_amdgcn_update_dpp(0, (int)o, 0x10c, 0xf, 0xf, true);
+        }
         if (t < nq && qi == h - 1)
             __hip_atomic_store(k.gran_h[plane] + (size_t)((y + h - 1) >> 2) * k.gran_w[plane] + (x >> 2) + (qj >> 2), tag | o,
                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -81,6 +81,24 @@ def main():
     for r in rows:
         print("%5d %6d %9.1f %8.1f %8.1f %8.1f %8.1f %8.2f" % r)
     print(f"total: work {tot_work / 1e3:.2f} ms, cross-strip waits {tot_wait / 1e3:.2f} ms, gaps {tot_gap / 1e3:.2f} ms")
+    if ok.any():
+        # the critical (last-ending) strip's groups by kind: large TBs (a side > 16, the
+        # whole workgroup on the generic path), inter-intra blends, small TBs (one per wave)
+        TXW = [4, 8, 16, 32, 64, 4, 8, 8, 16, 16, 32, 32, 64, 4, 16, 8, 32, 16, 64]
+        TXH = [4, 8, 16, 32, 64, 8, 4, 16, 8, 32, 16, 64, 32, 16, 4, 32, 8, 64, 16]
+        crit = max(rows, key=lambda r: r[3])[0]
+        ms = ok & (strip == crit)
+        kinds = {"large": [], "blend": [], "small": []}
+        for g in np.unique(grp[ms]):
+            mg = ms & (grp == g)
+            big = any(max(TXW[t], TXH[t]) > 16 for t in txs[mg])
+            k = "blend" if (kind[mg] != 0).any() else "large" if big else "small"
+            kinds[k].append((us(gend[mg].max() - t2[mg].min()), int(mg.sum())))
+        for k, v in kinds.items():
+            if v:
+                d = np.array([x[0] for x in v])
+                print(f"  strip {crit} {k:5s} groups {len(v):5d} items {sum(x[1] for x in v):5d} "
+                      f"dur p50 {np.median(d):.2f} mean {d.mean():.2f} sum {d.sum() / 1e3:.2f} ms")
     # median group phases (large vs small): item entry -> wait done, wait -> edges, ...
     w = us(t4 - t3).sum()
     tot = us(t5 - t2).sum()
