@@ -54,7 +54,7 @@ def main():
         w = write.get(st, 0.0) / max(nw, 1)
         stages[st] = {"fetch_bytes_raw": round(f), "fetch_bytes_x2": round(2 * f), "write_bytes": round(w),
                       "traffic_bytes": round(2 * f + w)}
-    res = {"config": "1080p", "streams": int(sys.argv[3]) if len(sys.argv) > 3 else 8,
+    res = {"config": sys.argv[4] if len(sys.argv) > 4 else "1080p", "streams": int(sys.argv[3]) if len(sys.argv) > 3 else 8,
            "frames_fetch": nf, "frames_write": nw,
            "git_head": os.environ.get("AV1R_GIT_HEAD"),  # the commit the counters were collected at (no .git on the box)
            "unit": "bytes per frame (per stage, all launches of the frame)",
