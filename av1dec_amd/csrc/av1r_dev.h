@@ -330,8 +330,9 @@ DEV void stp_c(const DevPlane& p, int x, int y, uint8_t v, bool coh)
 // arrives in a granule, after the wait that orders it; in k_strip it is a granule (another
 // strip's) or a ring read (this strip's).  (3) Its writer stores it sc1 in k_flow (stp4<true>,
 // stp_c with coh), and publishes a granule or a done flag if a consumer's wait names it.
-// The read sites today: coop_intra_edges_gran (intra_dev.h), tb_predict's CFL luma and
-// ii_item's edges and inter prediction (recon.hip); each is marked "(flow read site)".
+// The read sites today: gran_gather (intra_dev.h), tb_predict's CFL luma, fi_run's CFL
+// luma (intra_fast.h) and ii_item's edges and inter prediction (recon.hip); each is marked
+// "(flow read site)".  Scalar loads (sload / stab / sfield) are for batch data only.
 DEV bool strip_plain(int kstrip, bool gran) { return kstrip && gran; }  // (k_strip runs only with granules)
 
 // Work-item encoding of the per-level item lists (host schedule -> k_level):
