@@ -146,9 +146,9 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     const int log2W = F.log2W, log2H = F.log2H, w = 1 << log2W, h = 1 << log2H;
     const DevPlane& dst = k.cur.pl[plane];
     IntraLds& I = L.intra;
-    gran_gather<64>(dst, plane, x, y, F.hL, F.hA, F.aboveLimit, F.leftLimit, I, G);
     // CFL: the co-located luma of this lane's four pixels (flow read site: the block's luma,
-    // written by earlier items -- sc1 loads after the dependency wait, or this strip's ring)
+    // written by earlier items -- sc1 loads after the dependency wait, or this strip's ring),
+    // issued before the edge gather so that its loads overlap the granule polls
     const int nq = (w * h) >> 2;
     const int w4 = w >> 2;
     const int qi = t >> (log2W - 2), qj = (t & (w4 - 1)) << 2;  // this lane's quad: row, first column
@@ -174,6 +174,7 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
             }
         }
     }
+    gran_gather<64>(dst, plane, x, y, F.hL, F.hA, F.aboveLimit, F.leftLimit, I, G);
     coop_sync<64>();  // (wave level: the units are in LDS)
     trace_stamp(G.tr, 8);
     // raw AboveRow / LeftCol (coop_intra_edges' assembly, read in place from the units)
@@ -350,10 +351,7 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     }
     trace_stamp(G.tr, 9);
     const uint32_t o = add4(p, res);
-    if (t < nq) {
-        stp4_c(dst, x + qj, y + qi, o, G.coh);
-        if (ring.on) *reinterpret_cast<lds_u32*>(ring_px(ring, plane, x + qj, y + qi)) = o;
-    }
+    // the granules first (what the next items wait for), then the frame
     if (gran && (!ring.on || (tb.pub & 2))) {
         // granules from the registers: the bottom row's units are the last row's quads; a
         // right-column unit is byte 3 of four vertically adjacent quads
@@ -382,5 +380,9 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
             __hip_atomic_store(k.gran_v[plane] + (size_t)((x + w - 1) >> 2) * k.gran_hn[plane] + (y >> 2) + (qi >> 2), tag | v,
                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+    if (t < nq) {
+        stp4_c(dst, x + qj, y + qi, o, G.coh);
+        if (ring.on) *reinterpret_cast<lds_u32*>(ring_px(ring, plane, x + qj, y + qi)) = o;
     }
 }
