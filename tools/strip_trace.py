@@ -60,6 +60,31 @@ def main():
         q = lambda x, y: np.percentile(us(x[mm] - y[mm]), [50, 90])
         print(f"  tx {ts:2d} n={mm.sum():6d} resid %.2f/%.2f wait %.2f/%.2f edges %.2f/%.2f predict %.2f/%.2f store %.2f/%.2f publish %.2f/%.2f"
               % (*q(t3, t2), *q(t4, t3), *q(t8, t4), *q(t9, t8), *q(t10, t9), *q(t5, t10)))
+    # k_flow: what paces the chain -- per level (slot 6, written by the host), the time from
+    # the previous level's last store to this level's, attributed to the kind of the item
+    # that stored last (its transform size; blends as -1)
+    lvl = a[:, 6]
+    if (lvl > 0).any() and not (a[:, 15] > 0).any():
+        order = np.argsort(lvl, kind="stable")
+        lv_sorted = lvl[order]
+        bounds = np.flatnonzero(np.diff(lv_sorted)) + 1
+        groups = np.split(order, bounds)
+        prev = None
+        pace = {}
+        for g in groups:
+            e = t10[g] if (t10[g] > 0).all() else t5[g]
+            j = g[np.argmax(e)]
+            end = e.max()
+            if prev is not None and end > prev:
+                key = -1 if kind[j] != 0 else int(txs[j])
+                d = pace.setdefault(key, [0, 0.0])
+                d[0] += 1
+                d[1] += us(end - prev)
+            prev = end if prev is None else max(prev, end)
+        tot = sum(v[1] for v in pace.values())
+        print(f"levels {len(groups)}; chain advance {tot / 1e3:.2f} ms, by the kind of the level's last item:")
+        for key, (n, t) in sorted(pace.items(), key=lambda kv: -kv[1][1]):
+            print(f"  {'blend' if key < 0 else 'tx %2d' % key}: {n:5d} levels, {t / 1e3:.3f} ms ({t / max(n, 1):.2f} us each)")
     # per strip (slot 14: strip << 32 | group, 15: the group's end after the barrier)
     strip, grp, gend = a[:, 14] >> 32, a[:, 14] & 0xffffffff, a[:, 15]
     ok = gend > 0
