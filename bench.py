@@ -346,7 +346,7 @@ def load_traffic(path, config, S, stage):
     return None, None
 
 
-def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, prime_s=1.0):
+def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, prime_s=2.0):
     """One configuration's rates on this rank's streams: the host-inclusive pipeline (the
     headline), the device-only rate, and the per-stage device time with the roofline of the
     dominant stage.  Returns (result dict, the StreamScheduler over prepared handles, the
