@@ -252,7 +252,21 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     if (F.cls == FI_DC) {
         int v = (F.hA && t < w ? EA[t] : 0) + (F.hL && t < h ? EL[t] : 0);
         const int s = __builtin_amdgcn_readlane(fi_row_sum(v), 15);
-        if (F.hA && F.hL) dc = (s + ((w + h) >> 1)) / (w + h);
+        if (F.hA && F.hL) {
+            // (s + (w + h) / 2) / (w + h): a shift when square; otherwise w + h = 3 << k or
+            // 5 << k (sides 4..16): the quotient from a float reciprocal, then corrected
+            // by one either way (n < 2^14: exact within one ulp)
+            const int n = s + ((w + h) >> 1);
+            if (log2W == log2H) {
+                dc = n >> (log2W + 1);
+            } else {
+                const int d = w + h;
+                int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+                q += (q + 1) * d <= n;
+                q -= q * d > n;
+                dc = q;
+            }
+        }
         else if (F.hL) dc = clip1((s + (h >> 1)) >> log2H);
         else if (F.hA) dc = clip1((s + (w >> 1)) >> log2W);
     }
@@ -354,7 +368,8 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     // the granules first (what the next items wait for), then the frame
     if (gran && (!ring.on || (tb.pub & 2))) {
         // granules from the registers: the bottom row's units are the last row's quads; a
-        // right-column unit is byte 3 of four vertically adjacent quads
+        // right-column unit is byte 3 of four vertically adjacent quads (the plane's granule
+        // arrays from G, set up before the wait: no dependent parameter load here)
         const uint64_t tag = (uint64_t)epoch << 32;
         // the quads below in the same 16-lane DPP row (a publishing lane is the row's
         // lane w4 - 1 + 4 * w4 * k, so its three partners t + w4, + 2 w4, + 3 w4 stay in the row)
@@ -373,11 +388,11 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
             o3 = __builtin_amdgcn_update_dpp(0, (int)o, 0x10c, 0xf, 0xf, true);
         }
         if (t < nq && qi == h - 1)
-            __hip_atomic_store(k.gran_h[plane] + (size_t)((y + h - 1) >> 2) * k.gran_w[plane] + (x >> 2) + (qj >> 2), tag | o,
+            __hip_atomic_store(const_cast<uint64_t*>(G.h) + (size_t)((y + h - 1) >> 2) * G.gw + (x >> 2) + (qj >> 2), tag | o,
                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t < nq && qj == w - 4 && (qi & 3) == 0) {
             const uint32_t v = (o >> 24) | ((o1 >> 24) << 8) | ((o2 >> 24) << 16) | ((o3 >> 24) << 24);
-            __hip_atomic_store(k.gran_v[plane] + (size_t)((x + w - 1) >> 2) * k.gran_hn[plane] + (y >> 2) + (qi >> 2), tag | v,
+            __hip_atomic_store(const_cast<uint64_t*>(G.v) + (size_t)((x + w - 1) >> 2) * G.gh + (y >> 2) + (qi >> 2), tag | v,
                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
