@@ -138,6 +138,8 @@ struct av1r_ctx {
     Upload meta[kMetaRing];
     int metaIdx = 0;
     hipStream_t copyStream = nullptr;
+    hipStream_t aux = nullptr;              // k_inter_m / k_inter_s beside k_inter (AV1R_INTER_SPLIT)
+    hipEvent_t auxGo = nullptr, auxDone = nullptr;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
     // this context's latest work was launched on joinLead's stream (a batch it was a member
     // of) and nothing has been enqueued on its own stream since; ctx_join() orders its own
@@ -1637,10 +1639,25 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     uint32_t traceBase = 0;
     static std::atomic<uint32_t> epochs{0};
     if (flow) {
-        // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch
+        // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch.
+        // AV1R_INTER_SPLIT=1: the plain tiles (k_inter_m, k_inter_s) on the context's second
+        // stream beside the general k_inter (disjoint tiles).  Measured (tools/gpu_env_ab.sh):
+        // 4K x 2 streams device-only +3 % (inter 0.281 -> 0.245 ms/frame), 1080p x 8 -6 %
+        // (0.073 -> 0.087): off by default
+        static const bool split = getenv("AV1R_INTER_SPLIT") && atoi(getenv("AV1R_INTER_SPLIT")) != 0;
+        const bool aux = split && lc->aux && total[0] && (total[1] || total[2]) && !trace;
+        hipStream_t sp = aux ? lc->aux : st;
+        if (aux) {
+            HIPCHK(hipEventRecord(lc->auxGo, st));
+            HIPCHK(hipStreamWaitEvent(lc->aux, lc->auxGo, 0));
+        }
+        if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, sp);
+        if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, sp);
         if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
-        if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, st);
-        if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, st);
+        if (aux) {
+            HIPCHK(hipEventRecord(lc->auxDone, lc->aux));
+            HIPCHK(hipStreamWaitEvent(st, lc->auxDone, 0));
+        }
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
@@ -1873,6 +1890,9 @@ int av1r_create(int device, av1r_ctx** out)
     }
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->joinEv, hipEventDisableTiming);
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
+    (void)hipEventCreateWithFlags(&c->auxGo, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->auxDone, hipEventDisableTiming);
     for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
@@ -1895,6 +1915,7 @@ void av1r_destroy(av1r_ctx* c)
     }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
     {  // members of its batches: their pending join on its (now drained) stream is satisfied
         std::lock_guard<std::mutex> lock(g_ctxMu);
         for (av1r_ctx* m : g_ctxs)
@@ -1916,6 +1937,9 @@ void av1r_destroy(av1r_ctx* c)
     for (auto& u : c->meta) freeUpload(u);
     (void)hipStreamSynchronize(c->copyStream);
     (void)hipStreamDestroy(c->copyStream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    (void)hipEventDestroy(c->auxGo);
+    (void)hipEventDestroy(c->auxDone);
     if (c->resDev) (void)hipFree(c->resDev);
     if (c->granDev) (void)hipFree(c->granDev);
     {  // its stream leaves the device's k_flow chain (no later wait refers to it)
