@@ -195,62 +195,67 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     const int cs = F.corner ? r2(rawL(0) * 5 + corner0 * 6 + rawA(0) * 5, 4) : corner0;
     uint8_t* EA = I.above + EDGE_OFF;
     uint8_t* EL = I.left + EDGE_OFF;
-    // AboveRow / LeftCol in two passes with no per-tap branching: lane l writes the filter
-    // input e[l] (e[0] the corner or its filtered value, e[k] = raw [k - 1]); where a side is
-    // filtered, a second pass runs the 5-tap filter over e[] (clamped indices, plain LDS
-    // reads) into AboveRow / LeftCol; where no side is, e[] already is them (EA = eA + 1)
-    const bool filt = (F.strA | F.strL) != 0;
-    uint8_t* eA = filt ? I.upA : EA - 1;
-    uint8_t* eL = filt ? I.upL : EL - 1;
-    if (t <= w + h) {
-        eA[t] = (uint8_t)(t == 0 ? cs : rawA(t - 1));
-        eL[t] = (uint8_t)(t == 0 ? cs : rawL(t - 1));
-    }
-    if (filt) {
-        coop_sync<64>();
-        if (t <= w + h) {
-            int a = eA[t], l = eL[t];
-            if (F.strA && t >= 1 && t < F.nA) {
-                const int n1 = F.nA - 1, k0 = fi_ek0(F.strA), k1 = fi_ek1(F.strA), k2 = fi_ek2(F.strA);
-                a = (k0 * (eA[imax(t - 2, 0)] + eA[imin(t + 2, n1)]) + k1 * (eA[t - 1] + eA[imin(t + 1, n1)]) + k2 * a + 8) >> 4;
-            }
-            if (F.strL && t >= 1 && t < F.nL) {
-                const int n1 = F.nL - 1, k0 = fi_ek0(F.strL), k1 = fi_ek1(F.strL), k2 = fi_ek2(F.strL);
-                l = (k0 * (eL[imax(t - 2, 0)] + eL[imin(t + 2, n1)]) + k1 * (eL[t - 1] + eL[imin(t + 1, n1)]) + k2 * l + 8) >> 4;
-            }
-            EA[t - 1] = (uint8_t)a;
-            EL[t - 1] = (uint8_t)l;
-        }
-    }
-    coop_sync<64>();
-    trace_stamp(G.tr, 12);
-    // upsampling: buf[2i - 1], buf[2i] from the edge (index -2 .. 2n - 2)
+    // the directional classes build AboveRow / LeftCol (edge filter, upsampling) in LDS;
+    // the others (DC, V, H, smooth, Paeth: no filter, no upsampling) read the units directly
+    const bool dirc = F.cls == FI_Z1 || F.cls == FI_Z2 || F.cls == FI_Z3;
     const uint8_t* A = EA;
     const uint8_t* Lc = EL;
-    if (F.nUA | F.nUL) {
-#pragma unroll
-        for (int side = 0; side < 2; side++) {
-            const int n = side ? F.nUL : F.nUA;
-            if (!n) continue;
-            const uint8_t* e = side ? EL : EA;
-            uint8_t* buf = (side ? I.upL : I.upA) + EDGE_OFF;
-            if (t < n) {
-                const int d0 = t == 0 ? e[-1] : e[t - 2];
-                const int d1 = e[t - 1], d2 = e[t];
-                const int d3 = t + 1 <= n - 1 ? e[t + 1] : e[n - 1];
-                buf[2 * t - 1] = (uint8_t)clip1(r2(-d0 + 9 * d1 + 9 * d2 - d3, 4));
-                buf[2 * t] = (uint8_t)d2;
+    if (dirc) {
+        // AboveRow / LeftCol in two passes with no per-tap branching: lane l writes the filter
+        // input e[l] (e[0] the corner or its filtered value, e[k] = raw [k - 1]); where a side is
+        // filtered, a second pass runs the 5-tap filter over e[] (clamped indices, plain LDS
+        // reads) into AboveRow / LeftCol; where no side is, e[] already is them (EA = eA + 1)
+        const bool filt = (F.strA | F.strL) != 0;
+        uint8_t* eA = filt ? I.upA : EA - 1;
+        uint8_t* eL = filt ? I.upL : EL - 1;
+        if (t <= w + h) {
+            eA[t] = (uint8_t)(t == 0 ? cs : rawA(t - 1));
+            eL[t] = (uint8_t)(t == 0 ? cs : rawL(t - 1));
+        }
+        if (filt) {
+            coop_sync<64>();
+            if (t <= w + h) {
+                int a = eA[t], l = eL[t];
+                if (F.strA && t >= 1 && t < F.nA) {
+                    const int n1 = F.nA - 1, k0 = fi_ek0(F.strA), k1 = fi_ek1(F.strA), k2 = fi_ek2(F.strA);
+                    a = (k0 * (eA[imax(t - 2, 0)] + eA[imin(t + 2, n1)]) + k1 * (eA[t - 1] + eA[imin(t + 1, n1)]) + k2 * a + 8) >> 4;
+                }
+                if (F.strL && t >= 1 && t < F.nL) {
+                    const int n1 = F.nL - 1, k0 = fi_ek0(F.strL), k1 = fi_ek1(F.strL), k2 = fi_ek2(F.strL);
+                    l = (k0 * (eL[imax(t - 2, 0)] + eL[imin(t + 2, n1)]) + k1 * (eL[t - 1] + eL[imin(t + 1, n1)]) + k2 * l + 8) >> 4;
+                }
+                EA[t - 1] = (uint8_t)a;
+                EL[t - 1] = (uint8_t)l;
             }
-            if (t == 0) buf[-2] = e[-1];
         }
         coop_sync<64>();
-        if (F.nUA) A = I.upA + EDGE_OFF;
-        if (F.nUL) Lc = I.upL + EDGE_OFF;
+        trace_stamp(G.tr, 12);
+        // upsampling: buf[2i - 1], buf[2i] from the edge (index -2 .. 2n - 2)
+        if (F.nUA | F.nUL) {
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                const int n = side ? F.nUL : F.nUA;
+                if (!n) continue;
+                const uint8_t* e = side ? EL : EA;
+                uint8_t* buf = (side ? I.upL : I.upA) + EDGE_OFF;
+                if (t < n) {
+                    const int d0 = t == 0 ? e[-1] : e[t - 2];
+                    const int d1 = e[t - 1], d2 = e[t];
+                    const int d3 = t + 1 <= n - 1 ? e[t + 1] : e[n - 1];
+                    buf[2 * t - 1] = (uint8_t)clip1(r2(-d0 + 9 * d1 + 9 * d2 - d3, 4));
+                    buf[2 * t] = (uint8_t)d2;
+                }
+                if (t == 0) buf[-2] = e[-1];
+            }
+            coop_sync<64>();
+            if (F.nUA) A = I.upA + EDGE_OFF;
+            if (F.nUL) Lc = I.upL + EDGE_OFF;
+        }
     }
     // DC (and CFL's DC): the edge sums over lanes 0..15 (w, h <= 16)
     int dc = 128;
     if (F.cls == FI_DC) {
-        int v = (F.hA && t < w ? EA[t] : 0) + (F.hL && t < h ? EL[t] : 0);
+        int v = (F.hA && t < w ? rawA(t) : 0) + (F.hL && t < h ? rawL(t) : 0);
         const int s = __builtin_amdgcn_readlane(fi_row_sum(v), 15);
         if (F.hA && F.hL) {
             // (s + (w + h) / 2) / (w + h): a shift when square; otherwise w + h = 3 << k or
@@ -278,8 +283,8 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
         const int upA = F.nUA ? 1 : 0, upL = F.nUL ? 1 : 0;
         switch (F.cls) {
         case FI_DC: p = (uint32_t)dc * 0x01010101u; break;
-        case FI_V: p = *reinterpret_cast<const uint32_t*>(EA + qj); break;
-        case FI_H: p = (uint32_t)EL[i] * 0x01010101u; break;
+        case FI_V: p = rawA(qj) | rawA(qj + 1) << 8 | rawA(qj + 2) << 16 | (uint32_t)rawA(qj + 3) << 24; break;
+        case FI_H: p = (uint32_t)rawL(i) * 0x01010101u; break;
         case FI_Z1: {
             const int idx = (i + 1) * F.dx;
             const int shift = ((idx << upA) >> 1) & 0x1F;
@@ -323,8 +328,8 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
             break;
         }
         case FI_PAETH: {
-            const uint32_t a4 = *reinterpret_cast<const uint32_t*>(EA + qj);
-            const int l = EL[i], tl0 = EA[-1];
+            const uint32_t a4 = rawA(qj) | rawA(qj + 1) << 8 | rawA(qj + 2) << 16 | (uint32_t)rawA(qj + 3) << 24;
+            const int l = rawL(i), tl0 = corner0;
 #pragma unroll
             for (int b = 0; b < 4; b++) {
                 const int a = (a4 >> (8 * b)) & 0xff;
@@ -335,10 +340,10 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
             break;
         }
         default: {  // SMOOTH, SMOOTH_V, SMOOTH_H
-            const uint32_t a4 = *reinterpret_cast<const uint32_t*>(EA + qj);
+            const uint32_t a4 = rawA(qj) | rawA(qj + 1) << 8 | rawA(qj + 2) << 16 | (uint32_t)rawA(qj + 3) << 24;
             const uint32_t wx4 = fi_smw(log2W, qj >> 2);
             const int wy = (fi_smw(log2H, i >> 2) >> (8 * (i & 3))) & 0xff;
-            const int l = EL[i], bl = EL[h - 1], tr = EA[w - 1];
+            const int l = rawL(i), bl = rawL(h - 1), tr = rawA(w - 1);
 #pragma unroll
             for (int b = 0; b < 4; b++) {
                 const int a = (a4 >> (8 * b)) & 0xff, wx = (wx4 >> (8 * b)) & 0xff;
