@@ -307,7 +307,11 @@ DEV void gran_gather(const DevPlane& src, int plane, int x, int y, bool hL, bool
                     dead = true;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+#ifndef AV1R_POLL_BACKOFF
+#define AV1R_POLL_BACKOFF 8  // after this many polls a waiting wave sleeps 4x longer between polls (0: never); key frame -1 %
+#endif
+                if (AV1R_POLL_BACKOFF && spins > AV1R_POLL_BACKOFF) __builtin_amdgcn_s_sleep(4);
+                else __builtin_amdgcn_s_sleep(1);
             }
             if (act) (kind == 0 ? stA + u : kind == 1 ? stL + u : stL + 39)[0] = val;
         }
