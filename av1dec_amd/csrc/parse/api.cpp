@@ -1,7 +1,10 @@
 // api.cpp -- C-ABI of the host parser (include/av1p.h).
 #include "parser.h"
 
+#include <stdlib.h>
+
 #include <new>
+#include <thread>
 
 #include "av1p.h"
 
@@ -23,7 +26,20 @@ int av1p_create(av1p_ctx** out)
 {
     if (!out) return AV1R_E_INVALID;
     *out = new (std::nothrow) av1p_ctx;
-    return *out ? AV1R_OK : AV1R_E_NOMEM;
+    if (!*out) return AV1R_E_NOMEM;
+    // tile-parallel parsing by default (AV1P_TILE_THREADS overrides; 1 = serial)
+    int n = (int)std::thread::hardware_concurrency();
+    n = n < 1 ? 1 : n > 8 ? 8 : n;
+    if (const char* e = getenv("AV1P_TILE_THREADS")) n = atoi(e) > 0 ? atoi(e) : 1;
+    (*out)->parser.tile_threads = n;
+    return AV1R_OK;
+}
+
+int av1p_set_tile_threads(av1p_ctx* ctx, int n)
+{
+    if (!ctx || n < 1 || n > 64) return AV1R_E_INVALID;
+    ctx->parser.tile_threads = n;
+    return AV1R_OK;
 }
 
 void av1p_destroy(av1p_ctx* ctx)

@@ -246,12 +246,13 @@ struct MvStack {
 
 class BlockParser {
 public:
-    explicit BlockParser(Parser& p) : P(p), fh(p.fh), seq(p.seq), sd(p.sd), cdf(p.tcdf) {}
+    BlockParser(Parser& p, TileCtx& t) : P(p), T(t), fh(p.fh), seq(p.seq), sd(t.sd), cdf(t.tcdf) {}
     void decode_partition(int r, int c, int bsize);
     void read_lr(int r, int c, int bsize);
 
 private:
     Parser& P;
+    TileCtx& T;
     const FrameHdr& fh;
     const SeqHdr& seq;
     SymbolDecoder& sd;
@@ -265,7 +266,7 @@ private:
     int SN(uint16_t* c) { return sd.readN<N>(c); }
     uint32_t L(int n) { return sd.literal(n); }
     MiInfo& mi(int r, int c) { return P.mi_at(r, c); }
-    bool inside(int r, int c) const { return P.is_inside(r, c); }
+    bool inside(int r, int c) const { return T.is_inside(r, c); }
 
     void decode_block(int r, int c, int bsize);
     // mode info
@@ -335,7 +336,7 @@ private:
     int all_zero_ctx(const Blk& b, int plane, int txSz, int x4, int y4, int w, int h) const;
     // batch emission
     void emit(Blk& b);
-    bool flag(int plane, int r, int c) const { return P.decoded[plane][r + 1][c + 1] != 0; }
+    bool flag(int plane, int r, int c) const { return T.decoded[plane][r + 1][c + 1] != 0; }
 };
 
 // ------------------------------------------------------------------------------------
@@ -343,7 +344,7 @@ private:
 // ------------------------------------------------------------------------------------
 void BlockParser::decode_partition(int r, int c, int bsize)
 {
-    if (r >= fh.mi_rows || c >= fh.mi_cols || !P.err.empty()) return;
+    if (r >= fh.mi_rows || c >= fh.mi_cols || !T.err.empty()) return;
     const int num4x4 = bw4_of(bsize);
     const int half = num4x4 >> 1, quarter = half >> 1;
     const bool hasRows = (r + half) < fh.mi_rows;
@@ -387,7 +388,7 @@ void BlockParser::decode_partition(int r, int c, int bsize)
     const int subSize = bsize < BLOCK_8X8 ? bsize : kSubsize[partition][lvl];
     const int splitSize = bsize < BLOCK_8X8 ? bsize : kSubsize[PARTITION_SPLIT][lvl];
     if (subSize < 0) {
-        P.fail(AV1R_E_INVALID, "invalid partition %d for block size %d", partition, bsize);
+        T.fail(AV1R_E_INVALID, "invalid partition %d for block size %d", partition, bsize);
         return;
     }
     switch (partition) {
@@ -460,7 +461,7 @@ static ProfAcc g_prof;
 
 void BlockParser::decode_block(int r, int c, int bsize)
 {
-    if (!P.err.empty()) return;
+    if (!T.err.empty()) return;
     Blk b;
     b.r = r;
     b.c = c;
@@ -480,7 +481,7 @@ void BlockParser::decode_block(int r, int c, int bsize)
     } else {
         b.avail_u_uv = b.avail_l_uv = false;
     }
-    b.qindex = P.current_q;
+    b.qindex = T.current_q;
     tbs.clear();
 
     PROF_T(t0);
@@ -514,14 +515,14 @@ void BlockParser::decode_block(int r, int c, int bsize)
     PROF_T(t3);
     PROF_ADD(2, t1, t2);
     PROF_ADD(1, t2, t3);
-    if (!P.err.empty()) return;
+    if (!T.err.empty()) return;
     uint32_t palIdx = ~0u;
     if (b.pal_y || b.pal_uv) {
-        palIdx = (uint32_t)P.pal_colors.size();
+        palIdx = (uint32_t)T.pal_colors.size();
         std::vector<uint8_t> cols(16, 0);
         for (int i = 0; i < b.pal_y; i++) cols[i] = b.colors[0][i];
         for (int i = 0; i < b.pal_uv; i++) cols[8 + i] = b.colors[1][i];
-        P.pal_colors.push_back(cols);
+        T.pal_colors.push_back(cols);
     }
     for (int y = 0; y < b.bh4; y++)
         for (int x = 0; x < b.bw4; x++) {
@@ -533,7 +534,7 @@ void BlockParser::decode_block(int r, int c, int bsize)
             m.pal_size[0] = (uint8_t)b.pal_y;
             m.pal_size[1] = (uint8_t)b.pal_uv;
             m.pal_idx = palIdx;
-            for (int i = 0; i < 4; i++) m.delta_lf[i] = (int8_t)P.delta_lf[i];
+            for (int i = 0; i < 4; i++) m.delta_lf[i] = (int8_t)T.delta_lf[i];
         }
     PROF_T(t4);
     emit(b);
@@ -567,7 +568,7 @@ void BlockParser::read_delta_qindex(Blk& b)
 {
     const int sbSize = seq.use_128x128 ? BLOCK_128X128 : BLOCK_64X64;
     if (b.bsize == sbSize && b.skip) return;
-    if (!P.read_deltas) return;
+    if (!T.read_deltas) return;
     int abs = S(cdf.mode.delta_q, 4);
     if (abs == 3) {
         const int remBits = (int)L(3) + 1;
@@ -576,8 +577,8 @@ void BlockParser::read_delta_qindex(Blk& b)
     if (abs) {
         const int sign = (int)L(1);
         const int reduced = sign ? -abs : abs;
-        P.current_q = clip3(1, 255, P.current_q + reduced * (1 << fh.delta_q_res));
-        b.qindex = P.current_q;
+        T.current_q = clip3(1, 255, T.current_q + reduced * (1 << fh.delta_q_res));
+        b.qindex = T.current_q;
     }
 }
 
@@ -585,7 +586,7 @@ void BlockParser::read_delta_lf(Blk& b)
 {
     const int sbSize = seq.use_128x128 ? BLOCK_128X128 : BLOCK_64X64;
     if (b.bsize == sbSize && b.skip) return;
-    if (!(P.read_deltas && fh.delta_lf_present)) return;
+    if (!(T.read_deltas && fh.delta_lf_present)) return;
     const int count = fh.delta_lf_multi ? 4 : 1;
     for (int i = 0; i < count; i++) {
         int abs = S(fh.delta_lf_multi ? cdf.mode.delta_lf_multi[i] : cdf.mode.delta_lf, 4);
@@ -596,7 +597,7 @@ void BlockParser::read_delta_lf(Blk& b)
         if (abs) {
             const int sign = (int)L(1);
             const int reduced = sign ? -abs : abs;
-            P.delta_lf[i] = clip3(-63, 63, P.delta_lf[i] + reduced * (1 << fh.delta_lf_res));
+            T.delta_lf[i] = clip3(-63, 63, T.delta_lf[i] + reduced * (1 << fh.delta_lf_res));
         }
     }
 }
@@ -652,7 +653,7 @@ void BlockParser::intra_frame_mode_info(Blk& b)
     read_cdef(b);
     read_delta_qindex(b);
     read_delta_lf(b);
-    P.read_deltas = false;
+    T.read_deltas = false;
     b.ref[0] = INTRA_FRAME;
     b.ref[1] = NONE_FRAME;
     b.use_intrabc = fh.allow_intrabc ? S(cdf.mode.intrabc, 2) != 0 : false;
@@ -720,7 +721,7 @@ void BlockParser::inter_frame_mode_info(Blk& b)
     read_cdef(b);
     read_delta_qindex(b);
     read_delta_lf(b);
-    P.read_deltas = false;
+    T.read_deltas = false;
     // read_is_inter (Block.cpp:641-665)
     if (b.skip_mode) {
         b.is_inter = true;
@@ -1125,7 +1126,7 @@ void BlockParser::assign_mv(Blk& b, const MvStack& s, bool isCompound)
             if (pred[0].r == 0 && pred[0].c == 0) pred[0] = s.stack[1][0];
             if (pred[0].r == 0 && pred[0].c == 0) {
                 const int sbSize4 = seq.use_128x128 ? 32 : 16;
-                if (b.r - sbSize4 < P.mi_row_start) {
+                if (b.r - sbSize4 < T.mi_row_start) {
                     pred[0].r = 0;
                     pred[0].c = (int16_t)(-(sbSize4 * 4 + 256) * 8);
                 } else {
@@ -1704,12 +1705,12 @@ int BlockParser::palette_cache(const Blk& b, int plane, uint8_t* cache)
     if ((b.r * 4) % 64) {
         const MiInfo& m = mi(b.r - 1, b.c);
         aboveN = m.pal_size[plane];
-        if (aboveN) above = &P.pal_colors[m.pal_idx][plane * 8];
+        if (aboveN) above = &T.pal_colors[m.pal_idx][plane * 8];
     }
     if (b.avail_l) {
         const MiInfo& m = mi(b.r, b.c - 1);
         leftN = m.pal_size[plane];
-        if (leftN) left = &P.pal_colors[m.pal_idx][plane * 8];
+        if (leftN) left = &T.pal_colors[m.pal_idx][plane * 8];
     }
     int ai = 0, li = 0, n = 0;
     while (ai < aboveN && li < leftN) {
@@ -1965,10 +1966,10 @@ void BlockParser::reset_block_context(const Blk& b)
 {
     for (int plane = 0; plane < 1 + 2 * b.has_chroma; plane++) {
         const int sub = plane ? 1 : 0;
-        std::fill_n(&P.above_level[plane][b.c >> sub], b.bw4 >> sub, 0);
-        std::fill_n(&P.above_dc[plane][b.c >> sub], b.bw4 >> sub, 0);
-        std::fill_n(&P.left_level[plane][b.r >> sub], b.bh4 >> sub, 0);
-        std::fill_n(&P.left_dc[plane][b.r >> sub], b.bh4 >> sub, 0);
+        std::fill_n(&T.above_level[plane][b.c >> sub], b.bw4 >> sub, 0);
+        std::fill_n(&T.above_dc[plane][b.c >> sub], b.bw4 >> sub, 0);
+        std::fill_n(&T.left_level[plane][b.r >> sub], b.bh4 >> sub, 0);
+        std::fill_n(&T.left_dc[plane][b.r >> sub], b.bh4 >> sub, 0);
     }
 }
 
@@ -2007,7 +2008,7 @@ void BlockParser::residual(Blk& b)
                         for (int x = 0; x < n4w; x += stepX)
                             transform_block(b, plane, baseX, baseY, txSz, x + ((cx << 4) >> sub), y + ((cy << 4) >> sub));
                 }
-                if (!P.err.empty()) return;
+                if (!T.err.empty()) return;
             }
         }
 }
@@ -2049,14 +2050,14 @@ void BlockParser::transform_block(Blk& b, int plane, int baseX, int baseY, int t
     t.tx = txSz;
     t.eob = 0;
     t.type = 0;
-    t.coef_off = (uint32_t)P.cur->coefs.size();
+    t.coef_off = (uint32_t)T.coefs.size();
     t.coef_cnt = 0;
     const int x4 = startX >> 2, y4 = startY >> 2, w4 = av1r_tx_w[txSz] >> 2, h4 = av1r_tx_h[txSz] >> 2;
     if (b.skip) {
-        std::fill_n(&P.above_level[plane][x4], w4, 0);
-        std::fill_n(&P.above_dc[plane][x4], w4, 0);
-        std::fill_n(&P.left_level[plane][y4], h4, 0);
-        std::fill_n(&P.left_dc[plane][y4], h4, 0);
+        std::fill_n(&T.above_level[plane][x4], w4, 0);
+        std::fill_n(&T.above_dc[plane][x4], w4, 0);
+        std::fill_n(&T.left_level[plane][y4], h4, 0);
+        std::fill_n(&T.left_dc[plane][y4], h4, 0);
     } else {
         t.eob = coeffs(b, t);
     }
@@ -2107,9 +2108,9 @@ int BlockParser::all_zero_ctx(const Blk& b, int plane, int txSz, int x4, int y4,
     if (plane == 0) {
         int top = 0, left = 0;
         for (int k = 0; k < w4; k++)
-            if (x4 + k < maxX4) top = std::max(top, (int)P.above_level[plane][x4 + k]);
+            if (x4 + k < maxX4) top = std::max(top, (int)T.above_level[plane][x4 + k]);
         for (int k = 0; k < h4; k++)
-            if (y4 + k < maxY4) left = std::max(left, (int)P.left_level[plane][y4 + k]);
+            if (y4 + k < maxY4) left = std::max(left, (int)T.left_level[plane][y4 + k]);
         top = std::min(top, 255);
         left = std::min(left, 255);
         if (bw == w && bh == h) return 0;
@@ -2121,9 +2122,9 @@ int BlockParser::all_zero_ctx(const Blk& b, int plane, int txSz, int x4, int y4,
     }
     int above = 0, left = 0;
     for (int i = 0; i < w4; i++)
-        if (x4 + i < maxX4) above |= P.above_level[plane][x4 + i] | P.above_dc[plane][x4 + i];
+        if (x4 + i < maxX4) above |= T.above_level[plane][x4 + i] | T.above_dc[plane][x4 + i];
     for (int i = 0; i < h4; i++)
-        if (y4 + i < maxY4) left |= P.left_level[plane][y4 + i] | P.left_dc[plane][y4 + i];
+        if (y4 + i < maxY4) left |= T.left_level[plane][y4 + i] | T.left_dc[plane][y4 + i];
     int ctx = (above != 0) + (left != 0) + 7;
     if (bw * bh > w * h) ctx += 3;
     return ctx;
@@ -2279,12 +2280,12 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                     int dcSign = 0;
                     for (int k = 0; k < w4; k++)
                         if (x4 + k < maxX4) {
-                            const int s = P.above_dc[plane][x4 + k];
+                            const int s = T.above_dc[plane][x4 + k];
                             dcSign += s == 1 ? -1 : s == 2 ? 1 : 0;
                         }
                     for (int k = 0; k < h4; k++)
                         if (y4 + k < maxY4) {
-                            const int s = P.left_dc[plane][y4 + k];
+                            const int s = T.left_dc[plane][y4 + k];
                             dcSign += s == 1 ? -1 : s == 2 ? 1 : 0;
                         }
                     const int ctx = dcSign < 0 ? 1 : dcSign > 0 ? 2 : 0;
@@ -2303,7 +2304,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
 #endif
                     bit = L(1);
                     if (length > 32) {
-                        P.fail(AV1R_E_INVALID, "invalid Golomb code");
+                        T.fail(AV1R_E_INVALID, "invalid Golomb code");
                         return 0;
                     }
                 } while (!bit);
@@ -2327,7 +2328,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         PROF_ADD(7, c3, c4);
         // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j, in
         // raster order over the bounding box of the scanned positions, which is cleared again
-        std::vector<uint32_t>& out = P.cur->coefs;
+        std::vector<uint32_t>& out = T.coefs;
         int maxI = 0, maxJ = 0;
         const int twl = av1r_tx_w_log2[txSz] < 5 ? av1r_tx_w_log2[txSz] : 5;  // log2(tw)
         for (int c = 0; c < eob; c++) {
@@ -2342,7 +2343,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 if (!v) continue;
                 row[j] = 0;
                 if (v >= (1 << 21) || v < -(1 << 21)) {
-                    P.fail(AV1R_E_UNSUPPORTED, "coefficient out of packable range");
+                    T.fail(AV1R_E_UNSUPPORTED, "coefficient out of packable range");
                     return 0;
                 }
                 out.push_back(((uint32_t)v << 10) | (uint32_t)(i * tw + j));
@@ -2350,7 +2351,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         }
         t.coef_cnt = (uint32_t)out.size() - t.coef_off;
         if (!t.coef_cnt) {
-            P.fail(AV1R_E_INVALID, "transform block with eob %d and no non-zero coefficient", eob);
+            T.fail(AV1R_E_INVALID, "transform block with eob %d and no non-zero coefficient", eob);
             return 0;
         }
     }
@@ -2360,10 +2361,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         PROF_ADD(8, c0, c5);  // (head, eob: below)
     }
 #endif
-    std::fill_n(&P.above_level[plane][x4], w4, (int16_t)culLevel);
-    std::fill_n(&P.above_dc[plane][x4], w4, (uint8_t)dcCategory);
-    std::fill_n(&P.left_level[plane][y4], h4, (int16_t)culLevel);
-    std::fill_n(&P.left_dc[plane][y4], h4, (uint8_t)dcCategory);
+    std::fill_n(&T.above_level[plane][x4], w4, (int16_t)culLevel);
+    std::fill_n(&T.above_dc[plane][x4], w4, (uint8_t)dcCategory);
+    std::fill_n(&T.left_level[plane][y4], h4, (int16_t)culLevel);
+    std::fill_n(&T.left_dc[plane][y4], h4, (uint8_t)dcCategory);
     return eob;
 }
 
@@ -2372,7 +2373,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
 // ------------------------------------------------------------------------------------
 void BlockParser::emit(Blk& b)
 {
-    Frame& F = *P.cur;
+    TileCtx& F = T;  // (records tile-relative until merge_tile)
     av1r_block rec;
     memset(&rec, 0, sizeof(rec));
     rec.mi_row = (uint16_t)b.r;
@@ -2536,7 +2537,7 @@ void BlockParser::emit(Blk& b)
                         const int rr = row + (i << sub) + yy, cc = col + (j << sub) + xx;
                         if (rr < fh.aligned_mi_rows && cc < fh.aligned_mi_cols) mi(rr, cc).lf_tx[plane] = (uint8_t)t.tx;
                     }
-                P.decoded[plane][(sbRow >> sub) + i + 1][(sbCol >> sub) + j + 1] = 1;
+                T.decoded[plane][(sbRow >> sub) + i + 1][(sbCol >> sub) + j + 1] = 1;
             }
     }
     rec.n_tbs = (uint32_t)F.tbs.size() - rec.first_tb;
@@ -2606,9 +2607,9 @@ void BlockParser::read_lr(int r, int c, int bsize)
                         if (plane) u.wiener[pass][0] = 0;
                         for (int j = first; j < 3; j++) {
                             const int v = decode_signed_subexp_with_ref_bool(sd, kWienerTapsMin[j], kWienerTapsMax[j] + 1,
-                                                                             kWienerTapsK[j], P.ref_lr_wiener[plane][pass][j]);
+                                                                             kWienerTapsK[j], T.ref_lr_wiener[plane][pass][j]);
                             u.wiener[pass][j] = (int8_t)v;
-                            P.ref_lr_wiener[plane][pass][j] = v;
+                            T.ref_lr_wiener[plane][pass][j] = v;
                         }
                     }
                 } else if (type == AV1R_RESTORE_SGRPROJ) {
@@ -2619,13 +2620,13 @@ void BlockParser::read_lr(int r, int c, int bsize)
                         int v;
                         if (radius) {
                             v = decode_signed_subexp_with_ref_bool(sd, kSgrprojXqdMin[i], kSgrprojXqdMax[i] + 1, 4,
-                                                                   P.ref_sgr_xqd[plane][i]);
+                                                                   T.ref_sgr_xqd[plane][i]);
                         } else {
                             v = 0;
-                            if (i == 1) v = clip3(kSgrprojXqdMin[i], kSgrprojXqdMax[i], (1 << 7) - P.ref_sgr_xqd[plane][0]);
+                            if (i == 1) v = clip3(kSgrprojXqdMin[i], kSgrprojXqdMax[i], (1 << 7) - T.ref_sgr_xqd[plane][0]);
                         }
                         u.sgr_xqd[i] = (int8_t)v;
-                        P.ref_sgr_xqd[plane][i] = v;
+                        T.ref_sgr_xqd[plane][i] = v;
                     }
                 }
             }
@@ -2637,7 +2638,7 @@ void BlockParser::read_lr(int r, int c, int bsize)
 // ------------------------------------------------------------------------------------
 // tile (Tile::parse, Tile.cpp:122-160; BlockDecoded, Tile.cpp:41-90)
 // ------------------------------------------------------------------------------------
-void Parser::clear_block_decoded_flags(int r, int c, int sbSize4)
+void TileCtx::clear_block_decoded_flags(int r, int c, int sbSize4)
 {
     for (int plane = 0; plane < 3; plane++) {
         const int sub = plane ? 1 : 0;
@@ -2652,32 +2653,32 @@ void Parser::clear_block_decoded_flags(int r, int c, int sbSize4)
     }
 }
 
-int Parser::decode_tile()
+int Parser::decode_tile(TileCtx& T)
 {
     const int sbSize = seq.use_128x128 ? BLOCK_128X128 : BLOCK_64X64;
     const int sbSize4 = av1r_num4x4w[sbSize];
     for (int p = 0; p < 3; p++) {
-        above_level[p].assign(fh.aligned_mi_cols + 32, 0);
-        above_dc[p].assign(fh.aligned_mi_cols + 32, 0);
+        T.above_level[p].assign(fh.aligned_mi_cols + 32, 0);
+        T.above_dc[p].assign(fh.aligned_mi_cols + 32, 0);
     }
-    for (int i = 0; i < 4; i++) delta_lf[i] = 0;
+    for (int i = 0; i < 4; i++) T.delta_lf[i] = 0;
     for (int plane = 0; plane < 3; plane++)
         for (int pass = 0; pass < 2; pass++) {
-            ref_sgr_xqd[plane][pass] = kSgrprojXqdMid[pass];
-            for (int i = 0; i < 3; i++) ref_lr_wiener[plane][pass][i] = kWienerTapsMid[i];
+            T.ref_sgr_xqd[plane][pass] = kSgrprojXqdMid[pass];
+            for (int i = 0; i < 3; i++) T.ref_lr_wiener[plane][pass][i] = kWienerTapsMid[i];
         }
-    BlockParser bp(*this);
-    for (int r = mi_row_start; r < mi_row_end; r += sbSize4) {
+    BlockParser bp(*this, T);
+    for (int r = T.mi_row_start; r < T.mi_row_end; r += sbSize4) {
         for (int p = 0; p < 3; p++) {
-            left_level[p].assign(fh.aligned_mi_rows + 32, 0);
-            left_dc[p].assign(fh.aligned_mi_rows + 32, 0);
+            T.left_level[p].assign(fh.aligned_mi_rows + 32, 0);
+            T.left_dc[p].assign(fh.aligned_mi_rows + 32, 0);
         }
-        for (int c = mi_col_start; c < mi_col_end; c += sbSize4) {
-            read_deltas = fh.delta_q_present;
-            clear_block_decoded_flags(r, c, sbSize4);
+        for (int c = T.mi_col_start; c < T.mi_col_end; c += sbSize4) {
+            T.read_deltas = fh.delta_q_present;
+            T.clear_block_decoded_flags(r, c, sbSize4);
             bp.read_lr(r, c, sbSize);
             bp.decode_partition(r, c, sbSize);
-            if (!err.empty()) return AV1R_E_INVALID;
+            if (!T.err.empty()) return AV1R_E_INVALID;
         }
     }
     return AV1R_OK;

@@ -17,6 +17,9 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <new>
+#include <thread>
 
 #include "parser.h"
 
@@ -39,6 +42,22 @@ void Cdfs::reset_counters()
 }
 
 Parser::Parser() {}
+
+int TileCtx::fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (err.empty()) err = buf;  // (the first failure of the tile)
+    return code;
+}
+
+Parser::~Parser()
+{
+    for (TileCtx* t : par_tiles) delete t;
+}
 
 int Parser::fail(int code, const char* fmt, ...)
 {
@@ -907,7 +926,6 @@ void Parser::start_frame()
         memset(&u, 0, sizeof(u));
         lr_units.insert(lr_units.end(), (size_t)fh.lr_unit_rows[p] * fh.lr_unit_cols[p], u);
     }
-    pal_colors.clear();
     cur = new Frame;
     memset(&cur->hdr, 0, sizeof(cur->hdr));
     fill_header(cur->hdr);
@@ -1154,8 +1172,12 @@ int Parser::tile_group(BitReader& br, const uint8_t* data, size_t size)
     if (tgStart > tgEnd || tgEnd >= numTiles || tgStart != tile_num || !cur)
         return fail(AV1R_E_INVALID, "tile group %d..%d does not continue the frame (next tile %d of %d)", tgStart, tgEnd,
                     tile_num, numTiles);
+    // the tiles' byte ranges (tile_size_minus_1 prefixes), then their parse
+    struct TileSpan {
+        size_t off, size;
+    };
+    std::vector<TileSpan> spans;
     for (int tn = tgStart; tn <= tgEnd; tn++) {
-        const int tileRow = tn / fh.tile_cols, tileCol = tn % fh.tile_cols;
         size_t tileSize;
         if (tn == tgEnd) {
             tileSize = size - off;
@@ -1167,22 +1189,97 @@ int Parser::tile_group(BitReader& br, const uint8_t* data, size_t size)
             tileSize = (size_t)t + 1;
         }
         if (off + tileSize > size) return fail(AV1R_E_INVALID, "tile %d size %zu exceeds the tile group", tn, tileSize);
-        mi_row_start = fh.mi_row_starts[tileRow];
-        mi_row_end = fh.mi_row_starts[tileRow + 1];
-        mi_col_start = fh.mi_col_starts[tileCol];
-        mi_col_end = fh.mi_col_starts[tileCol + 1];
-        current_q = fh.base_q_idx;
-        tcdf = cdf;
-        sd.init(data + off, tileSize, fh.disable_cdf_update);
-        CHK(decode_tile());
-        if (tn == fh.context_update_tile_id) saved_cdf = tcdf;
+        spans.push_back({off, tileSize});
         off += tileSize;
-        tile_num = tn + 1;
+    }
+    const int n = tgEnd - tgStart + 1;
+    const int nThreads = std::min(tile_threads, n);
+    if (nThreads <= 1) {
+        for (int i = 0; i < n; i++) {
+            begin_tile(tile, tgStart + i, data + spans[i].off, spans[i].size);
+            const int rc = decode_tile(tile);
+            CHK(merge_tile(tile, tgStart + i));
+            if (rc) return rc;
+            tile_num = tgStart + i + 1;
+        }
+    } else {
+        // tile-parallel: every tile into its own context, the threads pulling tile indices
+        while ((int)par_tiles.size() < n) par_tiles.push_back(new TileCtx);
+        std::atomic<int> next{0};
+        std::vector<int> rcs(n, AV1R_OK);
+        auto work = [&]() {
+            for (int i; (i = next.fetch_add(1)) < n;) {
+                try {
+                    begin_tile(*par_tiles[i], tgStart + i, data + spans[i].off, spans[i].size);
+                    rcs[i] = decode_tile(*par_tiles[i]);
+                } catch (const std::bad_alloc&) {
+                    par_tiles[i]->err = "out of memory";
+                    rcs[i] = AV1R_E_NOMEM;
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int k = 1; k < nThreads; k++) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+        for (int i = 0; i < n; i++) {  // merged in tile order: the serial path's records
+            CHK(merge_tile(*par_tiles[i], tgStart + i));
+            if (rcs[i]) return rcs[i];
+            tile_num = tgStart + i + 1;
+        }
     }
     if (tgEnd == numTiles - 1) {
         CHK(finish_frame());
         seen_frame_header = false;
     }
+    return AV1R_OK;
+}
+
+void Parser::begin_tile(TileCtx& T, int tn, const uint8_t* data, size_t size)
+{
+    const int tileRow = tn / fh.tile_cols, tileCol = tn % fh.tile_cols;
+    T.mi_row_start = fh.mi_row_starts[tileRow];
+    T.mi_row_end = fh.mi_row_starts[tileRow + 1];
+    T.mi_col_start = fh.mi_col_starts[tileCol];
+    T.mi_col_end = fh.mi_col_starts[tileCol + 1];
+    T.current_q = fh.base_q_idx;
+    T.tcdf = cdf;
+    T.sd.init(data, size, fh.disable_cdf_update);
+    T.pal_colors.clear();
+    T.blocks.clear();
+    T.tbs.clear();
+    T.coefs.clear();
+    T.palette.clear();
+    T.err.clear();
+}
+
+int Parser::merge_tile(TileCtx& T, int tn)
+{
+    if (!T.err.empty()) err = T.err;
+    if (tn == fh.context_update_tile_id) saved_cdf = T.tcdf;
+    Frame& F = *cur;
+    if (F.blocks.empty() && F.tbs.empty() && F.coefs.empty() && F.palette.empty()) {
+        // the frame's first records: taken over as they are (indices already frame-relative)
+        F.blocks.swap(T.blocks);
+        F.tbs.swap(T.tbs);
+        F.coefs.swap(T.coefs);
+        F.palette.swap(T.palette);
+        return AV1R_OK;
+    }
+    const uint32_t blk0 = (uint32_t)F.blocks.size(), tb0 = (uint32_t)F.tbs.size(), coef0 = (uint32_t)F.coefs.size(),
+                   pal0 = (uint32_t)F.palette.size();
+    for (av1r_block& b : T.blocks) {
+        b.first_tb += tb0;
+        if (b.palette_size_y || b.palette_size_uv) b.palette_off += pal0;
+    }
+    for (av1r_tb& t : T.tbs) {
+        t.block += blk0;
+        t.coef_off += coef0;
+    }
+    F.blocks.insert(F.blocks.end(), T.blocks.begin(), T.blocks.end());
+    F.tbs.insert(F.tbs.end(), T.tbs.begin(), T.tbs.end());
+    F.coefs.insert(F.coefs.end(), T.coefs.begin(), T.coefs.end());
+    F.palette.insert(F.palette.end(), T.palette.begin(), T.palette.end());
     return AV1R_OK;
 }
 

@@ -410,6 +410,44 @@ struct FrameHdr {
 
 struct Frame;  // one decoded frame's batch (api.cpp)
 
+// Everything one tile's parse owns (Tile::parse, Tile.cpp:122-160): its entropy decoder and
+// CDFs, the above / left contexts, the per-tile delta and loop-restoration references, and
+// the records it emits.  Tiles are independent for entropy decoding and read only their own
+// region of the mode-info grid (every neighbour test is bounded by the tile), so the tiles of
+// a frame parse concurrently, one TileCtx each, and are merged into the frame in tile order
+// (Parser::merge_tile fixes the record indices).
+struct TileCtx {
+    int mi_row_start = 0, mi_row_end = 0, mi_col_start = 0, mi_col_end = 0;
+    SymbolDecoder sd;
+    Cdfs tcdf;  // the tile's CDFs
+    // level contexts are int16 as the reference's BlockContext::LevelContext: a Golomb level
+    // past int16 wraps negative and stays so in the context (TransformBlock.cpp:1620-1702)
+    std::vector<int16_t> above_level[3], left_level[3];
+    std::vector<uint8_t> above_dc[3], left_dc[3];
+    int delta_lf[4] = {};
+    int current_q = 0;
+    bool read_deltas = false;
+    int ref_sgr_xqd[3][2] = {};
+    int ref_lr_wiener[3][2][3] = {};
+    // decoded flags of the current superblock (Tile.cpp BlockDecoded), per plane, offset 1
+    static constexpr int kDecN = 35;
+    uint8_t decoded[3][kDecN][kDecN] = {};
+    std::vector<std::vector<uint8_t>> pal_colors;  // per palette block: 24 colours (y, u, v)
+    // this tile's records; block.first_tb / palette_off and tb.block / coef_off are
+    // tile-relative until the tile is merged into the frame
+    std::vector<av1r_block> blocks;
+    std::vector<av1r_tb> tbs;
+    std::vector<uint32_t> coefs;
+    std::vector<uint8_t> palette;
+    std::string err;
+    int fail(int code, const char* fmt, ...);
+    bool is_inside(int r, int c) const
+    {
+        return c >= mi_col_start && c < mi_col_end && r >= mi_row_start && r < mi_row_end;
+    }
+    void clear_block_decoded_flags(int r, int c, int sbSize4);
+};
+
 class Parser {
 public:
     Parser();
@@ -439,25 +477,15 @@ public:
     int cdef_cols = 0, cdef_rows = 0;
     std::vector<av1r_lr_unit> lr_units;  // frame order: plane 0 units, plane 1, plane 2
     int lr_off[3] = {};
-    std::vector<std::vector<uint8_t>> pal_colors;  // per palette block: 24 colours (y, u, v)
     Frame* cur = nullptr;
 
     // ---- per tile ----
-    int mi_row_start = 0, mi_row_end = 0, mi_col_start = 0, mi_col_end = 0;
-    SymbolDecoder sd;
-    Cdfs tcdf;  // the tile's CDFs
-    // level contexts are int16 as the reference's BlockContext::LevelContext: a Golomb level
-    // past int16 wraps negative and stays so in the context (TransformBlock.cpp:1620-1702)
-    std::vector<int16_t> above_level[3], left_level[3];
-    std::vector<uint8_t> above_dc[3], left_dc[3];
-    int delta_lf[4] = {};
-    int current_q = 0;
-    bool read_deltas = false;
-    int ref_sgr_xqd[3][2] = {};
-    int ref_lr_wiener[3][2][3] = {};
-    // decoded flags of the current superblock (Tile.cpp BlockDecoded), per plane, offset 1
-    static constexpr int kDecN = 35;
-    uint8_t decoded[3][kDecN][kDecN] = {};
+    TileCtx tile;  // the serial path's tile (and the bitstream writer's)
+    // tile-parallel parsing: up to `tile_threads` threads parse the tiles of a tile group
+    // (1: serial); one TileCtx per tile, kept between frames for their buffers
+    int tile_threads = 1;
+    std::vector<TileCtx*> par_tiles;
+    ~Parser();
 
     // ---- obu.cpp ----
     int parse_sequence_header(BitReader& br);
@@ -486,13 +514,14 @@ public:
     void show_existing();
     void fill_header(av1r_frame_hdr& o) const;
 
+    // tile `tn` of the frame over `size` bytes at `data`: T's bounds, CDFs, decoder, outputs
+    void begin_tile(TileCtx& T, int tn, const uint8_t* data, size_t size);
+    // T's records appended to the frame (indices made frame-relative), its CDFs saved when it
+    // is the context_update_tile_id tile, its error reported
+    int merge_tile(TileCtx& T, int tn);
+
     // ---- block.cpp (the block-level syntax lives in its BlockParser) ----
-    int decode_tile();
-    void clear_block_decoded_flags(int r, int c, int sbSize4);
-    bool is_inside(int r, int c) const
-    {
-        return c >= mi_col_start && c < mi_col_end && r >= mi_row_start && r < mi_row_end;
-    }
+    int decode_tile(TileCtx& T);
     MiInfo& mi_at(int r, int c) { return mi[(size_t)r * mi_stride + c]; }
 };
 

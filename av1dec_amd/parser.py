@@ -61,13 +61,17 @@ class ParseError(RuntimeError):
 class Parser:
     """One parsing context (one stream).  Not thread-safe; use one per thread."""
 
-    def __init__(self):
+    def __init__(self, tile_threads=None):
         self._l = native.parser_lib()
         h = C.c_void_p()
         rc = self._l.av1p_create(C.byref(h))
         if rc:
             raise ParseError(rc, "av1p_create failed")
         self._h = h
+        if tile_threads is not None:
+            rc = self._l.av1p_set_tile_threads(h, int(tile_threads))
+            if rc:
+                raise ParseError(rc, f"av1p_set_tile_threads({tile_threads})")
 
     def decode_tu(self, data):
         n = C.c_int(0)

@@ -15,6 +15,8 @@
  *                                  with Parser::parseSequenceHeader / parseFrameHeader /
  *                                  parseTileGroup and Tile::parse (Tile.cpp:122-160)
  *   av1p_frame                  -- the parsed frame the reference walks in decodeFrame
+ *   av1p_set_tile_threads       -- (no counterpart: the reference parses tiles one after
+ *                                  another, Parser::parseTileGroup, Parser.cpp:492-521)
  */
 #ifndef AV1P_H
 #define AV1P_H
@@ -37,6 +39,10 @@ void av1p_destroy(av1p_ctx* ctx);
 int av1p_decode_tu(av1p_ctx* ctx, const uint8_t* data, size_t size, int* n_frames);
 /* Frame batch i (0 <= i < n_frames) of the last av1p_decode_tu. */
 const av1r_frame_batch* av1p_frame(av1p_ctx* ctx, int i);
+/* Threads that parse the tiles of one frame concurrently (1: serial; default min(8, the
+ * hardware threads), or the AV1P_TILE_THREADS environment variable).  Tiles are independent
+ * for entropy decoding; the batch is identical whatever the setting. */
+int av1p_set_tile_threads(av1p_ctx* ctx, int n);
 /* Message of the last failure (empty string if none). */
 const char* av1p_last_error(av1p_ctx* ctx);
 

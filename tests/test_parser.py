@@ -133,3 +133,19 @@ def test_bitstream_to_pixels_matches_conformance_md5(parser_mod, stream):
                 h.update(plane.tobytes())
     o.close()
     assert h.hexdigest() == expect
+
+
+@pytest.mark.parametrize("name", ["4k_s2_tiles4x2", "640x360_tiles2x2_sb64"])
+def test_tile_parallel_parse_is_identical(parser_mod, name):
+    """Tiles parsed concurrently (one TileCtx per tile, merged in tile order) give the same
+    batches, byte for byte, as the serial parse (Parser::parseTileGroup's tile loop,
+    Parser.cpp:492-521)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools", "bsw"))
+    import pybsw
+    data = pybsw.stream_ivf(name, frames=3 if name.startswith("4k") else None)
+    serial = parser_mod.Parser(tile_threads=1).decode_ivf(data)
+    for n in (2, 8):
+        par = parser_mod.Parser(tile_threads=n).decode_ivf(data)
+        assert len(par) == len(serial)
+        for k, (f, g) in enumerate(zip(par, serial)):
+            assert _same(f, g), f"{name}: frame {k} differs with {n} tile threads"

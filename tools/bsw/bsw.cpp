@@ -335,7 +335,7 @@ public:
     }
     int mv_symbol(const uint16_t* p, int nsym)
     {
-        const MvCdfs& m = P.tcdf.mv[0];
+        const MvCdfs& m = P.tile.tcdf.mv[0];
         if (p == m.joints) return (mv_diff[0] != 0) * 2 + (mv_diff[1] != 0);
         for (int k = 0; k < 2; k++) {
             const MvComp& c = m.comp[k];
@@ -363,7 +363,7 @@ public:
     }
     int choose(uint16_t* cdf, int nsym)
     {
-        const uint8_t* base = (const uint8_t*)&P.tcdf;
+        const uint8_t* base = (const uint8_t*)&P.tile.tcdf;
         const ptrdiff_t off = (const uint8_t*)cdf - base;
         if (off < 0 || off >= (ptrdiff_t)sizeof(Cdfs)) {  // literal bits, derived CDFs
             if (force_bit >= 0) {
@@ -373,8 +373,8 @@ public:
             }
             return sample(cdf, nsym);
         }
-        const ModeCdfs& M = P.tcdf.mode;
-        if (in(cdf, P.tcdf.mv[0])) return mv_symbol(cdf, nsym);
+        const ModeCdfs& M = P.tile.tcdf.mode;
+        if (in(cdf, P.tile.tcdf.mv[0])) return mv_symbol(cdf, nsym);
         if (in(cdf, M.intra_inter)) return rng.bern(0.8);
         if (in(cdf, M.comp_inter)) return rng.bern(0.4);
         if (in(cdf, M.comp_group_idx)) return rng.bern(0.3);      // wedge + difference-weighted
@@ -749,21 +749,14 @@ public:
         }
         std::vector<uint8_t> payload = hw.b;
         for (int tn = 0; tn < numTiles; tn++) {
-            const int tileRow = tn / P.fh.tile_cols, tileCol = tn % P.fh.tile_cols;
-            P.mi_row_start = P.fh.mi_row_starts[tileRow];
-            P.mi_row_end = P.fh.mi_row_starts[tileRow + 1];
-            P.mi_col_start = P.fh.mi_col_starts[tileCol];
-            P.mi_col_end = P.fh.mi_col_starts[tileCol + 1];
-            P.current_q = P.fh.base_q_idx;
-            P.tcdf = P.cdf;
             static const uint8_t none = 0;
-            P.sd.init(&none, 0, P.fh.disable_cdf_update);
-            P.sd.hook = this;
+            P.begin_tile(P.tile, tn, &none, 0);
+            P.tile.sd.hook = this;
             enc.reset();
-            const int rc = P.decode_tile();
-            P.sd.hook = nullptr;
+            const int rc = P.decode_tile(P.tile);
+            P.tile.sd.hook = nullptr;
+            P.merge_tile(P.tile, tn);
             if (rc || !err.empty()) return fail("frame %d tile %d: %s", t, tn, err.empty() ? P.err.c_str() : err.c_str());
-            if (tn == P.fh.context_update_tile_id) P.saved_cdf = P.tcdf;
             std::vector<uint8_t> data = enc.finish();
             if (data.empty()) data.push_back(0);
             if (tn + 1 < numTiles) {

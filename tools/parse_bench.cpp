@@ -1,8 +1,8 @@
 // Host parser timing: parse an IVF file (every temporal unit, in order) `reps` times with
 // av1p_decode_tu and print ms per frame.  Links the parser sources directly, so builds with
 // other flags (-O3, -march, -pg) can be compared without touching the product build:
-//   g++ -std=c++17 -O2 -Iinclude -Iav1dec_amd/csrc/parse tools/parse_bench.cpp \
-//       av1dec_amd/csrc/parse/{obu,block,api}.cpp -o /tmp/parse_bench
+//   g++ -std=c++17 -O2 -Iinclude -Iav1dec_amd/csrc/parse tools/parse_bench.cpp
+//       av1dec_amd/csrc/parse/{obu,block,api}.cpp -pthread -o /tmp/parse_bench
 //   /tmp/parse_bench stream.ivf [reps]
 #include <chrono>
 #include <cstdio>
