@@ -219,23 +219,24 @@ class StreamScheduler:
             self.ex.shutdown()
 
 
-def ivf_streams(rank, S, frames):
+def ivf_streams(rank, S, frames, name="1080p_s1", seed=0x5EED1000):
     """Rank `rank`'s shard of configs[4] as real bitstreams: S synthetic 1080p IVF streams from
     the bitstream writer (tools/bsw, configuration 1080p_s1; stream i of the job has seed
     0x5EED1000 + i, so stream 0 is the one tests/golden/bsw.json pins to the reference's MD5),
-    written in parallel (untimed)."""
+    written in parallel (untimed).  (configs[3]: name 4k_s2_tiles4x2, seed 0x5EED2000.)"""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "tools", "bsw"))
     import pybsw
     ids = rank_stream_ids(rank, S)
     with ThreadPoolExecutor(min(S, 16)) as ex:
-        return list(ex.map(lambda i: pybsw.stream_ivf("1080p_s1", seed=0x5EED1000 + i, frames=frames), ids))
+        return list(ex.map(lambda i: pybsw.stream_ivf(name, seed=seed + i, frames=frames), ids))
 
 
-def ivf_leg(decs, streams, frames):
+def ivf_leg(decs, streams, frames, size="1920x1080", name="1080p_s1", seed=0x5EED1000):
     """configs[4] end to end: every stream's IVF parsed on its own host thread and packed
     while the GPU decodes, one frame of every ready stream per shared launch
-    (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one."""
+    (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one.  Multi-tile
+    frames (configs[3]) are parsed tile-parallel (av1p_set_tile_threads)."""
     from av1dec_amd.pipeline import run_native
     run_native(decs, "ivf", streams)
     t0 = time.perf_counter()
@@ -248,8 +249,8 @@ def ivf_leg(decs, streams, frames):
             "pack_ms_per_frame": round(1e3 * st["pack_s"] / n, 3),
             "stream_bytes_per_frame": int(sum(len(s) for s in streams) / n),
             "batches": int(st["batches"]),
-            "workload": f"{len(streams)} synthetic 1920x1080 IVF streams from tools/bsw (1080p_s1: 1 key + "
-                        f"{frames - 1} inter, seeds 0x5eed1000+stream), each parsed by the host parser and packed on "
+            "workload": f"{len(streams)} synthetic {size} IVF streams from tools/bsw ({name}: 1 key + "
+                        f"{frames - 1} inter, seeds {seed:#x}+stream), each parsed by the host parser and packed on "
                         f"its own native thread (av1r_pipeline_run), decoded in shared launches; parse inside "
                         f"the timed region"}
 
@@ -461,7 +462,7 @@ def key_frame_ms(dec, handle, reps=3):
     return {"recon": round(m[0], 4), "lf": round(m[1], 4), "cdef": round(m[2], 4), "lr": round(m[3], 4)}
 
 
-def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, traffic=None):
+def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, traffic=None, ivf_frames=8):
     """BASELINE configs[3]: S synthetic 3840x2160 streams with the 4x2 tile grid per GPU,
     host-inclusive and device-only, with its own per-stage times, roofline and PMC traffic."""
     from concurrent.futures import ThreadPoolExecutor
@@ -480,6 +481,14 @@ def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, tra
     for d, hs in zip(decs, handles):
         for hd in hs:
             d.release_prepared(hd)
+    # end to end from 4x2-tile IVF bitstreams: the tiles of a frame parsed concurrently
+    ivf = None
+    if ivf_frames > 0:
+        ivf = ivf_leg(decs, ivf_streams(rank, S, ivf_frames, "4k_s2_tiles4x2", 0x5EED2000), ivf_frames,
+                      f"{W}x{H} 4x2-tile", "4k_s2_tiles4x2", 0x5EED2000)
+        if dist:
+            ivf["fps_all_ranks"] = round(world * ivf["frames"] / max_over_ranks(ivf["elapsed_s"], dist), 3)
+    for d in decs:
         d.close()
     return {"fps": round(r["fps"], 3), "device_only_fps": round(r["device_fps"], 3), "streams_per_gpu": S,
             "steps": steps, "warmup": warmup, "ms_per_step": round(r["elapsed"] * 1e3 / steps, 4),
@@ -493,7 +502,8 @@ def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, tra
             "stage_ms_per_frame": {n: round(v, 4) for n, v in r["per_frame_ms"].items()},
             "recon_kernel_ms_per_frame": {n: round(v, 4) for n, v in r["kernel_ms"].items()},
             "key_frame_alone_ms": kf,
-            "host_profile": r["host_profile"]}
+            "host_profile": r["host_profile"],
+            "ivf_end_to_end": ivf}
 
 
 def main():
@@ -618,7 +628,8 @@ def main():
     # ---- configs[3]: 4K, 4x2 tiles (a bounded extra leg of the default run)
     k4 = None
     if args.config == "1080p" and not args.no_4k:
-        k4 = leg_4k(local, rank, world, dist, workers, traffic=args.traffic_4k)
+        k4 = leg_4k(local, rank, world, dist, workers, traffic=args.traffic_4k,
+                    ivf_frames=min(args.ivf_frames, 8))
 
     copy_peak = None
     try:
