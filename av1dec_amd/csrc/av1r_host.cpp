@@ -680,6 +680,41 @@ static void build_strips(av1r_ctx* c, const av1r_frame_batch* b)
 // was built too.
 // AV1R_PACK_FUSED=0: the map walks one by one (the fused walks must pack identical bytes)
 static const bool g_packFused = !getenv("AV1R_PACK_FUSED") || atoi(getenv("AV1R_PACK_FUSED")) != 0;
+// The pixels an intra prediction actually uses (IntraPredict::predict_intra,
+// IntraPredict.cpp:563-631, and the predictors it calls): the above-right run
+// (x + w .. x + 2w - 1) only by a directional prediction at an angle below 90 (the
+// zone-1 predictor, :379-483 with pAngle < 90, and its edge filter / upsampling over
+// w + h samples); the below-left run only by one above 180 (zone 3).  DC, V, H, smooth,
+// Paeth, CFL, filter-intra and the inter-intra modes (II_DC / V / H / SMOOTH) read at most
+// w samples above and h on the left.  A TB's dependencies (and granule masks) cover only
+// what its mode reads: the device gathers the rest of the run without waiting, and those
+// samples never reach a predicted pixel.  angle: -1 for a non-directional prediction.
+static int intra_angle(const av1r_block& blk, int p)
+{
+    if (p == 0 && (blk.flags & AV1R_BLK_FILTER_INTRA)) return -1;
+    const int mode = p ? blk.uv_mode : blk.y_mode;  // (UV_CFL_PRED: not directional)
+    if (mode < AV1R_V_PRED || mode > AV1R_D67_PRED) return -1;
+    return av1r_mode_to_angle[mode] + (p ? blk.angle_delta_uv : blk.angle_delta_y) * 3;
+}
+// Which of the edge runs the prediction uses (bit 0 the above run, bit 1 the left run,
+// bit 2 the corner pixel (x - 1, y - 1)): V reads only the row above and H only the column
+// on the left (the other one stands in when a side is missing, :571-590), zone 1 the row and
+// the corner (its edge filter / upsampling reach index -1), zone 3 the column and the
+// corner; DC, smooth and CFL no corner; Paeth, zone 2 and filter-intra everything.
+static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
+{
+    const int mode = p ? blk.uv_mode : blk.y_mode;
+    if ((p == 0 && (blk.flags & AV1R_BLK_FILTER_INTRA)) || mode == AV1R_PAETH_PRED) return 7;
+    const int ang = intra_angle(blk, p);
+    if (ang < 0) return 3;
+    if (ang == 90) return hA ? 1 : 3;
+    if (ang == 180) return hL ? 2 : 3;
+    if (ang < 90) return hA ? 5 : 7;
+    if (ang > 180) return hL ? 6 : 7;
+    return 7;
+}
+static bool g_modeEdges = !getenv("AV1R_MODE_EDGES") || atoi(getenv("AV1R_MODE_EDGES")) != 0;
+
 static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
 {
     const av1r_frame_hdr* h = b->hdr;
@@ -719,10 +754,11 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     };
     // the owners of the pixels an intra prediction reads (coop_intra_edges): with granules,
     // mask words nm[4 * slot ..] instead of dependencies (coop_intra_edges_gran's runs)
-    auto edge_owners = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int slot) {
+    auto edge_owners = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int slot, int need) {
         if (!c->granOk) {
-            if (hA) owners(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2);
-            if (hL) owners(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2);
+            if (hA && (need & 1)) owners(p, x >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2);
+            if (hL && (need & 2)) owners(p, (x - 1) >> 2, y >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2);
+            if (hA && hL && (need & 4)) owners(p, (x - 1) >> 2, (y - 1) >> 2, (x - 1) >> 2, (y - 1) >> 2);
             return;
         }
         uint32_t* m = nm + 4 * slot;
@@ -745,9 +781,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         // above run: row (y-1)/4 from x/4; left run: column (x-1)/4 from y/4; the corner
         // pixel (x-1, y-1) separately (m[1]: bit 0 written in the launch, bit 1 its
         // granule is its owner's right column instead of its bottom row)
-        if (hA) run(x >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, true, m);
-        if (hL) run(y >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2, false, m + 2);
-        if (hA && hL) {
+        if (hA && (need & 1)) run(x >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, true, m);
+        if (hL && (need & 2)) run(y >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2, false, m + 2);
+        if (hA && hL && (need & 4)) {
             const size_t i = (size_t)((y - 1) >> 2) * c->mapW[p] + ((x - 1) >> 2);
             const av1r_ctx::MapUnit& mu = c->umap[p][i];
             if (mu.owner >= 0) {
@@ -818,15 +854,16 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     // pixel (x, y) of plane p with the given edge availability (IntraPredict.cpp:563-631):
     // row y-1 over [x-1 | x, x + (AR ? 2w : w) - 1], column x-1 over [y-1 | y, y + (BL ? 2h : h) - 1];
     // with only one edge available its neighbouring corner pixel stands in for the other.
-    auto edge_level = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL) {
+    auto edge_level = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int need) {
         int m = -1;
-        if (hA) m = std::max(m, region_max(p, (hL ? x - 1 : x) >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2));
-        if (hL) m = std::max(m, region_max(p, (x - 1) >> 2, (hA ? y - 1 : y) >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2));
+        if (hA && (need & 1)) m = std::max(m, region_max(p, x >> 2, (y - 1) >> 2, (x + (hAR ? 2 * w : w) - 1) >> 2, (y - 1) >> 2));
+        if (hL && (need & 2)) m = std::max(m, region_max(p, (x - 1) >> 2, y >> 2, (x - 1) >> 2, (y + (hBL ? 2 * h : h) - 1) >> 2));
+        if (hA && hL && (need & 4)) m = std::max(m, region_max(p, (x - 1) >> 2, (y - 1) >> 2, (x - 1) >> 2, (y - 1) >> 2));
         return m;
     };
     // granule mode: edge_level and edge_owners in one walk over the same units (the above
     // run, the left run, the corner); returns the latest level
-    auto edge_scan = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int slot) {
+    auto edge_scan = [&](int p, int x, int y, int w, int h, bool hL, bool hA, bool hAR, bool hBL, int slot, int need) {
         int m = -1;
         uint32_t* mw = nm + 4 * slot;
         const int W = c->mapW[p], H = c->mapH[p];
@@ -839,17 +876,17 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             *word |= 1u << bit;
             if (!(mu.emit & need)) c->granOk = false;
         };
-        if (hA) {
+        if (hA && (need & 1)) {
             const int u0 = x >> 2, u1 = (x + (hAR ? 2 * w : w) - 1) >> 2, uy = (y - 1) >> 2;
             if (u1 - u0 >= 32) c->granOk = false;
             for (int u = u0; u <= u1 && u - u0 < 32; u++) unit(u, uy, u - u0, mw, 1);
         }
-        if (hL) {
+        if (hL && (need & 2)) {
             const int u0 = y >> 2, u1 = (y + (hBL ? 2 * h : h) - 1) >> 2, ux = (x - 1) >> 2;
             if (u1 - u0 >= 32) c->granOk = false;
             for (int u = u0; u <= u1 && u - u0 < 32; u++) unit(ux, u, u - u0, mw + 2, 2);
         }
-        if (hA && hL) {
+        if (hA && hL && (need & 4)) {
             const int ux = (x - 1) >> 2, uy = (y - 1) >> 2;
             if (ux >= 0 && uy >= 0 && ux < W && uy < H) {
                 const av1r_ctx::MapUnit& mu = map[(size_t)uy * W + ux];
@@ -892,9 +929,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                     bool hA = p ? (blk.flags & AV1R_BLK_AVAIL_U_UV) : (blk.flags & AV1R_BLK_AVAIL_U);
                     const int ex = (blk.mi_col >> sub) * 4, ey = (blk.mi_row >> sub) * 4;
                     const int ew = av1r_num4x4w[psz] * 4, eh = av1r_num4x4h[psz] * 4;
-                    const bool hAR = (blk.ii_edge >> (2 * p)) & 1, hBL = (blk.ii_edge >> (2 * p + 1)) & 1;
-                    dep = std::max(dep, edge_level(p, ex, ey, ew, eh, hL, hA, hAR, hBL));
-                    edge_owners(p, ex, ey, ew, eh, hL, hA, hAR, hBL, p);
+                    // (the inter-intra modes read neither the above-right nor the below-left run)
+                    const bool hAR = !g_modeEdges && ((blk.ii_edge >> (2 * p)) & 1);
+                    const bool hBL = !g_modeEdges && ((blk.ii_edge >> (2 * p + 1)) & 1);
+                    const int need = g_modeEdges ? 3 : 7;  // (II_DC / V / H / SMOOTH: no corner)
+                    dep = std::max(dep, edge_level(p, ex, ey, ew, eh, hL, hA, hAR, hBL, need));
+                    edge_owners(p, ex, ey, ew, eh, hL, hA, hAR, hBL, p, need);
                 }
                 blkLevel = dep + 1;
                 push(c->lvB, blkLevel, AV1R_ITEM(AV1R_ITEM_II, bi));
@@ -927,12 +967,15 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 int dep = -1;
                 if (!pal) {
                     const bool hL = t.flags & AV1R_TB_HAVE_LEFT, hA = t.flags & AV1R_TB_HAVE_ABOVE;
-                    const bool hAR = t.flags & AV1R_TB_HAVE_AR, hBL = t.flags & AV1R_TB_HAVE_BL;
+                    const int ang = g_modeEdges ? intra_angle(blk, p) : 0;
+                    const bool hAR = (t.flags & AV1R_TB_HAVE_AR) && (!g_modeEdges || (ang > 0 && ang < 90));
+                    const bool hBL = (t.flags & AV1R_TB_HAVE_BL) && (!g_modeEdges || ang > 180);
+                    const int need = g_modeEdges ? intra_needs(blk, p, hA, hL) : 7;
                     if (c->granOk && g_packFused) {
-                        dep = edge_scan(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0);
+                        dep = edge_scan(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0, need);
                     } else {
-                        dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL);
-                        edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0);
+                        dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, need);
+                        edge_owners(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0, need);
                     }
                     if (p && blk.uv_mode == AV1R_UV_CFL_PRED) {  // the co-located luma (incl. sub-8x8 neighbours)
                         const int lx0 = t.x >> 1, ly0 = t.y >> 1, lx1 = (2 * (t.x + w) - 1) >> 2, ly1 = (2 * (t.y + hh) - 1) >> 2;
@@ -1168,8 +1211,8 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
-        fprintf(stderr, "av1r pack: blocks %zu tbs %zu coefs %zu items %zu (%zu) deps %zu done %zu tbres %zu resid %zu lr %zu\n", szBlk,
-            szTb, szCoef, szItems, c->items.size(), szDeps, szDone, szTbRes, szResS + szResL, szLr);
+        fprintf(stderr, "av1r pack: blocks %zu tbs %zu coefs %zu items %zu (%zu) deps %zu done %zu tbres %zu resid %zu lr %zu levels %zu\n", szBlk,
+            szTb, szCoef, szItems, c->items.size(), szDeps, szDone, szTbRes, szResS + szResL, szLr, c->levels.size());
     if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {
