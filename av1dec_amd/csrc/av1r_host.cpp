@@ -1211,8 +1211,17 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
+    {
         fprintf(stderr, "av1r pack: blocks %zu tbs %zu coefs %zu items %zu (%zu) deps %zu done %zu tbres %zu resid %zu lr %zu levels %zu\n", szBlk,
             szTb, szCoef, szItems, c->items.size(), szDeps, szDone, szTbRes, szResS + szResL, szLr, c->levels.size());
+        // k_flow items (large, small) per level: the first levels, then the rest
+        uint32_t rest[2] = {};
+        for (size_t l = 0; l < c->levels.size(); l++) {
+            if (l < 4) fprintf(stderr, "  level %zu: %u large %u small\n", l, c->levels[l].fcnt[1], c->levels[l].fcnt[2]);
+            else rest[0] += c->levels[l].fcnt[1], rest[1] += c->levels[l].fcnt[2];
+        }
+        fprintf(stderr, "  levels 4+: %u large %u small\n", rest[0], rest[1]);
+    }
     if (!host) return AV1R_OK;
     size_t off = 0;
     auto put = [&](const void* src, size_t n, size_t sz) {

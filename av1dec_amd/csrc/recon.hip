@@ -502,27 +502,46 @@ DEV int pred_direct(const RefSel& R, int r, int c, int R0, int R1)
 }
 
 // Stage the (rh + 7) x (rw + 7) reference window of PU-relative region
-// [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin).  Rows are
-// clamped per row; when no column needs clamping the row is moved as aligned dwords
-// (two loads funnel-shifted into one aligned LDS dword), otherwise byte by byte.
-template <int NT = 64>
+// [rx0, rx0 + rw) x [ry0, ry0 + rh) (3 left/above, 4 right/below filter margin), for rw,
+// rh <= S.  Rows are clamped per row.  When no column needs clamping, each lane moves whole
+// rows: one row is at most ND + 1 aligned source dwords, loaded at once (wide loads) and
+// byte-aligned into ND window dwords -- a window costs one memory round trip (the earlier
+// per-dword loop waited for each iteration's loads: two round trips per 8x8 luma window of
+// k_inter_s, up to seven per 32x32 one of k_inter).  Otherwise byte by byte.  The last
+// source dword of a row may lie up to 7 bytes past the window's right edge: inside the
+// row's stride padding (planes carry a 64-pixel margin).
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+template <int NT = 64, int S = TS>
 DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, int rh, int wcs = WC)
 {
     const int wx0 = (R.startX >> 10) - 3 + rx0, wy0 = (R.startY >> 10) - 3 + ry0;
     const int wc = rw + 7, wr = rh + 7;
+    const int lane = il_lane<NT>();
     if (wx0 >= 0 && wx0 + wc - 1 <= R.lastX) {
-        const int ndw = (wc + 3) >> 2, sh = (wx0 & 3) * 8;
-        const int ax0 = wx0 & ~3;
-        for (int q = il_lane<NT>(); q < ndw * wr; q += NT) {
-            const int i = q / ndw, d = q - i * ndw;
-            const uint8_t* row = R.p.p + (size_t)CLIP3(0, R.lastY, wy0 + i) * R.p.stride + ax0 + 4 * d;
-            const uint32_t lo = *reinterpret_cast<const uint32_t*>(row);
-            const uint32_t hi = *reinterpret_cast<const uint32_t*>(row + 4);
-            *reinterpret_cast<uint32_t*>(win + i * wcs + 4 * d) = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+        constexpr int ND = (S + 7 + 3) / 4;     // window dwords per row, at most
+        constexpr int NV = (ND + 1 + 3) / 4;    // 16-byte source loads per row
+        const int ndw = (wc + 3) >> 2;
+        const uint32_t sh = (uint32_t)(wx0 & 3);
+        const uint8_t* base = R.p.p + (wx0 & ~3);
+        for (int i = lane; i < wr; i += NT) {
+            const u32x4a4* src = reinterpret_cast<const u32x4a4*>(base + (size_t)CLIP3(0, R.lastY, wy0 + i) * R.p.stride);
+            uint32_t v[4 * NV];
+#pragma unroll
+            for (int q = 0; q < NV; q++) {
+                const u32x4a4 x = src[q];
+                v[4 * q] = x.x;
+                v[4 * q + 1] = x.y;
+                v[4 * q + 2] = x.z;
+                v[4 * q + 3] = x.w;
+            }
+            uint32_t* dst = reinterpret_cast<uint32_t*>(win + i * wcs);
+#pragma unroll
+            for (int d = 0; d < ND; d++)
+                if (d < ndw) dst[d] = __builtin_amdgcn_alignbyte(v[d + 1], v[d], sh);
         }
         return;
     }
-    for (int q = il_lane<NT>(); q < wc * wr; q += NT) {
+    for (int q = lane; q < wc * wr; q += NT) {
         int i = q / wc, j = q - i * wc;
         int yy = CLIP3(0, R.lastY, wy0 + i), xx = CLIP3(0, R.lastX, wx0 + j);
         win[i * wcs + j] = R.p.p[(size_t)yy * R.p.stride + xx];
@@ -702,7 +721,40 @@ DEV WedgeSel wedge_select(int bs, int wedge)
 }
 
 // getDistanceWeights (InterPredict.cpp:917-960)
-DEV void distance_weights(const KParams& k, const av1r_mi& info, int& fwd, int& bck)
+// The mode info a prediction unit of block `blk` uses: the block's own, which its record
+// carries (loaded with the record: no dependent load), unless a sub-8x8 chroma unit takes a
+// neighbour's from the mode-info grid (Block.cpp:146-174)
+struct PuInfo {
+    int16_t mv[2][2];
+    int8_t ref_frame[2];
+    uint8_t filt;
+};
+DEV PuInfo pu_info(const KParams& k, const av1r_block& blk, int candRow, int candCol)
+{
+    PuInfo p;
+    if (candRow == blk.mi_row && candCol == blk.mi_col) {
+#pragma unroll
+        for (int l = 0; l < 2; l++) {
+            p.mv[l][0] = blk.mv[l][0];
+            p.mv[l][1] = blk.mv[l][1];
+            p.ref_frame[l] = blk.ref_frame[l];
+        }
+        p.filt = blk.filt;
+    } else {
+        const av1r_mi& m = mi_at(k, candRow, candCol);
+#pragma unroll
+        for (int l = 0; l < 2; l++) {
+            p.mv[l][0] = m.mv[l][0];
+            p.mv[l][1] = m.mv[l][1];
+            p.ref_frame[l] = m.ref_frame[l];
+        }
+        p.filt = m.filt;
+    }
+    return p;
+}
+
+template <class MI>
+DEV void distance_weights(const KParams& k, const MI& info, int& fwd, int& bck)
 {
     int d1 = k.hdr->ref_dist[info.ref_frame[0] & 7];
     int d0 = k.hdr->ref_dist[info.ref_frame[1] & 7];
@@ -735,7 +787,7 @@ DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, in
     int candRow, int candCol, RefSel* R)
 {
     const av1r_frame_hdr& hd = *k.hdr;
-    const av1r_mi& info = mi_at(k, candRow, candCol);
+    const PuInfo info = pu_info(k, blk, candRow, candCol);
     const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
     const int isIntrabc = (blk.flags & AV1R_BLK_INTRABC) != 0;
     const int isGlobalMode = blk.y_mode == AV1R_GLOBALMV || blk.y_mode == AV1R_GLOBAL_GLOBALMV;
@@ -775,7 +827,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, 
     int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy)
 {
     const int t = il_lane<NT>();
-    const av1r_mi& info = mi_at(k, candRow, candCol);
+    const PuInfo info = pu_info(k, blk, candRow, candCol);
     const int sub = plane ? 1 : 0;
     RefSel R[2];
     const int isCompound = setup_refs(k, blk, plane, x, y, w, h, candRow, candCol, R);
@@ -811,8 +863,8 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, 
     const int ryA = ry0, rhA = rh;
     for (int cy = 0; cy < rhA; cy += chunkH) {
     const int ry0 = ryA + cy, rh = imin(chunkH, rhA - cy);  // this chunk
-    if (R[0].useWin) load_window<NT>(R[0], L.win[0], rx0, ry0, rw, rh, L.WCS);
-    if (isCompound && R[1].useWin) load_window<NT>(R[1], L.win[1], rx0, ry0, rw, rh, L.WCS);
+    if (R[0].useWin) load_window<NT, TSZ>(R[0], L.win[0], rx0, ry0, rw, rh, L.WCS);
+    if (isCompound && R[1].useWin) load_window<NT, TSZ>(R[1], L.win[1], rx0, ry0, rw, rh, L.WCS);
     il_sync<NT>();
     if (R[0].useWin && !integer[0]) hpass<NT>(L.win[0], L.u.hbw[0], rw, rh, hf[0], R0, L.WCS, TSZ);
     if (R[0].warp) warp_hpass<NT>(R[0], L.u.hbw[0], rx0, ry0, rw, rh, x, y, sub, R0);
@@ -916,7 +968,7 @@ DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, i
     int ry0, int rw, int rh)
 {
     const int t = threadIdx.x;
-    const av1r_mi& info = mi_at(k, blk.mi_row, blk.mi_col);
+    const PuInfo info = pu_info(k, blk, blk.mi_row, blk.mi_col);
     RefSel R[2][2];
     const int isCompound = setup_refs(k, blk, 1, x, y, w, h, blk.mi_row, blk.mi_col, R[0]);
     if (!R[0][0].useWin || (isCompound && !R[0][1].useWin)) return false;
@@ -951,7 +1003,7 @@ DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, i
     for (int p = 0; p < 2; p++)
 #pragma unroll
         for (int l = 0; l < 2; l++)
-            if (l <= isCompound) load_window(R[p][l], win + (p * 2 + l) * C2_WIN, rx0, ry0, rw, rh, C2_WS);
+            if (l <= isCompound) load_window<64, 16>(R[p][l], win + (p * 2 + l) * C2_WIN, rx0, ry0, rw, rh, C2_WS);
     __syncthreads();
 #pragma unroll
     for (int p = 0; p < 2; p++)
@@ -1056,7 +1108,7 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int pl
                         vf[u] = av1r_subpel_filters[(R.filtY * 16 + vph) * 8 + u];
                     }
                     if (R.useWin) {
-                        load_window<NT>(R, L.win[0], rx0, ry0, rw, rh, L.WCS);
+                        load_window<NT, TSZ>(R, L.win[0], rx0, ry0, rw, rh, L.WCS);
                         il_sync<NT>();
                         if (!integer) hpass<NT>(L.win[0], L.u.hbw[0], rw, rh, hf, 3, L.WCS, TSZ);
                         il_sync<NT>();
@@ -1436,10 +1488,12 @@ struct SmallLds {
 // sub-pel filter, :319-383; the average / distance blend of :1022-1049) of w x h <= 8 x 8
 // at plane position (x, y), by NT lanes.
 template <int NT, int MS>
-DEV void small_pu(const KParams& k, SmallLds<MS>& L, int ct, int plane, int x, int y, int w, int h, int candRow, int candCol)
+DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int plane, int x, int y, int w, int h, int candRow,
+    int candCol)
 {
     const int t = threadIdx.x & (NT - 1);
-    const av1r_mi& info = mi_at(k, candRow, candCol);
+    const int ct = blk.compound_type;
+    const PuInfo info = pu_info(k, blk, candRow, candCol);
     const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
     int16_t hf[2][8], vf[2][8];
     int integer[2] = {1, 1};
@@ -1456,7 +1510,7 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, int ct, int plane, int x, i
             hf[l][u] = av1r_subpel_filters[(fx * 16 + hph) * 8 + u];
             vf[l][u] = av1r_subpel_filters[(fy * 16 + vph) * 8 + u];
         }
-        load_window<NT>(R, L.win[l], 0, 0, w, h, MS + 8);
+        load_window<NT, MS>(R, L.win[l], 0, 0, w, h, MS + 8);
     }
     coop_sync<NT>();
 #pragma unroll
@@ -1518,8 +1572,8 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
         for (int yy = 0; yy < G.ph; yy += G.predH, r++) {
             int c = 0;
             for (int xx = 0; xx < G.pw; xx += G.predW, c++)
-                small_pu<NT, MS>(k, L[g], blk.compound_type, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH,
-                    G.candRow + r, G.candCol + c);
+                small_pu<NT, MS>(k, L[g], blk, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
+                    G.candCol + c);
         }
     }
 }
