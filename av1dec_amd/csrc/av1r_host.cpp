@@ -222,6 +222,7 @@ struct av1r_ctx {
     size_t resCap = 0;
     uint32_t flowSpins = 0;     // av1r_set_flow_spins (0: FLOW_SPINS)
     int flowPerCU = 8;          // k_flow workgroups per CU of this context's launches (capped by occupancy)
+    int flowGridCap = 0;        // > 0: at most this many k_flow workgroups (a solo deep frame, AV1R_SOLO_GRID)
     // a deep frame launched alone on this context's own stream (batched entry points): its
     // completion; av1r_busy reports whether it is still running
     hipEvent_t soloDone = nullptr;
@@ -407,6 +408,66 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
     }
     if (b->n_blocks >= (1u << 26) || b->n_tbs >= (1u << 30))
         return fail(c, AV1R_E_UNSUPPORTED, "too many blocks / transform blocks in one frame");
+    // the checks below in branch-free passes first (every violation ORed into one word);
+    // only a batch that fails one walks the detailed loops, which name the first violation
+    {
+        uint32_t badB = 0, badT = 0;
+        bool anyPal = false;
+        for (uint32_t i = 0; i < b->n_blocks; i++) {
+            const av1r_block& k = b->blocks[i];
+            const uint32_t sz = k.mi_size < AV1R_BLOCK_SIZES ? k.mi_size : 0;
+            const bool inter = k.flags & AV1R_BLK_INTER;
+            badB |= (k.mi_size >= AV1R_BLOCK_SIZES) | ((uint32_t)k.mi_row + av1r_num4x4h[sz] > (uint32_t)ah4) |
+                    ((uint32_t)k.mi_col + av1r_num4x4w[sz] > (uint32_t)aw4) | ((uint64_t)k.first_tb + k.n_tbs > b->n_tbs) |
+                    (k.palette_size_y > 8) | (k.palette_size_uv > 8);
+            anyPal |= (k.palette_size_y | k.palette_size_uv) != 0;
+            const uint32_t badI = (k.motion_mode > 2) | (k.compound_type > 4) | (k.interintra_mode > 3) |
+                                  ((k.compound_type == AV1R_COMPOUND_WEDGE) & ((k.wedge_index > 15) | !av1r_wedge_bits[sz])) |
+                                  (((k.flags & AV1R_BLK_INTERINTRA) != 0) & ((k.mi_size < AV1R_BLOCK_8X8) | (k.mi_size > AV1R_BLOCK_32X32)));
+            const uint32_t badA = (k.y_mode > AV1R_PAETH_PRED) | (((k.flags & AV1R_BLK_HAS_CHROMA) != 0) & (k.uv_mode > AV1R_UV_CFL_PRED)) |
+                                  (((k.flags & AV1R_BLK_FILTER_INTRA) != 0) & (k.filter_intra_mode > 4));
+            badB |= inter ? badI : badA;
+        }
+        for (uint32_t i = 0; i < b->n_tbs; i++) {
+            const av1r_tb& t = b->tbs[i];
+            const uint32_t tx = t.tx_size < AV1R_TX_SIZES ? t.tx_size : 0;
+            const int sub = t.plane ? 1 : 0;
+            badT |= (t.block >= b->n_blocks) | (t.plane > 2) | (t.tx_size >= AV1R_TX_SIZES) | (t.tx_type > 15) |
+                    (t.x + av1r_tx_w[tx] > ((aw4 * 4) >> sub) + 64) | (t.y + av1r_tx_h[tx] > ((ah4 * 4) >> sub) + 64) |
+                    ((uint64_t)t.coef_off + t.coef_cnt > b->n_coefs);
+        }
+        uint32_t badC = 0;
+        if (!badT)
+            for (uint32_t i = 0; i < b->n_tbs; i++) {
+                const av1r_tb& t = b->tbs[i];
+                const int log2Area = std::min<int>(av1r_tx_w_log2[t.tx_size], 5) + std::min<int>(av1r_tx_h_log2[t.tx_size], 5);
+                uint32_t acc = 0;
+                const uint32_t* cf = b->coefs + t.coef_off;
+                for (int q = 0; q < t.coef_cnt; q++) acc |= cf[q];
+                badC |= (acc & 1023u) >> log2Area;
+            }
+        // palette blocks (rare): their records and the map windows of their transform blocks
+        for (uint32_t i = 0; anyPal && !badB && i < b->n_blocks; i++) {
+            const av1r_block& k = b->blocks[i];
+            if (!(k.palette_size_y || k.palette_size_uv)) continue;
+            if ((uint64_t)k.palette_off + AV1R_PALETTE_HDR > b->n_palette) badB = 1;
+            else {
+                const uint8_t* ph = b->palette + k.palette_off;
+                if ((uint64_t)k.palette_off + AV1R_PALETTE_HDR + ph[0] * ph[1] + ph[2] * ph[3] > b->n_palette) badB = 1;
+            }
+            if (badB || (k.flags & AV1R_BLK_INTER)) continue;
+            const uint8_t* ph = b->palette + k.palette_off;
+            for (uint32_t ti = k.first_tb; ti < k.first_tb + k.n_tbs; ti++) {
+                const av1r_tb& t = b->tbs[ti];
+                if (!(t.plane ? k.palette_size_uv : k.palette_size_y)) continue;
+                const int sub = t.plane ? 1 : 0;
+                const int bx = t.x - (k.mi_col >> sub) * 4, by = t.y - (k.mi_row >> sub) * 4;
+                const int mw = t.plane ? ph[2] : ph[0], mh = t.plane ? ph[3] : ph[1];
+                badT |= (bx < 0) | (by < 0) | (bx + av1r_tx_w[t.tx_size] > mw) | (by + av1r_tx_h[t.tx_size] > mh);
+            }
+        }
+        if (!badB && !badT && !badC) goto lr_check;
+    }
     for (uint32_t i = 0; i < b->n_blocks; i++) {
         const av1r_block& k = b->blocks[i];
         if (k.mi_size >= AV1R_BLOCK_SIZES || k.mi_row >= ah4 || k.mi_col >= aw4
@@ -458,6 +519,7 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                 return fail(c, AV1R_E_INVALID, "tb %u palette map window", i);
         }
     }
+lr_check:
     if (h->uses_lr) {
         for (int p = 0; p < 3; p++) {
             if (h->lr_type[p] == AV1R_RESTORE_NONE) continue;
@@ -1725,7 +1787,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             if (chain) lock.lock();
             // the persistent grid: every resident slot (lc->flowPerCU workgroups per CU; a
             // solo deep frame takes one per CU and leaves the rest to concurrent batches)
-            const int grid = (int)std::min<size_t>(flow_grid(lc->device, lc->flowPerCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            int grid = (int)std::min<size_t>(flow_grid(lc->device, lc->flowPerCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            if (lc->flowGridCap > 0) grid = std::max(FLOW_QUEUES, std::min(grid, lc->flowGridCap / FLOW_QUEUES * FLOW_QUEUES));
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
@@ -1855,10 +1918,15 @@ static int launch_solo(FrameJob& j)
     std::vector<FrameJob> one(1, j);
     // AV1R_SOLO_PER_CU: k_flow workgroups per CU of a solo deep frame (A/B)
     static const int soloPer = getenv("AV1R_SOLO_PER_CU") ? std::max(1, atoi(getenv("AV1R_SOLO_PER_CU"))) : 1;
+    // AV1R_SOLO_GRID: at most this many workgroups for it (0: one per CU) -- a key frame keeps
+    // ~60 items in flight, its idle pollers on every CU compete with the batches beside it
+    static const int soloGrid = getenv("AV1R_SOLO_GRID") ? std::max(0, atoi(getenv("AV1R_SOLO_GRID"))) : 0;
     const int per = m->flowPerCU;
     m->flowPerCU = soloPer;
+    m->flowGridCap = soloGrid;
     int rc = launch_jobs(m, one);
     m->flowPerCU = per;
+    m->flowGridCap = 0;
     if (rc) return rc;
     HIPCHK(hipEventRecord(m->soloDone, m->stream));
     m->soloPending = true;
