@@ -157,6 +157,62 @@ DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& 
     return true;
 }
 
+// The four lines of one edge unit from registers.  The unit's samples come in dwords: a
+// vertical edge (pass 0) at x reads x - 4 .. x + 3 of each of its rows (x - 8 .. x + 7 for a
+// 16-wide filter: its edge is >= 16 from the plane's left), a horizontal edge (pass 1) at y
+// rows y - 4 .. y + 3 (y - 8 .. y + 7) of its four columns, one dword per row.  All of a
+// unit's loads go out before its first filter (one memory round trip; the byte form issued
+// up to 56 byte loads per unit).  Written back: the samples a filter of this size may modify
+// (p1..q1 for 4 taps and chroma, p2..q2 for luma 8, p5..q5 for 16).  Rewriting an unmodified
+// sample there is safe: the filter length is bounded by the transform sizes on both sides,
+// so no other edge of the pass writes inside this footprint.
+DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const LfEdge& e)
+{
+    const bool wide = e.filterSize == 16;
+    const int n = wide ? 6 : (e.filterSize == 8 && !plane) ? 3 : 2;  // samples written per side
+    if (pass == 0) {
+        uint32_t d[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(P.p + (size_t)(yP + i) * P.stride + xP);
+            d[i][1] = row[-1];
+            d[i][2] = row[0];
+            d[i][0] = wide ? row[-2] : 0u;
+            d[i][3] = wide ? row[1] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            int v[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) v[q] = (d[i][q >> 2] >> (8 * (q & 3))) & 0xff;
+            lf_filter(v + 8, 1, plane, e.limit, e.blimit, e.thresh, e.filterSize);
+            uint8_t* row = P.p + (size_t)(yP + i) * P.stride + xP;
+#pragma unroll
+            for (int q = -6; q < 6; q++)
+                if (q >= -n && q < n) row[q] = (uint8_t)v[8 + q];
+        }
+        return;
+    }
+    uint32_t d[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const bool need = (r >= 4 && r < 12) || wide;
+        d[r] = need ? *reinterpret_cast<const uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) v[r] = (d[r] >> (8 * j)) & 0xff;
+        lf_filter(v + 8, 1, plane, e.limit, e.blimit, e.thresh, e.filterSize);
+#pragma unroll
+        for (int r = 2; r < 14; r++) d[r] = (d[r] & ~(0xffu << (8 * j))) | ((uint32_t)(v[r] & 0xff) << (8 * j));
+    }
+#pragma unroll
+    for (int r = 2; r < 14; r++)
+        if (r >= 8 - n && r < 8 + n) *reinterpret_cast<uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) = d[r];
+}
+
 // one lane per (plane, 4x4 unit) edge of pass `pass`
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass)
 {
@@ -186,11 +242,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int p
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
     LfEdge e;
     if (!lf_edge(k, plane, pass, xP, yP, e)) return;
-    const DevPlane& P = k.cur.pl[plane];
-    const int dx = pass == 0, dy = pass == 1;
-    const int step = dx + dy * P.stride;
-    for (int i = 0; i < 4; i++)
-        lf_filter(P.p + (size_t)(yP + dx * i) * P.stride + xP + dy * i, step, plane, e.limit, e.blimit, e.thresh, e.filterSize);
+    lf_unit(k.cur.pl[plane], plane, pass, xP, yP, e);
 }
 
 // ------------------------------------------------------------------------------------
@@ -403,9 +455,44 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
     const bool edge = x0 < CD_H || y0 < CD_H || x0 + 64 + CD_H > limX || y0 + 64 + CD_H > limY;
     const int cx0 = x0 / 2, cy0 = y0 / 2, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
     const bool cedge = cx0 < CD_H || cy0 < CD_H || cx0 + 32 + CD_H > climX || cy0 + 32 + CD_H > climY;
-    cd_stage(&L.y[0][0], CD_LS, CD_LR, k.cur.pl[0], x0, y0, edge, limX - 1, limY - 1);
-    cd_stage(&L.uv[0][0][0], CD_CS, CD_CR, k.cur.pl[1], cx0, cy0, cedge, climX - 1, climY - 1);
-    cd_stage(&L.uv[1][0][0], CD_CS, CD_CR, k.cur.pl[2], cx0, cy0, cedge, climX - 1, climY - 1);
+    if (!edge && !cedge) {
+        // away from the frame edges: every lane's dwords of the three tiles are loaded before
+        // its first LDS store (one memory round trip; the staging loop waited once per
+        // iteration, ~11 round trips per region)
+        constexpr int NDY = CD_LS / 4, NY = CD_LR * NDY, QY = (NY + 255) / 256;
+        constexpr int NDC = CD_CS / 4, NC = CD_CR * NDC, QC = (NC + 255) / 256;
+        uint32_t vy[QY], vc[2][QC];
+        // (lanes past a tile load its last dword again: no branch around the loads)
+        const DevPlane PY = k.cur.pl[0], PU = k.cur.pl[1], PV = k.cur.pl[2];
+#pragma unroll
+        for (int u = 0; u < QY; u++) {
+            const int q = imin(t + 256 * u, NY - 1), i = q / NDY, d = q - i * NDY;
+            vy[u] = *reinterpret_cast<const uint32_t*>(PY.p + (size_t)(y0 - CD_H + i) * PY.stride + x0 - CD_X + 4 * d);
+        }
+#pragma unroll
+        for (int u = 0; u < QC; u++) {
+            const int q = imin(t + 256 * u, NC - 1), i = q / NDC, d = q - i * NDC;
+            const size_t o = (size_t)(cy0 - CD_H + i) * PU.stride + cx0 - CD_X + 4 * d;
+            vc[0][u] = *reinterpret_cast<const uint32_t*>(PU.p + o);
+            vc[1][u] = *reinterpret_cast<const uint32_t*>(PV.p + o);
+        }
+#pragma unroll
+        for (int u = 0; u < QY; u++) {
+            const int q = t + 256 * u, i = q / NDY, d = q - i * NDY;
+            if (q < NY) *reinterpret_cast<uint32_t*>(&L.y[i][4 * d]) = vy[u];
+        }
+#pragma unroll
+        for (int pl = 0; pl < 2; pl++)
+#pragma unroll
+            for (int u = 0; u < QC; u++) {
+                const int q = t + 256 * u, i = q / NDC, d = q - i * NDC;
+                if (q < NC) *reinterpret_cast<uint32_t*>(&L.uv[pl][i][4 * d]) = vc[pl][u];
+            }
+    } else {
+        cd_stage(&L.y[0][0], CD_LS, CD_LR, k.cur.pl[0], x0, y0, edge, limX - 1, limY - 1);
+        cd_stage(&L.uv[0][0][0], CD_CS, CD_CR, k.cur.pl[1], cx0, cy0, cedge, climX - 1, climY - 1);
+        cd_stage(&L.uv[1][0][0], CD_CS, CD_CR, k.cur.pl[2], cx0, cy0, cedge, climX - 1, climY - 1);
+    }
     if (t < 64) {
         const int br = r0 + (t >> 3) * 2, bc = c0 + (t & 7) * 2;
         int f = 0;

@@ -1002,11 +1002,10 @@ int Parser::finish_frame()
     // CDFs of the context_update_tile_id tile (Tile::frame_end_update_cdf)
     if (!fh.disable_frame_end_update_cdf) cdf = saved_cdf;
     // mode-info grid (refdump.cpp fillFrameTables)
-    F.mi.resize(mi.size());
+    F.mi.resize(mi.size());  // (value-initialised: every field not set below is 0)
     for (size_t i = 0; i < mi.size(); i++) {
         const MiInfo& m = mi[i];
         av1r_mi& d = F.mi[i];
-        memset(&d, 0, sizeof(d));
         for (int l = 0; l < 2; l++) {
             d.mv[l][0] = m.mv[l].r;
             d.mv[l][1] = m.mv[l].c;

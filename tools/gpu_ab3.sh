@@ -6,7 +6,7 @@ mkdir -p gpurun_out/ab3
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
     > gpurun_out/gputest.log 2>&1 || { tail -40 gpurun_out/gputest.log; exit 1; }
 tail -2 gpurun_out/gputest.log
-for i in 1 2; do
+for i in $(seq 1 ${AB_ROUNDS:-2}); do
   for v in "" "$@"; do
     case "$v" in *.so) e="AV1R_LIB=$v";; *) e="$v";; esac
     env $e timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu --ivf-frames 0 --output-steps 0 \
