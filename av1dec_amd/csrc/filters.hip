@@ -720,7 +720,10 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
         anyW |= L.unit[u].type == AV1R_RESTORE_WIENER;
         anyS |= L.unit[u].type == AV1R_RESTORE_SGRPROJ;
     }
-    auto unitOf = [&](int c) { return imin((x0 + CLIP3(0, tw - 1, c)) / us, cols - 1) - uc0; };
+    const int usl = __builtin_ctz((unsigned)us);  // unit sizes are powers of two (32..256, validate())
+    auto unitOf = [&](int c) { return imin((x0 + CLIP3(0, tw - 1, c)) >> usl, cols - 1) - uc0; };
+    // q -> (row, column) of a tw-wide tile: a shift for the full-width tiles
+    const bool fullW = tw == LR_TW;
     const int rounds = anyW && anyS ? 2 : 1;
     for (int rd = 0; rd < rounds; rd++) {
         const bool doW = anyW && (rounds == 1 || rd == 0), doS = anyS && (rounds == 1 || rd == 1);
@@ -729,7 +732,7 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
             // wienerFilter horizontal pass (LoopRestoration.cpp:253-265)
             const int offset = 1 << (8 + 7 - 3 - 1), limit = (1 << (8 + 1 + 7 - 3)) - 1;
             for (int q = t; q < (th + 6) * tw; q += 256) {
-                int i = q / tw, c = q - i * tw;
+                const int i = fullW ? q / LR_TW : q / tw, c = q - i * tw;
                 const av1r_lr_unit& u = L.unit[unitOf(c)];
                 if (u.type != AV1R_RESTORE_WIENER) continue;
                 int hf3 = 128 - 2 * (u.wiener[1][0] + u.wiener[1][1] + u.wiener[1][2]);
@@ -787,7 +790,7 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
         }
         __syncthreads();
         for (int q = t; q < tw * th; q += 256) {
-            const int r = q / tw, c = q - r * tw;
+            const int r = fullW ? q / LR_TW : q / tw, c = q - r * tw;
             const int x = x0 + c, y = ty0 + r;
             const int cdef = L.src[r + 3][c + 4];
             int outv = cdef;

@@ -784,7 +784,7 @@ DEV void distance_weights(const KParams& k, const MI& info, int& fwd, int& bck)
 // motion vector scaling, warp choice (local / global, Block.cpp:1179-1200) and filters.
 // Returns isCompound.
 DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, int y, int w, int h,
-    int candRow, int candCol, RefSel* R)
+    int candRow, int candCol, RefSel* R, const int32_t* lw)
 {
     const av1r_frame_hdr& hd = *k.hdr;
     const PuInfo info = pu_info(k, blk, candRow, candCol);
@@ -804,7 +804,7 @@ DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, in
         if (!(w < 8 || h < 8) && !hd.force_integer_mv) {
             if (blk.motion_mode == AV1R_LOCALWARP && (blk.flags & AV1R_BLK_LOCAL_VALID)) {
                 R[l].warp = 1;
-                R[l].wp = blk.local_warp;
+                R[l].wp = lw;  // (the block record in memory: blk may be a register copy)
             } else if (isGlobalMode && hd.gm_type[refFrame & 7] > AV1R_GM_TRANSLATION && globalValid
                 && !R[l].scaled) {
                 R[l].warp = 2;
@@ -824,13 +824,13 @@ DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, in
 // L.tile[(toy + r) * TS + tox + c].  Ends with a barrier.
 template <int NT, int TSZ>
 DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int plane, int x, int y,
-    int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy)
+    int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy, const int32_t* lw)
 {
     const int t = il_lane<NT>();
     const PuInfo info = pu_info(k, blk, candRow, candCol);
     const int sub = plane ? 1 : 0;
     RefSel R[2];
-    const int isCompound = setup_refs(k, blk, plane, x, y, w, h, candRow, candCol, R);
+    const int isCompound = setup_refs(k, blk, plane, x, y, w, h, candRow, candCol, R, lw);
     const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
     int16_t hf[2][8], vf[2][8];
     int integer[2];
@@ -965,14 +965,14 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, 
 #define C2_HB (23 * C2_HS)         // one chroma intermediate
 #define C2_TILE (16 * TS)          // chroma tile of plane 2 after plane 1's
 DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, int x, int y, int w, int h, int rx0,
-    int ry0, int rw, int rh)
+    int ry0, int rw, int rh, const int32_t* lw)
 {
     const int t = threadIdx.x;
     const PuInfo info = pu_info(k, blk, blk.mi_row, blk.mi_col);
     RefSel R[2][2];
-    const int isCompound = setup_refs(k, blk, 1, x, y, w, h, blk.mi_row, blk.mi_col, R[0]);
+    const int isCompound = setup_refs(k, blk, 1, x, y, w, h, blk.mi_row, blk.mi_col, R[0], lw);
     if (!R[0][0].useWin || (isCompound && !R[0][1].useWin)) return false;
-    setup_refs(k, blk, 2, x, y, w, h, blk.mi_row, blk.mi_col, R[1]);
+    setup_refs(k, blk, 2, x, y, w, h, blk.mi_row, blk.mi_col, R[1], lw);
     const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
     int16_t hf[2][8], vf[2][8];
     int integer[2] = {1, 1};
@@ -1177,7 +1177,9 @@ template <int NT, int TSZ>
 DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ>& L, unsigned long long* tr)
 {
     const int t = il_lane<NT>();
-    const av1r_block& blk = k.blocks[bi];
+    // the block record in scalar registers (one scalar load: a tile's fields are uniform)
+    const av1r_block blk = sload(k.blocks + bi);
+    const int32_t* lw = k.blocks[bi].local_warp;
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
     // timeline (-DAV1R_TRACE): 1 = block size | motion mode << 8 | compound << 12, 8 + plane
     // after each plane's store, 11 after the luma geometry, 12 after the luma prediction
@@ -1189,7 +1191,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
         if constexpr (TSZ == TS) {
             if (plane == 1 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col &&
                 blk.motion_mode != AV1R_OBMC_CAUSAL && !(G.TW & 3) &&
-                predict_chroma2(k, blk, L, G.baseX, G.baseY, G.pw, G.ph, G.TX0, G.TY0, G.TW, G.TH)) {
+                predict_chroma2(k, blk, L, G.baseX, G.baseY, G.pw, G.ph, G.TX0, G.TY0, G.TW, G.TH, lw)) {
                 for (int q = t; q < 2 * G.TW * G.TH; q += NT) {
                     const int p = q >= G.TW * G.TH, e = q - p * G.TW * G.TH;
                     const int i = e / G.TW, j = e - i * G.TW;
@@ -1210,7 +1212,7 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
                     const int iy0 = imax(yy, G.TY0), iy1 = imin(yy + G.predH, G.TY0 + G.TH);
                     if (ix0 < ix1 && iy0 < iy1)
                         predict_pu<NT, TSZ>(k, blk, L, plane, G.baseX + xx, G.baseY + yy, G.predW, G.predH, G.candRow + r,
-                            G.candCol + c, ix0 - xx, iy0 - yy, ix1 - ix0, iy1 - iy0, xx - G.TX0, yy - G.TY0);
+                            G.candCol + c, ix0 - xx, iy0 - yy, ix1 - ix0, iy1 - iy0, xx - G.TX0, yy - G.TY0, lw);
                     c++;
                 }
                 r++;
