@@ -333,6 +333,12 @@ DEV void stp_c(const DevPlane& p, int x, int y, uint8_t v, bool coh)
 // The read sites today: gran_gather (intra_dev.h), tb_predict's CFL luma, fi_run's CFL
 // luma (intra_fast.h) and ii_item's edges and inter prediction (recon.hip); each is marked
 // "(flow read site)".  Scalar loads (sload / stab / sfield) are for batch data only.
+// One deliberate exception: an intra edge is gathered whole, but the host names (masks /
+// dependency lists) only the units the prediction mode uses (av1r_host.cpp intra_needs:
+// above-right for zone 1, below-left for zone 3, the corner for Paeth / directional /
+// filter-intra); the other units are read without a wait and may be stale or half-written,
+// and no predicted pixel depends on them.  A predictor that starts reading a sample its mode
+// did not read before must widen intra_needs first.
 DEV bool strip_plain(int kstrip, bool gran) { return kstrip && gran; }  // (k_strip runs only with granules)
 
 // Work-item encoding of the per-level item lists (host schedule -> k_level):
