@@ -141,8 +141,9 @@ DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& 
     const int skip = info.flags & AV1R_MI_SKIP;
     const int isIntra = info.ref_frame[0] <= AV1R_INTRA_FRAME;
     const int prevTx = mi_at(k, prevRow, prevCol).lf_tx[plane];
-    const int isBlockEdge = !pass ? !(xP % (av1r_num4x4w[psz] * 4)) : !(yP % (av1r_num4x4h[psz] * 4));
-    const int isTxEdge = !pass ? !(xP % av1r_tx_w[txSz]) : !(yP % av1r_tx_h[txSz]);
+    // (block and transform sides are powers of two: the remainders as masks, no division)
+    const int isBlockEdge = !pass ? !(xP & (av1r_num4x4w[psz] * 4 - 1)) : !(yP & (av1r_num4x4h[psz] * 4 - 1));
+    const int isTxEdge = !pass ? !(xP & (av1r_tx_w[txSz] - 1)) : !(yP & (av1r_tx_h[txSz] - 1));
     if (!(isTxEdge && (isBlockEdge || !skip || isIntra))) return false;
     const int base = !pass ? imin(av1r_tx_w[prevTx], av1r_tx_w[txSz]) : imin(av1r_tx_h[prevTx], av1r_tx_h[txSz]);
     e.filterSize = !plane ? imin(16, base) : imin(8, base);
