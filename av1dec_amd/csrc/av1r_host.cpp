@@ -446,7 +446,9 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                 for (int q = 0; q < t.coef_cnt; q++) acc |= cf[q];
                 badC |= (acc & 1023u) >> log2Area;
             }
-        // palette blocks (rare): their records and the map windows of their transform blocks
+        // palette blocks (rare): their records, then the map window of every transform block
+        // whose OWN block (t.block: what build_schedule and the device's tb_predict follow) is
+        // an intra palette block -- wherever that TB sits in the TB array
         for (uint32_t i = 0; anyPal && !badB && i < b->n_blocks; i++) {
             const av1r_block& k = b->blocks[i];
             if (!(k.palette_size_y || k.palette_size_uv)) continue;
@@ -455,16 +457,16 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                 const uint8_t* ph = b->palette + k.palette_off;
                 if ((uint64_t)k.palette_off + AV1R_PALETTE_HDR + ph[0] * ph[1] + ph[2] * ph[3] > b->n_palette) badB = 1;
             }
-            if (badB || (k.flags & AV1R_BLK_INTER)) continue;
+        }
+        for (uint32_t ti = 0; anyPal && !badB && !badT && ti < b->n_tbs; ti++) {
+            const av1r_tb& t = b->tbs[ti];
+            const av1r_block& k = b->blocks[t.block];
+            if ((k.flags & AV1R_BLK_INTER) || !(t.plane ? k.palette_size_uv : k.palette_size_y)) continue;
             const uint8_t* ph = b->palette + k.palette_off;
-            for (uint32_t ti = k.first_tb; ti < k.first_tb + k.n_tbs; ti++) {
-                const av1r_tb& t = b->tbs[ti];
-                if (!(t.plane ? k.palette_size_uv : k.palette_size_y)) continue;
-                const int sub = t.plane ? 1 : 0;
-                const int bx = t.x - (k.mi_col >> sub) * 4, by = t.y - (k.mi_row >> sub) * 4;
-                const int mw = t.plane ? ph[2] : ph[0], mh = t.plane ? ph[3] : ph[1];
-                badT |= (bx < 0) | (by < 0) | (bx + av1r_tx_w[t.tx_size] > mw) | (by + av1r_tx_h[t.tx_size] > mh);
-            }
+            const int sub = t.plane ? 1 : 0;
+            const int bx = t.x - (k.mi_col >> sub) * 4, by = t.y - (k.mi_row >> sub) * 4;
+            const int mw = t.plane ? ph[2] : ph[0], mh = t.plane ? ph[3] : ph[1];
+            badT |= (bx < 0) | (by < 0) | (bx + av1r_tx_w[t.tx_size] > mw) | (by + av1r_tx_h[t.tx_size] > mh);
         }
         if (!badB && !badT && !badC) goto lr_check;
     }
@@ -555,6 +557,11 @@ struct PackClock {
 // the filters fused into one kernel (av1r_set_filter_fusion; AV1R_FUSED=1)
 // the lean small-intra path of k_flow / k_strip (intra_fast.h); AV1R_FI=0 or
 // av1r_set_fast_intra(0): the generic path (A/B)
+static bool inter_split()
+{
+    static const bool on = getenv("AV1R_INTER_SPLIT") && atoi(getenv("AV1R_INTER_SPLIT")) != 0;
+    return on;
+}
 static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) : 1};
 static std::atomic<int> g_fusedFilters{getenv("AV1R_FUSED") ? atoi(getenv("AV1R_FUSED")) : 0};
 
@@ -1758,8 +1765,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         // stream beside the general k_inter (disjoint tiles).  Measured (tools/gpu_env_ab.sh):
         // 4K x 2 streams device-only +3 % (inter 0.281 -> 0.245 ms/frame), 1080p x 8 -6 %
         // (0.073 -> 0.087): off by default
-        static const bool split = getenv("AV1R_INTER_SPLIT") && atoi(getenv("AV1R_INTER_SPLIT")) != 0;
-        const bool aux = split && lc->aux && total[0] && (total[1] || total[2]) && !trace;
+        const bool aux = inter_split() && lc->aux && total[0] && (total[1] || total[2]) && !trace;
         hipStream_t sp = aux ? lc->aux : st;
         if (aux) {
             HIPCHK(hipEventRecord(lc->auxGo, st));
@@ -2010,9 +2016,14 @@ int av1r_create(int device, av1r_ctx** out)
     }
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->joinEv, hipEventDisableTiming);
-    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
-    (void)hipEventCreateWithFlags(&c->auxGo, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&c->auxDone, hipEventDisableTiming);
+    // the second stream of AV1R_INTER_SPLIT only where that A/B switch is on: streams map
+    // round-robin onto the process's hardware queues at creation, so an idle one per context
+    // would shift how the contexts' main streams share them
+    if (inter_split()) {
+        if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
+        (void)hipEventCreateWithFlags(&c->auxGo, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&c->auxDone, hipEventDisableTiming);
+    }
     for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
@@ -2058,8 +2069,8 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipStreamSynchronize(c->copyStream);
     (void)hipStreamDestroy(c->copyStream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
-    (void)hipEventDestroy(c->auxGo);
-    (void)hipEventDestroy(c->auxDone);
+    if (c->auxGo) (void)hipEventDestroy(c->auxGo);
+    if (c->auxDone) (void)hipEventDestroy(c->auxDone);
     if (c->resDev) (void)hipFree(c->resDev);
     if (c->granDev) (void)hipFree(c->granDev);
     {  // its stream leaves the device's k_flow chain (no later wait refers to it)
@@ -2381,6 +2392,7 @@ struct PipeProf {
     long batches = 0, frames = 0, soloFrames = 0;
 };
 static PipeProf g_pprof;
+static std::mutex g_pprofMu;  // av1r_decode_packed_batch may run on several threads at once
 static const bool g_pipeProf = getenv("AV1R_PIPE_PROF") && atoi(getenv("AV1R_PIPE_PROF")) != 0;
 static double now_s()
 {
@@ -2389,6 +2401,7 @@ static double now_s()
 extern "C" void av1r_pipe_prof_dump(double elapsed)
 {
     if (!g_pipeProf) return;
+    std::lock_guard<std::mutex> lock(g_pprofMu);
     const PipeProf& P = g_pprof;
     fprintf(stderr, "av1r pipe: %.1f ms elapsed, %ld batches (%.2f frames each, %ld solo), launcher: slot wait %.1f ms, "
             "solo launches %.1f ms, shared launches %.1f ms, other %.1f ms\n", 1e3 * elapsed, P.batches,
@@ -2402,7 +2415,12 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
     const double tIn = g_pipeProf ? now_s() : 0;
     struct Tot {
         double t;
-        ~Tot() { if (g_pipeProf) g_pprof.total += now_s() - t; }
+        ~Tot()
+        {
+            if (!g_pipeProf) return;
+            std::lock_guard<std::mutex> lock(g_pprofMu);
+            g_pprof.total += now_s() - t;
+        }
     } tot{tIn};
     if (!ctxs || !pks || n <= 0 || !ctxs[0]) return AV1R_E_INVALID;
     av1r_ctx* lc = ctxs[0];
@@ -2443,7 +2461,10 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         if (U.pending) {  // a launch three frames back may still read this slot
             const double w0 = g_pipeProf ? now_s() : 0;
             HIPCHK(hipEventSynchronize(U.done));
-            if (g_pipeProf) g_pprof.slotWait += now_s() - w0;
+            if (g_pipeProf) {
+                std::lock_guard<std::mutex> lock(g_pprofMu);
+                g_pprof.slotWait += now_s() - w0;
+            }
             U.pending = false;
         }
         if (U.cap < pk->P.cap) {
@@ -2478,6 +2499,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
     }
     const double s1 = g_pipeProf ? now_s() : 0;
     if (g_pipeProf) {
+        std::lock_guard<std::mutex> lock(g_pprofMu);
         g_pprof.solo += s1 - s0;
         g_pprof.batches++;
         g_pprof.frames += n;
@@ -2512,7 +2534,10 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             if (j.c != bl) j.c->joinLead = bl;
         for (auto& j : lv)
             if (j.c != bl) j.c->joinLead = bl;
-        if (g_pipeProf) g_pprof.shared += now_s() - s1;
+        if (g_pipeProf) {
+            std::lock_guard<std::mutex> lock(g_pprofMu);
+            g_pprof.shared += now_s() - s1;
+        }
     }
     for (int i = 0; i < n; i++) {  // the upload slots are free again after their launch
         if (!slots[i]) continue;

@@ -1,4 +1,5 @@
 // api.cpp -- C-ABI of the host parser (include/av1p.h).
+#include <algorithm>
 #include "parser.h"
 
 #include <stdlib.h>
@@ -30,7 +31,7 @@ int av1p_create(av1p_ctx** out)
     // tile-parallel parsing by default (AV1P_TILE_THREADS overrides; 1 = serial)
     int n = (int)std::thread::hardware_concurrency();
     n = n < 1 ? 1 : n > 8 ? 8 : n;
-    if (const char* e = getenv("AV1P_TILE_THREADS")) n = atoi(e) > 0 ? atoi(e) : 1;
+    if (const char* e = getenv("AV1P_TILE_THREADS")) n = std::min(64, std::max(1, atoi(e)));  // as av1p_set_tile_threads
     (*out)->parser.tile_threads = n;
     return AV1R_OK;
 }

@@ -13,6 +13,7 @@
 // and the batch assembly of the oracle harness (oracle/harness/refdump.cpp fillHeader /
 // fillFrameTables), which defines what the backend receives.
 #include <stdarg.h>
+#include <system_error>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -1217,8 +1218,20 @@ int Parser::tile_group(BitReader& br, const uint8_t* data, size_t size)
                 }
             }
         };
+        // a thread that cannot be started (EAGAIN under a thread limit, or no memory for
+        // its stack) is simply not there: the threads already running and this one share
+        // the tiles through `next`, and every started thread is joined before leaving
         std::vector<std::thread> pool;
-        for (int k = 1; k < nThreads; k++) pool.emplace_back(work);
+        pool.reserve(nThreads);
+        for (int k = 1; k < nThreads; k++) {
+            try {
+                pool.emplace_back(work);
+            } catch (const std::system_error&) {
+                break;
+            } catch (const std::bad_alloc&) {
+                break;
+            }
+        }
         work();
         for (auto& th : pool) th.join();
         for (int i = 0; i < n; i++) {  // merged in tile order: the serial path's records

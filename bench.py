@@ -9,14 +9,16 @@ j offset by j*F/S frames so every window of steps holds its share of key frames.
 = one frame of every stream through recon -> deblock -> CDEF -> loop restoration in shared
 launches.
 
-value (headline): the host-inclusive rate.  The frame batches (the host parser's output)
-sit in host memory; inside the timed region every frame is validated, scheduled and packed
+value (headline): the host-inclusive rate.  The frame batches (tools/synth's output, the
+same av1r_frame_batch records the host parser emits, checked against the pinned oracle) sit
+in host memory; inside the timed region every frame is validated, scheduled and packed
 by worker threads (av1r_pack) up to 3 steps ahead, uploaded over PCIe and decoded
 (av1r_decode_packed_batch).  Reported beside it: device_only_fps (batches already
 scheduled and resident in HBM, av1r_prepare), one stream alone, the per-frame streaming
 API from one thread and from one thread per stream.
 
-Multi-GPU (--gpus N, launched by torch.distributed.run): every rank decodes its own
+Multi-GPU (--gpus N: started as N rank processes by this script itself, or by
+torch.distributed.run, which sets WORLD_SIZE): every rank decodes its own
 streams on its own GPU -- streams shard over GPUs with no data-path collective (SURVEY.md
 8e); a gloo barrier brackets the timed region and the MAX elapsed over ranks is used.
 value = N * S * steps / max_elapsed ("weak" scaling).
@@ -122,7 +124,7 @@ class StreamScheduler:
     packed: the host-inclusive pipeline -- worker threads validate, schedule and pack
     (av1r_pack) each stream's next `depth` frames while the GPU decodes, and every round
     uploads and decodes the packed frames (av1r_decode_packed_batch); the frame batches
-    (the host parser's output) sit in host memory.  Otherwise frames come from
+    (tools/synth's av1r_frame_batch records) sit in host memory.  Otherwise frames come from
     per-stream lists of prepared handles (av1r_prepare: scheduled and resident in HBM)."""
 
     def __init__(self, decs, F, streams=None, handles=None, workers=1, depth=3):
@@ -360,7 +362,7 @@ def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, p
             d.synchronize()
 
     # ---- headline: the host-inclusive pipeline (per-frame validation, scheduling, packing
-    # and PCIe upload of the parser's batches inside the timed region, overlapped with the
+    # and PCIe upload of the synthetic batches inside the timed region, overlapped with the
     # GPU).  Setup (untimed): stream j brought to its own GOP phase, a priming pass of
     # ~prime_s, then the warmup steps.  (av1r_pipeline_run: producer threads pack each
     # stream's frames ahead, the calling thread launches one frame of every ready stream per
@@ -506,6 +508,80 @@ def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, tra
             "ivf_end_to_end": ivf}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` from a plain shell: start N rank processes of this script (rank r on
+    GPU r, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them)
+    and wait for them.  The parent never touches the GPU (no HIP call before or after the
+    children start, and no exec: the children are child processes); rank 0 prints the line.
+    If a rank fails the others are stopped, and the worst exit status is returned.  The unit
+    each rank replicates is the reference's single-stream decode loop (tests/Av1Dec.cpp:199-224),
+    over its own disjoint shard of the streams."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0:
+                    rc = rc or c
+                    for q in live:  # a lost rank would leave the others waiting at a barrier
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def dry_run(args, rank, world, dist):
+    """--dry-run: the N-rank plumbing without a GPU (CPU tests): every rank builds its own
+    shard exactly as the real run does (rank_streams, at 64x64 so it takes milliseconds),
+    times it through the same barrier + MAX-over-ranks, and rank 0 prints the line with every
+    rank's stream ids and a digest of its shard's batches (gathered for the report only)."""
+    import hashlib
+    S = max(1, args.streams)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    streams = rank_streams(args.config, rank, S, 2, width=64, height=64)
+    h = hashlib.md5()
+    for fr in streams:
+        for f in fr:
+            h.update(f.to_bytes())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+    mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
+            "stream_ids": rank_stream_ids(rank, S), "digest": h.hexdigest()}
+    shards = [mine]
+    if dist:
+        shards = [None] * world
+        dist.all_gather_object(shards, mine)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "elapsed": elapsed,
+                          "value": aggregate_fps(world, 2 * S, elapsed), "shards": shards,
+                          "config": {"parallelism": f"stream-per-GPU x{world}", "streams_per_gpu": S}}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -523,15 +599,29 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per frame (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-4k", default=os.path.join(ROOT, "profiles", "traffic_4k.json"))
+    ap.add_argument("--dry-run", action="store_true",
+                    help="the N-rank launch and sharding only, no GPU (tests/test_multi.py)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # plain `bench.py --gpus N`: one process per GPU, started here before anything
+        # touches a GPU (torch.distributed.run sets WORLD_SIZE itself and lands below)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")
+    if args.dry_run:
+        dry_run(args, rank, world, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from av1dec_amd import Decoder, native
 

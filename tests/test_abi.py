@@ -223,3 +223,30 @@ def test_pack_walks_fused_and_separate_pack_the_same_bytes():
     out = [subprocess.run([sys.executable, tool, "40"], capture_output=True, text=True, timeout=600,
                           env=dict(os.environ, AV1R_PACK_FUSED=v)).stdout.split() for v in ("1", "0")]
     assert out[0] and out[0] == out[1]
+
+
+def test_validation_palette_window_keyed_on_the_tbs_own_block(native_lib):
+    """A transform block's palette map window is checked against the block its `block` field
+    names (what build_schedule and the device follow), not against the block whose TB range it
+    sits in: a TB in a non-palette block's range that names a palette block elsewhere in the
+    frame must be rejected (it would read outside that block's colour map)."""
+    import numpy as np
+    fr = batchfile.load(golden.batch_path("Halo_426x240_1frames_intrabc"))[0]
+    err = C.create_string_buffer(256)
+    assert native_lib.av1r_check_batch(C.cast(fr.byref(), C.c_void_p), None, err, 256) == 0
+    blk = np.frombuffer(fr.sec["blocks"].tobytes(), abi.BLOCK_DTYPE)
+    tb = np.frombuffer(fr.sec["tbs"].tobytes(), abi.TB_DTYPE).copy()
+    pal = [i for i in range(len(blk)) if blk["palette_size_y"][i] and not blk["flags"][i] & 1]  # AV1R_BLK_INTER
+    assert pal
+    p = pal[0]
+    px, py = int(blk["mi_col"][p]) * 4, int(blk["mi_row"][p]) * 4
+    # a luma TB of a non-palette block far from the palette block
+    far = [i for i in range(len(tb)) if tb["plane"][i] == 0 and not blk["palette_size_y"][tb["block"][i]]
+           and (abs(int(tb["x"][i]) - px) > 64 or abs(int(tb["y"][i]) - py) > 64)]
+    assert far
+    tb["block"][far[0]] = p
+    secs = dict(fr.sec)
+    secs["tbs"] = tb.view(np.uint8).ravel()
+    bad = batchfile.Frame(secs)
+    assert native_lib.av1r_check_batch(C.cast(bad.byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_INVALID
+    assert b"palette map window" in err.value

@@ -124,3 +124,92 @@ def test_two_rank_real_shards():
             o.close()
             assert h.hexdigest() == d, f"rank {rank} stream {i}"
     assert len({d for _, _, ds, _ in res for d in ds}) == 2 * world  # the shards differ
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`bench.py --gpus 2` from a plain shell (no torch.distributed.run): the script starts two
+    rank processes itself, each builds its own disjoint shard with the real run's selection,
+    and rank 0's line says n_gpus 2 with every rank's stream ids (--dry-run: no GPU)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--streams", "8"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "stream-per-GPU x2"
+    sh = sorted(line["shards"], key=lambda s: s["rank"])
+    assert [s["rank"] for s in sh] == [0, 1] and [s["local_rank"] for s in sh] == [0, 1]
+    assert sh[0]["pid"] != sh[1]["pid"]  # two processes
+    assert sh[0]["stream_ids"] == list(range(8)) and sh[1]["stream_ids"] == list(range(8, 16))
+    assert sh[0]["digest"] != sh[1]["digest"]  # different streams
+
+
+def test_bench_gpus_mismatch_is_refused():
+    """A launcher's WORLD_SIZE must agree with --gpus (the line's n_gpus is the world size)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gpu_all_64_configs4_streams_match_oracle():
+    """BASELINE configs[4]: the 64 independent 1080p streams of the 8-GPU job, as the 8 ranks'
+    shards (bench.rank_streams(r, 8) for r = 0..7) decoded one shard after another on this
+    GPU through the bench's native pipeline (1 key + 3 inter frames of every stream, outputs
+    kept); every output frame equals the CPU oracle on the same batches."""
+    import hashlib
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(bench.ROOT, "oracle"))
+    import pyoracle
+    from av1dec_amd import Decoder
+    from av1dec_amd.pipeline import run_native
+
+    def md5s(planes_list):
+        return [b"".join(hashlib.md5(p.tobytes()).digest() for p in planes) for planes in planes_list]
+
+    def oracle(frames):
+        o = pyoracle.Oracle(keep_stages=False)
+        out = []
+        try:
+            for f in frames:
+                o.decode_frame(f)
+                while o.output_pending():
+                    out.append(o.get_output())
+        finally:
+            o.close()
+        return md5s(out)
+
+    S, F, world = 8, 4, 8
+    seen = set()
+    with ThreadPoolExecutor(16) as ex:
+        for rank in range(world):
+            ids = bench.rank_stream_ids(rank, S)
+            assert not seen & set(ids)
+            seen |= set(ids)
+            streams = bench.rank_streams("1080p", rank, S, F)
+            ref = [ex.submit(oracle, s) for s in streams]
+            decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+            try:
+                st = run_native(decs, "cycle", streams, [0] * S, max_frames=F)
+                assert st["frames"] == S * F
+                got = []
+                for d in decs:
+                    outs = []
+                    while d.output_pending():
+                        outs.append(d.get_output())
+                    got.append(md5s(outs))
+            finally:
+                for d in decs:
+                    d.close()
+            for j, r in enumerate(ref):
+                assert got[j] == r.result(), f"stream {ids[j]} (rank {rank} shard)"
+    assert seen == set(range(64))
