@@ -5,8 +5,9 @@
 // per frame, walks the tile trees (decodeFrame, 128-156) or shows a stored frame
 // (showExistingFrame, 158-169).  Here the parse is the host parser (av1p_decode_tu) and each
 // parsed frame goes to the MI355X backend as one batch (av1r_decode_frame) -- asynchronous:
-// the host parses frame t+1 while the GPU reconstructs frame t.  getOutput copies the oldest
-// shown frame back (av1r_get_output, which waits for that frame only).
+// the host parses frame t+1 while the GPU reconstructs frame t.  Every shown frame's read-back
+// starts as soon as it is launched (av1r_set_output_prefetch), and getOutput waits for the
+// oldest one's copy only (av1r_get_output).
 #include <stdlib.h>
 #include <string.h>
 
@@ -45,6 +46,9 @@ int av1d_create(int device, av1d_ctx** out)
         return rc;
     }
     av1r_set_keep_stages(c->recon, 0);  // no per-stage snapshots: output only
+    // every shown frame's read-back starts as soon as it is decoded, overlapping the parse
+    // and decode of the next units; getOutput then waits for that copy alone
+    av1r_set_output_prefetch(c->recon, 1);
     *out = c;
     return AV1R_OK;
 }

@@ -115,6 +115,20 @@ struct av1r_packed {
     bool copyPending = false;
 };
 
+// One asynchronous read-back of a shown frame (av1r_get_output_async): the frame stays
+// referenced (out of the pool) until the ticket is waited for.  The copies are issued on the
+// context's output stream only once the frame's kernels have completed (`ready` observed
+// by av1r_output_query / _wait), so the output stream never carries a cross-stream wait.
+struct av1r_output_ticket {
+    av1r_ctx* c = nullptr;
+    FrameBuf* f = nullptr;
+    uint8_t* dst[3] = {};
+    int ds[3] = {};
+    hipEvent_t ready = nullptr, done = nullptr;
+    int state = 0;  // 0 the frame's kernels may still run, 1 copies issued, 2 landed
+    bool live = false;
+};
+
 struct av1r_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -139,6 +153,22 @@ struct av1r_ctx {
     int metaIdx = 0;
     hipStream_t copyStream = nullptr;
     hipStream_t aux = nullptr;              // k_inter_m / k_inter_s beside k_inter (AV1R_INTER_SPLIT)
+    // asynchronous frame delivery (av1r_get_output_async): the read-back copies' own stream
+    // (created at the first such call) and every ticket ever allocated (free ones reused)
+    hipStream_t outStream = nullptr;
+    std::vector<av1r_output_ticket*> tickets;
+    // av1r_set_output_prefetch: every shown frame's read-back starts at once into a pinned
+    // staging buffer of the context (frames move from outq to `staged`, the older ones);
+    // av1r_get_output then waits for that copy only and copies the rows out on the host
+    struct Staged {
+        av1r_output_ticket* t;
+        uint8_t* buf;
+        size_t cap;
+        int w, h;
+    };
+    bool prefetch = false;
+    std::deque<Staged> staged;
+    std::vector<std::pair<uint8_t*, size_t>> stageFree;
     hipEvent_t auxGo = nullptr, auxDone = nullptr;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
     // this context's latest work was launched on joinLead's stream (a batch it was a member
@@ -293,6 +323,8 @@ static std::vector<av1r_ctx*> g_ctxs;
 
 // Lazy cross-stream ordering of batch members (av1r_decode_prepared_batch): called before
 // anything enqueues on, or waits for, the context's own stream.
+static int stage_outputs(av1r_ctx* c);
+
 static void ctx_join(av1r_ctx* c)
 {
     if (!c || !c->joinLead) return;
@@ -2047,6 +2079,18 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
+    if (c->outStream) (void)hipStreamSynchronize(c->outStream);
+    for (av1r_output_ticket* t : c->tickets) {  // tickets never waited for die with the context
+        if (t->ready) (void)hipEventDestroy(t->ready);
+        if (t->done) (void)hipEventDestroy(t->done);
+        delete t;
+    }
+    c->tickets.clear();
+    for (auto& S : c->staged) c->stageFree.push_back({S.buf, S.cap});
+    for (auto& b : c->stageFree) (void)hipHostFree(b.first);
+    c->staged.clear();
+    c->stageFree.clear();
+    if (c->outStream) (void)hipStreamDestroy(c->outStream);
     {  // members of its batches: their pending join on its (now drained) stream is satisfied
         std::lock_guard<std::mutex> lock(g_ctxMu);
         for (av1r_ctx* m : g_ctxs)
@@ -2113,7 +2157,8 @@ int av1r_decode_frame(av1r_ctx* c, const av1r_frame_batch* b)
     if (b->hdr->version != AV1R_VERSION) return fail(c, AV1R_E_INVALID, "batch version %u", b->hdr->version);
     (void)hipSetDevice(c->device);
     if (b->hdr->show_existing_frame) return av1r_show_existing(c, b->hdr->frame_to_show, b->hdr->refresh_frame_flags);
-    return run_frame(c, b);
+    const int rc = run_frame(c, b);
+    return rc ? rc : stage_outputs(c);
 }
 
 int av1r_frame_begin(av1r_ctx* c, const av1r_frame_batch* f)
@@ -2582,10 +2627,10 @@ int av1r_show_existing(av1r_ctx* c, int slot, int refresh)
             c->slots[i] = f;
         }
     frame_unref(c, f);
-    return AV1R_OK;
+    return stage_outputs(c);
 }
 
-int av1r_output_pending(av1r_ctx* c) { return c ? (int)c->outq.size() : 0; }
+int av1r_output_pending(av1r_ctx* c) { return c ? (int)(c->outq.size() + c->staged.size()) : 0; }
 
 static int copy_plane_d2h(av1r_ctx* c, const DevPlane& p, uint8_t* dst, int ds)
 {
@@ -2593,15 +2638,18 @@ static int copy_plane_d2h(av1r_ctx* c, const DevPlane& p, uint8_t* dst, int ds)
     return AV1R_OK;
 }
 
+static int get_staged(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height);
+
 int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height)
 {
     if (!c) return AV1R_E_INVALID;
+    if (!c->staged.empty()) return get_staged(c, y, ys, u, us, v, vs, width, height);
     if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
-    ctx_join(c);
     FrameBuf* f = c->outq.front();
     if (width) *width = f->d.width;
     if (height) *height = f->d.height;
-    if (!y) return AV1R_OK;
+    if (!y) return AV1R_OK;  // the size only: host state, no join of the context's stream
+    ctx_join(c);
     (void)hipSetDevice(c->device);
     int rc;
     if ((rc = copy_plane_d2h(c, f->d.pl[0], y, ys)) || (rc = copy_plane_d2h(c, f->d.pl[1], u, us)) || (rc = copy_plane_d2h(c, f->d.pl[2], v, vs)))
@@ -2613,6 +2661,171 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
     std::lock_guard<std::mutex> lock(g_recMu);
     if (frame_failed(c, f->seq)) return fail(c, AV1R_E_DEVICE, "frame %llu: %s", (unsigned long long)f->seq, c->err.c_str());
     return AV1R_OK;
+}
+
+int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
+                          av1r_output_ticket** out)
+{
+    if (!c || !out || !y || !u || !v) return AV1R_E_INVALID;
+    *out = nullptr;
+    if (!c->staged.empty()) return fail(c, AV1R_E_INVALID, "frames already staged by av1r_set_output_prefetch: use av1r_get_output");
+    if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
+    (void)hipSetDevice(c->device);
+    if (!c->outStream) HIPCHK(hipStreamCreateWithFlags(&c->outStream, hipStreamNonBlocking));
+    av1r_output_ticket* t = nullptr;
+    for (av1r_output_ticket* q : c->tickets)
+        if (!q->live) {
+            t = q;
+            break;
+        }
+    if (!t) {
+        t = new (std::nothrow) av1r_output_ticket;
+        if (!t) return AV1R_E_NOMEM;
+        if (hipEventCreateWithFlags(&t->ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&t->done, hipEventDisableTiming) != hipSuccess) {
+            if (t->ready) (void)hipEventDestroy(t->ready);
+            delete t;
+            return fail(c, AV1R_E_DEVICE, "hipEventCreate");
+        }
+        c->tickets.push_back(t);
+    }
+    FrameBuf* f = c->outq.front();
+    // the frame's last writer: this context's own stream, or the stream of the batch it was
+    // last launched in (ctx_join is not needed: nothing is enqueued on the context here)
+    HIPCHK(hipEventRecord(t->ready, c->joinLead ? c->joinLead->stream : c->stream));
+    c->outq.pop_front();  // the queue's reference passes to the ticket
+    t->c = c;
+    t->f = f;
+    t->dst[0] = y, t->dst[1] = u, t->dst[2] = v;
+    t->ds[0] = ys, t->ds[1] = us, t->ds[2] = vs;
+    t->state = 0;
+    t->live = true;
+    if (width) *width = f->d.width;
+    if (height) *height = f->d.height;
+    *out = t;
+    return AV1R_OK;
+}
+
+static int ticket_issue(av1r_output_ticket* t)
+{
+    av1r_ctx* c = t->c;
+    for (int p = 0; p < 3; p++) {
+        const DevPlane& P = t->f->d.pl[p];
+        HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], P.p, P.stride, P.w, P.h, hipMemcpyDeviceToHost, c->outStream));
+    }
+    HIPCHK(hipEventRecord(t->done, c->outStream));
+    t->state = 1;
+    return AV1R_OK;
+}
+
+int av1r_output_query(av1r_output_ticket* t)
+{
+    if (!t || !t->live) return AV1R_E_INVALID;
+    av1r_ctx* c = t->c;
+    (void)hipSetDevice(c->device);
+    if (t->state == 0) {
+        const hipError_t q = hipEventQuery(t->ready);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output: %s", hipGetErrorString(q));
+        const int rc = ticket_issue(t);
+        if (rc) return rc;
+    }
+    if (t->state == 1) {
+        const hipError_t q = hipEventQuery(t->done);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output copy: %s", hipGetErrorString(q));
+        t->state = 2;
+    }
+    return 1;
+}
+
+int av1r_output_wait(av1r_output_ticket* t)
+{
+    if (!t || !t->live) return AV1R_E_INVALID;
+    av1r_ctx* c = t->c;
+    (void)hipSetDevice(c->device);
+    int rc = AV1R_OK;
+    if (t->state == 0) {
+        if (hipEventSynchronize(t->ready) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output: frame wait failed");
+        if (!rc) rc = ticket_issue(t);
+    }
+    if (!rc && t->state == 1) {
+        if (hipEventSynchronize(t->done) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output copy wait failed");
+        t->state = 2;
+    }
+    if (t->state != 2) {
+        // a copy may still be in flight: keep the frame out of the pool until the stream is idle
+        (void)hipStreamSynchronize(c->outStream);
+    }
+    FrameBuf* f = t->f;
+    frame_unref(c, f);
+    t->f = nullptr;
+    t->live = false;
+    if (rc) return rc;
+    harvest(false);
+    std::lock_guard<std::mutex> lock(g_recMu);
+    if (frame_failed(c, f->seq)) return fail(c, AV1R_E_DEVICE, "frame %llu: %s", (unsigned long long)f->seq, c->err.c_str());
+    return AV1R_OK;
+}
+
+// av1r_set_output_prefetch: start the read-back of every queued frame into staging buffers
+static int stage_outputs(av1r_ctx* c)
+{
+    while (c->prefetch && !c->outq.empty()) {
+        FrameBuf* f = c->outq.front();
+        const int w = f->d.width, h = f->d.height, cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+        const size_t need = (size_t)w * h + 2 * (size_t)cw * ch;
+        av1r_ctx::Staged S{nullptr, nullptr, 0, w, h};
+        for (size_t i = 0; i < c->stageFree.size(); i++)
+            if (c->stageFree[i].second >= need) {
+                S.buf = c->stageFree[i].first;
+                S.cap = c->stageFree[i].second;
+                c->stageFree.erase(c->stageFree.begin() + i);
+                break;
+            }
+        if (!S.buf) {
+            (void)hipSetDevice(c->device);
+            if (hipHostMalloc((void**)&S.buf, need, 0) != hipSuccess) return fail(c, AV1R_E_NOMEM, "staging buffer");
+            S.cap = need;
+        }
+        uint8_t* u = S.buf + (size_t)w * h;
+        int rc = av1r_get_output_async(c, S.buf, w, u, cw, u + (size_t)cw * ch, cw, nullptr, nullptr, &S.t);
+        if (!rc && hipStreamWaitEvent(c->outStream, S.t->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
+        if (!rc) rc = ticket_issue(S.t);
+        if (rc) {
+            if (S.t) (void)av1r_output_wait(S.t);
+            c->stageFree.push_back({S.buf, S.cap});
+            return rc;
+        }
+        c->staged.push_back(S);
+    }
+    return AV1R_OK;
+}
+
+static int get_staged(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height)
+{
+    av1r_ctx::Staged S = c->staged.front();
+    if (width) *width = S.w;
+    if (height) *height = S.h;
+    if (!y) return AV1R_OK;
+    c->staged.pop_front();
+    const int rc = av1r_output_wait(S.t);
+    const int cw = (S.w + 1) >> 1, ch = (S.h + 1) >> 1;
+    const uint8_t* src = S.buf;
+    for (int r = 0; r < S.h; r++) memcpy(y + (size_t)r * ys, src + (size_t)r * S.w, S.w);
+    src += (size_t)S.w * S.h;
+    for (int r = 0; r < ch; r++) memcpy(u + (size_t)r * us, src + (size_t)r * cw, cw);
+    src += (size_t)cw * ch;
+    for (int r = 0; r < ch; r++) memcpy(v + (size_t)r * vs, src + (size_t)r * cw, cw);
+    c->stageFree.push_back({S.buf, S.cap});
+    return rc;
+}
+
+int av1r_set_output_prefetch(av1r_ctx* c, int on)
+{
+    if (!c) return AV1R_E_INVALID;
+    c->prefetch = on != 0;
+    return stage_outputs(c);
 }
 
 int av1r_read_stage(av1r_ctx* c, int stage, int plane, uint8_t* dst, int ds)
@@ -2807,3 +3020,90 @@ size_t av1r_sizeof(int which)
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// av1r_ring_sink: pinned host buffers for a pipeline's frame delivery (include/av1r.h)
+// ------------------------------------------------------------------------------------
+namespace {
+struct RingSink {
+    int n = 0, w = 0, h = 0, slots = 0;
+    size_t frameBytes = 0;
+    uint8_t* host = nullptr;  // n * slots frames
+    std::vector<int64_t> acquired, delivered;
+    std::vector<int> fw, fh;  // per (stream, slot): the frame's size
+};
+
+int ring_acquire(void* user, int s, int width, int height, uint8_t** planes, int* strides)
+{
+    RingSink* R = (RingSink*)user;
+    if (!R || s < 0 || s >= R->n || width <= 0 || height <= 0 || width > R->w || height > R->h) return AV1R_E_INVALID;
+    if (R->acquired[s] - R->delivered[s] >= R->slots) return AV1R_E_INVALID;  // every buffer is in flight
+    const int k = (int)(R->acquired[s]++ % R->slots);
+    uint8_t* f = R->host + ((size_t)s * R->slots + k) * R->frameBytes;
+    const int cw = (width + 1) >> 1, ch = (height + 1) >> 1;
+    planes[0] = f;
+    planes[1] = f + (size_t)width * height;
+    planes[2] = planes[1] + (size_t)cw * ch;
+    strides[0] = width;
+    strides[1] = strides[2] = cw;
+    R->fw[(size_t)s * R->slots + k] = width;
+    R->fh[(size_t)s * R->slots + k] = height;
+    return AV1R_OK;
+}
+
+void ring_deliver(void* user, int s, int status)
+{
+    RingSink* R = (RingSink*)user;
+    if (R && s >= 0 && s < R->n && status == AV1R_OK) R->delivered[s]++;
+}
+}  // namespace
+
+int av1r_ring_sink_create(int n_streams, int width, int height, int slots, av1r_output_sink* out)
+{
+    if (!out || n_streams <= 0 || n_streams > 1024 || width <= 0 || height <= 0 || width > 16384 || height > 16384 ||
+        slots < AV1R_SINK_INFLIGHT || slots > 1024)
+        return AV1R_E_INVALID;
+    RingSink* R = new (std::nothrow) RingSink;
+    if (!R) return AV1R_E_NOMEM;
+    R->n = n_streams, R->w = width, R->h = height, R->slots = slots;
+    R->frameBytes = align256((size_t)width * height + 2 * (size_t)((width + 1) >> 1) * ((height + 1) >> 1));
+    R->acquired.assign(n_streams, 0);
+    R->delivered.assign(n_streams, 0);
+    R->fw.assign((size_t)n_streams * slots, 0);
+    R->fh.assign((size_t)n_streams * slots, 0);
+    if (hipHostMalloc((void**)&R->host, R->frameBytes * n_streams * slots, 0) != hipSuccess) {
+        delete R;
+        return AV1R_E_NOMEM;
+    }
+    out->acquire = ring_acquire;
+    out->deliver = ring_deliver;
+    out->user = R;
+    return AV1R_OK;
+}
+
+void av1r_ring_sink_destroy(av1r_output_sink* sink)
+{
+    if (!sink || sink->acquire != ring_acquire || !sink->user) return;
+    RingSink* R = (RingSink*)sink->user;
+    (void)hipHostFree(R->host);
+    delete R;
+    sink->user = nullptr;
+}
+
+int64_t av1r_ring_sink_delivered(const av1r_output_sink* sink, int stream)
+{
+    if (!sink || sink->acquire != ring_acquire || !sink->user) return -1;
+    const RingSink* R = (const RingSink*)sink->user;
+    return stream >= 0 && stream < R->n ? R->delivered[stream] : -1;
+}
+
+const uint8_t* av1r_ring_sink_frame(const av1r_output_sink* sink, int stream, int64_t k, int* width, int* height)
+{
+    if (!sink || sink->acquire != ring_acquire || !sink->user) return nullptr;
+    const RingSink* R = (const RingSink*)sink->user;
+    if (stream < 0 || stream >= R->n || k < 0 || k >= R->delivered[stream] || k < R->acquired[stream] - R->slots) return nullptr;
+    const size_t i = (size_t)stream * R->slots + (size_t)(k % R->slots);
+    if (width) *width = R->fw[i];
+    if (height) *height = R->fh[i];
+    return R->host + i * R->frameBytes;
+}

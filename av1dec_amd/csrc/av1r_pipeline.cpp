@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -239,7 +240,10 @@ struct av1r_pipeline {
     std::vector<int64_t> launched;  // entries (frames, show-existing units) launched per stream
     std::vector<bool> ended;        // the stream's end (or error) entry was consumed
     int G = 1, g = 0;
-    explicit av1r_pipeline(int n) : R(n), launched(n, 0), ended(n, false) {}
+    // frame delivery (av1r_pipeline_set_output): per stream the read-backs in flight, in order
+    av1r_output_sink sink{};
+    std::vector<std::deque<av1r_output_ticket*>> tick;
+    explicit av1r_pipeline(int n) : R(n), launched(n, 0), ended(n, false), tick(n) {}
 };
 
 namespace {
@@ -268,6 +272,58 @@ int pipe_open(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64
     for (int w = 0; w < W; w++) P->th.emplace_back(worker, &R);
     *out = P;
     return AV1R_OK;
+}
+
+// Frame delivery: hand every landed read-back to the sink (in order per stream), then start
+// the read-back of every frame the contexts have queued since (finish: wait for all of them).
+// Runs on the launching thread between launches, so the copies overlap the next batches.
+int pipe_outputs(av1r_pipeline* P, bool finish, std::string& err)
+{
+    if (!P->sink.acquire) return AV1R_OK;
+    int rc = AV1R_OK;
+    const int n = (int)P->ctxs.size();
+    for (int s = 0; s < n; s++) {
+        av1r_ctx* c = P->ctxs[s];
+        auto& T = P->tick[s];
+        auto deliverFront = [&](bool block) {
+            av1r_output_ticket* t = T.front();
+            if (!block) {
+                const int q = av1r_output_query(t);
+                if (q == 0) return false;
+            }
+            const int st = av1r_output_wait(t);
+            T.pop_front();
+            P->sink.deliver(P->sink.user, s, st);
+            if (st && rc == AV1R_OK) {
+                rc = st;
+                err = av1r_last_error(c);
+            }
+            return true;
+        };
+        while (!T.empty() && deliverFront(false)) {
+        }
+        while (rc == AV1R_OK && av1r_output_pending(c) > 0) {
+            if ((int)T.size() >= AV1R_SINK_INFLIGHT) deliverFront(true);
+            int w = 0, h = 0;
+            uint8_t* pl[3] = {};
+            int st[3] = {};
+            int r = av1r_get_output(c, nullptr, 0, nullptr, 0, nullptr, 0, &w, &h);  // size only
+            if (!r && P->sink.acquire(P->sink.user, s, w, h, pl, st)) {
+                r = AV1R_E_INVALID;
+                err = "stream " + std::to_string(s) + ": the output sink gave no buffer";
+            }
+            av1r_output_ticket* t = nullptr;
+            if (!r && (r = av1r_get_output_async(c, pl[0], st[0], pl[1], st[1], pl[2], st[2], &w, &h, &t)))
+                err = av1r_last_error(c);
+            if (r) {
+                rc = r;
+                break;
+            }
+            T.push_back(t);
+        }
+        while (finish && !T.empty()) deliverFront(true);
+    }
+    return rc;
 }
 
 // Launch `frames` more entries of every stream (0: to the end of every stream), then
@@ -375,6 +431,7 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
             }
             nframes += bc.size();
             batches++;
+            if (rc == AV1R_OK) rc = pipe_outputs(P, false, err);
         } else if (live > 0 && rc == AV1R_OK && P->g == 0) {
             // nothing ready in any group: a worker's push wakes us; a key frame running alone does not,
             // hence the short bound
@@ -382,7 +439,13 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
             std::unique_lock<std::mutex> l(R.m);
             R.ready.wait_for(l, std::chrono::microseconds(50));
             wait_s += secs(Clock::now() - w0);
+            l.unlock();
+            if (rc == AV1R_OK) rc = pipe_outputs(P, false, err);
         }
+    }
+    {  // every frame of the step delivered before it returns
+        const int r = pipe_outputs(P, true, err);
+        if (r && rc == AV1R_OK) rc = r;
     }
     for (int s = 0; s < n; s++) {
         const int r = av1r_synchronize(ctxs[s]);
@@ -416,6 +479,8 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
 void pipe_close(av1r_pipeline* P)
 {
     Run& R = P->R;
+    for (auto& T : P->tick)  // read-backs of a failed step: released, not delivered
+        for (av1r_output_ticket* t : T) (void)av1r_output_wait(t);
     {  // stop and drain the workers
         std::lock_guard<std::mutex> l(R.m);
         R.stop.store(true);
@@ -468,6 +533,15 @@ int av1r_pipeline_step(av1r_pipeline* p, int64_t frames, av1r_pipeline_stats* st
     if (!p) return AV1R_E_INVALID;
     if (!cycle_ok(p->R.src, (int)p->ctxs.size(), frames)) return AV1R_E_INVALID;
     return pipe_step(p, frames, stats);
+}
+
+int av1r_pipeline_set_output(av1r_pipeline* p, const av1r_output_sink* sink)
+{
+    if (!p || (sink && (!sink->acquire || !sink->deliver))) return AV1R_E_INVALID;
+    for (auto& T : p->tick)
+        if (!T.empty()) return AV1R_E_INVALID;  // (never between steps: a step delivers everything)
+    p->sink = sink ? *sink : av1r_output_sink{};
+    return AV1R_OK;
 }
 
 int av1r_pipeline_launched(const av1r_pipeline* p, int64_t* counts, int n)

@@ -128,6 +128,25 @@ class Decoder:
                                            W >> 1, None, None), "av1r_get_output")
         return y, u, v
 
+    def get_output_async(self, y, u, v):
+        """Start the read-back of the oldest queued frame into numpy planes y, u, v (kept alive
+        by the caller until waited for; av1r_get_output_async).  Returns an OutputTicket, or None
+        when no frame is queued."""
+        t = C.c_void_p()
+        rc = self.l.av1r_get_output_async(self.c, y.ctypes.data, y.strides[0], u.ctypes.data, u.strides[0],
+                                          v.ctypes.data, v.strides[0], None, None, C.byref(t))
+        if rc == abi.AV1R_E_NO_OUTPUT:
+            return None
+        self._check(rc, "av1r_get_output_async")
+        return OutputTicket(self, t, (y, u, v))
+
+    def output_size(self):
+        """(width, height) of the oldest queued frame, or None."""
+        w, h = C.c_int(), C.c_int()
+        if self.l.av1r_get_output(self.c, None, 0, None, 0, None, 0, C.byref(w), C.byref(h)) != 0:
+            return None
+        return w.value, h.value
+
     def read_stage(self, stage):
         W, H = self.last.frame_width, self.last.frame_height
         out = []
@@ -169,3 +188,24 @@ class Decoder:
         lv, ub = C.c_int(), C.c_uint64()
         self.l.av1r_last_frame_stats(self.c, C.byref(lv), C.byref(ub))
         return lv.value, ub.value
+
+
+class OutputTicket:
+    """An asynchronous frame read-back (av1r_output_query / av1r_output_wait)."""
+
+    def __init__(self, dec, t, planes):
+        self.dec, self.t, self.planes = dec, t, planes
+
+    def ready(self):
+        rc = self.dec.l.av1r_output_query(self.t)
+        if rc < 0:
+            self.dec._check(rc, "av1r_output_query")
+        return rc == 1
+
+    def wait(self):
+        """Block until the planes have landed; returns them (the ticket is released)."""
+        t, self.t = self.t, None
+        if t is None:
+            raise BackendError("ticket already waited for")
+        self.dec._check(self.dec.l.av1r_output_wait(t), "av1r_output_wait")
+        return self.planes

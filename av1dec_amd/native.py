@@ -217,12 +217,35 @@ def lib():
     l.av1r_ivf_source_create.argtypes = [C.POINTER(vp), C.POINTER(C.c_size_t), i, C.POINTER(StreamSource)]
     l.av1r_ivf_source_destroy.argtypes = [C.POINTER(StreamSource)]
     l.av1r_ivf_source_destroy.restype = None
+    l.av1r_get_output_async.argtypes = [vp, u8p, i, u8p, i, u8p, i, C.POINTER(i), C.POINTER(i), C.POINTER(vp)]
+    l.av1r_output_query.argtypes = [vp]
+    l.av1r_output_wait.argtypes = [vp]
+    l.av1r_set_output_prefetch.argtypes = [vp, i]
+    l.av1r_pipeline_set_output.argtypes = [vp, C.POINTER(OutputSink)]
+    l.av1r_ring_sink_create.argtypes = [i, i, i, i, C.POINTER(OutputSink)]
+    l.av1r_ring_sink_destroy.argtypes = [C.POINTER(OutputSink)]
+    l.av1r_ring_sink_destroy.restype = None
+    l.av1r_ring_sink_delivered.argtypes = [C.POINTER(OutputSink), i]
+    l.av1r_ring_sink_delivered.restype = C.c_int64
+    l.av1r_ring_sink_frame.argtypes = [C.POINTER(OutputSink), i, C.c_int64, C.POINTER(i), C.POINTER(i)]
+    l.av1r_ring_sink_frame.restype = vp
     _lib = l
     return l
 
 
 class StreamSource(C.Structure):  # av1r_stream_source
     _fields_ = [("next", C.c_void_p), ("user", C.c_void_p), ("stable", C.c_int)]
+
+
+SINK_ACQUIRE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int))
+SINK_DELIVER = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int)
+
+
+class OutputSink(C.Structure):  # av1r_output_sink
+    _fields_ = [("acquire", C.c_void_p), ("deliver", C.c_void_p), ("user", C.c_void_p)]
+
+
+SINK_INFLIGHT = 8  # AV1R_SINK_INFLIGHT
 
 
 class PipelineStats(C.Structure):  # av1r_pipeline_stats
@@ -248,6 +271,8 @@ EXPORTS = [
     "av1r_pipeline_run", "av1r_pipeline_open", "av1r_pipeline_step", "av1r_pipeline_launched",
     "av1r_pipeline_close", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
     "av1r_set_strip_levels", "av1r_set_filter_fusion", "av1r_set_fast_intra", "av1r_packed_data",
+    "av1r_get_output_async", "av1r_output_query", "av1r_output_wait", "av1r_set_output_prefetch", "av1r_pipeline_set_output",
+    "av1r_ring_sink_create", "av1r_ring_sink_destroy", "av1r_ring_sink_delivered", "av1r_ring_sink_frame",
 ]
 
 

@@ -177,6 +177,13 @@ class NativePipeline:
             raise BackendError(f"av1r_pipeline_step failed ({rc}): {self.decs[0].l.av1r_last_error(self.decs[0].c).decode()}")
         return {k: getattr(st, k) for k, _ in native.PipelineStats._fields_}
 
+    def set_output(self, sink):
+        """Frame delivery (av1r_pipeline_set_output): a RingSink / ArraySink, or None."""
+        self.sink = sink
+        rc = self.l.av1r_pipeline_set_output(self.p, C.byref(sink.s) if sink is not None else None)
+        if rc:
+            raise BackendError(f"av1r_pipeline_set_output failed ({rc})")
+
     def positions(self):
         c = (C.c_int64 * self.n)()
         if self.l.av1r_pipeline_launched(self.p, c, self.n):
@@ -238,3 +245,55 @@ def run_native(decoders, source="cycle", streams=None, positions=None, max_frame
         # every producer fetched exactly the frames that were decoded (max_frames each)
         positions[:] = list(pos)
     return {k: getattr(st, k) for k, _ in native.PipelineStats._fields_}
+
+
+class RingSink:
+    """The library's pinned-buffer output sink (av1r_ring_sink_create): `slots` frames of at
+    most width x height per stream, reused in rotation; counts the frames delivered."""
+
+    def __init__(self, n_streams, width, height, slots=native.SINK_INFLIGHT * 2):
+        self.l = native.lib()
+        self.s = native.OutputSink()
+        rc = self.l.av1r_ring_sink_create(n_streams, width, height, slots, C.byref(self.s))
+        if rc:
+            raise BackendError(f"av1r_ring_sink_create failed ({rc})")
+        self.n = n_streams
+
+    def delivered(self, stream=None):
+        if stream is None:
+            return sum(self.delivered(j) for j in range(self.n))
+        return int(self.l.av1r_ring_sink_delivered(C.byref(self.s), stream))
+
+    def close(self):
+        if self.s.user:
+            self.l.av1r_ring_sink_destroy(C.byref(self.s))
+
+
+class ArraySink:
+    """An output sink in Python (tests): every delivered frame kept as numpy I420 planes, per
+    stream in delivery order, with its status."""
+
+    def __init__(self, n_streams):
+        import numpy as np
+        self.np = np
+        self.frames = [[] for _ in range(n_streams)]
+        self.status = [[] for _ in range(n_streams)]
+        self.inflight = [[] for _ in range(n_streams)]
+        self._acq = native.SINK_ACQUIRE(self._acquire)
+        self._del = native.SINK_DELIVER(self._deliver)
+        self.s = native.OutputSink(C.cast(self._acq, C.c_void_p).value, C.cast(self._del, C.c_void_p).value, None)
+
+    def _acquire(self, user, stream, w, h, planes, strides):
+        np = self.np
+        y = np.empty((h, w), np.uint8)
+        u = np.empty(((h + 1) >> 1, (w + 1) >> 1), np.uint8)
+        v = np.empty(((h + 1) >> 1, (w + 1) >> 1), np.uint8)
+        self.inflight[stream].append((y, u, v))
+        for k, a in enumerate((y, u, v)):
+            planes[k] = a.ctypes.data
+            strides[k] = a.strides[0]
+        return 0
+
+    def _deliver(self, user, stream, status):
+        self.frames[stream].append(self.inflight[stream].pop(0))
+        self.status[stream].append(status)

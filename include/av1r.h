@@ -25,6 +25,8 @@
  *   av1r_output_pending/av1r_get_output -- Decoder::getOutput (Av1Decoder.cpp:203-211) +
  *                                        the I420 row copy of DecodeOutput::output
  *                                        (tests/DecodeOutput.cpp:48-69)
+ *   av1r_get_output_async / av1r_output_query / av1r_output_wait
+ *                                     -- the same read-back overlapped with later frames' decoding
  *   av1r_read_stage                   -- debug read-back of one pipeline stage
  *                                        (the reference's DUMP hooks, Av1Decoder.cpp:142-152)
  */
@@ -276,6 +278,27 @@ int av1r_output_pending(av1r_ctx* ctx);
 int av1r_get_output(av1r_ctx* ctx, uint8_t* y, int y_stride, uint8_t* u, int u_stride,
                     uint8_t* v, int v_stride, int* width, int* height);
 
+/* Asynchronous form (the same Decoder::getOutput, Av1Decoder.cpp:203-211, without the
+ * wait): pops the oldest queued frame and returns at once with a ticket.  The frame's
+ * visible I420 planes are copied into the caller's buffers on the context's own read-back
+ * stream as soon as its kernels have completed, so the copy overlaps the decoding of later
+ * frames; the buffers must stay valid until the ticket is waited for, and should be pinned
+ * (hipHostMalloc) for the copy to be a DMA.  av1r_output_query advances a ticket without
+ * blocking (1: the bytes have landed, 0: not yet; it issues the copy once the frame is
+ * done); av1r_output_wait blocks until they have landed, releases the ticket (and the
+ * frame), and returns AV1R_E_DEVICE for a frame a device error touched.  A ticket belongs
+ * to the context's driving thread; av1r_destroy releases tickets never waited for. */
+typedef struct av1r_output_ticket av1r_output_ticket;
+int av1r_get_output_async(av1r_ctx* ctx, uint8_t* y, int y_stride, uint8_t* u, int u_stride,
+                          uint8_t* v, int v_stride, int* width, int* height, av1r_output_ticket** ticket);
+int av1r_output_query(av1r_output_ticket* ticket);
+int av1r_output_wait(av1r_output_ticket* ticket);
+/* 1: from now on every shown frame's read-back starts as soon as it is queued (into pinned
+ * staging memory of the context, on its read-back stream), so av1r_get_output waits for
+ * that copy alone -- the blocking getOutput of the Yami / YamiAv1 facades overlapping the
+ * decoding of the next frames.  (av1r_get_output_async is refused while frames are staged.) */
+int av1r_set_output_prefetch(av1r_ctx* ctx, int on);
+
 /* Copy the visible region of plane `plane` of stage `stage` of the last decoded frame. */
 int av1r_read_stage(av1r_ctx* ctx, int stage, int plane, uint8_t* dst, int dst_stride);
 
@@ -377,6 +400,32 @@ int av1r_pipeline_open(av1r_ctx* const* ctxs, int n, const av1r_stream_source* s
 int av1r_pipeline_step(av1r_pipeline* p, int64_t frames, av1r_pipeline_stats* stats);
 int av1r_pipeline_launched(const av1r_pipeline* p, int64_t* counts, int n);
 void av1r_pipeline_close(av1r_pipeline* p);
+/* Frame delivery from a pipeline (the reference application's getOutput after every
+ * decode call, tests/Av1Dec.cpp:216-220): with a sink set, the launching thread starts the
+ * read-back of every shown frame as soon as it is launched (av1r_get_output_async into the
+ * buffer `acquire` gives: planes[3] / strides[3] for a width x height I420 frame of
+ * `stream`; nonzero = error, the step fails), keeps decoding, and calls `deliver` for each
+ * frame once its bytes have landed, in order per stream (status AV1R_OK or AV1R_E_DEVICE).
+ * At most AV1R_SINK_INFLIGHT read-backs per stream are outstanding, so a sink needs that
+ * many buffers per stream in rotation; every frame of a step is delivered before the step
+ * returns.  NULL: shown frames stay queued in their contexts (av1r_get_output). */
+#define AV1R_SINK_INFLIGHT 8
+typedef struct av1r_output_sink {
+    int (*acquire)(void* user, int stream, int width, int height, uint8_t** planes, int* strides);
+    void (*deliver)(void* user, int stream, int status);
+    void* user;
+} av1r_output_sink;
+int av1r_pipeline_set_output(av1r_pipeline* p, const av1r_output_sink* sink);
+/* A sink of pinned host buffers (hipHostMalloc): `slots` (>= AV1R_SINK_INFLIGHT) frames of
+ * at most width x height per stream, reused in rotation; it counts what it was delivered
+ * (av1r_ring_sink_delivered: frames of `stream`, -1 for a bad argument) and a frame's
+ * buffer is readable from its delivery until `slots` later frames of that stream have
+ * been acquired (av1r_ring_sink_frame: the I420 planes of the stream's k-th delivered
+ * frame, NULL once overwritten). */
+int av1r_ring_sink_create(int n_streams, int width, int height, int slots, av1r_output_sink* out);
+void av1r_ring_sink_destroy(av1r_output_sink* sink);
+int64_t av1r_ring_sink_delivered(const av1r_output_sink* sink, int stream);
+const uint8_t* av1r_ring_sink_frame(const av1r_output_sink* sink, int stream, int64_t k, int* width, int* height);
 /* Source over in-memory batches: stream s (< n_streams) yields batches[s][pos[s] % count[s]],
  * then advances pos[s] (use av1r_cycle_next as `next` and an av1r_cycle as `user`).  It
  * never ends, so av1r_pipeline_run rejects it (AV1R_E_INVALID) without max_frames > 0 or

@@ -133,3 +133,110 @@ def test_gpu_headline_ivf_path_matches_reference_and_oracle():
         assert len(outs[j]) == frames
         for k, planes in enumerate(outs[j]):
             assert _frame_md5(planes) == ref[j][k], f"stream {j} frame {k}"
+
+
+class _DigestSink:
+    """An output sink (av1dec_amd.pipeline.ArraySink) that keeps each delivered frame's MD5s."""
+
+    def __init__(self, n):
+        from av1dec_amd.pipeline import ArraySink
+        self.sink = ArraySink(n)
+        self.md5 = [[] for _ in range(n)]
+        orig = self.sink._deliver
+
+        def deliver(user, stream, status):
+            orig(user, stream, status)
+            self.md5[stream].append(_frame_md5(self.sink.frames[stream].pop()))
+        self.sink._deliver = deliver
+        from av1dec_amd import native
+        import ctypes as C
+        self.sink._del = native.SINK_DELIVER(deliver)
+        self.sink.s.deliver = C.cast(self.sink._del, C.c_void_p).value
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gpu_headline_async_delivery_matches_oracle():
+    """bench.py's output leg: the headline pipeline with frame delivery (av1r_pipeline_set_output):
+    every shown frame's read-back starts on the context's read-back stream as soon as its batch is
+    launched and lands while later batches decode (av1r_get_output_async / av1r_output_query),
+    delivered in order per stream -- over one whole GOP of the 8 bench streams (key frames
+    included), every delivered frame equals the CPU oracle.  Reference: Decoder::getOutput
+    (decoder/Av1Decoder.cpp:203-211) drained after every unit (tests/Av1Dec.cpp:216-220)."""
+    import bench
+    from av1dec_amd import Decoder
+    from av1dec_amd.pipeline import NativePipeline
+    S, F = 8, 60
+    streams = bench.rank_streams("1080p", 0, S, F)
+    with ThreadPoolExecutor(min(S, 16)) as ex:
+        ref = [ex.submit(_oracle_md5s, s) for s in streams]
+        decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+        ds = _DigestSink(S)
+        try:
+            pos0 = [bench.gop_offsets(S, F)[j] for j in range(S)]
+            # every stream starts at its key frame here, then runs one GOP + its phase offset
+            pl = NativePipeline(decs, streams, [0] * S, depth=0, workers=bench.host_workers())
+            try:
+                pl.set_output(ds.sink)
+                n = sum(pl.step(k)["frames"] for k in (7, 23, F - 30))
+                assert n == S * F
+                pl.set_output(None)
+            finally:
+                pl.close()
+            assert all(d.output_pending() == 0 for d in decs)  # everything was delivered
+        finally:
+            for d in decs:
+                d.close()
+        ref = [r.result() for r in ref]
+    assert pos0  # (phases are exercised by the cycle test above)
+    for j in range(S):
+        assert ds.sink.status[j] == [0] * F
+        assert ds.md5[j] == ref[j], f"stream {j}"
+
+
+@pytest.mark.gpu
+def test_gpu_get_output_async_and_prefetch_match_oracle():
+    """av1r_get_output_async per frame (tickets polled, then waited for out of order across
+    streams) and av1r_set_output_prefetch (the Yami facade's mode: read-backs started at launch,
+    av1r_get_output waits for the staged copy) both return the oracle's frames, on a conformance
+    stream and two synthetic 1080p streams."""
+    import bench
+    import golden
+    import numpy as np
+    from av1dec_amd import Decoder, batchfile
+    sets = [batchfile.load(golden.batch_path("av1-1-b8-06-mfmv"))] + bench.rank_streams("1080p", 0, 2, 6)
+    for frames in sets:
+        ref = _oracle_md5s(frames)
+        # async: queue every frame's read-back, then wait in reverse order
+        d = Decoder(0, keep_stages=False)
+        try:
+            tickets = []
+            for f in frames:
+                d.decode_frame(f)
+                while d.output_pending():
+                    w, h = d.output_size()
+                    planes = (np.empty((h, w), np.uint8), np.empty((h >> 1, w >> 1), np.uint8),
+                              np.empty((h >> 1, w >> 1), np.uint8))
+                    tickets.append(d.get_output_async(*planes))
+            assert d.get_output_async(*planes) is None
+            got = [None] * len(tickets)
+            for k in reversed(range(len(tickets))):
+                tickets[k].ready()
+                got[k] = _frame_md5(tickets[k].wait())
+            assert got == ref
+        finally:
+            d.close()
+        # prefetch
+        d = Decoder(0, keep_stages=False)
+        try:
+            assert d.l.av1r_set_output_prefetch(d.c, 1) == 0
+            got = []
+            for f in frames:
+                d.decode_frame(f)
+                if d.output_pending() > 1:
+                    got.append(_frame_md5(d.get_output()))
+            while d.output_pending():
+                got.append(_frame_md5(d.get_output()))
+            assert got == ref
+        finally:
+            d.close()
