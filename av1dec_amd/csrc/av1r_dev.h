@@ -155,7 +155,9 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the launch's pinned host error word
 #define FLOW_SPINLIM (FLOW_ERR + 4)  // polls before a wait gives up (0: FLOW_SPINS)
 #define FLOW_ASSIGN (FLOW_ERR + FLOW_LINE)  // workgroup entries: entry k serves queue k % FLOW_QUEUES
-#define FLOW_CTL_BYTES 1280
+// per-wave small-item queues (AV1R_FLOW_WAVE): FLOW_QUEUES more heads, one line each
+#define FLOW_SMALLQ (FLOW_ASSIGN + FLOW_LINE)
+#define FLOW_CTL_BYTES (4 * (FLOW_SMALLQ + FLOW_QUEUES * FLOW_LINE))
 // k_strip: luma rows per strip (one workgroup each; chroma strips are the same rows at 4:2:0).
 // 64 = the largest transform side, so no transform block spans two strips
 #define AV1R_STRIP_H 64

@@ -43,7 +43,7 @@ uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset);
 #endif
 int flow_grid(int device, int maxPer);
 void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
-void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t nSmall, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s);
 void launch_k_strip(const KParams* kps, const void* groups, const uint32_t* stripStart, uint32_t nStrips, uint32_t* ctl,
     uint32_t epoch, unsigned long long* trace, hipStream_t s);
@@ -475,7 +475,15 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                 const int log2Area = std::min<int>(av1r_tx_w_log2[t.tx_size], 5) + std::min<int>(av1r_tx_h_log2[t.tx_size], 5);
                 uint32_t acc = 0;
                 const uint32_t* cf = b->coefs + t.coef_off;
-                for (int q = 0; q < t.coef_cnt; q++) acc |= cf[q];
+                const uint32_t n = t.coef_cnt;
+                if ((uint64_t)t.coef_off + 16 <= b->n_coefs) {
+                    // the first 16 (most TBs have fewer) masked, without a data-dependent
+                    // branch: a short loop per TB mispredicted its exit once per TB
+                    for (uint32_t q = 0; q < 16; q++) acc |= cf[q] & (q < n ? ~0u : 0u);
+                    for (uint32_t q = 16; q < n; q++) acc |= cf[q];
+                } else {
+                    for (uint32_t q = 0; q < n; q++) acc |= cf[q];
+                }
                 badC |= (acc & 1023u) >> log2Area;
             }
         // palette blocks (rare): their records, then the map window of every transform block
@@ -1585,20 +1593,27 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     flow = (flow || mustFlow) && allFlow;
     // k_flow groups of the frames without a strip schedule; k_strip strips and groups of the
     // others (deep frames, build_strips)
-    size_t nGroups = 0, nStripG = 0, nStripS = 0;
+    // AV1R_FLOW_WAVE=1: small items as single entries after the groups, served per wave
+    // (recon.hip, flow_small_wave); nGroups then counts the large items only
+    static const bool waveItems = getenv("AV1R_FLOW_WAVE") && atoi(getenv("AV1R_FLOW_WAVE")) != 0;
+    size_t nGroups = 0, nSmallItems = 0, nStripG = 0, nStripS = 0;
     for (auto& j : jobs) {
         if (flow && !j.P->stripGroups.empty()) {
             nStripG += j.P->stripGroups.size() / 2;
             nStripS += j.P->stripStart.size() - 1;
             continue;
         }
-        for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
+        for (const Level& lv : j.P->levels) {
+            nGroups += lv.fcnt[1] + (waveItems ? 0 : (lv.fcnt[2] + 3) / 4);
+            nSmallItems += waveItems ? lv.fcnt[2] : 0;
+        }
     }
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
     const size_t stripTabBytes = nStripS ? align256(4 * (2 * nStripS + 2)) : 0;
     const size_t stripBytes = nStripS ? stripTabBytes + 8 * nStripG : 0;
-    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nGroups + resTabBytes + stripBytes : 0);
-    const bool anyFlow = flow && (nGroups || nStripG);
+    const size_t nEntries = nGroups + nSmallItems;  // (the groups array: groups, then single small items)
+    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nEntries + resTabBytes + stripBytes : 0);
+    const bool anyFlow = flow && (nEntries || nStripG);
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % av1r_ctx::kMetaRing;
     if (M.pending) {
@@ -1696,8 +1711,18 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                     g[0] = (uint32_t)i << 8;
                     g[1] = lv.off[1] + q;
                 }
-                for (uint32_t q = 0; q < lv.fcnt[2]; q += 4, g += 2) {
+                for (uint32_t q = 0; q < lv.fcnt[2] && !waveItems; q += 4, g += 2) {
                     g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(4, lv.fcnt[2] - q);
+                    g[1] = lv.off[2] + q;
+                }
+            }
+        for (size_t l = 0; l < nLevels && waveItems; l++)  // the single small items, same order
+            for (int i = 0; i < n; i++) {
+                const auto& lvs = jobs[i].P->levels;
+                if (l >= lvs.size() || !jobs[i].P->stripGroups.empty()) continue;
+                const Level& lv = lvs[l];
+                for (uint32_t q = 0; q < lv.fcnt[2]; q++, g += 2) {
+                    g[0] = ((uint32_t)i << 8) | 1u;
                     g[1] = lv.off[2] + q;
                 }
             }
@@ -1711,7 +1736,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (nStripS) {
             // k_strip: [the strips' first groups (nStripS + 1)] [the strips' indices in their
             // frames (nStripS)] [groups {frame << 8 | n, first item}]
-            uint32_t* ss = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups + resTabBytes);
+            uint32_t* ss = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries + resTabBytes);
             uint32_t* sg = ss + stripTabBytes / 4;
             uint32_t gb = 0, si = 0;
             for (int i = 0; i < n; i++) {
@@ -1812,12 +1837,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         }
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
-        const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
-        const uint32_t* hrt = reinterpret_cast<const uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups);
+        const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries);
+        const uint32_t* hrt = reinterpret_cast<const uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries);
         if (hrt[n]) launch_k_resid(0, dk, drt, n, hrt[n], st);
         if (hrt[2 * n + 1]) launch_k_resid(1, dk, drt + n + 1, n, hrt[2 * n + 1], st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
-        if (nGroups) {
+        if (nEntries) {
             if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
             static const bool chain = getenv("AV1R_FLOW_CHAIN") && atoi(getenv("AV1R_FLOW_CHAIN")) != 0;
             FlowChain& F = g_flowChain[lc->device];
@@ -1827,6 +1852,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             // solo deep frame takes one per CU and leaves the rest to concurrent batches)
             int grid = (int)std::min<size_t>(flow_grid(lc->device, lc->flowPerCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             if (lc->flowGridCap > 0) grid = std::max(FLOW_QUEUES, std::min(grid, lc->flowGridCap / FLOW_QUEUES * FLOW_QUEUES));
+            // per-wave small items: every resident slot, and at least one server per queue of
+            // both populations (FLOW_LARGE_EVERY x FLOW_QUEUES workgroups, recon.hip)
+            if (nSmallItems) grid = std::max(64, std::max(grid, lc->flowGridCap > 0 ? std::min(flow_grid(lc->device, lc->flowPerCU), lc->flowGridCap) : flow_grid(lc->device, lc->flowPerCU)));
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
@@ -1836,20 +1864,20 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                 hipEvent_t ev = nullptr;
                 HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
                 if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
-                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
+                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, (uint32_t)nSmallItems, ctl, rec->err, epoch, grid, trace, st);
                 HIPCHK(hipEventRecord(ev, st));
                 if (F.done) (void)hipEventDestroy(F.done);
                 F.done = ev;
                 F.last = st;
             } else {
-                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
+                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, (uint32_t)nSmallItems, ctl, rec->err, epoch, grid, trace, st);
             }
             flow_debug_note(epoch, st);
         }
         if (nStripS) {  // deep frames: one workgroup per strip (build_strips)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
-            const uint8_t* sb = M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nGroups + resTabBytes;
+            const uint8_t* sb = M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries + resTabBytes;
             launch_k_strip(dk, sb + stripTabBytes, reinterpret_cast<const uint32_t*>(sb), (uint32_t)nStripS, ctl, epoch, trace, st);
         }
     }

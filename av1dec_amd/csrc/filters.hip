@@ -187,10 +187,23 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
 #pragma unroll
             for (int q = 0; q < 16; q++) v[q] = (d[i][q >> 2] >> (8 * (q & 3))) & 0xff;
             lf_filter(v + 8, 1, plane, e.limit, e.blimit, e.thresh, e.filterSize);
+            // the footprint x - n .. x + n - 1 in the widest aligned stores inside it (the
+            // neighbouring edges' footprints start at x - 4 - n' / x + 4 + n'': a store may
+            // not spill past x - n or x + n - 1)
             uint8_t* row = P.p + (size_t)(yP + i) * P.stride + xP;
-#pragma unroll
-            for (int q = -6; q < 6; q++)
-                if (q >= -n && q < n) row[q] = (uint8_t)v[8 + q];
+            auto pk2 = [&](int q) { return (uint16_t)(v[q] | (v[q + 1] << 8)); };
+            auto pk4 = [&](int q) { return (uint32_t)v[q] | ((uint32_t)v[q + 1] << 8) | ((uint32_t)v[q + 2] << 16) | ((uint32_t)v[q + 3] << 24); };
+            if (n == 6) {
+                *reinterpret_cast<uint16_t*>(row - 6) = pk2(2);
+                *reinterpret_cast<uint32_t*>(row - 4) = pk4(4);
+                *reinterpret_cast<uint32_t*>(row) = pk4(8);
+                *reinterpret_cast<uint16_t*>(row + 4) = pk2(12);
+            } else {
+                if (n == 3) row[-3] = (uint8_t)v[5];
+                *reinterpret_cast<uint16_t*>(row - 2) = pk2(6);
+                *reinterpret_cast<uint16_t*>(row) = pk2(8);
+                if (n == 3) row[2] = (uint8_t)v[10];
+            }
         }
         return;
     }
@@ -281,10 +294,10 @@ struct CdefLds {
 
 // partial[d][k] of cdefDirection (Cdef.cpp:203-261) for one line k of direction d, summed
 // over the 8x8 block at (bx, by) of the staged luma tile
-template <int d, class PX>
-DEV int cdef_cost(const PX* blk, int ts)  // blk: the block's top-left pixel in a tile of row stride ts
+// (px8(i, j): the block's pixel at row i, column j, minus 128; compile-time indices)
+template <int d, class F>
+DEV int cdef_cost_f(const F& px8)
 {
-    auto px8 = [&](int i, int j) { return (int)blk[i * ts + j] - 128; };
     int cost = 0;
     if (d == 2 || d == 6) {
 #pragma unroll
@@ -329,6 +342,11 @@ DEV int cdef_cost(const PX* blk, int ts)  // blk: the block's top-left pixel in 
         cost += s * s * w;
     }
     return cost;
+}
+template <int d, class PX>
+DEV int cdef_cost(const PX* blk, int ts)  // blk: the block's top-left pixel in a tile of row stride ts
+{
+    return cdef_cost_f<d>([&](int i, int j) { return (int)blk[i * ts + j] - 128; });
 }
 
 // cdefFilter (Cdef.cpp:158-198) for the four horizontally adjacent pixels at tile offset
@@ -505,26 +523,29 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
         L.filt[t] = (uint8_t)f;
     }
     __syncthreads();
-    // direction costs: lane = (direction d = t >> 5, blocks t & 31 and (t & 31) + 32)
+    // direction costs: wave w (wave-uniform directions 2w and 2w + 1), lane = 8x8 block; the
+    // block's 64 pixels read once as 16 dwords and kept in registers for both directions
     {
-        const int d = t >> 5;
-#pragma unroll
-        for (int hb = 0; hb < 2; hb++) {
-            const int b = (t & 31) + 32 * hb;
-            if (!L.filt[b]) continue;
+        const int b = t & 63, w = t >> 6;
+        if (L.filt[b]) {
             const int bx = (b & 7) * 8, by = (b >> 3) * 8;
-            int c;
-            switch (d) {
-            case 0: c = cdef_cost<0>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            case 1: c = cdef_cost<1>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            case 2: c = cdef_cost<2>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            case 3: c = cdef_cost<3>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            case 4: c = cdef_cost<4>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            case 5: c = cdef_cost<5>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            case 6: c = cdef_cost<6>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
-            default: c = cdef_cost<7>(&L.y[CD_H + by][CD_X + bx], CD_LS); break;
+            uint32_t rw[8][2];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint2 v = *reinterpret_cast<const uint2*>(&L.y[CD_H + by + i][CD_X + bx]);
+                rw[i][0] = v.x;
+                rw[i][1] = v.y;
             }
-            L.cost[b][d] = c;
+            auto px8 = [&](int i, int j) { return (int)((rw[i][j >> 2] >> (8 * (j & 3))) & 0xff) - 128; };
+            int c0, c1;
+            switch (__builtin_amdgcn_readfirstlane(w)) {
+            case 0: c0 = cdef_cost_f<0>(px8), c1 = cdef_cost_f<1>(px8); break;
+            case 1: c0 = cdef_cost_f<2>(px8), c1 = cdef_cost_f<3>(px8); break;
+            case 2: c0 = cdef_cost_f<4>(px8), c1 = cdef_cost_f<5>(px8); break;
+            default: c0 = cdef_cost_f<6>(px8), c1 = cdef_cost_f<7>(px8); break;
+            }
+            L.cost[b][2 * w] = c0;
+            L.cost[b][2 * w + 1] = c1;
         }
     }
     __syncthreads();
@@ -730,16 +751,33 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
         const bool doW = anyW && (rounds == 1 || rd == 0), doS = anyS && (rounds == 1 || rd == 1);
         if (rd) __syncthreads();  // round 0's reads of the shared LDS are done
         if (doW) {
-            // wienerFilter horizontal pass (LoopRestoration.cpp:253-265)
+            // wienerFilter horizontal pass (LoopRestoration.cpp:253-265), four columns per lane:
+            // a 4-column group lies in one restoration unit (units start at multiples of 32 of
+            // the plane, x0 at a multiple of 64), its 10 source bytes come from 3 aligned dwords
             const int offset = 1 << (8 + 7 - 3 - 1), limit = (1 << (8 + 1 + 7 - 3)) - 1;
-            for (int q = t; q < (th + 6) * tw; q += 256) {
-                const int i = fullW ? q / LR_TW : q / tw, c = q - i * tw;
-                const av1r_lr_unit& u = L.unit[unitOf(c)];
+            const int ng = (tw + 3) >> 2;
+            for (int q = t; q < (th + 6) * ng; q += 256) {
+                const int i = fullW ? q >> 4 : q / ng, c0 = 4 * (q - i * ng);
+                const av1r_lr_unit& u = L.unit[unitOf(c0)];
                 if (u.type != AV1R_RESTORE_WIENER) continue;
-                int hf3 = 128 - 2 * (u.wiener[1][0] + u.wiener[1][1] + u.wiener[1][2]);
-                const uint8_t* sp = &L.src[i][c + 1];
-                int hs = u.wiener[1][0] * (sp[0] + sp[6]) + u.wiener[1][1] * (sp[1] + sp[5]) + u.wiener[1][2] * (sp[2] + sp[4]) + hf3 * sp[3];
-                L.hw[i][c] = (int16_t)CLIP3(-offset, limit - offset, r2(hs, 3));
+                const int f0 = u.wiener[1][0], f1 = u.wiener[1][1], f2 = u.wiener[1][2];
+                const int hf3 = 128 - 2 * (f0 + f1 + f2);
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(&L.src[i][c0]);
+                const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+                int sp[10];  // L.src[i][c0 + 1 + k]
+#pragma unroll
+                for (int k = 0; k < 10; k++) {
+                    const int b = k + 1;
+                    const uint32_t dw = b < 4 ? d0 : (b < 8 ? d1 : d2);
+                    sp[k] = (dw >> (8 * (b & 3))) & 0xff;
+                }
+                int o[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int hs = f0 * (sp[j] + sp[j + 6]) + f1 * (sp[j + 1] + sp[j + 5]) + f2 * (sp[j + 2] + sp[j + 4]) + hf3 * sp[j + 3];
+                    o[j] = CLIP3(-offset, limit - offset, r2(hs, 3)) & 0xffff;
+                }
+                *reinterpret_cast<uint2*>(&L.hw[i][c0]) = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
             }
         }
         if (doS) {
@@ -790,60 +828,98 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
             }
         }
         __syncthreads();
-        for (int q = t; q < tw * th; q += 256) {
-            const int r = fullW ? q / LR_TW : q / tw, c = q - r * tw;
-            const int x = x0 + c, y = ty0 + r;
-            const int cdef = L.src[r + 3][c + 4];
-            int outv = cdef;
-            const int ui = unitOf(c);
+        // the output, four pixels per lane (one dword store): the group's unit and its
+        // parameters once, the Wiener column sums from int16 pairs, the self-guided A / B of
+        // the six columns c0 - 1 .. c0 + 4 once per row and pass, their cross-unit columns (only
+        // a group at a unit boundary has one) recomputed with this unit's set
+        const int ng = (tw + 3) >> 2;
+        for (int q = t; q < ng * th; q += 256) {
+            const int r = fullW ? q >> 4 : q / ng, c0 = 4 * (q - r * ng);
+            const int x = x0 + c0, y = ty0 + r;
+            const uint32_t cw = *reinterpret_cast<const uint32_t*>(&L.src[r + 3][c0 + 4]);
+            const int ui = unitOf(c0);
             const av1r_lr_unit& u = L.unit[ui];
-            const bool filt = x < planeEndX && y < planeEndY && u.type != AV1R_RESTORE_NONE;
-            // this round's pixels: Wiener and unfiltered ones in round 0, self-guided in round 1
+            // (x < planeEndX, y < planeEndY hold for every pixel of the tile: tw, th stop at the
+            // plane's edge, which is planeEndX / planeEndY)
+            const bool filt = u.type != AV1R_RESTORE_NONE;
+            // this round's groups: Wiener and unfiltered ones in round 0, self-guided in round 1
             if (rounds == 2 && (rd == 1) != (filt && u.type == AV1R_RESTORE_SGRPROJ)) continue;
-            if (filt) {
-                if (u.type == AV1R_RESTORE_WIENER) {
-                    int vf3 = 128 - 2 * (u.wiener[0][0] + u.wiener[0][1] + u.wiener[0][2]);
-                    int s = u.wiener[0][0] * (L.hw[r][c] + L.hw[r + 6][c]) + u.wiener[0][1] * (L.hw[r + 1][c] + L.hw[r + 5][c])
-                        + u.wiener[0][2] * (L.hw[r + 2][c] + L.hw[r + 4][c]) + vf3 * L.hw[r + 3][c];
-                    outv = clip1(r2(s, 11));
-                } else {
-                    // selfGuidedFilter (LoopRestoration.cpp:420-479)
-                    const int set = u.sgr_set;
-                    const int i = y - y0;
-                    const int uu = cdef << 4;
-                    const int w0 = u.sgr_xqd[0], w1 = u.sgr_xqd[1], w2 = (1 << 7) - w0 - w1;
-                    int v = w1 * uu;
-    #pragma unroll
-                    for (int pass = 0; pass < 2; pass++) {
-                        const int rad = av1r_sgr_params[set][pass * 2];
-                        const int w = pass ? w2 : w0;
-                        if (!rad) {
-                            v += w * uu;
-                            continue;
+            uint32_t ow = cw;
+            if (filt && u.type == AV1R_RESTORE_WIENER) {
+                const int g0 = u.wiener[0][0], g1 = u.wiener[0][1], g2 = u.wiener[0][2];
+                const int vf3 = 128 - 2 * (g0 + g1 + g2);
+                int hv[7][4];
+#pragma unroll
+                for (int k = 0; k < 7; k++) {
+                    const uint2 d = *reinterpret_cast<const uint2*>(&L.hw[r + k][c0]);
+                    hv[k][0] = (int16_t)(d.x & 0xffff), hv[k][1] = (int16_t)(d.x >> 16);
+                    hv[k][2] = (int16_t)(d.y & 0xffff), hv[k][3] = (int16_t)(d.y >> 16);
+                }
+                ow = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int sum = g0 * (hv[0][j] + hv[6][j]) + g1 * (hv[1][j] + hv[5][j]) + g2 * (hv[2][j] + hv[4][j]) + vf3 * hv[3][j];
+                    ow |= (uint32_t)clip1(r2(sum, 11)) << (8 * j);
+                }
+            } else if (filt) {
+                // selfGuidedFilter (LoopRestoration.cpp:420-479)
+                const int set = u.sgr_set;
+                const int i = y - y0;
+                const int w0 = u.sgr_xqd[0], w1 = u.sgr_xqd[1], w2 = (1 << 7) - w0 - w1;
+                const bool crossL = c0 > 0 && unitOf(c0 - 1) != ui, crossR = unitOf(c0 + 4) != ui;
+                int px4[4], v[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    px4[j] = (cw >> (8 * j)) & 0xff;
+                    v[j] = w1 * (px4[j] << 4);
+                }
+#pragma unroll
+                for (int pass = 0; pass < 2; pass++) {
+                    const int rad = av1r_sgr_params[set][pass * 2];
+                    const int w = pass ? w2 : w0;
+                    if (!rad) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) v[j] += w * (px4[j] << 4);
+                        continue;
+                    }
+                    const int shift = (pass == 0 && (i & 1)) ? 4 : 5;
+                    int a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++) {
+                        if (pass == 0 && !((i + dy) & 1)) continue;
+                        // A / B of columns c0 - 1 .. c0 + 4 (indices c0 .. c0 + 5 of the a/b planes)
+                        int Av[6], Bv[6];
+                        const uint32_t* ap = reinterpret_cast<const uint32_t*>(&L.A[pass][r + 1 + dy][c0]);
+#pragma unroll
+                        for (int k = 0; k < 3; k++) {
+                            const uint32_t d = ap[k];
+                            Av[2 * k] = (int16_t)(d & 0xffff);
+                            Av[2 * k + 1] = (int16_t)(d >> 16);
                         }
-                        const int shift = (pass == 0 && (i & 1)) ? 4 : 5;
-                        int a = 0, b = 0;
-                        for (int dy = -1; dy <= 1; dy++) {
-                            if (pass == 0 && !((i + dy) & 1)) continue;
+#pragma unroll
+                        for (int k = 0; k < 6; k++) Bv[k] = L.B[pass][r + 1 + dy][c0 + k];
+                        if (crossL) sgr_ab_lds(L, r + 3 + dy, c0 + 3, rad, set, pass, Av[0], Bv[0]);
+                        if (crossR) sgr_ab_lds(L, r + 3 + dy, c0 + 8, rad, set, pass, Av[5], Bv[5]);
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+#pragma unroll
                             for (int dx = -1; dx <= 1; dx++) {
                                 const int wt = pass == 0 ? (dx == 0 ? 6 : 5) : ((dx == 0 || dy == 0) ? 4 : 3);
-                                int A, B;
-                                if (unitOf(c + dx) == ui) {
-                                    A = L.A[pass][r + 1 + dy][c + 1 + dx];
-                                    B = L.B[pass][r + 1 + dy][c + 1 + dx];
-                                } else {  // neighbour column in another unit: this unit's parameters
-                                    sgr_ab_lds(L, r + 3 + dy, c + 4 + dx, rad, set, pass, A, B);
-                                }
-                                a += wt * A;
-                                b += wt * B;
+                                a[j] += wt * Av[j + 1 + dx];
+                                b[j] += wt * Bv[j + 1 + dx];
                             }
-                        }
-                        v += w * r2(a * cdef + b, 8 + shift - 4);
                     }
-                    outv = clip1(r2(v, 4 + 7));
+#pragma unroll
+                    for (int j = 0; j < 4; j++) v[j] += w * r2(a[j] * px4[j] + b[j], 8 + shift - 4);
                 }
+                ow = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) ow |= (uint32_t)clip1(r2(v[j], 4 + 7)) << (8 * j);
             }
-            O.p[(size_t)y * O.stride + x] = (uint8_t)outv;
+            uint8_t* dst = O.p + (size_t)y * O.stride + x;
+            if (c0 + 4 <= tw) *reinterpret_cast<uint32_t*>(dst) = ow;
+            else
+                for (int j = 0; j < tw - c0; j++) dst[j] = (uint8_t)(ow >> (8 * j));
         }
     }
 }

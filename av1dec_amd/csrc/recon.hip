@@ -1784,8 +1784,36 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 #define FLOW_DBG_PAIRS 256
 __device__ uint32_t g_flow_active[64], g_flow_overlap, g_flow_pairs[FLOW_DBG_PAIRS];
 #endif
+// Per-wave small items (nSmall > 0, the host's AV1R_FLOW_WAVE): groups[nGroups ..
+// nGroups + nSmall) are single small items (n = 1), in the same topological order, served by
+// WAVES instead of workgroups: of the workgroups, entry e with e % FLOW_LARGE_EVERY == 0
+// serves the group queue (e / FLOW_LARGE_EVERY) % FLOW_QUEUES as above, every other one puts
+// each of its four waves on small queue (4 e + wave) % FLOW_QUEUES, pulling one item per
+// atomic -- no group lock-step (a group of four waited for its slowest item) and no barrier
+// between items.  Progress as above, per population: each queue hands out its items in
+// topological order and a server holds only items taken before the queue's next one, so the
+// earliest unfinished item is held by a server whose inputs are complete, or is the next of
+// a queue whose servers all hold items of its level; once FLOW_LARGE_EVERY * FLOW_QUEUES
+// workgroups have started every queue of both populations has a resident server.
+#define FLOW_LARGE_EVERY 8
+DEV void flow_small_wave(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups, uint32_t nSmall,
+    uint32_t* ctl, uint32_t epoch, unsigned long long* trace, uint32_t q, TbLds<TB_SMALL>& L)
+{
+    uint32_t* head = ctl + FLOW_SMALLQ + q * FLOW_LINE;
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        uint32_t tk = 0;
+        if (lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t g = __builtin_amdgcn_readfirstlane(__shfl(tk, 0)) * FLOW_QUEUES + q;
+        if (g >= nSmall) return;
+        const uint2 gd = groups[nGroups + g];
+        const KParams& k = KP(kps, gd.x >> 8);
+        flow_item<64, TB_SMALL>(k, gd.y, L, epoch, ctl, trace, gd.x >> 8);
+    }
+}
+
 extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
-    uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
+    uint32_t nSmall, uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
     __shared__ __align__(16) uint8_t smem[kLds];
@@ -1798,7 +1826,8 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     // workgroups, and B's the other way round: the cross-stream timeout of round 1.)
     __shared__ uint32_t qsh;
     if (threadIdx.x == 0) {
-        qsh = __hip_atomic_fetch_add(ctl + FLOW_ASSIGN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % FLOW_QUEUES;
+        const uint32_t e = __hip_atomic_fetch_add(ctl + FLOW_ASSIGN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qsh = nSmall ? e : e % FLOW_QUEUES;
 #ifdef AV1R_FLOW_DEBUG
         atomicAdd(&g_flow_active[epoch & 63], 1u);
         for (uint32_t e = 1; e < 64; e++) {
@@ -1812,7 +1841,16 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 #endif
     }
     __syncthreads();
-    const uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
+    uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
+    if (nSmall) {  // qsh holds the entry number itself here
+        if (q % FLOW_LARGE_EVERY) {
+            const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            flow_small_wave(kps, groups, nGroups, nSmall, ctl, epoch, trace, (4 * q + wave) % FLOW_QUEUES,
+                reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave]);
+            return;
+        }
+        q = (q / FLOW_LARGE_EVERY) % FLOW_QUEUES;
+    }
     uint32_t* head = ctl + q * FLOW_LINE;
     if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -1891,11 +1929,11 @@ uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset)
 }
 #endif
 
-void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t nSmall, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s)
 {
     (void)hostErr;  // (its address travels in the control block: FLOW_HOSTERR)
-    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
+    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, nSmall, ctl, epoch,
         trace);
 }
 

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Fold rocprofv3 SQ counter passes (tools/gpu_pmc_sq.sh) per kernel name: totals, and
-the wave-cycle split WAIT_ANY (parked on waitcnt / barrier) / WAIT_INST_ANY (issue stall)
-/ ACTIVE_INST_ANY, per wave.  usage: python tools/pmc_sq_report.py gpurun_out/pmcsq"""
+"""Fold rocprofv3 SQ counter passes (tools/gpu_pmc_sq.sh, tools/gpu_evidence_r04.sh) per
+kernel name: totals, and the wave-cycle split WAIT_ANY (parked on waitcnt / barrier) /
+WAIT_INST_ANY (issue stall) / ACTIVE_INST_ANY, per wave; with GRBM_GUI_ACTIVE also the mean
+resident waves per CU (SQ_WAVE_CYCLES counts quad-cycles, MI355X_MICROARCH.md: waves =
+4 * WAVE_CYCLES / (GUI_ACTIVE / 8 XCDs * 256 CUs)) and VALU-busy = ACTIVE_INST_VALU share of
+the wave cycles.  usage: python tools/pmc_sq_report.py gpurun_out/pmcsq"""
 import csv
 import glob
 import sys
@@ -22,4 +25,6 @@ for k, c in sorted(tot.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
           f" SMEM {c['SQ_INSTS_SMEM'] / w:5.0f} | wave-cycles {wc / w:8.0f}: parked {c['SQ_WAIT_ANY'] / wc:5.1%}"
           f" issue-stall {c['SQ_WAIT_INST_ANY'] / wc:5.1%} active {c['SQ_ACTIVE_INST_ANY'] / wc:5.1%}"
           f" (VALU {c['SQ_ACTIVE_INST_VALU'] / wc:5.1%} LDS {c['SQ_ACTIVE_INST_LDS'] / wc:5.1%}) LDS-stall {c['SQ_WAIT_INST_LDS'] / wc:5.1%}"
-          f" bank-conf {c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_ACTIVE_INST_LDS'], 1):5.2f}x")
+          f" bank-conf {c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_ACTIVE_INST_LDS'], 1):5.2f}x"
+          + (f" | waves/CU {4 * c['SQ_WAVE_CYCLES'] / (c['GRBM_GUI_ACTIVE'] / 8 * 256):5.1f}"
+             f" (of 32) over {c['GRBM_GUI_ACTIVE'] / 8 / 2.1e3:7.1f} us busy" if c.get("GRBM_GUI_ACTIVE") else ""))
