@@ -1171,10 +1171,25 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         const bool large = av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
         return (large ? 0 : 2) + ((b->blocks[t.block].flags & AV1R_BLK_INTER) ? 1 : 0);
     };
+    // AV1R_INTER_ORDER=1: within each class the inter tiles grouped by their first reference
+    // (stable: raster order inside a group), so that the tiles an XCD runs together stream one
+    // reference's rows through its L2 instead of all seven (synthetic blocks pick among 7)
+    static const bool byRef = getenv("AV1R_INTER_ORDER") && atoi(getenv("AV1R_INTER_ORDER")) != 0;
+    std::vector<uint32_t> rk[8];
+    auto refSort = [&](uint32_t* v, uint32_t cnt) {
+        for (auto& r : rk) r.clear();
+        for (uint32_t q = 0; q < cnt; q++) rk[b->blocks[AV1R_ITEM_INDEX(v[q]) >> 4].ref_frame[0] & 7].push_back(v[q]);
+        for (auto& r : rk) {
+            std::copy(r.begin(), r.end(), v);
+            v += r.size();
+        }
+    };
     for (size_t l = 0; l < nl; l++) {
         // order: inter tiles, then k_tb's large items, then its small ones
         uint32_t pc[4] = {}, tc[4] = {};
         partition(c->lvP[l], 3, pc, plainClass);
+        if (byRef)
+            for (uint32_t q = 0, o = 0; q < 3; o += pc[q++]) refSort(c->lvP[l].data() + o, pc[q]);
         c->levels[l].pl[0] = pc[1];
         c->levels[l].pl[1] = pc[2];
         std::vector<uint32_t>& T = c->lvT[l];

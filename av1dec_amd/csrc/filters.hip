@@ -116,6 +116,82 @@ DEV void lf_filter(PX* c, int step, int plane, int limit, int blimit, int thresh
 #undef QQ
 }
 
+// lf_filter on two lines at once (two samples per 16-bit half of a dword, v_pk_* ops): the
+// same decisions and arithmetic per line, every quantity fits int16 (|values| < 16384), and a
+// line's filters are chosen with per-half masks (bitfield selects) instead of branches.  Each
+// path reads the unfiltered samples: the paths' write masks are disjoint, and a select leaves
+// the other line's samples untouched.  c: the first q sample (c[-7] .. c[6] are read).
+typedef short lf2 __attribute__((ext_vector_type(2)));
+DEV lf2 lf_abs(lf2 a) { return __builtin_elementwise_max(a, -a); }
+DEV lf2 lf_gt(lf2 a, lf2 b) { return (b - a) >> (short)15; }  // -1 where a > b
+DEV lf2 lf_clamp8(lf2 a) { return __builtin_elementwise_min(__builtin_elementwise_max(a, lf2{-128, -128}), lf2{127, 127}); }
+DEV lf2 lf_sel(lf2 m, lf2 a, lf2 b) { return (a & m) | (b & ~m); }
+DEV bool lf_any(lf2 m) { return (m.x | m.y) != 0; }
+template <int n, int log2Size, int n2>
+DEV void lf_wide2(lf2* c, lf2 m)
+{
+    lf2 F[2 * n];
+#pragma unroll
+    for (int i = -n; i < n; i++) {
+        lf2 t = {0, 0};
+#pragma unroll
+        for (int j = -n; j <= n; j++) {
+            const int p = CLIP3(-(n + 1), n, i + j);
+            t += (j <= n2 && j >= -n2) ? c[p] + c[p] : c[p];
+        }
+        F[i + n] = (t + (short)(1 << (log2Size - 1))) >> (short)log2Size;
+    }
+#pragma unroll
+    for (int i = -n; i < n; i++) c[i] = lf_sel(m, F[i + n], c[i]);
+}
+DEV void lf_filter2(lf2* c, int plane, int limit, int blimit, int thresh, int filterSize)
+{
+    const lf2 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3];
+    const lf2 p0 = c[-1], p1 = c[-2], p2 = c[-3], p3 = c[-4];
+    const lf2 L = {(short)limit, (short)limit}, T = {(short)thresh, (short)thresh}, one = {1, 1};
+    const lf2 ap1p0 = lf_abs(p1 - p0), aq1q0 = lf_abs(q1 - q0);
+    const lf2 hev = lf_gt(ap1p0, T) | lf_gt(aq1q0, T);
+    const int filterLen = filterSize == 4 ? 4 : (plane ? 6 : (filterSize == 8 ? 8 : 16));
+    lf2 mask = lf_gt(ap1p0, L) | lf_gt(aq1q0, L) |
+               lf_gt(lf_abs(p0 - q0) * (short)2 + (lf_abs(p1 - q1) >> (short)1), lf2{(short)blimit, (short)blimit});
+    if (filterLen >= 6) mask |= lf_gt(lf_abs(p2 - p1), L) | lf_gt(lf_abs(q2 - q1), L);
+    if (filterLen >= 8) mask |= lf_gt(lf_abs(p3 - p2), L) | lf_gt(lf_abs(q3 - q2), L);
+    const lf2 apply = ~mask;
+    if (!lf_any(apply)) return;
+    lf2 flat = {0, 0};
+    if (filterSize >= 8) {
+        lf2 m = lf_gt(ap1p0, one) | lf_gt(aq1q0, one) | lf_gt(lf_abs(p2 - p0), one) | lf_gt(lf_abs(q2 - q0), one);
+        if (filterLen >= 8) m |= lf_gt(lf_abs(p3 - p0), one) | lf_gt(lf_abs(q3 - q0), one);
+        flat = ~m;
+    }
+    const lf2 narrow = apply & ~flat;
+    if (lf_any(narrow)) {
+        const lf2 k128 = {128, 128};
+        const lf2 ps0 = p0 - k128, ps1 = p1 - k128, qs0 = q0 - k128, qs1 = q1 - k128;
+        lf2 filt = lf_clamp8(ps1 - qs1) & hev;
+        filt = lf_clamp8(filt + (qs0 - ps0) * (short)3);
+        const lf2 f1 = lf_clamp8(filt + (short)4) >> (short)3, f2 = lf_clamp8(filt + (short)3) >> (short)3;
+        c[0] = lf_sel(narrow, lf_clamp8(qs0 - f1) + k128, c[0]);
+        c[-1] = lf_sel(narrow, lf_clamp8(ps0 + f2) + k128, c[-1]);
+        const lf2 f = (f1 + (short)1) >> (short)1, n1 = narrow & ~hev;
+        c[1] = lf_sel(n1, lf_clamp8(qs1 - f) + k128, c[1]);
+        c[-2] = lf_sel(n1, lf_clamp8(ps1 + f) + k128, c[-2]);
+    }
+    lf2 wide = apply & flat;
+    if (!lf_any(wide)) return;
+    if (filterSize >= 16) {
+        const lf2 q4 = c[4], q5 = c[5], q6 = c[6], p4 = c[-5], p5 = c[-6], p6 = c[-7];
+        const lf2 m = lf_gt(lf_abs(p6 - p0), one) | lf_gt(lf_abs(q6 - q0), one) | lf_gt(lf_abs(p5 - p0), one) |
+                      lf_gt(lf_abs(q5 - q0), one) | lf_gt(lf_abs(p4 - p0), one) | lf_gt(lf_abs(q4 - q0), one);
+        const lf2 w16 = wide & ~m;
+        if (lf_any(w16)) lf_wide2<6, 4, 1>(c, w16);
+        wide &= m;
+        if (!lf_any(wide)) return;
+    }
+    if (!plane) lf_wide2<3, 3, 0>(c, wide);
+    else lf_wide2<2, 3, 1>(c, wide);
+}
+
 // The edge of pass `pass` (0: vertical edges, 1: horizontal) at plane position (xP, yP), a
 // multiple of 4, of plane `plane` (LoopFilter::loop_filter_edge, LoopFilter.cpp:85-126, and
 // the level / limit derivation, :301-359): false if no filter runs there, else its size
@@ -167,6 +243,14 @@ DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& 
 // (p1..q1 for 4 taps and chroma, p2..q2 for luma 8, p5..q5 for 16).  Rewriting an unmodified
 // sample there is safe: the filter length is bounded by the transform sizes on both sides,
 // so no other edge of the pass writes inside this footprint.
+DEV lf2 lf_pair(uint32_t a, uint32_t b, int k)  // {byte k of a, byte k of b} (k compile-time)
+{
+    return __builtin_bit_cast(lf2, __builtin_amdgcn_perm(b, a, 0x0c000c00u | ((uint32_t)(4 + k) << 16) | (uint32_t)k));
+}
+DEV uint32_t lf_lo2(lf2 a, lf2 b)  // bytes {a.x, b.x, a.y, b.y}
+{
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
+}
 DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const LfEdge& e)
 {
     const bool wide = e.filterSize == 16;
@@ -181,28 +265,41 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
             d[i][0] = wide ? row[-2] : 0u;
             d[i][3] = wide ? row[1] : 0u;
         }
+        // rows (0, 1) and (2, 3) filtered as pairs: v[q] = the two rows' samples at x - 8 + q
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            int v[16];
+        for (int h = 0; h < 2; h++) {
+            lf2 v[16];
 #pragma unroll
-            for (int q = 0; q < 16; q++) v[q] = (d[i][q >> 2] >> (8 * (q & 3))) & 0xff;
-            lf_filter(v + 8, 1, plane, e.limit, e.blimit, e.thresh, e.filterSize);
+            for (int q = 0; q < 16; q++) v[q] = lf_pair(d[2 * h][q >> 2], d[2 * h + 1][q >> 2], q & 3);
+            lf_filter2(v + 8, plane, e.limit, e.blimit, e.thresh, e.filterSize);
             // the footprint x - n .. x + n - 1 in the widest aligned stores inside it (the
             // neighbouring edges' footprints start at x - 4 - n' / x + 4 + n'': a store may
-            // not spill past x - n or x + n - 1)
-            uint8_t* row = P.p + (size_t)(yP + i) * P.stride + xP;
-            auto pk2 = [&](int q) { return (uint16_t)(v[q] | (v[q + 1] << 8)); };
-            auto pk4 = [&](int q) { return (uint32_t)v[q] | ((uint32_t)v[q + 1] << 8) | ((uint32_t)v[q + 2] << 16) | ((uint32_t)v[q + 3] << 24); };
+            // not spill past x - n or x + n - 1); u(q) = bytes {row a q, q + 1, row b q, q + 1}
+            uint8_t* ra = P.p + (size_t)(yP + 2 * h) * P.stride + xP;
+            uint8_t* rb = ra + P.stride;
+            auto u = [&](int q) { return lf_lo2(v[q], v[q + 1]); };
             if (n == 6) {
-                *reinterpret_cast<uint16_t*>(row - 6) = pk2(2);
-                *reinterpret_cast<uint32_t*>(row - 4) = pk4(4);
-                *reinterpret_cast<uint32_t*>(row) = pk4(8);
-                *reinterpret_cast<uint16_t*>(row + 4) = pk2(12);
+                const uint32_t u2 = u(2), u4 = u(4), u6 = u(6), u8 = u(8), u10 = u(10), u12 = u(12);
+                *reinterpret_cast<uint16_t*>(ra - 6) = (uint16_t)u2;
+                *reinterpret_cast<uint16_t*>(rb - 6) = (uint16_t)(u2 >> 16);
+                *reinterpret_cast<uint32_t*>(ra - 4) = __builtin_amdgcn_perm(u6, u4, 0x05040100u);
+                *reinterpret_cast<uint32_t*>(rb - 4) = __builtin_amdgcn_perm(u6, u4, 0x07060302u);
+                *reinterpret_cast<uint32_t*>(ra) = __builtin_amdgcn_perm(u10, u8, 0x05040100u);
+                *reinterpret_cast<uint32_t*>(rb) = __builtin_amdgcn_perm(u10, u8, 0x07060302u);
+                *reinterpret_cast<uint16_t*>(ra + 4) = (uint16_t)u12;
+                *reinterpret_cast<uint16_t*>(rb + 4) = (uint16_t)(u12 >> 16);
             } else {
-                if (n == 3) row[-3] = (uint8_t)v[5];
-                *reinterpret_cast<uint16_t*>(row - 2) = pk2(6);
-                *reinterpret_cast<uint16_t*>(row) = pk2(8);
-                if (n == 3) row[2] = (uint8_t)v[10];
+                const uint32_t u6 = u(6), u8 = u(8);
+                if (n == 3) {
+                    ra[-3] = (uint8_t)v[5].x;
+                    rb[-3] = (uint8_t)v[5].y;
+                    ra[2] = (uint8_t)v[10].x;
+                    rb[2] = (uint8_t)v[10].y;
+                }
+                *reinterpret_cast<uint16_t*>(ra - 2) = (uint16_t)u6;
+                *reinterpret_cast<uint16_t*>(rb - 2) = (uint16_t)(u6 >> 16);
+                *reinterpret_cast<uint16_t*>(ra) = (uint16_t)u8;
+                *reinterpret_cast<uint16_t*>(rb) = (uint16_t)(u8 >> 16);
             }
         }
         return;
@@ -213,18 +310,20 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
         const bool need = (r >= 4 && r < 12) || wide;
         d[r] = need ? *reinterpret_cast<const uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) : 0u;
     }
+    // columns (0, 1) and (2, 3) filtered as pairs
+    lf2 lo[16], hi[16];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        int v[16];
-#pragma unroll
-        for (int r = 0; r < 16; r++) v[r] = (d[r] >> (8 * j)) & 0xff;
-        lf_filter(v + 8, 1, plane, e.limit, e.blimit, e.thresh, e.filterSize);
-#pragma unroll
-        for (int r = 2; r < 14; r++) d[r] = (d[r] & ~(0xffu << (8 * j))) | ((uint32_t)(v[r] & 0xff) << (8 * j));
+    for (int r = 0; r < 16; r++) {
+        lo[r] = __builtin_bit_cast(lf2, __builtin_amdgcn_perm(0u, d[r], 0x0c010c00u));
+        hi[r] = __builtin_bit_cast(lf2, __builtin_amdgcn_perm(0u, d[r], 0x0c030c02u));
     }
+    lf_filter2(lo + 8, plane, e.limit, e.blimit, e.thresh, e.filterSize);
+    lf_filter2(hi + 8, plane, e.limit, e.blimit, e.thresh, e.filterSize);
 #pragma unroll
     for (int r = 2; r < 14; r++)
-        if (r >= 8 - n && r < 8 + n) *reinterpret_cast<uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) = d[r];
+        if (r >= 8 - n && r < 8 + n)
+            *reinterpret_cast<uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) =
+                __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u);
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
@@ -651,6 +750,18 @@ DEV int lr_src(const LrPix& S, int x, int y)
     return base[(size_t)y * stride + x];
 }
 
+// Four values in 0..255 as the bytes of a dword, through v_perm: written as shifts and ORs,
+// hipcc (ROCm 7.2) folds the clamp, shift and byte packing of two of them into
+// v_ashr_pk_u8_i32, which on gfx950 leaves the destination's upper half as it was while the
+// compiler assumes it zero -- bytes 2 of the packed dword came out ORed with stale bits
+// (measured: the loop-restoration output wrong at every x % 4 == 2 pixel).
+DEV uint32_t pack_u8x4(int a, int b, int c, int d)
+{
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x0c0c0400u);  // {a, b, 0, 0}
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)d, (uint32_t)c, 0x0c0c0400u);  // {c, d, 0, 0}
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
 // Tiles of LR_TW columns x one half-stripe (luma) / one stripe (chroma) rows: inside a
 // tile the stripe (hence get_source_sample's row mapping) and the restoration-unit row are
 // fixed, so the source is staged once in LDS with its 3-pixel halo and every filter reads
@@ -850,17 +961,16 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
                 const int vf3 = 128 - 2 * (g0 + g1 + g2);
                 int hv[7][4];
 #pragma unroll
-                for (int k = 0; k < 7; k++) {
-                    const uint2 d = *reinterpret_cast<const uint2*>(&L.hw[r + k][c0]);
-                    hv[k][0] = (int16_t)(d.x & 0xffff), hv[k][1] = (int16_t)(d.x >> 16);
-                    hv[k][2] = (int16_t)(d.y & 0xffff), hv[k][3] = (int16_t)(d.y >> 16);
-                }
-                ow = 0;
+                for (int k = 0; k < 7; k++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) hv[k][j] = L.hw[r + k][c0 + j];
+                int o[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int sum = g0 * (hv[0][j] + hv[6][j]) + g1 * (hv[1][j] + hv[5][j]) + g2 * (hv[2][j] + hv[4][j]) + vf3 * hv[3][j];
-                    ow |= (uint32_t)clip1(r2(sum, 11)) << (8 * j);
+                    o[j] = clip1(r2(sum, 11));
                 }
+                ow = pack_u8x4(o[0], o[1], o[2], o[3]);
             } else if (filt) {
                 // selfGuidedFilter (LoopRestoration.cpp:420-479)
                 const int set = u.sgr_set;
@@ -912,9 +1022,7 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
 #pragma unroll
                     for (int j = 0; j < 4; j++) v[j] += w * r2(a[j] * px4[j] + b[j], 8 + shift - 4);
                 }
-                ow = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) ow |= (uint32_t)clip1(r2(v[j], 4 + 7)) << (8 * j);
+                ow = pack_u8x4(clip1(r2(v[0], 4 + 7)), clip1(r2(v[1], 4 + 7)), clip1(r2(v[2], 4 + 7)), clip1(r2(v[3], 4 + 7)));
             }
             uint8_t* dst = O.p + (size_t)y * O.stride + x;
             if (c0 + 4 <= tw) *reinterpret_cast<uint32_t*>(dst) = ow;
