@@ -917,11 +917,15 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         }
     };
     auto end_node = [&]() {  // closes the node's dependency list; returns its id
-        std::sort(dl.begin(), dl.end());
-        dl.erase(std::unique(dl.begin(), dl.end()), dl.end());
-        c->nodeDeps.insert(c->nodeDeps.end(), dl.begin(), dl.end());
+        if (dl.size() > 1) {
+            std::sort(dl.begin(), dl.end());
+            dl.erase(std::unique(dl.begin(), dl.end()), dl.end());
+        }
+        if (!dl.empty()) c->nodeDeps.insert(c->nodeDeps.end(), dl.begin(), dl.end());
         dl.clear();
-        c->nodeMask.insert(c->nodeMask.end(), nm, nm + 12);
+        const size_t nmo = c->nodeMask.size();
+        c->nodeMask.resize(nmo + 12);
+        memcpy(c->nodeMask.data() + nmo, nm, sizeof(nm));
         memset(nm, 0, sizeof(nm));
         c->nodeDepStart.push_back((uint32_t)c->nodeDeps.size());
         return (int32_t)c->nodeDepStart.size() - 2;
@@ -1060,6 +1064,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                     own_set(p, blk.mi_col >> sub, blk.mi_row >> sub, av1r_num4x4w[psz], av1r_num4x4h[psz], iiNode);
                 }
         }
+        // (flowOnly: an inter block's transform blocks get no node, item or level -- k_resid
+        // adds their residuals before k_flow)
+        if (inter && flowOnly) continue;
         int lumaMax = -1;  // CFL reads this block's reconstructed luma
         for (uint32_t ti = blk.first_tb; ti < blk.first_tb + blk.n_tbs; ti++) {
             const av1r_tb& t = b->tbs[ti];
