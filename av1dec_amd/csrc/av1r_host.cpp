@@ -602,6 +602,8 @@ static bool inter_split()
     static const bool on = getenv("AV1R_INTER_SPLIT") && atoi(getenv("AV1R_INTER_SPLIT")) != 0;
     return on;
 }
+// k_flow's small items served per wave (av1r_set_flow_wave; AV1R_FLOW_WAVE)
+static std::atomic<int> g_flowWave{getenv("AV1R_FLOW_WAVE") ? atoi(getenv("AV1R_FLOW_WAVE")) : 0};
 static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) : 1};
 static std::atomic<int> g_fusedFilters{getenv("AV1R_FUSED") ? atoi(getenv("AV1R_FUSED")) : 0};
 
@@ -1617,7 +1619,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // others (deep frames, build_strips)
     // AV1R_FLOW_WAVE=1: small items as single entries after the groups, served per wave
     // (recon.hip, flow_small_wave); nGroups then counts the large items only
-    static const bool waveItems = getenv("AV1R_FLOW_WAVE") && atoi(getenv("AV1R_FLOW_WAVE")) != 0;
+    const bool waveItems = g_flowWave.load(std::memory_order_relaxed) != 0;
     size_t nGroups = 0, nSmallItems = 0, nStripG = 0, nStripS = 0;
     for (auto& j : jobs) {
         if (flow && !j.P->stripGroups.empty()) {
@@ -2920,6 +2922,8 @@ int av1r_set_strip_levels(int levels) { return g_stripLevels.exchange(levels < 0
 int av1r_set_filter_fusion(int on) { return g_fusedFilters.exchange(on ? 1 : 0); }
 
 int av1r_set_fast_intra(int on) { return g_fastIntra.exchange(on ? 1 : 0); }
+
+int av1r_set_flow_wave(int on) { return g_flowWave.exchange(on ? 1 : 0); }
 
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream)
 {

@@ -348,6 +348,11 @@ int av1r_set_filter_fusion(int on);
  * (default; environment AV1R_FI), 0 = the generic one.  Both are bit-exact (A/B).  Returns
  * the previous value. */
 int av1r_set_fast_intra(int on);
+/* Process-wide: 1 = the small items of k_flow launches from now on are served one per wave
+ * from their own queues (no group lock-step; recon.hip flow_small_wave), 0 = in groups of
+ * four per workgroup (default; environment AV1R_FLOW_WAVE).  Both are bit-exact.  Returns the
+ * previous value. */
+int av1r_set_flow_wave(int on);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);

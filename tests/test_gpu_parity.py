@@ -91,6 +91,22 @@ def test_gpu_fused_filters_match_reference(stream, fused_filters):
     assert got == out_md5 == BITS[stream]
 
 
+@pytest.fixture
+def flow_wave(native_lib):
+    prev = native_lib.av1r_set_flow_wave(1)
+    yield
+    native_lib.av1r_set_flow_wave(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", AB_STREAMS)
+def test_gpu_flow_wave_matches_reference(stream, flow_wave):
+    # k_flow's small items served per wave (av1r_set_flow_wave): every stage of every frame
+    bad, got, out_md5 = run_stream(stream)
+    assert not bad, bad[:3]
+    assert got == out_md5 == BITS[stream]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream", STREAMS)
 def test_gpu_level_schedule_matches_reference(stream):
