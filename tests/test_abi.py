@@ -250,3 +250,25 @@ def test_validation_palette_window_keyed_on_the_tbs_own_block(native_lib):
     bad = batchfile.Frame(secs)
     assert native_lib.av1r_check_batch(C.cast(bad.byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_INVALID
     assert b"palette map window" in err.value
+
+
+def test_shipped_code_has_no_ashr_pk_u8(tmp_path):
+    """Regression guard: hipcc (ROCm 7.2) folded a clamp + byte packing into
+    v_ashr_pk_u8_i32, whose destination's upper half gfx950 leaves as it was while the compiler
+    assumed it zero -- loop restoration came out wrong at every x % 4 == 2 pixel.  No gfx950
+    code object of libav1r.so may contain that instruction."""
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        import pytest
+        pytest.skip("llvm-objdump not present")
+    lib = tmp_path / "libav1r.so"
+    shutil.copy(native.LIB, lib)
+    subprocess.run([objdump, "--offloading", str(lib)], cwd=tmp_path, capture_output=True, check=True, timeout=120)
+    objs = sorted(p for p in tmp_path.iterdir() if p.name.endswith("gfx950"))
+    assert objs, "no gfx950 code object in libav1r.so"
+    for o in objs:
+        dis = subprocess.run([objdump, "-d", str(o)], capture_output=True, text=True, check=True, timeout=300).stdout
+        assert "k_flow" in dis or "k_lr" in dis or "k_inter" in dis
+        assert "v_ashr_pk_u8" not in dis, o.name
