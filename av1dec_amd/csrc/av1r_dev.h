@@ -182,6 +182,9 @@ DEV uint32_t flow_spin_limit(const uint32_t* ctl)
 
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
 DEV int clip1(int v) { return CLIP3(0, 255, v); }
+// log2 of a power of two (block, tile, prediction-unit and transform sides): the per-lane
+// loops over a w-wide region index rows by shifts, not by an integer division (~12 VALU ops)
+DEV int ilog2p(int x) { return 31 - __builtin_clz((unsigned)x); }
 DEV int r2(int x, int n) { return n == 0 ? x : ((x + (1 << (n - 1))) >> n); }
 DEV int r2s(int x, int n) { return x >= 0 ? r2(x, n) : -r2(-x, n); }
 DEV int64_t r2_64(int64_t x, int n) { return n == 0 ? x : ((x + ((int64_t)1 << (n - 1))) >> n); }

@@ -555,9 +555,9 @@ template <int NT = 64>
 DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0, int wcs = WC, int hstr = TS)
 {
     if ((rw & 3) == 0) {
-        const int g4 = rw >> 2;
+        const int g4 = rw >> 2, lg = ilog2p(g4);  // (rw: a power of two)
         for (int q = il_lane<NT>(); q < (rh + 7) * g4; q += NT) {
-            const int i = q / g4, g = q - i * g4;
+            const int i = q >> lg, g = q & (g4 - 1);
             const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + i * wcs) + g;
             const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2];
             int b[12];
@@ -926,9 +926,9 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, 
     };
     if ((rw & 3) == 0 && R[0].useWin && (!isCompound || R[1].useWin)) {
         // four adjacent samples per lane (window references only)
-        const int g4 = rw >> 2;
+        const int g4 = rw >> 2, lg = ilog2p(g4);  // (rw: a power of two)
         for (int q = t; q < rh * g4; q += NT) {
-            const int rr = q / g4, cc = (q - rr * g4) * 4;
+            const int rr = q >> lg, cc = (q & (g4 - 1)) * 4;
             int p0[4], p1[4] = {0, 0, 0, 0};
             pred_win4(L.win[0], L.u.hbw[0], rr, cc, R0, R1, vf[0], integer[0], p0, L.WCS, TSZ);
             if (isCompound) pred_win4(L.win[1], L.u.hbw[1], rr, cc, R0, R1, vf[1], integer[1], p1, L.WCS, TSZ);
@@ -943,8 +943,9 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, 
             }
         }
     } else {
+        const int lw = ilog2p(rw);
         for (int q = t; q < rw * rh; q += NT) {
-            const int rr = q / rw, cc = q - rr * rw;
+            const int rr = q >> lw, cc = q & (rw - 1);
             blend(sample(0, rr, cc), isCompound ? sample(1, rr, cc) : 0, ry0 + rr, rx0 + cc);
         }
     }
@@ -1113,8 +1114,9 @@ DEV void obmc(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int pl
                         if (!integer) hpass<NT>(L.win[0], L.u.hbw[0], rw, rh, hf, 3, L.WCS, TSZ);
                         il_sync<NT>();
                     }
+                    const int lw = ilog2p(rw);
                     for (int q = t; q < rw * rh; q += NT) {
-                        const int rr = q / rw, cc = q - rr * rw, i = ry0 + rr, j = rx0 + cc;
+                        const int rr = q >> lw, cc = q & (rw - 1), i = ry0 + rr, j = rx0 + cc;
                         int p = R.useWin ? pred_win(L.win[0], L.u.hbw[0], rr, cc, 3, 11, vf, integer, L.WCS, TSZ)
                                          : pred_direct(R, i, j, 3, 11);
                         int m = pass ? mask[j] : mask[i];
@@ -1192,10 +1194,13 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
             if (plane == 1 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col &&
                 blk.motion_mode != AV1R_OBMC_CAUSAL && !(G.TW & 3) &&
                 predict_chroma2(k, blk, L, G.baseX, G.baseY, G.pw, G.ph, G.TX0, G.TY0, G.TW, G.TH, lw)) {
-                for (int q = t; q < 2 * G.TW * G.TH; q += NT) {
-                    const int p = q >= G.TW * G.TH, e = q - p * G.TW * G.TH;
-                    const int i = e / G.TW, j = e - i * G.TW;
-                    px(k.cur.pl[1 + p], G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[p * C2_TILE + i * TS + j];
+                // (G.TW a multiple of 4: a dword per lane and row quad; x, TX0 multiples of 4)
+                const int lq = ilog2p(G.TW >> 2), nq = (G.TW * G.TH) >> 2;
+                for (int q = t; q < 2 * nq; q += NT) {
+                    const int p = q >= nq, e = q - p * nq;
+                    const int i = e >> lq, j = (e & ((G.TW >> 2) - 1)) * 4;
+                    *reinterpret_cast<uint32_t*>(&px(k.cur.pl[1 + p], G.baseX + G.TX0 + j, G.baseY + G.TY0 + i)) =
+                        *reinterpret_cast<const uint32_t*>(&L.tile[p * C2_TILE + i * TS + j]);
                 }
                 il_sync<NT>();
                 trace_stamp(tr, 9);
@@ -1222,9 +1227,19 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
         if (blk.motion_mode == AV1R_OBMC_CAUSAL)
             obmc<NT, TSZ>(k, blk, L, plane, G.baseX, G.baseY, G.predW, G.predH, G.TX0, G.TY0, G.TW, G.TH);
         const DevPlane& dst = k.cur.pl[plane];
-        for (int q = t; q < G.TW * G.TH; q += NT) {
-            int i = q / G.TW, j = q - i * G.TW;
-            px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[i * TSZ + j];
+        if (!(G.TW & 3)) {  // a dword per lane and row quad (x, TX0 multiples of 4)
+            const int lq = ilog2p(G.TW >> 2);
+            for (int q = t; q < (G.TW * G.TH) >> 2; q += NT) {
+                const int i = q >> lq, j = (q & ((G.TW >> 2) - 1)) * 4;
+                *reinterpret_cast<uint32_t*>(&px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i)) =
+                    *reinterpret_cast<const uint32_t*>(&L.tile[i * TSZ + j]);
+            }
+        } else {
+            const int lw = ilog2p(G.TW);
+            for (int q = t; q < G.TW * G.TH; q += NT) {
+                const int i = q >> lw, j = q & (G.TW - 1);
+                px(dst, G.baseX + G.TX0 + j, G.baseY + G.TY0 + i) = L.tile[i * TSZ + j];
+            }
         }
         il_sync<NT>();
         trace_stamp(tr, 8 + plane);
@@ -1286,8 +1301,9 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
         }
         const int sizeScale = 128 / imax(ph, pw);
         const bool addRes = COH;  // k_flow: the block's residuals are added here (tiles)
+        const int lpw = ilog2p(pw);
         for (int q = t; q < pw * ph; q += NT) {
-            const int i = q / pw, j = q - i * pw;
+            const int i = q >> lpw, j = q & (pw - 1);
             int m;
             if (!isWedge) {
                 m = im == AV1R_II_V_PRED ? av1r_ii_weights_1d[i * sizeScale]
@@ -1321,8 +1337,9 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
                 if (tb.plane != plane || !tb.coef_cnt) continue;
                 const int tw = av1r_tx_w[tb.tx_size], th = av1r_tx_h[tb.tx_size];
                 const int16_t* rt = k.res + k.tb_res[ti];
+                const int ltw = ilog2p(tw);
                 for (int q = t; q < tw * th; q += NT) {
-                    const int i = q / tw, j = q - i * tw;
+                    const int i = q >> ltw, j = q & (tw - 1);
                     uint8_t& v = L.pred[(tb.y - baseY + i) * 64 + tb.x - baseX + j];
                     v = (uint8_t)clip1(v + rt[q]);
                 }
@@ -1330,7 +1347,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
             }
             const bool coh = COH && !strip_plain(k.strip, gran);
             for (int q = t; q < pw * ph; q += NT) {
-                const int i = q / pw, j = q - i * pw;
+                const int i = q >> lpw, j = q & (pw - 1);
                 stp_c(dst, baseX + j, baseY + i, L.pred[i * 64 + j], coh);
             }
             if (COH && gran)
@@ -1446,7 +1463,7 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const
 extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint32_t* __restrict__ tab, int n,
     unsigned long long* trace, uint32_t traceBase)
 {
-    __shared__ InterLds L;
+    __shared__ __align__(16) InterLds L;
     const unsigned long long tEntry = trace ? trace_now() : 0;
     const KParams* kp;
     int s;
@@ -1530,9 +1547,9 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int 
     };
     const DevPlane& dst = k.cur.pl[plane];
     if (!(w & 3)) {
-        const int g4 = w >> 2;
+        const int g4 = w >> 2, lg = ilog2p(g4);  // (w: a power of two)
         for (int q = t; q < h * g4; q += NT) {
-            const int rr = q / g4, cc = (q - rr * g4) * 4;
+            const int rr = q >> lg, cc = (q & (g4 - 1)) * 4;
             int p0[4], p1[4] = {0, 0, 0, 0};
             pred_win4(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], p0, MS + 8, MS);
             if (isCompound) pred_win4(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], p1, MS + 8, MS);
@@ -1542,8 +1559,9 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int 
             *reinterpret_cast<uint32_t*>(&px(dst, x + cc, y + rr)) = v;  // x, cc: multiples of 4
         }
     } else {
+        const int lw = ilog2p(w);
         for (int q = t; q < h * w; q += NT) {
-            const int rr = q / w, cc = q - rr * w;
+            const int rr = q >> lw, cc = q & (w - 1);
             const int p0 = pred_win(L.win[0], L.hb[0], rr, cc, 3, R1, vf[0], integer[0], MS + 8, MS);
             const int p1 = isCompound ? pred_win(L.win[1], L.hb[1], rr, cc, 3, R1, vf[1], integer[1], MS + 8, MS) : 0;
             px(dst, x + cc, y + rr) = (uint8_t)blend(p0, p1);
