@@ -1066,9 +1066,16 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
     const int tw = imin(LR_TW, C.w - x0), th = ty1 - ty0;
     const av1r_frame_hdr& h = *k.hdr;
     if (h.lr_type[plane] == AV1R_RESTORE_NONE) {
-        for (int q = t; q < tw * th; q += 256) {
-            int r = q / tw, c = q - r * tw;
-            O.p[(size_t)(ty0 + r) * O.stride + x0 + c] = C.p[(size_t)(ty0 + r) * C.stride + x0 + c];
+        // the CDEF frame copied: a dword per lane (x0 a multiple of 64, strides of 256), the
+        // plane's last 1-3 columns (odd chroma widths) by bytes
+        const int ng = (tw + 3) >> 2;
+        for (int q = t; q < ng * th; q += 256) {
+            const int r = q / ng, c = 4 * (q - r * ng);
+            const uint8_t* sp = C.p + (size_t)(ty0 + r) * C.stride + x0 + c;
+            uint8_t* dp = O.p + (size_t)(ty0 + r) * O.stride + x0 + c;
+            if (c + 4 <= tw) *reinterpret_cast<uint32_t*>(dp) = *reinterpret_cast<const uint32_t*>(sp);
+            else
+                for (int j = 0; j < tw - c; j++) dp[j] = sp[j];
         }
         return;
     }
@@ -1468,9 +1475,9 @@ extern "C" __global__ __launch_bounds__(256) void k_mi_blocks(const KParams* kps
     m.uv_mode = b.uv_mode;
     uint32_t w[6];
     memcpy(w, &m, sizeof(w));
-    const int bw4 = av1r_num4x4w[b.mi_size], bh4 = av1r_num4x4h[b.mi_size], n = bw4 * bh4;
+    const int bw4 = av1r_num4x4w[b.mi_size], bh4 = av1r_num4x4h[b.mi_size], n = bw4 * bh4, lb = ilog2p(bw4);
     for (int q = threadIdx.x & 15; q < n; q += 16) {
-        const int r = b.mi_row + q / bw4, c = b.mi_col + q % bw4;
+        const int r = b.mi_row + (q >> lb), c = b.mi_col + (q & (bw4 - 1));
         uint32_t* d = reinterpret_cast<uint32_t*>(const_cast<av1r_mi*>(k.mi) + (size_t)r * k.mi_stride + c);
 #pragma unroll
         for (int i = 0; i < 6; i++) d[i] = w[i];

@@ -80,7 +80,7 @@ DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int1
     const int txSz = tb.tx_size;
     const int w = av1r_tx_w[txSz], h = av1r_tx_h[txSz];
     const int log2W = av1r_tx_w_log2[txSz], log2H = av1r_tx_h_log2[txSz];
-    const int tw = imin(w, 32), th = imin(h, 32);
+    const int tw = imin(w, 32), th = imin(h, 32), ltw = imin(log2W, 5);
     const av1r_frame_hdr& hd = *k.hdr;
     for (int q = t; q < th * w; q += NT) res[(q >> log2W) * RS + (q & (w - 1))] = 0;
     coop_sync<NT>();
@@ -101,7 +101,7 @@ DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int1
         int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
         int sign = d < 0 ? -1 : 1;
         int d2 = sign * (iabs(d) & 0xffffff) / dqDenom;
-        res[(pos / tw) * RS + (pos % tw)] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
+        res[(pos >> ltw) * RS + (pos & (tw - 1))] = (int16_t)CLIP3(-(1 << 15), (1 << 15) - 1, d2);
     }
     coop_sync<NT>();
     const int lossless = (blk.flags & AV1R_BLK_LOSSLESS) != 0;
