@@ -557,15 +557,18 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
     const int rows4 = imin(16, k.mi_rows - r0), cols4 = imin(16, k.mi_cols - c0);
     const int x0 = c0 * 4, y0 = r0 * 4;
     if (idx == -1) {
-        // not filtered: the output is the input (the reference filters into a copy)
-        for (int q = t; q < rows4 * 4 * cols4 * 4; q += 256) {
-            int i = q / (cols4 * 4), j = q - i * (cols4 * 4);
-            px(k.cdef.pl[0], x0 + j, y0 + i) = px(k.cur.pl[0], x0 + j, y0 + i);
+        // not filtered: the output is the input (the reference filters into a copy), luma as
+        // dwords (cols4 * 4 is a multiple of 4), chroma as 16-bit pairs (cols4 * 2 is even)
+        const int nl = cols4, nc = cols4;  // dwords per luma row, 16-bit pairs per chroma row
+        for (int q = t; q < rows4 * 4 * nl; q += 256) {
+            const int i = q / nl, j = 4 * (q - i * nl);
+            *reinterpret_cast<uint32_t*>(&px(k.cdef.pl[0], x0 + j, y0 + i)) = *reinterpret_cast<const uint32_t*>(&px(k.cur.pl[0], x0 + j, y0 + i));
         }
-        for (int q = t; q < 2 * rows4 * 2 * cols4 * 2; q += 256) {
-            int pl = 1 + (q >= rows4 * 2 * cols4 * 2), e = q - (pl - 1) * rows4 * 2 * cols4 * 2;
-            int i = e / (cols4 * 2), j = e - i * (cols4 * 2);
-            px(k.cdef.pl[pl], x0 / 2 + j, y0 / 2 + i) = px(k.cur.pl[pl], x0 / 2 + j, y0 / 2 + i);
+        for (int q = t; q < 2 * rows4 * 2 * nc; q += 256) {
+            const int pl = 1 + (q >= rows4 * 2 * nc), e = q - (pl - 1) * rows4 * 2 * nc;
+            const int i = e / nc, j = 2 * (e - i * nc);
+            *reinterpret_cast<uint16_t*>(&px(k.cdef.pl[pl], x0 / 2 + j, y0 / 2 + i)) =
+                *reinterpret_cast<const uint16_t*>(&px(k.cur.pl[pl], x0 / 2 + j, y0 / 2 + i));
         }
         return;
     }
