@@ -2715,12 +2715,25 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
     return AV1R_OK;
 }
 
+static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
+                         av1r_output_ticket** out);
+
 int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
                           av1r_output_ticket** out)
 {
     if (!c || !out || !y || !u || !v) return AV1R_E_INVALID;
     *out = nullptr;
+    // (the staged frames are older than the queued ones: they must leave first, through
+    // av1r_get_output)
     if (!c->staged.empty()) return fail(c, AV1R_E_INVALID, "frames already staged by av1r_set_output_prefetch: use av1r_get_output");
+    return output_ticket(c, y, ys, u, us, v, vs, width, height, out);
+}
+
+// the oldest queued frame into a ticket (av1r_get_output_async; stage_outputs)
+static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
+                         av1r_output_ticket** out)
+{
+    *out = nullptr;
     if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
     (void)hipSetDevice(c->device);
     if (!c->outStream) HIPCHK(hipStreamCreateWithFlags(&c->outStream, hipStreamNonBlocking));
@@ -2841,7 +2854,7 @@ static int stage_outputs(av1r_ctx* c)
             S.cap = need;
         }
         uint8_t* u = S.buf + (size_t)w * h;
-        int rc = av1r_get_output_async(c, S.buf, w, u, cw, u + (size_t)cw * ch, cw, nullptr, nullptr, &S.t);
+        int rc = output_ticket(c, S.buf, w, u, cw, u + (size_t)cw * ch, cw, nullptr, nullptr, &S.t);
         if (!rc && hipStreamWaitEvent(c->outStream, S.t->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
         if (!rc) rc = ticket_issue(S.t);
         if (rc) {
