@@ -2774,7 +2774,9 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
 static int ticket_issue(av1r_output_ticket* t)
 {
     av1r_ctx* c = t->c;
-    for (int p = 0; p < 3; p++) {
+    // AV1R_OUT_NOCOPY=1 (A/B of the delivery machinery alone): no bytes move
+    static const bool noCopy = getenv("AV1R_OUT_NOCOPY") && atoi(getenv("AV1R_OUT_NOCOPY")) != 0;
+    for (int p = 0; p < 3 && !noCopy; p++) {
         const DevPlane& P = t->f->d.pl[p];
         HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], P.p, P.stride, P.w, P.h, hipMemcpyDeviceToHost, c->outStream));
     }
