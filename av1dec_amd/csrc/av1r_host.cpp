@@ -37,6 +37,8 @@ void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_post(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
+void launch_k_out(const uint8_t* const src[3], const int ss[3], uint8_t* const dst[3], const int ds[3], const int w[3],
+                  const int h[3], hipStream_t st);
 void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s);
 #ifdef AV1R_FLOW_DEBUG
 uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset);
@@ -1663,10 +1665,11 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         }
         *rec->err = 0;
     }
-    if (M.cap < need) {
+    if (M.cap < need) {  // (rare: the frees stall the device; sizes are powers of two, >= 1 MiB)
         if (M.host) (void)hipHostFree(M.host);
         if (M.dev) (void)hipFree(M.dev);
-        size_t cap = need + need / 2 + 4096;
+        size_t cap = (size_t)1 << 20;
+        while (cap < need) cap <<= 1;
         HIPCHK(hipHostMalloc(&M.host, cap));
         HIPCHK(hipMalloc(&M.dev, cap));
         M.cap = cap;
@@ -2399,59 +2402,88 @@ static thread_local av1r_ctx t_packScratch;
 
 const char* av1r_pack_last_error(void) { return t_packScratch.err.c_str(); }
 
+// A pooled buffer for a frame of `need` bytes (0: a show-existing entry, no buffer): the
+// oldest released one that fits whose upload has completed, else the oldest that fits (its
+// upload waited for), else a new one.  Buffers are never freed while the pool is in use --
+// hipHostFree / hipHostMalloc cost milliseconds and stall the device and every other
+// thread's HIP calls -- and grow in whole MiB with a quarter's margin, so a running pipeline
+// stops allocating after its first GOPs.
+static av1r_packed* pack_buffer(size_t need)
+{
+    av1r_packed* pk = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_packMu);
+        size_t pick = SIZE_MAX;
+        for (size_t i = 0; i < g_packFree.size(); i++) {
+            av1r_packed* q = g_packFree[i];
+            if (q->cap < need) continue;
+            if (pick == SIZE_MAX) pick = i;
+            if (!q->copyPending || hipEventQuery(q->copied) == hipSuccess) {
+                q->copyPending = false;
+                pick = i;
+                break;
+            }
+        }
+        if (pick != SIZE_MAX) {
+            pk = g_packFree[pick];
+            g_packFree.erase(g_packFree.begin() + pick);
+        }
+    }
+    if (pk) {
+        if (pk->copyPending) {  // its previous upload may still read the host buffer
+            (void)hipEventSynchronize(pk->copied);
+            pk->copyPending = false;
+        }
+        return pk;
+    }
+    pk = new (std::nothrow) av1r_packed;
+    if (!pk || !need) return pk;
+    const size_t cap = (need + need / 4 + (1u << 20)) & ~(size_t)((1u << 20) - 1);
+    pk->pinned = hipHostMalloc(&pk->host, cap, hipHostMallocDefault) == hipSuccess;
+    if (!pk->pinned) pk->host = static_cast<uint8_t*>(malloc(cap));  // no device here (host-only use)
+    if (!pk->host) {
+        delete pk;
+        return nullptr;
+    }
+    pk->cap = cap;
+    return pk;
+}
+
 int av1r_pack(const av1r_frame_batch* b, av1r_packed** out)
 {
     if (!b || !b->hdr || !out) return AV1R_E_INVALID;
     *out = nullptr;
     av1r_ctx* c = &t_packScratch;  // per-thread schedule scratch: av1r_pack is thread-safe
     if (b->hdr->version != AV1R_VERSION) return fail(c, AV1R_E_INVALID, "batch version %u", b->hdr->version);
-    av1r_packed* pk = nullptr;
-    {
-        std::lock_guard<std::mutex> lock(g_packMu);
-        if (!g_packFree.empty()) {
-            pk = g_packFree.back();
-            g_packFree.pop_back();
-        }
+    if (b->hdr->show_existing_frame) {
+        av1r_packed* pk = pack_buffer(0);
+        if (!pk) return AV1R_E_NOMEM;
+        pk->P = Prepared();
+        pk->P.hdr = *b->hdr;
+        *out = pk;
+        return AV1R_OK;
     }
-    if (!pk) pk = new av1r_packed;
-    if (pk->copyPending) {  // its previous upload may still read the host buffer
-        (void)hipEventSynchronize(pk->copied);
-        pk->copyPending = false;
-    }
+    c->skipSlotCheck = true;
+    PackClock clk;
+    int rc = validate(c, b);
+    clk.lap(PP_VALIDATE);
+    c->skipSlotCheck = false;
+    if (rc) return rc;
+    build_schedule(c, b, true, true);
+    clk = PackClock();
+    Prepared tmp;
+    size_t need = 0;
+    pack_frame(c, b, tmp, nullptr, nullptr, &need);  // the size only (P untouched)
+    av1r_packed* pk = pack_buffer(need);
+    if (!pk) return AV1R_E_NOMEM;
     Prepared& P = pk->P;
     P = Prepared();
     P.hdr = *b->hdr;
-    if (!b->hdr->show_existing_frame) {
-        c->skipSlotCheck = true;
-        PackClock clk;
-        int rc = validate(c, b);
-        clk.lap(PP_VALIDATE);
-        c->skipSlotCheck = false;
-        if (rc) {
-            av1r_packed_free(pk);
-            return rc;
-        }
-        build_schedule(c, b, true, true);
-        clk = PackClock();
-        size_t need = 0;
-        pack_frame(c, b, P, nullptr, nullptr, &need);
-        if (pk->cap < need) {
-            if (pk->host) pk->pinned ? (void)hipHostFree(pk->host) : free(pk->host);
-            const size_t cap = need + need / 4 + 65536;
-            pk->pinned = hipHostMalloc(&pk->host, cap, hipHostMallocDefault) == hipSuccess;
-            if (!pk->pinned) pk->host = static_cast<uint8_t*>(malloc(cap));  // no device here (host-only use)
-            pk->cap = pk->host ? cap : 0;
-            if (!pk->host) {
-                delete pk;
-                return AV1R_E_NOMEM;
-            }
-        }
-        pack_frame(c, b, P, pk->host, nullptr, &need);
-        clk.lap(PP_COPY);
-        if (g_packProf) g_packNs[PP_N]++;
-        P.cap = need;
-        P.offsets = true;
-    }
+    pack_frame(c, b, P, pk->host, nullptr, &need);
+    clk.lap(PP_COPY);
+    if (g_packProf) g_packNs[PP_N]++;
+    P.cap = need;
+    P.offsets = true;
     *out = pk;
     return AV1R_OK;
 }
@@ -2566,7 +2598,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         }
         if (U.cap < pk->P.cap) {
             if (U.dev) (void)hipFree(U.dev);
-            U.cap = pk->P.cap + pk->P.cap / 4 + 65536;
+            U.cap = (pk->P.cap + pk->P.cap / 4 + (1u << 20)) & ~(size_t)((1u << 20) - 1);
             HIPCHK(hipMalloc(&U.dev, U.cap));
         }
         HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.upBytes, hipMemcpyHostToDevice, up->copyStream));
@@ -2717,6 +2749,7 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
 
 static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
                          av1r_output_ticket** out);
+static int ticket_issue(av1r_output_ticket* t);
 
 int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
                           av1r_output_ticket** out)
@@ -2726,7 +2759,15 @@ int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, u
     // (the staged frames are older than the queued ones: they must leave first, through
     // av1r_get_output)
     if (!c->staged.empty()) return fail(c, AV1R_E_INVALID, "frames already staged by av1r_set_output_prefetch: use av1r_get_output");
-    return output_ticket(c, y, ys, u, us, v, vs, width, height, out);
+    int rc = output_ticket(c, y, ys, u, us, v, vs, width, height, out);
+    // AV1R_OUT_EAGER=1 (A/B): the copies are queued at once behind a device-side wait for
+    // the frame instead of when the host sees it done
+    static const bool eager = getenv("AV1R_OUT_EAGER") && atoi(getenv("AV1R_OUT_EAGER")) != 0;
+    if (!rc && eager) {
+        if (hipStreamWaitEvent(c->outStream, (*out)->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
+        if (!rc) rc = ticket_issue(*out);
+    }
+    return rc;
 }
 
 // the oldest queued frame into a ticket (av1r_get_output_async; stage_outputs)
@@ -2757,7 +2798,8 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     FrameBuf* f = c->outq.front();
     // the frame's last writer: this context's own stream, or the stream of the batch it was
     // last launched in (ctx_join is not needed: nothing is enqueued on the context here)
-    HIPCHK(hipEventRecord(t->ready, c->joinLead ? c->joinLead->stream : c->stream));
+    static const bool noReady = getenv("AV1R_OUT_NOREADY") && atoi(getenv("AV1R_OUT_NOREADY")) != 0;  // (A/B with NOCOPY)
+    if (!noReady) HIPCHK(hipEventRecord(t->ready, c->joinLead ? c->joinLead->stream : c->stream));
     c->outq.pop_front();  // the queue's reference passes to the ticket
     t->c = c;
     t->f = f;
@@ -2771,14 +2813,38 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     return AV1R_OK;
 }
 
+// whether the device can store to `p` directly: pinned host memory mapped at the same
+// address (hipHostMalloc; hipHostRegister'd memory under another device address is not)
+static bool device_writable_host(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the error for later launch checks
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer == p;
+}
+
 static int ticket_issue(av1r_output_ticket* t)
 {
     av1r_ctx* c = t->c;
     // AV1R_OUT_NOCOPY=1 (A/B of the delivery machinery alone): no bytes move
     static const bool noCopy = getenv("AV1R_OUT_NOCOPY") && atoi(getenv("AV1R_OUT_NOCOPY")) != 0;
-    for (int p = 0; p < 3 && !noCopy; p++) {
-        const DevPlane& P = t->f->d.pl[p];
-        HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], P.p, P.stride, P.w, P.h, hipMemcpyDeviceToHost, c->outStream));
+    // pinned destinations: k_out on the read-back stream (the copy engine stays free for
+    // the uploads); AV1R_OUT_SDMA=1 (A/B) or other memory: hipMemcpy2DAsync
+    static const bool sdma = getenv("AV1R_OUT_SDMA") && atoi(getenv("AV1R_OUT_SDMA")) != 0;
+    const DevPlane* pl = t->f->d.pl;
+    if (!noCopy && !sdma && device_writable_host(t->dst[0]) && device_writable_host(t->dst[1]) &&
+        device_writable_host(t->dst[2])) {
+        const uint8_t* src[3] = {pl[0].p, pl[1].p, pl[2].p};
+        const int ss[3] = {pl[0].stride, pl[1].stride, pl[2].stride};
+        const int w[3] = {pl[0].w, pl[1].w, pl[2].w}, h[3] = {pl[0].h, pl[1].h, pl[2].h};
+        launch_k_out(src, ss, t->dst, t->ds, w, h, c->outStream);
+        HIPCHK(hipGetLastError());
+    } else {
+        for (int p = 0; p < 3 && !noCopy; p++)
+            HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], pl[p].p, pl[p].stride, pl[p].w, pl[p].h, hipMemcpyDeviceToHost,
+                                    c->outStream));
     }
     HIPCHK(hipEventRecord(t->done, c->outStream));
     t->state = 1;
@@ -2806,6 +2872,19 @@ int av1r_output_query(av1r_output_ticket* t)
     return 1;
 }
 
+int av1r_output_start(av1r_output_ticket* t)
+{
+    if (!t || !t->live) return AV1R_E_INVALID;
+    if (t->state) return 1;
+    av1r_ctx* c = t->c;
+    (void)hipSetDevice(c->device);
+    const hipError_t q = hipEventQuery(t->ready);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output: %s", hipGetErrorString(q));
+    const int rc = ticket_issue(t);
+    return rc ? rc : 1;
+}
+
 int av1r_output_wait(av1r_output_ticket* t)
 {
     if (!t || !t->live) return AV1R_E_INVALID;
@@ -2829,7 +2908,8 @@ int av1r_output_wait(av1r_output_ticket* t)
     t->f = nullptr;
     t->live = false;
     if (rc) return rc;
-    harvest(false);
+    static const bool noHarvest = getenv("AV1R_OUT_NOHARVEST") && atoi(getenv("AV1R_OUT_NOHARVEST")) != 0;  // (A/B)
+    if (!noHarvest) harvest(false);
     std::lock_guard<std::mutex> lock(g_recMu);
     if (frame_failed(c, f->seq)) return fail(c, AV1R_E_DEVICE, "frame %llu: %s", (unsigned long long)f->seq, c->err.c_str());
     return AV1R_OK;

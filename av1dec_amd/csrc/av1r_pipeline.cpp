@@ -243,6 +243,9 @@ struct av1r_pipeline {
     // frame delivery (av1r_pipeline_set_output): per stream the read-backs in flight, in order
     av1r_output_sink sink{};
     std::vector<std::deque<av1r_output_ticket*>> tick;
+    // AV1R_PIPE_PROF=1: pipe_outputs' time (s) polling landed read-backs, blocked on the oldest
+    // (in-flight cap), starting new ones, and draining at the step's end; tickets started
+    double oprof[4] = {}, oissued = 0;
     explicit av1r_pipeline(int n) : R(n), launched(n, 0), ended(n, false), tick(n) {}
 };
 
@@ -300,10 +303,27 @@ int pipe_outputs(av1r_pipeline* P, bool finish, std::string& err)
             }
             return true;
         };
+        auto a0 = Clock::now();
+        auto lap = [&](int k) {
+            const auto a1 = Clock::now();
+            P->oprof[k] += secs(a1 - a0);
+            a0 = a1;
+        };
         while (!T.empty() && deliverFront(false)) {
         }
+        // the read-backs of the later frames whose decode has finished start now too (each
+        // query issues its ticket's copies once the frame is ready; the copies run in order
+        // on the context's read-back stream), so one slow front does not hold them back
+        for (size_t i = 1; i < T.size(); i++)
+            if (av1r_output_start(T[i]) == 0) break;
+        lap(0);
         while (rc == AV1R_OK && av1r_output_pending(c) > 0) {
-            if ((int)T.size() >= AV1R_SINK_INFLIGHT) deliverFront(true);
+            if ((int)T.size() >= AV1R_SINK_INFLIGHT) {
+                lap(2);
+                deliverFront(true);
+                lap(1);
+            }
+            P->oissued++;
             int w = 0, h = 0;
             uint8_t* pl[3] = {};
             int st[3] = {};
@@ -321,7 +341,9 @@ int pipe_outputs(av1r_pipeline* P, bool finish, std::string& err)
             }
             T.push_back(t);
         }
+        lap(2);
         while (finish && !T.empty()) deliverFront(true);
+        lap(3);
     }
     return rc;
 }
@@ -351,10 +373,16 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
         }
     }
     uint64_t nframes = 0, batches = 0;
-    double wait_s = 0, launch_s = 0;
+    double wait_s = 0, launch_s = 0, output_s = 0;
     std::vector<av1r_ctx*> bc;
     std::vector<av1r_packed*> bp;
     std::string err;
+    auto outputs = [&](bool finish) {
+        const auto o0 = Clock::now();
+        const int r = pipe_outputs(P, finish, err);
+        output_s += secs(Clock::now() - o0);
+        return r;
+    };
     const int G = P->G;
     static const double fillUs = getenv("AV1R_PIPE_WAIT_US") ? atof(getenv("AV1R_PIPE_WAIT_US")) : 300.0;
     while (live > 0 && rc == AV1R_OK) {
@@ -431,7 +459,9 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
             }
             nframes += bc.size();
             batches++;
-            if (rc == AV1R_OK) rc = pipe_outputs(P, false, err);
+            // AV1R_OUT_EVERY=k (A/B): the deliveries handled after every k-th launch only
+            static const int outEvery = std::max(1, getenv("AV1R_OUT_EVERY") ? atoi(getenv("AV1R_OUT_EVERY")) : 1);
+            if (rc == AV1R_OK && batches % outEvery == 0) rc = outputs(false);
         } else if (live > 0 && rc == AV1R_OK && P->g == 0) {
             // nothing ready in any group: a worker's push wakes us; a key frame running alone does not,
             // hence the short bound
@@ -440,11 +470,11 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
             R.ready.wait_for(l, std::chrono::microseconds(50));
             wait_s += secs(Clock::now() - w0);
             l.unlock();
-            if (rc == AV1R_OK) rc = pipe_outputs(P, false, err);
+            if (rc == AV1R_OK) rc = outputs(false);
         }
     }
     {  // every frame of the step delivered before it returns
-        const int r = pipe_outputs(P, true, err);
+        const int r = outputs(true);
         if (r && rc == AV1R_OK) rc = r;
     }
     for (int s = 0; s < n; s++) {
@@ -470,8 +500,16 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
         stats->pack_s = pack_s - pack0;
         stats->wait_s = wait_s;
         stats->launch_s = launch_s;
+        stats->output_s = output_s;
     }
     if (rc) fprintf(stderr, "av1r_pipeline: %s\n", err.c_str());
+    static const bool prof = getenv("AV1R_PIPE_PROF") && atoi(getenv("AV1R_PIPE_PROF")) != 0;
+    if (prof && P->sink.acquire) {
+        fprintf(stderr, "av1r_pipeline outputs: %.0f started; poll %.1f ms, blocked %.1f ms, start %.1f ms, drain %.1f ms\n",
+                P->oissued, 1e3 * P->oprof[0], 1e3 * P->oprof[1], 1e3 * P->oprof[2], 1e3 * P->oprof[3]);
+        P->oissued = 0;
+        for (double& v : P->oprof) v = 0;
+    }
     av1r_pipe_prof_dump(secs(Clock::now() - t0));
     return rc;
 }

@@ -1437,6 +1437,61 @@ void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s)
         reinterpret_cast<uint32_t*>(const_cast<void*>(src)), n4);
 }
 
+// Frame read-back into pinned host memory (av1r_get_output_async, the pipeline's output
+// sink): the compute queue writes a frame's visible planes straight over the bus.  The copy
+// engine then carries the packed uploads alone -- read-backs queued on it ahead of the next
+// batch's upload held that batch back (0.82x of the undelivered rate).  One wave per row,
+// 16-byte non-temporal stores when every address and width allow, else dwords, else bytes.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct OutPlanes {
+    const uint8_t* src[3];
+    uint8_t* dst[3];
+    int ss[3], ds[3], w[3], h[3];
+};
+extern "C" __global__ __launch_bounds__(256) void k_out(OutPlanes o)
+{
+    const int p = blockIdx.y, lane = threadIdx.x & 63;
+    const int w = o.w[p], h = o.h[p], ss = o.ss[p], ds = o.ds[p];
+    const uint8_t* src = o.src[p];
+    uint8_t* dst = o.dst[p];
+    const uintptr_t al = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)ss | (uintptr_t)ds | (uintptr_t)w;
+    const int waves = gridDim.x * 4;
+    for (int y = blockIdx.x * 4 + (threadIdx.x >> 6); y < h; y += waves) {
+        const uint8_t* s = src + (size_t)y * ss;
+        uint8_t* d = dst + (size_t)y * ds;
+        if (!(al & 15)) {
+            for (int x = lane * 16; x < w; x += 2 * 64 * 16) {  // both loads of a 2 KB span first
+                const bool two = x + 64 * 16 < w;
+                const u32x4 a = *reinterpret_cast<const u32x4*>(s + x);
+                u32x4 b;
+                if (two) b = *reinterpret_cast<const u32x4*>(s + x + 64 * 16);
+                __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(d + x));
+                if (two) __builtin_nontemporal_store(b, reinterpret_cast<u32x4*>(d + x + 64 * 16));
+            }
+        } else if (!(al & 3)) {
+            for (int x = lane * 4; x < w; x += 64 * 4)
+                __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(s + x), reinterpret_cast<uint32_t*>(d + x));
+        } else {
+            for (int x = lane; x < w; x += 64) d[x] = s[x];
+        }
+    }
+}
+void launch_k_out(const uint8_t* const src[3], const int ss[3], uint8_t* const dst[3], const int ds[3], const int w[3],
+                  const int h[3], hipStream_t st)
+{
+    OutPlanes o;
+    for (int p = 0; p < 3; p++) {
+        o.src[p] = src[p];
+        o.dst[p] = dst[p];
+        o.ss[p] = ss[p];
+        o.ds[p] = ds[p];
+        o.w[p] = w[p];
+        o.h[p] = h[p];
+    }
+    // 128 rows in flight per plane: enough stores outstanding to fill the link, few CUs taken
+    hipLaunchKernelGGL(k_out, dim3(32, 3), dim3(256), 0, st, o);
+}
+
 // ------------------------------------------------------------------------------------
 // k_mi: the mode-info grid of each frame of the launch, derived from its records instead of
 // uploaded (24 B per 4x4 unit: 3.1 MB of a 1080p frame's ~7.6 MB batch).  What the parser

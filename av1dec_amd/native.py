@@ -220,6 +220,7 @@ def lib():
     l.av1r_ivf_source_destroy.restype = None
     l.av1r_get_output_async.argtypes = [vp, u8p, i, u8p, i, u8p, i, C.POINTER(i), C.POINTER(i), C.POINTER(vp)]
     l.av1r_output_query.argtypes = [vp]
+    l.av1r_output_start.argtypes = [vp]
     l.av1r_output_wait.argtypes = [vp]
     l.av1r_set_output_prefetch.argtypes = [vp, i]
     l.av1r_pipeline_set_output.argtypes = [vp, C.POINTER(OutputSink)]
@@ -252,7 +253,7 @@ SINK_INFLIGHT = 8  # AV1R_SINK_INFLIGHT
 class PipelineStats(C.Structure):  # av1r_pipeline_stats
     _fields_ = [("frames", C.c_uint64), ("batches", C.c_uint64), ("elapsed_s", C.c_double),
                 ("produce_s", C.c_double), ("pack_s", C.c_double), ("wait_s", C.c_double),
-                ("launch_s", C.c_double)]
+                ("launch_s", C.c_double), ("output_s", C.c_double)]
 
 
 class Cycle(C.Structure):  # av1r_cycle
@@ -272,7 +273,7 @@ EXPORTS = [
     "av1r_pipeline_run", "av1r_pipeline_open", "av1r_pipeline_step", "av1r_pipeline_launched",
     "av1r_pipeline_close", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
     "av1r_set_strip_levels", "av1r_set_filter_fusion", "av1r_set_fast_intra", "av1r_packed_data", "av1r_set_flow_wave",
-    "av1r_get_output_async", "av1r_output_query", "av1r_output_wait", "av1r_set_output_prefetch", "av1r_pipeline_set_output",
+    "av1r_get_output_async", "av1r_output_query", "av1r_output_start", "av1r_output_wait", "av1r_set_output_prefetch", "av1r_pipeline_set_output",
     "av1r_ring_sink_create", "av1r_ring_sink_destroy", "av1r_ring_sink_delivered", "av1r_ring_sink_frame",
 ]
 

@@ -264,6 +264,19 @@ class RingSink:
             return sum(self.delivered(j) for j in range(self.n))
         return int(self.l.av1r_ring_sink_delivered(C.byref(self.s), stream))
 
+    def frame(self, stream, k):
+        """Copies of the I420 planes of delivered frame k of `stream` (None once its slot has
+        been reused; av1r_ring_sink_frame)."""
+        import numpy as np
+        w, h = C.c_int(), C.c_int()
+        p = self.l.av1r_ring_sink_frame(C.byref(self.s), stream, k, C.byref(w), C.byref(h))
+        if not p:
+            return None
+        W, H = w.value, h.value
+        cw, ch = (W + 1) >> 1, (H + 1) >> 1
+        a = np.ctypeslib.as_array((C.c_uint8 * (W * H + 2 * cw * ch)).from_address(p)).copy()
+        return a[:W * H].reshape(H, W), a[W * H:W * H + cw * ch].reshape(ch, cw), a[W * H + cw * ch:].reshape(ch, cw)
+
     def close(self):
         if self.s.user:
             self.l.av1r_ring_sink_destroy(C.byref(self.s))

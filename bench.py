@@ -308,6 +308,10 @@ def output_leg(decs, streams, pos, steps, workers):
             d.set_discard_output(True)
     return {"fps": round(k / dt, 3), "frames": k, "decoded": int(st["frames"]), "elapsed_s": round(dt, 4),
             "delivered_GBps": round(k * W * H * 1.5 / dt / 1e9, 2),
+            "launcher_idle_ms_per_step": round(1e3 * st["wait_s"] / max(steps, 1), 3),
+            "launcher_submit_ms_per_step": round(1e3 * st["launch_s"] / max(steps, 1), 3),
+            "launcher_output_ms_per_step": round(1e3 * st["output_s"] / max(steps, 1), 3),
+            "pack_ms_per_frame": round(1e3 * st["pack_s"] / max(st["frames"], 1), 3), "batches": int(st["batches"]),
             "method": "native pipeline kept open, every shown frame read back asynchronously into pinned host "
                       "buffers while later batches decode (av1r_pipeline_set_output + av1r_ring_sink); "
                       "one GOP of priming untimed"}

@@ -285,13 +285,17 @@ int av1r_get_output(av1r_ctx* ctx, uint8_t* y, int y_stride, uint8_t* u, int u_s
  * frames; the buffers must stay valid until the ticket is waited for, and should be pinned
  * (hipHostMalloc) for the copy to be a DMA.  av1r_output_query advances a ticket without
  * blocking (1: the bytes have landed, 0: not yet; it issues the copy once the frame is
- * done); av1r_output_wait blocks until they have landed, releases the ticket (and the
- * frame), and returns AV1R_E_DEVICE for a frame a device error touched.  A ticket belongs
- * to the context's driving thread; av1r_destroy releases tickets never waited for. */
+ * done); av1r_output_start only issues the copy if the frame is done (1: issued now or
+ * before, 0: the frame is still decoding) -- a driver holding several tickets starts every
+ * finished frame's copy at once; av1r_output_wait blocks until they have landed, releases
+ * the ticket (and the frame), and returns AV1R_E_DEVICE for a frame a device error touched.
+ * A ticket belongs to the context's driving thread; av1r_destroy releases tickets never
+ * waited for. */
 typedef struct av1r_output_ticket av1r_output_ticket;
 int av1r_get_output_async(av1r_ctx* ctx, uint8_t* y, int y_stride, uint8_t* u, int u_stride,
                           uint8_t* v, int v_stride, int* width, int* height, av1r_output_ticket** ticket);
 int av1r_output_query(av1r_output_ticket* ticket);
+int av1r_output_start(av1r_output_ticket* ticket);
 int av1r_output_wait(av1r_output_ticket* ticket);
 /* 1: from now on every shown frame's read-back starts as soon as it is queued (into pinned
  * staging memory of the context, on its read-back stream), so av1r_get_output waits for
@@ -387,6 +391,7 @@ typedef struct av1r_pipeline_stats {
     double pack_s;     /* producer time in av1r_pack, summed over streams                 */
     double wait_s;     /* launcher time with no stream ready                               */
     double launch_s;   /* launcher time inside av1r_decode_packed_batch                    */
+    double output_s;   /* launcher time delivering frames (av1r_pipeline_set_output)       */
 } av1r_pipeline_stats;
 int av1r_pipeline_run(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64_t max_frames, int depth,
                       int workers, av1r_pipeline_stats* stats);

@@ -204,6 +204,7 @@ def test_gpu_get_output_async_and_prefetch_match_oracle():
     import golden
     import numpy as np
     from av1dec_amd import Decoder, batchfile
+    import ctypes
     sets = [batchfile.load(golden.batch_path("av1-1-b8-06-mfmv"))] + bench.rank_streams("1080p", 0, 2, 6)
     for frames in sets:
         ref = _oracle_md5s(frames)
@@ -226,6 +227,30 @@ def test_gpu_get_output_async_and_prefetch_match_oracle():
             assert got == ref
         finally:
             d.close()
+        # async into pinned host memory: the planes are stored by k_out on the read-back
+        # stream (the copy engine is not used), waited for in order
+        from av1dec_amd.native import PinnedBuffer
+        d = Decoder(0, keep_stages=False)
+        bufs = []
+        try:
+            tickets = []
+            for f in frames:
+                d.decode_frame(f)
+                while d.output_pending():
+                    w, h = d.output_size()
+                    cw, ch = (w + 1) >> 1, (h + 1) >> 1
+                    b = PinnedBuffer(w * h + 2 * cw * ch)
+                    bufs.append(b)
+                    a = np.ctypeslib.as_array((ctypes.c_uint8 * b.n).from_address(b.ptr.value))
+                    a[:] = 0xA5  # stale bytes must not survive
+                    tickets.append(d.get_output_async(a[:w * h].reshape(h, w), a[w * h:w * h + cw * ch].reshape(ch, cw),
+                                                      a[w * h + cw * ch:].reshape(ch, cw)))
+            got = [_frame_md5(t.wait()) for t in tickets]
+            assert got == ref
+        finally:
+            d.close()
+            for b in bufs:
+                b.close()
         # prefetch
         d = Decoder(0, keep_stages=False)
         try:
@@ -239,4 +264,35 @@ def test_gpu_get_output_async_and_prefetch_match_oracle():
                 got.append(_frame_md5(d.get_output()))
             assert got == ref
         finally:
+            d.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpu_ring_sink_frames_match_oracle():
+    """The bench's output sink (av1r_ring_sink_create: pinned slots, written by k_out over the
+    bus): two synthetic 1080p streams through the native pipeline, 12 frames each (key frame
+    first), every frame left in the ring equals the CPU oracle's."""
+    import bench
+    from av1dec_amd import Decoder
+    from av1dec_amd.pipeline import NativePipeline, RingSink
+    S, F = 2, 12
+    streams = bench.rank_streams("1080p", 0, S, F)
+    ref = [_oracle_md5s(s) for s in streams]
+    decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+    sink = RingSink(S, 1920, 1080)
+    try:
+        pl = NativePipeline(decs, streams, [0] * S, depth=0, workers=bench.host_workers())
+        try:
+            pl.set_output(sink)
+            assert pl.step(F)["frames"] == S * F
+            pl.set_output(None)
+        finally:
+            pl.close()
+        for j in range(S):
+            assert sink.delivered(j) == F
+            assert [_frame_md5(sink.frame(j, k)) for k in range(F)] == ref[j], f"stream {j}"
+    finally:
+        sink.close()
+        for d in decs:
             d.close()
