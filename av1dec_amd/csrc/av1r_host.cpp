@@ -129,6 +129,8 @@ struct av1r_output_ticket {
     hipEvent_t ready = nullptr, done = nullptr;
     int state = 0;  // 0 the frame's kernels may still run, 1 copies issued, 2 landed
     bool live = false;
+    uint32_t* flag = nullptr;  // pinned word the last copy sets to 1 (AV1R_OUT_FLAG)
+    bool flagged = false;      // this read-back completes by `flag`, not by `done`
 };
 
 struct av1r_ctx {
@@ -158,6 +160,7 @@ struct av1r_ctx {
     // asynchronous frame delivery (av1r_get_output_async): the read-back copies' own stream
     // (created at the first such call) and every ticket ever allocated (free ones reused)
     hipStream_t outStream = nullptr;
+    uint32_t* oneDev = nullptr;  // a device word holding 1 (the read-backs' completion flags)
     std::vector<av1r_output_ticket*> tickets;
     // av1r_set_output_prefetch: every shown frame's read-back starts at once into a pinned
     // staging buffer of the context (frames move from outq to `staged`, the older ones);
@@ -2138,6 +2141,7 @@ void av1r_destroy(av1r_ctx* c)
     for (av1r_output_ticket* t : c->tickets) {  // tickets never waited for die with the context
         if (t->ready) (void)hipEventDestroy(t->ready);
         if (t->done) (void)hipEventDestroy(t->done);
+        if (t->flag) (void)hipHostFree(t->flag);
         delete t;
     }
     c->tickets.clear();
@@ -2146,6 +2150,7 @@ void av1r_destroy(av1r_ctx* c)
     c->staged.clear();
     c->stageFree.clear();
     if (c->outStream) (void)hipStreamDestroy(c->outStream);
+    if (c->oneDev) (void)hipFree(c->oneDev);
     {  // members of its batches: their pending join on its (now drained) stream is satisfied
         std::lock_guard<std::mutex> lock(g_ctxMu);
         for (av1r_ctx* m : g_ctxs)
@@ -2749,6 +2754,18 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
 
 static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
                          av1r_output_ticket** out);
+
+// AV1R_OUT_FLAG=1 (A/B): a read-back's completion is a 4-byte copy of 1 into a pinned word
+// of the ticket after its planes, polled by the host, instead of an event recorded on the
+// read-back stream (a marker there is a barrier packet in whichever hardware queue the
+// stream shares with a compute stream: it holds that stream's next kernels until the copies
+// are done)
+static bool out_flag()
+{
+    static const bool on = getenv("AV1R_OUT_FLAG") && atoi(getenv("AV1R_OUT_FLAG")) != 0;
+    return on;
+}
+
 static int ticket_issue(av1r_output_ticket* t);
 
 int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
@@ -2777,7 +2794,22 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     *out = nullptr;
     if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
     (void)hipSetDevice(c->device);
-    if (!c->outStream) HIPCHK(hipStreamCreateWithFlags(&c->outStream, hipStreamNonBlocking));
+    if (!c->outStream) {
+        // AV1R_OUT_CUMASK=1 (A/B): the read-back stream created with a (full) CU mask, which
+        // the runtime gives a hardware queue of its own instead of sharing a compute stream's
+        static const bool cuMask = getenv("AV1R_OUT_CUMASK") && atoi(getenv("AV1R_OUT_CUMASK")) != 0;
+        if (cuMask) {
+            const uint32_t mask[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
+            HIPCHK(hipExtStreamCreateWithCUMask(&c->outStream, 8, mask));
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&c->outStream, hipStreamNonBlocking));
+        }
+        if (out_flag()) {
+            const uint32_t one = 1;
+            HIPCHK(hipMalloc(&c->oneDev, 4));
+            HIPCHK(hipMemcpy(c->oneDev, &one, 4, hipMemcpyHostToDevice));
+        }
+    }
     av1r_output_ticket* t = nullptr;
     for (av1r_output_ticket* q : c->tickets)
         if (!q->live) {
@@ -2793,6 +2825,7 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
             delete t;
             return fail(c, AV1R_E_DEVICE, "hipEventCreate");
         }
+        if (out_flag() && hipHostMalloc((void**)&t->flag, 64, 0) != hipSuccess) t->flag = nullptr;
         c->tickets.push_back(t);
     }
     FrameBuf* f = c->outq.front();
@@ -2830,23 +2863,33 @@ static int ticket_issue(av1r_output_ticket* t)
     av1r_ctx* c = t->c;
     // AV1R_OUT_NOCOPY=1 (A/B of the delivery machinery alone): no bytes move
     static const bool noCopy = getenv("AV1R_OUT_NOCOPY") && atoi(getenv("AV1R_OUT_NOCOPY")) != 0;
-    // pinned destinations: k_out on the read-back stream (the copy engine stays free for
-    // the uploads); AV1R_OUT_SDMA=1 (A/B) or other memory: hipMemcpy2DAsync
-    static const bool sdma = getenv("AV1R_OUT_SDMA") && atoi(getenv("AV1R_OUT_SDMA")) != 0;
+    // How the planes travel: three hipMemcpy2DAsync on the read-back stream (copy engine).
+    // AV1R_OUT_MODE=2 (A/B, pinned destinations): k_out stores them straight over the bus,
+    // leaving the copy engine to the uploads -- but the bus writes slowed every filter
+    // kernel 20-40% (8 x 1080p: 0.72x of the undelivered rate against 0.89x).  Packing the
+    // planes into device staging with k_out for one linear copy was slower still (0.55x):
+    // a kernel on the read-back stream stalls the compute stream sharing its queue.
+    static const int mode = getenv("AV1R_OUT_MODE") ? atoi(getenv("AV1R_OUT_MODE")) : 0;
     const DevPlane* pl = t->f->d.pl;
-    if (!noCopy && !sdma && device_writable_host(t->dst[0]) && device_writable_host(t->dst[1]) &&
-        device_writable_host(t->dst[2])) {
-        const uint8_t* src[3] = {pl[0].p, pl[1].p, pl[2].p};
-        const int ss[3] = {pl[0].stride, pl[1].stride, pl[2].stride};
-        const int w[3] = {pl[0].w, pl[1].w, pl[2].w}, h[3] = {pl[0].h, pl[1].h, pl[2].h};
+    const uint8_t* src[3] = {pl[0].p, pl[1].p, pl[2].p};
+    const int ss[3] = {pl[0].stride, pl[1].stride, pl[2].stride};
+    const int w[3] = {pl[0].w, pl[1].w, pl[2].w}, h[3] = {pl[0].h, pl[1].h, pl[2].h};
+    if (noCopy) {
+    } else if (mode == 2 && device_writable_host(t->dst[0]) && device_writable_host(t->dst[1]) &&
+               device_writable_host(t->dst[2])) {
         launch_k_out(src, ss, t->dst, t->ds, w, h, c->outStream);
         HIPCHK(hipGetLastError());
     } else {
-        for (int p = 0; p < 3 && !noCopy; p++)
-            HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], pl[p].p, pl[p].stride, pl[p].w, pl[p].h, hipMemcpyDeviceToHost,
-                                    c->outStream));
+        for (int p = 0; p < 3; p++)
+            HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], src[p], ss[p], w[p], h[p], hipMemcpyDeviceToHost, c->outStream));
     }
-    HIPCHK(hipEventRecord(t->done, c->outStream));
+    t->flagged = out_flag() && t->flag && c->oneDev;
+    if (t->flagged) {
+        __atomic_store_n(t->flag, 0u, __ATOMIC_RELEASE);
+        HIPCHK(hipMemcpyAsync(t->flag, c->oneDev, 4, hipMemcpyDeviceToHost, c->outStream));
+    } else {
+        HIPCHK(hipEventRecord(t->done, c->outStream));
+    }
     t->state = 1;
     return AV1R_OK;
 }
@@ -2864,9 +2907,13 @@ int av1r_output_query(av1r_output_ticket* t)
         if (rc) return rc;
     }
     if (t->state == 1) {
-        const hipError_t q = hipEventQuery(t->done);
-        if (q == hipErrorNotReady) return 0;
-        if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output copy: %s", hipGetErrorString(q));
+        if (t->flagged) {
+            if (__atomic_load_n(t->flag, __ATOMIC_ACQUIRE) != 1) return 0;
+        } else {
+            const hipError_t q = hipEventQuery(t->done);
+            if (q == hipErrorNotReady) return 0;
+            if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output copy: %s", hipGetErrorString(q));
+        }
         t->state = 2;
     }
     return 1;
@@ -2896,7 +2943,13 @@ int av1r_output_wait(av1r_output_ticket* t)
         if (!rc) rc = ticket_issue(t);
     }
     if (!rc && t->state == 1) {
-        if (hipEventSynchronize(t->done) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output copy wait failed");
+        if (t->flagged) {
+            // the stream drains (the flag's copy included) or fails; then the flag is final
+            if (hipStreamSynchronize(c->outStream) != hipSuccess || __atomic_load_n(t->flag, __ATOMIC_ACQUIRE) != 1)
+                rc = fail(c, AV1R_E_DEVICE, "output copy wait failed");
+        } else if (hipEventSynchronize(t->done) != hipSuccess) {
+            rc = fail(c, AV1R_E_DEVICE, "output copy wait failed");
+        }
         t->state = 2;
     }
     if (t->state != 2) {

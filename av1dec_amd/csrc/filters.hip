@@ -1437,11 +1437,10 @@ void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s)
         reinterpret_cast<uint32_t*>(const_cast<void*>(src)), n4);
 }
 
-// Frame read-back into pinned host memory (av1r_get_output_async, the pipeline's output
-// sink): the compute queue writes a frame's visible planes straight over the bus.  The copy
-// engine then carries the packed uploads alone -- read-backs queued on it ahead of the next
-// batch's upload held that batch back (0.82x of the undelivered rate).  One wave per row,
-// 16-byte non-temporal stores when every address and width allow, else dwords, else bytes.
+// Frame read-back straight into pinned host memory over the bus (av1r_get_output_async,
+// AV1R_OUT_MODE=2 A/B; the default moves the planes with the copy engine).  One wave per
+// row, 16-byte non-temporal stores when every address and width allow, else dwords, else
+// bytes.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct OutPlanes {
     const uint8_t* src[3];

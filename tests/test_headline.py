@@ -227,8 +227,8 @@ def test_gpu_get_output_async_and_prefetch_match_oracle():
             assert got == ref
         finally:
             d.close()
-        # async into pinned host memory: the planes are stored by k_out on the read-back
-        # stream (the copy engine is not used), waited for in order
+        # async into pinned host memory (hipHostMalloc: a DMA straight into the caller's
+        # planes; AV1R_OUT_MODE=2 stores them with k_out instead), waited for in order
         from av1dec_amd.native import PinnedBuffer
         d = Decoder(0, keep_stages=False)
         bufs = []
@@ -270,8 +270,8 @@ def test_gpu_get_output_async_and_prefetch_match_oracle():
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_gpu_ring_sink_frames_match_oracle():
-    """The bench's output sink (av1r_ring_sink_create: pinned slots, written by k_out over the
-    bus): two synthetic 1080p streams through the native pipeline, 12 frames each (key frame
+    """The bench's output sink (av1r_ring_sink_create: pinned slots in rotation): two synthetic
+    1080p streams through the native pipeline, 12 frames each (key frame
     first), every frame left in the ring equals the CPU oracle's."""
     import bench
     from av1dec_amd import Decoder
