@@ -327,7 +327,7 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
-extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass)
+DEV void lf_body(const KParams* kps, int pass)
 {
     const uint3 wg = xcd_block();
     const KParams& k = KP(kps, wg.y);  // frame of this launch row
@@ -356,6 +356,12 @@ extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int p
     LfEdge e;
     if (!lf_edge(k, plane, pass, xP, yP, e)) return;
     lf_unit(k.cur.pl[plane], plane, pass, xP, yP, e);
+}
+// occupancy A/B (AV1R_FILT_WPE=6: at most 80 VGPRs, 6 waves per SIMD instead of 5)
+extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_lf6(const KParams* kps, int pass)
+{
+    lf_body(kps, pass);
 }
 
 // ------------------------------------------------------------------------------------
@@ -544,7 +550,7 @@ DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int 
 }
 
 // grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.cur, writes k.cdef
-extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
+DEV void cdef_body(const KParams* kps)
 {
     __shared__ CdefLds L;
     const uint3 wg = xcd_block();
@@ -730,6 +736,11 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps)
             }
         }
     }
+}
+extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps) { cdef_body(kps); }
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_cdef6(const KParams* kps)
+{
+    cdef_body(kps);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1577,13 +1588,19 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 
 // ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
+static int filt_wpe()
+{
+    static const int v = getenv("AV1R_FILT_WPE") ? atoi(getenv("AV1R_FILT_WPE")) : 0;
+    return v;
+}
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
+    hipLaunchKernelGGL(filt_wpe() == 6 ? k_lf6 : k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
 }
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
+    hipLaunchKernelGGL(filt_wpe() == 6 ? k_cdef6 : k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0,
+                       s, kps);
 }
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {

@@ -231,6 +231,7 @@ def lib():
     l.av1r_ring_sink_delivered.restype = C.c_int64
     l.av1r_ring_sink_frame.argtypes = [C.POINTER(OutputSink), i, C.c_int64, C.POINTER(i), C.POINTER(i)]
     l.av1r_ring_sink_frame.restype = vp
+    l.av1r_frame_layout.argtypes = [i, i, C.POINTER(i), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
     _lib = l
     return l
 
@@ -275,6 +276,7 @@ EXPORTS = [
     "av1r_set_strip_levels", "av1r_set_filter_fusion", "av1r_set_fast_intra", "av1r_packed_data", "av1r_set_flow_wave",
     "av1r_get_output_async", "av1r_output_query", "av1r_output_start", "av1r_output_wait", "av1r_set_output_prefetch", "av1r_pipeline_set_output",
     "av1r_ring_sink_create", "av1r_ring_sink_destroy", "av1r_ring_sink_delivered", "av1r_ring_sink_frame",
+    "av1r_frame_layout",
 ]
 
 

@@ -273,9 +273,14 @@ class RingSink:
         if not p:
             return None
         W, H = w.value, h.value
-        cw, ch = (W + 1) >> 1, (H + 1) >> 1
-        a = np.ctypeslib.as_array((C.c_uint8 * (W * H + 2 * cw * ch)).from_address(p)).copy()
-        return a[:W * H].reshape(H, W), a[W * H:W * H + cw * ch].reshape(ch, cw), a[W * H + cw * ch:].reshape(ch, cw)
+        st, off, span = (C.c_int * 3)(), (C.c_size_t * 3)(), C.c_size_t()
+        self.l.av1r_frame_layout(W, H, st, off, C.byref(span))  # the slot's layout
+        a = np.ctypeslib.as_array((C.c_uint8 * span.value).from_address(p))
+        out = []
+        for q, (pw, ph) in enumerate(((W, H), (W >> 1, H >> 1), (W >> 1, H >> 1))):
+            rows = np.lib.stride_tricks.as_strided(a[off[q]:], (ph, pw), (st[q], 1))
+            out.append(rows.copy())
+        return tuple(out)
 
     def close(self):
         if self.s.user:

@@ -426,12 +426,19 @@ typedef struct av1r_output_sink {
     void* user;
 } av1r_output_sink;
 int av1r_pipeline_set_output(av1r_pipeline* p, const av1r_output_sink* sink);
+/* The library's frame layout in device memory: plane p of a width x height frame starts
+ * offsets[p] bytes after plane 0, rows strides[p] apart; `span` = plane 0's first byte to
+ * the last visible byte of plane 2.  A read-back destination laid out the same way (planes
+ * at those offsets from planes[0], those strides) travels as ONE linear copy of `span`
+ * bytes instead of three 2-D copies. */
+int av1r_frame_layout(int width, int height, int* strides, size_t* offsets, size_t* span);
 /* A sink of pinned host buffers (hipHostMalloc): `slots` (>= AV1R_SINK_INFLIGHT) frames of
- * at most width x height per stream, reused in rotation; it counts what it was delivered
- * (av1r_ring_sink_delivered: frames of `stream`, -1 for a bad argument) and a frame's
- * buffer is readable from its delivery until `slots` later frames of that stream have
- * been acquired (av1r_ring_sink_frame: the I420 planes of the stream's k-th delivered
- * frame, NULL once overwritten). */
+ * at most width x height per stream in the av1r_frame_layout of each frame, reused in
+ * rotation; it counts what it was delivered (av1r_ring_sink_delivered: frames of `stream`,
+ * -1 for a bad argument) and a frame's buffer is readable from its delivery until `slots`
+ * later frames of that stream have been acquired (av1r_ring_sink_frame: plane 0 of the
+ * stream's k-th delivered frame, the others at the layout's offsets; NULL once
+ * overwritten). */
 int av1r_ring_sink_create(int n_streams, int width, int height, int slots, av1r_output_sink* out);
 void av1r_ring_sink_destroy(av1r_output_sink* sink);
 int64_t av1r_ring_sink_delivered(const av1r_output_sink* sink, int stream);
