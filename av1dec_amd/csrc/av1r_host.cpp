@@ -2817,13 +2817,13 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
         // AV1R_OUT_CUMASK=1 (A/B): the read-back stream created with a (full) CU mask, which
         // the runtime gives a hardware queue of its own instead of sharing a compute stream's
         static const bool cuMask = getenv("AV1R_OUT_CUMASK") && atoi(getenv("AV1R_OUT_CUMASK")) != 0;
-        // the read-backs go on the context's upload stream: contexts create their streams in
-        // pairs (compute, upload) and the runtime maps streams round-robin onto 4 hardware
-        // queues, so upload streams share queues with upload streams only.  A stream of their
-        // own (AV1R_OUT_ON_COPY=0) shares one with a compute stream, whose kernels then wait
-        // behind every read-back's completion marker (8 x 1080p: 0.87-0.88x of the
-        // undelivered rate against 0.89-0.90x)
-        static const bool onCopy = !getenv("AV1R_OUT_ON_COPY") || atoi(getenv("AV1R_OUT_ON_COPY")) != 0;
+        // AV1R_OUT_ON_COPY=1 (A/B): the read-backs on the context's upload stream (whose
+        // hardware queue holds copy streams only) instead of a stream of their own.  With
+        // three 2-D copies per frame that measured a little faster (8 x 1080p: 0.89-0.90x of
+        // the undelivered rate against 0.87-0.88x); with one linear copy per frame (the
+        // default for destinations in the library's layout) it is slower -- the next
+        // batch's upload queues behind the read-backs in the same stream (0.82x against 0.89x)
+        static const bool onCopy = getenv("AV1R_OUT_ON_COPY") && atoi(getenv("AV1R_OUT_ON_COPY")) != 0;
         if (onCopy) {
             c->outStream = c->copyStream;
         } else if (cuMask) {

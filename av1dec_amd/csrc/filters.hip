@@ -357,12 +357,8 @@ DEV void lf_body(const KParams* kps, int pass)
     if (!lf_edge(k, plane, pass, xP, yP, e)) return;
     lf_unit(k.cur.pl[plane], plane, pass, xP, yP, e);
 }
-// occupancy A/B (AV1R_FILT_WPE=6: at most 80 VGPRs, 6 waves per SIMD instead of 5)
+// (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_lf6(const KParams* kps, int pass)
-{
-    lf_body(kps, pass);
-}
 
 // ------------------------------------------------------------------------------------
 // CDEF
@@ -737,11 +733,8 @@ DEV void cdef_body(const KParams* kps)
         }
     }
 }
+// (6 waves per SIMD instead of 5 measured no faster: the filters are not occupancy-bound)
 extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps) { cdef_body(kps); }
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_cdef6(const KParams* kps)
-{
-    cdef_body(kps);
-}
 
 // ------------------------------------------------------------------------------------
 // Loop restoration
@@ -1588,19 +1581,13 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 
 // ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
-static int filt_wpe()
-{
-    static const int v = getenv("AV1R_FILT_WPE") ? atoi(getenv("AV1R_FILT_WPE")) : 0;
-    return v;
-}
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
-    hipLaunchKernelGGL(filt_wpe() == 6 ? k_lf6 : k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
+    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
 }
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(filt_wpe() == 6 ? k_cdef6 : k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0,
-                       s, kps);
+    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
 }
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {
