@@ -2817,13 +2817,17 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
         // AV1R_OUT_CUMASK=1 (A/B): the read-back stream created with a (full) CU mask, which
         // the runtime gives a hardware queue of its own instead of sharing a compute stream's
         static const bool cuMask = getenv("AV1R_OUT_CUMASK") && atoi(getenv("AV1R_OUT_CUMASK")) != 0;
-        // AV1R_OUT_ON_COPY=1 (A/B): the read-backs on the context's upload stream (whose
-        // hardware queue holds copy streams only) instead of a stream of their own.  With
-        // three 2-D copies per frame that measured a little faster (8 x 1080p: 0.89-0.90x of
-        // the undelivered rate against 0.87-0.88x); with one linear copy per frame (the
-        // default for destinations in the library's layout) it is slower -- the next
-        // batch's upload queues behind the read-backs in the same stream (0.82x against 0.89x)
-        static const bool onCopy = getenv("AV1R_OUT_ON_COPY") && atoi(getenv("AV1R_OUT_ON_COPY")) != 0;
+        // The read-backs go on the context's upload stream (AV1R_OUT_ON_COPY=0: a stream of
+        // their own).  Each read-back's completion marker sits in whichever of the runtime's
+        // 4 hardware queues its stream landed on (streams attach to the least-used queue at
+        // creation), holding back the streams that share it.  A stream of their own, created
+        // late, shares a queue with a compute stream; the upload stream's queue holds copy
+        // streams, but the context's own uploads (a batch lead's, a key frame's) queue
+        // behind its read-backs.  Which costs more depends on the streams created before:
+        // the bench's delivery leg (after its other legs) 0.89-0.92x of the undelivered rate
+        // on the upload stream against 0.82-0.84x on their own; tools/out_probe.py (fresh
+        // contexts) the other way round, 0.82x against 0.89x
+        static const bool onCopy = !getenv("AV1R_OUT_ON_COPY") || atoi(getenv("AV1R_OUT_ON_COPY")) != 0;
         if (onCopy) {
             c->outStream = c->copyStream;
         } else if (cuMask) {

@@ -603,7 +603,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--ivf-frames", type=int, default=24, help="frames per stream of the IVF end-to-end leg (0: skip)")
     ap.add_argument("--no-4k", action="store_true", help="skip the configs[3] 4K leg of a 1080p run")
-    ap.add_argument("--output-steps", type=int, default=60, help="steps of the frame-delivery leg (0: skip)")
+    ap.add_argument("--output-steps", type=int, default=180, help="steps of the frame-delivery leg (0: skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per frame (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-4k", default=os.path.join(ROOT, "profiles", "traffic_4k.json"))
