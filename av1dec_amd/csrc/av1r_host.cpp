@@ -67,6 +67,11 @@ struct Upload {
     hipEvent_t done = nullptr;  // all work that reads this upload has finished
     hipEvent_t ready = nullptr; // meta: the upload (on the context's copy stream) has landed
     bool pending = false;
+    uint64_t gen = 0;  // meta: launches that have used this slot
+    // packed-frame slots (AV1R_SLOT_META): done when the launch that used meta slot waitMeta
+    // at generation waitGen is (that launch's own completion event, no event of this slot's)
+    const Upload* waitMeta = nullptr;
+    uint64_t waitGen = 0;
 };
 
 struct Level {
@@ -153,6 +158,7 @@ struct av1r_ctx {
     // of its own so that the copy of batch N + 1 overlaps the kernels of batch N
     static constexpr int kMetaRing = AV1R_RING;
     Upload meta[kMetaRing];
+    const Upload* lastMeta = nullptr;  // the meta slot of this context's last launch (launch_jobs)
     int metaIdx = 0;
     hipStream_t copyStream = nullptr;
     hipStream_t aux = nullptr;              // k_inter_m / k_inter_s beside k_inter (AV1R_INTER_SPLIT)
@@ -1668,6 +1674,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         M.pending = false;
         harvest(false);  // device errors reach their frames (av1r_get_output / av1r_synchronize)
     }
+    M.gen++;  // (a packed-frame slot waiting on this slot's previous launch sees it finished)
+    lc->lastMeta = &M;
     // the launch's status record (k_flow launches only)
     LaunchRec* rec = nullptr;
     if (anyFlow) {
@@ -2609,7 +2617,9 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         m->pkIdx = (m->pkIdx + 1) % av1r_ctx::kPackRing;
         if (U.pending) {  // a launch three frames back may still read this slot
             const double w0 = g_pipeProf ? now_s() : 0;
-            HIPCHK(hipEventSynchronize(U.done));
+            if (!U.waitMeta) HIPCHK(hipEventSynchronize(U.done));
+            else if (U.waitMeta->gen == U.waitGen) HIPCHK(hipEventSynchronize(U.waitMeta->done));
+            // (else that meta slot was reused: its launch was waited for then)
             if (g_pipeProf) {
                 std::lock_guard<std::mutex> lock(g_pprofMu);
                 g_pprof.slotWait += now_s() - w0;
@@ -2688,11 +2698,22 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             g_pprof.shared += now_s() - s1;
         }
     }
-    for (int i = 0; i < n; i++) {  // the upload slots are free again after their launch
+    // the upload slots are free again after their launch.  AV1R_SLOT_META=1 (A/B): a slot
+    // waits for its launch's own completion event (the launch's meta slot and generation)
+    // instead of an event of its own recorded after the launch -- n more markers per batch
+    static const bool slotMeta = getenv("AV1R_SLOT_META") && atoi(getenv("AV1R_SLOT_META")) != 0;
+    for (int i = 0; i < n; i++) {
         if (!slots[i]) continue;
         av1r_ctx* m = ctxs[i];
         const bool alone = std::any_of(solo.begin(), solo.end(), [&](const FrameJob& j) { return j.c == m; });
-        HIPCHK(hipEventRecord(slots[i]->done, alone ? m->stream : bl->stream));
+        const Upload* lm = (alone ? m : bl)->lastMeta;
+        if (slotMeta && lm) {
+            slots[i]->waitMeta = lm;
+            slots[i]->waitGen = lm->gen;
+        } else {
+            slots[i]->waitMeta = nullptr;
+            HIPCHK(hipEventRecord(slots[i]->done, alone ? m->stream : bl->stream));
+        }
         slots[i]->pending = true;
     }
     return AV1R_OK;
