@@ -67,7 +67,7 @@ struct Upload {
     hipEvent_t done = nullptr;  // all work that reads this upload has finished
     hipEvent_t ready = nullptr; // meta: the upload (on the context's copy stream) has landed
     bool pending = false;
-    uint64_t gen = 0;  // meta: launches that have used this slot
+    std::atomic<uint64_t> gen{0};  // meta: launches that have used this slot (read by packers)
     // packed-frame slots (AV1R_SLOT_META): done when the launch that used meta slot waitMeta
     // at generation waitGen is (that launch's own completion event, no event of this slot's)
     const Upload* waitMeta = nullptr;
@@ -120,6 +120,10 @@ struct av1r_packed {
     bool pinned = false;
     hipEvent_t copied = nullptr;  // the upload of this buffer (its host memory is in use until then)
     bool copyPending = false;
+    // ... or (slot_meta()) the completion of the launch that read the upload: its meta slot and
+    // that slot's generation then (see Upload::waitMeta)
+    const struct Upload* waitMeta = nullptr;
+    uint64_t waitGen = 0;
 };
 
 // One asynchronous read-back of a shown frame (av1r_get_output_async): the frame stays
@@ -282,10 +286,36 @@ struct av1r_ctx {
 struct LaunchRec {
     uint32_t* err = nullptr;
     hipEvent_t done = nullptr;
+    const struct Upload* meta = nullptr;  // (slot_meta()) completion = this launch's meta slot
+    uint64_t gen = 0;
     std::vector<std::pair<av1r_ctx*, uint64_t>> members;
 };
 static std::mutex g_recMu;
 static std::vector<LaunchRec*> g_recPending, g_recFree;
+// packed frames (av1r_pack) released by their launches, for reuse by any packing thread
+static std::mutex g_packMu;
+static std::vector<av1r_packed*> g_packFree;
+
+// Completion of a launch through its own meta slot (the one event every launch records on
+// its stream after its last kernel) instead of more events recorded after it: a launch
+// recorded one per packed-frame slot, one per packed buffer and one for its status record
+// -- each a marker packet in the compute stream's hardware queue.  Without them (the
+// default; AV1R_SLOT_META=0 restores them) the headline rose 6 100 -> 6 370 frames/s.
+// The meta slot's generation counts its launches: once it has moved on, the launch waited
+// for was synchronized before the slot's reuse.
+static bool slot_meta()
+{
+    static const bool on = !getenv("AV1R_SLOT_META") || atoi(getenv("AV1R_SLOT_META")) != 0;
+    return on;
+}
+static bool meta_done(const Upload* m, uint64_t gen)
+{
+    return m->gen.load(std::memory_order_acquire) != gen || hipEventQuery(m->done) == hipSuccess;
+}
+static void meta_wait(const Upload* m, uint64_t gen)
+{
+    if (m->gen.load(std::memory_order_acquire) == gen) (void)hipEventSynchronize(m->done);
+}
 
 // collect completed launch records (wait: block on each pending one first)
 static void harvest(bool wait)
@@ -293,10 +323,18 @@ static void harvest(bool wait)
     std::lock_guard<std::mutex> lock(g_recMu);
     for (size_t i = 0; i < g_recPending.size();) {
         LaunchRec* r = g_recPending[i];
-        if (wait) (void)hipEventSynchronize(r->done);
-        if (hipEventQuery(r->done) != hipSuccess) {
-            i++;
-            continue;
+        if (r->meta) {
+            if (wait) meta_wait(r->meta, r->gen);
+            if (!meta_done(r->meta, r->gen)) {
+                i++;
+                continue;
+            }
+        } else {
+            if (wait) (void)hipEventSynchronize(r->done);
+            if (hipEventQuery(r->done) != hipSuccess) {
+                i++;
+                continue;
+            }
         }
         if (const uint32_t e = *r->err) {
             for (auto& m : r->members) {
@@ -1674,7 +1712,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         M.pending = false;
         harvest(false);  // device errors reach their frames (av1r_get_output / av1r_synchronize)
     }
-    M.gen++;  // (a packed-frame slot waiting on this slot's previous launch sees it finished)
+    M.gen.fetch_add(1, std::memory_order_release);  // (waiters on this slot's previous launch see it finished)
     lc->lastMeta = &M;
     // the launch's status record (k_flow launches only)
     LaunchRec* rec = nullptr;
@@ -2006,7 +2044,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     M.pending = true;
     for (auto& j : jobs) job_end(j);
     if (rec) {
-        HIPCHK(hipEventRecord(rec->done, st));
+        rec->meta = slot_meta() ? &M : nullptr;
+        rec->gen = M.gen.load(std::memory_order_relaxed);
+        if (!rec->meta) HIPCHK(hipEventRecord(rec->done, st));
         std::lock_guard<std::mutex> lock(g_recMu);
         for (auto& j : jobs) rec->members.emplace_back(j.c, j.seq);
         g_recPending.push_back(rec);
@@ -2162,6 +2202,7 @@ void av1r_destroy(av1r_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
+    (void)hipStreamSynchronize(c->copyStream);
     if (c->outStream) (void)hipStreamSynchronize(c->outStream);
     for (av1r_output_ticket* t : c->tickets) {  // tickets never waited for die with the context
         if (t->ready) (void)hipEventDestroy(t->ready);
@@ -2179,6 +2220,28 @@ void av1r_destroy(av1r_ctx* c)
         for (av1r_ctx* m : g_ctxs)
             if (m->joinLead == c) m->joinLead = nullptr;
         g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), c), g_ctxs.end());
+        // what waits for a launch through this context's meta slots (slot_meta: other
+        // contexts' upload slots, pooled packed buffers, status records) is complete now
+        // (its streams are drained): forget the slots before they go
+        auto mine = [&](const Upload* m) { return m >= c->meta && m < c->meta + av1r_ctx::kMetaRing; };
+        for (av1r_ctx* m : g_ctxs)
+            for (auto& u : m->pk)
+                if (u.waitMeta && mine(u.waitMeta)) {
+                    u.waitMeta = nullptr;
+                    u.pending = false;
+                }
+        {
+            std::lock_guard<std::mutex> pl(g_packMu);
+            for (av1r_packed* q : g_packFree)
+                if (q->waitMeta && mine(q->waitMeta)) {
+                    q->waitMeta = nullptr;
+                    q->copyPending = false;
+                }
+        }
+        harvest(false);
+        std::lock_guard<std::mutex> rl(g_recMu);
+        for (LaunchRec* r : g_recPending)
+            if (r->meta && mine(r->meta)) r->meta = nullptr;  // (its never-recorded event queries complete)
     }
     for (FrameBuf* f : c->pool) {
         (void)hipFree(f->base);
@@ -2424,8 +2487,6 @@ int av1r_release_prepared(av1r_ctx* c, int handle)
 }
 
 // ---- packed frames: host work off the launching thread ----
-static std::mutex g_packMu;
-static std::vector<av1r_packed*> g_packFree;
 static thread_local av1r_ctx t_packScratch;
 
 const char* av1r_pack_last_error(void) { return t_packScratch.err.c_str(); }
@@ -2436,22 +2497,28 @@ const char* av1r_pack_last_error(void) { return t_packScratch.err.c_str(); }
 // hipHostFree / hipHostMalloc cost milliseconds and stall the device and every other
 // thread's HIP calls -- and grow in whole MiB with a quarter's margin, so a running pipeline
 // stops allocating after its first GOPs.
+static std::atomic<int> g_packCount{0};  // packed buffers allocated (pinned host memory)
 static av1r_packed* pack_buffer(size_t need)
 {
     av1r_packed* pk = nullptr;
     {
         std::lock_guard<std::mutex> lock(g_packMu);
         size_t pick = SIZE_MAX;
+        bool idle = false;
         for (size_t i = 0; i < g_packFree.size(); i++) {
             av1r_packed* q = g_packFree[i];
             if (q->cap < need) continue;
             if (pick == SIZE_MAX) pick = i;
-            if (!q->copyPending || hipEventQuery(q->copied) == hipSuccess) {
+            if (!q->copyPending || (q->waitMeta ? meta_done(q->waitMeta, q->waitGen) : !q->copied || hipEventQuery(q->copied) == hipSuccess)) {
                 q->copyPending = false;
                 pick = i;
+                idle = true;
                 break;
             }
         }
+        // none whose launch has finished: a new buffer rather than a wait, up to a bound (the
+        // pool settles at the pipeline's working set during its first GOPs)
+        if (!idle && pick != SIZE_MAX && g_packCount.load() < 384) pick = SIZE_MAX;
         if (pick != SIZE_MAX) {
             pk = g_packFree[pick];
             g_packFree.erase(g_packFree.begin() + pick);
@@ -2459,13 +2526,15 @@ static av1r_packed* pack_buffer(size_t need)
     }
     if (pk) {
         if (pk->copyPending) {  // its previous upload may still read the host buffer
-            (void)hipEventSynchronize(pk->copied);
+            if (pk->waitMeta) meta_wait(pk->waitMeta, pk->waitGen);
+            else if (pk->copied) (void)hipEventSynchronize(pk->copied);
             pk->copyPending = false;
         }
         return pk;
     }
     pk = new (std::nothrow) av1r_packed;
     if (!pk || !need) return pk;
+    g_packCount++;
     const size_t cap = (need + need / 4 + (1u << 20)) & ~(size_t)((1u << 20) - 1);
     pk->pinned = hipHostMalloc(&pk->host, cap, hipHostMallocDefault) == hipSuccess;
     if (!pk->pinned) pk->host = static_cast<uint8_t*>(malloc(cap));  // no device here (host-only use)
@@ -2597,6 +2666,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
     std::vector<FrameJob> jobs, solo;
     std::vector<Upload*> slots(n, nullptr);
     std::vector<hipEvent_t> waits;  // uploads on member copy streams the batch waits for
+    std::vector<bool> metaWait(n, false);  // packed buffers released by the launch's completion
     bool copies = false;
     for (int i = 0; i < n; i++) {
         av1r_ctx* m = ctxs[i];
@@ -2632,8 +2702,16 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             HIPCHK(hipMalloc(&U.dev, U.cap));
         }
         HIPCHK(hipMemcpyAsync(U.dev, pk->host, pk->P.upBytes, hipMemcpyHostToDevice, up->copyStream));
-        if (!pk->copied) HIPCHK(hipEventCreateWithFlags(&pk->copied, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(pk->copied, up->copyStream));
+        // the host buffer is free once the upload has landed: an event for a frame launched
+        // alone or uploaded on another stream (something waits for it), else its launch's
+        // completion (set below)
+        pk->waitMeta = nullptr;
+        if (alone || up != bl || !slot_meta()) {
+            if (!pk->copied) HIPCHK(hipEventCreateWithFlags(&pk->copied, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(pk->copied, up->copyStream));
+        } else {
+            metaWait[i] = true;
+        }
         pk->copyPending = true;
         if (alone) {
             ctx_join(m);
@@ -2698,18 +2776,21 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             g_pprof.shared += now_s() - s1;
         }
     }
-    // the upload slots are free again after their launch.  AV1R_SLOT_META=1 (A/B): a slot
-    // waits for its launch's own completion event (the launch's meta slot and generation)
-    // instead of an event of its own recorded after the launch -- n more markers per batch
-    static const bool slotMeta = getenv("AV1R_SLOT_META") && atoi(getenv("AV1R_SLOT_META")) != 0;
+    // the upload slots (and the packed buffers) are free again after their launch: its own
+    // completion event (slot_meta) or an event per slot
     for (int i = 0; i < n; i++) {
         if (!slots[i]) continue;
         av1r_ctx* m = ctxs[i];
         const bool alone = std::any_of(solo.begin(), solo.end(), [&](const FrameJob& j) { return j.c == m; });
         const Upload* lm = (alone ? m : bl)->lastMeta;
-        if (slotMeta && lm) {
+        if (metaWait[i]) {
+            pks[i]->waitMeta = bl->lastMeta;
+            pks[i]->waitGen = bl->lastMeta ? bl->lastMeta->gen.load(std::memory_order_relaxed) : 0;
+            if (!bl->lastMeta) pks[i]->copyPending = false;  // (no launch read it: nothing to wait for)
+        }
+        if (slot_meta() && lm) {
             slots[i]->waitMeta = lm;
-            slots[i]->waitGen = lm->gen;
+            slots[i]->waitGen = lm->gen.load(std::memory_order_relaxed);
         } else {
             slots[i]->waitMeta = nullptr;
             HIPCHK(hipEventRecord(slots[i]->done, alone ? m->stream : bl->stream));
