@@ -139,6 +139,10 @@ struct av1r_output_ticket {
     int state = 0;  // 0 the frame's kernels may still run, 1 copies issued, 2 landed
     bool live = false;
     bool sq = false;  // this read-back's landing is seen by the stream going idle (AV1R_OUT_SQ)
+    // the frame is done when this launch is (slot_meta(): the last launch on the frame's
+    // stream, through its metadata slot and generation) instead of by `ready`
+    const Upload* readyMeta = nullptr;
+    uint64_t readyGen = 0;
 };
 
 struct av1r_ctx {
@@ -2224,12 +2228,15 @@ void av1r_destroy(av1r_ctx* c)
         // contexts' upload slots, pooled packed buffers, status records) is complete now
         // (its streams are drained): forget the slots before they go
         auto mine = [&](const Upload* m) { return m >= c->meta && m < c->meta + av1r_ctx::kMetaRing; };
-        for (av1r_ctx* m : g_ctxs)
+        for (av1r_ctx* m : g_ctxs) {
             for (auto& u : m->pk)
                 if (u.waitMeta && mine(u.waitMeta)) {
                     u.waitMeta = nullptr;
                     u.pending = false;
                 }
+            for (av1r_output_ticket* t : m->tickets)
+                if (t->readyMeta && mine(t->readyMeta)) t->readyMeta = nullptr;  // (ready: its event was never recorded)
+        }
         {
             std::lock_guard<std::mutex> pl(g_packMu);
             for (av1r_packed* q : g_packFree)
@@ -2870,7 +2877,7 @@ int av1r_get_output(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t
 }
 
 static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
-                         av1r_output_ticket** out);
+                         av1r_output_ticket** out, bool needEvent = false);
 
 // No completion event after a read-back: an event recorded on the read-back stream is a
 // barrier packet in whichever hardware queue the stream shares with others, holding them
@@ -2907,7 +2914,7 @@ int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, u
 
 // the oldest queued frame into a ticket (av1r_get_output_async; stage_outputs)
 static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
-                         av1r_output_ticket** out)
+                         av1r_output_ticket** out, bool needEvent)
 {
     *out = nullptr;
     if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
@@ -2957,7 +2964,16 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     // the frame's last writer: this context's own stream, or the stream of the batch it was
     // last launched in (ctx_join is not needed: nothing is enqueued on the context here)
     static const bool noReady = getenv("AV1R_OUT_NOREADY") && atoi(getenv("AV1R_OUT_NOREADY")) != 0;  // (A/B with NOCOPY)
-    if (!noReady) HIPCHK(hipEventRecord(t->ready, c->joinLead ? c->joinLead->stream : c->stream));
+    // the last launch on that stream has it (members join a batch stream behind their own
+    // stream's work, ctx_join): its completion, or an event where a stream must wait on it
+    av1r_ctx* w = c->joinLead ? c->joinLead : c;
+    t->readyMeta = nullptr;
+    if (slot_meta() && !needEvent && w->lastMeta) {
+        t->readyMeta = w->lastMeta;
+        t->readyGen = w->lastMeta->gen.load(std::memory_order_relaxed);
+    } else if (!noReady) {
+        HIPCHK(hipEventRecord(t->ready, w->stream));
+    }
     c->outq.pop_front();  // the queue's reference passes to the ticket
     t->c = c;
     t->f = f;
@@ -3028,9 +3044,13 @@ int av1r_output_query(av1r_output_ticket* t)
     av1r_ctx* c = t->c;
     (void)hipSetDevice(c->device);
     if (t->state == 0) {
-        const hipError_t q = hipEventQuery(t->ready);
-        if (q == hipErrorNotReady) return 0;
-        if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output: %s", hipGetErrorString(q));
+        if (t->readyMeta) {
+            if (!meta_done(t->readyMeta, t->readyGen)) return 0;
+        } else {
+            const hipError_t q = hipEventQuery(t->ready);
+            if (q == hipErrorNotReady) return 0;
+            if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output: %s", hipGetErrorString(q));
+        }
         const int rc = ticket_issue(t);
         if (rc) return rc;
     }
@@ -3055,6 +3075,11 @@ int av1r_output_start(av1r_output_ticket* t)
     if (t->state) return 1;
     av1r_ctx* c = t->c;
     (void)hipSetDevice(c->device);
+    if (t->readyMeta) {
+        if (!meta_done(t->readyMeta, t->readyGen)) return 0;
+        const int rc = ticket_issue(t);
+        return rc ? rc : 1;
+    }
     const hipError_t q = hipEventQuery(t->ready);
     if (q == hipErrorNotReady) return 0;
     if (q != hipSuccess) return fail(c, AV1R_E_DEVICE, "output: %s", hipGetErrorString(q));
@@ -3069,7 +3094,8 @@ int av1r_output_wait(av1r_output_ticket* t)
     (void)hipSetDevice(c->device);
     int rc = AV1R_OK;
     if (t->state == 0) {
-        if (hipEventSynchronize(t->ready) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output: frame wait failed");
+        if (t->readyMeta) meta_wait(t->readyMeta, t->readyGen);
+        else if (hipEventSynchronize(t->ready) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output: frame wait failed");
         if (!rc) rc = ticket_issue(t);
     }
     if (!rc && t->state == 1) {
@@ -3117,7 +3143,7 @@ static int stage_outputs(av1r_ctx* c)
             S.cap = need;
         }
         uint8_t* u = S.buf + (size_t)w * h;
-        int rc = output_ticket(c, S.buf, w, u, cw, u + (size_t)cw * ch, cw, nullptr, nullptr, &S.t);
+        int rc = output_ticket(c, S.buf, w, u, cw, u + (size_t)cw * ch, cw, nullptr, nullptr, &S.t, true);
         if (!rc && hipStreamWaitEvent(c->outStream, S.t->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
         if (!rc) rc = ticket_issue(S.t);
         if (rc) {
