@@ -269,8 +269,11 @@ int pipe_open(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64
     // AV1R_PIPE_GROUPS=g: the streams form g groups whose batches go to g different HIP
     // streams (each batch runs on its first member's stream), so one group's latency-bound
     // k_flow overlaps the other groups' kernels
-    static const int groups = std::max(1, getenv("AV1R_PIPE_GROUPS") ? atoi(getenv("AV1R_PIPE_GROUPS")) : 1);
-    P->G = std::min(groups, n);
+    // (default: 2 groups from 8 streams up -- 8 x 1080p: 6 580-6 620 against 6 500 frames/s
+    // with one -- so a group's filters overlap the other's reconstruction; fewer streams, or
+    // frames being delivered (pipe_step): one)
+    static const int groups = getenv("AV1R_PIPE_GROUPS") ? std::max(1, atoi(getenv("AV1R_PIPE_GROUPS"))) : 0;
+    P->G = std::min(groups ? groups : (n >= 8 ? 2 : 1), n);
     P->th.reserve(W);
     for (int w = 0; w < W; w++) P->th.emplace_back(worker, &R);
     *out = P;
@@ -383,7 +386,10 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
         output_s += secs(Clock::now() - o0);
         return r;
     };
-    const int G = P->G;
+    // (with a sink, one group: the read-backs share the group leads' upload streams, and two
+    // leads uploading left them seldom idle -- the delivery leg fell to 0.84-0.88x)
+    const int G = P->sink.acquire && !getenv("AV1R_PIPE_GROUPS") ? 1 : P->G;
+    if (P->g >= G) P->g = 0;
     static const double fillUs = getenv("AV1R_PIPE_WAIT_US") ? atof(getenv("AV1R_PIPE_WAIT_US")) : 300.0;
     while (live > 0 && rc == AV1R_OK) {
         bc.clear();
