@@ -272,3 +272,19 @@ def test_shipped_code_has_no_ashr_pk_u8(tmp_path):
         dis = subprocess.run([objdump, "-d", str(o)], capture_output=True, text=True, check=True, timeout=300).stdout
         assert "k_flow" in dis or "k_lr" in dis or "k_inter" in dis
         assert "v_ashr_pk_u8" not in dis, o.name
+
+
+def test_frame_layout_describes_one_linear_read_back(native_lib):
+    """av1r_frame_layout (include/av1r.h): the library's frame layout, which a read-back
+    destination copies to get one linear transfer per frame (the ring sink's slots).  Plane
+    offsets and strides are 256-byte aligned, planes do not overlap, and `span` reaches the
+    last visible byte of plane 2; a bad size is refused.  Host-only: no device needed."""
+    st, off, span = (C.c_int * 3)(), (C.c_size_t * 3)(), C.c_size_t()
+    for w, h in ((1920, 1080), (3840, 2160), (226, 226), (64, 66), (16, 16)):
+        assert native_lib.av1r_frame_layout(w, h, st, off, C.byref(span)) == 0
+        assert off[0] == 0 and all(o % 256 == 0 for o in off) and all(s % 256 == 0 for s in st)
+        assert st[0] >= w and st[1] == st[2] >= w >> 1
+        assert off[1] >= st[0] * h and off[2] >= off[1] + st[1] * (h >> 1)  # no overlap
+        assert span.value == off[2] + st[2] * ((h >> 1) - 1) + (w >> 1)
+    assert native_lib.av1r_frame_layout(0, 1080, st, off, C.byref(span)) == abi.AV1R_E_INVALID
+    assert native_lib.av1r_frame_layout(1920, 1 << 20, st, off, C.byref(span)) == abi.AV1R_E_INVALID
