@@ -1643,12 +1643,20 @@ static double now_us()
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+static bool deep_frame(const Prepared& P);
+
 static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 {
     const double tp0 = host_prof() ? now_us() : 0;
     double tp1 = tp0, tp2 = tp0;
     av1r_ctx* c = lc;  // errors are reported on the launching context
     const int n = (int)jobs.size();
+    // k_flow workgroups per CU for a deep frame launched by itself (a key frame through the
+    // per-frame API; the pipeline's solo frames take 1): fewer idle pollers along its long
+    // chain -- a 1080p key frame alone 1.84 ms at the default 8, 1.73 at 4, 1.69 at 3, 1.67
+    // at 2 (AV1R_DEEP_PER_CU; 0 = the context's own setting)
+    static const int deepPer = getenv("AV1R_DEEP_PER_CU") ? atoi(getenv("AV1R_DEEP_PER_CU")) : 2;
+    const int perCU = deepPer > 0 && n == 1 && deep_frame(*jobs[0].P) ? std::min(lc->flowPerCU, deepPer) : lc->flowPerCU;
     if (n > AV1R_MAX_BATCH) return fail(c, AV1R_E_INVALID, "at most %d frames per batch", AV1R_MAX_BATCH);
     ctx_join(lc);
     hipStream_t st = lc->stream;
@@ -1947,11 +1955,11 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             if (chain) lock.lock();
             // the persistent grid: every resident slot (lc->flowPerCU workgroups per CU; a
             // solo deep frame takes one per CU and leaves the rest to concurrent batches)
-            int grid = (int)std::min<size_t>(flow_grid(lc->device, lc->flowPerCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            int grid = (int)std::min<size_t>(flow_grid(lc->device, perCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             if (lc->flowGridCap > 0) grid = std::max(FLOW_QUEUES, std::min(grid, lc->flowGridCap / FLOW_QUEUES * FLOW_QUEUES));
             // per-wave small items: every resident slot, and at least one server per queue of
             // both populations (FLOW_LARGE_EVERY x FLOW_QUEUES workgroups, recon.hip)
-            if (nSmallItems) grid = std::max(64, std::max(grid, lc->flowGridCap > 0 ? std::min(flow_grid(lc->device, lc->flowPerCU), lc->flowGridCap) : flow_grid(lc->device, lc->flowPerCU)));
+            if (nSmallItems) grid = std::max(64, std::max(grid, lc->flowGridCap > 0 ? std::min(flow_grid(lc->device, perCU), lc->flowGridCap) : flow_grid(lc->device, perCU)));
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;

@@ -1910,9 +1910,9 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 // CU), a multiple of FLOW_QUEUES
 int flow_grid(int device, int maxPer)
 {
-    static int cache[64][2] = {};
+    static int cache[64][9] = {};  // per device and workgroups-per-CU bound (1..8)
     if (device < 0 || device >= 64) return FLOW_QUEUES;
-    const int slot = maxPer < 8 ? 1 : 0;
+    const int slot = maxPer < 1 ? 1 : (maxPer > 8 ? 8 : maxPer);
     if (!cache[device][slot]) {
         int cus = 0, per = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 32;
