@@ -57,6 +57,10 @@ struct FrameBuf {
     size_t bytes = 0;
     int refcnt = 0;
     uint64_t seq = 0;  // the owning context's frame sequence number of the launch that wrote it
+    // the launch that wrote it: its metadata slot and that slot's generation (slot_meta();
+    // a read-back ticket waits for exactly this launch, whatever the context did since)
+    const struct Upload* wMeta = nullptr;
+    uint64_t wGen = 0;
     DevFrame d;
 };
 
@@ -299,6 +303,7 @@ static std::vector<LaunchRec*> g_recPending, g_recFree;
 // packed frames (av1r_pack) released by their launches, for reuse by any packing thread
 static std::mutex g_packMu;
 static std::vector<av1r_packed*> g_packFree;
+static std::vector<av1r_packed*> g_packAll;  // every packed buffer ever allocated (under g_packMu)
 
 // Completion of a launch through its own meta slot (the one event every launch records on
 // its stream after its last kernel) instead of more events recorded after it: a launch
@@ -1724,8 +1729,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         M.pending = false;
         harvest(false);  // device errors reach their frames (av1r_get_output / av1r_synchronize)
     }
-    M.gen.fetch_add(1, std::memory_order_release);  // (waiters on this slot's previous launch see it finished)
-    lc->lastMeta = &M;
     // the launch's status record (k_flow launches only)
     LaunchRec* rec = nullptr;
     if (anyFlow) {
@@ -2052,9 +2055,18 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     }
     HIPCHK(hipGetLastError());
+    // the slot's generation moves on only once this launch is certain to record its event
+    // (an early return above leaves waiters on the slot's previous launch, which completed)
+    M.gen.fetch_add(1, std::memory_order_release);  // (waiters on this slot's previous launch see it finished)
+    lc->lastMeta = &M;
     HIPCHK(hipEventRecord(M.done, st));
     M.pending = true;
-    for (auto& j : jobs) job_end(j);
+    const uint64_t gen = M.gen.load(std::memory_order_relaxed);
+    for (auto& j : jobs) {
+        for (FrameBuf* f : {j.R, j.C, j.L})
+            if (f) f->wMeta = &M, f->wGen = gen;
+        job_end(j);
+    }
     if (rec) {
         rec->meta = slot_meta() ? &M : nullptr;
         rec->gen = M.gen.load(std::memory_order_relaxed);
@@ -2244,10 +2256,12 @@ void av1r_destroy(av1r_ctx* c)
                 }
             for (av1r_output_ticket* t : m->tickets)
                 if (t->readyMeta && mine(t->readyMeta)) t->readyMeta = nullptr;  // (ready: its event was never recorded)
+            for (FrameBuf* f : m->pool)
+                if (f->wMeta && mine(f->wMeta)) f->wMeta = nullptr;
         }
-        {
+        {  // every packed buffer: the pooled ones and those still held by their callers
             std::lock_guard<std::mutex> pl(g_packMu);
-            for (av1r_packed* q : g_packFree)
+            for (av1r_packed* q : g_packAll)
                 if (q->waitMeta && mine(q->waitMeta)) {
                     q->waitMeta = nullptr;
                     q->copyPending = false;
@@ -2548,12 +2562,19 @@ static av1r_packed* pack_buffer(size_t need)
         return pk;
     }
     pk = new (std::nothrow) av1r_packed;
-    if (!pk || !need) return pk;
+    if (!pk) return pk;
+    {
+        std::lock_guard<std::mutex> lock(g_packMu);
+        g_packAll.push_back(pk);
+    }
+    if (!need) return pk;
     g_packCount++;
     const size_t cap = (need + need / 4 + (1u << 20)) & ~(size_t)((1u << 20) - 1);
     pk->pinned = hipHostMalloc(&pk->host, cap, hipHostMallocDefault) == hipSuccess;
     if (!pk->pinned) pk->host = static_cast<uint8_t*>(malloc(cap));  // no device here (host-only use)
     if (!pk->host) {
+        std::lock_guard<std::mutex> lock(g_packMu);
+        g_packAll.erase(std::remove(g_packAll.begin(), g_packAll.end(), pk), g_packAll.end());
         delete pk;
         return nullptr;
     }
@@ -2899,7 +2920,7 @@ static bool out_sq()
     return on;
 }
 
-static int ticket_issue(av1r_output_ticket* t);
+static int ticket_issue(av1r_output_ticket* t, bool event = false);
 
 int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, uint8_t* v, int vs, int* width, int* height,
                           av1r_output_ticket** out)
@@ -2915,7 +2936,7 @@ int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, u
     static const bool eager = getenv("AV1R_OUT_EAGER") && atoi(getenv("AV1R_OUT_EAGER")) != 0;
     if (!rc && eager) {
         if (hipStreamWaitEvent(c->outStream, (*out)->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
-        if (!rc) rc = ticket_issue(*out);
+        if (!rc) rc = ticket_issue(*out, true);
     }
     return rc;
 }
@@ -2974,11 +2995,13 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     static const bool noReady = getenv("AV1R_OUT_NOREADY") && atoi(getenv("AV1R_OUT_NOREADY")) != 0;  // (A/B with NOCOPY)
     // the last launch on that stream has it (members join a batch stream behind their own
     // stream's work, ctx_join): its completion, or an event where a stream must wait on it
+    // (the frame's own launch: a show-existing frame, or a context joined since -- ctx_join
+    // clears joinLead without enqueuing work -- is not the context's last launch)
     av1r_ctx* w = c->joinLead ? c->joinLead : c;
     t->readyMeta = nullptr;
-    if (slot_meta() && !needEvent && w->lastMeta) {
-        t->readyMeta = w->lastMeta;
-        t->readyGen = w->lastMeta->gen.load(std::memory_order_relaxed);
+    if (slot_meta() && !needEvent && f->wMeta) {
+        t->readyMeta = f->wMeta;
+        t->readyGen = f->wGen;
     } else if (!noReady) {
         HIPCHK(hipEventRecord(t->ready, w->stream));
     }
@@ -3007,7 +3030,10 @@ static bool device_writable_host(const void* p)
     return a.type == hipMemoryTypeHost && a.devicePointer == p;
 }
 
-static int ticket_issue(av1r_output_ticket* t)
+// event: record the read-back's own completion instead of watching its stream go idle --
+// for a copy queued behind a device-side wait (prefetch staging, AV1R_OUT_EAGER), whose
+// stream also carries every later frame's wait and copy
+static int ticket_issue(av1r_output_ticket* t, bool event)
 {
     av1r_ctx* c = t->c;
     // AV1R_OUT_NOCOPY=1 (A/B of the delivery machinery alone): no bytes move
@@ -3040,7 +3066,7 @@ static int ticket_issue(av1r_output_ticket* t)
         for (int p = 0; p < 3; p++)
             HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], src[p], ss[p], w[p], h[p], hipMemcpyDeviceToHost, c->outStream));
     }
-    t->sq = out_sq();
+    t->sq = out_sq() && !event;
     if (!t->sq) HIPCHK(hipEventRecord(t->done, c->outStream));
     t->state = 1;
     return AV1R_OK;
@@ -3153,7 +3179,7 @@ static int stage_outputs(av1r_ctx* c)
         uint8_t* u = S.buf + (size_t)w * h;
         int rc = output_ticket(c, S.buf, w, u, cw, u + (size_t)cw * ch, cw, nullptr, nullptr, &S.t, true);
         if (!rc && hipStreamWaitEvent(c->outStream, S.t->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
-        if (!rc) rc = ticket_issue(S.t);
+        if (!rc) rc = ticket_issue(S.t, true);
         if (rc) {
             if (S.t) (void)av1r_output_wait(S.t);
             c->stageFree.push_back({S.buf, S.cap});

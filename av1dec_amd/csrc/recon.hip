@@ -1718,7 +1718,10 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     trace_stamp(tr, 2);
     trace_put(tr, 0, wi.code);
     trace_put(tr, 1, ((unsigned long long)s << 32) | ((unsigned)wi.tx_size << 8) | wi.pred);
-    trace_put(tr, 7, ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 16) | wi.dep_cnt);
+    // (HW_ID in the upper half: wave, SIMD, CU, SH, SE of the wave -- tools/trace_run.py's
+    // per-slot occupancy)
+    trace_put(tr, 7, ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32) |
+                         ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 16) | wi.dep_cnt);
 #else
     unsigned long long* tr = nullptr;
     (void)trace;

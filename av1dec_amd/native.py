@@ -304,6 +304,7 @@ def hip():
         h.hipMemcpyAsync.argtypes = [vp, vp, C.c_size_t, C.c_int, vp]
         h.hipSetDevice.argtypes = [C.c_int]
         h.hipDeviceSynchronize.argtypes = []
+        h.hipDeviceGetPCIBusId.argtypes = [C.c_char_p, C.c_int, C.c_int]
         _hip = h
     return _hip
 

@@ -257,13 +257,89 @@ def ivf_leg(decs, streams, frames, size="1920x1080", name="1080p_s1", seed=0x5EE
                         f"the timed region"}
 
 
+_RANK_CPUS = None  # this rank's CPU set once bind_rank_cpus has bound it (N > 1)
+
+
 def host_workers():
     """Packing threads: the box's CPU share (OMP_NUM_THREADS is set to it there) less the
-    launching thread (AV1R_BENCH_WORKERS overrides, A/B)."""
+    launching thread (AV1R_BENCH_WORKERS overrides, A/B).  A rank bound to its own CPUs
+    (bind_rank_cpus, N > 1) takes its share of them: the node's CPUs divided by the ranks
+    on that node."""
     if os.environ.get("AV1R_BENCH_WORKERS"):
         return int(os.environ["AV1R_BENCH_WORKERS"])
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    if _RANK_CPUS is not None:
+        share = len(_RANK_CPUS)
     return max(1, min(share, 32) - 1)
+
+
+def parse_cpulist(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11] (sysfs cpulist format)."""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_numa_node(local):
+    """NUMA node of GPU `local`: its PCI bus id from the HIP runtime, then sysfs
+    (/sys/bus/pci/devices/<id>/numa_node); -1 when unknown."""
+    try:
+        import ctypes as C
+        from av1dec_amd import native
+        h = native.hip()
+        buf = C.create_string_buffer(64)
+        if h.hipDeviceGetPCIBusId(buf, 64, int(local)) != 0:
+            return -1
+        bus = buf.value.decode().lower()
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            return int(f.read().strip())
+    except Exception:
+        return -1
+
+
+def split_rank_cpus(allowed, nodes, rank, node_cpus):
+    """This rank's CPUs: the allowed CPUs of its GPU's NUMA node (all allowed CPUs when the
+    node is unknown or none of its CPUs is allowed), divided evenly among the ranks whose GPUs
+    sit on that node.  nodes: every rank's node; node_cpus(n) -> the CPUs of node n."""
+    node = nodes[rank]
+    pool = sorted(allowed)
+    if node >= 0:
+        local = [c for c in pool if c in set(node_cpus(node))]
+        pool = local or pool
+    peers = [r for r in range(len(nodes)) if nodes[r] == node]
+    k, i = len(peers), peers.index(rank)
+    chunk = pool[i * len(pool) // k:(i + 1) * len(pool) // k]
+    return chunk or [pool[i % len(pool)]]
+
+
+def bind_rank_cpus(rank, world, local, dist, probe_gpu=True):
+    """host threads near the GPU's NUMA node, one rank's threads apart from the
+    others'.  Rank r binds itself (and every thread it starts later: the native pipeline's
+    packing and parse threads inherit the affinity) to its share of GPU r's node
+    (split_rank_cpus), so 8 ranks of packers do not contend for the same cores.  N = 1 keeps
+    the process's affinity (AV1R_BIND=1 binds it too)."""
+    global _RANK_CPUS
+    if world <= 1 and os.environ.get("AV1R_BIND", "0") == "0":
+        return None
+    node = gpu_numa_node(local) if probe_gpu else -1
+    nodes = [node]
+    if dist:
+        nodes = [None] * world
+        dist.all_gather_object(nodes, node)
+
+    def node_cpus(n):
+        try:
+            return parse_cpulist(open(f"/sys/devices/system/node/node{n}/cpulist").read())
+        except OSError:
+            return []
+    cpus = split_rank_cpus(os.sched_getaffinity(0), nodes, rank if dist else 0, node_cpus)
+    os.sched_setaffinity(0, cpus)
+    _RANK_CPUS = cpus
+    return {"numa_node": node, "cpus": cpus}
 
 
 def copy_peak_gbps(local):
@@ -357,7 +433,7 @@ def load_traffic(path, config, S, stage):
     return None, None
 
 
-def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, prime_s=2.0):
+def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, prime_s=2.0, prime_steps=None):
     """One configuration's rates on this rank's streams: the host-inclusive pipeline (the
     headline), the device-only rate, and the per-stage device time with the roofline of the
     dominant stage.  Returns (result dict, the StreamScheduler over prepared handles, the
@@ -372,7 +448,8 @@ def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, p
     # ---- headline: the host-inclusive pipeline (per-frame validation, scheduling, packing
     # and PCIe upload of the synthetic batches inside the timed region, overlapped with the
     # GPU).  Setup (untimed): stream j brought to its own GOP phase, a priming pass of
-    # ~prime_s, then the warmup steps.  (av1r_pipeline_run: producer threads pack each
+    # ~prime_s (or exactly prime_steps GOPs: a fixed amount of work, so that separate
+    # profiling passes run the same launches), then the warmup steps.  (av1r_pipeline_run: producer threads pack each
     # stream's frames ahead, the calling thread launches one frame of every ready stream per
     # batch)
     pp = StreamScheduler(decs, F, streams=streams, workers=1)
@@ -388,9 +465,13 @@ def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, p
     from av1dec_amd.pipeline import NativePipeline
     pl = NativePipeline(decs, streams, pos, depth=depth, workers=workers)
     try:
-        t_prime = time.perf_counter()
-        while time.perf_counter() - t_prime < prime_s:
-            pl.step(F)
+        if prime_steps is not None:
+            for _ in range(prime_steps):
+                pl.step(F)
+        else:
+            t_prime = time.perf_counter()
+            while time.perf_counter() - t_prime < prime_s:
+                pl.step(F)
         pl.step(warmup)
         if dist:
             dist.barrier()
@@ -472,7 +553,8 @@ def key_frame_ms(dec, handle, reps=3):
     return {"recon": round(m[0], 4), "lf": round(m[1], 4), "cdef": round(m[2], 4), "lr": round(m[3], 4)}
 
 
-def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, traffic=None, ivf_frames=8):
+def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, traffic=None, ivf_frames=8,
+           prime_steps=None):
     """BASELINE configs[3]: S synthetic 3840x2160 streams with the 4x2 tile grid per GPU,
     host-inclusive and device-only, with its own per-stage times, roofline and PMC traffic."""
     from concurrent.futures import ThreadPoolExecutor
@@ -485,7 +567,8 @@ def leg_4k(local, rank, world, dist, workers, S=2, F=30, steps=12, warmup=3, tra
     decs = [Decoder(local, keep_stages=False, timing=False) for _ in range(S)]
     for d in decs:
         d.set_discard_output(True)
-    r, ss, handles, _ = measure("4k", decs, streams, steps, warmup, workers, 0, dist, world, prime_s=0.5)
+    r, ss, handles, _ = measure("4k", decs, streams, steps, warmup, workers, 0, dist, world, prime_s=0.5,
+                                prime_steps=prime_steps)
     kf = key_frame_ms(decs[0], handles[0][0], reps=2)
     tr, tsrc = load_traffic(traffic, "4k", S, r["dominant"]) if traffic else (None, None)
     for d, hs in zip(decs, handles):
@@ -569,6 +652,7 @@ def dry_run(args, rank, world, dist):
     rank's stream ids and a digest of its shard's batches (gathered for the report only)."""
     import hashlib
     S = max(1, args.streams)
+    bound = bind_rank_cpus(rank, world, int(os.environ.get("LOCAL_RANK", "0")), dist, probe_gpu=False)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -579,7 +663,8 @@ def dry_run(args, rank, world, dist):
             h.update(f.to_bytes())
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
-            "stream_ids": rank_stream_ids(rank, S), "digest": h.hexdigest()}
+            "stream_ids": rank_stream_ids(rank, S), "digest": h.hexdigest(),
+            "cpus": bound["cpus"] if bound else sorted(os.sched_getaffinity(0)), "host_workers": host_workers()}
     shards = [mine]
     if dist:
         shards = [None] * world
@@ -607,6 +692,9 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per frame (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-4k", default=os.path.join(ROOT, "profiles", "traffic_4k.json"))
+    ap.add_argument("--prime-steps", type=int, default=None,
+                    help="priming GOPs of the headline pipeline (default: ~2 s of them); a fixed count gives "
+                         "every rocprofv3 --pmc pass the same work (tools/gpu_evidence_r05.sh)")
     ap.add_argument("--dry-run", action="store_true",
                     help="the N-rank launch and sharding only, no GPU (tests/test_multi.py)")
     args = ap.parse_args()
@@ -634,6 +722,8 @@ def main():
     from av1dec_amd import Decoder, native
 
     native.lib()
+    # before any thread of ours starts: the rank's share of its GPU's NUMA node
+    bound = bind_rank_cpus(rank, world, local, dist)
     W, H, tiles, seed = CONFIGS[args.config]
     S = max(1, args.streams)
     F = args.frames
@@ -652,7 +742,8 @@ def main():
         for d in decs:
             d.synchronize()
 
-    r, ss, handles, pos = measure(args.config, decs, streams, args.steps, args.warmup, workers, depth, dist, world)
+    r, ss, handles, pos = measure(args.config, decs, streams, args.steps, args.warmup, workers, depth, dist, world,
+                                  prime_steps=args.prime_steps)
     fps, elapsed = r["fps"], r["elapsed"]
     dominant, achieved, per_frame_ms, sb = r["dominant"], r["achieved"], r["per_frame_ms"], r["stage_bytes"]
     traffic, traffic_src = load_traffic(args.traffic, args.config, S, dominant)
@@ -728,7 +819,7 @@ def main():
     k4 = None
     if args.config == "1080p" and not args.no_4k:
         k4 = leg_4k(local, rank, world, dist, workers, traffic=args.traffic_4k,
-                    ivf_frames=min(args.ivf_frames, 8))
+                    ivf_frames=min(args.ivf_frames, 8), prime_steps=args.prime_steps)
 
     copy_peak = None
     try:
@@ -802,6 +893,8 @@ def main():
                                    f"frames after the window while it runs; key frames run alone on their stream, overlapping "
                                    f"the other streams' batches); timed frames: {args.steps * S} of which {r['n_key']} key",
                        "host_threads": workers + 1,
+                       "cpus_per_rank": len(bound["cpus"]) if bound else None,
+                       "rank0_numa_node": bound["numa_node"] if bound else None,
                        "timed_key_frames": r["n_key"],
                        "streams_per_gpu": S, "frames_per_step": S,
                        "parallelism": f"stream-per-GPU x{world}"},

@@ -296,3 +296,61 @@ def test_gpu_ring_sink_frames_match_oracle():
         sink.close()
         for d in decs:
             d.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpu_sink_delivers_show_existing_frames():
+    """Frame delivery of show_existing_frame units in shared launches (advisor r04): the writer's
+    cif_hidden stream (hidden frames, then show_existing_frame units) on four contexts at
+    staggered phases through the native pipeline with an output sink, so that a stream's
+    show-existing entry is applied after its frames ran in batches led by other contexts, and
+    sometimes while it led a batch itself.  A read-back ticket must wait for the launch that
+    wrote the shown frame (FrameBuf::wMeta), not for the context's last launch: every delivered
+    frame equals the CPU oracle's.  Reference: Decoder::showExistingFrame
+    (decoder/Av1Decoder.cpp:158-169)."""
+    import bench
+    from av1dec_amd import Decoder, parser
+    from av1dec_amd.pipeline import NativePipeline
+    import pybsw
+    import pyoracle
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "bsw.json")))["cif_hidden"]
+    frames = parser.Parser().decode_ivf(pybsw.stream_ivf("cif_hidden", seed=gold["seed"]))
+    F, S = len(frames), 4
+    assert any(f.show_existing for f in frames)
+    # the oracle over two cycles: the outputs each entry produces (frame 0 refreshes every slot)
+    o = pyoracle.Oracle(keep_stages=False)
+    per_entry = []
+    try:
+        for f in frames + frames:
+            o.decode_frame(f)
+            outs = []
+            while o.output_pending():
+                outs.append(_frame_md5(o.get_output()))
+            per_entry.append(outs)
+    finally:
+        o.close()
+    offs = [1 + j * (F - 2) // S for j in range(S)]
+    decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+    ds = _DigestSink(S)
+    try:
+        for j, d in enumerate(decs):  # each stream alone to its phase, outputs drained
+            for f in frames[:offs[j]]:
+                d.decode_frame(f)
+            while d.output_pending():
+                d.get_output()
+        pl = NativePipeline(decs, [frames] * S, offs, depth=0, workers=bench.host_workers())
+        try:
+            pl.set_output(ds.sink)
+            assert pl.step(F)["frames"] == S * F
+            pl.set_output(None)
+        finally:
+            pl.close()
+        assert all(d.output_pending() == 0 for d in decs)
+    finally:
+        for d in decs:
+            d.close()
+    for j in range(S):
+        want = [m for e in range(offs[j], offs[j] + F) for m in per_entry[e]]
+        assert ds.sink.status[j] == [0] * len(want)
+        assert ds.md5[j] == want, f"stream {j}"

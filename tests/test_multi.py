@@ -146,6 +146,26 @@ def test_bench_gpus_2_launches_two_ranks():
     assert sh[0]["pid"] != sh[1]["pid"]  # two processes
     assert sh[0]["stream_ids"] == list(range(8)) and sh[1]["stream_ids"] == list(range(8, 16))
     assert sh[0]["digest"] != sh[1]["digest"]  # different streams
+    # each rank's host threads on CPUs of its own (the pipeline's threads inherit them)
+    c0, c1 = set(sh[0]["cpus"]), set(sh[1]["cpus"])
+    assert c0 and c1 and not c0 & c1
+    assert c0 | c1 <= set(os.sched_getaffinity(0))
+    assert all(s["host_workers"] == max(1, min(len(s["cpus"]), 32) - 1) for s in sh)
+
+
+def test_rank_cpu_split_by_numa_node():
+    """bench.split_rank_cpus: ranks whose GPUs share a NUMA node divide that node's allowed CPUs;
+    a rank alone on its node takes all of them; an unknown node (-1) shares the allowed set."""
+    node = {0: list(range(0, 8)), 1: list(range(8, 16))}.get
+    allowed = set(range(16))
+    nodes = [0, 0, 1, 1, 1, 0]
+    sets = [bench.split_rank_cpus(allowed, nodes, r, node) for r in range(6)]
+    assert sets[0] == [0, 1] and sets[1] == [2, 3, 4] and sets[5] == [5, 6, 7]
+    assert sets[2] == [8, 9] and sets[3] == [10, 11, 12] and sets[4] == [13, 14, 15]
+    assert bench.split_rank_cpus(allowed, [1], 0, node) == list(range(8, 16))
+    assert bench.split_rank_cpus({0, 1}, [1, 1], 1, node) == [1]  # node not allowed: the allowed set
+    assert bench.split_rank_cpus(set(range(4)), [-1, -1], 0, node) == [0, 1]
+    assert bench.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
 
 
 def test_bench_gpus_mismatch_is_refused():

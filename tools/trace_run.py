@@ -195,6 +195,49 @@ def summarise_flow(path, lo=0, hi=None):
         print(f"  t={us(edges[i] - f0):7.0f} us  waiting {wait[i]:6.0f}  working {work[i]:6.0f}")
 
 
+def summarise_slots(path, lo=0, hi=None):
+    """Where a batched k_flow launch's wave-time goes (lite timeline: every stamp is the time the
+    wave REACHED that point).  Per wave slot (HW_ID + XCC id of stamp 7) the items it ran in
+    entry order; the launch span split, summed over slots, into: between items (ticket atomic,
+    group load, the group's barrier: the slowest of the group's four items), setup (record,
+    block, residual prefetch, fi_setup: 2 -> 3), dependency wait (3 -> 4), edge gather incl.
+    granule polls (4 -> 8), prediction (8 -> 9), store (9 -> 10), publish (10 -> 5)."""
+    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
+    a = a[lo // 128: (hi // 128 if hi else None)]
+    code = a[:, 0]
+    kind = code >> 30
+    a = a[(a[:, 2] != 0) & (kind != 1)]
+    if not len(a):
+        return
+    t2, t3, t4, t5, t8, t9, t10 = (a[:, i] for i in (2, 3, 4, 5, 8, 9, 10))
+    x7 = a[:, 7].astype(np.uint64)
+    slot = (x7 >> np.uint64(16))  # HW_ID << 16 | XCC
+    us = lambda x: x / 100.0
+    span = t5.max() - t2.min()
+    slots = np.unique(slot)
+    between = 0
+    gaps = []
+    for s_ in slots:
+        m = np.flatnonzero(slot == s_)
+        o = m[np.argsort(t2[m])]
+        g = t2[o[1:]] - t5[o[:-1]]
+        gaps.append(g)
+        between += g.clip(min=0).sum()
+    gaps = np.concatenate(gaps) if gaps else np.zeros(1)
+    have = (t8 > 0) & (t9 > 0) & (t10 > 0)
+    tot = len(slots) * span
+    parts = {"setup 2->3": (t3 - t2).sum(), "dep wait 3->4": (t4 - t3).sum(),
+             "gather 4->8": np.where(have, t8 - t4, 0).sum(), "predict 8->9": np.where(have, t9 - t8, 0).sum(),
+             "store 9->10": np.where(have, t10 - t9, 0).sum(), "publish 10->5": np.where(have, t5 - t10, 0).sum(),
+             "other paths 4->5": np.where(have, 0, t5 - t4).sum(), "between items": between}
+    print(f"k_flow slots: {len(slots)} wave slots seen, {len(a)} items ({len(a) / len(slots):.1f} per slot), "
+          f"span {us(span):.1f} us; per item p50 {np.median(us(t5 - t2)):.2f} us, gap between a slot's items "
+          f"p50 {np.median(us(gaps)):.2f} p90 {np.percentile(us(gaps), 90):.2f} us")
+    for k, v in parts.items():
+        print(f"   {k:18s} {v / tot:6.1%} of slot-time  ({us(v) / len(a):6.2f} us per item)")
+    print(f"   {'idle (after last)':18s} {1 - sum(parts.values()) / tot:6.1%}")
+
+
 if __name__ == "__main__":
     nfr = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "trace.bin")
@@ -206,5 +249,6 @@ if __name__ == "__main__":
         summarise_flow(path, sizes[0], sizes[1])
         print("=== last step ===")
         summarise_flow(path, sizes[-2], sizes[-1])
+        summarise_slots(path, sizes[-2], sizes[-1])
     else:
         summarise(path)
