@@ -118,10 +118,7 @@ struct KParams {
     uint64_t* gran_v[3];
     int gran_w[3], gran_hn[3];
     int gran;
-    // k_strip (build_strips): this frame's items run one strip per workgroup, same-strip
-    // pixels read from the strip's LDS ring, the frame stored plainly
-    int strip;
-    int fi;  // k_flow / k_strip: small intra TBs take the lean path (intra_fast.h; AV1R_FI=0: off)
+    int fi;  // k_flow: small intra TBs take the lean path (intra_fast.h; AV1R_FI=0: off)
     uint32_t n_items;
     uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;
@@ -155,15 +152,7 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the launch's pinned host error word
 #define FLOW_SPINLIM (FLOW_ERR + 4)  // polls before a wait gives up (0: FLOW_SPINS)
 #define FLOW_ASSIGN (FLOW_ERR + FLOW_LINE)  // workgroup entries: entry k serves queue k % FLOW_QUEUES
-// per-wave small-item queues (AV1R_FLOW_WAVE): FLOW_QUEUES more heads, one line each
-#define FLOW_SMALLQ (FLOW_ASSIGN + FLOW_LINE)
-#define FLOW_CTL_BYTES (4 * (FLOW_SMALLQ + FLOW_QUEUES * FLOW_LINE))
-// k_strip: luma rows per strip (one workgroup each; chroma strips are the same rows at 4:2:0).
-// 64 = the largest transform side, so no transform block spans two strips
-#define AV1R_STRIP_H 64
-// k_strip: columns of a strip kept in its LDS ring (luma; chroma half): 64 x 512 + 2 x 32 x 256
-// = 48 KB.  The host checks that no ring cell is overwritten before its last read
-#define AV1R_RING_W 512
+#define FLOW_CTL_BYTES (4 * (FLOW_ASSIGN + FLOW_LINE))
 // k_flow spin bound, in polls of running waves (each a global load round trip, ~0.5-2 us),
 // not in wall-clock time: a wave that the hardware preempts (context save / restore) does
 // not count the time it was off the chip, so only a wait that makes no progress WHILE
@@ -223,7 +212,7 @@ DEV void coop_sync()
 // Wave-uniform reads of data no kernel of the launch writes (the batch's records, the
 // spec tables) through the scalar cache.  A global_load of a uniform value is a VECTOR
 // memory op: its s_waitcnt vmcnt counts every store the wave issued before it (gfx9 keeps
-// loads and stores in one in-order counter), so in k_flow / k_strip each record or table
+// loads and stores in one in-order counter), so in k_flow each record or table
 // read after an item's pixel stores waited for those stores to reach L2.  s_load (address
 // space 4, lgkmcnt) does not.  Only for data final before the launch: the scalar cache is
 // not coherent with vector stores (a dispatch's acquire invalidates it).
@@ -324,16 +313,12 @@ DEV void stp_c(const DevPlane& p, int x, int y, uint8_t v, bool coh)
 // THE INVARIANT of the dataflow kernels.  k_flow: every read of a pixel that another item
 // of the same launch may have written goes through the sc1 accessors (ldp<true> /
 // ldp4<true>) or a granule, and every such pixel is stored sc1 -- a plain load could return
-// a stale line from this CU's L1 (cdna_hip_programming.md §6 Guideline 16).  k_strip
-// (KParams::strip): such a pixel is either another strip's, read as a granule, or this
-// strip's, read from the workgroup's LDS ring behind the barrier that ended its writer's
-// group; the frame itself is then only written in the launch (plain stores), never read
-// for an in-launch pixel.  Checklist for a new read site in recon.hip's AV1R_FLOW_PART code
-// (k_flow, k_strip): (1) can another item of this launch have written the pixel?  If not
-// (batch data, reference frames, pixels final before the launch), any load will do.  (2) If
-// so: in k_flow it is read through ldp<true>/ldp4<true> (or ldp_c/ldp4_c with coh = true) or
-// arrives in a granule, after the wait that orders it; in k_strip it is a granule (another
-// strip's) or a ring read (this strip's).  (3) Its writer stores it sc1 in k_flow (stp4<true>,
+// a stale line from this CU's L1 (cdna_hip_programming.md §6 Guideline 16).  Checklist for a
+// new read site in recon.hip's AV1R_FLOW_PART code (k_flow): (1) can another item of this
+// launch have written the pixel?  If not (batch data, reference frames, pixels final before
+// the launch), any load will do.  (2) If so: it is read through ldp<true>/ldp4<true> (or
+// ldp_c/ldp4_c with coh = true) or arrives in a granule, after the wait that orders it.
+// (3) Its writer stores it sc1 (stp4<true>,
 // stp_c with coh), and publishes a granule or a done flag if a consumer's wait names it.
 // The read sites today: gran_gather (intra_dev.h), tb_predict's CFL luma, fi_run's CFL
 // luma (intra_fast.h) and ii_item's edges and inter prediction (recon.hip); each is marked
@@ -344,7 +329,6 @@ DEV void stp_c(const DevPlane& p, int x, int y, uint8_t v, bool coh)
 // filter-intra); the other units are read without a wait and may be stale or half-written,
 // and no predicted pixel depends on them.  A predictor that starts reading a sample its mode
 // did not read before must widen intra_needs first.
-DEV bool strip_plain(int kstrip, bool gran) { return kstrip && gran; }  // (k_strip runs only with granules)
 
 // Work-item encoding of the per-level item lists (host schedule -> k_level):
 // bits 31..30 kind, 29..0 index (TB index; block index for inter-intra blends;

@@ -45,10 +45,8 @@ uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset);
 #endif
 int flow_grid(int device, int maxPer);
 void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s);
-void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t nSmall, uint32_t* ctl, uint32_t* hostErr,
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s);
-void launch_k_strip(const KParams* kps, const void* groups, const uint32_t* stripStart, uint32_t nStrips, uint32_t* ctl,
-    uint32_t epoch, unsigned long long* trace, hipStream_t s);
 
 namespace {
 
@@ -110,9 +108,6 @@ struct Prepared {
     uint64_t bytes = 0;    // the packed layout (incl. the device-filled mode-info grid)
     size_t upBytes = 0;    // its uploaded prefix
     bool offsets = false;  // packed in host memory: base pointers are offsets into the upload
-    // k_strip schedule (deep frames; empty: k_flow): {n, first item} pairs per group and the
-    // strips' group ranges (av1r_ctx::stripGroups / stripStart)
-    std::vector<uint32_t> stripGroups, stripStart;
 };
 
 // A frame validated, scheduled and packed into (pinned) host memory by av1r_pack, on any
@@ -231,12 +226,6 @@ struct av1r_ctx {
     // item of the launch); granOk = every such unit a consumer reads has its granule
     std::vector<uint32_t> nodeMask;
     bool granOk = false;
-    // k_strip (deep frames, build_strips): one workgroup per 64-row strip runs the strip's
-    // groups in level order; stripGroups = {n, first item} pairs, strip s's groups at
-    // [stripStart[s], stripStart[s + 1]); itemStrip per item position
-    bool stripMode = false;
-    std::vector<uint32_t> stripGroups, stripStart;
-    std::vector<uint16_t> itemStrip;
     uint64_t* granDev = nullptr;
     size_t granCap = 0;  // bytes
     // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
@@ -670,192 +659,15 @@ struct PackClock {
 };
 
 // the filters fused into one kernel (av1r_set_filter_fusion; AV1R_FUSED=1)
-// the lean small-intra path of k_flow / k_strip (intra_fast.h); AV1R_FI=0 or
+// the lean small-intra path of k_flow (intra_fast.h); AV1R_FI=0 or
 // av1r_set_fast_intra(0): the generic path (A/B)
 static bool inter_split()
 {
     static const bool on = getenv("AV1R_INTER_SPLIT") && atoi(getenv("AV1R_INTER_SPLIT")) != 0;
     return on;
 }
-// k_flow's small items served per wave (av1r_set_flow_wave; AV1R_FLOW_WAVE)
-static std::atomic<int> g_flowWave{getenv("AV1R_FLOW_WAVE") ? atoi(getenv("AV1R_FLOW_WAVE")) : 0};
 static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) : 1};
 static std::atomic<int> g_fusedFilters{getenv("AV1R_FUSED") ? atoi(getenv("AV1R_FUSED")) : 0};
-
-// ------------------------------------------------------------------------------------
-// k_strip schedule of a deep frame (recon.hip, k_strip)
-// ------------------------------------------------------------------------------------
-// A key frame's intra TBs form a wavefront ~2 000 levels deep at 1080p.  On k_flow every
-// hop of that chain is a hand-off between workgroups on arbitrary CUs (a granule or flag
-// round trip through the device coherence point, ~3.4 us per level measured).  k_strip
-// instead gives each 64-row strip of the frame (AV1R_STRIP_H luma rows, the same rows of
-// chroma at 4:2:0) to ONE workgroup, which runs the strip's groups (one large item or up to
-// four small ones, as k_flow's) in level order, separated by its barrier, and keeps the
-// strip's reconstructed pixels in an LDS ring of AV1R_RING_W columns: an edge or CFL read
-// inside the strip is an LDS read of a pixel an earlier group wrote.  Only what crosses a
-// strip boundary -- the row above the strip's first row, below-left columns reaching into
-// the next strip -- keeps k_flow's granule hand-off.  Built after the k_flow schedule; the
-// frame keeps k_flow unless every condition holds:
-//   - granules (c->granOk) and nothing but intra / palette TBs (an intra frame: no inter
-//     tile, blend or inter TB, whose pixels the ring would not hold);
-//   - no dependency-list entry across strips (an intra frame's lists hold only CFL's luma,
-//     the same block's, hence the same strip's);
-//   - the ring never loses a pixel still to be read: simulated group by group, every ring
-//     cell read holds the column the reader wants (AV1R_RING_W columns of the strip are
-//     live at once; a strip's level order keeps its rows within a few hundred columns).
-// Then every item's edge mask words lose their same-strip units (read from the ring), the
-// owners of the units still masked -- read by the next or previous strip -- get pub bit 1
-// (they publish granules; the others skip it), and the frame's groups are listed per strip.
-// (default 0 = off until k_strip beats k_flow: 12.8 vs 6.9 ms per 1080p key frame, r03)
-static std::atomic<int> g_stripLevels{getenv("AV1R_STRIP_LEVELS") ? atoi(getenv("AV1R_STRIP_LEVELS")) : 0};
-
-static void build_strips(av1r_ctx* c, const av1r_frame_batch* b)
-{
-    c->stripMode = false;
-    const size_t ni = c->items.size();
-    const av1r_frame_hdr* h = b->hdr;
-    static const bool dbg = getenv("AV1R_STRIP_DEBUG") != nullptr;
-    auto bail = [&](const char* why) {
-        if (dbg) fprintf(stderr, "av1r strips: off (%s)\n", why);
-    };
-    if (!c->granOk) return bail("no granules");
-    for (const WorkItem& w : c->items)
-        if (AV1R_ITEM_KIND(w.code) != AV1R_ITEM_TB || w.pred == AV1R_PRED_INTER) return bail("not an intra frame");
-    const uint32_t nStrips = (uint32_t)(h->mi_rows * 4 + AV1R_STRIP_H - 1) / AV1R_STRIP_H;
-    std::vector<uint16_t>& st = c->itemStrip;
-    st.assign(ni, 0);
-    for (size_t i = 0; i < ni; i++) {
-        const WorkItem& w = c->items[i];
-        st[i] = (uint16_t)std::min<uint32_t>(((uint32_t)w.y << (w.plane ? 1 : 0)) / AV1R_STRIP_H, nStrips - 1);
-    }
-    // groups, strip by strip, each strip's in level order: a large item alone, small items of
-    // one level and strip by four (adjacent: build_schedule sorted them by strip)
-    std::vector<uint32_t> cnt(nStrips + 1, 0);
-    auto walk = [&](auto&& emit) {
-        for (const Level& L : c->levels) {
-            for (uint32_t q = 0; q < L.fcnt[1]; q++) emit(st[L.off[1] + q], 0u, L.off[1] + q);
-            for (uint32_t q = 0; q < L.fcnt[2];) {
-                const uint32_t pos = L.off[2] + q, s = st[pos];
-                uint32_t n = 1;
-                while (n < 4 && q + n < L.fcnt[2] && st[pos + n] == s) n++;
-                emit(s, n, pos);
-                q += n;
-            }
-        }
-    };
-    walk([&](uint32_t s, uint32_t, uint32_t) { cnt[s + 1]++; });
-    for (uint32_t s = 0; s < nStrips; s++) cnt[s + 1] += cnt[s];
-    std::vector<uint32_t> start = cnt, groups(2 * (size_t)cnt[nStrips], 0);
-    walk([&](uint32_t s, uint32_t n, uint32_t pos) {
-        const uint32_t g = cnt[s]++;
-        groups[2 * g] = n;
-        groups[2 * g + 1] = pos;
-    });
-    // the ring simulation: per strip and plane, cell (unit row in the strip, unit column mod
-    // the ring) = the unit column it holds (-1: none yet)
-    const int ringU[3] = {AV1R_RING_W / 4, AV1R_RING_W / 8, AV1R_RING_W / 8};
-    const int rowsU[3] = {AV1R_STRIP_H / 4, AV1R_STRIP_H / 8, AV1R_STRIP_H / 8};
-    std::vector<int32_t> cell[3];
-    bool ringOk = true;
-    for (uint32_t s = 0; s < nStrips && ringOk; s++) {
-        for (int p = 0; p < 3; p++) cell[p].assign((size_t)ringU[p] * rowsU[p], -1);
-        auto inStrip = [&](int p, int uy) { return uy >= (int)s * rowsU[p] && uy < ((int)s + 1) * rowsU[p]; };
-        auto rd = [&](int p, int ux, int uy) {
-            if (!inStrip(p, uy)) return;
-            if (cell[p][(size_t)(uy - s * rowsU[p]) * ringU[p] + (ux & (ringU[p] - 1))] != ux) ringOk = false;
-        };
-        for (uint32_t g = start[s]; g < start[s + 1] && ringOk; g++) {
-            const uint32_t n = std::max<uint32_t>(groups[2 * g], 1), pos0 = groups[2 * g + 1];
-            for (uint32_t q = 0; q < n; q++) {  // every read of the group, then its writes
-                const WorkItem& w = c->items[pos0 + q];
-                if (w.pred != AV1R_PRED_INTRA) continue;
-                const int p = w.plane, sub = p ? 1 : 0, x = w.x, y = w.y;
-                const int tw = av1r_tx_w[w.tx_size], th = av1r_tx_h[w.tx_size];
-                const bool hL = w.flags & AV1R_TB_HAVE_LEFT, hA = w.flags & AV1R_TB_HAVE_ABOVE;
-                const bool hAR = w.flags & AV1R_TB_HAVE_AR, hBL = w.flags & AV1R_TB_HAVE_BL;
-                const int maxX = ((h->mi_cols * 4) >> sub) - 1, maxY = ((h->mi_rows * 4) >> sub) - 1;
-                if (hA)
-                    for (int ux = x >> 2; ux <= std::min(maxX, x + (hAR ? 2 * tw : tw) - 1) >> 2; ux++) rd(p, ux, (y - 1) >> 2);
-                if (hL)
-                    for (int uy = y >> 2; uy <= std::min(maxY, y + (hBL ? 2 * th : th) - 1) >> 2; uy++) rd(p, (x - 1) >> 2, uy);
-                if (hA && hL) rd(p, (x - 1) >> 2, (y - 1) >> 2);
-                const av1r_block& blk = b->blocks[w.block];
-                if (p && blk.uv_mode == AV1R_UV_CFL_PRED) {  // tb_predict's co-located luma
-                    const int lx1 = std::min(2 * (x + tw) - 1, blk.max_luma_w - 1), ly1 = std::min(2 * (y + th) - 1, blk.max_luma_h - 1);
-                    for (int uy = (2 * y) >> 2; uy <= ly1 >> 2; uy++)
-                        for (int ux = (2 * x) >> 2; ux <= lx1 >> 2; ux++) rd(0, ux, uy);
-                }
-            }
-            for (uint32_t q = 0; q < n; q++) {
-                const WorkItem& w = c->items[pos0 + q];
-                const int p = w.plane;
-                const int tw = av1r_tx_w[w.tx_size], th = av1r_tx_h[w.tx_size];
-                for (int uy = w.y >> 2; uy < (w.y + th) >> 2; uy++)
-                    for (int ux = w.x >> 2; ux < (w.x + tw) >> 2; ux++)
-                        if (inStrip(p, uy)) cell[p][(size_t)(uy - s * rowsU[p]) * ringU[p] + (ux & (ringU[p] - 1))] = ux;
-            }
-        }
-    }
-    if (!ringOk) return bail("ring overrun");
-    // the masks and lists without their same-strip entries (into scratch; committed below)
-    auto ownerStrip = [&](int p, int ux, int uy, int32_t* pos) -> int {  // -1: not written in the launch
-        const int32_t node = c->umap[p][(size_t)uy * c->mapW[p] + ux].owner;
-        *pos = node < 0 ? -1 : c->nodePos[node];
-        return *pos < 0 ? -1 : st[*pos];
-    };
-    std::vector<uint32_t> nd;
-    nd.reserve(c->deps.size());
-    std::vector<uint32_t> off(ni), dcnt(ni);
-    std::vector<uint8_t> pub(ni, 0);
-    for (size_t i = 0; i < ni; i++) {
-        const WorkItem& w = c->items[i];
-        const int s = st[i];
-        uint32_t m[4];
-        for (int q = 0; q < 4; q++) m[q] = c->deps[w.dep_off - 4 + q];
-        const int p = w.plane, x = w.x, y = w.y;
-        int32_t o;
-        for (int u = 0; u < 32; u++) {
-            if ((m[0] >> u) & 1) {
-                if (ownerStrip(p, (x >> 2) + u, (y - 1) >> 2, &o) == s) m[0] &= ~(1u << u);
-                else if (o >= 0) pub[o] |= 2;
-            }
-            if ((m[2] >> u) & 1) {
-                if (ownerStrip(p, (x - 1) >> 2, (y >> 2) + u, &o) == s) m[2] &= ~(1u << u);
-                else if (o >= 0) pub[o] |= 2;
-            }
-        }
-        if (m[1] & 1) {
-            if (ownerStrip(p, (x - 1) >> 2, (y - 1) >> 2, &o) == s) m[1] = 0;
-            else if (o >= 0) pub[o] |= 2;
-        }
-        nd.insert(nd.end(), m, m + 4);
-        off[i] = (uint32_t)nd.size();
-        for (uint32_t d = w.dep_off; d < w.dep_off + w.dep_cnt; d++) {
-            const uint32_t pos = c->deps[d];
-            if (st[pos] != s) return bail("a dependency list crosses strips");
-        }
-        dcnt[i] = 0;
-    }
-    for (size_t i = 0; i < ni; i++) {
-        c->items[i].dep_off = off[i];
-        c->items[i].dep_cnt = (uint16_t)dcnt[i];
-        c->items[i].pub = pub[i];
-    }
-    c->deps.swap(nd);
-    c->stripStart.swap(start);
-    c->stripGroups.swap(groups);
-    c->stripMode = true;
-    if (dbg) {
-        uint32_t mx = 0, crossG = 0, pubs = 0;
-        for (uint32_t s = 0; s < nStrips; s++) mx = std::max(mx, c->stripStart[s + 1] - c->stripStart[s]);
-        for (size_t i = 0; i < ni; i++) {
-            for (int q = 0; q < 4; q++) crossG += __builtin_popcount(c->deps[c->items[i].dep_off - 4 + q]);
-            pubs += c->items[i].pub != 0;
-        }
-        fprintf(stderr, "av1r strips: %u strips, %u groups (max %u per strip), %zu levels, %u cross-strip granule units, %u publishing items\n",
-            nStrips, c->stripStart[nStrips], mx, c->levels.size(), crossG, pubs);
-    }
-}
 
 // ------------------------------------------------------------------------------------
 // dependency levels
@@ -1202,14 +1014,6 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         return;
     }
     const size_t nl = (size_t)(globalMax + 1);
-    // a deep frame (a key frame's intra wavefront) runs on k_strip: its items are ordered
-    // by strip within each level so that a strip's small items of one level are adjacent
-    const int stripLv = g_stripLevels.load(std::memory_order_relaxed);
-    c->stripMode = stripLv > 0 && (int)nl > stripLv;
-    auto stripOf = [&](const WorkItem& w) -> uint32_t {
-        if (AV1R_ITEM_KIND(w.code) == AV1R_ITEM_II) return (uint32_t)(b->blocks[w.block].mi_row * 4) / AV1R_STRIP_H;
-        return ((uint32_t)w.y << (w.plane ? 1 : 0)) / AV1R_STRIP_H;
-    };
     clk.lap(PP_SCHED_BLOCKS);
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
         if (v->size() < nl) v->resize(nl);
@@ -1255,25 +1059,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         const bool large = av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
         return (large ? 0 : 2) + ((b->blocks[t.block].flags & AV1R_BLK_INTER) ? 1 : 0);
     };
-    // AV1R_INTER_ORDER=1: within each class the inter tiles grouped by their first reference
-    // (stable: raster order inside a group), so that the tiles an XCD runs together stream one
-    // reference's rows through its L2 instead of all seven (synthetic blocks pick among 7)
-    static const bool byRef = getenv("AV1R_INTER_ORDER") && atoi(getenv("AV1R_INTER_ORDER")) != 0;
-    std::vector<uint32_t> rk[8];
-    auto refSort = [&](uint32_t* v, uint32_t cnt) {
-        for (auto& r : rk) r.clear();
-        for (uint32_t q = 0; q < cnt; q++) rk[b->blocks[AV1R_ITEM_INDEX(v[q]) >> 4].ref_frame[0] & 7].push_back(v[q]);
-        for (auto& r : rk) {
-            std::copy(r.begin(), r.end(), v);
-            v += r.size();
-        }
-    };
     for (size_t l = 0; l < nl; l++) {
         // order: inter tiles, then k_tb's large items, then its small ones
         uint32_t pc[4] = {}, tc[4] = {};
         partition(c->lvP[l], 3, pc, plainClass);
-        if (byRef)
-            for (uint32_t q = 0, o = 0; q < 3; o += pc[q++]) refSort(c->lvP[l].data() + o, pc[q]);
         c->levels[l].pl[0] = pc[1];
         c->levels[l].pl[1] = pc[2];
         std::vector<uint32_t>& T = c->lvT[l];
@@ -1316,12 +1105,6 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 }
                 c->items.push_back(w);
             }
-        }
-        if (c->stripMode) {
-            auto byStrip = [&](const WorkItem& a, const WorkItem& q) { return stripOf(a) < stripOf(q); };
-            const Level& L = c->levels[l];
-            std::stable_sort(c->items.begin() + L.off[1], c->items.begin() + L.off[1] + L.fcnt[1], byStrip);
-            std::stable_sort(c->items.begin() + L.off[2], c->items.begin() + L.off[2] + L.fcnt[2], byStrip);
         }
     }
     c->nLevelsLast = (int)nl;
@@ -1385,12 +1168,6 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->deps.push_back((uint32_t)pos);
             c->items[pos].pub = 1;
         }
-    }
-    if (c->stripMode && c->flowOk) build_strips(c, b);  // (clears stripMode where k_flow stays)
-    else c->stripMode = false;
-    if (!c->stripMode) {
-        c->stripGroups.clear();
-        c->stripStart.clear();
     }
     clk.lap(PP_SCHED_DEPS);
     if (flowOnly && !c->flowOk) build_schedule(c, b, allowGran, false);  // k_flow cannot take it: levels too
@@ -1475,8 +1252,6 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.frame_h = h->frame_height;
     P.hdr = *h;
     P.levels = c->levels;
-    P.stripGroups = c->stripGroups;
-    P.stripStart = c->stripStart;
     P.bytes = off;
     memcpy(P.usedRef, c->usedRef, sizeof(P.usedRef));
     P.levelsOk = c->levelsOk;
@@ -1698,29 +1473,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     }
     if (mustFlow && !allFlow) return fail(c, AV1R_E_INVALID, "a flow-only frame batched with a level-schedule frame");
     flow = (flow || mustFlow) && allFlow;
-    // k_flow groups of the frames without a strip schedule; k_strip strips and groups of the
-    // others (deep frames, build_strips)
-    // AV1R_FLOW_WAVE=1: small items as single entries after the groups, served per wave
-    // (recon.hip, flow_small_wave); nGroups then counts the large items only
-    const bool waveItems = g_flowWave.load(std::memory_order_relaxed) != 0;
-    size_t nGroups = 0, nSmallItems = 0, nStripG = 0, nStripS = 0;
-    for (auto& j : jobs) {
-        if (flow && !j.P->stripGroups.empty()) {
-            nStripG += j.P->stripGroups.size() / 2;
-            nStripS += j.P->stripStart.size() - 1;
-            continue;
-        }
-        for (const Level& lv : j.P->levels) {
-            nGroups += lv.fcnt[1] + (waveItems ? 0 : (lv.fcnt[2] + 3) / 4);
-            nSmallItems += waveItems ? lv.fcnt[2] : 0;
-        }
-    }
+    // k_flow groups: one large item, or up to four small ones
+    size_t nGroups = 0;
+    for (auto& j : jobs)
+        for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
-    const size_t stripTabBytes = nStripS ? align256(4 * (2 * nStripS + 2)) : 0;
-    const size_t stripBytes = nStripS ? stripTabBytes + 8 * nStripG : 0;
-    const size_t nEntries = nGroups + nSmallItems;  // (the groups array: groups, then single small items)
-    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nEntries + resTabBytes + stripBytes : 0);
-    const bool anyFlow = flow && (nEntries || nStripG);
+    const size_t nEntries = nGroups;
+    const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nEntries + resTabBytes : 0);
+    const bool anyFlow = flow && nEntries;
     Upload& M = lc->meta[lc->metaIdx];
     lc->metaIdx = (lc->metaIdx + 1) % av1r_ctx::kMetaRing;
     if (M.pending) {
@@ -1759,7 +1519,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     uint32_t frameRows = 0;  // k_flow-mode timeline: frame-major rows
     for (int i = 0; i < n; i++) {
         hk[i] = jobs[i].k;
-        hk[i].strip = flow && !jobs[i].P->stripGroups.empty();
         hk[i].fi = g_fastIntra.load(std::memory_order_relaxed);
         hk[i].trace_base = frameRows;
         for (const Level& lv : jobs[i].P->levels) frameRows += lv.cnt[0] + lv.cnt[1] + lv.cnt[2];
@@ -1813,24 +1572,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         for (size_t l = 0; l < nLevels; l++)
             for (int i = 0; i < n; i++) {
                 const auto& lvs = jobs[i].P->levels;
-                if (l >= lvs.size() || !jobs[i].P->stripGroups.empty()) continue;
+                if (l >= lvs.size()) continue;
                 const Level& lv = lvs[l];
                 for (uint32_t q = 0; q < lv.fcnt[1]; q++, g += 2) {
                     g[0] = (uint32_t)i << 8;
                     g[1] = lv.off[1] + q;
                 }
-                for (uint32_t q = 0; q < lv.fcnt[2] && !waveItems; q += 4, g += 2) {
+                for (uint32_t q = 0; q < lv.fcnt[2]; q += 4, g += 2) {
                     g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(4, lv.fcnt[2] - q);
-                    g[1] = lv.off[2] + q;
-                }
-            }
-        for (size_t l = 0; l < nLevels && waveItems; l++)  // the single small items, same order
-            for (int i = 0; i < n; i++) {
-                const auto& lvs = jobs[i].P->levels;
-                if (l >= lvs.size() || !jobs[i].P->stripGroups.empty()) continue;
-                const Level& lv = lvs[l];
-                for (uint32_t q = 0; q < lv.fcnt[2]; q++, g += 2) {
-                    g[0] = ((uint32_t)i << 8) | 1u;
                     g[1] = lv.off[2] + q;
                 }
             }
@@ -1840,28 +1589,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         for (int i = 0; i < n; i++) {
             rt[i + 1] = rt[i] + jobs[i].P->nResidS;
             rt[n + 2 + i] = rt[n + 1 + i] + jobs[i].P->nResidL;
-        }
-        if (nStripS) {
-            // k_strip: [the strips' first groups (nStripS + 1)] [the strips' indices in their
-            // frames (nStripS)] [groups {frame << 8 | n, first item}]
-            uint32_t* ss = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries + resTabBytes);
-            uint32_t* sg = ss + stripTabBytes / 4;
-            uint32_t gb = 0, si = 0;
-            for (int i = 0; i < n; i++) {
-                const Prepared& P = *jobs[i].P;
-                if (P.stripGroups.empty()) continue;
-                for (size_t s = 0; s + 1 < P.stripStart.size(); s++) {
-                    ss[nStripS + 1 + si] = (uint32_t)s;
-                    ss[si++] = gb + P.stripStart[s];
-                }
-                const size_t ng = P.stripGroups.size() / 2;
-                for (size_t q = 0; q < ng; q++) {
-                    sg[2 * (gb + q)] = ((uint32_t)i << 8) | P.stripGroups[2 * q];
-                    sg[2 * (gb + q) + 1] = P.stripGroups[2 * q + 1];
-                }
-                gb += (uint32_t)ng;
-            }
-            ss[si] = gb;
         }
     }
     if (host_prof()) tp2 = now_us();
@@ -1960,9 +1687,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             // solo deep frame takes one per CU and leaves the rest to concurrent batches)
             int grid = (int)std::min<size_t>(flow_grid(lc->device, perCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
             if (lc->flowGridCap > 0) grid = std::max(FLOW_QUEUES, std::min(grid, lc->flowGridCap / FLOW_QUEUES * FLOW_QUEUES));
-            // per-wave small items: every resident slot, and at least one server per queue of
-            // both populations (FLOW_LARGE_EVERY x FLOW_QUEUES workgroups, recon.hip)
-            if (nSmallItems) grid = std::max(64, std::max(grid, lc->flowGridCap > 0 ? std::min(flow_grid(lc->device, perCU), lc->flowGridCap) : flow_grid(lc->device, perCU)));
             // epochs in chain order (unique per launch; taken under the chain's lock)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
@@ -1972,21 +1696,15 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                 hipEvent_t ev = nullptr;
                 HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
                 if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
-                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, (uint32_t)nSmallItems, ctl, rec->err, epoch, grid, trace, st);
+                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
                 HIPCHK(hipEventRecord(ev, st));
                 if (F.done) (void)hipEventDestroy(F.done);
                 F.done = ev;
                 F.last = st;
             } else {
-                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, (uint32_t)nSmallItems, ctl, rec->err, epoch, grid, trace, st);
+                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
             }
             flow_debug_note(epoch, st);
-        }
-        if (nStripS) {  // deep frames: one workgroup per strip (build_strips)
-            uint32_t epoch = ++epochs;
-            if (!epoch) epoch = ++epochs;
-            const uint8_t* sb = M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries + resTabBytes;
-            launch_k_strip(dk, sb + stripTabBytes, reinterpret_cast<const uint32_t*>(sb), (uint32_t)nStripS, ctl, epoch, trace, st);
         }
     }
     if (!flow && lc->timing) {
@@ -3253,13 +2971,11 @@ int av1r_set_flow_spins(av1r_ctx* c, uint32_t spins)
     return AV1R_OK;
 }
 
-int av1r_set_strip_levels(int levels) { return g_stripLevels.exchange(levels < 0 ? 0 : levels); }
 
 int av1r_set_filter_fusion(int on) { return g_fusedFilters.exchange(on ? 1 : 0); }
 
 int av1r_set_fast_intra(int on) { return g_fastIntra.exchange(on ? 1 : 0); }
 
-int av1r_set_flow_wave(int on) { return g_flowWave.exchange(on ? 1 : 0); }
 
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream)
 {

@@ -192,29 +192,10 @@ DEV void coop_intra_edges(int miCols, int miRows, const DevPlane& src, int plane
 // were final before the launch and are read from the frame.  The runs are staged in
 // L.tmp / L.tmp2, then AboveRow / LeftCol are assembled as in coop_intra_edges.  Bounded:
 // a spin gives up after ~1 s (or once another wave has) and sets the launch's error word.
-// k_strip: the strip's reconstructed pixels in LDS (av1r_host.cpp build_strips).  Plane p
-// holds rows [top[p], top[p] + (AV1R_STRIP_H >> sub)), column c at c mod (AV1R_RING_W >> sub).
-// (LDS address-space pointers: through a generic pointer every ring access would be a
-// flat_ instruction, which also waits for the wave's outstanding global stores)
+// (LDS address-space pointers: through a generic pointer an LDS access is a flat_
+// instruction, which also waits for the wave's outstanding global stores)
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-struct RingView {  // (passed by value: a pointer to it made it a scratch object, and every
-                  // scratch reload waited for the wave's outstanding pixel stores)
-    lds_u8* base;  // luma [AV1R_STRIP_H][AV1R_RING_W], then U and V [AV1R_STRIP_H / 2][AV1R_RING_W / 2]
-    int top;       // the strip's first luma row
-    bool on;       // k_strip (false: k_flow, no ring)
-};
-DEV bool ring_has(const RingView& R, int p, int y)
-{
-    const int t = p ? R.top >> 1 : R.top;
-    return R.on && y >= t && y < t + (AV1R_STRIP_H >> (p ? 1 : 0));
-}
-DEV lds_u8* ring_px(const RingView& R, int p, int x, int y)
-{
-    const int w = AV1R_RING_W >> (p ? 1 : 0);
-    const int off = p ? AV1R_STRIP_H * AV1R_RING_W + (p - 1) * (AV1R_STRIP_H / 2) * (AV1R_RING_W / 2) : 0;
-    return R.base + off + (y - (p ? R.top >> 1 : R.top)) * w + (x & (w - 1));
-}
 
 struct GranEdges {
     const uint32_t* mask;  // 4 words: above, corner, left, (unused)
@@ -225,8 +206,7 @@ struct GranEdges {
     uint32_t epoch;
     uint32_t* ctl;         // k_flow control block (FLOW_ERR)
     unsigned long long* tr;  // -DAV1R_TRACE timeline row (or null)
-    bool coh;              // units read from the frame: sc1 (k_flow) or plain (k_strip: strip_plain)
-    RingView ring;         // k_strip: this strip's pixels (units of the strip's rows come from here)
+    bool coh;              // units read from the frame: sc1 or plain
 };
 // The gather half: the above run's units into L.tmp (pixel (x + i, y - 1) at byte i), the
 // left run's into L.tmp2 (pixel (x - 1, y + i) at byte i), the corner's unit at L.tmp2
@@ -259,21 +239,9 @@ DEV void gran_gather(const DevPlane& src, int plane, int x, int y, bool hL, bool
                               : (cm & 2) ? G.v + (size_t)((x - 1) >> 2) * G.gh + ((y - 1) >> 2)
                                          : G.h + (size_t)((y - 1) >> 2) * G.gw + ((x - 1) >> 2);
             uint32_t val = 0;
-            // (flow read site: in-launch units of other items are granules (inl), this strip's
-            // come from the ring; the frame is read only for pixels final before the launch)
-            if (act && !inl && ring_has(G.ring, plane, kind == 1 ? y + 4 * u : y - 1)) {
-                // k_strip: a unit of this strip, written by an earlier group (the LDS ring)
-                const RingView& R = G.ring;
-                if (kind == 0) {
-                    val = *reinterpret_cast<lds_u32*>(ring_px(R, plane, x + 4 * u, y - 1));
-                } else if (kind == 1) {
-                    const int py = y + 4 * u;
-                    val = *ring_px(R, plane, x - 1, py) | (*ring_px(R, plane, x - 1, py + 1) << 8) |
-                          (*ring_px(R, plane, x - 1, py + 2) << 16) | ((uint32_t)*ring_px(R, plane, x - 1, py + 3) << 24);
-                } else {
-                    val = (uint32_t)*ring_px(R, plane, x - 1, y - 1) << 24;
-                }
-            } else if (act && !inl) {  // final before this launch
+            // (flow read site: in-launch units of other items are granules (inl); the frame is
+            // read only for pixels final before the launch)
+            if (act && !inl) {  // final before this launch
                 const bool c = G.coh;
                 if (kind == 0) {
                     val = ldp4_c(src, x + 4 * u, y - 1, c);

@@ -1,6 +1,6 @@
 // intra_fast.h -- the dataflow kernels' lean path for small intra transform blocks.
 //
-// k_flow / k_strip items are chains: a transform block's prediction waits for its
+// k_flow items are chains: a transform block's prediction waits for its
 // neighbours' pixels, and a key frame is ~2 000 such hops deep, so what counts is the
 // time from "edges arrived" to "pixels published".  The generic path (tb_predict +
 // coop_intra_from_edges + tb_store_flow, written for any NT and any size) spent ~1 200
@@ -118,7 +118,7 @@ DEV int fi_ek2(int str) { return str == 1 ? 8 : str == 2 ? 6 : 4; }
 
 template <int MAX>
 DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<MAX>& L, const GranEdges& G, uint2 res,
-    uint32_t epoch, RingView ring, bool gran)
+    uint32_t epoch, bool gran)
 {
     FiParams F;
     F.cls = fi_uni(F0.cls);
@@ -147,7 +147,7 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     const DevPlane& dst = k.cur.pl[plane];
     IntraLds& I = L.intra;
     // CFL: the co-located luma of this lane's four pixels (flow read site: the block's luma,
-    // written by earlier items -- sc1 loads after the dependency wait, or this strip's ring),
+    // written by earlier items -- sc1 loads after the dependency wait),
     // issued before the edge gather so that its loads overlap the granule polls
     const int nq = (w * h) >> 2;
     const int w4 = w >> 2;
@@ -162,13 +162,8 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
 #pragma unroll
             for (int b = 0; b < 4; b++) {
                 const int lx = imin((x + qj + b) << 1, F.maxLW - 2);
-                int v;
-                if (ring.on)
-                    v = *ring_px(ring, 0, lx, ly) + *ring_px(ring, 0, lx + 1, ly) + *ring_px(ring, 0, lx, ly + 1) +
-                        *ring_px(ring, 0, lx + 1, ly + 1);
-                else
-                    v = ldp_c(luma, lx, ly, coh) + ldp_c(luma, lx + 1, ly, coh) + ldp_c(luma, lx, ly + 1, coh) +
-                        ldp_c(luma, lx + 1, ly + 1, coh);
+                const int v = ldp_c(luma, lx, ly, coh) + ldp_c(luma, lx + 1, ly, coh) + ldp_c(luma, lx, ly + 1, coh) +
+                              ldp_c(luma, lx + 1, ly + 1, coh);
                 cv[b] = v << 1;
                 csum += cv[b];
             }
@@ -371,7 +366,7 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
     trace_stamp(G.tr, 9);
     const uint32_t o = add4(p, res);
     // the granules first (what the next items wait for), then the frame
-    if (gran && (!ring.on || (tb.pub & 2))) {
+    if (gran) {
         // granules from the registers: the bottom row's units are the last row's quads; a
         // right-column unit is byte 3 of four vertically adjacent quads (the plane's granule
         // arrays from G, set up before the wait: no dependent parameter load here)
@@ -401,8 +396,5 @@ DEV void fi_run(const KParams& k, const WorkItem& tb, const FiParams& F0, TbLds<
                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (t < nq) {
-        stp4_c(dst, x + qj, y + qi, o, G.coh);
-        if (ring.on) *reinterpret_cast<lds_u32*>(ring_px(ring, plane, x + qj, y + qi)) = o;
-    }
+    if (t < nq) stp4_c(dst, x + qj, y + qi, o, G.coh);
 }

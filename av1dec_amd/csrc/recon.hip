@@ -201,18 +201,12 @@ DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk,
             const DevPlane& luma = k.cur.pl[0];
             const int maxLW = blk.max_luma_w, maxLH = blk.max_luma_h;
             // (flow read site: the same block's luma, written by earlier items of the launch:
-            // sc1 loads after the done-flag wait in k_flow, this strip's LDS ring in k_strip)
-            const bool ring = COH && gran && G->ring.on;
+            // sc1 loads after the done-flag wait in k_flow)
             for (int q = t; q < w * h; q += NT) {
                 int i = q >> log2W, j = q & (w - 1);
                 int ly = imin((y + i) << 1, maxLH - 2), lx = imin((x + j) << 1, maxLW - 2);
-                int v;
-                if (ring)
-                    v = (*ring_px(G->ring, 0, lx, ly) + *ring_px(G->ring, 0, lx + 1, ly) + *ring_px(G->ring, 0, lx, ly + 1) +
-                            *ring_px(G->ring, 0, lx + 1, ly + 1)) << 1;
-                else
-                    v = (ldp<COH>(luma, lx, ly) + ldp<COH>(luma, lx + 1, ly) + ldp<COH>(luma, lx, ly + 1) +
-                            ldp<COH>(luma, lx + 1, ly + 1)) << 1;
+                const int v = (ldp<COH>(luma, lx, ly) + ldp<COH>(luma, lx + 1, ly) + ldp<COH>(luma, lx, ly + 1) +
+                                  ldp<COH>(luma, lx + 1, ly + 1)) << 1;
                 L.cfl[i * CM + j] = (int16_t)v;
                 s += v;
             }
@@ -299,20 +293,15 @@ DEV uint32_t add4(uint32_t p, uint2 r)
     for (int b = 0; b < 4; b++) o |= (uint32_t)clip1((int)((p >> (8 * b)) & 0xff) + v[b]) << (8 * b);
     return o;
 }
-// k_strip (ring): the pixels also go to the strip's LDS ring, and the granules only where
-// another strip reads them (pub bit 1)
 template <int NT, int MAX>
-DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch,
-    RingView ring = {})
+DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, const ResQuads<NT, MAX>& R, uint32_t epoch)
 {
-
     const int t = coop_lane<NT>();
     const int l2q = ctab<NT>(av1r_tx_w_log2, tb.tx_size) - 2;
     const int tw = ctab<NT>(av1r_tx_w, tb.tx_size), th = ctab<NT>(av1r_tx_h, tb.tx_size);
     const int nq = (tw * th) >> 2;
     const DevPlane& dst = k.cur.pl[tb.plane];
     const bool gran = k.gran;
-    const bool coh = !strip_plain(k.strip, gran);
 #pragma unroll
     for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
         const int q = t + u * NT;
@@ -320,12 +309,11 @@ DEV void tb_store_flow(const KParams& k, const WorkItem& tb, TbLds<MAX>& L, cons
             const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
             uint32_t* pp = reinterpret_cast<uint32_t*>(&L.pred[i * MAX + j]);
             const uint32_t o = add4(*pp, R.r[u]);
-            stp4_c(dst, tb.x + j, tb.y + i, o, coh);
-            if (ring.on) *reinterpret_cast<lds_u32*>(ring_px(ring, tb.plane, tb.x + j, tb.y + i)) = o;
+            stp4<true>(dst, tb.x + j, tb.y + i, o);
             if (gran) *pp = o;  // the final pixels, for the edge granules
         }
     }
-    if (gran && (!ring.on || (tb.pub & 2))) {
+    if (gran) {
         coop_sync<NT>();
         const int p = tb.plane;
         coop_publish_gran<NT>(L.pred, MAX, tb.x, tb.y, tw, th, k.gran_h[p], k.gran_v[p],
@@ -1345,7 +1333,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
                 }
                 coop_sync<NT>();
             }
-            const bool coh = COH && !strip_plain(k.strip, gran);
+            const bool coh = COH;
             for (int q = t; q < pw * ph; q += NT) {
                 const int i = q >> lpw, j = q & (pw - 1);
                 stp_c(dst, baseX + j, baseY + i, L.pred[i * 64 + j], coh);
@@ -1699,7 +1687,7 @@ DEV void flow_publish(uint32_t* flag, uint32_t epoch)
 // 7 XCC id << 16 | dependency count
 template <int NT, int MAX>
 DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch, uint32_t* ctl,
-    unsigned long long* trace, uint32_t s, RingView ring = {})
+    unsigned long long* trace, uint32_t s)
 {
     // What the item reads from the batch after its wait -- its edge mask words, its block's
     // prediction fields, the edge-filter flag (and with AV1R_FLOW_ITEM_COPY its own record)
@@ -1742,8 +1730,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         G.gh = k.gran_hn[p];
         G.epoch = epoch;
         G.ctl = ctl;
-        G.coh = !strip_plain(k.strip, gran);
-        G.ring = ring;
+        G.coh = true;
         G.tr = tr;
     }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
@@ -1769,7 +1756,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
                 trace_stamp(tr, 3);
                 flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
                 trace_stamp(tr, 4);
-                fi_run<MAX>(k, wi, F, L, G, R.r[0], epoch, ring, gran);
+                fi_run<MAX>(k, wi, F, L, G, R.r[0], epoch, gran);
                 trace_stamp(tr, 10);
             }
         }
@@ -1779,7 +1766,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
             trace_stamp(tr, 4);
             tb_predict<NT, MAX, true>(k, wi, blk, L, &G, gran, edgeFilter);
             trace_stamp(tr, 9);
-            tb_store_flow<NT, MAX>(k, wi, L, R, epoch, ring);
+            tb_store_flow<NT, MAX>(k, wi, L, R, epoch);
             trace_stamp(tr, 10);
         }
     }
@@ -1805,36 +1792,8 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 #define FLOW_DBG_PAIRS 256
 __device__ uint32_t g_flow_active[64], g_flow_overlap, g_flow_pairs[FLOW_DBG_PAIRS];
 #endif
-// Per-wave small items (nSmall > 0, the host's AV1R_FLOW_WAVE): groups[nGroups ..
-// nGroups + nSmall) are single small items (n = 1), in the same topological order, served by
-// WAVES instead of workgroups: of the workgroups, entry e with e % FLOW_LARGE_EVERY == 0
-// serves the group queue (e / FLOW_LARGE_EVERY) % FLOW_QUEUES as above, every other one puts
-// each of its four waves on small queue (4 e + wave) % FLOW_QUEUES, pulling one item per
-// atomic -- no group lock-step (a group of four waited for its slowest item) and no barrier
-// between items.  Progress as above, per population: each queue hands out its items in
-// topological order and a server holds only items taken before the queue's next one, so the
-// earliest unfinished item is held by a server whose inputs are complete, or is the next of
-// a queue whose servers all hold items of its level; once FLOW_LARGE_EVERY * FLOW_QUEUES
-// workgroups have started every queue of both populations has a resident server.
-#define FLOW_LARGE_EVERY 8
-DEV void flow_small_wave(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups, uint32_t nSmall,
-    uint32_t* ctl, uint32_t epoch, unsigned long long* trace, uint32_t q, TbLds<TB_SMALL>& L)
-{
-    uint32_t* head = ctl + FLOW_SMALLQ + q * FLOW_LINE;
-    const int lane = threadIdx.x & 63;
-    for (;;) {
-        uint32_t tk = 0;
-        if (lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t g = __builtin_amdgcn_readfirstlane(__shfl(tk, 0)) * FLOW_QUEUES + q;
-        if (g >= nSmall) return;
-        const uint2 gd = groups[nGroups + g];
-        const KParams& k = KP(kps, gd.x >> 8);
-        flow_item<64, TB_SMALL>(k, gd.y, L, epoch, ctl, trace, gd.x >> 8);
-    }
-}
-
 extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const KParams* kps, const uint2* __restrict__ groups, uint32_t nGroups,
-    uint32_t nSmall, uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
+    uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
     __shared__ __align__(16) uint8_t smem[kLds];
@@ -1848,7 +1807,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     __shared__ uint32_t qsh;
     if (threadIdx.x == 0) {
         const uint32_t e = __hip_atomic_fetch_add(ctl + FLOW_ASSIGN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        qsh = nSmall ? e : e % FLOW_QUEUES;
+        qsh = e % FLOW_QUEUES;
 #ifdef AV1R_FLOW_DEBUG
         atomicAdd(&g_flow_active[epoch & 63], 1u);
         for (uint32_t e = 1; e < 64; e++) {
@@ -1862,16 +1821,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 #endif
     }
     __syncthreads();
-    uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
-    if (nSmall) {  // qsh holds the entry number itself here
-        if (q % FLOW_LARGE_EVERY) {
-            const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            flow_small_wave(kps, groups, nGroups, nSmall, ctl, epoch, trace, (4 * q + wave) % FLOW_QUEUES,
-                reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave]);
-            return;
-        }
-        q = (q / FLOW_LARGE_EVERY) % FLOW_QUEUES;
-    }
+    const uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
     uint32_t* head = ctl + q * FLOW_LINE;
     if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -1950,78 +1900,12 @@ uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset)
 }
 #endif
 
-void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t nSmall, uint32_t* ctl, uint32_t* hostErr,
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
     uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s)
 {
     (void)hostErr;  // (its address travels in the control block: FLOW_HOSTERR)
-    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, nSmall, ctl, epoch,
+    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
         trace);
-}
-
-// ---------------------------------------------------------------------------------
-// k_strip: the items of deep intra frames (a key frame's ~2 000-level wavefront), one
-// workgroup per 64-row strip of a frame (av1r_host.cpp build_strips).  The workgroup runs
-// its strip's groups -- k_flow's groups: one large item, or up to four small ones, one per
-// wave -- in level order, and keeps the strip's reconstructed pixels in an LDS ring
-// (AV1R_RING_W columns, RingView): an item reads the edge and CFL pixels of its own strip
-// from the ring, written by an earlier group before the barrier that ends every group, so
-// a same-strip hand-off costs an LDS round trip instead of a trip through the device
-// coherence point.  The frame is written with plain stores and never read for a pixel of
-// this launch; what crosses a strip boundary (the row above a strip, below-left columns
-// reaching into the next strip) travels as k_flow's granules, published only by the items
-// whose units another strip reads.  Progress: an item waits only for granules of items of
-// lower levels; every strip runs its groups in level order, so a wait chain strictly
-// descends in level and ends at an item whose strip is running it, once every strip's
-// workgroup is resident (a few dozen per frame; nothing else on the chip waits for them).
-// tab: [first group of each strip (nStrips + 1)] [each strip's index in its frame (nStrips)].
-// ---------------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(256) void k_strip(const KParams* kps, const uint2* __restrict__ groups,
-    const uint32_t* __restrict__ tab, uint32_t nStrips, uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
-{
-    constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
-    constexpr int kRingY = AV1R_STRIP_H * AV1R_RING_W, kRingC = (AV1R_STRIP_H / 2) * (AV1R_RING_W / 2);
-    __shared__ __align__(16) uint8_t smem[kLds];
-    __shared__ __align__(16) uint8_t ringMem[kRingY + 2 * kRingC];
-    const uint32_t s = blockIdx.x;
-    const uint32_t sid = tab[nStrips + 1 + s];
-    RingView R;
-    R.base = (lds_u8*)ringMem;
-    R.top = (int)sid * AV1R_STRIP_H;
-    R.on = true;
-    const uint32_t g1 = tab[s + 1];
-    for (uint32_t g = tab[s]; g < g1; g++) {
-        const uint2 gd = groups[g];
-        const KParams& k = KP(kps, gd.x >> 8);
-        const uint32_t n = gd.x & 0xff;
-        if (n == 0) {
-            flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8, R);
-        } else {
-            const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            if (wave < n)
-                flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
-                    gd.x >> 8, R);
-        }
-        // the group's ring writes are visible to every later group; its frame stores and
-        // granules need no drain (nothing in the strip reads them back)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#ifdef AV1R_TRACE
-        if (trace && threadIdx.x == 0) {  // row slots 14: strip << 32 | group, 15: group end
-            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t w = 0; w < (n ? n : 1); w++) {
-                unsigned long long* tr = trace + (size_t)(k.trace_base + gd.y + w) * AV1R_TRACE_W;
-                tr[14] = ((unsigned long long)s << 32) | g;
-                tr[15] = now;
-            }
-        }
-#endif
-    }
-}
-
-void launch_k_strip(const KParams* kps, const void* groups, const uint32_t* tab, uint32_t nStrips, uint32_t* ctl,
-    uint32_t epoch, unsigned long long* trace, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_strip, dim3(nStrips), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), tab, nStrips, ctl,
-        epoch, trace);
 }
 
 #endif  // AV1R_FLOW_PART

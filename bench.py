@@ -538,7 +538,7 @@ def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, p
 
 
 def key_frame_ms(dec, handle, reps=3):
-    """Device time (recon stage, k_flow / k_strip dominated) of one key frame alone on the
+    """Device time (recon stage, k_flow dominated) of one key frame alone on the
     chip, median of `reps`: the deep frames the batched pipeline launches solo.  (Decoding a
     key frame resets the stream's references: run it last.)"""
     dec.l.av1r_set_timing(dec.c, 1)

@@ -338,11 +338,6 @@ const char* av1r_last_error(av1r_ctx* ctx);
  * from different streams; -1 in a normal build. */
 int av1r_set_flow_spins(av1r_ctx* ctx, uint32_t spins);
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream);
-/* Process-wide: frames scheduled from now on with more than `levels` dependency levels
- * (a key frame's intra wavefront) run on k_strip, one workgroup per 64-row strip, instead
- * of k_flow; 0 = never.  Default 0 (environment AV1R_STRIP_LEVELS).  Returns the previous
- * value.  Both kernels are bit-exact; tests lower it to run every stream on k_strip. */
-int av1r_set_strip_levels(int levels);
 /* Process-wide: 1 = the in-loop filters of frames launched from now on run fused (k_post:
  * deblocking -> CDEF -> loop restoration per 64-row stripe tile in LDS, straight into the
  * output frame; not for frames whose stage snapshots are kept), 0 = the three stage kernels
@@ -352,11 +347,6 @@ int av1r_set_filter_fusion(int on);
  * (default; environment AV1R_FI), 0 = the generic one.  Both are bit-exact (A/B).  Returns
  * the previous value. */
 int av1r_set_fast_intra(int on);
-/* Process-wide: 1 = the small items of k_flow launches from now on are served one per wave
- * from their own queues (no group lock-step; recon.hip flow_small_wave), 0 = in groups of
- * four per workgroup (default; environment AV1R_FLOW_WAVE).  Both are bit-exact.  Returns the
- * previous value. */
-int av1r_set_flow_wave(int on);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);

@@ -10,13 +10,6 @@ from av1dec_amd import Decoder, abi, batchfile
 
 STREAMS = golden.streams()
 BITS = golden.bits_md5()
-# the opt-in A/B schedules (k_strip, fused filters: measured slower, off by default, DESIGN
-# 3.1b / 4.1) on a representative subset instead of all 172: every stream that is not one of
-# the 64 quantizer or ~96 frame-size sweeps, plus every 8th quantizer and every 6th size
-_Q = [s for s in STREAMS if "-quantizer-" in s]
-_S = [s for s in STREAMS if "-size-" in s]
-AB_STREAMS = [s for s in STREAMS if s not in _Q and s not in _S] + _Q[::8] + _S[::6]
-
 
 @pytest.fixture(scope="module")
 def dev(native_lib):
@@ -58,24 +51,6 @@ def test_gpu_matches_reference(stream):
 
 
 @pytest.fixture
-def strip_everywhere(native_lib):
-    # every frame with more than one dependency level on k_strip (one workgroup per 64-row
-    # strip; by default only deep frames -- > 400 levels -- take it)
-    prev = native_lib.av1r_set_strip_levels(1)
-    yield
-    native_lib.av1r_set_strip_levels(prev)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("stream", AB_STREAMS)
-def test_gpu_strip_schedule_matches_reference(stream, strip_everywhere):
-    # k_strip (av1r_host.cpp build_strips): every stage of every frame
-    bad, got, out_md5 = run_stream(stream)
-    assert not bad, bad[:3]
-    assert got == out_md5 == BITS[stream]
-
-
-@pytest.fixture
 def fused_filters(native_lib):
     prev = native_lib.av1r_set_filter_fusion(1)
     yield
@@ -83,27 +58,12 @@ def fused_filters(native_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stream", AB_STREAMS)
+@pytest.mark.parametrize("stream", STREAMS)
 def test_gpu_fused_filters_match_reference(stream, fused_filters):
     # the filters fused (k_post: deblocking -> CDEF -> loop restoration per stripe tile in
-    # LDS; frames without stage snapshots): the whole output equals the reference's MD5
+    # LDS; frames without stage snapshots): the whole output equals the reference's MD5, on
+    # every stream (the stage kernels' store paths are shared with k_post)
     bad, got, out_md5 = run_stream(stream, check_stages=False)
-    assert got == out_md5 == BITS[stream]
-
-
-@pytest.fixture
-def flow_wave(native_lib):
-    prev = native_lib.av1r_set_flow_wave(1)
-    yield
-    native_lib.av1r_set_flow_wave(prev)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("stream", AB_STREAMS)
-def test_gpu_flow_wave_matches_reference(stream, flow_wave):
-    # k_flow's small items served per wave (av1r_set_flow_wave): every stage of every frame
-    bad, got, out_md5 = run_stream(stream)
-    assert not bad, bad[:3]
     assert got == out_md5 == BITS[stream]
 
 

@@ -97,19 +97,6 @@ def test_gpu_synth_fused_filters(native_lib, w, h, tiles, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("w,h,tiles,seed", [(1920, 1080, (1, 1), 0x5EED0001), (3840, 2160, (4, 2), 0x5EED0002)])
-def test_gpu_synth_flow_wave(native_lib, w, h, tiles, seed):
-    """k_flow's small items served per wave (av1r_set_flow_wave) at 1080p and 4K 4x2 tiles:
-    every stage of a key frame and two inter frames bit-exact with the oracle."""
-    prev = native_lib.av1r_set_flow_wave(1)
-    try:
-        assert compare_gpu_oracle(pysynth.stream(w, h, 3, seed, tiles=tiles), stages=True) == 3
-    finally:
-        native_lib.av1r_set_flow_wave(prev)
-
-
-@pytest.mark.gpu
 def test_gpu_prepared_path_matches_streaming():
     frames = pysynth.stream(640, 360, 5, 9)
     d1 = Decoder(0)
