@@ -224,7 +224,7 @@ def summarise_slots(path, lo=0, hi=None):
         gaps.append(g)
         between += g.clip(min=0).sum()
     gaps = np.concatenate(gaps) if gaps else np.zeros(1)
-    have = (t8 > 0) & (t9 > 0) & (t10 > 0)
+    have = (t4 <= t8) & (t8 <= t9) & (t9 <= t10) & (t10 <= t5)  # the lean path's stamps (others: stale)
     tot = len(slots) * span
     parts = {"setup 2->3": (t3 - t2).sum(), "dep wait 3->4": (t4 - t3).sum(),
              "gather 4->8": np.where(have, t8 - t4, 0).sum(), "predict 8->9": np.where(have, t9 - t8, 0).sum(),
@@ -236,6 +236,15 @@ def summarise_slots(path, lo=0, hi=None):
     for k, v in parts.items():
         print(f"   {k:18s} {v / tot:6.1%} of slot-time  ({us(v) / len(a):6.2f} us per item)")
     print(f"   {'idle (after last)':18s} {1 - sum(parts.values()) / tot:6.1%}")
+    # the chain: per dependency level, when its items start, are released and finish
+    lvl = a[:, 6]
+    base = t2.min()
+    print("level  items  start p10/p50  released p50/p90  end p50/p90/max (us from the launch's first item)")
+    for l in np.unique(lvl):
+        m = lvl == l
+        q = lambda x, p: np.percentile(us(x[m] - base), p)
+        print(f"{l:5d} {m.sum():6d}   {q(t2, 10):7.1f} {q(t2, 50):7.1f}   {q(t4, 50):7.1f} {q(t4, 90):7.1f}"
+              f"   {q(t5, 50):7.1f} {q(t5, 90):7.1f} {q(t5, 100):7.1f}")
 
 
 if __name__ == "__main__":
