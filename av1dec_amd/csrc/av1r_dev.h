@@ -126,7 +126,8 @@ struct KParams {
     int mi_rows_alloc;
     uint32_t n_blocks, n_tbs;  // k_mi: the records the mode-info grid is derived from
     int frame_w, frame_h;
-    DevFrame cur;     // frame under reconstruction, deblocked in place
+    DevFrame cur;     // frame under reconstruction (k_lf: deblocked in place)
+    DevFrame dbk;     // the deblocked frame (k_deblock's output; k_lf: cur)
     DevFrame cdef;    // CDEF output (Cdef::filter's copy, Cdef.cpp:43)
     DevFrame lrout;   // loop-restoration output (LoopRestoration.cpp:216)
     DevFrame ref[8];  // reference store slots

@@ -31,10 +31,12 @@
 
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s);
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS,
+    unsigned long long* trace, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
+void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
-void launch_k_post(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
 void launch_k_out(const uint8_t* const src[3], const int ss[3], uint8_t* const dst[3], const int ds[3], const int w[3],
@@ -667,7 +669,6 @@ static bool inter_split()
     return on;
 }
 static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) : 1};
-static std::atomic<int> g_fusedFilters{getenv("AV1R_FUSED") ? atoi(getenv("AV1R_FUSED")) : 0};
 
 // ------------------------------------------------------------------------------------
 // dependency levels
@@ -1263,11 +1264,25 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
 // through recon -> LF -> CDEF -> LR in shared launches on one HIP stream: every level of
 // every frame in one k_level launch, every frame's filters in one launch per filter.
 // ------------------------------------------------------------------------------------
+// Deblocking both passes per tile in LDS (k_deblock, default) or in place per pass (k_lf,
+// AV1R_DEBLOCK_TILE=0).  k_deblock writes a frame of its own: tiles read their neighbours'
+// pixels as halo, so the reconstructed frame must stay intact while the launch runs.
+static bool deblock_tile()
+{
+    static const bool on = !getenv("AV1R_DEBLOCK_TILE") || atoi(getenv("AV1R_DEBLOCK_TILE")) != 0;
+    return on;
+}
+
 struct FrameJob {
     av1r_ctx* c = nullptr;
     const Prepared* P = nullptr;
     KParams k;
+    // the frame's buffers R, C, L and their roles: D the deblocked frame, Co the CDEF output,
+    // out the frame the frame store and the output queue keep.  k_deblock: reconstruction in
+    // R, deblocked into C, CDEF back into R (whose reconstruction is dead by then), loop
+    // restoration into L.  k_lf: deblocked in place in R, CDEF into C, LR into L.
     FrameBuf *R = nullptr, *C = nullptr, *L = nullptr;
+    FrameBuf *D = nullptr, *Co = nullptr, *out = nullptr;
     bool scaled = false;  // a reference differs in size from the frame (no k_inter_s tiles)
     uint64_t seq = 0;     // the context's frame sequence number
     uint8_t* dev = nullptr;  // P->offsets: the device copy of the packed buffer
@@ -1307,6 +1322,9 @@ static int job_begin(FrameJob& j)
     j.L = h->uses_lr ? frame_get(c, h->frame_width, h->frame_height) : nullptr;
     if (!j.R || !j.C || (h->uses_lr && !j.L)) return fail(c, AV1R_E_NOMEM, "frame allocation");
     j.k.cur = j.R->d;
+    j.D = deblock_tile() ? j.C : j.R;
+    j.Co = deblock_tile() ? j.R : j.C;
+    j.out = j.L ? j.L : j.Co;
     if (P.resElems > c->resCap) {
         if (c->resDev) {
             ctx_join(c);
@@ -1343,7 +1361,8 @@ static int job_begin(FrameJob& j)
             g += 2 * n;
         }
     }
-    j.k.cdef = j.C->d;
+    j.k.dbk = j.D->d;
+    j.k.cdef = j.Co->d;
     if (j.L) j.k.lrout = j.L->d;
     j.seq = ++c->seq;
     return AV1R_OK;
@@ -1354,7 +1373,7 @@ static void job_end(FrameJob& j)
 {
     av1r_ctx* c = j.c;
     const av1r_frame_hdr* h = &j.P->hdr;
-    FrameBuf* out = j.L ? j.L : j.C;
+    FrameBuf* out = j.out;
     out->seq = j.seq;
     c->lastSeq = j.seq;
     if (h->frame_type == 0 && h->refresh_frame_flags == 0xff) {  // KEY_FRAME refreshing every slot
@@ -1362,8 +1381,8 @@ static void job_end(FrameJob& j)
         if (c->failed.empty()) c->keySeqs.clear();
         c->keySeqs.push_back(j.seq);
     }
-    if (j.L) frame_unref(c, j.C);
-    frame_unref(c, j.R);
+    for (FrameBuf* f : {j.R, j.C, j.L})
+        if (f && f != out) frame_unref(c, f);
     if (c->keepStages) {
         frame_ref(out);
         frame_unref(c, c->stage[AV1R_STAGE_LR]);
@@ -1663,9 +1682,17 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
             HIPCHK(hipEventRecord(lc->auxGo, st));
             HIPCHK(hipStreamWaitEvent(lc->aux, lc->auxGo, 0));
         }
-        if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, sp);
-        if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, sp);
-        if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
+        // one grid for every inter tile (k_inter_all; AV1R_INTER_MERGED=0: the three kernels)
+        static const bool merged = !getenv("AV1R_INTER_MERGED") || atoi(getenv("AV1R_INTER_MERGED")) != 0;
+        auto pad8 = [](uint32_t v) { return (v + 7) & ~7u; };
+        if (merged && !aux) {
+            if (total[0] + total[1] + total[2])
+                launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), trace, st);
+        } else {
+            if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, sp);
+            if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, sp);
+            if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
+        }
         if (aux) {
             HIPCHK(hipEventRecord(lc->auxDone, lc->aux));
             HIPCHK(hipStreamWaitEvent(st, lc->auxDone, 0));
@@ -1746,32 +1773,28 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     HIPCHK(hipGetLastError());
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
-    // ---- the in-loop filters: the three stage kernels, or fused (av1r_set_filter_fusion /
-    // AV1R_FUSED=1: k_post, deblocking -> CDEF -> loop restoration per stripe tile in LDS,
-    // straight into the output frame; measured 1.9x slower) unless the stages
-    // are kept for av1r_read_stage
-    if (g_fusedFilters.load(std::memory_order_relaxed) && !snap) {
-        launch_k_post(dk, n, maxW, maxH, st);
-        if (lc->timing)  // (the whole fused time is reported as the deblocking stage's)
-            for (int e = 2; e <= 4; e++) HIPCHK(hipEventRecord(lc->ev[e], st));
-    } else {
-        // ---- deblocking (LoopFilter::filter, LoopFilter.cpp:40-58), in place, 2 passes
+    // ---- the in-loop filters (decode_frame_wrapup, Av1Decoder.cpp:181-189)
+    // deblocking (LoopFilter::filter, LoopFilter.cpp:40-58): both passes in one launch, tile by
+    // tile in LDS into the deblocked frame (k_deblock), or in place, one launch per pass (k_lf;
+    // AV1R_DEBLOCK_TILE=0)
+    if (deblock_tile()) launch_k_deblock(dk, n, maxW, maxH, st);
+    else {
         launch_k_lf(dk, n, 0, maxUnits, st);
         launch_k_lf(dk, n, 1, maxUnits, st);
-        if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].R))) return rc;
-        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
-        // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
-        launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
-        if (snap) {
-            frame_ref(jobs[0].C);
-            frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
-            lc->stage[AV1R_STAGE_CDEF] = jobs[0].C;
-        }
-        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
-        // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
-        if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
-        if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     }
+    if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].D))) return rc;
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
+    // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
+    launch_k_cdef(dk, n, maxMiCols, maxMiRows, st);
+    if (snap) {
+        frame_ref(jobs[0].Co);
+        frame_unref(lc, lc->stage[AV1R_STAGE_CDEF]);
+        lc->stage[AV1R_STAGE_CDEF] = jobs[0].Co;
+    }
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[3], st));
+    // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
+    if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
+    if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
     HIPCHK(hipGetLastError());
     // the slot's generation moves on only once this launch is certain to record its event
     // (an early return above leaves waiters on the slot's previous launch, which completed)
@@ -2972,7 +2995,6 @@ int av1r_set_flow_spins(av1r_ctx* c, uint32_t spins)
 }
 
 
-int av1r_set_filter_fusion(int on) { return g_fusedFilters.exchange(on ? 1 : 0); }
 
 int av1r_set_fast_intra(int on) { return g_fastIntra.exchange(on ? 1 : 0); }
 

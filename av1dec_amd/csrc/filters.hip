@@ -199,15 +199,25 @@ DEV void lf_filter2(lf2* c, int plane, int limit, int blimit, int thresh, int fi
 struct LfEdge {
     int filterSize, limit, blimit, thresh;
 };
-DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& e)
+// the limits of an edge of level lvl (LoopFilter.cpp:330-359)
+DEV void lf_limits(const av1r_frame_hdr& hd, int lvl, LfEdge& e)
+{
+    const int sharp = hd.lf_sharpness;
+    const int shift = sharp > 4 ? 2 : (sharp > 0 ? 1 : 0);
+    e.limit = sharp > 0 ? CLIP3(1, 9 - sharp, lvl >> shift) : imax(1, lvl >> shift);
+    e.blimit = 2 * (lvl + 2) + e.limit;
+    e.thresh = lvl >> 4;
+}
+// the edge's filter size (e.filterSize) and level (returned; <= 0: no filter)
+DEV int lf_edge_level(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& e)
 {
     const av1r_frame_hdr& hd = *k.hdr;
     const int sub = plane ? 1 : 0;
-    if (plane && !hd.lf_level[plane + 1]) return false;
+    if (plane && !hd.lf_level[plane + 1]) return 0;
     const int x = xP << sub, y = yP << sub;
-    if (x < 0 || y < 0 || x >= k.frame_w || y >= k.frame_h) return false;
-    if (!pass && !x) return false;
-    if (pass && !y) return false;
+    if (x < 0 || y < 0 || x >= k.frame_w || y >= k.frame_h) return 0;
+    if (!pass && !x) return 0;
+    if (pass && !y) return 0;
     const int dx = pass == 0, dy = pass == 1;
     const int row = (y >> 2) | sub, col = (x >> 2) | sub;
     const int prevRow = row - (dy << sub), prevCol = col - (dx << sub);
@@ -220,17 +230,18 @@ DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& 
     // (block and transform sides are powers of two: the remainders as masks, no division)
     const int isBlockEdge = !pass ? !(xP & (av1r_num4x4w[psz] * 4 - 1)) : !(yP & (av1r_num4x4h[psz] * 4 - 1));
     const int isTxEdge = !pass ? !(xP & (av1r_tx_w[txSz] - 1)) : !(yP & (av1r_tx_h[txSz] - 1));
-    if (!(isTxEdge && (isBlockEdge || !skip || isIntra))) return false;
+    if (!(isTxEdge && (isBlockEdge || !skip || isIntra))) return 0;
     const int base = !pass ? imin(av1r_tx_w[prevTx], av1r_tx_w[txSz]) : imin(av1r_tx_h[prevTx], av1r_tx_h[txSz]);
     e.filterSize = !plane ? imin(16, base) : imin(8, base);
     int lvl = lf_level(k, row, col, plane, pass);
     if (!lvl) lvl = lf_level(k, prevRow, prevCol, plane, pass);
+    return lvl;
+}
+DEV bool lf_edge(const KParams& k, int plane, int pass, int xP, int yP, LfEdge& e)
+{
+    const int lvl = lf_edge_level(k, plane, pass, xP, yP, e);
     if (lvl <= 0) return false;
-    const int sharp = hd.lf_sharpness;
-    const int shift = sharp > 4 ? 2 : (sharp > 0 ? 1 : 0);
-    e.limit = sharp > 0 ? CLIP3(1, 9 - sharp, lvl >> shift) : imax(1, lvl >> shift);
-    e.blimit = 2 * (lvl + 2) + e.limit;
-    e.thresh = lvl >> 4;
+    lf_limits(*k.hdr, lvl, e);
     return true;
 }
 
@@ -251,7 +262,31 @@ DEV uint32_t lf_lo2(lf2 a, lf2 b)  // bytes {a.x, b.x, a.y, b.y}
 {
     return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
 }
-DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const LfEdge& e)
+// The unit's pixels: the frame (k_lf, in place) or a tile staged in LDS (k_deblock).  x of
+// the 32-bit forms is a multiple of 4, of the 16-bit forms of 2.
+struct LfGlobalPx {
+    uint8_t* p;
+    int stride;
+    DEV uint8_t* at(int x, int y) const { return p + (size_t)y * stride + x; }
+    DEV uint32_t ld32(int x, int y) const { return *reinterpret_cast<const uint32_t*>(at(x, y)); }
+    DEV void st32(int x, int y, uint32_t v) const { *reinterpret_cast<uint32_t*>(at(x, y)) = v; }
+    DEV void st16(int x, int y, uint32_t v) const { *reinterpret_cast<uint16_t*>(at(x, y)) = (uint16_t)v; }
+    DEV void st8(int x, int y, uint32_t v) const { *at(x, y) = (uint8_t)v; }
+};
+typedef __attribute__((address_space(3))) uint8_t lf_lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lf_lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lf_lds_u32;
+struct LfLdsPx {
+    lf_lds_u8* p;
+    int stride;
+    DEV lf_lds_u8* at(int x, int y) const { return p + y * stride + x; }
+    DEV uint32_t ld32(int x, int y) const { return *reinterpret_cast<lf_lds_u32*>(at(x, y)); }
+    DEV void st32(int x, int y, uint32_t v) const { *reinterpret_cast<lf_lds_u32*>(at(x, y)) = v; }
+    DEV void st16(int x, int y, uint32_t v) const { *reinterpret_cast<lf_lds_u16*>(at(x, y)) = (uint16_t)v; }
+    DEV void st8(int x, int y, uint32_t v) const { *at(x, y) = (uint8_t)v; }
+};
+template <class PX>
+DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e)
 {
     const bool wide = e.filterSize == 16;
     const int n = wide ? 6 : (e.filterSize == 8 && !plane) ? 3 : 2;  // samples written per side
@@ -259,11 +294,10 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
         uint32_t d[4][4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(P.p + (size_t)(yP + i) * P.stride + xP);
-            d[i][1] = row[-1];
-            d[i][2] = row[0];
-            d[i][0] = wide ? row[-2] : 0u;
-            d[i][3] = wide ? row[1] : 0u;
+            d[i][1] = P.ld32(xP - 4, yP + i);
+            d[i][2] = P.ld32(xP, yP + i);
+            d[i][0] = wide ? P.ld32(xP - 8, yP + i) : 0u;
+            d[i][3] = wide ? P.ld32(xP + 4, yP + i) : 0u;
         }
         // rows (0, 1) and (2, 3) filtered as pairs: v[q] = the two rows' samples at x - 8 + q
 #pragma unroll
@@ -275,31 +309,30 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
             // the footprint x - n .. x + n - 1 in the widest aligned stores inside it (the
             // neighbouring edges' footprints start at x - 4 - n' / x + 4 + n'': a store may
             // not spill past x - n or x + n - 1); u(q) = bytes {row a q, q + 1, row b q, q + 1}
-            uint8_t* ra = P.p + (size_t)(yP + 2 * h) * P.stride + xP;
-            uint8_t* rb = ra + P.stride;
+            const int ya = yP + 2 * h, yb = ya + 1;
             auto u = [&](int q) { return lf_lo2(v[q], v[q + 1]); };
             if (n == 6) {
                 const uint32_t u2 = u(2), u4 = u(4), u6 = u(6), u8 = u(8), u10 = u(10), u12 = u(12);
-                *reinterpret_cast<uint16_t*>(ra - 6) = (uint16_t)u2;
-                *reinterpret_cast<uint16_t*>(rb - 6) = (uint16_t)(u2 >> 16);
-                *reinterpret_cast<uint32_t*>(ra - 4) = __builtin_amdgcn_perm(u6, u4, 0x05040100u);
-                *reinterpret_cast<uint32_t*>(rb - 4) = __builtin_amdgcn_perm(u6, u4, 0x07060302u);
-                *reinterpret_cast<uint32_t*>(ra) = __builtin_amdgcn_perm(u10, u8, 0x05040100u);
-                *reinterpret_cast<uint32_t*>(rb) = __builtin_amdgcn_perm(u10, u8, 0x07060302u);
-                *reinterpret_cast<uint16_t*>(ra + 4) = (uint16_t)u12;
-                *reinterpret_cast<uint16_t*>(rb + 4) = (uint16_t)(u12 >> 16);
+                P.st16(xP - 6, ya, u2);
+                P.st16(xP - 6, yb, u2 >> 16);
+                P.st32(xP - 4, ya, __builtin_amdgcn_perm(u6, u4, 0x05040100u));
+                P.st32(xP - 4, yb, __builtin_amdgcn_perm(u6, u4, 0x07060302u));
+                P.st32(xP, ya, __builtin_amdgcn_perm(u10, u8, 0x05040100u));
+                P.st32(xP, yb, __builtin_amdgcn_perm(u10, u8, 0x07060302u));
+                P.st16(xP + 4, ya, u12);
+                P.st16(xP + 4, yb, u12 >> 16);
             } else {
                 const uint32_t u6 = u(6), u8 = u(8);
                 if (n == 3) {
-                    ra[-3] = (uint8_t)v[5].x;
-                    rb[-3] = (uint8_t)v[5].y;
-                    ra[2] = (uint8_t)v[10].x;
-                    rb[2] = (uint8_t)v[10].y;
+                    P.st8(xP - 3, ya, (uint32_t)(uint16_t)v[5].x);
+                    P.st8(xP - 3, yb, (uint32_t)(uint16_t)v[5].y);
+                    P.st8(xP + 2, ya, (uint32_t)(uint16_t)v[10].x);
+                    P.st8(xP + 2, yb, (uint32_t)(uint16_t)v[10].y);
                 }
-                *reinterpret_cast<uint16_t*>(ra - 2) = (uint16_t)u6;
-                *reinterpret_cast<uint16_t*>(rb - 2) = (uint16_t)(u6 >> 16);
-                *reinterpret_cast<uint16_t*>(ra) = (uint16_t)u8;
-                *reinterpret_cast<uint16_t*>(rb) = (uint16_t)(u8 >> 16);
+                P.st16(xP - 2, ya, u6);
+                P.st16(xP - 2, yb, u6 >> 16);
+                P.st16(xP, ya, u8);
+                P.st16(xP, yb, u8 >> 16);
             }
         }
         return;
@@ -308,7 +341,7 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const bool need = (r >= 4 && r < 12) || wide;
-        d[r] = need ? *reinterpret_cast<const uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) : 0u;
+        d[r] = need ? P.ld32(xP, yP - 8 + r) : 0u;
     }
     // columns (0, 1) and (2, 3) filtered as pairs
     lf2 lo[16], hi[16];
@@ -322,8 +355,8 @@ DEV void lf_unit(const DevPlane& P, int plane, int pass, int xP, int yP, const L
 #pragma unroll
     for (int r = 2; r < 14; r++)
         if (r >= 8 - n && r < 8 + n)
-            *reinterpret_cast<uint32_t*>(P.p + (size_t)(yP - 8 + r) * P.stride + xP) =
-                __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u);
+            P.st32(xP, yP - 8 + r,
+                __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u));
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
@@ -355,10 +388,175 @@ DEV void lf_body(const KParams* kps, int pass)
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
     LfEdge e;
     if (!lf_edge(k, plane, pass, xP, yP, e)) return;
-    lf_unit(k.cur.pl[plane], plane, pass, xP, yP, e);
+    const DevPlane& P = k.cur.pl[plane];
+    lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
+
+// ------------------------------------------------------------------------------------
+// k_deblock: both deblocking passes of one 64x64 luma tile and its two 32x32 chroma tiles
+// in ONE workgroup, in LDS, into the deblocked frame (k.dbk).  LoopFilter::filter
+// (LoopFilter.cpp:40-58) runs pass 0 (vertical edges) over the whole frame, then pass 1;
+// within a tile the same order holds, and what a tile's pixels depend on is bounded:
+//   * an edge at x modifies at most 6 luma / 2 chroma samples on each side and reads 7 / 3
+//     (the filter length is capped by the transform sizes on both sides), so the pixels of
+//     [x0, x0 + 64) after pass 0 are set by the vertical edges x0 .. x0 + 64, which read
+//     [x0 - 8, x0 + 72);
+//   * pass 1 over columns [x0, x0 + 64) needs the pass-0 pixels of rows [y0 - 8, y0 + 72)
+//     (edges y0 .. y0 + 64).
+// So the tile stages [x0 - 8, x0 + 72) x [y0 - 8, y0 + 72) (chroma [cx0 - 8, cx0 + 40) x
+// [cy0 - 8, cy0 + 40)), runs pass 0 over all its rows and pass 1 over its columns, and
+// writes back only its own 64 x 64 (32 x 32).  The boundary edges are computed by both
+// tiles they touch, identically (1.3x the edges of pass 0, 1.06x of pass 1).  Each edge's
+// decision (filter size and level, lf_edge: LoopFilter.cpp:85-126, 301-359) is taken once,
+// up front, into a byte of LDS: the mode-info loads go out together with the pixel loads.
+// Reads k.cur (reconstruction, intact during the launch), writes k.dbk.
+// ------------------------------------------------------------------------------------
+#define DB_YS 80  // luma tile: 80 x 80 (64 + 8 each side)
+#define DB_CS 48  // chroma tile: 48 x 48 (32 + 8 each side)
+struct DbLds {
+    uint8_t y[DB_YS * DB_YS];
+    uint8_t uv[2][DB_CS * DB_CS];
+    uint8_t c0y[20 * 17];     // pass 0 luma: unit row u (rows y0 - 8 + 4u), edge e (x0 + 4e): [u * 17 + e]
+    uint8_t c1y[17 * 16];     // pass 1 luma: edge e (y0 + 4e), unit column u (x0 + 4u): [e * 16 + u]
+    uint8_t c0c[2][12 * 9];   // pass 0 chroma: unit row u (cy0 - 8 + 4u), edge e (cx0 + 4e)
+    uint8_t c1c[2][9 * 8];    // pass 1 chroma: edge e (cy0 + 4e), unit column u (cx0 + 4u)
+};
+// an edge decision as one byte: the level (1..63) and the filter size (4 / 8 / 16 as 0 / 1 / 2
+// in bits 6..7); 0 = no filter
+DEV uint32_t lf_code(const KParams& k, int plane, int pass, int xP, int yP)
+{
+    LfEdge e;
+    const int lvl = lf_edge_level(k, plane, pass, xP, yP, e);
+    if (lvl <= 0) return 0;
+    return (uint32_t)lvl | ((e.filterSize == 4 ? 0u : e.filterSize == 8 ? 1u : 2u) << 6);
+}
+DEV LfEdge lf_decode(const av1r_frame_hdr& hd, uint32_t code)
+{
+    LfEdge e;
+    e.filterSize = 4 << (code >> 6);
+    lf_limits(hd, (int)(code & 63), e);
+    return e;
+}
+extern "C" __global__ __launch_bounds__(256) void k_deblock(const KParams* kps)
+{
+    __shared__ __align__(16) DbLds L;
+    const int t = threadIdx.x;
+    const uint3 wg = xcd_block();  // x: 64-column tile, y: 64-row tile, z: frame
+    const KParams& k = KP(kps, wg.z);
+    const av1r_frame_hdr& hd = *k.hdr;
+    const int x0 = (int)wg.x * 64, y0 = (int)wg.y * 64;
+    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
+    if (x0 >= limX || y0 >= limY) return;
+    const int cx0 = x0 >> 1, cy0 = y0 >> 1;
+    // ---- stage the reconstructed pixels: every lane's dwords loaded before its first LDS
+    // store (one memory round trip).  Dwords outside [0, lim + 8) (the frame's top / left
+    // margin does not exist; nothing past the mi grid + 8 is read by a filter) stay 0.
+    constexpr int NDY = DB_YS / 4, NY = DB_YS * NDY, QY = (NY + 255) / 256;
+    constexpr int NDC = DB_CS / 4, NC = DB_CS * NDC, QC = (2 * NC + 255) / 256;
+    uint32_t vy[QY], vc[QC];
+#pragma unroll
+    for (int u = 0; u < QY; u++) {
+        const int q = t + 256 * u, i = q / NDY, d = q - i * NDY;
+        const int y = y0 - 8 + i, x = x0 - 8 + 4 * d;
+        vy[u] = q < NY && y >= 0 && x >= 0 && y < limY + 8 && x < limX + 8
+                    ? *reinterpret_cast<const uint32_t*>(k.cur.pl[0].p + (size_t)y * k.cur.pl[0].stride + x) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < QC; u++) {
+        const int q = t + 256 * u, pl = q >= NC, r = q - pl * NC, i = r / NDC, d = r - i * NDC;
+        const int y = cy0 - 8 + i, x = cx0 - 8 + 4 * d;
+        const DevPlane& P = k.cur.pl[1 + pl];
+        vc[u] = q < 2 * NC && y >= 0 && x >= 0 && y < (limY >> 1) + 8 && x < (limX >> 1) + 8
+                    ? *reinterpret_cast<const uint32_t*>(P.p + (size_t)y * P.stride + x) : 0u;
+    }
+    // ---- the edge decisions of both passes (mode info only; their loads overlap the above)
+    const bool on = hd.lf_level[0] || hd.lf_level[1];  // else LoopFilter::filter is skipped: a copy
+    for (int q = t; q < 20 * 17 + 17 * 16 + 2 * (12 * 9 + 9 * 8); q += 256) {
+        uint32_t c = 0;
+        if (q < 340) {
+            const int u = q / 17, e = q - u * 17;
+            if (on) c = lf_code(k, 0, 0, x0 + 4 * e, y0 - 8 + 4 * u);
+            L.c0y[q] = (uint8_t)c;
+        } else if (q < 340 + 272) {
+            const int r = q - 340, e = r >> 4, u = r & 15;
+            if (on) c = lf_code(k, 0, 1, x0 + 4 * u, y0 + 4 * e);
+            L.c1y[r] = (uint8_t)c;
+        } else {
+            const int r = q - 612, pl = r >= 180, r2 = r - 180 * pl;
+            if (r2 < 108) {
+                const int u = r2 / 9, e = r2 - u * 9;
+                if (on) c = lf_code(k, 1 + pl, 0, cx0 + 4 * e, cy0 - 8 + 4 * u);
+                L.c0c[pl][r2] = (uint8_t)c;
+            } else {
+                const int r3 = r2 - 108, e = r3 >> 3, u = r3 & 7;
+                if (on) c = lf_code(k, 1 + pl, 1, cx0 + 4 * u, cy0 + 4 * e);
+                L.c1c[pl][r3] = (uint8_t)c;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < QY; u++) {
+        const int q = t + 256 * u;
+        if (q < NY) reinterpret_cast<uint32_t*>(L.y)[q] = vy[u];
+    }
+#pragma unroll
+    for (int u = 0; u < QC; u++) {
+        const int q = t + 256 * u, pl = q >= NC;
+        if (q < 2 * NC) reinterpret_cast<uint32_t*>(L.uv[pl])[q - pl * NC] = vc[u];
+    }
+    __syncthreads();
+    if (on) {
+        // ---- pass 0: vertical edges over every staged row
+        for (int q = t; q < 340 + 216; q += 256) {
+            uint32_t c;
+            int plane, xT, yT;
+            if (q < 340) {
+                const int u = q / 17, e = q - u * 17;
+                c = L.c0y[q], plane = 0, xT = 8 + 4 * e, yT = 4 * u;
+            } else {
+                const int r = q - 340, pl = r >= 108, r2 = r - 108 * pl, u = r2 / 9, e = r2 - u * 9;
+                c = L.c0c[pl][r2], plane = 1 + pl, xT = 8 + 4 * e, yT = 4 * u;
+            }
+            if (!c) continue;
+            const LfLdsPx P{(lf_lds_u8*)(plane ? L.uv[plane - 1] : L.y), plane ? DB_CS : DB_YS};
+            lf_unit(P, plane, 0, xT, yT, lf_decode(hd, c));
+        }
+        __syncthreads();
+        // ---- pass 1: horizontal edges over the tile's own columns
+        for (int q = t; q < 272 + 144; q += 256) {
+            uint32_t c;
+            int plane, xT, yT;
+            if (q < 272) {
+                const int e = q >> 4, u = q & 15;
+                c = L.c1y[q], plane = 0, xT = 8 + 4 * u, yT = 8 + 4 * e;
+            } else {
+                const int r = q - 272, pl = r >= 72, r2 = r - 72 * pl, e = r2 >> 3, u = r2 & 7;
+                c = L.c1c[pl][r2], plane = 1 + pl, xT = 8 + 4 * u, yT = 8 + 4 * e;
+            }
+            if (!c) continue;
+            const LfLdsPx P{(lf_lds_u8*)(plane ? L.uv[plane - 1] : L.y), plane ? DB_CS : DB_YS};
+            lf_unit(P, plane, 1, xT, yT, lf_decode(hd, c));
+        }
+        __syncthreads();
+    }
+    // ---- the tile's own pixels into the deblocked frame (the mi grid's extent)
+    const int rowsY = imin(64, limY - y0), colsY = imin(64, limX - x0);  // (multiples of 4)
+    for (int q = t; q < 64 * 16; q += 256) {
+        const int i = q >> 4, d = q & 15;
+        if (i < rowsY && 4 * d < colsY)
+            *reinterpret_cast<uint32_t*>(k.dbk.pl[0].p + (size_t)(y0 + i) * k.dbk.pl[0].stride + x0 + 4 * d) =
+                *reinterpret_cast<const uint32_t*>(&L.y[(8 + i) * DB_YS + 8 + 4 * d]);
+    }
+    const int rowsC = rowsY >> 1, colsC = colsY >> 1;  // (multiples of 2)
+    for (int q = t; q < 2 * 32 * 16; q += 256) {
+        const int pl = q >> 9, r = q & 511, i = r >> 4, d = r & 15;  // 16-bit pairs
+        if (i < rowsC && 2 * d < colsC)
+            *reinterpret_cast<uint16_t*>(k.dbk.pl[1 + pl].p + (size_t)(cy0 + i) * k.dbk.pl[1 + pl].stride + cx0 + 2 * d) =
+                *reinterpret_cast<const uint16_t*>(&L.uv[pl][(8 + i) * DB_CS + 8 + 2 * d]);
+    }
+}
 
 // ------------------------------------------------------------------------------------
 // CDEF
@@ -545,7 +743,7 @@ DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int 
     }
 }
 
-// grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.cur, writes k.cdef
+// grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.dbk, writes k.cdef
 DEV void cdef_body(const KParams* kps)
 {
     __shared__ CdefLds L;
@@ -564,13 +762,13 @@ DEV void cdef_body(const KParams* kps)
         const int nl = cols4, nc = cols4;  // dwords per luma row, 16-bit pairs per chroma row
         for (int q = t; q < rows4 * 4 * nl; q += 256) {
             const int i = q / nl, j = 4 * (q - i * nl);
-            *reinterpret_cast<uint32_t*>(&px(k.cdef.pl[0], x0 + j, y0 + i)) = *reinterpret_cast<const uint32_t*>(&px(k.cur.pl[0], x0 + j, y0 + i));
+            *reinterpret_cast<uint32_t*>(&px(k.cdef.pl[0], x0 + j, y0 + i)) = *reinterpret_cast<const uint32_t*>(&px(k.dbk.pl[0], x0 + j, y0 + i));
         }
         for (int q = t; q < 2 * rows4 * 2 * nc; q += 256) {
             const int pl = 1 + (q >= rows4 * 2 * nc), e = q - (pl - 1) * rows4 * 2 * nc;
             const int i = e / nc, j = 2 * (e - i * nc);
             *reinterpret_cast<uint16_t*>(&px(k.cdef.pl[pl], x0 / 2 + j, y0 / 2 + i)) =
-                *reinterpret_cast<const uint16_t*>(&px(k.cur.pl[pl], x0 / 2 + j, y0 / 2 + i));
+                *reinterpret_cast<const uint16_t*>(&px(k.dbk.pl[pl], x0 / 2 + j, y0 / 2 + i));
         }
         return;
     }
@@ -586,7 +784,7 @@ DEV void cdef_body(const KParams* kps)
         constexpr int NDC = CD_CS / 4, NC = CD_CR * NDC, QC = (NC + 255) / 256;
         uint32_t vy[QY], vc[2][QC];
         // (lanes past a tile load its last dword again: no branch around the loads)
-        const DevPlane PY = k.cur.pl[0], PU = k.cur.pl[1], PV = k.cur.pl[2];
+        const DevPlane PY = k.dbk.pl[0], PU = k.dbk.pl[1], PV = k.dbk.pl[2];
 #pragma unroll
         for (int u = 0; u < QY; u++) {
             const int q = imin(t + 256 * u, NY - 1), i = q / NDY, d = q - i * NDY;
@@ -612,9 +810,9 @@ DEV void cdef_body(const KParams* kps)
                 if (q < NC) *reinterpret_cast<uint32_t*>(&L.uv[pl][i][4 * d]) = vc[pl][u];
             }
     } else {
-        cd_stage(&L.y[0][0], CD_LS, CD_LR, k.cur.pl[0], x0, y0, edge, limX - 1, limY - 1);
-        cd_stage(&L.uv[0][0][0], CD_CS, CD_CR, k.cur.pl[1], cx0, cy0, cedge, climX - 1, climY - 1);
-        cd_stage(&L.uv[1][0][0], CD_CS, CD_CR, k.cur.pl[2], cx0, cy0, cedge, climX - 1, climY - 1);
+        cd_stage(&L.y[0][0], CD_LS, CD_LR, k.dbk.pl[0], x0, y0, edge, limX - 1, limY - 1);
+        cd_stage(&L.uv[0][0][0], CD_CS, CD_CR, k.dbk.pl[1], cx0, cy0, cedge, climX - 1, climY - 1);
+        cd_stage(&L.uv[1][0][0], CD_CS, CD_CR, k.dbk.pl[2], cx0, cy0, cedge, climX - 1, climY - 1);
     }
     if (t < 64) {
         const int br = r0 + (t >> 3) * 2, bc = c0 + (t & 7) * 2;
@@ -740,8 +938,8 @@ extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps) { c
 // Loop restoration
 // ------------------------------------------------------------------------------------
 struct LrPix {
-    DevPlane cdefP;  // CDEF output (k.cur)
-    DevPlane preP;   // deblocked, pre-CDEF frame (k.cur)
+    DevPlane cdefP;  // CDEF output (k.cdef)
+    DevPlane preP;   // deblocked, pre-CDEF frame (k.dbk)
     int start, end;  // stripe
 };
 // get_source_sample (LoopRestoration.cpp:234-246) + extendBorder(3) as clamping
@@ -1040,7 +1238,7 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
 }
 
 // one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
-// frame (k.cdef) and the deblocked frame (k.cur, stripe rows), writes k.lrout.
+// frame (k.cdef) and the deblocked frame (k.dbk, stripe rows), writes k.lrout.
 extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
 {
     __shared__ LrLds L;
@@ -1065,7 +1263,7 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
     const int sNum = wg.y / perStripe, half = wg.y - sNum * perStripe;
     LrPix S;
     S.cdefP = C;
-    S.preP = k.cur.pl[plane];
+    S.preP = k.dbk.pl[plane];
     S.start = sNum * stripeH - off;
     S.end = S.start + stripeH;
     const int ty0 = imax(0, S.start + half * LR_TH), ty1 = imin(S.start + (half + 1) * LR_TH, C.h);
@@ -1134,293 +1332,6 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
     }
     __syncthreads();
     lr_filter_tile(L, h, plane, x0, tw, ty0, th, y0, us, cols, uc0, nU, planeEndX, planeEndY, O);
-}
-
-// ------------------------------------------------------------------------------------
-// k_post: deblocking -> CDEF -> loop restoration fused, one workgroup per (frame, 64-row
-// loop-restoration stripe, 64 luma columns) with its two chroma tiles.  The reference runs
-// the three filters frame after frame (Av1Decoder.cpp:171-192: LoopFilter::filter, then
-// Cdef::filter into a new frame, Cdef.cpp:43, then LoopRestoration::filter into another,
-// LoopRestoration.cpp:191-219); here the reconstructed pixels the tile needs are read once
-// into LDS, deblocked there (both passes, LoopFilter.cpp:40-126), CDEF'd into LDS
-// (Cdef.cpp:72-198) and restored (LoopRestoration.cpp:136-479) straight to the output
-// frame: neither the deblocked nor the CDEF frame exists in memory.
-//
-// Geometry (luma; chroma the same at half size, with its shorter filters).  Stripe k covers
-// rows [s0, s0 + 64), s0 = 64k - 8 (LoopRestoration.cpp:136-189).  Loop restoration of the
-// tile reads the source 3 pixels around it: CDEF output inside the stripe, deblocked rows
-// s0 - 2, s0 - 1, s0 + 64, s0 + 65 outside it (get_source_sample, :234-246).  CDEF of the
-// 4-pixel groups x0 - 4 .. x0 + 67 over the stripe's rows works on the 8x8 blocks x0 - 8 ..
-// x0 + 71 (direction search per block) and reads deblocked pixels 2 around them.  Those are
-// the output of the horizontal-edge pass at edges s0 - 4 .. s0 + 68 (a 16-wide filter
-// writes 6 and reads 7 rows on each side), which reads the vertical-edge pass's output over
-// rows s0 - 11 .. s0 + 74; the vertical edges x0 - 8 .. x0 + 72 that write the columns
-// needed read x0 - 15 .. x0 + 78.  So the tile stages reconstructed rows [s0 - 12, s0 + 76)
-// x columns [x0 - 16, x0 + 80) (chroma: [cs0 - 4, cs0 + 36) x [cx0 - 8, cx0 + 40)) and runs
-// every edge of each pass that touches them; a pass's edges never overlap (the filter lengths
-// are bounded by the transform sizes on both sides), exactly as on the whole frame.
-// Recomputed halo: 1.9x the tile's deblocking, 1.25x its CDEF; no frame round trips.
-// ------------------------------------------------------------------------------------
-#define PY_R 88   // luma: rows s0 - 12 .. s0 + 75
-#define PY_C 96   // luma: columns x0 - 16 .. x0 + 79
-#define PY_OY 12
-#define PY_OX 16
-#define PC_R 40   // chroma: rows cs0 - 4 .. cs0 + 35
-#define PC_C 48   // chroma: columns cx0 - 8 .. cx0 + 39
-#define PC_OY 4
-#define PC_OX 8
-#define PO_YC 72  // CDEF output, luma: columns x0 - 4 .. x0 + 67, rows s0 .. s0 + 63
-#define PO_CC 40  // chroma: columns cx0 - 4 .. cx0 + 35, rows cs0 .. cs0 + 31
-#define PB_X 10   // 8x8 luma blocks: columns x0 - 8 .. x0 + 71
-#define PB (PB_X * 8)
-struct PostLds {
-    uint8_t y[PY_R][PY_C];
-    uint8_t uv[2][PC_R][PC_C];
-    uint8_t oy[64][PO_YC];
-    uint8_t ouv[2][32][PO_CC];
-    int cost[PB][8];
-    int16_t pri[PB];
-    int8_t idx[PB];
-    uint8_t filt[PB];
-    int16_t offY[PB][6], offC[PB][6];
-    LrLds lr;
-};
-
-// stage rows [y0, y0 + nr) x columns [x0, x0 + nc) (nc a multiple of 4, x0 of 4) of plane P
-// into t (row stride ts): dwords where the row and columns lie inside [0, mx] x [0, my] (the
-// mi grid), else bytes with clamped coordinates (never read by a filter that runs)
-DEV void post_stage(uint8_t* t, int ts, int nr, int nc, const DevPlane& P, int x0, int y0, int mx, int my)
-{
-    const int nd = nc / 4;
-    for (int q = threadIdx.x; q < nr * nd; q += 256) {
-        const int i = q / nd, d = q - i * nd;
-        const int y = y0 + i, x = x0 + 4 * d;
-        uint32_t v;
-        if (y >= 0 && y <= my && x >= 0 && x + 3 <= mx) {
-            v = *reinterpret_cast<const uint32_t*>(P.p + (size_t)y * P.stride + x);
-        } else {
-            const int yy = CLIP3(0, my, y);
-            v = 0;
-#pragma unroll
-            for (int b = 0; b < 4; b++) v |= (uint32_t)px(P, CLIP3(0, mx, x + b), yy) << (8 * b);
-        }
-        *reinterpret_cast<uint32_t*>(t + i * ts + 4 * d) = v;
-    }
-}
-
-extern "C" __global__ __launch_bounds__(256) void k_post(const KParams* kps)
-{
-    __shared__ PostLds L;
-    const int t = threadIdx.x;
-    const uint3 wg = xcd_block();  // x: 64-column tile, y: stripe, z: frame
-    const KParams& k = KP(kps, wg.z);
-    const av1r_frame_hdr& h = *k.hdr;
-    const int x0 = (int)wg.x * 64, s0 = (int)wg.y * 64 - 8;
-    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
-    if (x0 >= k.frame_w || imax(s0, 0) >= k.frame_h) return;
-    const int cx0 = x0 >> 1, cs0 = s0 >> 1, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
-    // ---- the reconstructed pixels
-    post_stage(&L.y[0][0], PY_C, PY_R, PY_C, k.cur.pl[0], x0 - PY_OX, s0 - PY_OY, limX - 1, limY - 1);
-    for (int pl = 0; pl < 2; pl++)
-        post_stage(&L.uv[pl][0][0], PC_C, PC_R, PC_C, k.cur.pl[1 + pl], cx0 - PC_OX, cs0 - PC_OY, climX - 1, climY - 1);
-    // ---- CDEF's per-block parameters (mode info only: overlaps the staging loads)
-    if (t < PB) {
-        const int bx = x0 - 8 + 8 * (t % PB_X), by = s0 + 8 * (t / PB_X);
-        int idx = -1, f = 0;
-        if (bx >= 0 && by >= 0 && bx < limX && by < limY) {
-            idx = k.cdef_idx[(by >> 6) * h.cdef_cols + (bx >> 6)];
-            const int br = by >> 2, bc = bx >> 2;
-            // cdef_block's skip test (Cdef.cpp:79-82)
-            f = idx != -1 && !((mi_at(k, br, bc).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc).flags & AV1R_MI_SKIP)
-                && (mi_at(k, br, bc + 1).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc + 1).flags & AV1R_MI_SKIP));
-        }
-        L.idx[t] = (int8_t)idx;
-        L.filt[t] = (uint8_t)f;
-    }
-    __syncthreads();
-    // ---- deblocking, both passes over the staged tiles (LoopFilter::filter, LoopFilter.cpp:40-58)
-    if (h.lf_level[0] || h.lf_level[1]) {
-        for (int pass = 0; pass < 2; pass++) {
-            // pass 0: luma edge columns x0 - 8 .. x0 + 72 (21) x 4-row units s0 - 12 .. s0 + 72 (22);
-            //         chroma edge columns cx0 - 4 .. cx0 + 36 (11) x 4-row units cs0 - 4 .. cs0 + 32 (10)
-            // pass 1: luma edge rows s0 - 4 .. s0 + 68 (19) x 4-column units x0 - 8 .. x0 + 68 (20);
-            //         chroma edge rows cs0 .. cs0 + 32 (9) x 4-column units cx0 - 8 .. cx0 + 36 (12)
-            const int nEy = pass ? 19 : 21, nUy = pass ? 20 : 22;
-            const int nEc = pass ? 9 : 11, nUc = pass ? 12 : 10;
-            const int nY = nEy * nUy, nT = nY + 2 * nEc * nUc;
-            for (int q = t; q < nT; q += 256) {
-                int plane, e, u;
-                if (q < nY) {
-                    plane = 0;
-                    e = q / nUy;
-                    u = q - e * nUy;
-                } else {
-                    const int r = q - nY;
-                    plane = 1 + (r >= nEc * nUc);
-                    const int r2 = r - (plane - 1) * nEc * nUc;
-                    e = r2 / nUc;
-                    u = r2 - e * nUc;
-                }
-                int xP, yP;
-                if (!plane) {
-                    xP = pass ? x0 - 8 + 4 * u : x0 - 8 + 4 * e;
-                    yP = pass ? s0 - 4 + 4 * e : s0 - 12 + 4 * u;
-                } else {
-                    xP = pass ? cx0 - 8 + 4 * u : cx0 - 4 + 4 * e;
-                    yP = pass ? cs0 + 4 * e : cs0 - 4 + 4 * u;
-                }
-                LfEdge ed;
-                if (!lf_edge(k, plane, pass, xP, yP, ed)) continue;
-                uint8_t* tile = plane ? &L.uv[plane - 1][0][0] : &L.y[0][0];
-                const int ts = plane ? PC_C : PY_C;
-                uint8_t* c = plane ? tile + (yP - cs0 + PC_OY) * ts + (xP - cx0 + PC_OX)
-                                   : tile + (yP - s0 + PY_OY) * ts + (xP - x0 + PY_OX);
-                const int step = pass ? ts : 1, along = pass ? 1 : ts;
-                for (int i = 0; i < 4; i++) lf_filter(c + along * i, step, plane, ed.limit, ed.blimit, ed.thresh, ed.filterSize);
-            }
-            __syncthreads();
-        }
-    }
-    // ---- CDEF direction search (cdefDirection, Cdef.cpp:203-261): one lane per (block, direction)
-    for (int q = t; q < PB * 8; q += 256) {
-        const int b = q >> 3, d = q & 7;
-        if (!L.filt[b]) continue;
-        const uint8_t* blk = &L.y[PY_OY + 8 * (b / PB_X)][PY_OX - 8 + 8 * (b % PB_X)];
-        int c;
-        switch (d) {
-        case 0: c = cdef_cost<0>(blk, PY_C); break;
-        case 1: c = cdef_cost<1>(blk, PY_C); break;
-        case 2: c = cdef_cost<2>(blk, PY_C); break;
-        case 3: c = cdef_cost<3>(blk, PY_C); break;
-        case 4: c = cdef_cost<4>(blk, PY_C); break;
-        case 5: c = cdef_cost<5>(blk, PY_C); break;
-        case 6: c = cdef_cost<6>(blk, PY_C); break;
-        default: c = cdef_cost<7>(blk, PY_C); break;
-        }
-        L.cost[b][d] = c;
-    }
-    __syncthreads();
-    if (t < PB && L.filt[t]) {
-        int best = 0, yDir = 0;
-        for (int d = 0; d < 8; d++)
-            if (L.cost[t][d] > best) {
-                best = L.cost[t][d];
-                yDir = d;
-            }
-        const int idx = L.idx[t];
-        const int var = (best - L.cost[t][(yDir + 4) & 7]) >> 10;
-        const int priStr = h.cdef_y_pri[idx];
-        const int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
-        L.pri[t] = (int16_t)(var ? (priStr * (4 + varStr) + 8) >> 4 : 0);
-        const int dy0 = priStr == 0 ? 0 : yDir, dc0 = h.cdef_uv_pri[idx] == 0 ? 0 : av1r_cdef_uv_dir420[yDir];
-#pragma unroll
-        for (int s = 0; s < 3; s++)
-#pragma unroll
-            for (int kk = 0; kk < 2; kk++) {
-                const int dl = s == 0 ? dy0 : ((dy0 + (s == 1 ? -2 : 2)) & 7);
-                const int dc = s == 0 ? dc0 : ((dc0 + (s == 1 ? -2 : 2)) & 7);
-                L.offY[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dl][kk][0] * PY_C + av1r_cdef_directions[dl][kk][1]);
-                L.offC[t][s * 2 + kk] = (int16_t)(av1r_cdef_directions[dc][kk][0] * PC_C + av1r_cdef_directions[dc][kk][1]);
-            }
-    }
-    __syncthreads();
-    // ---- CDEF filter (cdefFilter, Cdef.cpp:158-198): luma 4-pixel groups x0 - 4 .. x0 + 64
-    // over the stripe's rows, chroma groups cx0 - 4 .. cx0 + 32 (unfiltered blocks: copied)
-    for (int q = t; q < 64 * 18 + 2 * 32 * 10; q += 256) {
-        int plane, r, x, y;
-        if (q < 64 * 18) {
-            plane = 0;
-            r = q / 18;
-            x = x0 - 4 + 4 * (q - r * 18);
-            y = s0 + r;
-            if (x < 0 || x >= limX || y < 0 || y >= limY) continue;
-        } else {
-            const int e = q - 64 * 18;
-            plane = 1 + (e >= 320);
-            const int e2 = e - (plane - 1) * 320;
-            r = e2 / 10;
-            x = cx0 - 4 + 4 * (e2 - r * 10);
-            y = cs0 + r;
-            if (x < 0 || x >= climX || y < 0 || y >= climY) continue;
-        }
-        const int sub = plane ? 1 : 0;
-        const int b = (r >> (3 - sub)) * PB_X + ((x - ((x0 - 8) >> sub)) >> (3 - sub));
-        const uint8_t* tile = plane ? &L.uv[plane - 1][0][0] : &L.y[0][0];
-        const int ts = plane ? PC_C : PY_C;
-        const int p = plane ? (y - cs0 + PC_OY) * ts + (x - cx0 + PC_OX) : (y - s0 + PY_OY) * ts + (x - x0 + PY_OX);
-        const int mx = plane ? climX : limX, my = plane ? climY : limY;
-        uint32_t o;
-        if (!L.filt[b]) {
-            o = *reinterpret_cast<const uint32_t*>(tile + p);
-        } else {
-            const int idx = L.idx[b];
-            const int pri = plane ? h.cdef_uv_pri[idx] : L.pri[b];
-            const int sec = plane ? h.cdef_uv_sec[idx] : h.cdef_y_sec[idx];
-            const int damping = h.cdef_damping - sub;
-            const int16_t* off = plane ? L.offC[b] : L.offY[b];
-            if (x < CD_H || y < CD_H || x + 4 + CD_H > mx || y + CD_H >= my)
-                o = cdef_quad<true>(tile, p, off, pri, sec, damping, x, y, ts, mx, my);
-            else
-                o = cdef_quad<false>(tile, p, off, pri, sec, damping, 0, 0, ts, 0, 0);
-        }
-        uint8_t* dst = plane ? &L.ouv[plane - 1][r][x - cx0 + 4] : &L.oy[r][x - x0 + 4];
-        *reinterpret_cast<uint32_t*>(dst) = o;
-    }
-    __syncthreads();
-    // ---- loop restoration (or the CDEF output itself) into the output frame
-    for (int plane = 0; plane < 3; plane++) {
-        const int sub = plane ? 1 : 0;
-        const DevPlane O = h.uses_lr ? k.lrout.pl[plane] : k.cdef.pl[plane];
-        const int Wp = O.w, Hp = O.h;
-        const int px0 = x0 >> sub, start = s0 >> sub, stripeH = 64 >> sub;
-        const int tw = imin(64 >> sub, Wp - px0);
-        if (tw <= 0) continue;
-        const uint8_t* cd = plane ? &L.ouv[plane - 1][0][0] : &L.oy[0][0];  // CDEF output, rows from start
-        const int cs = plane ? PO_CC : PO_YC;
-        if (!h.uses_lr || h.lr_type[plane] == AV1R_RESTORE_NONE) {
-            const int r0 = imax(start, 0), r1 = imin(start + stripeH, Hp);
-            for (int q = t; q < (r1 - r0) * tw; q += 256) {
-                const int i = q / tw, c = q - i * tw;
-                O.p[(size_t)(r0 + i) * O.stride + px0 + c] = cd[(r0 + i - start) * cs + c + 4];
-            }
-            continue;
-        }
-        const uint8_t* db = plane ? &L.uv[plane - 1][0][0] : &L.y[0][0];  // deblocked
-        const int dbs = plane ? PC_C : PY_C, dby = plane ? cs0 - PC_OY : s0 - PY_OY, dbx = plane ? cx0 - PC_OX : x0 - PY_OX;
-        const int us = h.lr_unit_size[plane];
-        const int rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
-        const int planeEndX = r2(k.frame_w, sub), planeEndY = r2(k.frame_h, sub);
-        const int off = 8 >> sub, end = start + stripeH;
-        for (int half = 0; half < stripeH / LR_TH; half++) {
-            const int ty0 = imax(0, start + half * LR_TH), ty1 = imin(start + (half + 1) * LR_TH, Hp);
-            if (ty0 >= ty1) continue;
-            const int th = ty1 - ty0;
-            const int ur = imin((ty0 + off) / us, rows - 1);
-            const int uc0 = imin(px0 / us, cols - 1);
-            const int nU = imin((px0 + tw - 1) / us, cols - 1) - uc0 + 1;
-            if (t < nU) L.lr.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
-            // the source (get_source_sample, LoopRestoration.cpp:234-246, with extendBorder(3)
-            // as clamping): CDEF output inside the stripe, deblocked rows outside it
-            for (int q = t; q < (th + 6) * (tw + 8); q += 256) {
-                const int i = q / (tw + 8), j = q - i * (tw + 8);
-                int y = ty0 - 3 + i;
-                const bool pre = y < start || y >= end;
-                if (y < start) y = imax(start - 2, y);
-                else if (y >= end) y = imin(end + 1, y);
-                y = CLIP3(0, Hp - 1, y);
-                const int x = CLIP3(0, Wp - 1, px0 - 4 + j);
-                L.lr.src[i][j] = pre ? db[(y - dby) * dbs + (x - dbx)] : cd[(y - start) * cs + (x - px0 + 4)];
-            }
-            __syncthreads();
-            lr_filter_tile(L.lr, h, plane, px0, tw, ty0, th, imax(start, 0), us, cols, uc0, nU, planeEndX, planeEndY, O);
-            __syncthreads();  // L.lr is staged again by the next half / plane
-        }
-    }
-}
-
-void launch_k_post(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_post, dim3((maxW + 63) / 64, (maxH + 8 + 63) / 64, n), dim3(256), 0, s, kps);
 }
 
 // The launch metadata, copied by the compute queue itself from pinned host memory (the
@@ -1584,6 +1495,10 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
     hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
+}
+void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_deblock, dim3((maxW + 63) / 64, (maxH + 63) / 64, n), dim3(256), 0, s, kps);
 }
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {

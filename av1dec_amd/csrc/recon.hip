@@ -1448,14 +1448,12 @@ extern "C" __global__ __launch_bounds__(256) void k_tb(const KParams* kps, const
 #else
 #define K_INTER_BOUNDS __launch_bounds__(64, AV1R_INTER_WAVES)
 #endif
-extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint32_t* __restrict__ tab, int n,
+DEV void inter_general(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, InterLds& L,
     unsigned long long* trace, uint32_t traceBase)
 {
-    __shared__ __align__(16) InterLds L;
     const unsigned long long tEntry = trace ? trace_now() : 0;
     const KParams* kp;
     int s;
-    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const WorkItem& wi = table_item(kps, tab, n, b, kp, s);
     const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
 #ifdef AV1R_TRACE
@@ -1472,6 +1470,12 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint
     trace_stamp(tr, 3);
     inter_tile<64, TS>(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
     trace_stamp(tr, 5);
+}
+extern "C" __global__ K_INTER_BOUNDS void k_inter(const KParams* kps, const uint32_t* __restrict__ tab, int n,
+    unsigned long long* trace, uint32_t traceBase)
+{
+    __shared__ __align__(16) InterLds L;
+    inter_general(kps, tab, n, xcd_order(blockIdx.x, gridDim.x), L, trace, traceBase);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1561,10 +1565,9 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int 
 // Frames' lists are dealt in groups of 64 / NT (a frame's last group may be partial), so
 // the parameters of a workgroup stay uniform.  tab: [group prefix (n + 1)][offsets (n)][counts (n)].
 template <int NT, int MS>
-DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, SmallLds<MS>* L)
+DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, SmallLds<MS>* L)
 {
     const int lane = threadIdx.x & 63;
-    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     const KParams& k = KP(kps, s);
@@ -1596,12 +1599,49 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
 extern "C" __global__ K_PLAIN_BOUNDS void k_inter_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ SmallLds<8> L[4];
-    inter_plain<16, 8>(kps, tab, n, L);
+    inter_plain<16, 8>(kps, tab, n, xcd_order(blockIdx.x, gridDim.x), L);
 }
 extern "C" __global__ K_PLAIN_BOUNDS void k_inter_m(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ SmallLds<16> L[2];
-    inter_plain<32, 16>(kps, tab, n, L);
+    inter_plain<32, 16>(kps, tab, n, xcd_order(blockIdx.x, gridDim.x), L);
+}
+
+// All inter tiles of a launch in ONE grid (the dataflow schedule's level 0): the general
+// tiles (k_inter: warps, OBMC, masked compounds, scaled references, larger blocks), then the
+// medium and the small plain blocks (k_inter_m / k_inter_s), as three kernels one after the
+// other left each one's tail of idle CUs before the next could start.  Every class count is
+// padded to a multiple of 8 (padding workgroups return at once), and XCD x (blockIdx % 8, as
+// the hardware deals workgroups) runs the x-th contiguous eighth of each class in class order:
+// each XCD takes its share of the long general tiles first, and a frame's tiles of one class
+// stay on one XCD's L2 (as xcd_order gives each kernel).  Placement is a speed heuristic only:
+// every logical index is run by exactly one workgroup wherever it lands.
+// tab: [k_inter table][k_inter_m table][k_inter_s table] (launch_jobs); gI / gM / gS the classes'
+// padded workgroup counts.
+extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const uint32_t* __restrict__ tab, int n,
+    uint32_t gI, uint32_t gM, uint32_t gS, unsigned long long* trace)
+{
+    union Lds {
+        InterLds g;
+        SmallLds<16> m[2];
+        SmallLds<8> s[4];
+    };
+    __shared__ __align__(16) Lds L;
+    const uint32_t x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const uint32_t qI = gI >> 3, qM = gM >> 3, qS = gS >> 3;
+    const uint32_t* tI = tab;
+    const uint32_t* tM = tI + 2 * n + 1;
+    const uint32_t* tS = tM + 3 * n + 1;
+    if (j < qI) {
+        const uint32_t b = x * qI + j;
+        if (b < tI[n]) inter_general(kps, tI, n, b, L.g, trace, ~0u);
+    } else if (j < qI + qM) {
+        const uint32_t b = x * qM + (j - qI);
+        if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m);
+    } else if (j < qI + qM + qS) {
+        const uint32_t b = x * qS + (j - qI - qM);
+        if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s);
+    }
 }
 
 #endif  // !AV1R_FLOW_PART
@@ -1975,6 +2015,11 @@ void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, u
 
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4);
 // kind 2 / 3: medium / small plain inter blocks, `items` groups of two / four
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS,
+    unsigned long long* trace, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, trace);
+}
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
 {

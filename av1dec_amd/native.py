@@ -192,7 +192,6 @@ def lib():
     l.av1r_sizeof.restype = C.c_size_t
     l.av1r_set_flow_spins.argtypes = [vp, C.c_uint32]
     l.av1r_flow_debug.argtypes = [C.POINTER(C.c_uint32), i, i, C.POINTER(i)]
-    l.av1r_set_filter_fusion.argtypes = [i]
     l.av1r_set_fast_intra.argtypes = [i]
     l.av1r_packed_data.argtypes = [vp, C.POINTER(C.c_size_t)]
     l.av1r_packed_data.restype = vp
@@ -271,7 +270,7 @@ EXPORTS = [
     "av1r_packed_bytes", "av1r_pack_last_error", "av1r_decode_packed_batch", "av1r_busy", "av1r_pack_profile",
     "av1r_pipeline_run", "av1r_pipeline_open", "av1r_pipeline_step", "av1r_pipeline_launched",
     "av1r_pipeline_close", "av1r_cycle_next", "av1r_ivf_source_create", "av1r_ivf_source_destroy",
-    "av1r_set_filter_fusion", "av1r_set_fast_intra", "av1r_packed_data",
+    "av1r_set_fast_intra", "av1r_packed_data",
     "av1r_get_output_async", "av1r_output_query", "av1r_output_start", "av1r_output_wait", "av1r_set_output_prefetch", "av1r_pipeline_set_output",
     "av1r_ring_sink_create", "av1r_ring_sink_destroy", "av1r_ring_sink_delivered", "av1r_ring_sink_frame",
     "av1r_frame_layout",

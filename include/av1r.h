@@ -338,11 +338,6 @@ const char* av1r_last_error(av1r_ctx* ctx);
  * from different streams; -1 in a normal build. */
 int av1r_set_flow_spins(av1r_ctx* ctx, uint32_t spins);
 int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream);
-/* Process-wide: 1 = the in-loop filters of frames launched from now on run fused (k_post:
- * deblocking -> CDEF -> loop restoration per 64-row stripe tile in LDS, straight into the
- * output frame; not for frames whose stage snapshots are kept), 0 = the three stage kernels
- * (default; environment AV1R_FUSED).  Both are bit-exact.  Returns the previous value. */
-int av1r_set_filter_fusion(int on);
 /* Process-wide: 1 = small intra transform blocks of the dataflow kernels take the lean path
  * (default; environment AV1R_FI), 0 = the generic one.  Both are bit-exact (A/B).  Returns
  * the previous value. */

@@ -50,23 +50,6 @@ def test_gpu_matches_reference(stream):
     assert got == out_md5 == BITS[stream]
 
 
-@pytest.fixture
-def fused_filters(native_lib):
-    prev = native_lib.av1r_set_filter_fusion(1)
-    yield
-    native_lib.av1r_set_filter_fusion(prev)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("stream", STREAMS)
-def test_gpu_fused_filters_match_reference(stream, fused_filters):
-    # the filters fused (k_post: deblocking -> CDEF -> loop restoration per stripe tile in
-    # LDS; frames without stage snapshots): the whole output equals the reference's MD5, on
-    # every stream (the stage kernels' store paths are shared with k_post)
-    bad, got, out_md5 = run_stream(stream, check_stages=False)
-    assert got == out_md5 == BITS[stream]
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream", STREAMS)
 def test_gpu_level_schedule_matches_reference(stream):

@@ -83,20 +83,6 @@ def test_gpu_synth_4k_tiles():
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("w,h,tiles,seed", [(1920, 1080, (1, 1), 0x5EED0001), (3840, 2160, (4, 2), 0x5EED0002),
-                                            (424, 232, (1, 1), 77)])
-def test_gpu_synth_fused_filters(native_lib, w, h, tiles, seed):
-    """The filters fused (k_post, av1r_set_filter_fusion) at 1080p, 4K 4x2 tiles and an odd
-    size: every output bit-exact with the oracle."""
-    prev = native_lib.av1r_set_filter_fusion(1)
-    try:
-        assert compare_gpu_oracle(pysynth.stream(w, h, 3, seed, tiles=tiles), stages=False) == 3
-    finally:
-        native_lib.av1r_set_filter_fusion(prev)
-
-
-@pytest.mark.gpu
 def test_gpu_prepared_path_matches_streaming():
     frames = pysynth.stream(640, 360, 5, 9)
     d1 = Decoder(0)
