@@ -93,6 +93,9 @@ static_assert(sizeof(WorkItem) == 32, "WorkItem layout");
 struct KParams {
     const av1r_frame_hdr* hdr;
     const av1r_mi* mi;
+    // deblocking edge codes (k_lfcode -> k_lf / k_deblock): per pass, a byte per 4x4 unit in
+    // k_lf's unit order (luma row-major, then U, then V): level | filter size << 6, 0 = none
+    uint8_t* lfc;
     const av1r_block* blocks;
     const av1r_tb* tbs;
     const uint32_t* coefs;

@@ -35,6 +35,7 @@ void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t
     unsigned long long* trace, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
 void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
+void launch_k_lfcode(const KParams* kps, int n, int maxUnits, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
@@ -218,6 +219,11 @@ struct av1r_ctx {
     // dependency nodes (CSR); then, in item order, the dependencies' item positions
     std::vector<uint32_t> nodeDepStart;
     std::vector<int32_t> nodeDeps, nodeOfTb, nodeOfBlk, nodePos;
+    // critical-path order (flow-only frames, build_schedule): per node its level and the
+    // producers of the edge units it reads through granules (not in nodeDeps), as CSR; the
+    // height (longest chain of consumers below a node)
+    std::vector<int32_t> nodeLvl, edgeDeps, nodeHeight;
+    std::vector<uint32_t> edgeStart;
     std::vector<uint32_t> deps;
     bool flowOk = false;
     bool levelsOk = true;  // the level schedule was built too (not a flow-only schedule)
@@ -736,6 +742,13 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     uint32_t nm[12] = {};  // mask words of the node being built
     c->nodeDepStart.assign(1, 0);
     c->nodeDeps.clear();
+    c->nodeLvl.clear();
+    c->edgeDeps.clear();
+    c->edgeStart.assign(1, 0);
+    // critical-path order (below): how far each item moves toward its latest level, in percent
+    // of its slack (AV1R_ALAP; 0 = the plain level order)
+    static const int alapPct = getenv("AV1R_ALAP") ? std::max(0, std::min(100, atoi(getenv("AV1R_ALAP")))) : 50;
+    const bool alap = alapPct > 0 && flowOnly;
     c->nodeOfTb.assign(b->n_tbs, -1);
     c->nodeOfBlk.assign(b->n_blocks, -1);
     std::vector<int32_t> dl;  // dependencies of the node being built
@@ -770,6 +783,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 const av1r_ctx::MapUnit& mu = c->umap[p][i];
                 if (mu.owner < 0) continue;
                 *mw |= 1u << (u - u0);
+                if (alap) c->edgeDeps.push_back(mu.owner);
                 if (!(mu.emit & (horiz ? 1 : 2))) {
                     if (c->granOk && getenv("AV1R_GRAN_DEBUG"))
                         fprintf(stderr, "no granule: plane %d unit %d,%d %s (consumer %d,%d %dx%d)\n", p, ux, uy, horiz ? "h" : "v", x, y, w, h);
@@ -788,6 +802,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             if (mu.owner >= 0) {
                 m[1] = (mu.emit & 1) ? 1u : 3u;
                 if (!mu.emit) c->granOk = false;
+                if (alap) c->edgeDeps.push_back(mu.owner);
             }
         }
     };
@@ -818,6 +833,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         memcpy(c->nodeMask.data() + nmo, nm, sizeof(nm));
         memset(nm, 0, sizeof(nm));
         c->nodeDepStart.push_back((uint32_t)c->nodeDeps.size());
+        c->edgeStart.push_back((uint32_t)c->edgeDeps.size());
         return (int32_t)c->nodeDepStart.size() - 2;
     };
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
@@ -878,6 +894,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             if (mu.owner < 0) return;
             *word |= 1u << bit;
             if (!(mu.emit & need)) c->granOk = false;
+            if (alap) c->edgeDeps.push_back(mu.owner);
         };
         if (hA && (need & 1)) {
             const int u0 = x >> 2, u1 = (x + (hAR ? 2 * w : w) - 1) >> 2, uy = (y - 1) >> 2;
@@ -897,6 +914,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 if (mu.owner >= 0) {
                     mw[1] = (mu.emit & 1) ? 1u : 3u;
                     if (!mu.emit) c->granOk = false;
+                    if (alap) c->edgeDeps.push_back(mu.owner);
                 }
             }
         }
@@ -942,6 +960,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 blkLevel = dep + 1;
                 push(c->lvB, blkLevel, AV1R_ITEM(AV1R_ITEM_II, bi));
                 iiNode = c->nodeOfBlk[bi] = end_node();
+                c->nodeLvl.push_back(blkLevel);
             }
             globalMax = std::max(globalMax, blkLevel);
             // (flowOnly: a plain inter block is level 0 and owns nothing -- the maps' initial
@@ -998,6 +1017,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             push(c->lvT, lv, AV1R_ITEM(AV1R_ITEM_TB, ti));
             globalMax = std::max(globalMax, lv);
             const int32_t node = c->nodeOfTb[ti] = end_node();
+            c->nodeLvl.push_back(lv);
             // an inter TB's pixels are final before k_flow (k_inter + k_resid) unless the
             // block is inter-intra, whose blend item adds the residuals
             if (!inter && g_packFused) {
@@ -1013,6 +1033,43 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     if (c->granOk != (granEnv && allowGran)) {  // a unit without its granule: dependency flags throughout
         build_schedule(c, b, false, flowOnly);
         return;
+    }
+    // Critical-path order (flow-only frames; AV1R_ALAP=0: off).  k_flow hands its groups out
+    // in level order, so an item of a long chain waits in the queue behind every item of the
+    // levels before it, and the chain's tail runs alone after the bulk (a batched inter step:
+    // levels 10-46 all released ~185 us into a 256 us launch, then one hop after another).
+    // Each item moves toward the LATEST level it can have without lengthening the schedule,
+    // L - height (height = the longest chain of consumers below it, through nodeDeps and the
+    // edge producers recorded above; L = max(level + height)): to level + a * slack, slack =
+    // L - height - level, a = AV1R_ALAP / 100.  For a producer P of C, level(C) >= level(P) + 1
+    // and L - height(C) >= L - height(P) + 1, so every such mix keeps C after P: the order stays
+    // topological (k_flow's progress argument holds).  The items on the chains keep their level
+    // (no slack) while those nothing waits for (height 0) move back, behind the chains' heads.
+    if (alap && !c->nodeLvl.empty()) {
+        const size_t nn = c->nodeLvl.size();
+        c->nodeHeight.assign(nn, 0);
+        int32_t* ht = c->nodeHeight.data();
+        for (size_t n = nn; n-- > 0;) {  // decode order is topological: consumers after producers
+            const int32_t hn = ht[n] + 1;
+            for (uint32_t d = c->nodeDepStart[n]; d < c->nodeDepStart[n + 1]; d++) ht[c->nodeDeps[d]] = std::max(ht[c->nodeDeps[d]], hn);
+            for (uint32_t d = c->edgeStart[n]; d < c->edgeStart[n + 1]; d++) ht[c->edgeDeps[d]] = std::max(ht[c->edgeDeps[d]], hn);
+        }
+        int L = 0;
+        for (size_t n = 0; n < nn; n++) L = std::max(L, c->nodeLvl[n] + ht[n]);
+        for (size_t n = 0; n < nn; n++) ht[n] = c->nodeLvl[n] + (L - ht[n] - c->nodeLvl[n]) * alapPct / 100;  // (the new level)
+        auto relevel = [&](std::vector<std::vector<uint32_t>>& v, bool ii) {
+            std::vector<std::vector<uint32_t>> out(std::max<size_t>(v.size(), (size_t)L + 1));
+            for (auto& lvList : v)
+                for (uint32_t code : lvList) {
+                    const uint32_t idx = AV1R_ITEM_INDEX(code);
+                    const int32_t node = ii ? c->nodeOfBlk[idx] : c->nodeOfTb[idx];
+                    out[node >= 0 ? ht[node] : 0].push_back(code);
+                }
+            v.swap(out);
+        };
+        relevel(c->lvB, true);
+        relevel(c->lvT, false);
+        globalMax = std::max(globalMax, L);
     }
     const size_t nl = (size_t)(globalMax + 1);
     clk.lap(PP_SCHED_BLOCKS);
@@ -1157,6 +1214,9 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         if (c->granOk) {  // the mask words precede the list: 12 for a blend, 4 for a TB
             const uint32_t* m = &c->nodeMask[(size_t)node * 12];
             c->deps.insert(c->deps.end(), m, m + (AV1R_ITEM_KIND(code) == AV1R_ITEM_II ? 12 : 4));
+            // a TB's fourth word (no edge run uses it): its residual tile's offset, so that
+            // k_flow fetches the residual with the masks' scalar load instead of through tb_res
+            if (AV1R_ITEM_KIND(code) == AV1R_ITEM_TB) c->deps.back() = w.coef_cnt ? c->tbRes[idx] : ~0u;
         }
         w.dep_off = (uint32_t)c->deps.size();
         w.dep_cnt = (uint16_t)(d1 - d0);
@@ -1181,6 +1241,8 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const av1r_frame_hdr* h = b->hdr;
     const size_t szHdr = align256(sizeof(av1r_frame_hdr));
     const size_t szMi = align256(sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc);
+    // the deblocking edge codes (k_lfcode): a byte per (pass, plane, 4x4 unit), device-filled
+    const size_t szLfc = align256(2 * ((size_t)h->mi_rows * h->mi_cols + 2 * (size_t)((h->mi_rows + 1) / 2) * ((h->mi_cols + 1) / 2)));
     const size_t szBlk = align256(sizeof(av1r_block) * (size_t)b->n_blocks);
     const size_t szTb = align256(sizeof(av1r_tb) * (size_t)b->n_tbs);
     const size_t szCoef = align256(4 * (size_t)b->n_coefs);
@@ -1194,7 +1256,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi;
+    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi + szLfc;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
@@ -1234,6 +1296,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
     P.upBytes = off;  // everything up to here travels; the grid below is filled on the device
     k.mi = (const av1r_mi*)put(nullptr, 0, szMi);
+    k.lfc = (uint8_t*)put(nullptr, 0, szLfc);
     P.flowOk = c->flowOk;
     k.gran = c->flowOk && c->granOk;
     for (int p = 0; p < 3; p++) {
@@ -1306,7 +1369,7 @@ static int job_begin(FrameJob& j)
         auto rb = [&](auto& ptr) {
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
-        rb(j.k.hdr), rb(j.k.mi), rb(j.k.blocks), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
+        rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
         rb(j.k.lr), rb(j.k.items), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
     }
     for (int s = 0; s < 8; s++)
@@ -1777,6 +1840,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // deblocking (LoopFilter::filter, LoopFilter.cpp:40-58): both passes in one launch, tile by
     // tile in LDS into the deblocked frame (k_deblock), or in place, one launch per pass (k_lf;
     // AV1R_DEBLOCK_TILE=0)
+    launch_k_lfcode(dk, n, maxUnits, st);
     if (deblock_tile()) launch_k_deblock(dk, n, maxW, maxH, st);
     else {
         launch_k_lf(dk, n, 0, maxUnits, st);

@@ -359,6 +359,56 @@ DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge&
                 __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u));
 }
 
+// an edge decision as one byte: the level (1..63) and the filter size (4 / 8 / 16 as 0 / 1 / 2
+// in bits 6..7); 0 = no filter
+DEV uint32_t lf_code(const KParams& k, int plane, int pass, int xP, int yP)
+{
+    LfEdge e;
+    const int lvl = lf_edge_level(k, plane, pass, xP, yP, e);
+    if (lvl <= 0) return 0;
+    return (uint32_t)lvl | ((e.filterSize == 4 ? 0u : e.filterSize == 8 ? 1u : 2u) << 6);
+}
+DEV LfEdge lf_decode(const av1r_frame_hdr& hd, uint32_t code)
+{
+    LfEdge e;
+    e.filterSize = 4 << (code >> 6);
+    lf_limits(hd, (int)(code & 63), e);
+    return e;
+}
+
+// k_lfcode: every edge decision of both passes, one lane per (plane, 4x4 unit), into k.lfc
+// (LoopFilter::loop_filter_edge's tests and the level / limit derivation, LoopFilter.cpp:85-126,
+// 301-359): the mode-info walk once per unit and pass, ahead of the filters.
+extern "C" __global__ __launch_bounds__(256) void k_lfcode(const KParams* kps)
+{
+    const uint3 wg = xcd_block();
+    const KParams& k = KP(kps, wg.y);
+    const av1r_frame_hdr& hd = *k.hdr;
+    if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped (k_lf / k_deblock test it)
+    const int nY = k.mi_rows * k.mi_cols;
+    const int cCols = (k.mi_cols + 1) / 2, nC = ((k.mi_rows + 1) / 2) * cCols;
+    const int id = wg.x * blockDim.x + threadIdx.x;
+    int plane, row0, col0;
+    if (id < nY) {
+        plane = 0;
+        row0 = id / k.mi_cols;
+        col0 = id - row0 * k.mi_cols;
+    } else if (id < nY + 2 * nC) {
+        int u = id - nY;
+        plane = 1 + (u >= nC);
+        if (u >= nC) u -= nC;
+        const int r = u / cCols;
+        row0 = r * 2;
+        col0 = (u - r * cCols) * 2;
+    } else {
+        return;
+    }
+    const int sub = plane ? 1 : 0;
+    const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
+    k.lfc[id] = (uint8_t)lf_code(k, plane, 0, xP, yP);
+    k.lfc[nY + 2 * nC + id] = (uint8_t)lf_code(k, plane, 1, xP, yP);
+}
+
 // one lane per (plane, 4x4 unit) edge of pass `pass`
 DEV void lf_body(const KParams* kps, int pass)
 {
@@ -386,10 +436,11 @@ DEV void lf_body(const KParams* kps, int pass)
     }
     const int sub = plane ? 1 : 0;
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
-    LfEdge e;
-    if (!lf_edge(k, plane, pass, xP, yP, e)) return;
+    // the edge's decision, taken by k_lfcode (one coalesced byte instead of the mode-info walk)
+    const uint32_t code = k.lfc[(size_t)pass * (nY + 2 * nC) + id];
+    if (!code) return;
     const DevPlane& P = k.cur.pl[plane];
-    lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
+    lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, lf_decode(hd, code));
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
@@ -423,22 +474,6 @@ struct DbLds {
     uint8_t c0c[2][12 * 9];   // pass 0 chroma: unit row u (cy0 - 8 + 4u), edge e (cx0 + 4e)
     uint8_t c1c[2][9 * 8];    // pass 1 chroma: edge e (cy0 + 4e), unit column u (cx0 + 4u)
 };
-// an edge decision as one byte: the level (1..63) and the filter size (4 / 8 / 16 as 0 / 1 / 2
-// in bits 6..7); 0 = no filter
-DEV uint32_t lf_code(const KParams& k, int plane, int pass, int xP, int yP)
-{
-    LfEdge e;
-    const int lvl = lf_edge_level(k, plane, pass, xP, yP, e);
-    if (lvl <= 0) return 0;
-    return (uint32_t)lvl | ((e.filterSize == 4 ? 0u : e.filterSize == 8 ? 1u : 2u) << 6);
-}
-DEV LfEdge lf_decode(const av1r_frame_hdr& hd, uint32_t code)
-{
-    LfEdge e;
-    e.filterSize = 4 << (code >> 6);
-    lf_limits(hd, (int)(code & 63), e);
-    return e;
-}
 extern "C" __global__ __launch_bounds__(256) void k_deblock(const KParams* kps)
 {
     __shared__ __align__(16) DbLds L;
@@ -471,28 +506,33 @@ extern "C" __global__ __launch_bounds__(256) void k_deblock(const KParams* kps)
         vc[u] = q < 2 * NC && y >= 0 && x >= 0 && y < (limY >> 1) + 8 && x < (limX >> 1) + 8
                     ? *reinterpret_cast<const uint32_t*>(P.p + (size_t)y * P.stride + x) : 0u;
     }
-    // ---- the edge decisions of both passes (mode info only; their loads overlap the above)
+    // ---- the edge decisions of both passes (k_lfcode's bytes; their loads go out with the
+    // pixels')
     const bool on = hd.lf_level[0] || hd.lf_level[1];  // else LoopFilter::filter is skipped: a copy
+    const int nY = k.mi_rows * k.mi_cols, cCols = (k.mi_cols + 1) / 2, cRows = (k.mi_rows + 1) / 2;
+    const int nU = nY + 2 * cRows * cCols;
+    // the code of the unit at plane position (xP, yP) for `pass` (0 outside the mi grid)
+    auto code_at = [&](int plane, int pass, int xP, int yP) -> uint32_t {
+        const int col = xP >> 2, row = yP >> 2;
+        if (!on || xP < 0 || yP < 0) return 0u;
+        if (!plane) return row < k.mi_rows && col < k.mi_cols ? k.lfc[(size_t)pass * nU + row * k.mi_cols + col] : 0u;
+        return row < cRows && col < cCols ? k.lfc[(size_t)pass * nU + nY + (plane - 1) * cRows * cCols + row * cCols + col] : 0u;
+    };
     for (int q = t; q < 20 * 17 + 17 * 16 + 2 * (12 * 9 + 9 * 8); q += 256) {
-        uint32_t c = 0;
         if (q < 340) {
             const int u = q / 17, e = q - u * 17;
-            if (on) c = lf_code(k, 0, 0, x0 + 4 * e, y0 - 8 + 4 * u);
-            L.c0y[q] = (uint8_t)c;
+            L.c0y[q] = (uint8_t)code_at(0, 0, x0 + 4 * e, y0 - 8 + 4 * u);
         } else if (q < 340 + 272) {
             const int r = q - 340, e = r >> 4, u = r & 15;
-            if (on) c = lf_code(k, 0, 1, x0 + 4 * u, y0 + 4 * e);
-            L.c1y[r] = (uint8_t)c;
+            L.c1y[r] = (uint8_t)code_at(0, 1, x0 + 4 * u, y0 + 4 * e);
         } else {
             const int r = q - 612, pl = r >= 180, r2 = r - 180 * pl;
             if (r2 < 108) {
                 const int u = r2 / 9, e = r2 - u * 9;
-                if (on) c = lf_code(k, 1 + pl, 0, cx0 + 4 * e, cy0 - 8 + 4 * u);
-                L.c0c[pl][r2] = (uint8_t)c;
+                L.c0c[pl][r2] = (uint8_t)code_at(1 + pl, 0, cx0 + 4 * e, cy0 - 8 + 4 * u);
             } else {
                 const int r3 = r2 - 108, e = r3 >> 3, u = r3 & 7;
-                if (on) c = lf_code(k, 1 + pl, 1, cx0 + 4 * u, cy0 + 4 * e);
-                L.c1c[pl][r3] = (uint8_t)c;
+                L.c1c[pl][r3] = (uint8_t)code_at(1 + pl, 1, cx0 + 4 * u, cy0 + 4 * e);
             }
         }
     }
@@ -1495,6 +1535,10 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
     hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
+}
+void launch_k_lfcode(const KParams* kps, int n, int maxUnits, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_lfcode, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps);
 }
 void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {

@@ -272,12 +272,12 @@ struct ResQuads {
     static constexpr int N = (MAX * MAX / 4 + NT - 1) / NT;
     uint2 r[N];
 };
+// ro: the TB's residual tile offset (KParams::tb_res; ~0u: none), known to the caller
 template <int NT, int MAX>
-DEV void res_prefetch(const KParams& k, const WorkItem& tb, ResQuads<NT, MAX>& R)
+DEV void res_prefetch(const KParams& k, const WorkItem& tb, uint32_t ro, ResQuads<NT, MAX>& R)
 {
     const int t = coop_lane<NT>();
     const int nq = (ctab<NT>(av1r_tx_w, tb.tx_size) * ctab<NT>(av1r_tx_h, tb.tx_size)) >> 2;
-    const uint32_t ro = tb.coef_cnt ? (NT >= 64 ? sload(k.tb_res + AV1R_ITEM_INDEX(tb.code)) : k.tb_res[AV1R_ITEM_INDEX(tb.code)]) : ~0u;
     const uint2* q4 = reinterpret_cast<const uint2*>(k.res + ro);
 #pragma unroll
     for (int u = 0; u < ResQuads<NT, MAX>::N; u++) {
@@ -1760,10 +1760,13 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     // &G or null made G a 64 B/lane stack object -- scratch traffic on every item)
     const bool gran = k.gran;
     GranEdges G = {};
+    uint32_t resOff = ~0u;  // a TB's residual tile: the fourth mask word (granules), else tb_res
     if (gran) {
         const int p = AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 0 : wi.plane;
         G.mask = k.deps + wi.dep_off - (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II ? 12 : 4);
-        G.mA = sload(G.mask), G.mC = sload(G.mask + 1), G.mL = sload(G.mask + 2);
+        const uint4 m4 = sload(reinterpret_cast<const uint4*>(G.mask));
+        G.mA = m4.x, G.mC = m4.y, G.mL = m4.z;
+        resOff = m4.w;
         G.h = k.gran_h[p];
         G.v = k.gran_v[p];
         G.gw = k.gran_w[p];
@@ -1784,7 +1787,8 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     } else {
         // intra / palette TB: its residual tile (k_resid) is fetched before the wait
         ResQuads<NT, MAX> R;
-        res_prefetch<NT, MAX>(k, wi, R);
+        if (!gran) resOff = wi.coef_cnt ? sload(k.tb_res + AV1R_ITEM_INDEX(wi.code)) : ~0u;
+        res_prefetch<NT, MAX>(k, wi, resOff, R);
         const av1r_block blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
         const int edgeFilter = sfield(&k.hdr->enable_intra_edge_filter);
         bool lean = false;
