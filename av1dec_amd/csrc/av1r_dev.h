@@ -155,6 +155,7 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_ERR (FLOW_QUEUES * FLOW_LINE)
 #define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the launch's pinned host error word
 #define FLOW_SPINLIM (FLOW_ERR + 4)  // polls before a wait gives up (0: FLOW_SPINS)
+#define FLOW_FLAGS (FLOW_ERR + 5)    // bit 0: take the next ticket before running a group
 #define FLOW_ASSIGN (FLOW_ERR + FLOW_LINE)  // workgroup entries: entry k serves queue k % FLOW_QUEUES
 #define FLOW_CTL_BYTES (4 * (FLOW_ASSIGN + FLOW_LINE))
 // k_flow spin bound, in polls of running waves (each a global load round trip, ~0.5-2 us),

@@ -1650,6 +1650,10 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         uint32_t* hctl = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes);
         *reinterpret_cast<uint32_t**>(hctl + FLOW_HOSTERR) = rec ? rec->err : nullptr;
         hctl[FLOW_SPINLIM] = lc->flowSpins;
+        // AV1R_TICKET_PF=1: a workgroup takes its next group's ticket as it starts a group, so
+        // the atomic's round trip overlaps the group's work (recon.hip, k_flow)
+        static const uint32_t ticketPf = getenv("AV1R_TICKET_PF") ? (uint32_t)atoi(getenv("AV1R_TICKET_PF")) : 0u;
+        hctl[FLOW_FLAGS] = ticketPf ? 1u : 0u;
         uint32_t* g = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES);
         for (size_t l = 0; l < nLevels; l++)
             for (int i = 0; i < n; i++) {

@@ -1867,6 +1867,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     __syncthreads();
     const uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
     uint32_t* head = ctl + q * FLOW_LINE;
+    const bool pf = (sload(ctl + FLOW_FLAGS) & 1u) != 0;
     if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     for (uint32_t it = 0;; it ^= 1) {
@@ -1877,13 +1878,13 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 #endif
             return;
         }
-        // AV1R_TICKET_PREFETCH: take the next ticket before running this group (holding it
-        // early keeps the progress argument: a held group waits only for earlier ones);
-        // measured no faster, so off
+        // pf (FLOW_FLAGS bit 0, the host's AV1R_TICKET_PF): take the next ticket before running
+        // this group, its round trip hidden behind the group's work.  Progress holds: the
+        // earliest unfinished group cannot be a held "next" one (its holder's current group is
+        // earlier and unfinished), so it is some workgroup's current group, whose inputs are
+        // complete.
         uint32_t next = 0;
-#ifdef AV1R_TICKET_PREFETCH
-        if (threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+        if (pf && threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint2 gd = groups[g];
         const KParams& k = KP(kps, gd.x >> 8);
         const uint32_t n = gd.x & 0xff;
@@ -1895,9 +1896,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
                 flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
                     gd.x >> 8);
         }
-#ifndef AV1R_TICKET_PREFETCH
-        if (threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+        if (!pf && threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (threadIdx.x == 0) ticket[it ^ 1] = next;
         __syncthreads();  // the LDS tiles are free again; the next ticket is published
     }
