@@ -743,12 +743,14 @@ DEV uint32_t cdef_quad(const uint8_t* t, int p, const int16_t* off, int pri, int
                 const short w = s == 0 ? (kk ? tap1 : tap0) : (kk ? 1 : 2);  // Cdef_Sec_Taps = {2, 1}
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
+                    // constrain (Cdef.cpp:111-118): sign(d) * min(|d|, max(0, thr - (|d| >> adj))),
+                    // i.e. d clamped to [-v, v] with v = max(0, thr - (|d| >> adj)) (v <= |d| is
+                    // not needed: the clamp leaves a smaller |d| as it is); 0 for thr 0
                     const cd2 d = q[h] - x[h];
                     const cd2 ad = __builtin_elementwise_max(d, -d);
-                    cd2 v = __builtin_elementwise_min(ad, __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0}));
-                    const cd2 neg = d >> cd2{15, 15};
-                    v = (v ^ neg) - neg;  // constrain (0 for thr 0)
-                    sum[h] += cd2{w, w} * v;
+                    const cd2 v = __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0});
+                    const cd2 c = __builtin_elementwise_min(__builtin_elementwise_max(d, -v), v);
+                    sum[h] += cd2{w, w} * c;
                     mx[h] = __builtin_elementwise_max(q[h], mx[h]);
                     mn[h] = __builtin_elementwise_min(q[h], mn[h]);
                 }
