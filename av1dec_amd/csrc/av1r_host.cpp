@@ -1251,12 +1251,12 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
     const size_t szItems = align256(sizeof(WorkItem) * c->items.size() + 4);
     const size_t szDeps = align256(4 * c->deps.size() + 4);
-    const size_t szDone = align256(4 * c->items.size() + 4);  // zeroed: no launch's epoch
+    const size_t szDone = align256(4 * c->items.size() + 4);  // zeroed on the device (k_mi_zero): no launch's epoch
     const size_t szTbRes = align256(4 * c->tbRes.size() + 4);
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szDone + szTbRes + szResS + szResL + szMi + szLfc;
+    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
@@ -1289,12 +1289,12 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
     P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
     k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);
-    memset(host + off, 0, szDone);
-    k.done = (uint32_t*)put(nullptr, 0, szDone);
     k.tb_res = (const uint32_t*)put(c->tbRes.data(), 4 * c->tbRes.size(), szTbRes);
     k.resid_s = (const uint32_t*)put(c->residS.data(), 4 * c->residS.size(), szResS);
     k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
-    P.upBytes = off;  // everything up to here travels; the grid below is filled on the device
+    P.upBytes = off;  // everything up to here travels; what follows is filled on the device
+    k.done = (uint32_t*)put(nullptr, 0, szDone);
+    k.n_items = (uint32_t)c->items.size();
     k.mi = (const av1r_mi*)put(nullptr, 0, szMi);
     k.lfc = (uint8_t*)put(nullptr, 0, szLfc);
     P.flowOk = c->flowOk;
@@ -1719,7 +1719,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     {  // the frames' mode-info grids, derived on the device from their blocks and TBs
         uint32_t maxUnits = 0, maxBlocks = 0, maxTbs = 0;
         for (auto& j : jobs) {
-            maxUnits = std::max(maxUnits, (uint32_t)(j.k.mi_stride * j.k.mi_rows_alloc));
+            maxUnits = std::max({maxUnits, (uint32_t)(j.k.mi_stride * j.k.mi_rows_alloc), j.k.n_items});
             maxBlocks = std::max(maxBlocks, j.k.n_blocks);
             maxTbs = std::max(maxTbs, j.k.n_tbs);
         }
