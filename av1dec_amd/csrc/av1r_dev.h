@@ -102,7 +102,8 @@ struct KParams {
     const uint8_t* palette;
     const int8_t* cdef_idx;
     const av1r_lr_unit* lr;
-    const WorkItem* items;  // this frame's level-ordered work items
+    const WorkItem* items;  // this frame's level-ordered work items (transform blocks, inter-intra blends)
+    const uint32_t* tiles;  // its inter tiles, level-ordered: AV1R_ITEM(AV1R_ITEM_INTER, block << 4 | row << 2 | col)
     const uint32_t* deps;   // k_flow: dependency lists (positions in items)
     uint32_t* done;         // k_flow: per item, the epoch of the launch that completed it
     // k_flow mode: residuals precomputed by k_resid.  tb_res[tb]: the TB's residual tile

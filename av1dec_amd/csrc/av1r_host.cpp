@@ -212,7 +212,8 @@ struct av1r_ctx {
     std::vector<MapUnit> umap[3];
     int mapW[3] = {}, mapH[3] = {};
     std::vector<std::vector<uint32_t>> lvP, lvB, lvT;  // inter tiles, inter-intra blends, TBs per level
-    std::vector<WorkItem> items;
+    std::vector<WorkItem> items;  // transform blocks and inter-intra blends
+    std::vector<uint32_t> tiles;  // inter tiles (codes): Level::off[0] indexes them
     std::vector<Level> levels;
     // k_flow dependencies: per 4x4 unit the node (TB / inter-intra item, decode order) that
     // last wrote it (-1: nothing, or an inter tile of the preceding launch); per node its
@@ -1076,10 +1077,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     for (auto* v : {&c->lvP, &c->lvB, &c->lvT})
         if (v->size() < nl) v->resize(nl);
     c->items.clear();
+    c->tiles.clear();
     c->levels.assign(nl, Level());
-    size_t nItems = 0;
-    for (size_t l = 0; l < nl; l++) nItems += c->lvP[l].size() + c->lvB[l].size() + c->lvT[l].size();
+    size_t nItems = 0, nTiles = 0;
+    for (size_t l = 0; l < nl; l++) nItems += c->lvB[l].size() + c->lvT[l].size(), nTiles += c->lvP[l].size();
     c->items.reserve(nItems);
+    c->tiles.reserve(nTiles);
     // stable partition of a level's list by a small class key (counting sort, one pass)
     std::vector<uint32_t> bk[4];
     auto partition = [&](std::vector<uint32_t>& v, int nk, uint32_t* counts, auto key) {
@@ -1126,23 +1129,23 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         std::vector<uint32_t>& T = c->lvT[l];
         partition(T, 4, tc, tbClass);
         const uint32_t nLargeT = tc[0] + tc[1], nLargeIntra = tc[0], nSmallIntra = tc[2];
-        c->levels[l].off[0] = (uint32_t)c->items.size();
+        c->levels[l].off[0] = (uint32_t)c->tiles.size();
         c->levels[l].cnt[0] = (uint32_t)c->lvP[l].size();
-        c->levels[l].off[1] = c->levels[l].off[0] + c->levels[l].cnt[0];
+        c->tiles.insert(c->tiles.end(), c->lvP[l].begin(), c->lvP[l].end());
+        c->levels[l].off[1] = (uint32_t)c->items.size();
         c->levels[l].cnt[1] = (uint32_t)c->lvB[l].size() + nLargeT;
         c->levels[l].off[2] = c->levels[l].off[1] + c->levels[l].cnt[1];
         c->levels[l].cnt[2] = (uint32_t)T.size() - nLargeT;
         c->levels[l].fcnt[0] = 0;
         c->levels[l].fcnt[1] = (uint32_t)c->lvB[l].size() + nLargeIntra;
         c->levels[l].fcnt[2] = nSmallIntra;
-        for (auto* v : {&c->lvP, &c->lvB, &c->lvT}) {
+        for (auto* v : {&c->lvB, &c->lvT}) {
             for (uint32_t code : (*v)[l]) {
                 WorkItem w;
                 memset(&w, 0, sizeof(w));
                 w.code = code;
                 const uint32_t idx = AV1R_ITEM_INDEX(code);
                 switch (AV1R_ITEM_KIND(code)) {
-                case AV1R_ITEM_INTER: w.block = idx >> 4; break;
                 case AV1R_ITEM_II: w.block = idx; break;
                 default: {
                     const av1r_tb& t = b->tbs[idx];
@@ -1250,13 +1253,14 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szCdef = align256((size_t)h->cdef_rows * h->cdef_cols);
     const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
     const size_t szItems = align256(sizeof(WorkItem) * c->items.size() + 4);
+    const size_t szTiles = align256(4 * c->tiles.size() + 4);
     const size_t szDeps = align256(4 * c->deps.size() + 4);
     const size_t szDone = align256(4 * c->items.size() + 4);  // zeroed on the device (k_mi_zero): no launch's epoch
     const size_t szTbRes = align256(4 * c->tbRes.size() + 4);
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
+    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
@@ -1288,6 +1292,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.cdef_idx = (const int8_t*)put(b->cdef_idx, (size_t)h->cdef_rows * h->cdef_cols, szCdef);
     k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
     P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
+    k.tiles = (const uint32_t*)put(c->tiles.data(), 4 * c->tiles.size(), szTiles);
     k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);
     k.tb_res = (const uint32_t*)put(c->tbRes.data(), 4 * c->tbRes.size(), szTbRes);
     k.resid_s = (const uint32_t*)put(c->residS.data(), 4 * c->residS.size(), szResS);
@@ -1370,7 +1375,7 @@ static int job_begin(FrameJob& j)
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
         rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
-        rb(j.k.lr), rb(j.k.items), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
+        rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
     }
     for (int s = 0; s < 8; s++)
         if (c->slots[s]) j.k.ref[s] = c->slots[s]->d;
@@ -1821,12 +1826,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         std::vector<unsigned long long> hv((size_t)allItems * 16);
         HIPCHK(hipMemcpyAsync(hv.data(), trace, hv.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        if (flow) {  // frame-major rows: each frame's items in its level order
+        if (flow) {  // frame-major rows: each frame's items in their level order, then its tiles
             size_t q = 0;
-            for (auto& j : jobs)
+            for (auto& j : jobs) {
                 for (size_t l = 0; l < j.P->levels.size(); l++)
-                    for (int kk = 0; kk < 3; kk++)
-                        for (uint32_t i = 0; i < j.P->levels[l].cnt[kk]; i++, q++) hv[q * 16 + 6] = l;
+                    for (uint32_t i = 0; i < j.P->levels[l].cnt[1] + j.P->levels[l].cnt[2]; i++, q++) hv[q * 16 + 6] = l;
+                for (size_t l = 0; l < j.P->levels.size(); l++)
+                    for (uint32_t i = 0; i < j.P->levels[l].cnt[0]; i++, q++) hv[q * 16 + 6] = l;
+            }
             hv.resize(q * 16);
         } else {
             size_t q = 0;

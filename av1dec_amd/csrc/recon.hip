@@ -1454,11 +1454,17 @@ DEV void inter_general(const KParams* kps, const uint32_t* __restrict__ tab, int
     const unsigned long long tEntry = trace ? trace_now() : 0;
     const KParams* kp;
     int s;
-    const WorkItem& wi = table_item(kps, tab, n, b, kp, s);
-    const uint32_t idx = AV1R_ITEM_INDEX(wi.code);
+    // the tile's code (frame of tile b: the number of frames whose tiles all precede it)
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+    s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    kp = &KP(kps, s);
+    const uint32_t pos = tab[n + 1 + s] + (b - tab[s]);
+    const uint32_t code = sload(kp->tiles + pos);
+    const uint32_t idx = AV1R_ITEM_INDEX(code);
 #ifdef AV1R_TRACE
-    // traceBase ~0u (k_flow mode): frame-major rows, this frame's base + the item position
-    const size_t row = traceBase == ~0u ? kp->trace_base + (size_t)(&wi - kp->items) : (size_t)traceBase + b;
+    // traceBase ~0u (k_flow mode): frame-major rows, this frame's base + its items + the tile position
+    const size_t row = traceBase == ~0u ? kp->trace_base + kp->n_items + pos : (size_t)traceBase + b;
     unsigned long long* tr = trace ? trace + row * AV1R_TRACE_W : nullptr;
 #else
     unsigned long long* tr = nullptr;
@@ -1466,7 +1472,7 @@ DEV void inter_general(const KParams* kps, const uint32_t* __restrict__ tab, int
     (void)traceBase;
 #endif
     trace_put(tr, 2, tEntry);
-    trace_put(tr, 0, wi.code);
+    trace_put(tr, 0, code);
     trace_stamp(tr, 3);
     inter_tile<64, TS>(*kp, idx >> 4, idx & 3, (idx >> 2) & 3, L, tr);
     trace_stamp(tr, 5);
@@ -1574,7 +1580,7 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
     const int g = threadIdx.x / NT;
     const uint32_t i = (64 / NT) * (b - tab[s]) + g;
     if (i >= tab[2 * n + 1 + s]) return;  // (wave-level ordering only: no barrier follows)
-    const av1r_block& blk = k.blocks[AV1R_ITEM_INDEX(k.items[tab[n + 1 + s] + i].code) >> 4];
+    const av1r_block& blk = k.blocks[AV1R_ITEM_INDEX(k.tiles[tab[n + 1 + s] + i]) >> 4];
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
     for (int plane = 0; plane < nPl; plane++) {
         // (sub-8x8 chroma may gather up to four units of neighbouring blocks)
