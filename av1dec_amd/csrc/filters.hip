@@ -714,6 +714,9 @@ DEV uint32_t cdef_quad(const uint8_t* t, int p, const int16_t* off, int pri, int
     int ts, int limX, int limY)
 {
     const uint32_t xw = *reinterpret_cast<const uint32_t*>(t + p);
+    // both strengths 0: every constrained difference is 0, so the clamp to the taps' range
+    // returns x itself
+    if (!pri && !sec) return xw;
     const cd2 x[2] = {cd_lo(xw), cd_hi(xw)};
     cd2 sum[2] = {cd2{0, 0}, cd2{0, 0}}, mx[2] = {x[0], x[1]}, mn[2] = {x[0], x[1]};
     const short adjP = (short)imax(0, damping - floor_log2(imax(pri, 1)));
@@ -745,12 +748,16 @@ DEV uint32_t cdef_quad(const uint8_t* t, int p, const int16_t* off, int pri, int
                 for (int h = 0; h < 2; h++) {
                     // constrain (Cdef.cpp:111-118): sign(d) * min(|d|, max(0, thr - (|d| >> adj))),
                     // i.e. d clamped to [-v, v] with v = max(0, thr - (|d| >> adj)) (v <= |d| is
-                    // not needed: the clamp leaves a smaller |d| as it is); 0 for thr 0
-                    const cd2 d = q[h] - x[h];
-                    const cd2 ad = __builtin_elementwise_max(d, -d);
-                    const cd2 v = __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0});
-                    const cd2 c = __builtin_elementwise_min(__builtin_elementwise_max(d, -v), v);
-                    sum[h] += cd2{w, w} * c;
+                    // not needed: the clamp leaves a smaller |d| as it is); 0 for thr 0, so a
+                    // tap of strength 0 only widens the range (min / max: every tap counts,
+                    // Cdef.cpp:177-190)
+                    if (thr) {
+                        const cd2 d = q[h] - x[h];
+                        const cd2 ad = __builtin_elementwise_max(d, -d);
+                        const cd2 v = __builtin_elementwise_max(cd2{thr, thr} - (ad >> cd2{adj, adj}), cd2{0, 0});
+                        const cd2 c = __builtin_elementwise_min(__builtin_elementwise_max(d, -v), v);
+                        sum[h] += cd2{w, w} * c;
+                    }
                     mx[h] = __builtin_elementwise_max(q[h], mx[h]);
                     mn[h] = __builtin_elementwise_min(q[h], mn[h]);
                 }
