@@ -1795,22 +1795,27 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         ResQuads<NT, MAX> R;
         if (!gran) resOff = wi.coef_cnt ? sload(k.tb_res + AV1R_ITEM_INDEX(wi.code)) : ~0u;
         res_prefetch<NT, MAX>(k, wi, resOff, R);
-        const av1r_block blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
-        const int edgeFilter = sfield(&k.hdr->enable_intra_edge_filter);
         bool lean = false;
         if constexpr (NT == 64 && MAX == TB_SMALL) {
-            // small intra TBs: the lean path (intra_fast.h), its parameters set up before the wait
-            if (gran && k.fi && fi_ok(wi, blk)) {
-                lean = true;
-                const FiParams F = fi_setup(k, wi, blk, edgeFilter);
-                trace_stamp(tr, 3);
-                flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
-                trace_stamp(tr, 4);
-                fi_run<MAX>(k, wi, F, L, G, R.r[0], epoch, gran);
-                trace_stamp(tr, 10);
+            // small intra TBs: the lean path (intra_fast.h), its parameters derived by k_fiprep
+            // ahead of the launch (one scalar load here, issued with the item's other loads;
+            // the block record is not needed)
+            if (gran && k.fi) {
+                const FiPacked FP = sload(reinterpret_cast<const FiPacked*>(k.fip) + pos);
+                if (FP.w[0] >> 31) {
+                    lean = true;
+                    const FiParams F = fi_unpack(FP);
+                    trace_stamp(tr, 3);
+                    flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
+                    trace_stamp(tr, 4);
+                    fi_run<MAX>(k, wi, F, L, G, R.r[0], epoch, gran);
+                    trace_stamp(tr, 10);
+                }
             }
         }
         if (!lean) {
+            const av1r_block blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
+            const int edgeFilter = sfield(&k.hdr->enable_intra_edge_filter);
             trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
             trace_stamp(tr, 4);
@@ -1906,6 +1911,35 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
         if (threadIdx.x == 0) ticket[it ^ 1] = next;
         __syncthreads();  // the LDS tiles are free again; the next ticket is published
     }
+}
+
+// k_fiprep: every small intra item's lean-path parameters (fi_setup) into k.fip, one lane per
+// item, ahead of k_flow: there they were a chain of dependent scalar loads (item -> block ->
+// tables) on every item before its dependency wait.
+extern "C" __global__ __launch_bounds__(256) void k_fiprep(const KParams* kps, const uint32_t* __restrict__ pre, int n)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    // frame of item i (a prefix table of the frames' item counts, as table_item)
+    const uint32_t p = lane + 1 < n ? pre[lane + 1] : 0xffffffffu;
+    const uint32_t b = i;
+    const int s = __popcll(__ballot(b >= p));
+    if (s >= n || i >= pre[n]) return;
+    const KParams& k = KP(kps, s);
+    const uint32_t pos = i - pre[s];
+    const WorkItem& wi = k.items[pos];
+    FiPacked P = {};
+    if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_TB && av1r_tx_w[wi.tx_size] <= TB_SMALL && av1r_tx_h[wi.tx_size] <= TB_SMALL) {
+        const av1r_block& blk = k.blocks[wi.block];
+        if (fi_ok(wi, blk)) P = fi_pack(fi_setup_v(k, wi, blk, k.hdr->enable_intra_edge_filter), true);
+    }
+    uint4* d = reinterpret_cast<uint4*>(k.fip + 8 * (size_t)pos);
+    d[0] = make_uint4(P.w[0], P.w[1], P.w[2], P.w[3]);
+    d[1] = make_uint4(P.w[4], P.w[5], P.w[6], P.w[7]);
+}
+void launch_k_fiprep(const KParams* kps, const uint32_t* pre, int n, uint32_t items, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_fiprep, dim3((items + 255) / 256), dim3(256), 0, s, kps, pre, n);
 }
 
 // persistent grid of k_flow on `device`: every CU's resident workgroups (capped at 8 per
