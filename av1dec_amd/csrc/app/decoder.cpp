@@ -40,6 +40,7 @@ int av1d_create(int device, av1d_ctx** out)
     av1d_ctx* c = new (std::nothrow) av1d_ctx;
     if (!c) return AV1R_E_NOMEM;
     int rc = av1p_create(&c->parser);
+    if (!rc) av1p_set_mode_info(c->parser, 0);  // av1r_decode_frame rebuilds it on the device
     if (!rc) rc = av1r_create(device, &c->recon);
     if (rc) {
         av1d_destroy(c);

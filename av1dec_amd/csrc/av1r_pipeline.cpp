@@ -204,6 +204,7 @@ int av1r_ivf_source_create(const uint8_t* const* files, const size_t* sizes, int
         t.size = sizes[i];
         int rc = (t.size < 32 || memcmp(t.data, "DKIF", 4)) ? AV1R_E_INVALID : av1p_create(&t.parser);
         if (!rc) t.pos = t.data[6] | t.data[7] << 8;  // header length
+        if (!rc) av1p_set_mode_info(t.parser, 0);      // av1r_pack rebuilds it on the device
         if (rc) {
             for (auto& u : S->st)
                 if (u.parser) av1p_destroy(u.parser);

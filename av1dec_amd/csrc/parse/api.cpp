@@ -43,6 +43,13 @@ int av1p_set_tile_threads(av1p_ctx* ctx, int n)
     return AV1R_OK;
 }
 
+int av1p_set_mode_info(av1p_ctx* ctx, int emit)
+{
+    if (!ctx) return AV1R_E_INVALID;
+    ctx->parser.emit_mi = emit != 0;
+    return AV1R_OK;
+}
+
 void av1p_destroy(av1p_ctx* ctx)
 {
     if (!ctx) return;

@@ -1002,9 +1002,10 @@ int Parser::finish_frame()
     Frame& F = *cur;
     // CDFs of the context_update_tile_id tile (Tile::frame_end_update_cdf)
     if (!fh.disable_frame_end_update_cdf) cdf = saved_cdf;
-    // mode-info grid (refdump.cpp fillFrameTables)
-    F.mi.resize(mi.size());  // (value-initialised: every field not set below is 0)
-    for (size_t i = 0; i < mi.size(); i++) {
+    // mode-info grid (refdump.cpp fillFrameTables); left out when the consumer rebuilds
+    // it on the device from the block records (av1p_set_mode_info(ctx, 0))
+    F.mi.resize(emit_mi ? mi.size() : 0);  // (value-initialised: every field not set below is 0)
+    for (size_t i = 0; i < F.mi.size(); i++) {
         const MiInfo& m = mi[i];
         av1r_mi& d = F.mi[i];
         for (int l = 0; l < 2; l++) {
@@ -1299,7 +1300,7 @@ void Frame::bind()
 {
     memset(&batch, 0, sizeof(batch));
     batch.hdr = &hdr;
-    batch.mi = mi.data();
+    batch.mi = mi.empty() ? nullptr : mi.data();
     batch.blocks = blocks.data();
     batch.n_blocks = (uint32_t)blocks.size();
     batch.tbs = tbs.data();

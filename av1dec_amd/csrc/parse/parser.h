@@ -484,6 +484,8 @@ public:
     // tile-parallel parsing: up to `tile_threads` threads parse the tiles of a tile group
     // (1: serial); one TileCtx per tile, kept between frames for their buffers
     int tile_threads = 1;
+    // fill the batch's per-4x4 mode-info grid (av1p_set_mode_info)
+    bool emit_mi = true;
     std::vector<TileCtx*> par_tiles;
     ~Parser();
 

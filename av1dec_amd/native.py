@@ -141,11 +141,13 @@ def parser_lib():
     l.av1p_last_error.argtypes = [vp]
     l.av1p_last_error.restype = C.c_char_p
     l.av1p_set_tile_threads.argtypes = [vp, C.c_int]
+    l.av1p_set_mode_info.argtypes = [vp, C.c_int]
     _plib = l
     return l
 
 
-PARSE_EXPORTS = ["av1p_create", "av1p_destroy", "av1p_decode_tu", "av1p_frame", "av1p_last_error", "av1p_set_tile_threads"]
+PARSE_EXPORTS = ["av1p_create", "av1p_destroy", "av1p_decode_tu", "av1p_frame", "av1p_last_error", "av1p_set_tile_threads",
+                 "av1p_set_mode_info"]
 
 
 _lib = None

@@ -40,7 +40,7 @@ def frame_from_batch(ptr):
     b = abi.FrameBatch.from_address(ptr)
     hdr = abi.FrameHdr.from_address(b.hdr)
     secs = {"hdr": _copy(b.hdr, C.sizeof(abi.FrameHdr))}
-    n_mi = 0 if hdr.show_existing_frame else hdr.mi_rows_alloc * hdr.mi_stride
+    n_mi = 0 if hdr.show_existing_frame or not b.mi else hdr.mi_rows_alloc * hdr.mi_stride
     secs["mi"] = _copy(b.mi, n_mi * abi.SIZEOF_MI)
     secs["blocks"] = _copy(b.blocks, b.n_blocks * abi.SIZEOF_BLOCK)
     secs["tbs"] = _copy(b.tbs, b.n_tbs * abi.SIZEOF_TB)
@@ -61,7 +61,7 @@ class ParseError(RuntimeError):
 class Parser:
     """One parsing context (one stream).  Not thread-safe; use one per thread."""
 
-    def __init__(self, tile_threads=None):
+    def __init__(self, tile_threads=None, mode_info=True):
         self._l = native.parser_lib()
         h = C.c_void_p()
         rc = self._l.av1p_create(C.byref(h))
@@ -72,6 +72,8 @@ class Parser:
             rc = self._l.av1p_set_tile_threads(h, int(tile_threads))
             if rc:
                 raise ParseError(rc, f"av1p_set_tile_threads({tile_threads})")
+        if not mode_info:  # frames carry no mode-info grid (av1p_set_mode_info)
+            self._l.av1p_set_mode_info(h, 0)
 
     def decode_tu(self, data):
         n = C.c_int(0)

@@ -31,6 +31,7 @@ def _plib():
     l.av1p_frame.restype = vp
     l.av1p_last_error.argtypes = [vp]
     l.av1p_last_error.restype = C.c_char_p
+    l.av1p_set_mode_info.argtypes = [vp, C.c_int]
     return l
 
 
@@ -56,6 +57,7 @@ class IvfPipeline:
             err.append("av1p_create failed")
             q.put(None)
             return
+        l.av1p_set_mode_info(p, 0)  # the mode-info grid is rebuilt on the device (k_mi)
         n = C.c_int()
         try:
             for tu in self.tus[j]:

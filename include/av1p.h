@@ -17,6 +17,8 @@
  *   av1p_frame                  -- the parsed frame the reference walks in decodeFrame
  *   av1p_set_tile_threads       -- (no counterpart: the reference parses tiles one after
  *                                  another, Parser::parseTileGroup, Parser.cpp:492-521)
+ *   av1p_set_mode_info          -- (no counterpart: refdump.cpp fillFrameTables always
+ *                                  builds the grid)
  */
 #ifndef AV1P_H
 #define AV1P_H
@@ -43,6 +45,10 @@ const av1r_frame_batch* av1p_frame(av1p_ctx* ctx, int i);
  * hardware threads), or the AV1P_TILE_THREADS environment variable).  Tiles are independent
  * for entropy decoding; the batch is identical whatever the setting. */
 int av1p_set_tile_threads(av1p_ctx* ctx, int n);
+/* 1 (default): each frame's av1r_frame_batch.mi holds the per-4x4 mode-info grid;
+ * 0: mi is NULL. av1r_pack / av1r_decode_frame rebuild the grid on the device from the
+ * block records and do not read it; av1r_frame_begin (tile-split decoding) needs it. */
+int av1p_set_mode_info(av1p_ctx* ctx, int emit);
 /* Message of the last failure (empty string if none). */
 const char* av1p_last_error(av1p_ctx* ctx);
 

@@ -149,3 +149,20 @@ def test_tile_parallel_parse_is_identical(parser_mod, name):
         assert len(par) == len(serial)
         for k, (f, g) in enumerate(zip(par, serial)):
             assert _same(f, g), f"{name}: frame {k} differs with {n} tile threads"
+
+
+@needs_bits
+@pytest.mark.parametrize("name", ["av1-1-b8-01-size-66x66", "av1-1-b8-06-mfmv"])
+def test_parse_without_mode_info_grid(parser_mod, name):
+    """av1p_set_mode_info(ctx, 0): every section but the mode-info grid is unchanged, and
+    that one is empty (the product paths rebuild it on the device)."""
+    with open(golden.ivf_path(name), "rb") as f:
+        data = f.read()
+    full = parser_mod.Parser().decode_ivf(data)
+    lean = parser_mod.Parser(mode_info=False).decode_ivf(data)
+    assert len(full) == len(lean)
+    for f, g in zip(full, lean):
+        assert g.sec["mi"].size == 0
+        for s in batchfile.SECTIONS:
+            if s != "mi":
+                assert np.array_equal(f.sec[s], g.sec[s]), s

@@ -39,6 +39,7 @@ int main(int argc, char** argv)
     for (int r = 0; r < reps; r++) {
         av1p_ctx* ctx;
         if (av1p_create(&ctx)) return 1;
+        if (getenv("AV1P_NO_MI")) av1p_set_mode_info(ctx, 0);
         frames = 0;
         const auto t0 = std::chrono::steady_clock::now();
         for (auto& tu : tus) {
