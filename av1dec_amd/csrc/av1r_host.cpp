@@ -722,6 +722,59 @@ static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
 }
 static bool g_modeEdges = !getenv("AV1R_MODE_EDGES") || atoi(getenv("AV1R_MODE_EDGES")) != 0;
 
+// AV1R_SCHED_CHECK=1 (debug aid): the invariants k_flow relies on, checked on the host for a
+// frame's flow schedule -- every index in range, every dependency (listed or through an edge
+// granule) in an earlier k_flow group, residual tiles inside the residual buffer.  Prints
+// the violations found and a summary line.
+static void schedule_check(av1r_ctx* c, const av1r_frame_batch* b)
+{
+    long bad = 0;
+    auto report = [&](const char* what, size_t i, long a, long b2) {
+        if (bad++ < 20) fprintf(stderr, "av1r sched check: %s (item %zu: %ld %ld)\n", what, i, a, b2);
+    };
+    const size_t ni = c->items.size();
+    std::vector<int64_t> grp(ni, -1);
+    int64_t g = 0;
+    for (size_t l = 0; l < c->levels.size(); l++) {
+        const Level& lv = c->levels[l];
+        if (lv.off[0] + lv.cnt[0] > c->tiles.size()) report("tiles range", l, lv.off[0], lv.cnt[0]);
+        if (lv.off[1] + lv.cnt[1] > ni || lv.off[2] != lv.off[1] + lv.cnt[1] || lv.off[2] + lv.cnt[2] > ni)
+            report("items range", l, lv.off[1], lv.cnt[1]);
+        if (lv.fcnt[1] > lv.cnt[1] || lv.fcnt[2] > lv.cnt[2]) report("flow counts", l, lv.fcnt[1], lv.fcnt[2]);
+        for (uint32_t q = 0; q < lv.fcnt[1]; q++) grp[lv.off[1] + q] = g++;
+        for (uint32_t q = 0; q < lv.fcnt[2]; q++) grp[lv.off[2] + q] = g + q / 4;
+        g += (lv.fcnt[2] + 3) / 4;
+    }
+    for (uint32_t t : c->tiles)
+        if (AV1R_ITEM_KIND(t) != AV1R_ITEM_INTER || (AV1R_ITEM_INDEX(t) >> 4) >= b->n_blocks) report("tile code", 0, t, b->n_blocks);
+    for (size_t i = 0; i < ni; i++) {
+        const WorkItem& w = c->items[i];
+        const uint32_t kind = AV1R_ITEM_KIND(w.code), idx = AV1R_ITEM_INDEX(w.code);
+        if (kind == AV1R_ITEM_TB ? idx >= b->n_tbs : kind == AV1R_ITEM_II ? idx >= b->n_blocks : true) report("item code", i, w.code, 0);
+        if (w.block >= b->n_blocks) report("item block", i, w.block, b->n_blocks);
+        if (grp[i] < 0) continue;  // (not a k_flow item)
+        if ((size_t)w.dep_off + w.dep_cnt > c->deps.size()) report("deps range", i, w.dep_off, w.dep_cnt);
+        for (uint32_t d = 0; d < w.dep_cnt && (size_t)w.dep_off + d < c->deps.size(); d++) {
+            const uint32_t p = c->deps[w.dep_off + d];
+            if (p >= i || grp[p] < 0 || grp[p] >= grp[i]) report("listed dependency order", i, p, p < ni ? grp[p] : -1);
+        }
+        if (c->granOk && kind == AV1R_ITEM_TB) {
+            const uint32_t ro = w.dep_off >= 1 ? c->deps[w.dep_off - 1] : 0;
+            const size_t area = (size_t)av1r_tx_w[w.tx_size] * av1r_tx_h[w.tx_size];
+            if (ro != ~0u && (size_t)ro + area > c->resElems) report("residual tile", i, ro, (long)c->resElems);
+            if ((ro == ~0u) != (w.coef_cnt == 0)) report("residual presence", i, ro, w.coef_cnt);
+        }
+        const int32_t node = kind == AV1R_ITEM_TB ? c->nodeOfTb[idx] : kind == AV1R_ITEM_II ? c->nodeOfBlk[idx] : -1;
+        if (node < 0 || c->edgeStart.size() <= (size_t)node + 1) continue;
+        for (uint32_t e = c->edgeStart[node]; e < c->edgeStart[node + 1]; e++) {
+            const int32_t pn = c->edgeDeps[e];
+            const int32_t p = pn >= 0 && (size_t)pn < c->nodePos.size() ? c->nodePos[pn] : -1;
+            if (p < 0 || grp[p] < 0 || grp[p] >= grp[i]) report("edge producer order", i, p, p >= 0 ? grp[p] : -1);
+        }
+    }
+    fprintf(stderr, "av1r sched check: %zu items, %zu tiles, %lld groups, %ld violations\n", ni, c->tiles.size(), (long long)g, bad);
+}
+
 static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
 {
     const av1r_frame_hdr* h = b->hdr;
@@ -1235,7 +1288,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         }
     }
     clk.lap(PP_SCHED_DEPS);
-    if (flowOnly && !c->flowOk) build_schedule(c, b, allowGran, false);  // k_flow cannot take it: levels too
+    if (flowOnly && !c->flowOk) {
+        build_schedule(c, b, allowGran, false);  // k_flow cannot take it: levels too
+        return;
+    }
+    static const bool check = getenv("AV1R_SCHED_CHECK") != nullptr;
+    if (check && c->flowOk) schedule_check(c, b);
 }
 
 // ------------------------------------------------------------------------------------

@@ -1919,12 +1919,13 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 extern "C" __global__ __launch_bounds__(256) void k_fiprep(const KParams* kps, const uint32_t* __restrict__ pre, int n)
 {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    // frame of item i (a prefix table of the frames' item counts, as table_item)
-    const uint32_t p = lane + 1 < n ? pre[lane + 1] : 0xffffffffu;
-    const uint32_t b = i;
-    const int s = __popcll(__ballot(b >= p));
-    if (s >= n || i >= pre[n]) return;
+    if (i >= pre[n]) return;
+    // frame of item i: the last s with pre[s] <= i in the prefix table of the frames' item
+    // counts (a per-lane binary search: i differs between the lanes, so table_item's ballot
+    // over one wave-uniform index does not apply)
+    int s = 0;
+    for (int w = 32; w; w >>= 1)
+        if (s + w < n && pre[s + w] <= i) s += w;
     const KParams& k = KP(kps, s);
     const uint32_t pos = i - pre[s];
     const WorkItem& wi = k.items[pos];
