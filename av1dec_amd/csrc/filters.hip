@@ -629,8 +629,6 @@ struct CdefLds {
     int16_t pri[64];               // adjusted luma primary strength
     uint8_t filt[64];              // block is filtered (not skip)
     int16_t offY[64][6], offC[64][6];  // tap offsets in the staged tiles (cdef_pair)
-    uint8_t blist[64];             // the filtered blocks first (nf of them), then the others
-    int nf;
 };
 
 // partial[d][k] of cdefDirection (Cdef.cpp:203-261) for one line k of direction d, summed
@@ -902,15 +900,6 @@ DEV void cdef_body(const KParams* kps)
         }
     }
     __syncthreads();
-    if (t < 64) {
-        // the block list: filtered blocks first, so that the filter phase below spreads them
-        // over every lane (a block that is skipped or outside the grid is only copied)
-        const uint64_t fm = __ballot(L.filt[t] != 0);
-        const int before = __popcll(fm & ((1ull << t) - 1));
-        const int nf = __popcll(fm);
-        L.blist[L.filt[t] ? before : nf + (t - before)] = (uint8_t)t;
-        if (t == 0) L.nf = nf;
-    }
     if (t < 64 && L.filt[t]) {
         int best = 0, yDir = 0;
         for (int d = 0; d < 8; d++)
@@ -936,44 +925,57 @@ DEV void cdef_body(const KParams* kps)
             }
     }
     __syncthreads();
-    // the filter (cdefFilter, Cdef.cpp:158-198) over the filtered blocks' 4-pixel groups --
-    // per block 16 of luma (8 rows x 2) and 8 of chroma (2 planes x 4 rows) -- dealt to every
-    // lane in turn, then the other blocks' groups copied (a lane per group, no idle lanes
-    // beside the filtering ones)
+    // luma: 4 lanes per 8x8 block, two rows of 8 (two 4-pixel groups) each
     {
-        const int nf = L.nf;
+        const int b = t >> 2, bi = b >> 3, bj = b & 7;
+        const int j0 = bj * 8;
         const int ySec = h.cdef_y_sec[idx];
+        if (j0 < cols4 * 4) {
+            const bool full = j0 + 8 <= cols4 * 4;  // else only the left 4 columns are in the grid
+            const bool f = L.filt[b];
+            const int pri = L.pri[b];
+            for (int r = 0; r < 2; r++) {
+                const int i = bi * 8 + (t & 3) * 2 + r;
+                if (i >= rows4 * 4) break;
+                const int p = (CD_H + i) * CD_LS + CD_X + j0;
+                uint32_t o[2] = {0, 0};
+#pragma unroll
+                for (int g = 0; g < 2; g++) {
+                    if (g && !full) break;
+                    if (!f) o[g] = *reinterpret_cast<const uint32_t*>(&L.y[0][0] + p + 4 * g);
+                    else if (edge)
+                        o[g] = cdef_quad<true>(&L.y[0][0], p + 4 * g, L.offY[b], pri, ySec, h.cdef_damping, x0 + j0 + 4 * g, y0 + i, CD_LS, limX, limY);
+                    else
+                        o[g] = cdef_quad<false>(&L.y[0][0], p + 4 * g, L.offY[b], pri, ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
+                }
+                uint8_t* dst = &px(k.cdef.pl[0], x0 + j0, y0 + i);
+                if (full) *reinterpret_cast<uint2*>(dst) = make_uint2(o[0], o[1]);
+                else *reinterpret_cast<uint32_t*>(dst) = o[0];
+            }
+        }
+    }
+    // chroma: 2 lanes per 4x4 block and plane, two rows of 4 each
+    {
         const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
-        for (int q = t; q < 64 * 24; q += 256) {
-            const bool filt = q < nf * 24;
-            const int e = filt ? q : q - nf * 24;
-            const int b = L.blist[(filt ? 0 : nf) + e / 24], u = e % 24;
-            const int bi = b >> 3, bj = b & 7;
-            if (u < 16) {  // luma: row bi * 8 + u / 2, columns bj * 8 + 4 (u & 1) ..
-                const int i = bi * 8 + (u >> 1), j = bj * 8 + 4 * (u & 1);
-                if (i >= rows4 * 4 || j >= cols4 * 4) continue;
-                const int p = (CD_H + i) * CD_LS + CD_X + j;
+        const int pl = t >> 7, b = (t >> 1) & 63, bi = b >> 3, bj = b & 7;
+        const int j0 = bj * 4;
+        if (j0 < cols4 * 2) {
+            const bool full = j0 + 4 <= cols4 * 2;  // else only the left 2 columns are in the grid
+            const bool f = L.filt[b];
+            const uint8_t* tile = &L.uv[pl][0][0];
+            for (int r = 0; r < 2; r++) {
+                const int i = bi * 4 + (t & 1) * 2 + r;
+                if (i >= rows4 * 2) break;
+                const int p = (CD_H + i) * CD_CS + CD_X + j0;
                 uint32_t o;
-                if (!filt) o = *reinterpret_cast<const uint32_t*>(&L.y[0][0] + p);
-                else if (edge)
-                    o = cdef_quad<true>(&L.y[0][0], p, L.offY[b], L.pri[b], ySec, h.cdef_damping, x0 + j, y0 + i, CD_LS, limX, limY);
-                else
-                    o = cdef_quad<false>(&L.y[0][0], p, L.offY[b], L.pri[b], ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
-                *reinterpret_cast<uint32_t*>(&px(k.cdef.pl[0], x0 + j, y0 + i)) = o;
-            } else {  // chroma plane (u - 16) / 4: row bi * 4 + (u & 3), columns bj * 4 ..
-                const int pl = (u - 16) >> 2, i = bi * 4 + (u & 3), j = bj * 4;
-                if (i >= rows4 * 2 || j >= cols4 * 2) continue;
-                const uint8_t* tile = &L.uv[pl][0][0];
-                const int p = (CD_H + i) * CD_CS + CD_X + j;
-                uint32_t o;
-                if (!filt) o = *reinterpret_cast<const uint32_t*>(tile + p);
+                if (!f) o = *reinterpret_cast<const uint32_t*>(tile + p);
                 else if (cedge)
-                    o = cdef_quad<true>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j, cy0 + i, CD_CS, climX, climY);
+                    o = cdef_quad<true>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, cx0 + j0, cy0 + i, CD_CS, climX, climY);
                 else
                     o = cdef_quad<false>(tile, p, L.offC[b], uvPri, uvSec, h.cdef_damping - 1, 0, 0, CD_CS, 0, 0);
-                uint8_t* dst = &px(k.cdef.pl[1 + pl], cx0 + j, cy0 + i);
-                if (j + 4 <= cols4 * 2) *reinterpret_cast<uint32_t*>(dst) = o;
-                else *reinterpret_cast<uint16_t*>(dst) = (uint16_t)o;  // (only the left 2 columns are in the grid)
+                uint8_t* dst = &px(k.cdef.pl[1 + pl], cx0 + j0, cy0 + i);
+                if (full) *reinterpret_cast<uint32_t*>(dst) = o;
+                else *reinterpret_cast<uint16_t*>(dst) = (uint16_t)o;
             }
         }
     }
