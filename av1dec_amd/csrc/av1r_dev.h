@@ -106,7 +106,6 @@ struct KParams {
     const uint32_t* tiles;  // its inter tiles, level-ordered: AV1R_ITEM(AV1R_ITEM_INTER, block << 4 | row << 2 | col)
     const uint32_t* deps;   // k_flow: dependency lists (positions in items)
     uint32_t* done;         // k_flow: per item, the epoch of the launch that completed it
-    uint32_t* fip;          // k_flow: per item, its lean-path parameters (k_fiprep, 8 words)
     // k_flow mode: residuals precomputed by k_resid.  tb_res[tb]: the TB's residual tile
     // (w x h int16, row-major) at res + tb_res[tb], or ~0u (no coefficients, or an inter
     // TB outside an inter-intra block: k_resid adds it into the frame directly)

@@ -36,7 +36,6 @@ void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
 void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_lfcode(const KParams* kps, int n, int maxUnits, hipStream_t s);
-void launch_k_fiprep(const KParams* kps, const uint32_t* pre, int n, uint32_t items, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
@@ -1315,12 +1314,11 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szTiles = align256(4 * c->tiles.size() + 4);
     const size_t szDeps = align256(4 * c->deps.size() + 4);
     const size_t szDone = align256(4 * c->items.size() + 4);  // zeroed on the device (k_mi_zero): no launch's epoch
-    const size_t szFip = align256(32 * c->items.size() + 4);  // k_fiprep's records (device-filled)
     const size_t szTbRes = align256(4 * c->tbRes.size() + 4);
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szFip + szMi + szLfc;
+    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
@@ -1359,7 +1357,6 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
     P.upBytes = off;  // everything up to here travels; what follows is filled on the device
     k.done = (uint32_t*)put(nullptr, 0, szDone);
-    k.fip = (uint32_t*)put(nullptr, 0, szFip);
     k.n_items = (uint32_t)c->items.size();
     k.mi = (const av1r_mi*)put(nullptr, 0, szMi);
     k.lfc = (uint8_t*)put(nullptr, 0, szLfc);
@@ -1436,7 +1433,7 @@ static int job_begin(FrameJob& j)
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
         rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
-        rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.fip), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
+        rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
     }
     for (int s = 0; s < 8; s++)
         if (c->slots[s]) j.k.ref[s] = c->slots[s]->d;
@@ -1625,7 +1622,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     size_t nGroups = 0;
     for (auto& j : jobs)
         for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
-    const size_t resTabBytes = align256(4 * 3 * ((size_t)n + 1));  // k_resid's two tables, k_fiprep's
+    const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
     const size_t nEntries = nGroups;
     const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nEntries + resTabBytes : 0);
     const bool anyFlow = flow && nEntries;
@@ -1735,14 +1732,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                     g[1] = lv.off[2] + q;
                 }
             }
-        // k_resid tables: prefix sums of the frames' workgroup counts (small, large); then
-        // k_fiprep's: of their item counts
+        // k_resid tables: prefix sums of the frames' workgroup counts (small, large)
         uint32_t* rt = g;
-        rt[0] = rt[n + 1] = rt[2 * n + 2] = 0;
+        rt[0] = rt[n + 1] = 0;
         for (int i = 0; i < n; i++) {
             rt[i + 1] = rt[i] + jobs[i].P->nResidS;
             rt[n + 2 + i] = rt[n + 1 + i] + jobs[i].P->nResidL;
-            rt[2 * n + 3 + i] = rt[2 * n + 2 + i] + jobs[i].k.n_items;
         }
     }
     if (host_prof()) tp2 = now_us();
@@ -1836,8 +1831,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries);
         const uint32_t* hrt = reinterpret_cast<const uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries);
-        // the small intra items' lean-path parameters (k_fiprep), off k_flow's chains
-        if (hrt[3 * n + 2] && g_fastIntra.load(std::memory_order_relaxed)) launch_k_fiprep(dk, drt + 2 * n + 2, n, hrt[3 * n + 2], st);
         if (hrt[n]) launch_k_resid(0, dk, drt, n, hrt[n], st);
         if (hrt[2 * n + 1]) launch_k_resid(1, dk, drt + n + 1, n, hrt[2 * n + 1], st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));

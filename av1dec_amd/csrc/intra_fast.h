@@ -41,15 +41,13 @@ DEV bool fi_ok(const WorkItem& tb, const av1r_block& blk)
     return tb.pred == AV1R_PRED_INTRA && !(tb.plane == 0 && (blk.flags & AV1R_BLK_FILTER_INTRA));
 }
 
-// Every parameter of the prediction from the batch only: uniform (NT = 64: scalar table
-// reads) or per lane (NT = 1: k_fiprep, one item per lane)
-template <int NT>
-DEV FiParams fi_setup_t(const KParams& k, const WorkItem& tb, const av1r_block& blk, int edgeFilter)
+// Every parameter of the prediction (uniform: scalar registers), from the batch only
+DEV FiParams fi_setup(const KParams& k, const WorkItem& tb, const av1r_block& blk, int edgeFilter)
 {
     FiParams F;
     const int plane = tb.plane, x = tb.x, y = tb.y, sub = plane ? 1 : 0;
-    F.log2W = ctab<NT>(av1r_tx_w_log2, tb.tx_size);
-    F.log2H = ctab<NT>(av1r_tx_h_log2, tb.tx_size);
+    F.log2W = stab(av1r_tx_w_log2, tb.tx_size);
+    F.log2H = stab(av1r_tx_h_log2, tb.tx_size);
     const int w = 1 << F.log2W, h = 1 << F.log2H;
     const int maxXd = (k.mi_cols * 4) >> sub, maxYd = (k.mi_rows * 4) >> sub;
     F.hA = (tb.flags & AV1R_TB_HAVE_ABOVE) != 0;
@@ -65,7 +63,7 @@ DEV FiParams fi_setup_t(const KParams& k, const WorkItem& tb, const av1r_block& 
                              : ((blk.flags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
     F.strA = F.strL = F.nA = F.nL = F.nUA = F.nUL = F.corner = F.dx = F.dy = 0;
     if (mode >= AV1R_V_PRED && mode <= AV1R_D67_PRED) {
-        const int pAngle = ctab<NT>(av1r_mode_to_angle, mode) + (plane == 0 ? blk.angle_delta_y : blk.angle_delta_uv) * 3;
+        const int pAngle = stab(av1r_mode_to_angle, mode) + (plane == 0 ? blk.angle_delta_y : blk.angle_delta_uv) * 3;
         F.cls = pAngle < 90 ? FI_Z1 : pAngle == 90 ? FI_V : pAngle < 180 ? FI_Z2 : pAngle == 180 ? FI_H : FI_Z3;
         if (edgeFilter && pAngle != 90 && pAngle != 180) {
             F.corner = pAngle > 90 && pAngle < 180 && (w + h) >= 24;
@@ -76,68 +74,14 @@ DEV FiParams fi_setup_t(const KParams& k, const WorkItem& tb, const av1r_block& 
             F.nUA = edge_upsample_used(w, h, smooth, pAngle - 90) ? w + (pAngle < 90 ? h : 0) : 0;
             F.nUL = edge_upsample_used(w, h, smooth, pAngle - 180) ? h + (pAngle > 180 ? w : 0) : 0;
         }
-        if (pAngle < 90) F.dx = ctab<NT>(av1r_dr_intra_derivative, pAngle);
-        else if (pAngle > 90 && pAngle < 180) F.dx = ctab<NT>(av1r_dr_intra_derivative, 180 - pAngle);
-        if (pAngle > 90 && pAngle < 180) F.dy = ctab<NT>(av1r_dr_intra_derivative, pAngle - 90);
-        else if (pAngle > 180) F.dy = ctab<NT>(av1r_dr_intra_derivative, 270 - pAngle);
+        if (pAngle < 90) F.dx = stab(av1r_dr_intra_derivative, pAngle);
+        else if (pAngle > 90 && pAngle < 180) F.dx = stab(av1r_dr_intra_derivative, 180 - pAngle);
+        if (pAngle > 90 && pAngle < 180) F.dy = stab(av1r_dr_intra_derivative, pAngle - 90);
+        else if (pAngle > 180) F.dy = stab(av1r_dr_intra_derivative, 270 - pAngle);
     } else {
         F.cls = mode == AV1R_DC_PRED ? FI_DC : mode == AV1R_SMOOTH_PRED ? FI_SMOOTH : mode == AV1R_SMOOTH_V_PRED ? FI_SMOOTH_V
               : mode == AV1R_SMOOTH_H_PRED ? FI_SMOOTH_H : FI_PAETH;
     }
-    return F;
-}
-
-DEV FiParams fi_setup(const KParams& k, const WorkItem& tb, const av1r_block& blk, int edgeFilter)
-{
-    return fi_setup_t<64>(k, tb, blk, edgeFilter);
-}
-DEV FiParams fi_setup_v(const KParams& k, const WorkItem& tb, const av1r_block& blk, int edgeFilter)
-{
-    return fi_setup_t<1>(k, tb, blk, edgeFilter);
-}
-
-// FiParams as 8 dwords (k_fiprep's record per item, read by k_flow with one scalar load);
-// word 0 bit 31: the item takes the lean path (else the generic one, block record needed)
-struct FiPacked {
-    uint32_t w[8];
-};
-DEV FiPacked fi_pack(const FiParams& F, bool lean)
-{
-    FiPacked P;
-    P.w[0] = (uint32_t)F.cls | (uint32_t)F.log2W << 4 | (uint32_t)F.log2H << 7 | (uint32_t)F.hA << 10 | (uint32_t)F.hL << 11 |
-             (uint32_t)F.cfl << 12 | (uint32_t)F.corner << 13 | (uint32_t)F.strA << 14 | (uint32_t)F.strL << 16 |
-             (lean ? 1u << 31 : 0u);
-    P.w[1] = (uint32_t)(F.aboveLimit & 0xffff) | (uint32_t)F.leftLimit << 16;
-    P.w[2] = (uint32_t)F.nA | (uint32_t)F.nL << 8 | (uint32_t)F.nUA << 16 | (uint32_t)F.nUL << 24;
-    P.w[3] = (uint32_t)(F.dx & 0xffff) | (uint32_t)F.dy << 16;
-    P.w[4] = (uint32_t)(F.alpha & 0xff);
-    P.w[5] = (uint32_t)(F.maxLW & 0xffff) | (uint32_t)F.maxLH << 16;
-    P.w[6] = P.w[7] = 0;
-    return P;
-}
-DEV FiParams fi_unpack(const FiPacked& P)
-{
-    FiParams F;
-    F.cls = P.w[0] & 15;
-    F.log2W = (P.w[0] >> 4) & 7;
-    F.log2H = (P.w[0] >> 7) & 7;
-    F.hA = (P.w[0] >> 10) & 1;
-    F.hL = (P.w[0] >> 11) & 1;
-    F.cfl = (P.w[0] >> 12) & 1;
-    F.corner = (P.w[0] >> 13) & 1;
-    F.strA = (P.w[0] >> 14) & 3;
-    F.strL = (P.w[0] >> 16) & 3;
-    F.aboveLimit = (int)(P.w[1] & 0xffff);
-    F.leftLimit = (int)(P.w[1] >> 16);
-    F.nA = P.w[2] & 0xff;
-    F.nL = (P.w[2] >> 8) & 0xff;
-    F.nUA = (P.w[2] >> 16) & 0xff;
-    F.nUL = P.w[2] >> 24;
-    F.dx = (int)(P.w[3] & 0xffff);
-    F.dy = (int)(P.w[3] >> 16);
-    F.alpha = (int8_t)(P.w[4] & 0xff);
-    F.maxLW = (int)(P.w[5] & 0xffff);
-    F.maxLH = (int)(P.w[5] >> 16);
     return F;
 }
 
