@@ -1908,4 +1908,133 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     }
 }
 
->>>>>>> parent of 04053cb (k_fiprep: small intra items' lean-path parameters derived per item ahead of k_flow (one scalar load instead of item -> block -> tables))
+// persistent grid of k_flow on `device`: every CU's resident workgroups (capped at 8 per
+// CU), a multiple of FLOW_QUEUES
+int flow_grid(int device, int maxPer)
+{
+    static int cache[64][9] = {};  // per device and workgroups-per-CU bound (1..8)
+    if (device < 0 || device >= 64) return FLOW_QUEUES;
+    const int slot = maxPer < 1 ? 1 : (maxPer > 8 ? 8 : maxPer);
+    if (!cache[device][slot]) {
+        int cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 32;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k_flow), 256, 0) != hipSuccess || per <= 0)
+            per = 1;
+        per = per > 8 ? 8 : per;
+        per = per > maxPer ? maxPer : per;
+        // AV1R_FLOW_PER_CU: fewer resident workgroups per CU (A/B of polling pressure)
+        if (const char* e = getenv("AV1R_FLOW_PER_CU")) per = per < atoi(e) ? per : (atoi(e) > 0 ? atoi(e) : per);
+        int g = ((cus * per) / FLOW_QUEUES) * FLOW_QUEUES;
+        cache[device][slot] = g < FLOW_QUEUES ? FLOW_QUEUES : g;
+    }
+    return cache[device][slot];
+}
+
+#ifdef AV1R_FLOW_DEBUG
+// overlap count since the last reset; pairs[] (up to n) the (earlier epoch slot << 16 |
+// entering epoch) of the first overlaps; reset = 1 zeroes the counters afterwards
+uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset)
+{
+    uint32_t v = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_flow_overlap), sizeof(v));
+    if (pairs && n > 0) (void)hipMemcpyFromSymbol(pairs, HIP_SYMBOL(g_flow_pairs), 4 * (n < FLOW_DBG_PAIRS ? n : FLOW_DBG_PAIRS));
+    if (reset) {
+        const uint32_t z[64] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_flow_overlap), z, 4);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_flow_active), z, sizeof(z));
+        (void)hipDeviceSynchronize();
+    }
+    return v;
+}
+#endif
+
+void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uint32_t* ctl, uint32_t* hostErr,
+    uint32_t epoch, int grid, unsigned long long* trace, hipStream_t s)
+{
+    (void)hostErr;  // (its address travels in the control block: FLOW_HOSTERR)
+    hipLaunchKernelGGL(k_flow, dim3(grid), dim3(256), 0, s, kps, reinterpret_cast<const uint2*>(groups), nGroups, ctl, epoch,
+        trace);
+}
+
+#endif  // AV1R_FLOW_PART
+
+#ifndef AV1R_FLOW_PART
+// ---------------------------------------------------------------------------------
+// k_resid (k_flow mode, after k_inter): the residual of every TB with coefficients
+// (TransformBlock::reconstruct + inverseTransform, TransformBlock.cpp:2173-2276), with no
+// dependencies at all.  An inter TB outside an inter-intra block is added to its
+// prediction in the frame right here (TransformBlock.cpp:2440-2456); every other residual
+// is stored as an int16 tile for the k_flow item (intra TB, inter-intra blend) that adds
+// it.  k_resid_s: 16 TBs with sides <= 16 per 256-lane workgroup, 16 lanes each;
+// k_resid_l: one larger TB per 64-lane workgroup.  tab: [prefix of the frames' workgroup
+// counts (n + 1)].
+// ---------------------------------------------------------------------------------
+template <int NT, int MAX>
+DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
+{
+    constexpr int RS = MAX + 2;
+    const int t = coop_lane<NT>();
+    const av1r_tb& tb = k.tbs[ti];
+    const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
+    const av1r_block& blk = k.blocks[tb.block];
+    const uint32_t ro = k.tb_res[ti];
+    tb_residual<NT, MAX>(k, tb, blk, res, c0);
+    const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;
+    const int nq = (av1r_tx_w[tb.tx_size] * av1r_tx_h[tb.tx_size]) >> 2;
+    const DevPlane& dst = k.cur.pl[tb.plane];
+    for (int q = t; q < nq; q += NT) {
+        const int i = q >> l2q, j = (q & ((1 << l2q) - 1)) << 2;
+        const uint32_t r01 = *reinterpret_cast<const uint32_t*>(&res[i * RS + j]);
+        const uint32_t r23 = *reinterpret_cast<const uint32_t*>(&res[i * RS + j + 2]);
+        if (ro == ~0u) stp4<false>(dst, tb.x + j, tb.y + i, add4(ldp4<false>(dst, tb.x + j, tb.y + i), make_uint2(r01, r23)));
+        else reinterpret_cast<uint2*>(k.res + ro)[q] = make_uint2(r01, r23);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ __align__(16) int16_t res[16][16 * 18];
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+    const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    const KParams& k = KP(kps, s);
+    const int g = threadIdx.x >> 4;
+    const uint32_t ti = k.resid_s[(b - tab[s]) * 16 + g];
+    if (ti != ~0u) resid_one<16, 16>(k, ti, res[g]);
+}
+
+extern "C" __global__ __launch_bounds__(64) void k_resid_l(const KParams* kps, const uint32_t* __restrict__ tab, int n)
+{
+    __shared__ __align__(16) int16_t res[64 * 66];
+    const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
+    const int lane = threadIdx.x & 63;
+    const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
+    const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
+    const KParams& k = KP(kps, s);
+    resid_one<64, 64>(k, k.resid_l[b - tab[s]], res);
+}
+
+void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s)
+{
+    if (large) hipLaunchKernelGGL(k_resid_l, dim3(groups), dim3(64), 0, s, kps, tab, n);
+    else hipLaunchKernelGGL(k_resid_s, dim3(groups), dim3(256), 0, s, kps, tab, n);
+}
+
+// kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4);
+// kind 2 / 3: medium / small plain inter blocks, `items` groups of two / four
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS,
+    unsigned long long* trace, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, trace);
+}
+void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
+    uint32_t traceBase, hipStream_t s)
+{
+    if (kind == 0) hipLaunchKernelGGL(k_inter, dim3(items), dim3(64), 0, s, kps, tab, n, trace, traceBase);
+    else if (kind == 2) hipLaunchKernelGGL(k_inter_m, dim3(items), dim3(64), 0, s, kps, tab, n);
+    else if (kind == 3) hipLaunchKernelGGL(k_inter_s, dim3(items), dim3(64), 0, s, kps, tab, n);
+    else hipLaunchKernelGGL(k_tb, dim3(items), dim3(256), 0, s, kps, tab, n, trace, traceBase);
+}
+#endif  // !AV1R_FLOW_PART
