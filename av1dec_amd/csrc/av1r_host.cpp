@@ -721,6 +721,17 @@ static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
 }
 static bool g_modeEdges = !getenv("AV1R_MODE_EDGES") || atoi(getenv("AV1R_MODE_EDGES")) != 0;
 
+// k_flow's small-item groups: four items (one per wave) on a thin level, AV1R_FLOW_G (8:
+// two per wave, run one after the other) on a level of at least AV1R_FLOW_G_MIN small items
+// of the frame, where the workgroup's ticket, group load and closing barrier are paid once per
+// two items per wave (a level that crowded is far from the dependency chains' tail)
+static uint32_t flow_small_group(const Level& lv)
+{
+    static const uint32_t G = getenv("AV1R_FLOW_G") ? (uint32_t)std::max(4, std::min(64, atoi(getenv("AV1R_FLOW_G")))) : 8u;
+    static const uint32_t minItems = getenv("AV1R_FLOW_G_MIN") ? (uint32_t)std::max(0, atoi(getenv("AV1R_FLOW_G_MIN"))) : 256u;
+    return lv.fcnt[2] >= minItems ? G : 4u;
+}
+
 // AV1R_SCHED_CHECK=1 (debug aid): the invariants k_flow relies on, checked on the host for a
 // frame's flow schedule -- every index in range, every dependency (listed or through an edge
 // granule) in an earlier k_flow group, residual tiles inside the residual buffer.  Prints
@@ -741,8 +752,9 @@ static void schedule_check(av1r_ctx* c, const av1r_frame_batch* b)
             report("items range", l, lv.off[1], lv.cnt[1]);
         if (lv.fcnt[1] > lv.cnt[1] || lv.fcnt[2] > lv.cnt[2]) report("flow counts", l, lv.fcnt[1], lv.fcnt[2]);
         for (uint32_t q = 0; q < lv.fcnt[1]; q++) grp[lv.off[1] + q] = g++;
-        for (uint32_t q = 0; q < lv.fcnt[2]; q++) grp[lv.off[2] + q] = g + q / 4;
-        g += (lv.fcnt[2] + 3) / 4;
+        const uint32_t G = flow_small_group(lv);
+        for (uint32_t q = 0; q < lv.fcnt[2]; q++) grp[lv.off[2] + q] = g + q / G;
+        g += (lv.fcnt[2] + G - 1) / G;
     }
     for (uint32_t t : c->tiles)
         if (AV1R_ITEM_KIND(t) != AV1R_ITEM_INTER || (AV1R_ITEM_INDEX(t) >> 4) >= b->n_blocks) report("tile code", 0, t, b->n_blocks);
@@ -1623,7 +1635,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // k_flow groups: one large item, or up to four small ones
     size_t nGroups = 0;
     for (auto& j : jobs)
-        for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + 3) / 4;
+        for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + flow_small_group(lv) - 1) / flow_small_group(lv);
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
     const size_t nEntries = nGroups;
     const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nEntries + resTabBytes : 0);
@@ -1710,7 +1722,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (flow) {
         // control block (zeroed) + the groups in topological order: level by level, the
         // frames interleaved; {frame << 8 | n, first item}: n = 0 one large item, else
-        // 1..4 small items
+        // 1..flow_small_group() small items
         memset(M.host + kBytes + tabBytes, 0, FLOW_CTL_BYTES);
         uint32_t* hctl = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes);
         *reinterpret_cast<uint32_t**>(hctl + FLOW_HOSTERR) = rec ? rec->err : nullptr;
@@ -1729,8 +1741,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                     g[0] = (uint32_t)i << 8;
                     g[1] = lv.off[1] + q;
                 }
-                for (uint32_t q = 0; q < lv.fcnt[2]; q += 4, g += 2) {
-                    g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(4, lv.fcnt[2] - q);
+                const uint32_t G = flow_small_group(lv);
+                for (uint32_t q = 0; q < lv.fcnt[2]; q += G, g += 2) {
+                    g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(G, lv.fcnt[2] - q);
                     g[1] = lv.off[2] + q;
                 }
             }

@@ -1829,7 +1829,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 }
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
-// workgroup), n = 1..4 small items (one per wave)
+// workgroup), n >= 1 small items (wave w runs items w, w + 4, ..)
 #ifndef AV1R_FLOW_WAVES
 #define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better)
 #endif
@@ -1897,9 +1897,12 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
         if (n == 0) {
             flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8);
         } else {
+            // small items: wave w runs items w, w + 4, .. of the group, one after the other in
+            // its own LDS tiles (the host's groups hold 4, or 8 on crowded levels: items of
+            // one level, none waiting for another)
             const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (a scalar branch: no item code runs with exec = 0)
-            if (wave < n)
-                flow_item<64, TB_SMALL>(k, gd.y + wave, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
+            for (uint32_t w = wave; w < n; w += 4)
+                flow_item<64, TB_SMALL>(k, gd.y + w, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
                     gd.x >> 8);
         }
         if (!pf && threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
