@@ -15,7 +15,10 @@ struct av1p_ctx {
     std::string err;
     void release()
     {
-        for (auto* f : frames) delete f;
+        for (auto* f : frames) {
+            if (parser.spare.size() < 4) parser.spare.push_back(f);  // (Parser::take_frame)
+            else delete f;
+        }
         frames.clear();
     }
     ~av1p_ctx() { release(); }

@@ -192,6 +192,47 @@ int tx_class(int type)
     return TX_CLASS_2D;
 }
 
+// Per scan position of a transform size and class, everything the level loop of coeffs()
+// derives from the position (built once): its offset in the padded level map, its raster
+// position, the base-level context offset (kCoeffBaseCtxOffset / kCoeffBasePosCtxOffset;
+// bit 7: the DC of a 2D class, whose context is 0) and the range context offset (0 / 7 / 14,
+// TransformBlock::get_br_ctx).  The scan orders and offsets are the spec's
+// (TransformBlock.cpp:1402-1424, 1462-1580).
+struct ScanEntry {
+    uint16_t pad, pos;
+    uint8_t base, br;
+};
+struct ScanTables {
+    std::vector<ScanEntry> t[19][3];  // [tx size][class]
+    ScanTables()
+    {
+        static const int kTypeOfClass[3] = {DCT_DCT, H_DCT, V_DCT};  // TX_CLASS_2D / HORIZ / VERT
+        for (int tx = 0; tx < 19; tx++)
+            for (int cls = 0; cls < 3; cls++) {
+                // (the 1D classes -- V_* / H_* types -- only in transform sets of sizes up to 16x16)
+                if (cls != TX_CLASS_2D && kTxSizeSqrUp[tx] > 2) continue;
+                const int16_t* scan = get_scan(tx, kTypeOfClass[cls]);
+                const int adj = kAdjustedTxSize[tx];
+                const int bwl = av1r_tx_w_log2[adj], width = 1 << bwl, height = av1r_tx_h[adj], ps = width + 4;
+                std::vector<ScanEntry>& v = t[tx][cls];
+                v.resize((size_t)height << bwl);
+                for (size_t c = 0; c < v.size(); c++) {
+                    const int pos = scan[c], row = pos >> bwl, col = pos - (row << bwl);
+                    ScanEntry& e = v[c];
+                    e.pad = (uint16_t)(row * ps + col);
+                    e.pos = (uint16_t)pos;
+                    if (cls == TX_CLASS_2D) e.base = pos == 0 ? 0x80 : kCoeffBaseCtxOffset[tx][std::min(row, 4)][std::min(col, 4)];
+                    else e.base = kCoeffBasePosCtxOffset[std::min(cls == TX_CLASS_VERT ? row : col, 2)];
+                    if (pos == 0) e.br = 0;
+                    else if (cls == TX_CLASS_2D) e.br = (row < 2 && col < 2) ? 7 : 14;
+                    else if (cls == TX_CLASS_HORIZ) e.br = col == 0 ? 7 : 14;
+                    else e.br = row == 0 ? 7 : 14;
+                }
+            }
+    }
+};
+const ScanTables kScanTables;
+
 // ---- per-block parse state (the members of the reference's Block, Block.h:198-275) ----
 struct Blk {
     int r, c, bsize, bw4, bh4;
@@ -259,7 +300,8 @@ private:
     Cdfs& cdf;
     std::vector<Tb> tbs;
     std::vector<int> quant;  // Quant[] of the transform block being parsed
-    uint8_t lvl[36 * 36] = {};  // coefficient levels while parsing them, padded (coeffs())
+    // coefficient levels while parsing them, padded (coeffs()): level << 8 | min(level, 3)
+    uint16_t lvl[36 * 36] = {};
 
     int S(uint16_t* c, int n) { return sd.read(c, n); }
     template <int N>
@@ -447,8 +489,8 @@ struct ProfAcc {
     uint64_t t[10] = {};
     ~ProfAcc()
     {
-        fprintf(stderr, "av1p prof (Mcycles): mode %.1f residual %.1f mi %.1f emit %.1f | coef: head %.1f eob %.1f levels %.1f signs %.1f pack %.1f\n",
-                t[0] / 1e6, t[1] / 1e6, t[2] / 1e6, t[3] / 1e6, t[4] / 1e6, t[5] / 1e6, t[6] / 1e6, t[7] / 1e6, t[8] / 1e6);
+        fprintf(stderr, "av1p prof (Mcycles): mode %.1f residual %.1f mi %.1f emit %.1f | coef %.1f: head %.1f eob %.1f levels %.1f signs %.1f pack %.1f\n",
+                t[0] / 1e6, t[1] / 1e6, t[2] / 1e6, t[3] / 1e6, t[9] / 1e6, t[4] / 1e6, t[5] / 1e6, t[6] / 1e6, t[7] / 1e6, t[8] / 1e6);
     }
 };
 static ProfAcc g_prof;
@@ -2178,9 +2220,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             }
             set_luma_type(type);
         }
+        PROF_T(c1);
+        PROF_ADD(4, c0, c1);
         t.type = compute_tx_type(b, plane, txSz, x4, y4);
         const int cls = tx_class(t.type);
-        const int16_t* scan = get_scan(txSz, t.type);
         // eob (TransformBlock::getEob, 1440-1460)
         const int eobMultisize = std::min(av1r_tx_w_log2[txSz], (uint8_t)5) + std::min(av1r_tx_h_log2[txSz], (uint8_t)5) - 4;
         const int eobCtx = cls == TX_CLASS_2D ? 0 : 1;
@@ -2205,22 +2248,30 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             }
         }
         PROF_T(c2);
+        PROF_ADD(5, c1, c2);
         // levels, in reverse scan order
         const int adj = kAdjustedTxSize[txSz];
         const int bwl = av1r_tx_w_log2[adj];
         const int width = 1 << bwl, height = av1r_tx_h[adj];
         // levels so far, padded by 4 zero rows / columns below and right (every context offset
-        // is non-negative): the neighbour sums need no bounds checks
+        // is non-negative): the neighbour sums need no bounds checks.  Each entry holds
+        // level << 8 | min(level, 3), and the range context's 3 neighbours are the first 3 of
+        // the base context's 5 (both offset lists of the spec, for every class), so one pass of
+        // 16-bit sums gives both: the 5-sum's low byte (<= 15) the base magnitude, the 3-sum's
+        // high byte the range magnitude
         const int ps = width + 4;
-        // the context neighbours as offsets into lvl[] (per transform block, not per level)
-        int sigOff[5], magOff[3];
-        for (int k = 0; k < 5; k++) sigOff[k] = kSigRefDiffOffset[cls][k][0] * ps + kSigRefDiffOffset[cls][k][1];
-        for (int k = 0; k < 3; k++) magOff[k] = kMagRefOffset[cls][k][0] * ps + kMagRefOffset[cls][k][1];
+        int off[5];  // kSigRefDiffOffset in lvl[] units (per transform block, not per level)
+        for (int k = 0; k < 5; k++) off[k] = kSigRefDiffOffset[cls][k][0] * ps + kSigRefDiffOffset[cls][k][1];
+        const ScanEntry* se = kScanTables.t[txSz][cls].data();
+        uint16_t* const cb = cdf.coef.coeff_base[txSzCtx][ptype][0];
+        uint16_t* const cbr = cdf.coef.coeff_br[std::min(txSzCtx, 3)][ptype][0];
+        constexpr int kCbStride = sizeof(cdf.coef.coeff_base[0][0][0]) / sizeof(uint16_t);
+        constexpr int kBrStride = sizeof(cdf.coef.coeff_br[0][0][0]) / sizeof(uint16_t);
         for (int c = eob - 1; c >= 0; c--) {
-            const int pos = scan[c];
+            const ScanEntry e = se[c];
+            uint16_t* lp = &lvl[e.pad];
+            const uint32_t s3 = (uint32_t)lp[off[0]] + lp[off[1]] + lp[off[2]];
             int level;
-            const int row = pos >> bwl, col = pos - (row << bwl);
-            const uint8_t* lp = &lvl[row * ps + col];
             if (c == eob - 1) {
                 int ctx;
                 if (c == 0) ctx = kSigCoefContexts - 4;
@@ -2230,45 +2281,32 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 ctx = ctx - kSigCoefContexts + kSigCoefContextsEob;
                 level = SN<3>(cdf.coef.coeff_base_eob[txSzCtx][ptype][ctx]) + 1;
             } else {
-                int mag = 0;
-                for (int k = 0; k < 5; k++) mag += std::min((int)lp[sigOff[k]], 3);
-                int ctx = std::min((mag + 1) >> 1, 4);
-                if (cls == TX_CLASS_2D) {
-                    ctx = (row == 0 && col == 0) ? 0 : ctx + kCoeffBaseCtxOffset[txSz][std::min(row, 4)][std::min(col, 4)];
-                } else {
-                    const int idx = cls == TX_CLASS_VERT ? row : col;
-                    ctx += kCoeffBasePosCtxOffset[std::min(idx, 2)];
-                }
-                level = SN<4>(cdf.coef.coeff_base[txSzCtx][ptype][ctx]);
+                const uint32_t mag = (s3 + lp[off[3]] + lp[off[4]]) & 0xff;
+                const int ctx = (e.base & 0x80) ? 0 : std::min((int)(mag + 1) >> 1, 4) + e.base;
+                level = SN<4>(cb + ctx * kCbStride);
             }
             if (level > kNumBaseLevels) {
+                const int ctx = std::min((int)((s3 >> 8) + 1) >> 1, 6) + e.br;
+                uint16_t* const bc = cbr + ctx * kBrStride;
                 for (int idx = 0; idx < kCoeffBaseRange / (kBrCdfSize - 1); idx++) {
-                    int mag = 0;  // levels here are at most 15 = COEFF_BASE_RANGE + NUM_BASE_LEVELS + 1
-                    for (int k = 0; k < 3; k++) mag += lp[magOff[k]];
-                    mag = std::min((mag + 1) >> 1, 6);
-                    int ctx;
-                    if (pos == 0) ctx = mag;
-                    else if (cls == TX_CLASS_2D) ctx = (row < 2 && col < 2) ? mag + 7 : mag + 14;
-                    else if (cls == TX_CLASS_HORIZ) ctx = col == 0 ? mag + 7 : mag + 14;
-                    else ctx = row == 0 ? mag + 7 : mag + 14;
-                    const int br = SN<4>(cdf.coef.coeff_br[std::min(txSzCtx, 3)][ptype][ctx]);
+                    const int br = SN<4>(bc);
                     level += br;
                     if (br < kBrCdfSize - 1) break;
                 }
             }
-            quant[pos] = level;
-            lvl[row * ps + col] = (uint8_t)level;
+            quant[e.pos] = level;
+            *lp = (uint16_t)(level << 8 | std::min(level, 3));
         }
-        for (int c = 0; c < eob; c++) {  // back to all zero for the next transform block
-            const int pos = scan[c];
-            lvl[(pos >> bwl) * ps + (pos & (width - 1))] = 0;
-        }
+        for (int c = 0; c < eob; c++) lvl[se[c].pad] = 0;  // back to all zero for the next transform block
         (void)height;
         PROF_T(c3);
         PROF_ADD(6, c2, c3);
-        // signs and Golomb remainders, in scan order
+        // signs and Golomb remainders, in scan order; the non-zero positions also into a
+        // bitmap of rows (the packing below walks only them)
+        const int twl = av1r_tx_w_log2[txSz] < 5 ? av1r_tx_w_log2[txSz] : 5;  // log2(tw)
+        uint32_t nzRow[32] = {};
         for (int c = 0; c < eob; c++) {
-            const int pos = scan[c];
+            const int pos = se[c].pos;
             bool sign = false;
             if (quant[pos]) {
                 if (c == 0) {
@@ -2314,6 +2352,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 quant[pos] = (int16_t)((int16_t)x + kCoeffBaseRange + kNumBaseLevels);
             }
             if (pos == 0 && quant[pos] > 0) dcCategory = sign ? 1 : 2;
+            if (quant[pos]) nzRow[pos >> twl] |= 1u << (pos & (tw - 1));
             culLevel += quant[pos];
             if (sign) quant[pos] = -quant[pos];
         }
@@ -2327,20 +2366,13 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         PROF_T(c4);
         PROF_ADD(7, c3, c4);
         // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j, in
-        // raster order over the bounding box of the scanned positions, which is cleared again
+        // raster order (the rows' bitmaps, lowest bit first), cleared again
         std::vector<uint32_t>& out = T.coefs;
-        int maxI = 0, maxJ = 0;
-        const int twl = av1r_tx_w_log2[txSz] < 5 ? av1r_tx_w_log2[txSz] : 5;  // log2(tw)
-        for (int c = 0; c < eob; c++) {
-            const int pos = scan[c];
-            maxI = std::max(maxI, pos >> twl);
-            maxJ = std::max(maxJ, pos & (tw - 1));
-        }
-        for (int i = 0; i <= maxI; i++) {
+        for (int i = 0; i < 32; i++) {
             int* row = &quant[i * tw];
-            for (int j = 0; j <= maxJ; j++) {
+            for (uint32_t m = nzRow[i]; m; m &= m - 1) {
+                const int j = __builtin_ctz(m);
                 const int v = row[j];
-                if (!v) continue;
                 row[j] = 0;
                 if (v >= (1 << 21) || v < -(1 << 21)) {
                     T.fail(AV1R_E_UNSUPPORTED, "coefficient out of packable range");
@@ -2350,6 +2382,12 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             }
         }
         t.coef_cnt = (uint32_t)out.size() - t.coef_off;
+#ifdef AV1P_PROF
+        {
+            PROF_T(c6);
+            PROF_ADD(8, c4, c6);
+        }
+#endif
         if (!t.coef_cnt) {
             T.fail(AV1R_E_INVALID, "transform block with eob %d and no non-zero coefficient", eob);
             return 0;
@@ -2358,7 +2396,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
 #ifdef AV1P_PROF
     {
         PROF_T(c5);
-        PROF_ADD(8, c0, c5);  // (head, eob: below)
+        PROF_ADD(9, c0, c5);
     }
 #endif
     std::fill_n(&T.above_level[plane][x4], w4, (int16_t)culLevel);
@@ -2532,11 +2570,13 @@ void BlockParser::emit(Blk& b)
         }
         for (int i = 0; i < stepY; i++)
             for (int j = 0; j < stepX; j++) {
-                for (int xx = 0; xx <= sub; xx++)
-                    for (int yy = 0; yy <= sub; yy++) {
-                        const int rr = row + (i << sub) + yy, cc = col + (j << sub) + xx;
-                        if (rr < fh.aligned_mi_rows && cc < fh.aligned_mi_cols) mi(rr, cc).lf_tx[plane] = (uint8_t)t.tx;
-                    }
+                // (the loop filter's transform sizes: only the emitted mode-info grid reads them)
+                if (P.emit_mi)
+                    for (int xx = 0; xx <= sub; xx++)
+                        for (int yy = 0; yy <= sub; yy++) {
+                            const int rr = row + (i << sub) + yy, cc = col + (j << sub) + xx;
+                            if (rr < fh.aligned_mi_rows && cc < fh.aligned_mi_cols) mi(rr, cc).lf_tx[plane] = (uint8_t)t.tx;
+                        }
                 T.decoded[plane][(sbRow >> sub) + i + 1][(sbCol >> sub) + j + 1] = 1;
             }
     }

@@ -58,6 +58,23 @@ int TileCtx::fail(int code, const char* fmt, ...)
 Parser::~Parser()
 {
     for (TileCtx* t : par_tiles) delete t;
+    for (Frame* f : spare) delete f;
+}
+
+Frame* Parser::take_frame()
+{
+    if (spare.empty()) return new Frame;
+    Frame* f = spare.back();
+    spare.pop_back();
+    f->blocks.clear();
+    f->mi.clear();
+    f->tbs.clear();
+    f->coefs.clear();
+    f->palette.clear();
+    f->cdef.clear();
+    f->lr.clear();
+    memset(&f->batch, 0, sizeof(f->batch));
+    return f;
 }
 
 int Parser::fail(int code, const char* fmt, ...)
@@ -927,7 +944,7 @@ void Parser::start_frame()
         memset(&u, 0, sizeof(u));
         lr_units.insert(lr_units.end(), (size_t)fh.lr_unit_rows[p] * fh.lr_unit_cols[p], u);
     }
-    cur = new Frame;
+    cur = take_frame();
     memset(&cur->hdr, 0, sizeof(cur->hdr));
     fill_header(cur->hdr);
 }
@@ -1075,7 +1092,7 @@ void Parser::reference_update()  // Parser::finishFrame (Parser.cpp:1784-1818)
 // show_existing_frame (spec 7.21 reference frame loading; Av1Decoder.cpp:158-169)
 void Parser::show_existing()
 {
-    Frame* F = new Frame;
+    Frame* F = take_frame();
     memset(&F->hdr, 0, sizeof(F->hdr));
     const RefSlot& r = slots[fh.frame_to_show];
     // the header the harness records for it (refdump.cpp showExisting: fillHeader only)

@@ -148,6 +148,18 @@ struct SymbolDecoder {
     void refill()
     {
         int sh = 64 - 9 - (cnt + 15);
+        if (end - p >= 8 && sh >= 0) {
+            // 8 bytes at once (big-endian): byte k to shift sh - 8k, for the nb bytes that fit
+            // whole (the next byte's bits below the last one's are masked off)
+            uint64_t w;
+            memcpy(&w, p, 8);
+            w = __builtin_bswap64(w);
+            const int nb = (sh >> 3) + 1, lo = sh - 8 * (nb - 1);
+            dif ^= (w >> (56 - sh)) & ~((1ull << lo) - 1);
+            cnt += 8 * nb;
+            p += nb;
+            return;
+        }
         for (; sh >= 0 && p < end; sh -= 8, p++) {
             dif ^= (uint64_t)*p << sh;
             cnt += 8;
@@ -478,6 +490,10 @@ public:
     std::vector<av1r_lr_unit> lr_units;  // frame order: plane 0 units, plane 1, plane 2
     int lr_off[3] = {};
     Frame* cur = nullptr;
+    // frames handed back by av1p_decode_tu's next call, reused with their vectors' capacity
+    // (a 1080p frame's records grow to ~3 MB: no reallocation and first-touch faults per frame)
+    std::vector<Frame*> spare;
+    Frame* take_frame();
 
     // ---- per tile ----
     TileCtx tile;  // the serial path's tile (and the bitstream writer's)
