@@ -31,7 +31,7 @@
 
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s);
-void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS,
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc,
     unsigned long long* trace, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
 void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
@@ -1829,10 +1829,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         }
         // one grid for every inter tile (k_inter_all; AV1R_INTER_MERGED=0: the three kernels)
         static const bool merged = !getenv("AV1R_INTER_MERGED") || atoi(getenv("AV1R_INTER_MERGED")) != 0;
-        auto pad8 = [](uint32_t v) { return (v + 7) & ~7u; };
+        // AV1R_INTER_CHUNKS: chunks per XCD of each class (k_inter_all's inter_deal; 1 = one
+        // contiguous eighth each)
+        static const uint32_t kc = getenv("AV1R_INTER_CHUNKS") ? (uint32_t)std::max(1, atoi(getenv("AV1R_INTER_CHUNKS"))) : 1u;
+        auto pad8 = [](uint32_t v) { return (v + 8 * kc - 1) / (8 * kc) * (8 * kc); };
         if (merged && !aux) {
             if (total[0] + total[1] + total[2])
-                launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), trace, st);
+                launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), kc, trace, st);
         } else {
             if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, sp);
             if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, sp);

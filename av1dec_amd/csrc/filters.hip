@@ -14,6 +14,7 @@
 //           (:284-479) with the stripe/unit geometry of :33-189; the 3-pixel border
 //           extension (:196-198) is coordinate clamping.
 #include <algorithm>
+#include <cstdlib>
 
 #include "av1r_dev.h"
 
@@ -410,9 +411,11 @@ extern "C" __global__ __launch_bounds__(256) void k_lfcode(const KParams* kps)
 }
 
 // one lane per (plane, 4x4 unit) edge of pass `pass`
-DEV void lf_body(const KParams* kps, int pass)
+DEV void lf_body(const KParams* kps, int pass, int perFrame)
 {
-    const uint3 wg = xcd_block();
+    // (perFrame: every XCD takes an eighth of every frame's units instead of a contiguous
+    // eighth of the whole launch, i.e. about one frame each; the frames differ in cost)
+    const uint3 wg = perFrame ? make_uint3(xcd_order(blockIdx.x, gridDim.x), blockIdx.y, 0) : xcd_block();
     const KParams& k = KP(kps, wg.y);  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
     if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
@@ -444,7 +447,7 @@ DEV void lf_body(const KParams* kps, int pass)
     lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
-extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
+extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass, int perFrame) { lf_body(kps, pass, perFrame); }
 
 // ------------------------------------------------------------------------------------
 // k_deblock: both deblocking passes of one 64x64 luma tile and its two 32x32 chroma tiles
@@ -794,10 +797,10 @@ DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int 
 }
 
 // grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.dbk, writes k.cdef
-DEV void cdef_body(const KParams* kps)
+DEV void cdef_body(const KParams* kps, int perFrame)
 {
     __shared__ CdefLds L;
-    const uint3 wg = xcd_block();
+    const uint3 wg = perFrame ? xcd_block_xy() : xcd_block();  // (as lf_body)
     const KParams& k = KP(kps, wg.z);
     const int t = threadIdx.x;
     const int r0 = wg.y * 16, c0 = wg.x * 16;  // mi units
@@ -982,7 +985,7 @@ DEV void cdef_body(const KParams* kps)
     }
 }
 // (6 waves per SIMD instead of 5 measured no faster: the filters are not occupancy-bound)
-extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps) { cdef_body(kps); }
+extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps, int perFrame) { cdef_body(kps, perFrame); }
 
 // ------------------------------------------------------------------------------------
 // Loop restoration
@@ -1544,9 +1547,15 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 
 // ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
+// AV1R_FILT_XCD=1: k_lf and k_cdef deal every frame over the XCDs (lf_body)
+static int filt_per_frame()
+{
+    static const int v = getenv("AV1R_FILT_XCD") ? atoi(getenv("AV1R_FILT_XCD")) : 0;
+    return v;
+}
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
+    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass, filt_per_frame());
 }
 void launch_k_lfcode(const KParams* kps, int n, int maxUnits, hipStream_t s)
 {
@@ -1558,7 +1567,7 @@ void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t
 }
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
+    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps, filt_per_frame());
 }
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {

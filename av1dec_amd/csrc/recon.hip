@@ -1624,8 +1624,17 @@ extern "C" __global__ K_PLAIN_BOUNDS void k_inter_m(const KParams* kps, const ui
 // every logical index is run by exactly one workgroup wherever it lands.
 // tab: [k_inter table][k_inter_m table][k_inter_s table] (launch_jobs); gI / gM / gS the classes'
 // padded workgroup counts.
+// kc (>= 1): each class is cut into 8 * kc chunks, chunk c to XCD c % 8 -- kc = 1 gives every
+// XCD one contiguous eighth; larger kc mixes several frames' regions into each XCD's share
+// (a batch's frames differ in cost) while a chunk keeps its neighbouring tiles on one L2.
+// The class counts are padded to multiples of 8 * kc.
+DEV uint32_t inter_deal(uint32_t x, uint32_t j, uint32_t q, uint32_t kc)
+{
+    const uint32_t C = q / kc, kk = j / C;  // chunk size (workgroups), this XCD's chunk number
+    return (kk * 8 + x) * C + (j - kk * C);
+}
 extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const uint32_t* __restrict__ tab, int n,
-    uint32_t gI, uint32_t gM, uint32_t gS, unsigned long long* trace)
+    uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc, unsigned long long* trace)
 {
     union Lds {
         InterLds g;
@@ -1639,13 +1648,13 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const 
     const uint32_t* tM = tI + 2 * n + 1;
     const uint32_t* tS = tM + 3 * n + 1;
     if (j < qI) {
-        const uint32_t b = x * qI + j;
+        const uint32_t b = inter_deal(x, j, qI, kc);
         if (b < tI[n]) inter_general(kps, tI, n, b, L.g, trace, ~0u);
     } else if (j < qI + qM) {
-        const uint32_t b = x * qM + (j - qI);
+        const uint32_t b = inter_deal(x, j - qI, qM, kc);
         if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m);
     } else if (j < qI + qM + qS) {
-        const uint32_t b = x * qS + (j - qI - qM);
+        const uint32_t b = inter_deal(x, j - qI - qM, qS, kc);
         if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s);
     }
 }
@@ -2027,10 +2036,10 @@ void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, u
 
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4);
 // kind 2 / 3: medium / small plain inter blocks, `items` groups of two / four
-void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS,
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc,
     unsigned long long* trace, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, trace);
+    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, kc, trace);
 }
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
