@@ -286,20 +286,20 @@ struct LfLdsPx {
     DEV void st16(int x, int y, uint32_t v) const { *reinterpret_cast<lf_lds_u16*>(at(x, y)) = (uint16_t)v; }
     DEV void st8(int x, int y, uint32_t v) const { *at(x, y) = (uint8_t)v; }
 };
+// lf_unit_d: the unit filtered from its samples already loaded, dd[16]: pass 0 row i's dwords
+// at x - 8, x - 4, x, x + 4 in dd[4i .. 4i + 3]; pass 1 the dword of row y - 8 + r in dd[r]
+// (the outer ones only read by a 16-wide filter)
 template <class PX>
-DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e)
+DEV void lf_unit_d(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e, const uint32_t* dd)
 {
     const bool wide = e.filterSize == 16;
     const int n = wide ? 6 : (e.filterSize == 8 && !plane) ? 3 : 2;  // samples written per side
     if (pass == 0) {
         uint32_t d[4][4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            d[i][1] = P.ld32(xP - 4, yP + i);
-            d[i][2] = P.ld32(xP, yP + i);
-            d[i][0] = wide ? P.ld32(xP - 8, yP + i) : 0u;
-            d[i][3] = wide ? P.ld32(xP + 4, yP + i) : 0u;
-        }
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) d[i][j] = dd[4 * i + j];
         // rows (0, 1) and (2, 3) filtered as pairs: v[q] = the two rows' samples at x - 8 + q
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -338,12 +338,7 @@ DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge&
         }
         return;
     }
-    uint32_t d[16];
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const bool need = (r >= 4 && r < 12) || wide;
-        d[r] = need ? P.ld32(xP, yP - 8 + r) : 0u;
-    }
+    const uint32_t* d = dd;
     // columns (0, 1) and (2, 3) filtered as pairs
     lf2 lo[16], hi[16];
 #pragma unroll
@@ -358,6 +353,23 @@ DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge&
         if (r >= 8 - n && r < 8 + n)
             P.st32(xP, yP - 8 + r,
                 __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u));
+}
+// the unit's samples (the outer ones for a 16-wide filter only), then lf_unit_d
+template <class PX>
+DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e)
+{
+    const bool wide = e.filterSize == 16;
+    uint32_t d[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        if (pass == 0) {
+            const int i = r >> 2, j = r & 3;
+            d[r] = (j == 1 || j == 2 || wide) ? P.ld32(xP - 8 + 4 * j, yP + i) : 0u;
+        } else {
+            d[r] = ((r >= 4 && r < 12) || wide) ? P.ld32(xP, yP - 8 + r) : 0u;
+        }
+    }
+    lf_unit_d(P, plane, pass, xP, yP, e, d);
 }
 
 // an edge decision as one byte: the level (1..63) and the filter size (4 / 8 / 16 as 0 / 1 / 2
@@ -439,12 +451,29 @@ DEV void lf_body(const KParams* kps, int pass, int perFrame)
     }
     const int sub = plane ? 1 : 0;
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
+    // the unit's samples loaded before its edge decision (speculatively: the decision's
+    // mode-info loads and these go out together, one memory round trip instead of two); the
+    // outer dwords only where a 16-wide (luma) filter could run, and nothing left of x = 4 /
+    // above y = 4, where no edge is filtered
+    const DevPlane& P = k.cur.pl[plane];
+    const LfGlobalPx G{P.p, P.stride};
+    const int pos = pass ? yP : xP;
+    const bool inner = pos >= 4, outer = !plane && pos >= 8;
+    uint32_t d[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        if (pass == 0) {
+            const int i = r >> 2, j = r & 3;
+            d[r] = ((j == 1 || j == 2) ? inner : outer) ? G.ld32(xP - 8 + 4 * j, yP + i) : 0u;
+        } else {
+            d[r] = ((r >= 4 && r < 12) ? inner : outer) ? G.ld32(xP, yP - 8 + r) : 0u;
+        }
+    }
     // the edge's decision from the mode info, in the lane (k_lfcode's bytes ahead of the
     // launch measured slower here: 0.0116 against 0.0108 ms per 1080p frame with its launch)
     LfEdge e;
     if (!lf_edge(k, plane, pass, xP, yP, e)) return;
-    const DevPlane& P = k.cur.pl[plane];
-    lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
+    lf_unit_d(G, plane, pass, xP, yP, e, d);
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass, int perFrame) { lf_body(kps, pass, perFrame); }
@@ -825,6 +854,15 @@ DEV void cdef_body(const KParams* kps, int perFrame)
         }
         return;
     }
+    // cdef_block's skip test (Cdef.cpp:79-82) per 8x8 block, its mode-info loads issued with
+    // the pixel loads below (one memory round trip for both)
+    int fBlk = 0;
+    if (t < 64) {
+        const int br = r0 + (t >> 3) * 2, bc = c0 + (t & 7) * 2;
+        if ((t >> 3) * 2 < rows4 && (t & 7) * 2 < cols4)
+            fBlk = !((mi_at(k, br, bc).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc).flags & AV1R_MI_SKIP)
+                && (mi_at(k, br, bc + 1).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc + 1).flags & AV1R_MI_SKIP));
+    }
     const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
     const bool edge = x0 < CD_H || y0 < CD_H || x0 + 64 + CD_H > limX || y0 + 64 + CD_H > limY;
     const int cx0 = x0 / 2, cy0 = y0 / 2, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
@@ -867,16 +905,7 @@ DEV void cdef_body(const KParams* kps, int perFrame)
         cd_stage(&L.uv[0][0][0], CD_CS, CD_CR, k.dbk.pl[1], cx0, cy0, cedge, climX - 1, climY - 1);
         cd_stage(&L.uv[1][0][0], CD_CS, CD_CR, k.dbk.pl[2], cx0, cy0, cedge, climX - 1, climY - 1);
     }
-    if (t < 64) {
-        const int br = r0 + (t >> 3) * 2, bc = c0 + (t & 7) * 2;
-        int f = 0;
-        if ((t >> 3) * 2 < rows4 && (t & 7) * 2 < cols4) {
-            // cdef_block's skip test (Cdef.cpp:79-82)
-            f = !((mi_at(k, br, bc).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc).flags & AV1R_MI_SKIP)
-                && (mi_at(k, br, bc + 1).flags & AV1R_MI_SKIP) && (mi_at(k, br + 1, bc + 1).flags & AV1R_MI_SKIP));
-        }
-        L.filt[t] = (uint8_t)f;
-    }
+    if (t < 64) L.filt[t] = (uint8_t)fBlk;
     __syncthreads();
     // direction costs: wave w (wave-uniform directions 2w and 2w + 1), lane = 8x8 block; the
     // block's 64 pixels read once as 16 dwords and kept in registers for both directions
