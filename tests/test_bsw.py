@@ -165,3 +165,29 @@ def test_gpu_native_pipeline_ivf_matches_reference_md5(native_lib):
     finally:
         for d in decs:
             d.close()
+
+
+def test_flow_schedules_hold_their_invariants():
+    """Every packed frame of five writer streams (av1r_pack, the pipeline's flow-only
+    schedule) through the host-side schedule check (AV1R_SCHED_CHECK=1, schedule_check in
+    av1r_host.cpp): indices in range, every listed or edge-granule dependency in an earlier
+    k_flow group, residual tiles inside the residual buffer.  Host only."""
+    code = (
+        "import sys, ctypes as C\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tools', 'bsw')!r})\n"
+        "import pybsw, json\n"
+        "from av1dec_amd import native, parser\n"
+        "l = native.lib()\n"
+        f"gold = json.load(open({os.path.join(ROOT, 'tests', 'golden', 'bsw.json')!r}))\n"
+        "for n in ['cif_s1', '640x360_tiles2x2_sb64', 'odd_416x234_key3', 'cif_hidden', 'cif_gm_affine_sb64']:\n"
+        "    for f in parser.Parser(mode_info=False).decode_ivf(pybsw.stream_ivf(n, seed=gold[n]['seed'])):\n"
+        "        pk = C.c_void_p()\n"
+        "        assert l.av1r_pack(C.cast(f.byref(), C.c_void_p), C.byref(pk)) == 0\n"
+        "        l.av1r_packed_free(pk)\n")
+    env = dict(os.environ, AV1R_SCHED_CHECK="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stderr.splitlines() if x.startswith("av1r sched check:")]
+    summaries = [x for x in lines if "violations" in x]
+    assert summaries, r.stderr[-2000:]
+    assert all(x.endswith(" 0 violations") for x in summaries), "\n".join(lines[:30])
