@@ -1568,10 +1568,96 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int 
     coop_sync<NT>();  // the next unit reuses the windows
 }
 
+// Both chroma planes of a block whose chroma is ONE prediction unit (the usual case): U and V
+// share the unit's motion, filters and window geometry, so their windows -- two planes x up
+// to two references -- go out in one memory round trip (per plane, small_pu costs one each),
+// then the passes run over both.  The windows and intermediates are laid over the group's
+// SmallLds (4 windows of (MS/2 + 7) x (MS/2 + 8) bytes, then 4 intermediates).
+template <int NT, int MS>
+DEV void small_pu_c2(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int x, int y, int w, int h, int candRow,
+    int candCol)
+{
+    constexpr int CS = MS / 2, WS = CS + 8, WSZ = (CS + 7) * WS, HSZ = (CS + 7) * CS;
+    constexpr int WALL = (4 * WSZ + 7) & ~7;
+    static_assert(WALL + 4 * HSZ * 2 <= sizeof(SmallLds<MS>), "chroma pair windows exceed the group's LDS");
+    uint8_t* win = reinterpret_cast<uint8_t*>(&L);
+    int16_t* hb = reinterpret_cast<int16_t*>(win + WALL);
+    const int t = threadIdx.x & (NT - 1);
+    const int ct = blk.compound_type;
+    const PuInfo info = pu_info(k, blk, candRow, candCol);
+    const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
+    int16_t hf[2][8], vf[2][8];
+    int integer[2] = {1, 1};
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+        if (l > isCompound) break;
+        const int slot = k.hdr->ref_frame_idx[info.ref_frame[l] - 1];
+        RefSel R;
+        select_ref(k, R, slot, 1, x, y, info.mv[l]);
+        const int fx = filter_idx(info.filt, w, 1), fy = filter_idx(info.filt, h, 0);
+        const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
+        integer[l] = !hph && !vph;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            hf[l][u] = av1r_subpel_filters[(fx * 16 + hph) * 8 + u];
+            vf[l][u] = av1r_subpel_filters[(fy * 16 + vph) * 8 + u];
+        }
+        load_window<NT, CS>(R, win + l * WSZ, 0, 0, w, h, WS);
+        R.p = k.ref[slot].pl[2];  // V: the same extent as U
+        load_window<NT, CS>(R, win + (2 + l) * WSZ, 0, 0, w, h, WS);
+    }
+    coop_sync<NT>();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int l = q & 1;
+        if (l <= isCompound && !integer[l]) hpass<NT>(win + q * WSZ, hb + q * HSZ, w, h, hf[l], 3, WS, CS);
+    }
+    coop_sync<NT>();
+    const int R1 = isCompound ? 7 : 11, PostRound = 14 - (3 + R1);
+    int fwd = 0, bck = 0;
+    const int dist = isCompound && ct == AV1R_COMPOUND_DISTANCE;
+    if (dist) distance_weights(k, info, fwd, bck);
+    auto blend = [&](int p0, int p1) {
+        return !isCompound ? clip1(p0)
+             : dist        ? clip1(r2(fwd * p0 + bck * p1, 4 + PostRound))
+                           : clip1(r2(p0 + p1, 1 + PostRound));
+    };
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+        const DevPlane& dst = k.cur.pl[1 + p];
+        const uint8_t* w0 = win + (2 * p) * WSZ;
+        const uint8_t* w1 = win + (2 * p + 1) * WSZ;
+        const int16_t* h0 = hb + (2 * p) * HSZ;
+        const int16_t* h1 = hb + (2 * p + 1) * HSZ;
+        if (!(w & 3)) {
+            const int g4 = w >> 2, lg = ilog2p(g4);
+            for (int q = t; q < h * g4; q += NT) {
+                const int rr = q >> lg, cc = (q & (g4 - 1)) * 4;
+                int p0[4], p1[4] = {0, 0, 0, 0};
+                pred_win4(w0, h0, rr, cc, 3, R1, vf[0], integer[0], p0, WS, CS);
+                if (isCompound) pred_win4(w1, h1, rr, cc, 3, R1, vf[1], integer[1], p1, WS, CS);
+                uint32_t v = 0;
+#pragma unroll
+                for (int m = 0; m < 4; m++) v |= (uint32_t)blend(p0[m], p1[m]) << (8 * m);
+                *reinterpret_cast<uint32_t*>(&px(dst, x + cc, y + rr)) = v;
+            }
+        } else {
+            const int lw = ilog2p(w);
+            for (int q = t; q < h * w; q += NT) {
+                const int rr = q >> lw, cc = q & (w - 1);
+                const int p0 = pred_win(w0, h0, rr, cc, 3, R1, vf[0], integer[0], WS, CS);
+                const int p1 = isCompound ? pred_win(w1, h1, rr, cc, 3, R1, vf[1], integer[1], WS, CS) : 0;
+                px(dst, x + cc, y + rr) = (uint8_t)blend(p0, p1);
+            }
+        }
+    }
+    coop_sync<NT>();  // the next block's units reuse the LDS
+}
+
 // Frames' lists are dealt in groups of 64 / NT (a frame's last group may be partial), so
 // the parameters of a workgroup stay uniform.  tab: [group prefix (n + 1)][offsets (n)][counts (n)].
 template <int NT, int MS>
-DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, SmallLds<MS>* L)
+DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, SmallLds<MS>* L, int chroma2 = 1)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
@@ -1585,6 +1671,10 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
     for (int plane = 0; plane < nPl; plane++) {
         // (sub-8x8 chroma may gather up to four units of neighbouring blocks)
         const PlaneGeo G = plane_geo<MS>(k, blk, plane, 0, 0);
+        if (plane == 1 && chroma2 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col) {
+            small_pu_c2<NT, MS>(k, L[g], blk, G.baseX, G.baseY, G.pw, G.ph, G.candRow, G.candCol);
+            break;
+        }
         int r = 0;
         for (int yy = 0; yy < G.ph; yy += G.predH, r++) {
             int c = 0;
@@ -1634,7 +1724,7 @@ DEV uint32_t inter_deal(uint32_t x, uint32_t j, uint32_t q, uint32_t kc)
     return (kk * 8 + x) * C + (j - kk * C);
 }
 extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const uint32_t* __restrict__ tab, int n,
-    uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc, unsigned long long* trace)
+    uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc, int c2, unsigned long long* trace)
 {
     union Lds {
         InterLds g;
@@ -1652,10 +1742,10 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const 
         if (b < tI[n]) inter_general(kps, tI, n, b, L.g, trace, ~0u);
     } else if (j < qI + qM) {
         const uint32_t b = inter_deal(x, j - qI, qM, kc);
-        if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m);
+        if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m, c2);
     } else if (j < qI + qM + qS) {
         const uint32_t b = inter_deal(x, j - qI - qM, qS, kc);
-        if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s);
+        if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s, c2);
     }
 }
 
@@ -2039,7 +2129,9 @@ void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, u
 void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc,
     unsigned long long* trace, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, kc, trace);
+    // AV1R_CHROMA2=0: plain blocks' chroma planes one after the other (small_pu per plane)
+    static const int c2 = getenv("AV1R_CHROMA2") ? atoi(getenv("AV1R_CHROMA2")) : 1;
+    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, kc, c2, trace);
 }
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)
