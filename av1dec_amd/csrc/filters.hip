@@ -451,29 +451,14 @@ DEV void lf_body(const KParams* kps, int pass, int perFrame)
     }
     const int sub = plane ? 1 : 0;
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
-    // the unit's samples loaded before its edge decision (speculatively: the decision's
-    // mode-info loads and these go out together, one memory round trip instead of two); the
-    // outer dwords only where a 16-wide (luma) filter could run, and nothing left of x = 4 /
-    // above y = 4, where no edge is filtered
-    const DevPlane& P = k.cur.pl[plane];
-    const LfGlobalPx G{P.p, P.stride};
-    const int pos = pass ? yP : xP;
-    const bool inner = pos >= 4, outer = !plane && pos >= 8;
-    uint32_t d[16];
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        if (pass == 0) {
-            const int i = r >> 2, j = r & 3;
-            d[r] = ((j == 1 || j == 2) ? inner : outer) ? G.ld32(xP - 8 + 4 * j, yP + i) : 0u;
-        } else {
-            d[r] = ((r >= 4 && r < 12) ? inner : outer) ? G.ld32(xP, yP - 8 + r) : 0u;
-        }
-    }
     // the edge's decision from the mode info, in the lane (k_lfcode's bytes ahead of the
-    // launch measured slower here: 0.0116 against 0.0108 ms per 1080p frame with its launch)
+    // launch measured slower here: 0.0116 against 0.0108 ms per 1080p frame with its launch;
+    // the unit's samples loaded speculatively with the mode info, before the decision:
+    // 0.0119 against 0.0105, profiles/r05_ab_lf_spec.txt -- most units filter nothing)
     LfEdge e;
     if (!lf_edge(k, plane, pass, xP, yP, e)) return;
-    lf_unit_d(G, plane, pass, xP, yP, e, d);
+    const DevPlane& P = k.cur.pl[plane];
+    lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass, int perFrame) { lf_body(kps, pass, perFrame); }

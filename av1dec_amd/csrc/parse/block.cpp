@@ -303,30 +303,7 @@ private:
     // coefficient levels while parsing them, padded (coeffs()): level << 8 | min(level, 3)
     uint16_t lvl[36 * 36] = {};
 
-    // every alphabet size through the unrolled, branch-free readN (the generic read's interval
-    // search exits early, a data-dependent branch per boundary); n is a constant at most call
-    // sites, so the switch folds away
-    __attribute__((always_inline)) int S(uint16_t* c, int n)
-    {
-        switch (n) {
-        case 2: return sd.readN<2>(c);
-        case 3: return sd.readN<3>(c);
-        case 4: return sd.readN<4>(c);
-        case 5: return sd.readN<5>(c);
-        case 6: return sd.readN<6>(c);
-        case 7: return sd.readN<7>(c);
-        case 8: return sd.readN<8>(c);
-        case 9: return sd.readN<9>(c);
-        case 10: return sd.readN<10>(c);
-        case 11: return sd.readN<11>(c);
-        case 12: return sd.readN<12>(c);
-        case 13: return sd.readN<13>(c);
-        case 14: return sd.readN<14>(c);
-        case 15: return sd.readN<15>(c);
-        case 16: return sd.readN<16>(c);
-        default: return sd.read(c, n);
-        }
-    }
+    int S(uint16_t* c, int n) { return sd.read(c, n); }  // (every size through readN: 20.27 -> 20.45 ms/frame, r05_ab_lf_spec.txt)
     template <int N>
     int SN(uint16_t* c) { return sd.readN<N>(c); }
     uint32_t L(int n) { return sd.literal(n); }
