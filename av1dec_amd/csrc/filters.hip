@@ -286,20 +286,20 @@ struct LfLdsPx {
     DEV void st16(int x, int y, uint32_t v) const { *reinterpret_cast<lf_lds_u16*>(at(x, y)) = (uint16_t)v; }
     DEV void st8(int x, int y, uint32_t v) const { *at(x, y) = (uint8_t)v; }
 };
-// lf_unit_d: the unit filtered from its samples already loaded, dd[16]: pass 0 row i's dwords
-// at x - 8, x - 4, x, x + 4 in dd[4i .. 4i + 3]; pass 1 the dword of row y - 8 + r in dd[r]
-// (the outer ones only read by a 16-wide filter)
 template <class PX>
-DEV void lf_unit_d(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e, const uint32_t* dd)
+DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e)
 {
     const bool wide = e.filterSize == 16;
     const int n = wide ? 6 : (e.filterSize == 8 && !plane) ? 3 : 2;  // samples written per side
     if (pass == 0) {
         uint32_t d[4][4];
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) d[i][j] = dd[4 * i + j];
+        for (int i = 0; i < 4; i++) {
+            d[i][1] = P.ld32(xP - 4, yP + i);
+            d[i][2] = P.ld32(xP, yP + i);
+            d[i][0] = wide ? P.ld32(xP - 8, yP + i) : 0u;
+            d[i][3] = wide ? P.ld32(xP + 4, yP + i) : 0u;
+        }
         // rows (0, 1) and (2, 3) filtered as pairs: v[q] = the two rows' samples at x - 8 + q
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -338,7 +338,12 @@ DEV void lf_unit_d(const PX& P, int plane, int pass, int xP, int yP, const LfEdg
         }
         return;
     }
-    const uint32_t* d = dd;
+    uint32_t d[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const bool need = (r >= 4 && r < 12) || wide;
+        d[r] = need ? P.ld32(xP, yP - 8 + r) : 0u;
+    }
     // columns (0, 1) and (2, 3) filtered as pairs
     lf2 lo[16], hi[16];
 #pragma unroll
@@ -353,23 +358,6 @@ DEV void lf_unit_d(const PX& P, int plane, int pass, int xP, int yP, const LfEdg
         if (r >= 8 - n && r < 8 + n)
             P.st32(xP, yP - 8 + r,
                 __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u));
-}
-// the unit's samples (the outer ones for a 16-wide filter only), then lf_unit_d
-template <class PX>
-DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge& e)
-{
-    const bool wide = e.filterSize == 16;
-    uint32_t d[16];
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        if (pass == 0) {
-            const int i = r >> 2, j = r & 3;
-            d[r] = (j == 1 || j == 2 || wide) ? P.ld32(xP - 8 + 4 * j, yP + i) : 0u;
-        } else {
-            d[r] = ((r >= 4 && r < 12) || wide) ? P.ld32(xP, yP - 8 + r) : 0u;
-        }
-    }
-    lf_unit_d(P, plane, pass, xP, yP, e, d);
 }
 
 // an edge decision as one byte: the level (1..63) and the filter size (4 / 8 / 16 as 0 / 1 / 2
