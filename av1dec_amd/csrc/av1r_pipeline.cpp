@@ -58,7 +58,7 @@ struct Run {
     const av1r_stream_source* src = nullptr;
     int64_t maxFrames = 0;
     int depth = 3;
-    bool stable = false;
+    bool stable = false;  // src->stable != 0: the next fetch of a stream may overlap this pack
     std::atomic<bool> stop{false};
     std::mutex m;  // guards every StreamQ's bookkeeping (operations are tiny)
     std::condition_variable work, ready;
@@ -107,6 +107,10 @@ void worker(Run* R)
         const auto t1 = Clock::now();
         double packS = 0;
         bool released = false;
+        // (stable 2: the batch goes back to the source once packed)
+        auto giveBack = [&]() {
+            if (R->src->stable == 2 && R->src->release && rc == 0 && b) R->src->release(R->src->user, s, b);
+        };
         if (rc == 0 && b && b->hdr && !b->hdr->show_existing_frame) {
             if (R->stable) {  // the batch outlives the next fetch: let another worker fetch
                 l.lock();
@@ -116,6 +120,7 @@ void worker(Run* R)
                 released = true;
             }
             const int pr = av1r_pack(b, &e.p);
+            giveBack();
             packS = secs(Clock::now() - t1);
             if (pr) {
                 e.kind = 3;
@@ -129,6 +134,7 @@ void worker(Run* R)
             e.kind = 1;
             e.show = b->hdr->frame_to_show;
             e.refresh = b->hdr->refresh_frame_flags;
+            giveBack();
         } else if (rc == 1) {
             e.kind = 2;
         } else {
@@ -148,14 +154,24 @@ void worker(Run* R)
 }
 
 // ---- built-in sources ----
+// The IVF source keeps two generations of parsed frames (av1p_set_frame_generations): the
+// frames of unit g stay valid while unit g + 1 is parsed, and before unit g + 2 is parsed
+// (which recycles unit g's) every frame of unit g must be back (release): the next frame's
+// parse runs while the pipeline packs this one (av1r_stream_source.stable = 2).
 struct IvfStream {
     const uint8_t* data = nullptr;
     size_t size = 0, pos = 32;
     av1p_ctx* parser = nullptr;
     int have = 0, next = 0;  // frames of the last unit, the next one to hand out
+    int64_t gen = 0;         // units parsed
+    int out[2] = {0, 0};     // frames of unit gen - 1 / gen still held by the pipeline (by gen & 1)
+    std::vector<std::pair<const av1r_frame_batch*, int64_t>> held;  // frames handed out, their unit
+    std::mutex m;
+    std::condition_variable back;
 };
 struct IvfSource {
     std::vector<IvfStream> st;
+    explicit IvfSource(int n) : st(n) {}
 };
 
 int ivf_next(void* user, int s, const av1r_frame_batch** out)
@@ -166,15 +182,39 @@ int ivf_next(void* user, int s, const av1r_frame_batch** out)
         const uint32_t sz = S.data[S.pos] | S.data[S.pos + 1] << 8 | S.data[S.pos + 2] << 16 | (uint32_t)S.data[S.pos + 3] << 24;
         S.pos += 12;
         if (S.pos + sz > S.size) return AV1R_E_INVALID;
+        {  // parsing unit gen + 1 recycles unit gen - 1's frames: all of them back first
+            std::unique_lock<std::mutex> l(S.m);
+            S.back.wait(l, [&] { return S.out[(S.gen + 1) & 1] == 0; });
+        }
         int n = 0;
         const int rc = av1p_decode_tu(S.parser, S.data + S.pos, sz, &n);
         S.pos += sz;
         if (rc) return rc;
+        S.gen++;
         S.have = n;
         S.next = 0;
     }
-    *out = av1p_frame(S.parser, S.next++);
+    const av1r_frame_batch* b = av1p_frame(S.parser, S.next++);
+    {
+        std::lock_guard<std::mutex> l(S.m);
+        S.out[S.gen & 1]++;
+        S.held.push_back({b, S.gen});
+    }
+    *out = b;
     return 0;
+}
+
+void ivf_release(void* user, int s, const av1r_frame_batch* b)
+{
+    IvfStream& S = ((IvfSource*)user)->st[s];
+    std::lock_guard<std::mutex> l(S.m);
+    for (size_t i = 0; i < S.held.size(); i++)
+        if (S.held[i].first == b) {
+            S.out[S.held[i].second & 1]--;
+            S.held.erase(S.held.begin() + i);
+            S.back.notify_all();
+            return;
+        }
 }
 
 }  // namespace
@@ -195,9 +235,8 @@ int av1r_cycle_next(void* user, int stream, const av1r_frame_batch** batch)
 int av1r_ivf_source_create(const uint8_t* const* files, const size_t* sizes, int n, av1r_stream_source* out)
 {
     if (!files || !sizes || n <= 0 || !out) return AV1R_E_INVALID;
-    IvfSource* S = new (std::nothrow) IvfSource;
+    IvfSource* S = new (std::nothrow) IvfSource(n);
     if (!S) return AV1R_E_NOMEM;
-    S->st.resize(n);
     for (int i = 0; i < n; i++) {
         IvfStream& t = S->st[i];
         t.data = files[i];
@@ -205,6 +244,7 @@ int av1r_ivf_source_create(const uint8_t* const* files, const size_t* sizes, int
         int rc = (t.size < 32 || memcmp(t.data, "DKIF", 4)) ? AV1R_E_INVALID : av1p_create(&t.parser);
         if (!rc) t.pos = t.data[6] | t.data[7] << 8;  // header length
         if (!rc) av1p_set_mode_info(t.parser, 0);      // av1r_pack rebuilds it on the device
+        if (!rc) av1p_set_frame_generations(t.parser, 2);  // (IvfStream)
         if (rc) {
             for (auto& u : S->st)
                 if (u.parser) av1p_destroy(u.parser);
@@ -214,7 +254,8 @@ int av1r_ivf_source_create(const uint8_t* const* files, const size_t* sizes, int
     }
     out->next = ivf_next;
     out->user = S;
-    out->stable = 0;  // a unit's batches live until the parser's next unit
+    out->stable = 2;  // a unit's batches live until they are released (IvfStream)
+    out->release = ivf_release;
     return AV1R_OK;
 }
 

@@ -12,16 +12,31 @@
 struct av1p_ctx {
     av1p::Parser parser;
     std::vector<av1p::Frame*> frames;
+    std::vector<av1p::Frame*> prev;  // av1p_set_frame_generations(ctx, 2): the unit before
+    int generations = 1;
     std::string err;
-    void release()
+    void recycle(std::vector<av1p::Frame*>& v)
     {
-        for (auto* f : frames) {
+        for (auto* f : v) {
             if (parser.spare.size() < 4) parser.spare.push_back(f);  // (Parser::take_frame)
             else delete f;
         }
-        frames.clear();
+        v.clear();
     }
-    ~av1p_ctx() { release(); }
+    void release()
+    {
+        if (generations == 2) {
+            recycle(prev);
+            prev.swap(frames);
+        } else {
+            recycle(frames);
+        }
+    }
+    ~av1p_ctx()
+    {
+        recycle(prev);
+        recycle(frames);
+    }
 };
 
 extern "C" {
@@ -43,6 +58,14 @@ int av1p_set_tile_threads(av1p_ctx* ctx, int n)
 {
     if (!ctx || n < 1 || n > 64) return AV1R_E_INVALID;
     ctx->parser.tile_threads = n;
+    return AV1R_OK;
+}
+
+int av1p_set_frame_generations(av1p_ctx* ctx, int n)
+{
+    if (!ctx || n < 1 || n > 2) return AV1R_E_INVALID;
+    ctx->generations = n;
+    if (n == 1) ctx->recycle(ctx->prev);
     return AV1R_OK;
 }
 

@@ -142,12 +142,13 @@ def parser_lib():
     l.av1p_last_error.restype = C.c_char_p
     l.av1p_set_tile_threads.argtypes = [vp, C.c_int]
     l.av1p_set_mode_info.argtypes = [vp, C.c_int]
+    l.av1p_set_frame_generations.argtypes = [vp, C.c_int]
     _plib = l
     return l
 
 
 PARSE_EXPORTS = ["av1p_create", "av1p_destroy", "av1p_decode_tu", "av1p_frame", "av1p_last_error", "av1p_set_tile_threads",
-                 "av1p_set_mode_info"]
+                 "av1p_set_mode_info", "av1p_set_frame_generations"]
 
 
 _lib = None
@@ -236,7 +237,7 @@ def lib():
 
 
 class StreamSource(C.Structure):  # av1r_stream_source
-    _fields_ = [("next", C.c_void_p), ("user", C.c_void_p), ("stable", C.c_int)]
+    _fields_ = [("next", C.c_void_p), ("user", C.c_void_p), ("stable", C.c_int), ("release", C.c_void_p)]
 
 
 SINK_ACQUIRE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int))

@@ -19,6 +19,8 @@
  *                                  another, Parser::parseTileGroup, Parser.cpp:492-521)
  *   av1p_set_mode_info          -- (no counterpart: refdump.cpp fillFrameTables always
  *                                  builds the grid)
+ *   av1p_set_frame_generations  -- (no counterpart: the reference decodes a frame before
+ *                                  parsing the next)
  */
 #ifndef AV1P_H
 #define AV1P_H
@@ -49,6 +51,10 @@ int av1p_set_tile_threads(av1p_ctx* ctx, int n);
  * 0: mi is NULL. av1r_pack / av1r_decode_frame rebuild the grid on the device from the
  * block records and do not read it; av1r_frame_begin (tile-split decoding) needs it. */
 int av1p_set_mode_info(av1p_ctx* ctx, int emit);
+/* How long av1p_frame's batches stay valid: 1 (default) until the next av1p_decode_tu, 2
+ * until the one after it (the frames of the previous unit are kept alive while the next
+ * one is parsed: a consumer may still read them on another thread). */
+int av1p_set_frame_generations(av1p_ctx* ctx, int n);
 /* Message of the last failure (empty string if none). */
 const char* av1p_last_error(av1p_ctx* ctx);
 

@@ -365,8 +365,11 @@ typedef struct av1r_stream_source {
     int (*next)(void* user, int stream, const av1r_frame_batch** batch);
     void* user;
     /* 1: a returned batch stays valid until the run ends (then several frames of a stream
-     * are packed concurrently); 0: only until the next call for that stream */
+     * are packed concurrently); 0: only until the next call for that stream; 2: until the
+     * pipeline hands it back through `release` (called once per batch `next` returned, when
+     * it has been packed), so the next frame's fetch overlaps this one's packing */
     int stable;
+    void (*release)(void* user, int stream, const av1r_frame_batch* batch);  /* stable == 2 only */
 } av1r_stream_source;
 typedef struct av1r_pipeline_stats {
     uint64_t frames;   /* frames decoded (shown-existing included), all streams          */

@@ -166,3 +166,29 @@ def test_parse_without_mode_info_grid(parser_mod, name):
         for s in batchfile.SECTIONS:
             if s != "mi":
                 assert np.array_equal(f.sec[s], g.sec[s]), s
+
+
+@needs_bits
+def test_two_frame_generations_keep_the_previous_unit(parser_mod):
+    """av1p_set_frame_generations(ctx, 2): a unit's frame batches stay intact while the next
+    unit is parsed (the native IVF source packs unit g while unit g + 1 parses)."""
+    import ctypes as C
+    with open(golden.ivf_path("av1-1-b8-01-size-66x66"), "rb") as f:
+        tus = list(parser_mod.ivf_frames(f.read()))
+    l = native.parser_lib()
+    h = C.c_void_p()
+    assert l.av1p_create(C.byref(h)) == 0
+    try:
+        assert l.av1p_set_frame_generations(h, 2) == 0
+        assert l.av1p_set_frame_generations(h, 3) != 0
+        n = C.c_int()
+        prev = None
+        for tu in tus:
+            assert l.av1p_decode_tu(h, tu, len(tu), C.byref(n)) == 0
+            if prev is not None:  # the previous unit's frames, after this unit's parse
+                for ptr, frame in prev:
+                    again = parser_mod.frame_from_batch(ptr)
+                    assert all(np.array_equal(frame.sec[s], again.sec[s]) for s in batchfile.SECTIONS)
+            prev = [(p, parser_mod.frame_from_batch(p)) for p in (l.av1p_frame(h, i) for i in range(n.value))]
+    finally:
+        l.av1p_destroy(h)
