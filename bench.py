@@ -240,9 +240,12 @@ def ivf_leg(decs, streams, frames, size="1920x1080", name="1080p_s1", seed=0x5EE
     (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one.  Multi-tile
     frames (configs[3]) are parsed tile-parallel (av1p_set_tile_threads)."""
     from av1dec_amd.pipeline import run_native
-    run_native(decs, "ivf", streams)
+    # up to two workers per stream: one parses a stream's next frame while another packs
+    # the frame before (the IVF source keeps two parsed units alive, av1r_pipeline.cpp)
+    workers = max(len(streams), min(2 * len(streams), host_workers()))
+    run_native(decs, "ivf", streams, workers=workers)
     t0 = time.perf_counter()
-    st = run_native(decs, "ivf", streams)
+    st = run_native(decs, "ivf", streams, workers=workers)
     dt = time.perf_counter() - t0
     n = int(st["frames"])
     return {"fps": round(n / dt, 3), "streams": len(streams), "frames_per_stream": frames,
@@ -250,11 +253,12 @@ def ivf_leg(decs, streams, frames, size="1920x1080", name="1080p_s1", seed=0x5EE
             "parse_ms_per_frame": round(1e3 * st["produce_s"] / n, 3),
             "pack_ms_per_frame": round(1e3 * st["pack_s"] / n, 3),
             "stream_bytes_per_frame": int(sum(len(s) for s in streams) / n),
-            "batches": int(st["batches"]),
+            "batches": int(st["batches"]), "host_workers": workers,
             "workload": f"{len(streams)} synthetic {size} IVF streams from tools/bsw ({name}: 1 key + "
-                        f"{frames - 1} inter, seeds {seed:#x}+stream), each parsed by the host parser and packed on "
-                        f"its own native thread (av1r_pipeline_run), decoded in shared launches; parse inside "
-                        f"the timed region"}
+                        f"{frames - 1} inter, seeds {seed:#x}+stream), parsed by the host parser (one frame of a stream at a "
+                        f"time) and packed by {workers} native workers (av1r_pipeline_run: a stream's next frame "
+                        f"parses while its previous one packs), decoded in shared launches; parse inside the timed "
+                        f"region"}
 
 
 _RANK_CPUS = None  # this rank's CPU set once bind_rank_cpus has bound it (N > 1)
