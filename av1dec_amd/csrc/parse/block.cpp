@@ -576,7 +576,8 @@ void BlockParser::decode_block(int r, int c, int bsize)
             m.pal_size[0] = (uint8_t)b.pal_y;
             m.pal_size[1] = (uint8_t)b.pal_uv;
             m.pal_idx = palIdx;
-            for (int i = 0; i < 4; i++) m.delta_lf[i] = (int8_t)T.delta_lf[i];
+            if (P.emit_mi)
+                for (int i = 0; i < 4; i++) P.mi_dlf[((size_t)(r + y) * P.mi_stride + c + x) * 4 + i] = (int8_t)T.delta_lf[i];
         }
     PROF_T(t4);
     emit(b);
@@ -2438,7 +2439,7 @@ void BlockParser::emit(Blk& b)
             rec.ref_frame[l] = m.ref[l];
         }
         rec.filt = (uint8_t)((m.interp[0] & 15) | (m.interp[1] << 4));
-        for (int i = 0; i < 4; i++) rec.delta_lf[i] = m.delta_lf[i];
+        for (int i = 0; i < 4; i++) rec.delta_lf[i] = (int8_t)T.delta_lf[i];  // (the block's, as stored over its units)
     }
     uint32_t f = 0;
     const bool ii = b.is_inter && b.interintra && !b.use_intrabc;
@@ -2575,7 +2576,7 @@ void BlockParser::emit(Blk& b)
                     for (int xx = 0; xx <= sub; xx++)
                         for (int yy = 0; yy <= sub; yy++) {
                             const int rr = row + (i << sub) + yy, cc = col + (j << sub) + xx;
-                            if (rr < fh.aligned_mi_rows && cc < fh.aligned_mi_cols) mi(rr, cc).lf_tx[plane] = (uint8_t)t.tx;
+                            if (rr < fh.aligned_mi_rows && cc < fh.aligned_mi_cols) P.mi_lftx[((size_t)rr * P.mi_stride + cc) * 3 + plane] = (uint8_t)t.tx;
                         }
                 T.decoded[plane][(sbRow >> sub) + i + 1][(sbCol >> sub) + j + 1] = 1;
             }

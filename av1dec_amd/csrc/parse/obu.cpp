@@ -927,6 +927,10 @@ void Parser::start_frame()
     memset(&z, 0, sizeof(z));
     z.pal_idx = ~0u;
     mi.assign((size_t)fh.aligned_mi_rows * mi_stride, z);
+    if (emit_mi) {
+        mi_lftx.assign(mi.size() * 3, 0);
+        mi_dlf.assign(mi.size() * 4, 0);
+    }
     mf_ref.assign((size_t)fh.mi_rows * fh.mi_cols, -1);
     mf_mv.assign((size_t)fh.mi_rows * fh.mi_cols, Mv());
     cdef_rows = (fh.mi_rows + 15) / 16;
@@ -1035,8 +1039,8 @@ int Parser::finish_frame()
         d.uv_mode = m.uv_mode;
         d.filt = (uint8_t)((m.interp[0] & 15) | (m.interp[1] << 4));
         d.flags = (m.skip ? AV1R_MI_SKIP : 0) | (m.is_inter ? AV1R_MI_INTER : 0);
-        for (int p = 0; p < 3; p++) d.lf_tx[p] = m.lf_tx[p];
-        for (int k = 0; k < 4; k++) d.delta_lf[k] = m.delta_lf[k];
+        for (int p = 0; p < 3; p++) d.lf_tx[p] = mi_lftx[i * 3 + p];
+        for (int k = 0; k < 4; k++) d.delta_lf[k] = mi_dlf[i * 4 + k];
     }
     F.cdef = cdef_idx;
     F.lr = lr_units;

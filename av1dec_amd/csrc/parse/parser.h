@@ -361,10 +361,12 @@ struct MiInfo {
     uint8_t interp[2];
     uint8_t comp_group_idx, compound_idx;
     uint8_t pal_size[2];
-    uint8_t lf_tx[3];
-    int8_t delta_lf[4];
+    uint8_t pad[4];
     uint32_t pal_idx;  // this block's palette colours (Parser::pal_colors), ~0u: none
 };
+// (32 bytes: two per cache line, none straddling one; the loop filter's transform sizes and
+// delta LF live in Parser::mi_lftx / mi_dlf, filled only for an emitted mode-info grid)
+static_assert(sizeof(MiInfo) == 32, "MiInfo layout");
 
 // ---- frame header (spec 5.9 uncompressed_header) and everything derived from it ----
 struct FrameHdr {
@@ -482,6 +484,9 @@ public:
     // per frame
     std::vector<MiInfo> mi;
     int mi_stride = 0;
+    // per 4x4 unit, for the emitted grid only (emit_mi): lf_tx of the 3 planes, delta LF x 4
+    std::vector<uint8_t> mi_lftx;
+    std::vector<int8_t> mi_dlf;
     std::vector<int8_t> mf_ref;          // MfRefFrames of this frame (motion vector storage)
     std::vector<Mv> mf_mv;
     std::vector<Mv> motion_field[8];     // MotionFieldMvs[ref][row >> 1][col >> 1]
