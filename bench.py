@@ -240,9 +240,11 @@ def ivf_leg(decs, streams, frames, size="1920x1080", name="1080p_s1", seed=0x5EE
     (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one.  Multi-tile
     frames (configs[3]) are parsed tile-parallel (av1p_set_tile_threads)."""
     from av1dec_amd.pipeline import run_native
-    # up to two workers per stream: one parses a stream's next frame while another packs
-    # the frame before (the IVF source keeps two parsed units alive, av1r_pipeline.cpp)
-    workers = max(len(streams), min(2 * len(streams), host_workers()))
+    # one worker per stream (a stream's next frame may still parse while its previous one
+    # packs: the IVF source keeps two parsed units alive, av1r_pipeline.cpp).  Two workers
+    # per stream measured no faster (320-334 against 335 frames/s): the parse threads ran
+    # slower beside 8 more busy cores (23.3 against 21.5 ms/frame), profiles/r05_ab_ivf_workers.txt
+    workers = len(streams)
     run_native(decs, "ivf", streams, workers=workers)
     t0 = time.perf_counter()
     st = run_native(decs, "ivf", streams, workers=workers)
