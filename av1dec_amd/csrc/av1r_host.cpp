@@ -784,6 +784,33 @@ static void schedule_check(av1r_ctx* c, const av1r_frame_batch* b)
         }
     }
     fprintf(stderr, "av1r sched check: %zu items, %zu tiles, %lld groups, %ld violations\n", ni, c->tiles.size(), (long long)g, bad);
+    static const bool chains = getenv("AV1R_SCHED_CHECK") && atoi(getenv("AV1R_SCHED_CHECK")) >= 2;
+    if (chains) {
+        // (debug aid) the longest dependency chain in items, and with the hops between items of
+        // one block free (as if a block's items ran in one wave, one after the other)
+        std::vector<int32_t> depth(ni, 1), depthB(ni, 1);
+        int32_t maxD = 0, maxB = 0;
+        for (size_t i = 0; i < ni; i++) {
+            const WorkItem& w = c->items[i];
+            const uint32_t kind = AV1R_ITEM_KIND(w.code), idx = AV1R_ITEM_INDEX(w.code);
+            const int32_t node = kind == AV1R_ITEM_TB ? c->nodeOfTb[idx] : kind == AV1R_ITEM_II ? c->nodeOfBlk[idx] : -1;
+            auto dep = [&](int32_t p) {
+                if (p < 0 || (size_t)p >= i) return;
+                depth[i] = std::max(depth[i], depth[p] + 1);
+                depthB[i] = std::max(depthB[i], depthB[p] + (c->items[p].block == w.block ? 0 : 1));
+            };
+            for (uint32_t d = 0; d < w.dep_cnt; d++) dep((int32_t)c->deps[w.dep_off + d]);
+            if (node >= 0 && c->edgeStart.size() > (size_t)node + 1)
+                for (uint32_t e = c->edgeStart[node]; e < c->edgeStart[node + 1]; e++) {
+                    const int32_t pn = c->edgeDeps[e];
+                    dep(pn >= 0 && (size_t)pn < c->nodePos.size() ? c->nodePos[pn] : -1);
+                }
+            maxD = std::max(maxD, depth[i]);
+            maxB = std::max(maxB, depthB[i]);
+        }
+        fprintf(stderr, "av1r sched chains: %zu levels, longest chain %d items, %d with a block's own hops free\n", c->levels.size(), maxD,
+            maxB);
+    }
 }
 
 static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
