@@ -810,6 +810,91 @@ static void schedule_check(av1r_ctx* c, const av1r_frame_batch* b)
         }
         fprintf(stderr, "av1r sched chains: %zu levels, longest chain %d items, %d with a block's own hops free\n", c->levels.size(), maxD,
             maxB);
+        // time model of the critical path (us): an item 6 (records, wait, gather, predict,
+        // store, hand-off); a block-plane chain of small TBs run by one wave: 6 for its first
+        // TB and 1.7 for each next one, the chain starting once every external producer of any
+        // of its TBs is done
+        std::vector<double> fin(ni, 0.0);
+        std::vector<int32_t> chainOf(ni, -1);
+        double tItems = 0, tChains = 0;
+        {
+            std::vector<double> f1(ni, 0.0);
+            for (size_t i = 0; i < ni; i++) {
+                const WorkItem& w = c->items[i];
+                double st = 0;
+                auto ext = [&](int32_t p) { if (p >= 0 && (size_t)p < i) st = std::max(st, f1[p]); };
+                for (uint32_t d = 0; d < w.dep_cnt; d++) ext((int32_t)c->deps[w.dep_off + d]);
+                const uint32_t kind = AV1R_ITEM_KIND(w.code), idx = AV1R_ITEM_INDEX(w.code);
+                const int32_t node = kind == AV1R_ITEM_TB ? c->nodeOfTb[idx] : kind == AV1R_ITEM_II ? c->nodeOfBlk[idx] : -1;
+                if (node >= 0)
+                    for (uint32_t e = c->edgeStart[node]; e < c->edgeStart[node + 1]; e++)
+                        ext(c->edgeDeps[e] >= 0 && (size_t)c->edgeDeps[e] < c->nodePos.size() ? c->nodePos[c->edgeDeps[e]] : -1);
+                f1[i] = st + 6.0;
+                tItems = std::max(tItems, f1[i]);
+            }
+            // chains: items in decode order (TB index order) of one block and plane, small TBs
+            std::vector<int32_t> byTb(b->n_tbs, -1);
+            for (size_t i = 0; i < ni; i++)
+                if (AV1R_ITEM_KIND(c->items[i].code) == AV1R_ITEM_TB) byTb[AV1R_ITEM_INDEX(c->items[i].code)] = (int32_t)i;
+            std::vector<std::vector<int32_t>> chainItems;
+            for (uint32_t ti = 0; ti < b->n_tbs; ti++) {
+                const int32_t i = byTb[ti];
+                if (i < 0) continue;
+                const WorkItem& w = c->items[i];
+                const bool small = av1r_tx_w[w.tx_size] <= 16 && av1r_tx_h[w.tx_size] <= 16;
+                const int32_t prevI = ti ? byTb[ti - 1] : -1;
+                const bool cont = small && prevI >= 0 && c->items[prevI].block == w.block && c->items[prevI].plane == w.plane &&
+                                  chainOf[prevI] >= 0 && chainItems[chainOf[prevI]].size() < 63;
+                if (cont) {
+                    chainOf[i] = chainOf[prevI];
+                    chainItems[chainOf[i]].push_back(i);
+                } else if (small) {
+                    chainOf[i] = (int32_t)chainItems.size();
+                    chainItems.push_back({i});
+                }
+            }
+            // finish times in decode (node) order, which every dependency follows; a chain's
+            // start waits for its externals (all its TBs')
+            std::vector<double> chainStart(chainItems.size(), -1.0);
+            for (size_t nd = 0; nd < c->nodePos.size(); nd++) {
+                if (c->nodePos[nd] < 0) continue;
+                const size_t i = (size_t)c->nodePos[nd];
+                const WorkItem& w = c->items[i];
+                auto externals = [&](size_t it, double& st) {
+                    const WorkItem& x = c->items[it];
+                    auto ext = [&](int32_t p) {
+                        if (p < 0 || (size_t)p >= ni) return;
+                        if (chainOf[it] >= 0 && chainOf[p] == chainOf[it]) return;  // internal
+                        st = std::max(st, fin[p]);
+                    };
+                    for (uint32_t d = 0; d < x.dep_cnt; d++) ext((int32_t)c->deps[x.dep_off + d]);
+                    const uint32_t kind = AV1R_ITEM_KIND(x.code), idx = AV1R_ITEM_INDEX(x.code);
+                    const int32_t node = kind == AV1R_ITEM_TB ? c->nodeOfTb[idx] : kind == AV1R_ITEM_II ? c->nodeOfBlk[idx] : -1;
+                    if (node >= 0)
+                        for (uint32_t e = c->edgeStart[node]; e < c->edgeStart[node + 1]; e++)
+                            ext(c->edgeDeps[e] >= 0 && (size_t)c->edgeDeps[e] < c->nodePos.size() ? c->nodePos[c->edgeDeps[e]] : -1);
+                };
+                const int32_t ch = chainOf[i];
+                if (ch < 0) {
+                    double st = 0;
+                    externals(i, st);
+                    fin[i] = st + 6.0;
+                } else {
+                    const auto& v = chainItems[ch];
+                    if (chainStart[ch] < 0) {
+                        double st = 0;
+                        for (int32_t it : v) externals((size_t)it, st);  // (externals precede the chain in item order)
+                        chainStart[ch] = st;
+                    }
+                    size_t k = 0;
+                    while (v[k] != (int32_t)i) k++;
+                    fin[i] = chainStart[ch] + 6.0 + 1.7 * (double)k;
+                }
+                (void)w;
+                tChains = std::max(tChains, fin[i]);
+            }
+        }
+        fprintf(stderr, "av1r sched chains: critical path (time model) items %.0f us, block-plane chains %.0f us\n", tItems, tChains);
     }
 }
 
