@@ -1943,11 +1943,14 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         static const bool merged = !getenv("AV1R_INTER_MERGED") || atoi(getenv("AV1R_INTER_MERGED")) != 0;
         // AV1R_INTER_CHUNKS: chunks per XCD of each class (k_inter_all's inter_deal; 1 = one
         // contiguous eighth each)
-        static const uint32_t kc = getenv("AV1R_INTER_CHUNKS") ? (uint32_t)std::max(1, atoi(getenv("AV1R_INTER_CHUNKS"))) : 1u;
-        auto pad8 = [](uint32_t v) { return (v + 8 * kc - 1) / (8 * kc) * (8 * kc); };
+        static const uint32_t kc = getenv("AV1R_INTER_CHUNKS") ? (uint32_t)std::max(1, std::min(255, atoi(getenv("AV1R_INTER_CHUNKS")))) : 1u;
+        // AV1R_INTER_BANDS: each XCD's share walked band by band over the three classes
+        static const uint32_t nb = getenv("AV1R_INTER_BANDS") ? (uint32_t)std::max(1, std::min(64, atoi(getenv("AV1R_INTER_BANDS")))) : 1u;
+        const uint32_t unit = 8 * kc * nb;
+        auto pad8 = [unit](uint32_t v) { return (v + unit - 1) / unit * unit; };
         if (merged && !aux) {
             if (total[0] + total[1] + total[2])
-                launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), kc, trace, st);
+                launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), kc | (nb << 8), trace, st);
         } else {
             if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, sp);
             if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, sp);

@@ -1737,14 +1737,34 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const 
     const uint32_t* tI = tab;
     const uint32_t* tM = tI + 2 * n + 1;
     const uint32_t* tS = tM + 3 * n + 1;
-    if (j < qI) {
-        const uint32_t b = inter_deal(x, j, qI, kc);
+    // kc: chunks per XCD (bits 0-7) and bands (bits 8-15, AV1R_INTER_BANDS): with nb > 1 each
+    // XCD walks its share band by band -- the general, medium and small tiles of band 0, then of
+    // band 1, ... (the class lists are in decode order, so a band is a stretch of the frame) --
+    // so that a region's reference lines are fetched once for all three classes, not once per
+    // class sweep.  The class counts are padded to multiples of 8 * chunks * bands.
+    const uint32_t kcc = kc & 0xffu, nb = (kc >> 8) ? (kc >> 8) : 1u;
+    uint32_t cls = 3, jj = 0;
+    if (nb == 1) {
+        if (j < qI) cls = 0, jj = j;
+        else if (j < qI + qM) cls = 1, jj = j - qI;
+        else if (j < qI + qM + qS) cls = 2, jj = j - qI - qM;
+    } else {
+        const uint32_t bI = qI / nb, bM = qM / nb, bS = qS / nb, per = bI + bM + bS;
+        const uint32_t band = j / per, r = j - band * per;
+        if (band < nb) {
+            if (r < bI) cls = 0, jj = band * bI + r;
+            else if (r < bI + bM) cls = 1, jj = band * bM + (r - bI);
+            else cls = 2, jj = band * bS + (r - bI - bM);
+        }
+    }
+    if (cls == 0) {
+        const uint32_t b = inter_deal(x, jj, qI, kcc);
         if (b < tI[n]) inter_general(kps, tI, n, b, L.g, trace, ~0u);
-    } else if (j < qI + qM) {
-        const uint32_t b = inter_deal(x, j - qI, qM, kc);
+    } else if (cls == 1) {
+        const uint32_t b = inter_deal(x, jj, qM, kcc);
         if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m, c2);
-    } else if (j < qI + qM + qS) {
-        const uint32_t b = inter_deal(x, j - qI - qM, qS, kc);
+    } else if (cls == 2) {
+        const uint32_t b = inter_deal(x, jj, qS, kcc);
         if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s, c2);
     }
 }
