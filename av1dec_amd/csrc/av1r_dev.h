@@ -87,6 +87,38 @@ static_assert(sizeof(WorkItem) == 32, "WorkItem layout");
 #define AV1R_PRED_PALETTE 1
 #define AV1R_PRED_INTER 2
 
+// The device's block record: the fields of av1r_block that the kernels read, packed (52 bytes
+// against 84: a 1080p inter frame uploads ~0.45 MB less).  Left out, into KParams::bext at
+// index palette_off (a palette block is never inter, so the field is free for the inter
+// blocks that need it): the 24-byte local-warp parameters of an AV1R_BLK_LOCAL_VALID block
+// and the transform-block range of an AV1R_BLK_INTERINTRA block (k_flow's ii_item adds
+// its residuals), 8 words each: LocalWarpParams[6], first_tb, n_tbs.  Every other kernel
+// reaches a TB's block, never the reverse.  Written by pack_frame (av1r_host.cpp).
+struct DevBlock {
+    // av1r_block's first 32 bytes, as they are
+    uint16_t mi_row, mi_col;
+    uint8_t mi_size, qindex, y_mode, uv_mode;
+    int8_t angle_delta_y, angle_delta_uv;
+    uint8_t filter_intra_mode;
+    int8_t cfl_alpha_u, cfl_alpha_v;
+    uint8_t palette_size_y, palette_size_uv;
+    uint8_t motion_mode, compound_type, interintra_mode, wedge_index, wedge_sign, mask_type, ii_edge;
+    uint8_t pad0[2];
+    uint32_t flags;
+    uint16_t max_luma_w, max_luma_h;
+    uint32_t palette_off;  // palette blocks: their palette record; LOCAL_VALID / INTERINTRA blocks: their bext index
+    // av1r_block's last 16 bytes, as they are
+    int16_t mv[2][2];
+    int8_t ref_frame[2];
+    uint8_t filt;
+    uint8_t pad1;
+    int8_t delta_lf[4];
+};
+static_assert(sizeof(DevBlock) == 52, "DevBlock layout");
+static_assert(offsetof(av1r_block, max_luma_h) == 30 && offsetof(DevBlock, max_luma_h) == 30, "DevBlock head");
+static_assert(offsetof(av1r_block, mv) + 16 == sizeof(av1r_block) && offsetof(DevBlock, mv) + 16 == sizeof(DevBlock),
+    "DevBlock tail");
+
 // Everything the stage kernels read about one frame.  A launch covers n frames (one per
 // stream of a batch): the kernels receive a device array of n KParams and pick theirs
 // by blockIdx (see k_level / k_lf / k_cdef / k_lr).
@@ -96,7 +128,8 @@ struct KParams {
     // deblocking edge codes (k_lfcode -> k_lf / k_deblock): per pass, a byte per 4x4 unit in
     // k_lf's unit order (luma row-major, then U, then V): level | filter size << 6, 0 = none
     uint8_t* lfc;
-    const av1r_block* blocks;
+    const DevBlock* blocks;
+    const int32_t* bext;  // LOCAL_VALID / INTERINTRA blocks' warp parameters and TB range, 8 words each (DevBlock)
     const av1r_tb* tbs;
     const uint32_t* coefs;
     const uint8_t* palette;

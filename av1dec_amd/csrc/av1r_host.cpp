@@ -1428,7 +1428,13 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szMi = align256(sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc);
     // the deblocking edge codes (k_lfcode): a byte per (pass, plane, 4x4 unit), device-filled
     const size_t szLfc = align256(2 * ((size_t)h->mi_rows * h->mi_cols + 2 * (size_t)((h->mi_rows + 1) / 2) * ((h->mi_cols + 1) / 2)));
-    const size_t szBlk = align256(sizeof(av1r_block) * (size_t)b->n_blocks);
+    // the blocks in the device's record (DevBlock), the warp parameters and TB ranges of the
+    // LOCAL_VALID / INTERINTRA blocks beside them (bext, 8 words each)
+    const uint32_t extFlags = AV1R_BLK_LOCAL_VALID | AV1R_BLK_INTERINTRA;
+    size_t nExt = 0;
+    for (uint32_t i = 0; i < b->n_blocks; i++) nExt += (b->blocks[i].flags & extFlags) != 0;
+    const size_t szBlk = align256(sizeof(DevBlock) * (size_t)b->n_blocks);
+    const size_t szExt = align256(32 * nExt + 4);
     const size_t szTb = align256(sizeof(av1r_tb) * (size_t)b->n_tbs);
     const size_t szCoef = align256(4 * (size_t)b->n_coefs);
     const size_t szPal = align256(b->n_palette);
@@ -1442,7 +1448,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szTb + szCoef + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
+    *need = szHdr + szBlk + szExt + szTb + szCoef + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
@@ -1467,7 +1473,27 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     KParams& k = P.base;
     memset(&k, 0, sizeof(k));
     k.hdr = (const av1r_frame_hdr*)put(h, sizeof(av1r_frame_hdr), szHdr);
-    k.blocks = (const av1r_block*)put(b->blocks, sizeof(av1r_block) * (size_t)b->n_blocks, szBlk);
+    {
+        DevBlock* db = reinterpret_cast<DevBlock*>(host + off);
+        k.blocks = (const DevBlock*)put(nullptr, 0, szBlk);
+        int32_t* dx = reinterpret_cast<int32_t*>(host + off);
+        k.bext = (const int32_t*)put(nullptr, 0, szExt);
+        uint32_t w = 0;
+        for (uint32_t i = 0; i < b->n_blocks; i++) {
+            const av1r_block& s = b->blocks[i];
+            DevBlock& d = db[i];
+            memcpy(&d, &s, offsetof(DevBlock, palette_off));
+            d.palette_off = s.palette_off;
+            memcpy(d.mv, s.mv, 16);
+            if (s.flags & extFlags) {
+                int32_t* e = dx + 8 * (size_t)w;
+                memcpy(e, s.local_warp, 24);
+                e[6] = (int32_t)s.first_tb;
+                e[7] = (int32_t)s.n_tbs;
+                d.palette_off = w++;
+            }
+        }
+    }
     k.tbs = (const av1r_tb*)put(b->tbs, sizeof(av1r_tb) * (size_t)b->n_tbs, szTb);
     k.coefs = (const uint32_t*)put(b->coefs, 4 * (size_t)b->n_coefs, szCoef);
     k.palette = put(b->palette, b->n_palette, szPal);
@@ -1558,7 +1584,7 @@ static int job_begin(FrameJob& j)
         auto rb = [&](auto& ptr) {
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
-        rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
+        rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.bext), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
         rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
     }
     for (int s = 0; s < 8; s++)

@@ -1488,7 +1488,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mi_blocks(const KParams* kps
     const KParams& k = KP(kps, blockIdx.y);
     const uint32_t bi = blockIdx.x * 16 + (threadIdx.x >> 4);
     if (bi >= k.n_blocks) return;
-    const av1r_block& b = k.blocks[bi];
+    const DevBlock& b = k.blocks[bi];
     av1r_mi m;
     memset(&m, 0, sizeof(m));
     for (int l = 0; l < 2; l++) {

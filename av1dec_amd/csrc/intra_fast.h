@@ -36,13 +36,13 @@ struct FiParams {
 };
 
 // the lean path takes this item: an intra TB (not palette) of a one-wave item, no filter-intra
-DEV bool fi_ok(const WorkItem& tb, const av1r_block& blk)
+DEV bool fi_ok(const WorkItem& tb, const DevBlock& blk)
 {
     return tb.pred == AV1R_PRED_INTRA && !(tb.plane == 0 && (blk.flags & AV1R_BLK_FILTER_INTRA));
 }
 
 // Every parameter of the prediction (uniform: scalar registers), from the batch only
-DEV FiParams fi_setup(const KParams& k, const WorkItem& tb, const av1r_block& blk, int edgeFilter)
+DEV FiParams fi_setup(const KParams& k, const WorkItem& tb, const DevBlock& blk, int edgeFilter)
 {
     FiParams F;
     const int plane = tb.plane, x = tb.x, y = tb.y, sub = plane ? 1 : 0;

@@ -73,7 +73,7 @@ DEV void col_pass(const int16_t* col, int16_t* out, int kind, int colShift, int 
 // dataflow kernel runs it before the item's dependencies are complete.  c0: the lane's
 // first coefficient, prefetched by the caller.  Ends with a coop_sync.
 template <int NT, int MAX, class TB>
-DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int16_t* res, uint32_t c0)
+DEV void tb_residual(const KParams& k, const TB& tb, const DevBlock& blk, int16_t* res, uint32_t c0)
 {
     constexpr int RS = MAX + 2;
     const int t = coop_lane<NT>();
@@ -146,7 +146,7 @@ DEV void tb_residual(const KParams& k, const TB& tb, const av1r_block& blk, int1
 // IntraPredict::predict_intra with CFL (IntraPredict.cpp:563-667).  Inter TBs predict
 // nothing here (their prediction is already in the frame).  Ends with a coop_sync.
 template <int NT, int MAX, bool COH>
-DEV void tb_predict(const KParams& k, const WorkItem& tb, const av1r_block& blk, TbLds<MAX>& L, const GranEdges* G = nullptr,
+DEV void tb_predict(const KParams& k, const WorkItem& tb, const DevBlock& blk, TbLds<MAX>& L, const GranEdges* G = nullptr,
     bool gran = false, int edgeFilter = -1)
 {
     constexpr int CM = TbLds<MAX>::CM;
@@ -328,7 +328,7 @@ DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned l
 {
     const int t = coop_lane<NT>();
     const uint32_t c0 = t < wi.coef_cnt ? k.coefs[wi.coef_off + t] : 0u;
-    const av1r_block& blk = k.blocks[wi.block];
+    const DevBlock& blk = k.blocks[wi.block];
     tb_predict<NT, MAX, false>(k, wi, blk, L);
     trace_stamp(tr, 4);
     if (wi.coef_cnt) tb_residual<NT, MAX>(k, wi, blk, L.res, c0);
@@ -717,7 +717,7 @@ struct PuInfo {
     int8_t ref_frame[2];
     uint8_t filt;
 };
-DEV PuInfo pu_info(const KParams& k, const av1r_block& blk, int candRow, int candCol)
+DEV PuInfo pu_info(const KParams& k, const DevBlock& blk, int candRow, int candCol)
 {
     PuInfo p;
     if (candRow == blk.mi_row && candCol == blk.mi_col) {
@@ -771,7 +771,7 @@ DEV void distance_weights(const KParams& k, const MI& info, int& fwd, int& bck)
 // The references of one prediction unit (predict_inter, InterPredict.cpp:962-1021):
 // motion vector scaling, warp choice (local / global, Block.cpp:1179-1200) and filters.
 // Returns isCompound.
-DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, int y, int w, int h,
+DEV int setup_refs(const KParams& k, const DevBlock& blk, int plane, int x, int y, int w, int h,
     int candRow, int candCol, RefSel* R, const int32_t* lw)
 {
     const av1r_frame_hdr& hd = *k.hdr;
@@ -811,7 +811,7 @@ DEV int setup_refs(const KParams& k, const av1r_block& blk, int plane, int x, in
 // w x h prediction unit at plane position (x, y); sample (r, c) of the PU lands in
 // L.tile[(toy + r) * TS + tox + c].  Ends with a barrier.
 template <int NT, int TSZ>
-DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int plane, int x, int y,
+DEV void predict_pu(const KParams& k, const DevBlock& blk, InterLdsT<TSZ>& L, int plane, int x, int y,
     int w, int h, int candRow, int candCol, int rx0, int ry0, int rw, int rh, int tox, int toy, const int32_t* lw)
 {
     const int t = il_lane<NT>();
@@ -953,7 +953,7 @@ DEV void predict_pu(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, 
 #define C2_HS 16                   // chroma intermediate row stride
 #define C2_HB (23 * C2_HS)         // one chroma intermediate
 #define C2_TILE (16 * TS)          // chroma tile of plane 2 after plane 1's
-DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, int x, int y, int w, int h, int rx0,
+DEV bool predict_chroma2(const KParams& k, const DevBlock& blk, InterLds& L, int x, int y, int w, int h, int rx0,
     int ry0, int rw, int rh, const int32_t* lw)
 {
     const int t = threadIdx.x;
@@ -1050,7 +1050,7 @@ DEV bool predict_chroma2(const KParams& k, const av1r_block& blk, InterLds& L, i
 // overlappedMotionCompensation (InterPredict.cpp:611-709) restricted to the tile
 // [TX0, TX0 + TW) x [TY0, TY0 + TH) (block-relative plane coordinates).
 template <int NT, int TSZ>
-DEV void obmc(const KParams& k, const av1r_block& blk, InterLdsT<TSZ>& L, int plane, int baseX, int baseY, int w, int h,
+DEV void obmc(const KParams& k, const DevBlock& blk, InterLdsT<TSZ>& L, int plane, int baseX, int baseY, int w, int h,
     int TX0, int TY0, int TW, int TH)
 {
     const int t = il_lane<NT>();
@@ -1126,7 +1126,7 @@ struct PlaneGeo {
     int candRow, candCol, predW, predH;  // prediction units (Block.cpp:146-174)
 };
 template <int TSZ>
-DEV PlaneGeo plane_geo(const KParams& k, const av1r_block& blk, int plane, int tx, int ty)
+DEV PlaneGeo plane_geo(const KParams& k, const DevBlock& blk, int plane, int tx, int ty)
 {
     PlaneGeo G;
     const int bs = blk.mi_size;
@@ -1168,8 +1168,8 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
 {
     const int t = il_lane<NT>();
     // the block record in scalar registers (one scalar load: a tile's fields are uniform)
-    const av1r_block blk = sload(k.blocks + bi);
-    const int32_t* lw = k.blocks[bi].local_warp;
+    const DevBlock blk = sload(k.blocks + bi);
+    const int32_t* lw = (blk.flags & AV1R_BLK_LOCAL_VALID) ? k.bext + 8 * (size_t)blk.palette_off : nullptr;
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
     // timeline (-DAV1R_TRACE): 1 = block size | motion mode << 8 | compound << 12, 8 + plane
     // after each plane's store, 11 after the luma geometry, 12 after the luma prediction
@@ -1239,10 +1239,10 @@ DEV void inter_tile(const KParams& k, uint32_t bi, int tx, int ty, InterLdsT<TSZ
 // inter prediction inter_tile stored in the frame.
 template <int NT, bool COH>
 DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G = nullptr, bool gran = false,
-    const av1r_block* pre = nullptr)
+    const DevBlock* pre = nullptr)
 {
     const int t = coop_lane<NT>();
-    const av1r_block& blk = pre ? *pre : k.blocks[bi];  // (k_flow: loaded before the wait)
+    const DevBlock& blk = pre ? *pre : k.blocks[bi];  // (k_flow: loaded before the wait)
     const int hasChroma = (blk.flags & AV1R_BLK_HAS_CHROMA) != 0;
     const int bs = blk.mi_size;
     const int im = blk.interintra_mode;
@@ -1320,7 +1320,9 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
         if (addRes) {
             // TransformBlock::decode's add and clip for this plane's TBs with coefficients
             // (TBs never overlap: in place in L.pred), then the whole plane is stored
-            for (uint32_t ti = blk.first_tb; ti < blk.first_tb + blk.n_tbs; ti++) {
+            const int32_t* ext = k.bext + 8 * (size_t)blk.palette_off;
+            const uint32_t firstTb = (uint32_t)ext[6], nTbs = (uint32_t)ext[7];
+            for (uint32_t ti = firstTb; ti < firstTb + nTbs; ti++) {
                 const av1r_tb& tb = k.tbs[ti];
                 if (tb.plane != plane || !tb.coef_cnt) continue;
                 const int tw = av1r_tx_w[tb.tx_size], th = av1r_tx_h[tb.tx_size];
@@ -1505,7 +1507,7 @@ struct SmallLds {
 // sub-pel filter, :319-383; the average / distance blend of :1022-1049) of w x h <= 8 x 8
 // at plane position (x, y), by NT lanes.
 template <int NT, int MS>
-DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int plane, int x, int y, int w, int h, int candRow,
+DEV void small_pu(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int plane, int x, int y, int w, int h, int candRow,
     int candCol)
 {
     const int t = threadIdx.x & (NT - 1);
@@ -1574,7 +1576,7 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int 
 // then the passes run over both.  The windows and intermediates are laid over the group's
 // SmallLds (4 windows of (MS/2 + 7) x (MS/2 + 8) bytes, then 4 intermediates).
 template <int NT, int MS>
-DEV void small_pu_c2(const KParams& k, SmallLds<MS>& L, const av1r_block& blk, int x, int y, int w, int h, int candRow,
+DEV void small_pu_c2(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int x, int y, int w, int h, int candRow,
     int candCol)
 {
     constexpr int CS = MS / 2, WS = CS + 8, WSZ = (CS + 7) * WS, HSZ = (CS + 7) * CS;
@@ -1666,7 +1668,7 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
     const int g = threadIdx.x / NT;
     const uint32_t i = (64 / NT) * (b - tab[s]) + g;
     if (i >= tab[2 * n + 1 + s]) return;  // (wave-level ordering only: no barrier follows)
-    const av1r_block& blk = k.blocks[AV1R_ITEM_INDEX(k.tiles[tab[n + 1 + s] + i]) >> 4];
+    const DevBlock& blk = k.blocks[AV1R_ITEM_INDEX(k.tiles[tab[n + 1 + s] + i]) >> 4];
     const int nPl = (blk.flags & AV1R_BLK_HAS_CHROMA) ? 3 : 1;
     for (int plane = 0; plane < nPl; plane++) {
         // (sub-8x8 chroma may gather up to four units of neighbouring blocks)
@@ -1903,7 +1905,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     }
     if (AV1R_ITEM_KIND(wi.code) == AV1R_ITEM_II) {
         if constexpr (MAX == 64) {  // blends are always large items
-            const av1r_block blk = sload(k.blocks + AV1R_ITEM_INDEX(wi.code));
+            const DevBlock blk = sload(k.blocks + AV1R_ITEM_INDEX(wi.code));
             trace_stamp(tr, 3);
             flow_wait<NT>(k.deps + wi.dep_off, wi.dep_cnt, k.done, epoch, ctl);
             trace_stamp(tr, 4);
@@ -1914,7 +1916,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
         ResQuads<NT, MAX> R;
         if (!gran) resOff = wi.coef_cnt ? sload(k.tb_res + AV1R_ITEM_INDEX(wi.code)) : ~0u;
         res_prefetch<NT, MAX>(k, wi, resOff, R);
-        const av1r_block blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
+        const DevBlock blk = sload(k.blocks + wi.block);  // (a copy: only the fields predict reads are loaded)
         const int edgeFilter = sfield(&k.hdr->enable_intra_edge_filter);
         bool lean = false;
         if constexpr (NT == 64 && MAX == TB_SMALL) {
@@ -2099,7 +2101,7 @@ DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
     const int t = coop_lane<NT>();
     const av1r_tb& tb = k.tbs[ti];
     const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
-    const av1r_block& blk = k.blocks[tb.block];
+    const DevBlock& blk = k.blocks[tb.block];
     const uint32_t ro = k.tb_res[ti];
     tb_residual<NT, MAX>(k, tb, blk, res, c0);
     const int l2q = av1r_tx_w_log2[tb.tx_size] - 2;

@@ -40,12 +40,13 @@ def main():
             ps = list(ex.map(Decoder.pack, frames))
         wall = time.perf_counter() - t
         l.av1r_pack_profile(ns, 7, 0)
+        packed = sum(l.av1r_packed_bytes(p) for p in ps) / max(len(ps), 1)
         for p in ps:
             Decoder.free_packed(p)
         n = max(int(ns[6]), 1)
         r = {"threads": a.threads, "frames": len(frames), "wall_ms_per_frame": round(1e3 * wall / len(frames), 3),
              "phase_ms_per_frame": {ph: round(ns[i] / n / 1e6, 3) for i, ph in enumerate(PHASES)},
-             "packed_MB_per_frame": round(l.av1r_packed_bytes(ps[0]) / 1e6, 2) if ps else 0}
+             "packed_MB_per_frame": round(packed / 1e6, 3)}
         r["cpu_ms_per_frame"] = round(sum(r["phase_ms_per_frame"].values()), 3)
         if best is None or r["cpu_ms_per_frame"] < best["cpu_ms_per_frame"]:
             best = r
