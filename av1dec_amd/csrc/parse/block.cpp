@@ -285,6 +285,17 @@ struct MvStack {
     uint8_t drl_ctx[kMaxRefMvStack + 1] = {};
 };
 
+// extraSearch's candidate lists: never more than 2 entries, kept on the stack
+struct MvList2 {
+    Mv v[2];
+    size_t n = 0;
+    size_t size() const { return n; }
+    void push_back(const Mv& m) { v[n++] = m; }
+    const Mv& operator[](size_t i) const { return v[i]; }
+    const Mv* begin() const { return v; }
+    const Mv* end() const { return v + n; }
+};
+
 class BlockParser {
 public:
     BlockParser(Parser& p, TileCtx& t) : P(p), T(t), fh(p.fh), seq(p.seq), sd(t.sd), cdf(t.tcdf) {}
@@ -302,6 +313,7 @@ private:
     std::vector<int> quant;  // Quant[] of the transform block being parsed
     // coefficient levels while parsing them, padded (coeffs()): level << 8 | min(level, 3)
     uint16_t lvl[36 * 36] = {};
+    uint16_t nzc[1024];  // the scan indices of a transform block's non-zero levels, last first
 
     int S(uint16_t* c, int n) { return sd.read(c, n); }  // (every size through readN: 20.27 -> 20.45 ms/frame, r05_ab_lf_spec.txt)
     template <int N>
@@ -349,10 +361,8 @@ private:
     void search_stack(const Blk& b, MvStack& s, int mvRow, int mvCol, int candList, uint32_t weight);
     void search_compound_stack(const Blk& b, MvStack& s, int mvRow, int mvCol, uint32_t weight);
     void temporal_scan(const Blk& b, MvStack& s);
-    void add_tpl_ref_mv(const Blk& b, MvStack& s, int deltaRow, int deltaCol);
     void extra_search(const Blk& b, MvStack& s);
-    void add_extra_mv_candidate(const Blk& b, MvStack& s, int mvRow, int mvCol, std::vector<Mv>* idMvs,
-                                std::vector<Mv>* diffMvs);
+    void add_extra_mv_candidate(const Blk& b, MvStack& s, int mvRow, int mvCol, MvList2* idMvs, MvList2* diffMvs);
     // local warp
     void find_warp_samples(Blk& b);
     void add_sample(Blk& b, int deltaRow, int deltaCol);
@@ -535,9 +545,20 @@ void BlockParser::decode_block(int r, int c, int bsize)
     const bool isCompound = b.ref[1] > INTRA_FRAME;
     PROF_T(t1);
     PROF_ADD(0, t0, t1);
-    for (int y = 0; y < b.bh4; y++)
+    uint32_t palIdx = ~0u;
+    if (b.pal_y || b.pal_uv) {
+        palIdx = (uint32_t)T.pal_colors.size();
+        std::vector<uint8_t> cols(16, 0);
+        for (int i = 0; i < b.pal_y; i++) cols[i] = b.colors[0][i];
+        for (int i = 0; i < b.pal_uv; i++) cols[8 + i] = b.colors[1][i];
+        T.pal_colors.push_back(cols);
+    }
+    // the block's mode info into every 4x4 unit it covers, in one pass (the residual below
+    // reads only the units' transform sizes and types)
+    for (int y = 0; y < b.bh4; y++) {
+        MiInfo* row = &mi(r + y, c);
         for (int x = 0; x < b.bw4; x++) {
-            MiInfo& m = mi(r + y, c + x);
+            MiInfo& m = row[x];
             m.y_mode = (uint8_t)b.y_mode;
             if (b.ref[0] == INTRA_FRAME && b.has_chroma) m.uv_mode = (uint8_t)b.uv_mode;
             m.ref[0] = (int8_t)b.ref[0];
@@ -551,24 +572,6 @@ void BlockParser::decode_block(int r, int c, int bsize)
                 m.interp[1] = (uint8_t)b.interp[1];
                 for (int l = 0; l < 1 + isCompound; l++) m.mv[l] = b.mv[l];
             }
-        }
-    PROF_T(t2);
-    residual(b);
-    PROF_T(t3);
-    PROF_ADD(2, t1, t2);
-    PROF_ADD(1, t2, t3);
-    if (!T.err.empty()) return;
-    uint32_t palIdx = ~0u;
-    if (b.pal_y || b.pal_uv) {
-        palIdx = (uint32_t)T.pal_colors.size();
-        std::vector<uint8_t> cols(16, 0);
-        for (int i = 0; i < b.pal_y; i++) cols[i] = b.colors[0][i];
-        for (int i = 0; i < b.pal_uv; i++) cols[8 + i] = b.colors[1][i];
-        T.pal_colors.push_back(cols);
-    }
-    for (int y = 0; y < b.bh4; y++)
-        for (int x = 0; x < b.bw4; x++) {
-            MiInfo& m = mi(r + y, c + x);
             m.is_inter = b.is_inter;
             m.skip_mode = b.skip_mode;
             m.skip = b.skip;
@@ -576,13 +579,20 @@ void BlockParser::decode_block(int r, int c, int bsize)
             m.pal_size[0] = (uint8_t)b.pal_y;
             m.pal_size[1] = (uint8_t)b.pal_uv;
             m.pal_idx = palIdx;
-            if (P.emit_mi)
-                for (int i = 0; i < 4; i++) P.mi_dlf[((size_t)(r + y) * P.mi_stride + c + x) * 4 + i] = (int8_t)T.delta_lf[i];
         }
+        if (P.emit_mi)
+            for (int x = 0; x < b.bw4; x++)
+                for (int i = 0; i < 4; i++) P.mi_dlf[((size_t)(r + y) * P.mi_stride + c + x) * 4 + i] = (int8_t)T.delta_lf[i];
+    }
+    PROF_T(t2);
+    residual(b);
+    PROF_T(t3);
+    PROF_ADD(2, t1, t2);
+    PROF_ADD(1, t2, t3);
+    if (!T.err.empty()) return;
     PROF_T(t4);
     emit(b);
     PROF_T(t5);
-    PROF_ADD(2, t3, t4);
     PROF_ADD(3, t4, t5);
 }
 
@@ -1349,73 +1359,74 @@ void BlockParser::scan_point(const Blk& b, MvStack& s, int deltaRow, int deltaCo
     if (inside(mvRow, mvCol)) add_ref_mv_candidate(b, s, mvRow, mvCol, 4);
 }
 
-void BlockParser::add_tpl_ref_mv(const Blk& b, MvStack& s, int deltaRow, int deltaCol)
-{
-    const int mvRow = (b.r + deltaRow) | 1, mvCol = (b.c + deltaCol) | 1;
-    if (!inside(mvRow, mvCol)) return;
-    const int x8 = mvCol >> 1, y8 = mvRow >> 1;
-    const size_t at = (size_t)y8 * (fh.aligned_mi_cols >> 1) + x8;
-    if (deltaRow == 0 && deltaCol == 0) s.zero_ctx = 1;
-    const bool isCompound = b.ref[1] > INTRA_FRAME;
-    if (!isCompound) {
-        Mv cand = P.motion_field[b.ref[0]][at];
-        if (cand.r == (int16_t)INT16_MIN) return;
-        lower_mv_precision(cand);
-        if (deltaRow == 0 && deltaCol == 0)
-            s.zero_ctx = (abs(cand.r - s.global[0].r) >= 16 || abs(cand.c - s.global[0].c) >= 16) ? 1 : 0;
-        int idx;
-        for (idx = 0; idx < s.num; idx++)
-            if (cand.r == s.stack[idx][0].r && cand.c == s.stack[idx][0].c) break;
-        if (idx < s.num) {
-            s.weight[idx] += 2;
-        } else if (s.num < kMaxRefMvStack) {
-            s.stack[s.num][0] = cand;
-            s.weight[s.num] = 2;
-            s.num++;
-        }
-    } else {
-        Mv c0 = P.motion_field[b.ref[0]][at];
-        if (c0.r == (int16_t)INT16_MIN) return;
-        Mv c1 = P.motion_field[b.ref[1]][at];
-        if (c1.r == (int16_t)INT16_MIN) return;
-        lower_mv_precision(c0);
-        lower_mv_precision(c1);
-        if (deltaRow == 0 && deltaCol == 0)
-            s.zero_ctx = (abs(c0.r - s.global[0].r) >= 16 || abs(c0.c - s.global[0].c) >= 16 ||
-                          abs(c1.r - s.global[1].r) >= 16 || abs(c1.c - s.global[1].c) >= 16)
-                             ? 1
-                             : 0;
-        int idx;
-        for (idx = 0; idx < s.num; idx++)
-            if (c0 == s.stack[idx][0] && c1 == s.stack[idx][1]) break;
-        if (idx < s.num) {
-            s.weight[idx] += 2;
-        } else if (s.num < kMaxRefMvStack) {
-            s.stack[s.num][0] = c0;
-            s.stack[s.num][1] = c1;
-            s.weight[s.num] = 2;
-            s.num++;
-        }
-    }
-}
-
+// add_tpl_ref_mv (InterPredict.cpp:1051-1126) for every position of temporalScan
+// (InterPredict.cpp:1128-1153), with the block's invariants hoisted (the reference lists'
+// motion fields, the compound test) and the last stack entry a position matched (neighbouring positions mostly project the
+// same motion vector; the stack holds distinct entries, so a match there is the match the
+// spec's linear search finds)
 void BlockParser::temporal_scan(const Blk& b, MvStack& s)
 {
     const int stepW4 = b.bw4 >= 16 ? 4 : 2, stepH4 = b.bh4 >= 16 ? 4 : 2;
+    const bool isCompound = b.ref[1] > INTRA_FRAME;
+    const Mv* mf0 = P.motion_field[b.ref[0]].data();
+    const Mv* mf1 = isCompound ? P.motion_field[b.ref[1]].data() : nullptr;
+    const size_t stride8 = (size_t)(fh.aligned_mi_cols >> 1);
+    int last = -1;
+    auto add = [&](int deltaRow, int deltaCol) {
+        const int mvRow = (b.r + deltaRow) | 1, mvCol = (b.c + deltaCol) | 1;
+        if (!inside(mvRow, mvCol)) return;
+        const size_t at = (size_t)(mvRow >> 1) * stride8 + (mvCol >> 1);
+        const bool origin = deltaRow == 0 && deltaCol == 0;
+        if (origin) s.zero_ctx = 1;
+        Mv c0 = mf0[at];
+        if (c0.r == (int16_t)INT16_MIN) return;
+        Mv c1 = {0, 0};
+        if (isCompound) {
+            c1 = mf1[at];
+            if (c1.r == (int16_t)INT16_MIN) return;
+            lower_mv_precision(c1);
+        }
+        lower_mv_precision(c0);
+        if (origin)
+            s.zero_ctx = (abs(c0.r - s.global[0].r) >= 16 || abs(c0.c - s.global[0].c) >= 16 ||
+                          (isCompound && (abs(c1.r - s.global[1].r) >= 16 || abs(c1.c - s.global[1].c) >= 16)))
+                             ? 1
+                             : 0;
+        auto same = [&](int idx) { return c0 == s.stack[idx][0] && (!isCompound || c1 == s.stack[idx][1]); };
+        int idx = -1;
+        if (last >= 0 && same(last)) {
+            idx = last;
+        } else {
+            for (int i = 0; i < s.num; i++)
+                if (same(i)) {
+                    idx = i;
+                    break;
+                }
+        }
+        if (idx >= 0) {
+            s.weight[idx] += 2;
+            last = idx;
+        } else if (s.num < kMaxRefMvStack) {
+            s.stack[s.num][0] = c0;
+            if (isCompound) s.stack[s.num][1] = c1;
+            s.weight[s.num] = 2;
+            last = s.num++;
+        }
+    };
     for (int dr = 0; dr < std::min(b.bh4, 16); dr += stepH4)
-        for (int dc = 0; dc < std::min(b.bw4, 16); dc += stepW4) add_tpl_ref_mv(b, s, dr, dc);
+        for (int dc = 0; dc < std::min(b.bw4, 16); dc += stepW4) add(dr, dc);
     const bool allowExtension = b.bh4 >= 2 && b.bh4 < 16 && b.bw4 >= 2 && b.bw4 < 16;
     if (allowExtension) {
         const int pos[3][2] = {{b.bh4, -2}, {b.bh4, b.bw4}, {b.bh4 - 2, b.bw4}};
         for (auto& p : pos) {
             const int row = (b.r & 15) + p[0], col = (b.c & 15) + p[1];
-            if (row >= 0 && row < 16 && col >= 0 && col < 16) add_tpl_ref_mv(b, s, p[0], p[1]);
+            if (row >= 0 && row < 16 && col >= 0 && col < 16) add(p[0], p[1]);
         }
     }
 }
 
-void BlockParser::add_extra_mv_candidate(const Blk& b, MvStack& s, int mvRow, int mvCol, std::vector<Mv>* idMvs,
-                                         std::vector<Mv>* diffMvs)
+void BlockParser::add_extra_mv_candidate(const Blk& b, MvStack& s, int mvRow, int mvCol, MvList2* idMvs,
+                                         MvList2* diffMvs)
 {
     const MiInfo& m = mi(mvRow, mvCol);
     if (b.ref[1] > INTRA_FRAME) {
@@ -1458,7 +1469,7 @@ void BlockParser::add_extra_mv_candidate(const Blk& b, MvStack& s, int mvRow, in
 
 void BlockParser::extra_search(const Blk& b, MvStack& s)
 {
-    std::vector<Mv> idMvs[2], diffMvs[2];
+    MvList2 idMvs[2], diffMvs[2];  // at most 2 each (the spec's idMvs / diffMvs)
     int w4 = std::min(16, b.bw4), h4 = std::min(16, b.bh4);
     w4 = std::min(w4, fh.mi_cols - b.c);
     h4 = std::min(h4, fh.mi_rows - b.r);
@@ -1474,7 +1485,7 @@ void BlockParser::extra_search(const Blk& b, MvStack& s)
         }
     }
     if (b.ref[1] > INTRA_FRAME) {
-        std::vector<Mv> comb[2];
+        MvList2 comb[2];
         for (int list = 0; list < 2; list++) {
             for (const Mv& m : idMvs[list]) comb[list].push_back(m);
             for (size_t i = 0; i < diffMvs[list].size() && comb[list].size() < 2; i++) comb[list].push_back(diffMvs[list][i]);
@@ -2268,6 +2279,7 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         uint16_t* const cbr = cdf.coef.coeff_br[std::min(txSzCtx, 3)][ptype][0];
         constexpr int kCbStride = sizeof(cdf.coef.coeff_base[0][0][0]) / sizeof(uint16_t);
         constexpr int kBrStride = sizeof(cdf.coef.coeff_br[0][0][0]) / sizeof(uint16_t);
+        int nnz = 0;
         for (int c = eob - 1; c >= 0; c--) {
             const ScanEntry e = se[c];
             uint16_t* lp = &lvl[e.pad];
@@ -2297,19 +2309,22 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             }
             quant[e.pos] = level;
             *lp = (uint16_t)(level << 8 | std::min(level, 3));
+            nzc[nnz] = (uint16_t)c;
+            nnz += level != 0;
         }
         for (int c = 0; c < eob; c++) lvl[se[c].pad] = 0;  // back to all zero for the next transform block
         (void)height;
         PROF_T(c3);
         PROF_ADD(6, c2, c3);
-        // signs and Golomb remainders, in scan order; the non-zero positions also into a
-        // bitmap of rows (the packing below walks only them)
+        // signs and Golomb remainders of the non-zero levels, in scan order (nzc from its end);
+        // the non-zero positions also into a bitmap of rows (the packing below walks only them)
         const int twl = av1r_tx_w_log2[txSz] < 5 ? av1r_tx_w_log2[txSz] : 5;  // log2(tw)
         uint32_t nzRow[32] = {};
-        for (int c = 0; c < eob; c++) {
+        for (int q = nnz - 1; q >= 0; q--) {
+            const int c = nzc[q];
             const int pos = se[c].pos;
             bool sign = false;
-            if (quant[pos]) {
+            {
                 if (c == 0) {
                     int maxX4 = fh.mi_cols, maxY4 = fh.mi_rows;
                     if (plane) {
@@ -2369,7 +2384,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         // packed non-zero coefficients (refdump.cpp dumpBlock), Quant[] layout i * tw + j, in
         // raster order (the rows' bitmaps, lowest bit first), cleared again
         std::vector<uint32_t>& out = T.coefs;
-        for (int i = 0; i < 32; i++) {
+        out.resize(t.coef_off + nnz);
+        uint32_t* o = out.data() + t.coef_off;
+        const int th = std::min(h, 32);  // the coded rows
+        for (int i = 0; i < th; i++) {
             int* row = &quant[i * tw];
             for (uint32_t m = nzRow[i]; m; m &= m - 1) {
                 const int j = __builtin_ctz(m);
@@ -2379,9 +2397,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                     T.fail(AV1R_E_UNSUPPORTED, "coefficient out of packable range");
                     return 0;
                 }
-                out.push_back(((uint32_t)v << 10) | (uint32_t)(i * tw + j));
+                *o++ = ((uint32_t)v << 10) | (uint32_t)(i * tw + j);
             }
         }
+        out.resize((size_t)(o - out.data()));
         t.coef_cnt = (uint32_t)out.size() - t.coef_off;
 #ifdef AV1P_PROF
         {

@@ -628,23 +628,27 @@ bool Parser::mv_project(int src, int dstSign)
         v8 += sign * off8;
         return !(v8 < 0 || v8 >= max8 || v8 < base8 - maxOff8 || v8 >= base8 + 8 + maxOff8);
     };
+    // the order-hint distances, once per call rather than per unit
+    const int refToCur = relative_dist(fh.order_hints[src], fh.order_hint);
+    int refOffsetOf[8], refToDst[8];
+    for (int k = 0; k < 8; k++) refOffsetOf[k] = relative_dist(fh.order_hints[src], r.saved_order_hints[k]);
+    for (int dst = LAST_FRAME; dst <= ALTREF_FRAME; dst++) refToDst[dst] = relative_dist(fh.order_hint, fh.order_hints[dst]);
+    Mv* mf[8];
+    for (int dst = LAST_FRAME; dst <= ALTREF_FRAME; dst++) mf[dst] = motion_field[dst].data();
     for (int y8 = 0; y8 < h8; y8++)
         for (int x8 = 0; x8 < w8; x8++) {
             const int row = 2 * y8 + 1, col = 2 * x8 + 1;
             const int srcRef = r.mf_ref[(size_t)row * r.mi_cols + col];
             if (srcRef <= INTRA_FRAME) continue;
-            const int refToCur = relative_dist(fh.order_hints[src], fh.order_hint);
-            const int refOffset = relative_dist(fh.order_hints[src], r.saved_order_hints[srcRef]);
+            const int refOffset = refOffsetOf[srcRef];
             if (!(abs(refToCur) <= AV1R_MAX_FRAME_DISTANCE && abs(refOffset) <= AV1R_MAX_FRAME_DISTANCE && refOffset > 0))
                 continue;
             const Mv mv = r.mf_mv[(size_t)row * r.mi_cols + col];
             Mv proj = mv_projection(mv, refToCur * dstSign, refOffset);
             int px = x8, py = y8;
             if (!(project(px, proj.c, dstSign, w8, 8) && project(py, proj.r, dstSign, h8, 0))) continue;
-            for (int dst = LAST_FRAME; dst <= ALTREF_FRAME; dst++) {
-                const int refToDst = relative_dist(fh.order_hint, fh.order_hints[dst]);
-                motion_field[dst][(size_t)py * mfw + px] = mv_projection(mv, refToDst, refOffset);
-            }
+            for (int dst = LAST_FRAME; dst <= ALTREF_FRAME; dst++)
+                mf[dst][(size_t)py * mfw + px] = mv_projection(mv, refToDst[dst], refOffset);
         }
     return true;
 }
@@ -1044,13 +1048,16 @@ int Parser::finish_frame()
     }
     F.cdef = cdef_idx;
     F.lr = lr_units;
-    // motion vector storage (Parser.cpp:1699-1720)
+    // motion vector storage (Parser.cpp:1699-1720); which references lie behind this frame,
+    // once per frame rather than per unit
+    bool behind[8] = {};
+    for (int r = INTRA_FRAME + 1; r < 8; r++) behind[r] = relative_dist(fh.order_hints[r], fh.order_hint) < 0;
     for (int row = 0; row < fh.mi_rows; row++)
         for (int col = 0; col < fh.mi_cols; col++) {
             const MiInfo& m = mi_at(row, col);
             for (int list = 0; list < 2; list++) {
                 const int r = m.ref[list];
-                if (r > INTRA_FRAME && relative_dist(fh.order_hints[r], fh.order_hint) < 0) {
+                if (r > INTRA_FRAME && behind[r]) {
                     const int lim = (1 << 12) - 1;
                     if (abs(m.mv[list].r) <= lim && abs(m.mv[list].c) <= lim) {
                         mf_ref[(size_t)row * fh.mi_cols + col] = (int8_t)r;

@@ -201,6 +201,28 @@ struct SymbolDecoder {
             return s;
         }
 #endif
+#if !defined(AV1P_WRITER) && !defined(AV1P_TRACE)
+        // the alphabets the syntax uses, each as readN (branch-free interval search, unrolled
+        // adaptation): the loop below mispredicts once per symbol on the larger ones
+        switch (nsym) {
+        case 2: return readN<2>(cdf);
+        case 3: return readN<3>(cdf);
+        case 4: return readN<4>(cdf);
+        case 5: return readN<5>(cdf);
+        case 6: return readN<6>(cdf);
+        case 7: return readN<7>(cdf);
+        case 8: return readN<8>(cdf);
+        case 9: return readN<9>(cdf);
+        case 10: return readN<10>(cdf);
+        case 11: return readN<11>(cdf);
+        case 12: return readN<12>(cdf);
+        case 13: return readN<13>(cdf);
+        case 14: return readN<14>(cdf);
+        case 15: return readN<15>(cdf);
+        case 16: return readN<16>(cdf);
+        default: break;
+        }
+#endif
         const uint32_t c = (uint32_t)(dif >> 48);
         uint32_t cur = range, prev;
         int sym = -1;
