@@ -268,9 +268,14 @@ struct SymbolDecoder {
         if (!noUpdate) {
             const int cnt = cdf[N];
             const int rate = 3 + (cnt > 15) + (cnt > 31) + (N >= 4 ? 2 : N >= 2 ? 1 : 0);
+            // branch-free: the symbol decides the direction of every entry, and a branch on
+            // it mispredicts as often as the symbol changes
 #pragma GCC unroll 16
-            for (int i = 0; i < N - 1; i++)
-                cdf[i] = i < sym ? cdf[i] + (uint16_t)((32768u - cdf[i]) >> rate) : cdf[i] - (uint16_t)(cdf[i] >> rate);
+            for (int i = 0; i < N - 1; i++) {
+                const uint32_t m = 0u - (uint32_t)(i < sym);
+                const uint32_t up = (32768u - cdf[i]) >> rate, dn = (uint32_t)cdf[i] >> rate;
+                cdf[i] = (uint16_t)(cdf[i] + ((up & m) - (dn & ~m)));
+            }
             cdf[N] += cdf[N] < 32;
         }
         return sym;
@@ -290,15 +295,12 @@ struct SymbolDecoder {
     {
 #if !defined(AV1P_WRITER) && !defined(AV1P_TRACE)
         // read() over the CDF {16384, 0}: the first interval boundary, then the same renormalisation
+        // (selects, not a branch: these bits are close to random)
         const uint32_t v0 = ((range >> 8) << 7) + 4;
-        if ((uint32_t)(dif >> 48) >= v0) {
-            range -= v0;
-            renorm(dif - ((uint64_t)v0 << 48));
-            return 0;
-        }
-        range = v0;
-        renorm(dif);
-        return 1;
+        const bool one = (uint32_t)(dif >> 48) < v0;
+        range = one ? v0 : range - v0;
+        renorm(one ? dif : dif - ((uint64_t)v0 << 48));
+        return one;
 #endif
         uint16_t c[3] = {16384, 0, 0};
         const bool nu = noUpdate;
