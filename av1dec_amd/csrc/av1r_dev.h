@@ -119,6 +119,21 @@ static_assert(offsetof(av1r_block, max_luma_h) == 30 && offsetof(DevBlock, max_l
 static_assert(offsetof(av1r_block, mv) + 16 == sizeof(av1r_block) && offsetof(DevBlock, mv) + 16 == sizeof(DevBlock),
     "DevBlock tail");
 
+// The device's transform-block record (16 bytes against av1r_tb's 20, pack_frame): the
+// same fields, the small ones as bit-fields, and the coefficient width: a TB whose levels all
+// fit 6 signed bits (nearly every one) keeps its coefficients as 16-bit words in
+// KParams::coefs16, the others as av1r_tb's 32-bit words in KParams::coefs (coef_off indexes
+// the array its width selects; coef_at below reads either as the 32-bit form).
+#define AV1R_TBD_WIDE 16u  // flags bit (device only; WorkItem::flags too)
+struct DevTb {
+    uint32_t block;
+    uint32_t coef_off;
+    uint16_t x, y;
+    uint16_t coef_cnt;
+    uint16_t plane : 2, tx_size : 5, tx_type : 4, flags : 5;
+};
+static_assert(sizeof(DevTb) == 16, "DevTb layout");
+
 // Everything the stage kernels read about one frame.  A launch covers n frames (one per
 // stream of a batch): the kernels receive a device array of n KParams and pick theirs
 // by blockIdx (see k_level / k_lf / k_cdef / k_lr).
@@ -130,8 +145,9 @@ struct KParams {
     uint8_t* lfc;
     const DevBlock* blocks;
     const int32_t* bext;  // LOCAL_VALID / INTERINTRA blocks' warp parameters and TB range, 8 words each (DevBlock)
-    const av1r_tb* tbs;
-    const uint32_t* coefs;
+    const DevTb* tbs;
+    const uint32_t* coefs;    // the coefficients of the wide TBs (AV1R_TBD_WIDE), av1r_tb's form
+    const uint16_t* coefs16;  // everyone else's: (level << 10 | pos) as int16 (|level| < 32)
     const uint8_t* palette;
     const int8_t* cdef_idx;
     const av1r_lr_unit* lr;
@@ -169,6 +185,13 @@ struct KParams {
     DevFrame lrout;   // loop-restoration output (LoopRestoration.cpp:216)
     DevFrame ref[8];  // reference store slots
 };
+
+// Coefficient q of a TB whose first coefficient is `off` (DevTb / WorkItem coef_off), in
+// av1r_tb's 32-bit form: a 16-bit word (level << 10 | pos, |level| < 32) sign-extends to it.
+DEV uint32_t coef_at(const KParams& k, uint32_t off, uint32_t flags, int q)
+{
+    return (flags & AV1R_TBD_WIDE) ? k.coefs[off + q] : (uint32_t)(int32_t)(int16_t)k.coefs16[off + q];
+}
 
 // launch batches: at most AV1R_MAX_BATCH frames per launch
 #define AV1R_MAX_BATCH 32

@@ -213,6 +213,13 @@ struct av1r_ctx {
     int mapW[3] = {}, mapH[3] = {};
     std::vector<std::vector<uint32_t>> lvP, lvB, lvT;  // inter tiles, inter-intra blends, TBs per level
     std::vector<WorkItem> items;  // transform blocks and inter-intra blends
+    // pack_frame, from its size pass for its packing pass: whether any TB has a level that
+    // needs more than 6 signed bits, and then per TB its width (AV1R_TBD_WIDE) and a wide
+    // TB's offset in the 32-bit array
+    bool anyWide = false;
+    std::vector<uint32_t> tbCoefOff;
+    std::vector<uint8_t> tbWide;
+    size_t nCoef32 = 0;
     std::vector<uint32_t> tiles;  // inter tiles (codes): Level::off[0] indexes them
     std::vector<Level> levels;
     // k_flow dependencies: per 4x4 unit the node (TB / inter-intra item, decode order) that
@@ -1435,8 +1442,37 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     for (uint32_t i = 0; i < b->n_blocks; i++) nExt += (b->blocks[i].flags & extFlags) != 0;
     const size_t szBlk = align256(sizeof(DevBlock) * (size_t)b->n_blocks);
     const size_t szExt = align256(32 * nExt + 4);
-    const size_t szTb = align256(sizeof(av1r_tb) * (size_t)b->n_tbs);
-    const size_t szCoef = align256(4 * (size_t)b->n_coefs);
+    const size_t szTb = align256(sizeof(DevTb) * (size_t)b->n_tbs);
+    if (!host) {
+        // the coefficient widths: 16 bits when a level fits 6 signed bits, i.e. (level << 10
+        // | pos) fits int16.  One vectorised OR over the whole array first; only a frame with
+        // some wider level classifies its TBs
+        const uint32_t* cf = b->coefs;
+        uint32_t out = 0;
+        for (uint32_t q = 0; q < b->n_coefs; q++) out |= (cf[q] + 0x8000u) >> 16;
+        c->anyWide = out != 0;
+        c->nCoef32 = 0;
+        if (c->anyWide) {
+            c->tbCoefOff.resize(b->n_tbs);
+            c->tbWide.resize(b->n_tbs);
+            size_t n32 = 0;
+            for (uint32_t i = 0; i < b->n_tbs; i++) {
+                const av1r_tb& t = b->tbs[i];
+                uint32_t o = 0;
+                for (uint32_t q = 0; q < t.coef_cnt; q++) o |= (cf[t.coef_off + q] + 0x8000u) >> 16;
+                c->tbWide[i] = o != 0;
+                c->tbCoefOff[i] = (uint32_t)n32;
+                if (o) n32 += t.coef_cnt;
+            }
+            c->nCoef32 = n32;
+        }
+    } else if (c->anyWide && c->tbWide.size() != b->n_tbs) {
+        return fail(c, AV1R_E_INVALID, "pack without its size pass");
+    }
+    // every coefficient in 16 bits at its own index (a wide TB's there are truncated and
+    // unread), the wide TBs' again in 32 bits
+    const size_t szCoef = align256(4 * c->nCoef32 + 4);
+    const size_t szCoef16 = align256(2 * (size_t)b->n_coefs + 4);
     const size_t szPal = align256(b->n_palette);
     const size_t szCdef = align256((size_t)h->cdef_rows * h->cdef_cols);
     const size_t szLr = align256(sizeof(av1r_lr_unit) * (size_t)b->n_lr_units);
@@ -1448,12 +1484,12 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szExt + szTb + szCoef + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
+    *need = szHdr + szBlk + szExt + szTb + szCoef + szCoef16 + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
         fprintf(stderr, "av1r pack: blocks %zu tbs %zu coefs %zu items %zu (%zu) deps %zu done %zu tbres %zu resid %zu lr %zu levels %zu\n", szBlk,
-            szTb, szCoef, szItems, c->items.size(), szDeps, szDone, szTbRes, szResS + szResL, szLr, c->levels.size());
+            szTb, szCoef + szCoef16, szItems, c->items.size(), szDeps, szDone, szTbRes, szResS + szResL, szLr, c->levels.size());
         // k_flow items (large, small) per level: the first levels, then the rest
         uint32_t rest[2] = {};
         for (size_t l = 0; l < c->levels.size(); l++) {
@@ -1494,12 +1530,66 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
             }
         }
     }
-    k.tbs = (const av1r_tb*)put(b->tbs, sizeof(av1r_tb) * (size_t)b->n_tbs, szTb);
-    k.coefs = (const uint32_t*)put(b->coefs, 4 * (size_t)b->n_coefs, szCoef);
+    {
+        // the TBs in the device's record, their coefficients split by width (the size pass's
+        // classification)
+        DevTb* dt = reinterpret_cast<DevTb*>(host + off);
+        k.tbs = (const DevTb*)put(nullptr, 0, szTb);
+        uint32_t* c32 = reinterpret_cast<uint32_t*>(host + off);
+        k.coefs = (const uint32_t*)put(nullptr, 0, szCoef);
+        uint16_t* c16 = reinterpret_cast<uint16_t*>(host + off);
+        k.coefs16 = (const uint16_t*)put(nullptr, 0, szCoef16);
+        for (uint32_t q = 0; q < b->n_coefs; q++) c16[q] = (uint16_t)b->coefs[q];
+        for (uint32_t i = 0; i < b->n_tbs; i++) {
+            const av1r_tb& t = b->tbs[i];
+            const bool wide = c->anyWide && c->tbWide[i];
+            DevTb d;  // (composed in registers, stored whole)
+            d.block = t.block;
+            d.coef_off = wide ? c->tbCoefOff[i] : t.coef_off;
+            d.x = t.x;
+            d.y = t.y;
+            d.coef_cnt = t.coef_cnt;
+            d.plane = t.plane;
+            d.tx_size = t.tx_size;
+            d.tx_type = t.tx_type;
+            d.flags = (t.flags & 15u) | (wide ? AV1R_TBD_WIDE : 0u);
+            dt[i] = d;
+            if (wide) memcpy(c32 + c->tbCoefOff[i], b->coefs + t.coef_off, 4 * (size_t)t.coef_cnt);
+        }
+    }
     k.palette = put(b->palette, b->n_palette, szPal);
     k.cdef_idx = (const int8_t*)put(b->cdef_idx, (size_t)h->cdef_rows * h->cdef_cols, szCdef);
     k.lr = (const av1r_lr_unit*)put(b->lr_units, sizeof(av1r_lr_unit) * (size_t)b->n_lr_units, szLr);
-    P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
+    static const bool verify = getenv("AV1R_PACK_VERIFY") != nullptr;
+    if (verify) {  // (AV1R_PACK_VERIFY, tests/test_abi.py) the device records read back as the kernels read them
+        const DevTb* dt = reinterpret_cast<const DevTb*>(host + ((const uint8_t*)k.tbs - dev));
+        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(host + ((const uint8_t*)k.coefs - dev));
+        const uint16_t* c16 = reinterpret_cast<const uint16_t*>(host + ((const uint8_t*)k.coefs16 - dev));
+        for (uint32_t i = 0; i < b->n_tbs; i++) {
+            const av1r_tb& t = b->tbs[i];
+            const DevTb& d = dt[i];
+            if (d.block != t.block || d.x != t.x || d.y != t.y || d.coef_cnt != t.coef_cnt || d.plane != t.plane ||
+                d.tx_size != t.tx_size || d.tx_type != t.tx_type || (d.flags & 15u) != t.flags)
+                return fail(c, AV1R_E_INVALID, "pack verify: tb %u fields", i);
+            for (uint32_t q = 0; q < t.coef_cnt; q++) {
+                const uint32_t v = (d.flags & AV1R_TBD_WIDE) ? c32[d.coef_off + q] : (uint32_t)(int32_t)(int16_t)c16[d.coef_off + q];
+                if (v != b->coefs[t.coef_off + q]) return fail(c, AV1R_E_INVALID, "pack verify: tb %u coefficient %u", i, q);
+            }
+        }
+    }
+    {
+        // the items' coefficient references follow their TBs' (offset and width)
+        WorkItem* wi = reinterpret_cast<WorkItem*>(host + off);
+        P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
+        for (size_t i = 0; c->anyWide && i < c->items.size(); i++) {
+            const uint32_t code = wi[i].code;
+            if (AV1R_ITEM_KIND(code) != AV1R_ITEM_TB) continue;
+            const uint32_t ti = AV1R_ITEM_INDEX(code);
+            if (!c->tbWide[ti]) continue;
+            wi[i].coef_off = c->tbCoefOff[ti];
+            wi[i].flags |= AV1R_TBD_WIDE;
+        }
+    }
     k.tiles = (const uint32_t*)put(c->tiles.data(), 4 * c->tiles.size(), szTiles);
     k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);
     k.tb_res = (const uint32_t*)put(c->tbRes.data(), 4 * c->tbRes.size(), szTbRes);
@@ -1510,6 +1600,20 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.n_items = (uint32_t)c->items.size();
     k.mi = (const av1r_mi*)put(nullptr, 0, szMi);
     k.lfc = (uint8_t*)put(nullptr, 0, szLfc);
+    if (verify) {
+        // every section placed, in order, inside the buffer (a section left out of the
+        // packing sequence keeps the null of the memset: below the header's successors)
+        const void* secs[] = {k.hdr, k.blocks, k.bext, k.tbs, k.coefs, k.coefs16, k.palette, k.cdef_idx, k.lr, P.dItems,
+                              k.tiles, k.deps, k.tb_res, k.resid_s, k.resid_l, k.done, k.mi, k.lfc};
+        const uint8_t* prev = dev;
+        for (size_t i = 0; i < sizeof(secs) / sizeof(secs[0]); i++) {
+            const uint8_t* q = (const uint8_t*)secs[i];
+            if (q < prev || (size_t)(q - dev) >= off)  // (empty sections may share an offset)
+                return fail(c, AV1R_E_INVALID, "pack verify: section %zu misplaced", i);
+            prev = q;
+        }
+        if (off != *need) return fail(c, AV1R_E_INVALID, "pack verify: %zu bytes packed, %zu sized", off, *need);
+    }
     P.flowOk = c->flowOk;
     k.gran = c->flowOk && c->granOk;
     for (int p = 0; p < 3; p++) {
@@ -1584,7 +1688,7 @@ static int job_begin(FrameJob& j)
         auto rb = [&](auto& ptr) {
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
-        rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.bext), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.palette), rb(j.k.cdef_idx);
+        rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.bext), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.coefs16), rb(j.k.palette), rb(j.k.cdef_idx);
         rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
     }
     for (int s = 0; s < 8; s++)
@@ -2190,7 +2294,7 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
         HIPCHK(hipMalloc(&U.dev, cap));
         U.cap = cap;
     }
-    pack_frame(c, b, P, U.host, U.dev, &need);
+    if (int prc = pack_frame(c, b, P, U.host, U.dev, &need)) return prc;
     HIPCHK(hipMemcpyAsync(U.dev, U.host, P.upBytes, hipMemcpyHostToDevice, c->stream));
     rc = launch_frame(c, P);
     if (rc) return rc;
@@ -2457,7 +2561,11 @@ int av1r_prepare(av1r_ctx* c, const av1r_frame_batch* b, int* handle)
         }
         P->owned = true;
         P->cap = need;
-        pack_frame(c, b, *P, host.data(), P->dev, &need);
+        if (int prc = pack_frame(c, b, *P, host.data(), P->dev, &need)) {
+            (void)hipFree(P->dev);
+            delete P;
+            return prc;
+        }
         if (hipMemcpy(P->dev, host.data(), P->upBytes, hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(P->dev);
             delete P;
@@ -2648,7 +2756,10 @@ int av1r_pack(const av1r_frame_batch* b, av1r_packed** out)
     Prepared& P = pk->P;
     P = Prepared();
     P.hdr = *b->hdr;
-    pack_frame(c, b, P, pk->host, nullptr, &need);
+    if (int prc = pack_frame(c, b, P, pk->host, nullptr, &need)) {
+        av1r_packed_free(pk);
+        return prc;
+    }
     clk.lap(PP_COPY);
     if (g_packProf) g_packNs[PP_N]++;
     P.cap = need;

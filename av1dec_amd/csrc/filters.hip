@@ -1519,7 +1519,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mi_tbs(const KParams* kps)
     const KParams& k = KP(kps, blockIdx.y);
     const uint32_t ti = blockIdx.x * 16 + (threadIdx.x >> 4);
     if (ti >= k.n_tbs) return;
-    const av1r_tb& t = k.tbs[ti];
+    const DevTb& t = k.tbs[ti];
     const int sub = t.plane ? 1 : 0;
     const int row = (t.y << sub) >> 2, col = (t.x << sub) >> 2;
     const int w4 = (av1r_tx_w[t.tx_size] >> 2) << sub, h4 = (av1r_tx_h[t.tx_size] >> 2) << sub;

@@ -94,9 +94,8 @@ DEV void tb_residual(const KParams& k, const TB& tb, const DevBlock& blk, int16_
     const int acDelta = plane == 0 ? 0 : plane == 1 ? hd.delta_q_u_ac : hd.delta_q_v_ac;
     const int dcQ = av1r_dc_qlookup[CLIP3(0, 255, blk.qindex + dcDelta)];
     const int acQ = av1r_ac_qlookup[CLIP3(0, 255, blk.qindex + acDelta)];
-    const uint32_t* cf = k.coefs + tb.coef_off;
     for (int q = t; q < tb.coef_cnt; q += NT) {
-        const uint32_t c = q == t ? c0 : cf[q];  // the first NT were prefetched by the caller
+        const uint32_t c = q == t ? c0 : coef_at(k, tb.coef_off, tb.flags, q);  // the first NT were prefetched by the caller
         int pos = AV1R_COEF_POS(c), level = AV1R_COEF_LEVEL(c);
         int d = (int)((uint32_t)level * (uint32_t)(pos == 0 ? dcQ : acQ));
         int sign = d < 0 ? -1 : 1;
@@ -327,7 +326,7 @@ template <int NT, int MAX>
 DEV void tb_item(const KParams& k, const WorkItem& wi, TbLds<MAX>& L, unsigned long long* tr)
 {
     const int t = coop_lane<NT>();
-    const uint32_t c0 = t < wi.coef_cnt ? k.coefs[wi.coef_off + t] : 0u;
+    const uint32_t c0 = t < wi.coef_cnt ? coef_at(k, wi.coef_off, wi.flags, t) : 0u;
     const DevBlock& blk = k.blocks[wi.block];
     tb_predict<NT, MAX, false>(k, wi, blk, L);
     trace_stamp(tr, 4);
@@ -1323,7 +1322,7 @@ DEV void ii_item(const KParams& k, uint32_t bi, TbLds<64>& L, const GranEdges* G
             const int32_t* ext = k.bext + 8 * (size_t)blk.palette_off;
             const uint32_t firstTb = (uint32_t)ext[6], nTbs = (uint32_t)ext[7];
             for (uint32_t ti = firstTb; ti < firstTb + nTbs; ti++) {
-                const av1r_tb& tb = k.tbs[ti];
+                const DevTb& tb = k.tbs[ti];
                 if (tb.plane != plane || !tb.coef_cnt) continue;
                 const int tw = av1r_tx_w[tb.tx_size], th = av1r_tx_h[tb.tx_size];
                 const int16_t* rt = k.res + k.tb_res[ti];
@@ -2099,8 +2098,8 @@ DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
 {
     constexpr int RS = MAX + 2;
     const int t = coop_lane<NT>();
-    const av1r_tb& tb = k.tbs[ti];
-    const uint32_t c0 = t < tb.coef_cnt ? k.coefs[tb.coef_off + t] : 0u;
+    const DevTb& tb = k.tbs[ti];
+    const uint32_t c0 = t < tb.coef_cnt ? coef_at(k, tb.coef_off, tb.flags, t) : 0u;
     const DevBlock& blk = k.blocks[tb.block];
     const uint32_t ro = k.tb_res[ti];
     tb_residual<NT, MAX>(k, tb, blk, res, c0);

@@ -288,3 +288,35 @@ def test_frame_layout_describes_one_linear_read_back(native_lib):
         assert span.value == off[2] + st[2] * ((h >> 1) - 1) + (w >> 1)
     assert native_lib.av1r_frame_layout(0, 1080, st, off, C.byref(span)) == abi.AV1R_E_INVALID
     assert native_lib.av1r_frame_layout(1920, 1 << 20, st, off, C.byref(span)) == abi.AV1R_E_INVALID
+
+
+def test_pack_layout_verified():
+    """av1r_pack under AV1R_PACK_VERIFY=1 (read once per process, hence the child): every
+    section of the packed frame placed in order inside the buffer, and every device
+    transform-block record and coefficient (16-bit and 32-bit forms) read back as the kernels
+    read them equal to the batch's -- on streams with large levels (quantizer-00), palette,
+    loop restoration and intra block copy."""
+    import subprocess
+    import sys
+    code = r"""
+import sys
+sys.path.insert(0, %r)
+sys.path.insert(0, %r)
+import golden
+from av1dec_amd import Decoder, batchfile, native
+l = native.lib()
+n = 0
+for s in ("av1-1-b8-00-quantizer-00", "av1-1-b8-06-mfmv", "av1-1-b8-04-cdfupdate", "Halo_426x240_1frames_intrabc", "64x64"):
+    for fr in batchfile.load(golden.batch_path(s)):
+        if fr.show_existing:
+            continue
+        p = Decoder.pack(fr)
+        Decoder.free_packed(p)
+        n += 1
+print("packed", n)
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AV1R_PACK_VERIFY="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "packed" in r.stdout
+
