@@ -491,7 +491,15 @@ def measure(config, decs, streams, steps, warmup, workers, depth, dist, world, p
     fps = aggregate_fps(world, steps * S, elapsed)
     timed = [(j, t % F) for j in range(S) for t in range(pos0[j], pos0[j] + steps)]
     n_key = sum(1 for j, t in timed if streams[j][t].hdr.frame_type == 0)
+    from av1dec_amd import Decoder, native
+    lib = native.lib()
+    sizes = []
+    for fr in streams[0][1:9]:  # the packed batch of an inter frame (untimed)
+        pk = Decoder.pack(fr)
+        sizes.append(lib.av1r_packed_bytes(pk))
+        Decoder.free_packed(pk)
     host_profile = {  # where the host-inclusive pipeline spends its time (rank 0)
+        "packed_MB_per_inter_frame": round(sum(sizes) / max(len(sizes), 1) / 1e6, 3),
         "packing_threads": workers,
         "pack_ms_per_frame": round(1e3 * pr["pack_s"] / max(pr["frames"], 1), 3),
         "producer_utilisation": round(pr["pack_s"] / (workers * elapsed), 3),
