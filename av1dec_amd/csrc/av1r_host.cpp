@@ -216,7 +216,7 @@ struct av1r_ctx {
     // pack_frame, from its size pass for its packing pass: whether any TB has a level that
     // needs more than 6 signed bits, and then per TB its width (AV1R_TBD_WIDE) and a wide
     // TB's offset in the 32-bit array
-    bool anyWide = false;
+    bool anyWide = false, wideKnown = false;  // (wideKnown: validate's fast pass classified)
     std::vector<uint32_t> tbCoefOff;
     std::vector<uint8_t> tbWide;
     size_t nCoef32 = 0;
@@ -549,23 +549,35 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                     ((uint64_t)t.coef_off + t.coef_cnt > b->n_coefs);
         }
         uint32_t badC = 0;
+        // (with the positions, each TB's coefficient width for pack_frame: a level outside 6
+        // signed bits makes (c + 0x8000) >> 16 non-zero)
+        c->tbWide.resize(b->n_tbs);
+        uint32_t anyWide = 0;
         if (!badT)
             for (uint32_t i = 0; i < b->n_tbs; i++) {
                 const av1r_tb& t = b->tbs[i];
                 const int log2Area = std::min<int>(av1r_tx_w_log2[t.tx_size], 5) + std::min<int>(av1r_tx_h_log2[t.tx_size], 5);
-                uint32_t acc = 0;
+                uint32_t acc = 0, wide = 0;
                 const uint32_t* cf = b->coefs + t.coef_off;
                 const uint32_t n = t.coef_cnt;
                 if ((uint64_t)t.coef_off + 16 <= b->n_coefs) {
                     // the first 16 (most TBs have fewer) masked, without a data-dependent
                     // branch: a short loop per TB mispredicted its exit once per TB
-                    for (uint32_t q = 0; q < 16; q++) acc |= cf[q] & (q < n ? ~0u : 0u);
-                    for (uint32_t q = 16; q < n; q++) acc |= cf[q];
+                    for (uint32_t q = 0; q < 16; q++) {
+                        const uint32_t m = q < n ? ~0u : 0u;
+                        acc |= cf[q] & m;
+                        wide |= ((cf[q] + 0x8000u) >> 16) & m;
+                    }
+                    for (uint32_t q = 16; q < n; q++) acc |= cf[q], wide |= (cf[q] + 0x8000u) >> 16;
                 } else {
-                    for (uint32_t q = 0; q < n; q++) acc |= cf[q];
+                    for (uint32_t q = 0; q < n; q++) acc |= cf[q], wide |= (cf[q] + 0x8000u) >> 16;
                 }
                 badC |= (acc & 1023u) >> log2Area;
+                c->tbWide[i] = wide != 0;
+                anyWide |= wide;
             }
+        c->anyWide = anyWide != 0;
+        c->wideKnown = !badT;
         // palette blocks (rare): their records, then the map window of every transform block
         // whose OWN block (t.block: what build_schedule and the device's tb_predict follow) is
         // an intra palette block -- wherever that TB sits in the TB array
@@ -1448,21 +1460,26 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
         // | pos) fits int16.  One vectorised OR over the whole array first; only a frame with
         // some wider level classifies its TBs
         const uint32_t* cf = b->coefs;
-        uint32_t out = 0;
-        for (uint32_t q = 0; q < b->n_coefs; q++) out |= (cf[q] + 0x8000u) >> 16;
-        c->anyWide = out != 0;
-        c->nCoef32 = 0;
-        if (c->anyWide) {
-            c->tbCoefOff.resize(b->n_tbs);
+        if (!c->wideKnown || c->tbWide.size() != b->n_tbs) {  // (validate's slow path ran)
             c->tbWide.resize(b->n_tbs);
-            size_t n32 = 0;
+            uint32_t any = 0;
             for (uint32_t i = 0; i < b->n_tbs; i++) {
                 const av1r_tb& t = b->tbs[i];
                 uint32_t o = 0;
                 for (uint32_t q = 0; q < t.coef_cnt; q++) o |= (cf[t.coef_off + q] + 0x8000u) >> 16;
                 c->tbWide[i] = o != 0;
+                any |= o;
+            }
+            c->anyWide = any != 0;
+        }
+        c->wideKnown = false;  // (one frame's)
+        c->nCoef32 = 0;
+        if (c->anyWide) {
+            c->tbCoefOff.resize(b->n_tbs);
+            size_t n32 = 0;
+            for (uint32_t i = 0; i < b->n_tbs; i++) {
                 c->tbCoefOff[i] = (uint32_t)n32;
-                if (o) n32 += t.coef_cnt;
+                if (c->tbWide[i]) n32 += b->tbs[i].coef_cnt;
             }
             c->nCoef32 = n32;
         }
