@@ -2432,8 +2432,9 @@ int BlockParser::coeffs(Blk& b, Tb& t)
 void BlockParser::emit(Blk& b)
 {
     TileCtx& F = T;  // (records tile-relative until merge_tile)
-    av1r_block rec;
-    memset(&rec, 0, sizeof(rec));
+    const uint32_t blockIdx = (uint32_t)F.blocks.size();
+    F.blocks.emplace_back();  // (value-initialised, i.e. zeroed, and written in place)
+    av1r_block& rec = F.blocks.back();
     rec.mi_row = (uint16_t)b.r;
     rec.mi_col = (uint16_t)b.c;
     rec.mi_size = (uint8_t)b.bsize;
@@ -2554,7 +2555,6 @@ void BlockParser::emit(Blk& b)
         }
     }
     rec.flags = f;
-    const uint32_t blockIdx = (uint32_t)F.blocks.size();
     rec.first_tb = (uint32_t)F.tbs.size();
     int maxLumaW = 0, maxLumaH = 0;
     for (const Tb& t : tbs) {
@@ -2562,8 +2562,8 @@ void BlockParser::emit(Blk& b)
         const int row = (t.y << sub) >> 2, col = (t.x << sub) >> 2;
         const int sbRow = row & sbMask, sbCol = col & sbMask;
         const int stepX = av1r_tx_w[t.tx] >> 2, stepY = av1r_tx_h[t.tx] >> 2;
-        av1r_tb tr;
-        memset(&tr, 0, sizeof(tr));
+        F.tbs.emplace_back();  // (zeroed)
+        av1r_tb& tr = F.tbs.back();
         tr.block = blockIdx;
         tr.x = (uint16_t)t.x;
         tr.y = (uint16_t)t.y;
@@ -2582,7 +2582,6 @@ void BlockParser::emit(Blk& b)
             rec.max_luma_w = (uint16_t)maxLumaW;
             rec.max_luma_h = (uint16_t)maxLumaH;
         }
-        F.tbs.push_back(tr);
         // TransformBlock::decode side effects (TransformBlock.cpp:2418-2454)
         if (!b.is_inter && plane == 0) {
             maxLumaW = t.x + stepX * 4;
@@ -2601,7 +2600,6 @@ void BlockParser::emit(Blk& b)
             }
     }
     rec.n_tbs = (uint32_t)F.tbs.size() - rec.first_tb;
-    F.blocks.push_back(rec);
 }
 
 // ------------------------------------------------------------------------------------

@@ -637,13 +637,12 @@ bool Parser::mv_project(int src, int dstSign)
     for (int dst = LAST_FRAME; dst <= ALTREF_FRAME; dst++) mf[dst] = motion_field[dst].data();
     for (int y8 = 0; y8 < h8; y8++)
         for (int x8 = 0; x8 < w8; x8++) {
-            const int row = 2 * y8 + 1, col = 2 * x8 + 1;
-            const int srcRef = r.mf_ref[(size_t)row * r.mi_cols + col];
+            const int srcRef = r.mf_ref[(size_t)y8 * w8 + x8];  // (unit 2 y8 + 1, 2 x8 + 1: motion vector storage)
             if (srcRef <= INTRA_FRAME) continue;
             const int refOffset = refOffsetOf[srcRef];
             if (!(abs(refToCur) <= AV1R_MAX_FRAME_DISTANCE && abs(refOffset) <= AV1R_MAX_FRAME_DISTANCE && refOffset > 0))
                 continue;
-            const Mv mv = r.mf_mv[(size_t)row * r.mi_cols + col];
+            const Mv mv = r.mf_mv[(size_t)y8 * w8 + x8];
             Mv proj = mv_projection(mv, refToCur * dstSign, refOffset);
             int px = x8, py = y8;
             if (!(project(px, proj.c, dstSign, w8, 8) && project(py, proj.r, dstSign, h8, 0))) continue;
@@ -935,8 +934,6 @@ void Parser::start_frame()
         mi_lftx.assign(mi.size() * 3, 0);
         mi_dlf.assign(mi.size() * 4, 0);
     }
-    mf_ref.assign((size_t)fh.mi_rows * fh.mi_cols, -1);
-    mf_mv.assign((size_t)fh.mi_rows * fh.mi_cols, Mv());
     cdef_rows = (fh.mi_rows + 15) / 16;
     cdef_cols = (fh.mi_cols + 15) / 16;
     cdef_idx.assign((size_t)cdef_rows * cdef_cols, -1);
@@ -1052,16 +1049,22 @@ int Parser::finish_frame()
     // once per frame rather than per unit
     bool behind[8] = {};
     for (int r = INTRA_FRAME + 1; r < 8; r++) behind[r] = relative_dist(fh.order_hints[r], fh.order_hint) < 0;
-    for (int row = 0; row < fh.mi_rows; row++)
-        for (int col = 0; col < fh.mi_cols; col++) {
-            const MiInfo& m = mi_at(row, col);
+    // Only the units the motion-field projection reads are stored: (2 y8 + 1, 2 x8 + 1) of every
+    // 8x8 (the motion field projection, spec 7.9.2 / Parser.cpp:772-910, reads no other unit), a quarter of the grid,
+    // which the reference slots then copy
+    const int h8 = fh.mi_rows >> 1, w8 = fh.mi_cols >> 1;
+    mf_ref.assign((size_t)h8 * w8, -1);
+    mf_mv.assign((size_t)h8 * w8, Mv());
+    for (int y8 = 0; y8 < h8; y8++)
+        for (int x8 = 0; x8 < w8; x8++) {
+            const MiInfo& m = mi_at(2 * y8 + 1, 2 * x8 + 1);
             for (int list = 0; list < 2; list++) {
                 const int r = m.ref[list];
                 if (r > INTRA_FRAME && behind[r]) {
                     const int lim = (1 << 12) - 1;
                     if (abs(m.mv[list].r) <= lim && abs(m.mv[list].c) <= lim) {
-                        mf_ref[(size_t)row * fh.mi_cols + col] = (int8_t)r;
-                        mf_mv[(size_t)row * fh.mi_cols + col] = m.mv[list];
+                        mf_ref[(size_t)y8 * w8 + x8] = (int8_t)r;
+                        mf_mv[(size_t)y8 * w8 + x8] = m.mv[list];
                     }
                 }
             }

@@ -201,7 +201,7 @@ struct SymbolDecoder {
             return s;
         }
 #endif
-#if !defined(AV1P_WRITER) && !defined(AV1P_TRACE)
+#if !defined(AV1P_WRITER) && !defined(AV1P_TRACE) && !defined(AV1P_READ_LOOP)
         // the alphabets the syntax uses, each as readN (branch-free interval search, unrolled
         // adaptation): the loop below mispredicts once per symbol on the larger ones
         switch (nsym) {
@@ -369,7 +369,7 @@ struct RefSlot {
     int saved_order_hints[8] = {};
     int32_t saved_gm[8][6] = {};
     int8_t lf_ref_deltas[8] = {}, lf_mode_deltas[2] = {};
-    std::vector<int8_t> mf_ref;  // MfRefFrames, mi_rows x mi_cols
+    std::vector<int8_t> mf_ref;  // MfRefFrames at (2 y8 + 1, 2 x8 + 1), (mi_rows / 2) x (mi_cols / 2)
     std::vector<Mv> mf_mv;       // MfMvs
     Cdfs cdfs;
     bool showable = false;
@@ -511,7 +511,7 @@ public:
     // per 4x4 unit, for the emitted grid only (emit_mi): lf_tx of the 3 planes, delta LF x 4
     std::vector<uint8_t> mi_lftx;
     std::vector<int8_t> mi_dlf;
-    std::vector<int8_t> mf_ref;          // MfRefFrames of this frame (motion vector storage)
+    std::vector<int8_t> mf_ref;          // MfRefFrames of this frame (motion vector storage), per 8x8
     std::vector<Mv> mf_mv;
     std::vector<Mv> motion_field[8];     // MotionFieldMvs[ref][row >> 1][col >> 1]
     std::vector<int8_t> cdef_idx;        // per 64x64 (frame cdef grid)
