@@ -2312,14 +2312,14 @@ int BlockParser::coeffs(Blk& b, Tb& t)
             nzc[nnz] = (uint16_t)c;
             nnz += level != 0;
         }
-        for (int c = 0; c < eob; c++) lvl[se[c].pad] = 0;  // back to all zero for the next transform block
+        for (int q = 0; q < nnz; q++) lvl[se[nzc[q]].pad] = 0;  // back to all zero for the next transform block (zero levels stored 0)
         (void)height;
         PROF_T(c3);
         PROF_ADD(6, c2, c3);
         // signs and Golomb remainders of the non-zero levels, in scan order (nzc from its end);
         // the non-zero positions also into a bitmap of rows (the packing below walks only them)
         const int twl = av1r_tx_w_log2[txSz] < 5 ? av1r_tx_w_log2[txSz] : 5;  // log2(tw)
-        uint32_t nzRow[32] = {};
+        uint32_t nzRow[32] = {}, rowMask = 0;
         for (int q = nnz - 1; q >= 0; q--) {
             const int c = nzc[q];
             const int pos = se[c].pos;
@@ -2368,7 +2368,10 @@ int BlockParser::coeffs(Blk& b, Tb& t)
                 quant[pos] = (int16_t)((int16_t)x + kCoeffBaseRange + kNumBaseLevels);
             }
             if (pos == 0 && quant[pos] > 0) dcCategory = sign ? 1 : 2;
-            if (quant[pos]) nzRow[pos >> twl] |= 1u << (pos & (tw - 1));
+            if (quant[pos]) {
+                nzRow[pos >> twl] |= 1u << (pos & (tw - 1));
+                rowMask |= 1u << (pos >> twl);
+            }
             culLevel += quant[pos];
             if (sign) quant[pos] = -quant[pos];
         }
@@ -2386,8 +2389,8 @@ int BlockParser::coeffs(Blk& b, Tb& t)
         std::vector<uint32_t>& out = T.coefs;
         out.resize(t.coef_off + nnz);
         uint32_t* o = out.data() + t.coef_off;
-        const int th = std::min(h, 32);  // the coded rows
-        for (int i = 0; i < th; i++) {
+        for (uint32_t rm = rowMask; rm; rm &= rm - 1) {  // the rows holding a non-zero level, in order
+            const int i = __builtin_ctz(rm);
             int* row = &quant[i * tw];
             for (uint32_t m = nzRow[i]; m; m &= m - 1) {
                 const int j = __builtin_ctz(m);
