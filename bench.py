@@ -240,11 +240,13 @@ def ivf_leg(decs, streams, frames, size="1920x1080", name="1080p_s1", seed=0x5EE
     (av1dec_amd.pipeline.IvfPipeline); one untimed pass, then a timed one.  Multi-tile
     frames (configs[3]) are parsed tile-parallel (av1p_set_tile_threads)."""
     from av1dec_amd.pipeline import run_native
-    # one worker per stream (a stream's next frame may still parse while its previous one
-    # packs: the IVF source keeps two parsed units alive, av1r_pipeline.cpp).  Two workers
-    # per stream measured no faster (320-334 against 335 frames/s): the parse threads ran
-    # slower beside 8 more busy cores (23.3 against 21.5 ms/frame), profiles/r05_ab_ivf_workers.txt
-    workers = len(streams)
+    # two workers per stream: a stream's next frame parses while its previous one packs (the
+    # IVF source keeps two parsed units alive, av1r_pipeline.cpp).  Against one worker per
+    # stream: 1080p 365-382 vs 352-357 frames/s, 4K 4x2 tiles 97-101 vs 75-77
+    # (profiles/r05_ab_ivf_workers2.txt; with the slower parser of r05_ab_ivf_workers.txt the
+    # 1080p leg had measured no faster)
+    per = int(os.environ.get("AV1R_BENCH_IVF_WORKERS_PER_STREAM", "2"))  # (A/B)
+    workers = per * len(streams)
     run_native(decs, "ivf", streams, workers=workers)
     t0 = time.perf_counter()
     st = run_native(decs, "ivf", streams, workers=workers)
