@@ -1951,7 +1951,7 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
 // workgroup), n >= 1 small items (wave w runs items w, w + 4, ..)
 #ifndef AV1R_FLOW_WAVES
-#define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better)
+#define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better; 8 = 64 VGPRs + spills: 4K recon +3 %, profiles/r05_ab_flow_waves8.txt)
 #endif
 #ifdef AV1R_FLOW_DEBUG
 // -DAV1R_FLOW_DEBUG: counts workgroup entries that find another launch's k_flow
