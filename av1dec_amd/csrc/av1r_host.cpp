@@ -539,6 +539,14 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
             const uint32_t badA = (k.y_mode > AV1R_PAETH_PRED) | (((k.flags & AV1R_BLK_HAS_CHROMA) != 0) & (k.uv_mode > AV1R_UV_CFL_PRED)) |
                                   (((k.flags & AV1R_BLK_FILTER_INTRA) != 0) & (k.filter_intra_mode > 4));
             badB |= inter ? badI : badA;
+            // the device reaches an inter-intra block's TB range and a local warp through
+            // palette_off (DevBlock, pack_frame): those flags only on inter blocks without a
+            // palette, and INTERINTRA exactly when build_schedule makes the block an
+            // inter-intra item (inter with ref_frame[1] == INTRA_FRAME)
+            const bool ext = (k.flags & (AV1R_BLK_LOCAL_VALID | AV1R_BLK_INTERINTRA)) != 0;
+            const bool ii = inter && k.ref_frame[1] == AV1R_INTRA_FRAME;
+            badB |= (ext & (!inter | ((k.palette_size_y | k.palette_size_uv) != 0))) |
+                    (ii != ((k.flags & AV1R_BLK_INTERINTRA) != 0));
         }
         for (uint32_t i = 0; i < b->n_tbs; i++) {
             const av1r_tb& t = b->tbs[i];
@@ -623,7 +631,13 @@ static int validate(av1r_ctx* c, const av1r_frame_batch* b)
                 return fail(c, AV1R_E_INVALID, "wedge on a block size without wedges");
             if (k.flags & AV1R_BLK_INTERINTRA)
                 if (k.mi_size < AV1R_BLOCK_8X8 || k.mi_size > AV1R_BLOCK_32X32) return fail(c, AV1R_E_INVALID, "interintra size");
-        } else {
+            if ((k.ref_frame[1] == AV1R_INTRA_FRAME) != ((k.flags & AV1R_BLK_INTERINTRA) != 0))
+                return fail(c, AV1R_E_INVALID, "block %u: INTERINTRA flag disagrees with ref_frame[1]", i);
+        }
+        if ((k.flags & (AV1R_BLK_LOCAL_VALID | AV1R_BLK_INTERINTRA))
+            && (!(k.flags & AV1R_BLK_INTER) || k.palette_size_y || k.palette_size_uv))
+            return fail(c, AV1R_E_INVALID, "block %u: warp / inter-intra flags on an intra or palette block", i);
+        if (!(k.flags & AV1R_BLK_INTER)) {
             if (k.y_mode > AV1R_PAETH_PRED || ((k.flags & AV1R_BLK_HAS_CHROMA) && k.uv_mode > AV1R_UV_CFL_PRED)
                 || ((k.flags & AV1R_BLK_FILTER_INTRA) && k.filter_intra_mode > 4))
                 return fail(c, AV1R_E_INVALID, "block %u intra modes", i);
@@ -3035,6 +3049,22 @@ int av1r_show_existing(av1r_ctx* c, int slot, int refresh)
     frame_unref(c, f);
     return stage_outputs(c);
 }
+
+int av1r_ref_release(av1r_ctx* c, int slotMask)
+{
+    if (!c || (slotMask & ~0xff)) return AV1R_E_INVALID;
+    ctx_join(c);  // (as show_existing: a buffer reused later is written behind the queued reads, in stream order)
+    for (int i = 0; i < 8; i++)
+        if (slotMask & (1 << i)) {
+            frame_unref(c, c->slots[i]);
+            c->slots[i] = nullptr;
+        }
+    return AV1R_OK;
+}
+
+int av1r_set_strip_levels(int) { return 0; }
+int av1r_set_filter_fusion(int) { return 0; }
+int av1r_set_flow_wave(int) { return 0; }
 
 int av1r_output_pending(av1r_ctx* c) { return c ? (int)(c->outq.size() + c->staged.size()) : 0; }
 

@@ -166,6 +166,10 @@ class Decoder:
         """Test hook: polls before a k_flow wait gives up (0 = default; 1 forces timeouts)."""
         self._check(self.l.av1r_set_flow_spins(self.c, int(spins)), "av1r_set_flow_spins")
 
+    def ref_release(self, slot_mask):
+        """Drop the reference store's hold on the slots of `slot_mask` (av1r_ref_release)."""
+        self._check(self.l.av1r_ref_release(self.c, int(slot_mask)), "av1r_ref_release")
+
     def set_schedule(self, mode):
         """1: dataflow kernel k_flow (default), 0: one launch per dependency level."""
         self._check(self.l.av1r_set_schedule(self.c, int(mode)), "av1r_set_schedule")

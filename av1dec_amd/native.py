@@ -276,7 +276,8 @@ EXPORTS = [
     "av1r_set_fast_intra", "av1r_packed_data",
     "av1r_get_output_async", "av1r_output_query", "av1r_output_start", "av1r_output_wait", "av1r_set_output_prefetch", "av1r_pipeline_set_output",
     "av1r_ring_sink_create", "av1r_ring_sink_destroy", "av1r_ring_sink_delivered", "av1r_ring_sink_frame",
-    "av1r_frame_layout",
+    "av1r_frame_layout", "av1r_ref_release",
+    "av1r_set_strip_levels", "av1r_set_filter_fusion", "av1r_set_flow_wave",  # (deprecated no-ops)
 ]
 
 

@@ -293,19 +293,29 @@ def parse_cpulist(text):
 
 
 def gpu_numa_node(local):
-    """NUMA node of GPU `local`: its PCI bus id from the HIP runtime, then sysfs
-    (/sys/bus/pci/devices/<id>/numa_node); -1 when unknown."""
+    """NUMA node of GPU `local`, read without starting the HIP runtime (whose threads would
+    keep the full CPU mask when the rank binds itself afterwards): the KFD topology's GPU
+    nodes in enumeration order (the order the runtime numbers devices in, filtered by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES), the node's PCI location, then sysfs
+    (/sys/bus/pci/devices/<bdf>/numa_node); -1 when unknown."""
     try:
-        import ctypes as C
-        from av1dec_amd import native
-        h = native.hip()
-        buf = C.create_string_buffer(64)
-        if h.hipDeviceGetPCIBusId(buf, 64, int(local)) != 0:
-            return -1
-        bus = buf.value.decode().lower()
-        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+        base = "/sys/class/kfd/kfd/topology/nodes"
+        gpus = []
+        for n in sorted((d for d in os.listdir(base) if d.isdigit()), key=int):
+            with open(f"{base}/{n}/properties") as f:
+                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            if int(props.get("simd_count", "0")) > 0:
+                gpus.append(props)
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+            vis = os.environ.get(var, "")
+            if vis and all(v.strip().isdigit() for v in vis.split(",")):
+                gpus = [gpus[int(v)] for v in vis.split(",")]
+        p = gpus[int(local)]
+        loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7}"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
             return int(f.read().strip())
-    except Exception:
+    except (OSError, ValueError, IndexError, KeyError):
         return -1
 
 
@@ -735,11 +745,12 @@ def main():
             dist.destroy_process_group()
         return
 
+    # before any thread of ours (or of the HIP runtime) starts: the rank's share of its GPU's
+    # NUMA node, found from sysfs
+    bound = bind_rank_cpus(rank, world, local, dist)
     from av1dec_amd import Decoder, native
 
     native.lib()
-    # before any thread of ours starts: the rank's share of its GPU's NUMA node
-    bound = bind_rank_cpus(rank, world, local, dist)
     W, H, tiles, seed = CONFIGS[args.config]
     S = max(1, args.streams)
     F = args.frames

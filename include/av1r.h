@@ -22,6 +22,8 @@
  *                                        (Av1Decoder.cpp:128-156, 171-192)
  *   av1r_frame_begin/submit_tile/end  -- the same, split per Tile (Tile::decode, Tile.cpp:168-178)
  *   av1r_show_existing                -- Decoder::showExistingFrame (Av1Decoder.cpp:158-169)
+ *   av1r_ref_release                  -- a slot dropped from the FrameStore (updateFrameStore,
+ *                                        Av1Decoder.cpp:111-119)
  *   av1r_output_pending/av1r_get_output -- Decoder::getOutput (Av1Decoder.cpp:203-211) +
  *                                        the I420 row copy of DecodeOutput::output
  *                                        (tests/DecodeOutput.cpp:48-69)
@@ -271,6 +273,14 @@ int av1r_set_discard_output(av1r_ctx* ctx, int discard);
 
 /* show_existing_frame: queue slot `slot` for output and refresh per `refresh_flags`. */
 int av1r_show_existing(av1r_ctx* ctx, int slot, int refresh_flags);
+/* Drop the reference store's hold on the slots in `slot_mask` (bit i = slot i), as the
+ * reference drops a slot's shared_ptr when updateFrameStore replaces it
+ * (Av1Decoder.cpp:111-119) -- for a caller that resets or flushes a stream between GOPs.
+ * Refresh releases the replaced frames by itself, so a decoder running a stream never needs
+ * it.  Work already queued that reads those slots completes first (the frames are
+ * refcounted); a later frame that references an emptied slot fails validation with
+ * AV1R_E_INVALID. */
+int av1r_ref_release(av1r_ctx* ctx, int slot_mask);
 
 /* Output queue.  av1r_get_output copies the oldest queued frame's visible I420 planes
  * (width x height, (width>>1) x (height>>1)) into the caller's buffers and pops it. */
@@ -342,6 +352,12 @@ int av1r_flow_debug(uint32_t* pairs, int n, int reset, int* cross_stream);
  * (default; environment AV1R_FI), 0 = the generic one.  Both are bit-exact (A/B).  Returns
  * the previous value. */
 int av1r_set_fast_intra(int on);
+/* Removed in round 5 (the strip schedule k_strip, the fused filter kernel k_post and per-wave
+ * k_flow items, each measured slower: DESIGN.md 3.1b, 4.1): kept as no-ops returning 0 for
+ * one release so that existing callers still link.  Deprecated. */
+int av1r_set_strip_levels(int levels);
+int av1r_set_filter_fusion(int on);
+int av1r_set_flow_wave(int on);
 /* Host-only check of a batch: validation + dependency schedule, no device needed.
  * Returns the status; *levels = recon launch levels.  err receives the message. */
 int av1r_check_batch(const av1r_frame_batch* batch, int* levels, char* err, int err_len);

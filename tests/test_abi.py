@@ -78,7 +78,9 @@ def test_validation_rejects_bad_batches(native_lib):
     hdr.bitdepth = 10
     secs = dict(fr.sec)
     secs["hdr"] = np.frombuffer(bytes(hdr), np.uint8).copy()
-    assert native_lib.av1r_check_batch(C.cast(batchfile.Frame(secs).byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_UNSUPPORTED
+    bad = batchfile.Frame(secs)
+    assert native_lib.av1r_check_batch(C.cast(bad.byref(), C.c_void_p), None, err, 256) == abi.AV1R_E_UNSUPPORTED
+    assert b"8-bit" in err.value
 
 
 def test_pack_is_host_only_and_thread_safe(native_lib):
@@ -319,4 +321,45 @@ print("packed", n)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "packed" in r.stdout
+
+
+
+def test_validation_rejects_ext_flags_that_disagree_with_the_block(native_lib):
+    """The device reaches an inter-intra block's TB range and a local warp through the
+    block's palette_off (DevBlock): validate() must reject INTERINTRA / LOCAL_VALID on an
+    intra block, INTERINTRA on an inter block whose ref_frame[1] is not INTRA_FRAME, and an
+    inter-intra block (ref_frame[1] == INTRA_FRAME) without the flag."""
+    import numpy as np
+    INTER, INTERINTRA, LOCAL_VALID = 1, 1 << 5, 1 << 7
+    err = C.create_string_buffer(256)
+    fr = batchfile.load(golden.batch_path("av1-1-b8-06-mfmv"))[1]
+    assert native_lib.av1r_check_batch(C.cast(fr.byref(), C.c_void_p), None, err, 256) == 0
+    blk0 = np.frombuffer(fr.sec["blocks"].tobytes(), abi.BLOCK_DTYPE)
+
+    def check(mut):
+        blk = blk0.copy()
+        mut(blk)
+        secs = dict(fr.sec)
+        secs["blocks"] = blk.view(np.uint8).ravel()
+        bad = batchfile.Frame(secs)  # (kept alive across the call: byref points into it)
+        return native_lib.av1r_check_batch(C.cast(bad.byref(), C.c_void_p), None, err, 256)
+
+    intra = [i for i in range(len(blk0)) if not blk0["flags"][i] & INTER]
+    inter = [i for i in range(len(blk0)) if blk0["flags"][i] & INTER and blk0["ref_frame"][i][1] != 0
+             and 3 <= blk0["mi_size"][i] <= 9]  # BLOCK_8X8 .. BLOCK_32X32
+    assert intra and inter
+
+    def set_flag(i, f):
+        def m(b):
+            b["flags"][i] |= f
+        return m
+    assert check(set_flag(intra[0], LOCAL_VALID)) == abi.AV1R_E_INVALID
+    assert check(set_flag(intra[0], INTERINTRA)) == abi.AV1R_E_INVALID
+    assert check(set_flag(inter[0], INTERINTRA)) == abi.AV1R_E_INVALID
+    assert b"INTERINTRA" in err.value
+
+    def make_ii_unflagged(b):
+        b["ref_frame"][inter[0]][1] = 0
+        b["flags"][inter[0]] &= 0xFFFFFFFF ^ INTERINTRA
+    assert check(make_ii_unflagged) == abi.AV1R_E_INVALID
 

@@ -109,3 +109,25 @@ def split_tiles(dec, fr):
         secs["palette"] = pal[p0:p1].copy()
         tiles.append(batchfile.Frame(secs))
     dec.decode_tiles(fr, tiles)
+
+
+@pytest.mark.gpu
+def test_gpu_ref_release():
+    """av1r_ref_release empties slots: the key frame still decodes and reads back equal to an
+    untouched decoder, an inter frame that needs an emptied slot is rejected, and a mask
+    outside the 8 slots is refused."""
+    import numpy as np
+    from av1dec_amd.decoder import BackendError
+    frames = [f for f in batchfile.load(golden.batch_path("av1-1-b8-06-mfmv")) if not f.show_existing]
+    d1, d2 = Decoder(0), Decoder(0)
+    d1.decode_frame(frames[0])
+    d2.decode_frame(frames[0])
+    d2.ref_release(0xff)
+    for x, y in zip(d1.get_output(), d2.get_output()):
+        assert np.array_equal(x, y)
+    with pytest.raises(BackendError):
+        d2.decode_frame(frames[1])
+    with pytest.raises(BackendError):
+        d2.ref_release(0x100)
+    d1.close()
+    d2.close()
