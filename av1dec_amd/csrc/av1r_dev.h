@@ -140,9 +140,6 @@ static_assert(sizeof(DevTb) == 16, "DevTb layout");
 struct KParams {
     const av1r_frame_hdr* hdr;
     const av1r_mi* mi;
-    // deblocking edge codes (k_lfcode -> k_lf / k_deblock): per pass, a byte per 4x4 unit in
-    // k_lf's unit order (luma row-major, then U, then V): level | filter size << 6, 0 = none
-    uint8_t* lfc;
     const DevBlock* blocks;
     const int32_t* bext;  // LOCAL_VALID / INTERINTRA blocks' warp parameters and TB range, 8 words each (DevBlock)
     const DevTb* tbs;
@@ -180,7 +177,7 @@ struct KParams {
     uint32_t n_blocks, n_tbs;  // k_mi: the records the mode-info grid is derived from
     int frame_w, frame_h;
     DevFrame cur;     // frame under reconstruction (k_lf: deblocked in place)
-    DevFrame dbk;     // the deblocked frame (k_deblock's output; k_lf: cur)
+    DevFrame dbk;     // the deblocked frame (k_lf deblocks cur in place: cur)
     DevFrame cdef;    // CDEF output (Cdef::filter's copy, Cdef.cpp:43)
     DevFrame lrout;   // loop-restoration output (LoopRestoration.cpp:216)
     DevFrame ref[8];  // reference store slots
@@ -212,7 +209,6 @@ typedef const __attribute__((address_space(4))) KParams* KpConst;
 #define FLOW_ERR (FLOW_QUEUES * FLOW_LINE)
 #define FLOW_HOSTERR (FLOW_ERR + 2)  // (8 bytes) address of the launch's pinned host error word
 #define FLOW_SPINLIM (FLOW_ERR + 4)  // polls before a wait gives up (0: FLOW_SPINS)
-#define FLOW_FLAGS (FLOW_ERR + 5)    // bit 0: take the next ticket before running a group
 #define FLOW_ASSIGN (FLOW_ERR + FLOW_LINE)  // workgroup entries: entry k serves queue k % FLOW_QUEUES
 #define FLOW_CTL_BYTES (4 * (FLOW_ASSIGN + FLOW_LINE))
 // k_flow spin bound, in polls of running waves (each a global load round trip, ~0.5-2 us),

@@ -31,17 +31,13 @@
 
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s);
-void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc,
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t nb,
     unsigned long long* trace, hipStream_t s);
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
-void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
-void launch_k_lfcode(const KParams* kps, int n, int maxUnits, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
-void launch_k_out(const uint8_t* const src[3], const int ss[3], uint8_t* const dst[3], const int ds[3], const int w[3],
-                  const int h[3], hipStream_t st);
 void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s);
 #ifdef AV1R_FLOW_DEBUG
 uint32_t flow_debug_overlaps(uint32_t* pairs, int n, int reset);
@@ -58,7 +54,7 @@ struct FrameBuf {
     size_t bytes = 0;
     int refcnt = 0;
     uint64_t seq = 0;  // the owning context's frame sequence number of the launch that wrote it
-    // the launch that wrote it: its metadata slot and that slot's generation (slot_meta();
+    // the launch that wrote it: its metadata slot and that slot's generation (
     // a read-back ticket waits for exactly this launch, whatever the context did since)
     const struct Upload* wMeta = nullptr;
     uint64_t wGen = 0;
@@ -70,7 +66,6 @@ struct Upload {
     uint8_t* dev = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;  // all work that reads this upload has finished
-    hipEvent_t ready = nullptr; // meta: the upload (on the context's copy stream) has landed
     bool pending = false;
     std::atomic<uint64_t> gen{0};  // meta: launches that have used this slot (read by packers)
     // packed-frame slots (AV1R_SLOT_META): done when the launch that used meta slot waitMeta
@@ -122,7 +117,7 @@ struct av1r_packed {
     bool pinned = false;
     hipEvent_t copied = nullptr;  // the upload of this buffer (its host memory is in use until then)
     bool copyPending = false;
-    // ... or (slot_meta()) the completion of the launch that read the upload: its meta slot and
+    // ... or the completion of the launch that read the upload: its meta slot and
     // that slot's generation then (see Upload::waitMeta)
     const struct Upload* waitMeta = nullptr;
     uint64_t waitGen = 0;
@@ -140,8 +135,8 @@ struct av1r_output_ticket {
     hipEvent_t ready = nullptr, done = nullptr;
     int state = 0;  // 0 the frame's kernels may still run, 1 copies issued, 2 landed
     bool live = false;
-    bool sq = false;  // this read-back's landing is seen by the stream going idle (AV1R_OUT_SQ)
-    // the frame is done when this launch is (slot_meta(): the last launch on the frame's
+    bool sq = false;  // this read-back's landing is seen by the stream going idle
+    // the frame is done when this launch is (the last launch on the frame's
     // stream, through its metadata slot and generation) instead of by `ready`
     const Upload* readyMeta = nullptr;
     uint64_t readyGen = 0;
@@ -171,7 +166,6 @@ struct av1r_ctx {
     const Upload* lastMeta = nullptr;  // the meta slot of this context's last launch (launch_jobs)
     int metaIdx = 0;
     hipStream_t copyStream = nullptr;
-    hipStream_t aux = nullptr;              // k_inter_m / k_inter_s beside k_inter (AV1R_INTER_SPLIT)
     // asynchronous frame delivery (av1r_get_output_async): the read-back copies' own stream
     // (created at the first such call) and every ticket ever allocated (free ones reused)
     hipStream_t outStream = nullptr;
@@ -188,7 +182,6 @@ struct av1r_ctx {
     bool prefetch = false;
     std::deque<Staged> staged;
     std::vector<std::pair<uint8_t*, size_t>> stageFree;
-    hipEvent_t auxGo = nullptr, auxDone = nullptr;
     hipEvent_t sync = nullptr;  // cross-context ordering of batched launches
     // this context's latest work was launched on joinLead's stream (a batch it was a member
     // of) and nothing has been enqueued on its own stream since; ctx_join() orders its own
@@ -278,7 +271,6 @@ struct av1r_ctx {
     size_t resCap = 0;
     uint32_t flowSpins = 0;     // av1r_set_flow_spins (0: FLOW_SPINS)
     int flowPerCU = 8;          // k_flow workgroups per CU of this context's launches (capped by occupancy)
-    int flowGridCap = 0;        // > 0: at most this many k_flow workgroups (a solo deep frame, AV1R_SOLO_GRID)
     // a deep frame launched alone on this context's own stream (batched entry points): its
     // completion; av1r_busy reports whether it is still running
     hipEvent_t soloDone = nullptr;
@@ -299,7 +291,7 @@ struct av1r_ctx {
 struct LaunchRec {
     uint32_t* err = nullptr;
     hipEvent_t done = nullptr;
-    const struct Upload* meta = nullptr;  // (slot_meta()) completion = this launch's meta slot
+    const struct Upload* meta = nullptr;  // completion = this launch's meta slot
     uint64_t gen = 0;
     std::vector<std::pair<av1r_ctx*, uint64_t>> members;
 };
@@ -313,15 +305,10 @@ static std::vector<av1r_packed*> g_packAll;  // every packed buffer ever allocat
 // Completion of a launch through its own meta slot (the one event every launch records on
 // its stream after its last kernel) instead of more events recorded after it: a launch
 // recorded one per packed-frame slot, one per packed buffer and one for its status record
-// -- each a marker packet in the compute stream's hardware queue.  Without them (the
-// default; AV1R_SLOT_META=0 restores them) the headline rose 6 100 -> 6 370 frames/s.
+// -- each a marker packet in the compute stream's hardware queue.  Without them (round 4)
+// the headline rose 6 100 -> 6 370 frames/s.
 // The meta slot's generation counts its launches: once it has moved on, the launch waited
 // for was synchronized before the slot's reuse.
-static bool slot_meta()
-{
-    static const bool on = !getenv("AV1R_SLOT_META") || atoi(getenv("AV1R_SLOT_META")) != 0;
-    return on;
-}
 static bool meta_done(const Upload* m, uint64_t gen)
 {
     return m->gen.load(std::memory_order_acquire) != gen || hipEventQuery(m->done) == hipSuccess;
@@ -700,15 +687,9 @@ struct PackClock {
     }
 };
 
-// the filters fused into one kernel (av1r_set_filter_fusion; AV1R_FUSED=1)
-// the lean small-intra path of k_flow (intra_fast.h); AV1R_FI=0 or
-// av1r_set_fast_intra(0): the generic path (A/B)
-static bool inter_split()
-{
-    static const bool on = getenv("AV1R_INTER_SPLIT") && atoi(getenv("AV1R_INTER_SPLIT")) != 0;
-    return on;
-}
-static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) : 1};
+// the lean small-intra path of k_flow (intra_fast.h); av1r_set_fast_intra(0): the generic
+// path (A/B)
+static std::atomic<int> g_fastIntra{1};
 
 // ------------------------------------------------------------------------------------
 // dependency levels
@@ -717,8 +698,6 @@ static std::atomic<int> g_fastIntra{getenv("AV1R_FI") ? atoi(getenv("AV1R_FI")) 
 // outside inter-intra blocks -- finished by k_resid before k_flow -- get no node, item or
 // level: only the level launches need them.  c->levelsOk says whether the level schedule
 // was built too.
-// AV1R_PACK_FUSED=0: the map walks one by one (the fused walks must pack identical bytes)
-static const bool g_packFused = !getenv("AV1R_PACK_FUSED") || atoi(getenv("AV1R_PACK_FUSED")) != 0;
 // The pixels an intra prediction actually uses (IntraPredict::predict_intra,
 // IntraPredict.cpp:563-631, and the predictors it calls): the above-right run
 // (x + w .. x + 2w - 1) only by a directional prediction at an angle below 90 (the
@@ -752,17 +731,15 @@ static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
     if (ang > 180) return hL ? 6 : 7;
     return 7;
 }
-static bool g_modeEdges = !getenv("AV1R_MODE_EDGES") || atoi(getenv("AV1R_MODE_EDGES")) != 0;
 
-// k_flow's small-item groups: four items (one per wave) on a thin level, AV1R_FLOW_G (8:
-// two per wave, run one after the other) on a level of at least AV1R_FLOW_G_MIN small items
-// of the frame, where the workgroup's ticket, group load and closing barrier are paid once per
-// two items per wave (a level that crowded is far from the dependency chains' tail)
+// k_flow's small-item groups: four items (one per wave) on a thin level, 8 (two per wave,
+// run one after the other) on a level of at least 256 small items of the frame, where the
+// workgroup's ticket, group load and closing barrier are paid once per two items per wave (a
+// level that crowded is far from the dependency chains' tail; round 5: 16 per group, or 8 on
+// every level, measured slower, profiles/r05_ab_flow_groups.txt)
 static uint32_t flow_small_group(const Level& lv)
 {
-    static const uint32_t G = getenv("AV1R_FLOW_G") ? (uint32_t)std::max(4, std::min(64, atoi(getenv("AV1R_FLOW_G")))) : 8u;
-    static const uint32_t minItems = getenv("AV1R_FLOW_G_MIN") ? (uint32_t)std::max(0, atoi(getenv("AV1R_FLOW_G_MIN"))) : 256u;
-    return lv.fcnt[2] >= minItems ? G : 4u;
+    return lv.fcnt[2] >= 256u ? 8u : 4u;
 }
 
 // AV1R_SCHED_CHECK=1 (debug aid): the invariants k_flow relies on, checked on the host for a
@@ -947,8 +924,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         // plain inter blocks need not be painted (below)
         c->umap[p].assign((size_t)c->mapW[p] * c->mapH[p], av1r_ctx::MapUnit{-1, (int16_t)(flowOnly ? 0 : -1), 0, 0});
     }
-    static const bool granEnv = !getenv("AV1R_GRAN") || atoi(getenv("AV1R_GRAN")) != 0;
-    c->granOk = granEnv && allowGran;
+    c->granOk = allowGran;
     c->nodeMask.clear();
     uint32_t nm[12] = {};  // mask words of the node being built
     c->nodeDepStart.assign(1, 0);
@@ -956,10 +932,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     c->nodeLvl.clear();
     c->edgeDeps.clear();
     c->edgeStart.assign(1, 0);
-    // critical-path order (below): how far each item moves toward its latest level, in percent
-    // of its slack (AV1R_ALAP; 0 = the plain level order)
-    static const int alapPct = getenv("AV1R_ALAP") ? std::max(0, std::min(100, atoi(getenv("AV1R_ALAP")))) : 50;
-    const bool alap = alapPct > 0 && flowOnly;
+    // critical-path order (below): each item moves half of its slack toward its latest level
+    // (round 5: 0 / 50 / 100 % measured the same device time, 50 the best host-inclusive rate)
+    const int alapPct = 50;
+    const bool alap = flowOnly;
     c->nodeOfTb.assign(b->n_tbs, -1);
     c->nodeOfBlk.assign(b->n_blocks, -1);
     std::vector<int32_t> dl;  // dependencies of the node being built
@@ -995,11 +971,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 if (mu.owner < 0) continue;
                 *mw |= 1u << (u - u0);
                 if (alap) c->edgeDeps.push_back(mu.owner);
-                if (!(mu.emit & (horiz ? 1 : 2))) {
-                    if (c->granOk && getenv("AV1R_GRAN_DEBUG"))
-                        fprintf(stderr, "no granule: plane %d unit %d,%d %s (consumer %d,%d %dx%d)\n", p, ux, uy, horiz ? "h" : "v", x, y, w, h);
-                    c->granOk = false;
-                }
+                if (!(mu.emit & (horiz ? 1 : 2))) c->granOk = false;
             }
         };
         // above run: row (y-1)/4 from x/4; left run: column (x-1)/4 from y/4; the corner
@@ -1018,10 +990,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         }
     };
     auto own_set = [&](int p, int x0, int y0, int w4, int h4, int32_t node) {
-        if (x0 + w4 > c->mapW[p] || y0 + h4 > c->mapH[p]) {  // its granules would not fit
-            if (c->granOk && getenv("AV1R_GRAN_DEBUG")) fprintf(stderr, "outside: plane %d %d,%d %dx%d\n", p, x0, y0, w4, h4);
-            c->granOk = false;
-        }
+        if (x0 + w4 > c->mapW[p] || y0 + h4 > c->mapH[p]) c->granOk = false;  // its granules would not fit
         int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
         for (int y = y0; y < y1; y++) {
             av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
@@ -1069,10 +1038,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
         }
     };
     auto region_own_set = [&](int p, int x0, int y0, int w4, int h4, int lv, int32_t node) {  // both at once
-        if (x0 + w4 > c->mapW[p] || y0 + h4 > c->mapH[p]) {
-            if (c->granOk && getenv("AV1R_GRAN_DEBUG")) fprintf(stderr, "outside: plane %d %d,%d %dx%d\n", p, x0, y0, w4, h4);
-            c->granOk = false;
-        }
+        if (x0 + w4 > c->mapW[p] || y0 + h4 > c->mapH[p]) c->granOk = false;
         int x1 = std::min(x0 + w4, c->mapW[p]), y1 = std::min(y0 + h4, c->mapH[p]);
         for (int y = y0; y < y1; y++) {
             av1r_ctx::MapUnit* row = &c->umap[p][(size_t)y * c->mapW[p]];
@@ -1161,10 +1127,10 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                     bool hA = p ? (blk.flags & AV1R_BLK_AVAIL_U_UV) : (blk.flags & AV1R_BLK_AVAIL_U);
                     const int ex = (blk.mi_col >> sub) * 4, ey = (blk.mi_row >> sub) * 4;
                     const int ew = av1r_num4x4w[psz] * 4, eh = av1r_num4x4h[psz] * 4;
-                    // (the inter-intra modes read neither the above-right nor the below-left run)
-                    const bool hAR = !g_modeEdges && ((blk.ii_edge >> (2 * p)) & 1);
-                    const bool hBL = !g_modeEdges && ((blk.ii_edge >> (2 * p + 1)) & 1);
-                    const int need = g_modeEdges ? 3 : 7;  // (II_DC / V / H / SMOOTH: no corner)
+                    // (the inter-intra modes read neither the above-right nor the below-left
+                    // run, nor the corner: II_DC / V / H / SMOOTH)
+                    const bool hAR = false, hBL = false;
+                    const int need = 3;
                     dep = std::max(dep, edge_level(p, ex, ey, ew, eh, hL, hA, hAR, hBL, need));
                     edge_owners(p, ex, ey, ew, eh, hL, hA, hAR, hBL, p, need);
                 }
@@ -1203,11 +1169,11 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 int dep = -1;
                 if (!pal) {
                     const bool hL = t.flags & AV1R_TB_HAVE_LEFT, hA = t.flags & AV1R_TB_HAVE_ABOVE;
-                    const int ang = g_modeEdges ? intra_angle(blk, p) : 0;
-                    const bool hAR = (t.flags & AV1R_TB_HAVE_AR) && (!g_modeEdges || (ang > 0 && ang < 90));
-                    const bool hBL = (t.flags & AV1R_TB_HAVE_BL) && (!g_modeEdges || ang > 180);
-                    const int need = g_modeEdges ? intra_needs(blk, p, hA, hL) : 7;
-                    if (c->granOk && g_packFused) {
+                    const int ang = intra_angle(blk, p);
+                    const bool hAR = (t.flags & AV1R_TB_HAVE_AR) && ang > 0 && ang < 90;
+                    const bool hBL = (t.flags & AV1R_TB_HAVE_BL) && ang > 180;
+                    const int need = intra_needs(blk, p, hA, hL);
+                    if (c->granOk) {
                         dep = edge_scan(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, 0, need);
                     } else {
                         dep = edge_level(p, t.x, t.y, w, hh, hL, hA, hAR, hBL, need);
@@ -1231,7 +1197,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->nodeLvl.push_back(lv);
             // an inter TB's pixels are final before k_flow (k_inter + k_resid) unless the
             // block is inter-intra, whose blend item adds the residuals
-            if (!inter && g_packFused) {
+            if (!inter) {
                 region_own_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv, node);
             } else {
                 region_set(p, t.x >> 2, t.y >> 2, w >> 2, hh >> 2, lv);
@@ -1239,20 +1205,18 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             }
         }
     }
-    static const bool granDbg = getenv("AV1R_GRAN_DEBUG") != nullptr;
-    if (granDbg) fprintf(stderr, "av1r: granules %s (frame %dx%d)\n", c->granOk ? "on" : "off", h->frame_width, h->frame_height);
-    if (c->granOk != (granEnv && allowGran)) {  // a unit without its granule: dependency flags throughout
+    if (c->granOk != allowGran) {  // a unit without its granule: dependency flags throughout
         build_schedule(c, b, false, flowOnly);
         return;
     }
-    // Critical-path order (flow-only frames; AV1R_ALAP=0: off).  k_flow hands its groups out
+    // Critical-path order (flow-only frames).  k_flow hands its groups out
     // in level order, so an item of a long chain waits in the queue behind every item of the
     // levels before it, and the chain's tail runs alone after the bulk (a batched inter step:
     // levels 10-46 all released ~185 us into a 256 us launch, then one hop after another).
     // Each item moves toward the LATEST level it can have without lengthening the schedule,
     // L - height (height = the longest chain of consumers below it, through nodeDeps and the
     // edge producers recorded above; L = max(level + height)): to level + a * slack, slack =
-    // L - height - level, a = AV1R_ALAP / 100.  For a producer P of C, level(C) >= level(P) + 1
+    // L - height - level, a = alapPct / 100.  For a producer P of C, level(C) >= level(P) + 1
     // and L - height(C) >= L - height(P) + 1, so every such mix keeps C after P: the order stays
     // topological (k_flow's progress argument holds).  The items on the chains keep their level
     // (no slack) while those nothing waits for (height 0) move back, behind the chains' heads.
@@ -1460,7 +1424,6 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szHdr = align256(sizeof(av1r_frame_hdr));
     const size_t szMi = align256(sizeof(av1r_mi) * (size_t)h->mi_stride * h->mi_rows_alloc);
     // the deblocking edge codes (k_lfcode): a byte per (pass, plane, 4x4 unit), device-filled
-    const size_t szLfc = align256(2 * ((size_t)h->mi_rows * h->mi_cols + 2 * (size_t)((h->mi_rows + 1) / 2) * ((h->mi_cols + 1) / 2)));
     // the blocks in the device's record (DevBlock), the warp parameters and TB ranges of the
     // LOCAL_VALID / INTERINTRA blocks beside them (bext, 8 words each)
     const uint32_t extFlags = AV1R_BLK_LOCAL_VALID | AV1R_BLK_INTERINTRA;
@@ -1515,7 +1478,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     const size_t szResS = align256(4 * c->residS.size() + 4);
     const size_t szResL = align256(4 * c->residL.size() + 4);
     // the mode-info grid goes last and is not uploaded: k_mi derives it in place
-    *need = szHdr + szBlk + szExt + szTb + szCoef + szCoef16 + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi + szLfc;
+    *need = szHdr + szBlk + szExt + szTb + szCoef + szCoef16 + szPal + szCdef + szLr + szItems + szTiles + szDeps + szTbRes + szResS + szResL + szDone + szMi;
     static const bool sizeDbg = getenv("AV1R_PACK_SIZES") != nullptr;
     if (sizeDbg && host)
     {
@@ -1531,8 +1494,12 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     }
     if (!host) return AV1R_OK;
     size_t off = 0;
-    auto put = [&](const void* src, size_t n, size_t sz) {
+    // a section of sz bytes at `off`: n bytes copied from src (or, src null, `used` bytes the
+    // caller writes in place), the rest of the uploaded sections zeroed -- the packed bytes
+    // are a pure function of the frame (no heap contents travel; tests/test_abi.py's digest)
+    auto put = [&](const void* src, size_t n, size_t sz, size_t used = 0, bool uploaded = true) {
         if (n) memcpy(host + off, src, n);
+        if (uploaded) memset(host + off + (n ? n : used), 0, sz - (n ? n : used));
         size_t o = off;
         off += sz;
         return dev + o;
@@ -1542,9 +1509,9 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.hdr = (const av1r_frame_hdr*)put(h, sizeof(av1r_frame_hdr), szHdr);
     {
         DevBlock* db = reinterpret_cast<DevBlock*>(host + off);
-        k.blocks = (const DevBlock*)put(nullptr, 0, szBlk);
+        k.blocks = (const DevBlock*)put(nullptr, 0, szBlk, sizeof(DevBlock) * (size_t)b->n_blocks);
         int32_t* dx = reinterpret_cast<int32_t*>(host + off);
-        k.bext = (const int32_t*)put(nullptr, 0, szExt);
+        k.bext = (const int32_t*)put(nullptr, 0, szExt, 32 * nExt);
         uint32_t w = 0;
         for (uint32_t i = 0; i < b->n_blocks; i++) {
             const av1r_block& s = b->blocks[i];
@@ -1565,11 +1532,11 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
         // the TBs in the device's record, their coefficients split by width (the size pass's
         // classification)
         DevTb* dt = reinterpret_cast<DevTb*>(host + off);
-        k.tbs = (const DevTb*)put(nullptr, 0, szTb);
+        k.tbs = (const DevTb*)put(nullptr, 0, szTb, sizeof(DevTb) * (size_t)b->n_tbs);
         uint32_t* c32 = reinterpret_cast<uint32_t*>(host + off);
-        k.coefs = (const uint32_t*)put(nullptr, 0, szCoef);
+        k.coefs = (const uint32_t*)put(nullptr, 0, szCoef, 4 * c->nCoef32);
         uint16_t* c16 = reinterpret_cast<uint16_t*>(host + off);
-        k.coefs16 = (const uint16_t*)put(nullptr, 0, szCoef16);
+        k.coefs16 = (const uint16_t*)put(nullptr, 0, szCoef16, 2 * (size_t)b->n_coefs);
         for (uint32_t q = 0; q < b->n_coefs; q++) c16[q] = (uint16_t)b->coefs[q];
         for (uint32_t i = 0; i < b->n_tbs; i++) {
             const av1r_tb& t = b->tbs[i];
@@ -1627,15 +1594,14 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.resid_s = (const uint32_t*)put(c->residS.data(), 4 * c->residS.size(), szResS);
     k.resid_l = (const uint32_t*)put(c->residL.data(), 4 * c->residL.size(), szResL);
     P.upBytes = off;  // everything up to here travels; what follows is filled on the device
-    k.done = (uint32_t*)put(nullptr, 0, szDone);
+    k.done = (uint32_t*)put(nullptr, 0, szDone, 0, false);
     k.n_items = (uint32_t)c->items.size();
-    k.mi = (const av1r_mi*)put(nullptr, 0, szMi);
-    k.lfc = (uint8_t*)put(nullptr, 0, szLfc);
+    k.mi = (const av1r_mi*)put(nullptr, 0, szMi, 0, false);
     if (verify) {
         // every section placed, in order, inside the buffer (a section left out of the
         // packing sequence keeps the null of the memset: below the header's successors)
         const void* secs[] = {k.hdr, k.blocks, k.bext, k.tbs, k.coefs, k.coefs16, k.palette, k.cdef_idx, k.lr, P.dItems,
-                              k.tiles, k.deps, k.tb_res, k.resid_s, k.resid_l, k.done, k.mi, k.lfc};
+                              k.tiles, k.deps, k.tb_res, k.resid_s, k.resid_l, k.done, k.mi};
         const uint8_t* prev = dev;
         for (size_t i = 0; i < sizeof(secs) / sizeof(secs[0]); i++) {
             const uint8_t* q = (const uint8_t*)secs[i];
@@ -1675,25 +1641,13 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
 // through recon -> LF -> CDEF -> LR in shared launches on one HIP stream: every level of
 // every frame in one k_level launch, every frame's filters in one launch per filter.
 // ------------------------------------------------------------------------------------
-// Deblocking in place, one launch per pass (k_lf, default), or both passes per tile in LDS
-// (k_deblock, AV1R_DEBLOCK_TILE=1; its edge decisions from k_lfcode).  k_deblock writes a
-// frame of its own: tiles read their neighbours' pixels as halo, so the reconstructed frame
-// must stay intact while the launch runs.  Measured (profiles/r05_ab_switches.txt, 1080p x
-// 8): k_lf 0.0108 ms per frame, k_deblock + k_lfcode 0.0141-0.0147.
-static bool deblock_tile()
-{
-    static const bool on = getenv("AV1R_DEBLOCK_TILE") && atoi(getenv("AV1R_DEBLOCK_TILE")) != 0;
-    return on;
-}
-
 struct FrameJob {
     av1r_ctx* c = nullptr;
     const Prepared* P = nullptr;
     KParams k;
     // the frame's buffers R, C, L and their roles: D the deblocked frame, Co the CDEF output,
-    // out the frame the frame store and the output queue keep.  k_deblock: reconstruction in
-    // R, deblocked into C, CDEF back into R (whose reconstruction is dead by then), loop
-    // restoration into L.  k_lf: deblocked in place in R, CDEF into C, LR into L.
+    // out the frame the frame store and the output queue keep: deblocked in place in R, CDEF
+    // into C, LR into L.
     FrameBuf *R = nullptr, *C = nullptr, *L = nullptr;
     FrameBuf *D = nullptr, *Co = nullptr, *out = nullptr;
     bool scaled = false;  // a reference differs in size from the frame (no k_inter_s tiles)
@@ -1719,7 +1673,7 @@ static int job_begin(FrameJob& j)
         auto rb = [&](auto& ptr) {
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
-        rb(j.k.hdr), rb(j.k.mi), rb(j.k.lfc), rb(j.k.blocks), rb(j.k.bext), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.coefs16), rb(j.k.palette), rb(j.k.cdef_idx);
+        rb(j.k.hdr), rb(j.k.mi), rb(j.k.blocks), rb(j.k.bext), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.coefs16), rb(j.k.palette), rb(j.k.cdef_idx);
         rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
     }
     for (int s = 0; s < 8; s++)
@@ -1735,8 +1689,8 @@ static int job_begin(FrameJob& j)
     j.L = h->uses_lr ? frame_get(c, h->frame_width, h->frame_height) : nullptr;
     if (!j.R || !j.C || (h->uses_lr && !j.L)) return fail(c, AV1R_E_NOMEM, "frame allocation");
     j.k.cur = j.R->d;
-    j.D = deblock_tile() ? j.C : j.R;
-    j.Co = deblock_tile() ? j.R : j.C;
+    j.D = j.R;
+    j.Co = j.C;
     j.out = j.L ? j.L : j.Co;
     if (P.resElems > c->resCap) {
         if (c->resDev) {
@@ -1816,19 +1770,10 @@ static void job_end(FrameJob& j)
     c->lastUploadBytes = j.P->upBytes;
 }
 
-// AV1R_FLOW_CHAIN=1: the k_flow launches of a device form ONE chain (each waits for the
-// previous one, whichever stream launched it).  Round 1 needed it; since k_flow's
-// workgroups take their queues in entry order, overlapping grids cannot starve each other
-// (recon.hip, k_flow), so by default k_flow grids of different streams may run together:
-// a deep frame (a key frame's long intra chain) launched alone on its own stream overlaps
-// the other streams' batches.
-struct FlowChain {
-    std::mutex m;
-    hipStream_t last = nullptr;
-    hipEvent_t done = nullptr;
-};
-static FlowChain g_flowChain[64];
-
+// k_flow launches of different streams may run together: k_flow's workgroups take their
+// queues in entry order, so overlapping grids cannot starve each other (recon.hip, k_flow;
+// round 1 chained them, each waiting for the previous one): a deep frame (a key frame's long
+// intra chain) launched alone on its own stream overlaps the other streams' batches.
 // -DAV1R_FLOW_DEBUG: the stream that launched each epoch (av1r_flow_debug classifies the
 // overlapping pairs the kernel records as same-stream or cross-stream)
 #ifdef AV1R_FLOW_DEBUG
@@ -1866,9 +1811,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // k_flow workgroups per CU for a deep frame launched by itself (a key frame through the
     // per-frame API; the pipeline's solo frames take 1): fewer idle pollers along its long
     // chain -- a 1080p key frame alone 1.84 ms at the default 8, 1.73 at 4, 1.69 at 3, 1.67
-    // at 2 (AV1R_DEEP_PER_CU; 0 = the context's own setting)
-    static const int deepPer = getenv("AV1R_DEEP_PER_CU") ? atoi(getenv("AV1R_DEEP_PER_CU")) : 2;
-    const int perCU = deepPer > 0 && n == 1 && deep_frame(*jobs[0].P) ? std::min(lc->flowPerCU, deepPer) : lc->flowPerCU;
+    // at 2 (round 4)
+    const int deepPer = 2;
+    const int perCU = n == 1 && deep_frame(*jobs[0].P) ? std::min(lc->flowPerCU, deepPer) : lc->flowPerCU;
     if (n > AV1R_MAX_BATCH) return fail(c, AV1R_E_INVALID, "at most %d frames per batch", AV1R_MAX_BATCH);
     ctx_join(lc);
     hipStream_t st = lc->stream;
@@ -2000,10 +1945,6 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         uint32_t* hctl = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes);
         *reinterpret_cast<uint32_t**>(hctl + FLOW_HOSTERR) = rec ? rec->err : nullptr;
         hctl[FLOW_SPINLIM] = lc->flowSpins;
-        // AV1R_TICKET_PF=1: a workgroup takes its next group's ticket as it starts a group, so
-        // the atomic's round trip overlaps the group's work (recon.hip, k_flow)
-        static const uint32_t ticketPf = getenv("AV1R_TICKET_PF") ? (uint32_t)atoi(getenv("AV1R_TICKET_PF")) : 0u;
-        hctl[FLOW_FLAGS] = ticketPf ? 1u : 0u;
         uint32_t* g = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes + FLOW_CTL_BYTES);
         for (size_t l = 0; l < nLevels; l++)
             for (int i = 0; i < n; i++) {
@@ -2029,15 +1970,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         }
     }
     if (host_prof()) tp2 = now_us();
-    // AV1R_META_COPY=1: an SDMA copy on the context's copy stream instead of k_fetch
-    static const bool sdma = getenv("AV1R_META_COPY") && atoi(getenv("AV1R_META_COPY")) != 0;
-    if (sdma) {
-        HIPCHK(hipMemcpyAsync(M.dev, M.host, need, hipMemcpyHostToDevice, lc->copyStream));
-        HIPCHK(hipEventRecord(M.ready, lc->copyStream));
-        HIPCHK(hipStreamWaitEvent(st, M.ready, 0));
-    } else {
-        launch_k_fetch(M.dev, M.host, need, st);
-    }
+    launch_k_fetch(M.dev, M.host, need, st);
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
 
     if (lc->timing) {
@@ -2089,40 +2022,17 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     uint32_t traceBase = 0;
     static std::atomic<uint32_t> epochs{0};
     if (flow) {
-        // level 0's inter tiles, then every TB / inter-intra item in one dataflow launch.
-        // AV1R_INTER_SPLIT=1: the plain tiles (k_inter_m, k_inter_s) on the context's second
-        // stream beside the general k_inter (disjoint tiles).  Measured (tools/gpu_env_ab.sh):
-        // 4K x 2 streams device-only +3 % (inter 0.281 -> 0.245 ms/frame), 1080p x 8 -6 %
-        // (0.073 -> 0.087): off by default
-        const bool aux = inter_split() && lc->aux && total[0] && (total[1] || total[2]) && !trace;
-        hipStream_t sp = aux ? lc->aux : st;
-        if (aux) {
-            HIPCHK(hipEventRecord(lc->auxGo, st));
-            HIPCHK(hipStreamWaitEvent(lc->aux, lc->auxGo, 0));
-        }
-        // one grid for every inter tile (k_inter_all; AV1R_INTER_MERGED=0: the three kernels)
-        static const bool merged = !getenv("AV1R_INTER_MERGED") || atoi(getenv("AV1R_INTER_MERGED")) != 0;
-        // AV1R_INTER_CHUNKS: chunks per XCD of each class (k_inter_all's inter_deal; 1 = one
-        // contiguous eighth each)
-        static const uint32_t kc = getenv("AV1R_INTER_CHUNKS") ? (uint32_t)std::max(1, std::min(255, atoi(getenv("AV1R_INTER_CHUNKS")))) : 1u;
+        // level 0's inter tiles in one grid (k_inter_all: the general, medium and small
+        // classes; round 5: three launches 0.058 ms/frame, one 0.049), then every TB /
+        // inter-intra item in one dataflow launch.
         // AV1R_INTER_BANDS: each XCD's share walked band by band over the three classes.
         // Measured (profiles/r05_ab_inter_bands.txt, 1080p x 8): 4 bands fetch 22.3 instead of
         // 29.2 MB per frame in the same time (16: 21.8 MB, 4 % slower)
         static const uint32_t nb = getenv("AV1R_INTER_BANDS") ? (uint32_t)std::max(1, std::min(64, atoi(getenv("AV1R_INTER_BANDS")))) : 4u;
-        const uint32_t unit = 8 * kc * nb;
+        const uint32_t unit = 8 * nb;
         auto pad8 = [unit](uint32_t v) { return (v + unit - 1) / unit * unit; };
-        if (merged && !aux) {
-            if (total[0] + total[1] + total[2])
-                launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), kc | (nb << 8), trace, st);
-        } else {
-            if (total[1]) launch_k_level(2, dk, dtab + tabI, n, total[1], trace, ~0u, sp);
-            if (total[2]) launch_k_level(3, dk, dtab + tabI + tabS, n, total[2], trace, ~0u, sp);
-            if (total[0]) launch_k_level(0, dk, dtab, n, total[0], trace, ~0u, st);
-        }
-        if (aux) {
-            HIPCHK(hipEventRecord(lc->auxDone, lc->aux));
-            HIPCHK(hipStreamWaitEvent(st, lc->auxDone, 0));
-        }
+        if (total[0] + total[1] + total[2])
+            launch_k_inter_all(dk, dtab, n, pad8(total[0]), pad8(total[1]), pad8(total[2]), nb, trace, st);
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[5], st));
         // every residual (inter TBs outside inter-intra blocks added in place)
         const uint32_t* drt = reinterpret_cast<const uint32_t*>(M.dev + kBytes + tabBytes + FLOW_CTL_BYTES + 8 * nEntries);
@@ -2132,31 +2042,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         if (lc->timing) HIPCHK(hipEventRecord(lc->ev[6], st));
         if (nEntries) {
             if (lc->device < 0 || lc->device >= 64) return fail(c, AV1R_E_DEVICE, "device index");
-            static const bool chain = getenv("AV1R_FLOW_CHAIN") && atoi(getenv("AV1R_FLOW_CHAIN")) != 0;
-            FlowChain& F = g_flowChain[lc->device];
-            std::unique_lock<std::mutex> lock(F.m, std::defer_lock);
-            if (chain) lock.lock();
             // the persistent grid: every resident slot (lc->flowPerCU workgroups per CU; a
             // solo deep frame takes one per CU and leaves the rest to concurrent batches)
-            int grid = (int)std::min<size_t>(flow_grid(lc->device, perCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
-            if (lc->flowGridCap > 0) grid = std::max(FLOW_QUEUES, std::min(grid, lc->flowGridCap / FLOW_QUEUES * FLOW_QUEUES));
-            // epochs in chain order (unique per launch; taken under the chain's lock)
+            const int grid = (int)std::min<size_t>(flow_grid(lc->device, perCU), (nGroups + FLOW_QUEUES - 1) / FLOW_QUEUES * FLOW_QUEUES);
+            // (unique per launch)
             uint32_t epoch = ++epochs;
             if (!epoch) epoch = ++epochs;
-            if (chain) {
-                // a fresh event per k_flow: never re-recorded while another stream's wait may
-                // still refer to it (the previous one is released once waited for)
-                hipEvent_t ev = nullptr;
-                HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-                if (F.last && F.last != st) HIPCHK(hipStreamWaitEvent(st, F.done, 0));
-                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
-                HIPCHK(hipEventRecord(ev, st));
-                if (F.done) (void)hipEventDestroy(F.done);
-                F.done = ev;
-                F.last = st;
-            } else {
-                launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
-            }
+            launch_k_flow(dk, M.dev + kBytes + tabBytes + FLOW_CTL_BYTES, (uint32_t)nGroups, ctl, rec->err, epoch, grid, trace, st);
             flow_debug_note(epoch, st);
         }
     }
@@ -2203,15 +2095,11 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
     // ---- the in-loop filters (decode_frame_wrapup, Av1Decoder.cpp:181-189)
     // deblocking (LoopFilter::filter, LoopFilter.cpp:40-58): in place, one launch per pass
-    // (k_lf), or both passes in one launch, tile by tile in LDS into the deblocked frame
-    // (k_deblock; AV1R_DEBLOCK_TILE=1)
-    if (deblock_tile()) {
-        launch_k_lfcode(dk, n, maxUnits, st);
-        launch_k_deblock(dk, n, maxW, maxH, st);
-    } else {
-        launch_k_lf(dk, n, 0, maxUnits, st);
-        launch_k_lf(dk, n, 1, maxUnits, st);
-    }
+    // (k_lf).  Round 5 measured both passes of a 64x64 tile in LDS into a frame of their own
+    // (k_deblock, its edge decisions from a separate k_lfcode launch): 0.0141-0.0147 ms per
+    // 1080p frame against k_lf's 0.0108 (profiles/r05_ab_switches.txt); removed in round 6.
+    launch_k_lf(dk, n, 0, maxUnits, st);
+    launch_k_lf(dk, n, 1, maxUnits, st);
     if (snap && (rc = snapshot(AV1R_STAGE_LF, jobs[0].D))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[2], st));
     // ---- CDEF into its own frame (Cdef::filter copies the frame, Cdef.cpp:43)
@@ -2239,9 +2127,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         job_end(j);
     }
     if (rec) {
-        rec->meta = slot_meta() ? &M : nullptr;
+        rec->meta = &M;
         rec->gen = M.gen.load(std::memory_order_relaxed);
-        if (!rec->meta) HIPCHK(hipEventRecord(rec->done, st));
         std::lock_guard<std::mutex> lock(g_recMu);
         for (auto& j : jobs) rec->members.emplace_back(j.c, j.seq);
         g_recPending.push_back(rec);
@@ -2259,12 +2146,13 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
 // A frame whose dependency chain is long -- a key frame's intra wavefront: ~2 000 levels
 // at 1080p against ~80 for an inter frame -- holds a shared batch for its whole chain.  The
 // batched entry points launch it alone on its own context's stream instead (k_flow on one
-// workgroup per CU), where it overlaps the other streams' batches (AV1R_SOLO_LEVELS: the
-// level count above which a frame goes alone, 0 = never).
+// workgroup per CU), where it overlaps the other streams' batches: frames of more than 400
+// levels.  Round 5: kept in the shared batches -12 % device-only, alone on two workgroups per
+// CU -2 % (profiles/r05_ab_solo.txt); round 3: on at most 64 workgroups, k_flow +10 % (1080p)
+// and +85 % (4K).
 static bool deep_frame(const Prepared& P)
 {
-    static const int lim = getenv("AV1R_SOLO_LEVELS") ? atoi(getenv("AV1R_SOLO_LEVELS")) : 400;
-    return lim > 0 && P.flowOk && (int)P.levels.size() > lim;
+    return P.flowOk && (int)P.levels.size() > 400;
 }
 
 static int launch_solo(FrameJob& j)
@@ -2272,17 +2160,11 @@ static int launch_solo(FrameJob& j)
     av1r_ctx* m = j.c;
     av1r_ctx* c = m;
     std::vector<FrameJob> one(1, j);
-    // AV1R_SOLO_PER_CU: k_flow workgroups per CU of a solo deep frame (A/B)
-    static const int soloPer = getenv("AV1R_SOLO_PER_CU") ? std::max(1, atoi(getenv("AV1R_SOLO_PER_CU"))) : 1;
-    // AV1R_SOLO_GRID: at most this many workgroups for it (0: one per CU) -- a key frame keeps
-    // ~60 items in flight, its idle pollers on every CU compete with the batches beside it
-    static const int soloGrid = getenv("AV1R_SOLO_GRID") ? std::max(0, atoi(getenv("AV1R_SOLO_GRID"))) : 0;
+    // one k_flow workgroup per CU for a solo deep frame
     const int per = m->flowPerCU;
-    m->flowPerCU = soloPer;
-    m->flowGridCap = soloGrid;
+    m->flowPerCU = 1;
     int rc = launch_jobs(m, one);
     m->flowPerCU = per;
-    m->flowGridCap = 0;
     if (rc) return rc;
     HIPCHK(hipEventRecord(m->soloDone, m->stream));
     m->soloPending = true;
@@ -2357,7 +2239,6 @@ int av1r_create(int device, av1r_ctx** out)
     (void)hipEventCreateWithFlags(&c->soloDone, hipEventDisableTiming);
     for (auto& m : c->meta) {
         (void)hipEventCreateWithFlags(&m.done, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&m.ready, hipEventDisableTiming);
     }
     if (hipStreamCreateWithFlags(&c->copyStream, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
@@ -2366,14 +2247,6 @@ int av1r_create(int device, av1r_ctx** out)
     }
     (void)hipEventCreateWithFlags(&c->sync, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->joinEv, hipEventDisableTiming);
-    // the second stream of AV1R_INTER_SPLIT only where that A/B switch is on: streams map
-    // round-robin onto the process's hardware queues at creation, so an idle one per context
-    // would shift how the contexts' main streams share them
-    if (inter_split()) {
-        if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
-        (void)hipEventCreateWithFlags(&c->auxGo, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&c->auxDone, hipEventDisableTiming);
-    }
     for (int i = 0; i < 7; i++) (void)hipEventCreate(&c->ev[i]);
     c->evPool.reserve(64);
     if (const char* tf = getenv("AV1R_TRACE_FILE")) c->traceFile = fopen(tf, "ab");
@@ -2396,7 +2269,6 @@ void av1r_destroy(av1r_ctx* c)
     }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    if (c->aux) (void)hipStreamSynchronize(c->aux);
     (void)hipStreamSynchronize(c->copyStream);
     if (c->outStream) (void)hipStreamSynchronize(c->outStream);
     for (av1r_output_ticket* t : c->tickets) {  // tickets never waited for die with the context
@@ -2415,7 +2287,7 @@ void av1r_destroy(av1r_ctx* c)
         for (av1r_ctx* m : g_ctxs)
             if (m->joinLead == c) m->joinLead = nullptr;
         g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), c), g_ctxs.end());
-        // what waits for a launch through this context's meta slots (slot_meta: other
+        // what waits for a launch through this context's meta slots (other
         // contexts' upload slots, pooled packed buffers, status records) is complete now
         // (its streams are drained): forget the slots before they go
         auto mine = [&](const Upload* m) { return m >= c->meta && m < c->meta + av1r_ctx::kMetaRing; };
@@ -2451,27 +2323,14 @@ void av1r_destroy(av1r_ctx* c)
         if (u.host) (void)hipHostFree(u.host);
         if (u.dev) (void)hipFree(u.dev);
         (void)hipEventDestroy(u.done);
-        if (u.ready) (void)hipEventDestroy(u.ready);
     };
     for (auto& u : c->up) freeUpload(u);
     for (auto& u : c->pk) freeUpload(u);
     for (auto& u : c->meta) freeUpload(u);
     (void)hipStreamSynchronize(c->copyStream);
     (void)hipStreamDestroy(c->copyStream);
-    if (c->aux) (void)hipStreamDestroy(c->aux);
-    if (c->auxGo) (void)hipEventDestroy(c->auxGo);
-    if (c->auxDone) (void)hipEventDestroy(c->auxDone);
     if (c->resDev) (void)hipFree(c->resDev);
     if (c->granDev) (void)hipFree(c->granDev);
-    {  // its stream leaves the device's k_flow chain (no later wait refers to it)
-        FlowChain& F = g_flowChain[c->device & 63];
-        std::lock_guard<std::mutex> lock(F.m);
-        if (F.last == c->stream) {
-            if (F.done) (void)hipEventDestroy(F.done);
-            F.done = nullptr;
-            F.last = nullptr;
-        }
-    }
     harvest(false);  // records of launches on its (now idle) stream are complete
     {  // the context leaves every launch record still pending
         std::lock_guard<std::mutex> lock(g_recMu);
@@ -2652,12 +2511,10 @@ int av1r_decode_prepared_batch(av1r_ctx* const* ctxs, const int* handles, int n)
         jobs.push_back(j);
     }
     if (jobs.empty()) return AV1R_OK;
-    // AV1R_SPLIT=k: k sub-batches, each launched on its first member's stream, so that one
-    // sub-batch's low-parallelism phases (the k_flow tail) overlap another's launches
-    static const int split = std::max(1, getenv("AV1R_SPLIT") ? atoi(getenv("AV1R_SPLIT")) : 1);
-    const size_t k = std::min<size_t>(split, jobs.size());
-    for (size_t part = 0; part < k; part++) {
-        std::vector<FrameJob> sub(jobs.begin() + part * jobs.size() / k, jobs.begin() + (part + 1) * jobs.size() / k);
+    // one launch on the first member's stream (round 2: sub-batches on their own members'
+    // streams, so that one's k_flow tail overlaps another's launches, measured -25 %)
+    {
+        std::vector<FrameJob>& sub = jobs;
         av1r_ctx* sl = sub[0].c;
         av1r_ctx* c = sl;
         // the launch stream waits for every member's earlier work on its own stream (none
@@ -2879,7 +2736,6 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
     if (bl) ctx_join(bl);
     std::vector<FrameJob> jobs, solo;
     std::vector<Upload*> slots(n, nullptr);
-    std::vector<hipEvent_t> waits;  // uploads on member copy streams the batch waits for
     std::vector<bool> metaWait(n, false);  // packed buffers released by the launch's completion
     bool copies = false;
     for (int i = 0; i < n; i++) {
@@ -2891,11 +2747,10 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             continue;
         }
         const bool alone = n > 1 && deep_frame(pk->P);
-        // whose copy stream carries the upload: the batch lead's (AV1R_COPY_SPREAD=1: every
-        // member's own, spreading a batch's copies over the copy engines -- measured slower,
-        // 2 834 vs 3 179 frames/s host-inclusive)
-        static const bool spread = getenv("AV1R_COPY_SPREAD") && atoi(getenv("AV1R_COPY_SPREAD")) != 0;
-        av1r_ctx* up = alone || spread ? m : bl;
+        // whose copy stream carries the upload: the batch lead's (round 2: every member's own,
+        // spreading a batch's copies over the copy engines, measured slower -- 2 834 vs 3 179
+        // frames/s host-inclusive)
+        av1r_ctx* up = alone ? m : bl;
         Upload& U = m->pk[m->pkIdx];
         slots[i] = &U;
         m->pkIdx = (m->pkIdx + 1) % av1r_ctx::kPackRing;
@@ -2920,7 +2775,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         // alone or uploaded on another stream (something waits for it), else its launch's
         // completion (set below)
         pk->waitMeta = nullptr;
-        if (alone || up != bl || !slot_meta()) {
+        if (alone) {
             if (!pk->copied) HIPCHK(hipEventCreateWithFlags(&pk->copied, hipEventDisableTiming));
             HIPCHK(hipEventRecord(pk->copied, up->copyStream));
         } else {
@@ -2930,8 +2785,6 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         if (alone) {
             ctx_join(m);
             HIPCHK(hipStreamWaitEvent(m->stream, pk->copied, 0));
-        } else if (up != bl) {
-            waits.push_back(pk->copied);
         } else {
             copies = true;
         }
@@ -2968,7 +2821,6 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             HIPCHK(hipEventRecord(bl->pkReady, bl->copyStream));
             HIPCHK(hipStreamWaitEvent(bl->stream, bl->pkReady, 0));
         }
-        for (hipEvent_t e : waits) HIPCHK(hipStreamWaitEvent(bl->stream, e, 0));
         // a flow-only frame and a level-schedule frame (intra block copy) cannot share launches
         std::vector<FrameJob> lv;
         for (size_t i = 0; i < jobs.size();)
@@ -2991,7 +2843,9 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
         }
     }
     // the upload slots (and the packed buffers) are free again after their launch: its own
-    // completion event (slot_meta) or an event per slot
+    // completion event, through the launch's metadata slot (round 4: an event recorded per
+    // slot, per packed buffer and per status record, each a marker packet in the compute
+    // stream's hardware queue, held the headline at 6 100 against 6 370 frames/s)
     for (int i = 0; i < n; i++) {
         if (!slots[i]) continue;
         av1r_ctx* m = ctxs[i];
@@ -3002,7 +2856,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             pks[i]->waitGen = bl->lastMeta ? bl->lastMeta->gen.load(std::memory_order_relaxed) : 0;
             if (!bl->lastMeta) pks[i]->copyPending = false;  // (no launch read it: nothing to wait for)
         }
-        if (slot_meta() && lm) {
+        if (lm) {
             slots[i]->waitMeta = lm;
             slots[i]->waitGen = lm->gen.load(std::memory_order_relaxed);
         } else {
@@ -3106,13 +2960,8 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
 // barrier packet in whichever hardware queue the stream shares with others, holding them
 // until the copy is done.  A read-back counts as landed once its stream has gone idle
 // (copies on a stream complete in order): the bench's delivery leg 0.96x of the
-// undelivered rate against 0.88-0.90x with an event per read-back (AV1R_OUT_SQ=0).  (A
-// 4-byte copy of a flag word after the planes instead of the event measured 0.59x.)
-static bool out_sq()
-{
-    static const bool on = !getenv("AV1R_OUT_SQ") || atoi(getenv("AV1R_OUT_SQ")) != 0;
-    return on;
-}
+// undelivered rate against 0.88-0.90x with an event per read-back (round 4).  (A 4-byte
+// copy of a flag word after the planes instead of the event measured 0.59x.)
 
 static int ticket_issue(av1r_output_ticket* t, bool event = false);
 
@@ -3124,15 +2973,9 @@ int av1r_get_output_async(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, u
     // (the staged frames are older than the queued ones: they must leave first, through
     // av1r_get_output)
     if (!c->staged.empty()) return fail(c, AV1R_E_INVALID, "frames already staged by av1r_set_output_prefetch: use av1r_get_output");
-    int rc = output_ticket(c, y, ys, u, us, v, vs, width, height, out);
-    // AV1R_OUT_EAGER=1 (A/B): the copies are queued at once behind a device-side wait for
-    // the frame instead of when the host sees it done
-    static const bool eager = getenv("AV1R_OUT_EAGER") && atoi(getenv("AV1R_OUT_EAGER")) != 0;
-    if (!rc && eager) {
-        if (hipStreamWaitEvent(c->outStream, (*out)->ready, 0) != hipSuccess) rc = fail(c, AV1R_E_DEVICE, "output stream wait");
-        if (!rc) rc = ticket_issue(*out, true);
-    }
-    return rc;
+    // (round 4: the copies queued at once behind a device-side wait for the frame, instead
+    // of when the host sees it done, measured 0.48x of the undelivered rate)
+    return output_ticket(c, y, ys, u, us, v, vs, width, height, out);
 }
 
 // the oldest queued frame into a ticket (av1r_get_output_async; stage_outputs)
@@ -3143,11 +2986,8 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     if (c->outq.empty()) return AV1R_E_NO_OUTPUT;
     (void)hipSetDevice(c->device);
     if (!c->outStream) {
-        // AV1R_OUT_CUMASK=1 (A/B): the read-back stream created with a (full) CU mask, which
-        // the runtime gives a hardware queue of its own instead of sharing a compute stream's
-        static const bool cuMask = getenv("AV1R_OUT_CUMASK") && atoi(getenv("AV1R_OUT_CUMASK")) != 0;
-        // The read-backs go on the context's upload stream (AV1R_OUT_ON_COPY=0: a stream of
-        // their own).  Each read-back's completion marker sits in whichever of the runtime's
+        // The read-backs go on the context's upload stream (round 4 measured a stream of their
+        // own, also one created with a full CU mask: 0.84x).  Each read-back's completion marker sits in whichever of the runtime's
         // 4 hardware queues its stream landed on (streams attach to the least-used queue at
         // creation), holding back the streams that share it.  A stream of their own, created
         // late, shares a queue with a compute stream; the upload stream's queue holds copy
@@ -3156,15 +2996,7 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
         // the bench's delivery leg (after its other legs) 0.89-0.92x of the undelivered rate
         // on the upload stream against 0.82-0.84x on their own; tools/out_probe.py (fresh
         // contexts) the other way round, 0.82x against 0.89x
-        static const bool onCopy = !getenv("AV1R_OUT_ON_COPY") || atoi(getenv("AV1R_OUT_ON_COPY")) != 0;
-        if (onCopy) {
-            c->outStream = c->copyStream;
-        } else if (cuMask) {
-            const uint32_t mask[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
-            HIPCHK(hipExtStreamCreateWithCUMask(&c->outStream, 8, mask));
-        } else {
-            HIPCHK(hipStreamCreateWithFlags(&c->outStream, hipStreamNonBlocking));
-        }
+        c->outStream = c->copyStream;
     }
     av1r_output_ticket* t = nullptr;
     for (av1r_output_ticket* q : c->tickets)
@@ -3186,17 +3018,16 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     FrameBuf* f = c->outq.front();
     // the frame's last writer: this context's own stream, or the stream of the batch it was
     // last launched in (ctx_join is not needed: nothing is enqueued on the context here)
-    static const bool noReady = getenv("AV1R_OUT_NOREADY") && atoi(getenv("AV1R_OUT_NOREADY")) != 0;  // (A/B with NOCOPY)
     // the last launch on that stream has it (members join a batch stream behind their own
     // stream's work, ctx_join): its completion, or an event where a stream must wait on it
     // (the frame's own launch: a show-existing frame, or a context joined since -- ctx_join
     // clears joinLead without enqueuing work -- is not the context's last launch)
     av1r_ctx* w = c->joinLead ? c->joinLead : c;
     t->readyMeta = nullptr;
-    if (slot_meta() && !needEvent && f->wMeta) {
+    if (!needEvent && f->wMeta) {
         t->readyMeta = f->wMeta;
         t->readyGen = f->wGen;
-    } else if (!noReady) {
+    } else {
         HIPCHK(hipEventRecord(t->ready, w->stream));
     }
     c->outq.pop_front();  // the queue's reference passes to the ticket
@@ -3212,55 +3043,35 @@ static int output_ticket(av1r_ctx* c, uint8_t* y, int ys, uint8_t* u, int us, ui
     return AV1R_OK;
 }
 
-// whether the device can store to `p` directly: pinned host memory mapped at the same
-// address (hipHostMalloc; hipHostRegister'd memory under another device address is not)
-static bool device_writable_host(const void* p)
-{
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();  // pageable memory: clear the error for later launch checks
-        return false;
-    }
-    return a.type == hipMemoryTypeHost && a.devicePointer == p;
-}
-
 // event: record the read-back's own completion instead of watching its stream go idle --
-// for a copy queued behind a device-side wait (prefetch staging, AV1R_OUT_EAGER), whose
-// stream also carries every later frame's wait and copy
+// for a copy queued behind a device-side wait (prefetch staging), whose stream also carries
+// every later frame's wait and copy
 static int ticket_issue(av1r_output_ticket* t, bool event)
 {
     av1r_ctx* c = t->c;
-    // AV1R_OUT_NOCOPY=1 (A/B of the delivery machinery alone): no bytes move
-    static const bool noCopy = getenv("AV1R_OUT_NOCOPY") && atoi(getenv("AV1R_OUT_NOCOPY")) != 0;
-    // How the planes travel: three hipMemcpy2DAsync on the read-back stream (copy engine).
-    // AV1R_OUT_MODE=2 (A/B, pinned destinations): k_out stores them straight over the bus,
-    // leaving the copy engine to the uploads -- but the bus writes slowed every filter
-    // kernel 20-40% (8 x 1080p: 0.72x of the undelivered rate against 0.89x).  Packing the
-    // planes into device staging with k_out for one linear copy was slower still (0.55x):
-    // a kernel on the read-back stream stalls the compute stream sharing its queue.
-    static const int mode = getenv("AV1R_OUT_MODE") ? atoi(getenv("AV1R_OUT_MODE")) : 0;
+    // How the planes travel: on the read-back stream (copy engine), one linear transfer or
+    // three 2-D ones.  Round 4 measured a kernel (k_out) storing them straight over the bus
+    // into pinned memory: the bus writes slowed every filter kernel 20-40% (8 x 1080p: 0.72x
+    // of the undelivered rate against 0.89x); packing them into device staging for one linear
+    // copy 0.55x (a kernel on the read-back stream stalls the compute stream sharing its
+    // queue).  k_out was removed in round 6.
     const DevPlane* pl = t->f->d.pl;
     const uint8_t* src[3] = {pl[0].p, pl[1].p, pl[2].p};
     const int ss[3] = {pl[0].stride, pl[1].stride, pl[2].stride};
     const int w[3] = {pl[0].w, pl[1].w, pl[2].w}, h[3] = {pl[0].h, pl[1].h, pl[2].h};
     const bool sameLayout = t->dst[1] - t->dst[0] == src[1] - src[0] && t->dst[2] - t->dst[0] == src[2] - src[0] &&
                             t->ds[0] == ss[0] && t->ds[1] == ss[1] && t->ds[2] == ss[2];
-    if (noCopy) {
-    } else if (mode == 0 && sameLayout) {
+    if (sameLayout) {
         // a destination in the library's own layout (av1r_frame_layout; the ring sink): the
         // frame in ONE linear transfer, padding included (three 2-D copies left the copy
         // engine idle between them, ~10 us each)
         const size_t span = (size_t)(src[2] - src[0]) + (size_t)ss[2] * (h[2] - 1) + w[2];
         HIPCHK(hipMemcpyAsync(t->dst[0], src[0], span, hipMemcpyDeviceToHost, c->outStream));
-    } else if (mode == 2 && device_writable_host(t->dst[0]) && device_writable_host(t->dst[1]) &&
-               device_writable_host(t->dst[2])) {
-        launch_k_out(src, ss, t->dst, t->ds, w, h, c->outStream);
-        HIPCHK(hipGetLastError());
     } else {
         for (int p = 0; p < 3; p++)
             HIPCHK(hipMemcpy2DAsync(t->dst[p], t->ds[p], src[p], ss[p], w[p], h[p], hipMemcpyDeviceToHost, c->outStream));
     }
-    t->sq = out_sq() && !event;
+    t->sq = !event;
     if (!t->sq) HIPCHK(hipEventRecord(t->done, c->outStream));
     t->state = 1;
     return AV1R_OK;
@@ -3343,8 +3154,7 @@ int av1r_output_wait(av1r_output_ticket* t)
     t->f = nullptr;
     t->live = false;
     if (rc) return rc;
-    static const bool noHarvest = getenv("AV1R_OUT_NOHARVEST") && atoi(getenv("AV1R_OUT_NOHARVEST")) != 0;  // (A/B)
-    if (!noHarvest) harvest(false);
+    harvest(false);
     std::lock_guard<std::mutex> lock(g_recMu);
     if (frame_failed(c, f->seq)) return fail(c, AV1R_E_DEVICE, "frame %llu: %s", (unsigned long long)f->seq, c->err.c_str());
     return AV1R_OK;

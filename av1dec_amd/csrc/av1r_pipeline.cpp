@@ -437,12 +437,11 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
         bc.clear();
         bp.clear();
         const int g = P->g;
-        // group g: the g-th contiguous share of the streams, or (AV1R_PIPE_INTERLEAVE=1, A/B)
-        // streams g, g + G, ..., whose leads' streams land on different hardware queues
-        // (contexts create two streams each, dealt round-robin over 4 queues): measured
-        // 6 490-6 540 against 6 560-6 670 frames/s, so contiguous
-        static const bool inter = getenv("AV1R_PIPE_INTERLEAVE") && atoi(getenv("AV1R_PIPE_INTERLEAVE")) != 0;
-        const int sBeg = inter ? g : g * n / G, sEnd = inter ? n : (g + 1) * n / G, sStep = inter ? G : 1;
+        // group g: the g-th contiguous share of the streams (round 4: streams g, g + G, ...,
+        // whose leads' streams land on different hardware queues -- contexts create two
+        // streams each, dealt round-robin over 4 queues -- measured 6 490-6 540 against
+        // 6 560-6 670 frames/s)
+        const int sBeg = g * n / G, sEnd = (g + 1) * n / G, sStep = 1;
         P->g = (g + 1) % G;
         // full batches: while a stream that could join (live, not running a key frame alone)
         // has nothing packed yet, wait for it up to AV1R_PIPE_WAIT_US (bigger launches keep
@@ -512,9 +511,7 @@ int pipe_step(av1r_pipeline* P, int64_t frames, av1r_pipeline_stats* stats)
             }
             nframes += bc.size();
             batches++;
-            // AV1R_OUT_EVERY=k (A/B): the deliveries handled after every k-th launch only
-            static const int outEvery = std::max(1, getenv("AV1R_OUT_EVERY") ? atoi(getenv("AV1R_OUT_EVERY")) : 1);
-            if (rc == AV1R_OK && batches % outEvery == 0) rc = outputs(false);
+            if (rc == AV1R_OK) rc = outputs(false);
         } else if (live > 0 && rc == AV1R_OK && P->g == 0) {
             // nothing ready in any group: a worker's push wakes us; a key frame running alone does not,
             // hence the short bound

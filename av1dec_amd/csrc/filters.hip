@@ -263,8 +263,8 @@ DEV uint32_t lf_lo2(lf2 a, lf2 b)  // bytes {a.x, b.x, a.y, b.y}
 {
     return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
 }
-// The unit's pixels: the frame (k_lf, in place) or a tile staged in LDS (k_deblock).  x of
-// the 32-bit forms is a multiple of 4, of the 16-bit forms of 2.
+// The unit's pixels: the frame (k_lf, in place) or a tile staged in LDS.  x of the 32-bit
+// forms is a multiple of 4, of the 16-bit forms of 2.
 struct LfGlobalPx {
     uint8_t* p;
     int stride;
@@ -360,62 +360,12 @@ DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge&
                 __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u));
 }
 
-// an edge decision as one byte: the level (1..63) and the filter size (4 / 8 / 16 as 0 / 1 / 2
-// in bits 6..7); 0 = no filter
-DEV uint32_t lf_code(const KParams& k, int plane, int pass, int xP, int yP)
-{
-    LfEdge e;
-    const int lvl = lf_edge_level(k, plane, pass, xP, yP, e);
-    if (lvl <= 0) return 0;
-    return (uint32_t)lvl | ((e.filterSize == 4 ? 0u : e.filterSize == 8 ? 1u : 2u) << 6);
-}
-DEV LfEdge lf_decode(const av1r_frame_hdr& hd, uint32_t code)
-{
-    LfEdge e;
-    e.filterSize = 4 << (code >> 6);
-    lf_limits(hd, (int)(code & 63), e);
-    return e;
-}
-
-// k_lfcode: every edge decision of both passes, one lane per (plane, 4x4 unit), into k.lfc
-// (LoopFilter::loop_filter_edge's tests and the level / limit derivation, LoopFilter.cpp:85-126,
-// 301-359): the mode-info walk once per unit and pass, ahead of the filters.
-extern "C" __global__ __launch_bounds__(256) void k_lfcode(const KParams* kps)
-{
-    const uint3 wg = xcd_block();
-    const KParams& k = KP(kps, wg.y);
-    const av1r_frame_hdr& hd = *k.hdr;
-    if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped (k_lf / k_deblock test it)
-    const int nY = k.mi_rows * k.mi_cols;
-    const int cCols = (k.mi_cols + 1) / 2, nC = ((k.mi_rows + 1) / 2) * cCols;
-    const int id = wg.x * blockDim.x + threadIdx.x;
-    int plane, row0, col0;
-    if (id < nY) {
-        plane = 0;
-        row0 = id / k.mi_cols;
-        col0 = id - row0 * k.mi_cols;
-    } else if (id < nY + 2 * nC) {
-        int u = id - nY;
-        plane = 1 + (u >= nC);
-        if (u >= nC) u -= nC;
-        const int r = u / cCols;
-        row0 = r * 2;
-        col0 = (u - r * cCols) * 2;
-    } else {
-        return;
-    }
-    const int sub = plane ? 1 : 0;
-    const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
-    k.lfc[id] = (uint8_t)lf_code(k, plane, 0, xP, yP);
-    k.lfc[nY + 2 * nC + id] = (uint8_t)lf_code(k, plane, 1, xP, yP);
-}
-
 // one lane per (plane, 4x4 unit) edge of pass `pass`
-DEV void lf_body(const KParams* kps, int pass, int perFrame)
+DEV void lf_body(const KParams* kps, int pass)
 {
-    // (perFrame: every XCD takes an eighth of every frame's units instead of a contiguous
-    // eighth of the whole launch, i.e. about one frame each; the frames differ in cost)
-    const uint3 wg = perFrame ? make_uint3(xcd_order(blockIdx.x, gridDim.x), blockIdx.y, 0) : xcd_block();
+    // (each XCD a contiguous eighth of the whole launch, i.e. about one frame; round 5: an
+    // eighth of every frame's units per XCD measured within noise, r05_ab_xcd_dealing.txt)
+    const uint3 wg = xcd_block();
     const KParams& k = KP(kps, wg.y);  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
     if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
@@ -439,8 +389,9 @@ DEV void lf_body(const KParams* kps, int pass, int perFrame)
     }
     const int sub = plane ? 1 : 0;
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
-    // the edge's decision from the mode info, in the lane (k_lfcode's bytes ahead of the
-    // launch measured slower here: 0.0116 against 0.0108 ms per 1080p frame with its launch;
+    // the edge's decision from the mode info, in the lane (round 5: every decision taken by a
+    // separate launch ahead, k_lfcode, measured slower: 0.0116 against 0.0108 ms per 1080p
+    // frame with its launch;
     // the unit's samples loaded speculatively with the mode info, before the decision:
     // 0.0119 against 0.0105, profiles/r05_ab_lf_spec.txt -- most units filter nothing)
     LfEdge e;
@@ -449,160 +400,7 @@ DEV void lf_body(const KParams* kps, int pass, int perFrame)
     lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
-extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass, int perFrame) { lf_body(kps, pass, perFrame); }
-
-// ------------------------------------------------------------------------------------
-// k_deblock: both deblocking passes of one 64x64 luma tile and its two 32x32 chroma tiles
-// in ONE workgroup, in LDS, into the deblocked frame (k.dbk).  LoopFilter::filter
-// (LoopFilter.cpp:40-58) runs pass 0 (vertical edges) over the whole frame, then pass 1;
-// within a tile the same order holds, and what a tile's pixels depend on is bounded:
-//   * an edge at x modifies at most 6 luma / 2 chroma samples on each side and reads 7 / 3
-//     (the filter length is capped by the transform sizes on both sides), so the pixels of
-//     [x0, x0 + 64) after pass 0 are set by the vertical edges x0 .. x0 + 64, which read
-//     [x0 - 8, x0 + 72);
-//   * pass 1 over columns [x0, x0 + 64) needs the pass-0 pixels of rows [y0 - 8, y0 + 72)
-//     (edges y0 .. y0 + 64).
-// So the tile stages [x0 - 8, x0 + 72) x [y0 - 8, y0 + 72) (chroma [cx0 - 8, cx0 + 40) x
-// [cy0 - 8, cy0 + 40)), runs pass 0 over all its rows and pass 1 over its columns, and
-// writes back only its own 64 x 64 (32 x 32).  The boundary edges are computed by both
-// tiles they touch, identically (1.3x the edges of pass 0, 1.06x of pass 1).  Each edge's
-// decision (filter size and level, lf_edge: LoopFilter.cpp:85-126, 301-359) is taken once,
-// up front, into a byte of LDS: the mode-info loads go out together with the pixel loads.
-// Reads k.cur (reconstruction, intact during the launch), writes k.dbk.
-// ------------------------------------------------------------------------------------
-#define DB_YS 80  // luma tile: 80 x 80 (64 + 8 each side)
-#define DB_CS 48  // chroma tile: 48 x 48 (32 + 8 each side)
-struct DbLds {
-    uint8_t y[DB_YS * DB_YS];
-    uint8_t uv[2][DB_CS * DB_CS];
-    uint8_t c0y[20 * 17];     // pass 0 luma: unit row u (rows y0 - 8 + 4u), edge e (x0 + 4e): [u * 17 + e]
-    uint8_t c1y[17 * 16];     // pass 1 luma: edge e (y0 + 4e), unit column u (x0 + 4u): [e * 16 + u]
-    uint8_t c0c[2][12 * 9];   // pass 0 chroma: unit row u (cy0 - 8 + 4u), edge e (cx0 + 4e)
-    uint8_t c1c[2][9 * 8];    // pass 1 chroma: edge e (cy0 + 4e), unit column u (cx0 + 4u)
-};
-extern "C" __global__ __launch_bounds__(256) void k_deblock(const KParams* kps)
-{
-    __shared__ __align__(16) DbLds L;
-    const int t = threadIdx.x;
-    const uint3 wg = xcd_block();  // x: 64-column tile, y: 64-row tile, z: frame
-    const KParams& k = KP(kps, wg.z);
-    const av1r_frame_hdr& hd = *k.hdr;
-    const int x0 = (int)wg.x * 64, y0 = (int)wg.y * 64;
-    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4;
-    if (x0 >= limX || y0 >= limY) return;
-    const int cx0 = x0 >> 1, cy0 = y0 >> 1;
-    // ---- stage the reconstructed pixels: every lane's dwords loaded before its first LDS
-    // store (one memory round trip).  Dwords outside [0, lim + 8) (the frame's top / left
-    // margin does not exist; nothing past the mi grid + 8 is read by a filter) stay 0.
-    constexpr int NDY = DB_YS / 4, NY = DB_YS * NDY, QY = (NY + 255) / 256;
-    constexpr int NDC = DB_CS / 4, NC = DB_CS * NDC, QC = (2 * NC + 255) / 256;
-    uint32_t vy[QY], vc[QC];
-#pragma unroll
-    for (int u = 0; u < QY; u++) {
-        const int q = t + 256 * u, i = q / NDY, d = q - i * NDY;
-        const int y = y0 - 8 + i, x = x0 - 8 + 4 * d;
-        vy[u] = q < NY && y >= 0 && x >= 0 && y < limY + 8 && x < limX + 8
-                    ? *reinterpret_cast<const uint32_t*>(k.cur.pl[0].p + (size_t)y * k.cur.pl[0].stride + x) : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < QC; u++) {
-        const int q = t + 256 * u, pl = q >= NC, r = q - pl * NC, i = r / NDC, d = r - i * NDC;
-        const int y = cy0 - 8 + i, x = cx0 - 8 + 4 * d;
-        const DevPlane& P = k.cur.pl[1 + pl];
-        vc[u] = q < 2 * NC && y >= 0 && x >= 0 && y < (limY >> 1) + 8 && x < (limX >> 1) + 8
-                    ? *reinterpret_cast<const uint32_t*>(P.p + (size_t)y * P.stride + x) : 0u;
-    }
-    // ---- the edge decisions of both passes (k_lfcode's bytes; their loads go out with the
-    // pixels')
-    const bool on = hd.lf_level[0] || hd.lf_level[1];  // else LoopFilter::filter is skipped: a copy
-    const int nY = k.mi_rows * k.mi_cols, cCols = (k.mi_cols + 1) / 2, cRows = (k.mi_rows + 1) / 2;
-    const int nU = nY + 2 * cRows * cCols;
-    // the code of the unit at plane position (xP, yP) for `pass` (0 outside the mi grid)
-    auto code_at = [&](int plane, int pass, int xP, int yP) -> uint32_t {
-        const int col = xP >> 2, row = yP >> 2;
-        if (!on || xP < 0 || yP < 0) return 0u;
-        if (!plane) return row < k.mi_rows && col < k.mi_cols ? k.lfc[(size_t)pass * nU + row * k.mi_cols + col] : 0u;
-        return row < cRows && col < cCols ? k.lfc[(size_t)pass * nU + nY + (plane - 1) * cRows * cCols + row * cCols + col] : 0u;
-    };
-    for (int q = t; q < 20 * 17 + 17 * 16 + 2 * (12 * 9 + 9 * 8); q += 256) {
-        if (q < 340) {
-            const int u = q / 17, e = q - u * 17;
-            L.c0y[q] = (uint8_t)code_at(0, 0, x0 + 4 * e, y0 - 8 + 4 * u);
-        } else if (q < 340 + 272) {
-            const int r = q - 340, e = r >> 4, u = r & 15;
-            L.c1y[r] = (uint8_t)code_at(0, 1, x0 + 4 * u, y0 + 4 * e);
-        } else {
-            const int r = q - 612, pl = r >= 180, r2 = r - 180 * pl;
-            if (r2 < 108) {
-                const int u = r2 / 9, e = r2 - u * 9;
-                L.c0c[pl][r2] = (uint8_t)code_at(1 + pl, 0, cx0 + 4 * e, cy0 - 8 + 4 * u);
-            } else {
-                const int r3 = r2 - 108, e = r3 >> 3, u = r3 & 7;
-                L.c1c[pl][r3] = (uint8_t)code_at(1 + pl, 1, cx0 + 4 * u, cy0 + 4 * e);
-            }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < QY; u++) {
-        const int q = t + 256 * u;
-        if (q < NY) reinterpret_cast<uint32_t*>(L.y)[q] = vy[u];
-    }
-#pragma unroll
-    for (int u = 0; u < QC; u++) {
-        const int q = t + 256 * u, pl = q >= NC;
-        if (q < 2 * NC) reinterpret_cast<uint32_t*>(L.uv[pl])[q - pl * NC] = vc[u];
-    }
-    __syncthreads();
-    if (on) {
-        // ---- pass 0: vertical edges over every staged row
-        for (int q = t; q < 340 + 216; q += 256) {
-            uint32_t c;
-            int plane, xT, yT;
-            if (q < 340) {
-                const int u = q / 17, e = q - u * 17;
-                c = L.c0y[q], plane = 0, xT = 8 + 4 * e, yT = 4 * u;
-            } else {
-                const int r = q - 340, pl = r >= 108, r2 = r - 108 * pl, u = r2 / 9, e = r2 - u * 9;
-                c = L.c0c[pl][r2], plane = 1 + pl, xT = 8 + 4 * e, yT = 4 * u;
-            }
-            if (!c) continue;
-            const LfLdsPx P{(lf_lds_u8*)(plane ? L.uv[plane - 1] : L.y), plane ? DB_CS : DB_YS};
-            lf_unit(P, plane, 0, xT, yT, lf_decode(hd, c));
-        }
-        __syncthreads();
-        // ---- pass 1: horizontal edges over the tile's own columns
-        for (int q = t; q < 272 + 144; q += 256) {
-            uint32_t c;
-            int plane, xT, yT;
-            if (q < 272) {
-                const int e = q >> 4, u = q & 15;
-                c = L.c1y[q], plane = 0, xT = 8 + 4 * u, yT = 8 + 4 * e;
-            } else {
-                const int r = q - 272, pl = r >= 72, r2 = r - 72 * pl, e = r2 >> 3, u = r2 & 7;
-                c = L.c1c[pl][r2], plane = 1 + pl, xT = 8 + 4 * u, yT = 8 + 4 * e;
-            }
-            if (!c) continue;
-            const LfLdsPx P{(lf_lds_u8*)(plane ? L.uv[plane - 1] : L.y), plane ? DB_CS : DB_YS};
-            lf_unit(P, plane, 1, xT, yT, lf_decode(hd, c));
-        }
-        __syncthreads();
-    }
-    // ---- the tile's own pixels into the deblocked frame (the mi grid's extent)
-    const int rowsY = imin(64, limY - y0), colsY = imin(64, limX - x0);  // (multiples of 4)
-    for (int q = t; q < 64 * 16; q += 256) {
-        const int i = q >> 4, d = q & 15;
-        if (i < rowsY && 4 * d < colsY)
-            *reinterpret_cast<uint32_t*>(k.dbk.pl[0].p + (size_t)(y0 + i) * k.dbk.pl[0].stride + x0 + 4 * d) =
-                *reinterpret_cast<const uint32_t*>(&L.y[(8 + i) * DB_YS + 8 + 4 * d]);
-    }
-    const int rowsC = rowsY >> 1, colsC = colsY >> 1;  // (multiples of 2)
-    for (int q = t; q < 2 * 32 * 16; q += 256) {
-        const int pl = q >> 9, r = q & 511, i = r >> 4, d = r & 15;  // 16-bit pairs
-        if (i < rowsC && 2 * d < colsC)
-            *reinterpret_cast<uint16_t*>(k.dbk.pl[1 + pl].p + (size_t)(cy0 + i) * k.dbk.pl[1 + pl].stride + cx0 + 2 * d) =
-                *reinterpret_cast<const uint16_t*>(&L.uv[pl][(8 + i) * DB_CS + 8 + 2 * d]);
-    }
-}
+extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
 
 // ------------------------------------------------------------------------------------
 // CDEF
@@ -620,15 +418,31 @@ DEV int constrain(int diff, int threshold, int damping)
 // chroma regions.  The deblocked pixels with a 2-pixel halo are staged in LDS once (rows
 // of aligned dwords away from the frame edge); the direction search runs one lane per
 // (8x8 block, direction) pair summing each partial line straight from LDS; the filter
-// runs two horizontally adjacent pixels per packed 16-bit operation, each lane on rows of
-// one block (luma: 4 lanes per 8x8 block, chroma: 2 lanes per 4x4 block and plane).
+// runs two horizontally adjacent pixels per packed 16-bit operation, one 4-pixel group per
+// lane and instruction.
+//
+// LDS banks (round 6).  Every tap read is a pair of ds_read_b32 (bank = dword mod 32, two
+// 32-lane groups), so the row strides and the lane -> (row, group) maps are chosen together:
+//  - luma: a half-wave holds rows r and r + 4 of one 8-row block row x the 16 dword groups
+//    of the region's 64 columns; at 20 dwords per row, 4 rows are 80 = 16 (mod 32) dwords,
+//    so the centre reads of the 32 lanes land on 32 distinct banks (round 5: 72-byte rows,
+//    the 4 lanes of a block 2 rows apart -> 14 banks for 32 lanes, 56.7 % of LDS cycles
+//    were conflicts);
+//  - chroma: a half-wave holds rows r, r + 2, r + 4, r + 6 x the 8 dword groups of one
+//    plane's 32 columns; at 12 dwords per row, 2 rows are 24 dwords, and {0, 24, 48, 72}
+//    = {0, 24, 16, 8} (mod 32);
+//  - the direction search reads each block's rows as 8-byte ds_read_b64 (bank = dword mod
+//    64): blocks 8 rows apart are 160 = 32 (mod 64) dwords apart, so lanes of block rows by
+//    and by + 2 read their rows in the order i ^ 4 (80 = 16 (mod 64) dwords further).
+// A tap of another direction still shifts a block's lanes (per-block directions), so tap
+// reads of neighbouring blocks may meet on a bank; the centre and equal-direction reads do not.
 #define CD_H 2            // tap reach (Cdef_Directions)
-#define CD_X 4            // LDS column of plane column x0 (dword-aligned staging from x0 - 4)
-#define CD_LS 72          // luma tile: columns x0 - 4 .. x0 + 67
+#define CD_X 8            // LDS column of plane column x0 (dword-aligned staging from x0 - 8)
+#define CD_LS 80          // luma tile: columns x0 - 8 .. x0 + 71 (20 dwords)
 #define CD_LR (64 + 2 * CD_H)
-#define CD_CS 40          // chroma tile: columns x0 / 2 - 4 .. x0 / 2 + 35
+#define CD_CS 48          // chroma tile: columns x0 / 2 - 8 .. x0 / 2 + 39 (12 dwords)
 #define CD_CR (32 + 2 * CD_H)
-struct CdefLds {
+struct alignas(16) CdefLds {
     uint8_t y[CD_LR][CD_LS];
     uint8_t uv[2][CD_CR][CD_CS];
     int cost[64][8];
@@ -799,10 +613,10 @@ DEV void cd_stage(uint8_t* t, int ts, int nrows, const DevPlane& P, int x0, int 
 }
 
 // grid (ceil(MiCols / 16), ceil(MiRows / 16), frames); reads k.dbk, writes k.cdef
-DEV void cdef_body(const KParams* kps, int perFrame)
+DEV void cdef_body(const KParams* kps)
 {
     __shared__ CdefLds L;
-    const uint3 wg = perFrame ? xcd_block_xy() : xcd_block();  // (as lf_body)
+    const uint3 wg = xcd_block();  // (as lf_body)
     const KParams& k = KP(kps, wg.z);
     const int t = threadIdx.x;
     const int r0 = wg.y * 16, c0 = wg.x * 16;  // mi units
@@ -886,12 +700,23 @@ DEV void cdef_body(const KParams* kps, int perFrame)
         const int b = t & 63, w = t >> 6;
         if (L.filt[b]) {
             const int bx = (b & 7) * 8, by = (b >> 3) * 8;
+            // rows in the order i ^ 4 for block rows 2, 3, 6, 7 (banks: header above)
+            const int rot = (b >> 4) & 1;
+            // (each row index opaque to the compiler: one ds_read_b64 per row, not pairs
+            // merged into ds_read2_b64, whose 16-lane groups bank mod 32)
+            uint64_t v[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                int row = CD_H + by + (i ^ (4 * rot));
+                asm volatile("" : "+v"(row));
+                v[i] = *reinterpret_cast<const uint64_t*>(&L.y[row][CD_X + bx]);
+            }
             uint32_t rw[8][2];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const uint2 v = *reinterpret_cast<const uint2*>(&L.y[CD_H + by + i][CD_X + bx]);
-                rw[i][0] = v.x;
-                rw[i][1] = v.y;
+                const uint64_t r = rot ? v[i ^ 4] : v[i];
+                rw[i][0] = (uint32_t)r;
+                rw[i][1] = (uint32_t)(r >> 32);
             }
             auto px8 = [&](int i, int j) { return (int)((rw[i][j >> 2] >> (8 * (j & 3))) & 0xff) - 128; };
             int c0, c1;
@@ -931,46 +756,45 @@ DEV void cdef_body(const KParams* kps, int perFrame)
             }
     }
     __syncthreads();
-    // luma: 4 lanes per 8x8 block, two rows of 8 (two 4-pixel groups) each
+    // luma: half-wave hw = block row; lane (k, d) takes the 4-pixel group d (0..15) of rows
+    // u + 4k (u = 0..3) of that block row, all in the 8x8 block d / 2
     {
-        const int b = t >> 2, bi = b >> 3, bj = b & 7;
-        const int j0 = bj * 8;
+        const int bi = t >> 5, d = t & 15, kq = (t >> 4) & 1;
+        const int b = bi * 8 + (d >> 1);
+        const int j0 = 4 * d;
         const int ySec = h.cdef_y_sec[idx];
-        if (j0 < cols4 * 4) {
-            const bool full = j0 + 8 <= cols4 * 4;  // else only the left 4 columns are in the grid
+        if (d < cols4) {  // (a group is one mi column)
             const bool f = L.filt[b];
             const int pri = L.pri[b];
-            for (int r = 0; r < 2; r++) {
-                const int i = bi * 8 + (t & 3) * 2 + r;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = bi * 8 + u + 4 * kq;
                 if (i >= rows4 * 4) break;
                 const int p = (CD_H + i) * CD_LS + CD_X + j0;
-                uint32_t o[2] = {0, 0};
-#pragma unroll
-                for (int g = 0; g < 2; g++) {
-                    if (g && !full) break;
-                    if (!f) o[g] = *reinterpret_cast<const uint32_t*>(&L.y[0][0] + p + 4 * g);
-                    else if (edge)
-                        o[g] = cdef_quad<true>(&L.y[0][0], p + 4 * g, L.offY[b], pri, ySec, h.cdef_damping, x0 + j0 + 4 * g, y0 + i, CD_LS, limX, limY);
-                    else
-                        o[g] = cdef_quad<false>(&L.y[0][0], p + 4 * g, L.offY[b], pri, ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
-                }
-                uint8_t* dst = &px(k.cdef.pl[0], x0 + j0, y0 + i);
-                if (full) *reinterpret_cast<uint2*>(dst) = make_uint2(o[0], o[1]);
-                else *reinterpret_cast<uint32_t*>(dst) = o[0];
+                uint32_t o;
+                if (!f) o = *reinterpret_cast<const uint32_t*>(&L.y[0][0] + p);
+                else if (edge)
+                    o = cdef_quad<true>(&L.y[0][0], p, L.offY[b], pri, ySec, h.cdef_damping, x0 + j0, y0 + i, CD_LS, limX, limY);
+                else
+                    o = cdef_quad<false>(&L.y[0][0], p, L.offY[b], pri, ySec, h.cdef_damping, 0, 0, CD_LS, 0, 0);
+                *reinterpret_cast<uint32_t*>(&px(k.cdef.pl[0], x0 + j0, y0 + i)) = o;
             }
         }
     }
-    // chroma: 2 lanes per 4x4 block and plane, two rows of 4 each
+    // chroma: half-wave hw -> plane hw / 4 and 8 rows (two 4x4 block rows); lane (k, d) takes
+    // the 4-pixel group d (one 4x4 block column) of rows u + 2k (u = 0, 1), in block row k / 2
     {
         const int uvPri = h.cdef_uv_pri[idx], uvSec = h.cdef_uv_sec[idx];
-        const int pl = t >> 7, b = (t >> 1) & 63, bi = b >> 3, bj = b & 7;
+        const int hw = t >> 5, pl = hw >> 2, bj = t & 7, kq = (t >> 3) & 3;
+        const int bi = 2 * (hw & 3) + (kq >> 1), b = bi * 8 + bj;
         const int j0 = bj * 4;
         if (j0 < cols4 * 2) {
             const bool full = j0 + 4 <= cols4 * 2;  // else only the left 2 columns are in the grid
             const bool f = L.filt[b];
             const uint8_t* tile = &L.uv[pl][0][0];
+#pragma unroll
             for (int r = 0; r < 2; r++) {
-                const int i = bi * 4 + (t & 1) * 2 + r;
+                const int i = 8 * (hw & 3) + r + 2 * kq;
                 if (i >= rows4 * 2) break;
                 const int p = (CD_H + i) * CD_CS + CD_X + j0;
                 uint32_t o;
@@ -987,7 +811,7 @@ DEV void cdef_body(const KParams* kps, int perFrame)
     }
 }
 // (6 waves per SIMD instead of 5 measured no faster: the filters are not occupancy-bound)
-extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps, int perFrame) { cdef_body(kps, perFrame); }
+extern "C" __global__ __launch_bounds__(256) void k_cdef(const KParams* kps) { cdef_body(kps); }
 
 // ------------------------------------------------------------------------------------
 // Loop restoration
@@ -1407,60 +1231,6 @@ void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s)
         reinterpret_cast<uint32_t*>(const_cast<void*>(src)), n4);
 }
 
-// Frame read-back straight into pinned host memory over the bus (av1r_get_output_async,
-// AV1R_OUT_MODE=2 A/B; the default moves the planes with the copy engine).  One wave per
-// row, 16-byte non-temporal stores when every address and width allow, else dwords, else
-// bytes.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct OutPlanes {
-    const uint8_t* src[3];
-    uint8_t* dst[3];
-    int ss[3], ds[3], w[3], h[3];
-};
-extern "C" __global__ __launch_bounds__(256) void k_out(OutPlanes o)
-{
-    const int p = blockIdx.y, lane = threadIdx.x & 63;
-    const int w = o.w[p], h = o.h[p], ss = o.ss[p], ds = o.ds[p];
-    const uint8_t* src = o.src[p];
-    uint8_t* dst = o.dst[p];
-    const uintptr_t al = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)ss | (uintptr_t)ds | (uintptr_t)w;
-    const int waves = gridDim.x * 4;
-    for (int y = blockIdx.x * 4 + (threadIdx.x >> 6); y < h; y += waves) {
-        const uint8_t* s = src + (size_t)y * ss;
-        uint8_t* d = dst + (size_t)y * ds;
-        if (!(al & 15)) {
-            for (int x = lane * 16; x < w; x += 2 * 64 * 16) {  // both loads of a 2 KB span first
-                const bool two = x + 64 * 16 < w;
-                const u32x4 a = *reinterpret_cast<const u32x4*>(s + x);
-                u32x4 b;
-                if (two) b = *reinterpret_cast<const u32x4*>(s + x + 64 * 16);
-                __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(d + x));
-                if (two) __builtin_nontemporal_store(b, reinterpret_cast<u32x4*>(d + x + 64 * 16));
-            }
-        } else if (!(al & 3)) {
-            for (int x = lane * 4; x < w; x += 64 * 4)
-                __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(s + x), reinterpret_cast<uint32_t*>(d + x));
-        } else {
-            for (int x = lane; x < w; x += 64) d[x] = s[x];
-        }
-    }
-}
-void launch_k_out(const uint8_t* const src[3], const int ss[3], uint8_t* const dst[3], const int ds[3], const int w[3],
-                  const int h[3], hipStream_t st)
-{
-    OutPlanes o;
-    for (int p = 0; p < 3; p++) {
-        o.src[p] = src[p];
-        o.dst[p] = dst[p];
-        o.ss[p] = ss[p];
-        o.ds[p] = ds[p];
-        o.w[p] = w[p];
-        o.h[p] = h[p];
-    }
-    // 128 rows in flight per plane: enough stores outstanding to fill the link, few CUs taken
-    hipLaunchKernelGGL(k_out, dim3(32, 3), dim3(256), 0, st, o);
-}
-
 // ------------------------------------------------------------------------------------
 // k_mi: the mode-info grid of each frame of the launch, derived from its records instead of
 // uploaded (24 B per 4x4 unit: 3.1 MB of a 1080p frame's ~7.6 MB batch).  What the parser
@@ -1549,27 +1319,13 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 
 // ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
-// AV1R_FILT_XCD=1: k_lf and k_cdef deal every frame over the XCDs (lf_body)
-static int filt_per_frame()
-{
-    static const int v = getenv("AV1R_FILT_XCD") ? atoi(getenv("AV1R_FILT_XCD")) : 0;
-    return v;
-}
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass, filt_per_frame());
-}
-void launch_k_lfcode(const KParams* kps, int n, int maxUnits, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_lfcode, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps);
-}
-void launch_k_deblock(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_deblock, dim3((maxW + 63) / 64, (maxH + 63) / 64, n), dim3(256), 0, s, kps);
+    hipLaunchKernelGGL(k_lf, dim3((maxUnits + 255) / 256, n), dim3(256), 0, s, kps, pass);
 }
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps, filt_per_frame());
+    hipLaunchKernelGGL(k_cdef, dim3((maxMiCols + 15) / 16, (maxMiRows + 15) / 16, n), dim3(256), 0, s, kps);
 }
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {

@@ -1658,7 +1658,7 @@ DEV void small_pu_c2(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int
 // Frames' lists are dealt in groups of 64 / NT (a frame's last group may be partial), so
 // the parameters of a workgroup stay uniform.  tab: [group prefix (n + 1)][offsets (n)][counts (n)].
 template <int NT, int MS>
-DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, SmallLds<MS>* L, int chroma2 = 1)
+DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n, uint32_t b, SmallLds<MS>* L)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
@@ -1672,7 +1672,9 @@ DEV void inter_plain(const KParams* kps, const uint32_t* __restrict__ tab, int n
     for (int plane = 0; plane < nPl; plane++) {
         // (sub-8x8 chroma may gather up to four units of neighbouring blocks)
         const PlaneGeo G = plane_geo<MS>(k, blk, plane, 0, 0);
-        if (plane == 1 && chroma2 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col) {
+        // (a block whose chroma is one prediction unit: both planes' windows in one memory
+        // round trip -- round 5: 0.0484 -> 0.0480 ms/frame, kept)
+        if (plane == 1 && G.predW == G.pw && G.predH == G.ph && G.candRow == blk.mi_row && G.candCol == blk.mi_col) {
             small_pu_c2<NT, MS>(k, L[g], blk, G.baseX, G.baseY, G.pw, G.ph, G.candRow, G.candCol);
             break;
         }
@@ -1715,17 +1717,15 @@ extern "C" __global__ K_PLAIN_BOUNDS void k_inter_m(const KParams* kps, const ui
 // every logical index is run by exactly one workgroup wherever it lands.
 // tab: [k_inter table][k_inter_m table][k_inter_s table] (launch_jobs); gI / gM / gS the classes'
 // padded workgroup counts.
-// kc (>= 1): each class is cut into 8 * kc chunks, chunk c to XCD c % 8 -- kc = 1 gives every
-// XCD one contiguous eighth; larger kc mixes several frames' regions into each XCD's share
-// (a batch's frames differ in cost) while a chunk keeps its neighbouring tiles on one L2.
-// The class counts are padded to multiples of 8 * kc.
-DEV uint32_t inter_deal(uint32_t x, uint32_t j, uint32_t q, uint32_t kc)
+// Each class is cut into 8 contiguous eighths, eighth x to XCD x (round 5: several chunks per
+// XCD, mixing frames' regions into each share, measured within noise,
+// profiles/r05_ab_xcd_dealing.txt).  The class counts are padded to multiples of 8 * bands.
+DEV uint32_t inter_deal(uint32_t x, uint32_t j, uint32_t q)
 {
-    const uint32_t C = q / kc, kk = j / C;  // chunk size (workgroups), this XCD's chunk number
-    return (kk * 8 + x) * C + (j - kk * C);
+    return x * q + j;
 }
 extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const uint32_t* __restrict__ tab, int n,
-    uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc, int c2, unsigned long long* trace)
+    uint32_t gI, uint32_t gM, uint32_t gS, uint32_t nb, unsigned long long* trace)
 {
     union Lds {
         InterLds g;
@@ -1738,12 +1738,11 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const 
     const uint32_t* tI = tab;
     const uint32_t* tM = tI + 2 * n + 1;
     const uint32_t* tS = tM + 3 * n + 1;
-    // kc: chunks per XCD (bits 0-7) and bands (bits 8-15, AV1R_INTER_BANDS): with nb > 1 each
-    // XCD walks its share band by band -- the general, medium and small tiles of band 0, then of
-    // band 1, ... (the class lists are in decode order, so a band is a stretch of the frame) --
-    // so that a region's reference lines are fetched once for all three classes, not once per
-    // class sweep.  The class counts are padded to multiples of 8 * chunks * bands.
-    const uint32_t kcc = kc & 0xffu, nb = (kc >> 8) ? (kc >> 8) : 1u;
+    // nb: bands (AV1R_INTER_BANDS): with nb > 1 each XCD walks its share band by band -- the
+    // general, medium and small tiles of band 0, then of band 1, ... (the class lists are in
+    // decode order, so a band is a stretch of the frame) -- so that a region's reference lines
+    // are fetched once for all three classes, not once per class sweep.  The class counts are
+    // padded to multiples of 8 * bands.
     uint32_t cls = 3, jj = 0;
     if (nb == 1) {
         if (j < qI) cls = 0, jj = j;
@@ -1759,14 +1758,14 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const 
         }
     }
     if (cls == 0) {
-        const uint32_t b = inter_deal(x, jj, qI, kcc);
+        const uint32_t b = inter_deal(x, jj, qI);
         if (b < tI[n]) inter_general(kps, tI, n, b, L.g, trace, ~0u);
     } else if (cls == 1) {
-        const uint32_t b = inter_deal(x, jj, qM, kcc);
-        if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m, c2);
+        const uint32_t b = inter_deal(x, jj, qM);
+        if (b < tM[n]) inter_plain<32, 16>(kps, tM, n, b, L.m);
     } else if (cls == 2) {
-        const uint32_t b = inter_deal(x, jj, qS, kcc);
-        if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s, c2);
+        const uint32_t b = inter_deal(x, jj, qS);
+        if (b < tS[n]) inter_plain<16, 8>(kps, tS, n, b, L.s);
     }
 }
 
@@ -1993,7 +1992,6 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     __syncthreads();
     const uint32_t q = __builtin_amdgcn_readfirstlane(qsh);
     uint32_t* head = ctl + q * FLOW_LINE;
-    const bool pf = (sload(ctl + FLOW_FLAGS) & 1u) != 0;
     if (threadIdx.x == 0) ticket[0] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     for (uint32_t it = 0;; it ^= 1) {
@@ -2004,13 +2002,9 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
 #endif
             return;
         }
-        // pf (FLOW_FLAGS bit 0, the host's AV1R_TICKET_PF): take the next ticket before running
-        // this group, its round trip hidden behind the group's work.  Progress holds: the
-        // earliest unfinished group cannot be a held "next" one (its holder's current group is
-        // earlier and unfinished), so it is some workgroup's current group, whose inputs are
-        // complete.
-        uint32_t next = 0;
-        if (pf && threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (the next ticket is taken after the group: taken before it, its round trip hidden
+        // behind the group's work, k_flow measured 0.060 -> 0.070 ms/frame in round 5 -- a held
+        // ticket delays the group most likely on the critical path)
         const uint2 gd = groups[g];
         const KParams& k = KP(kps, gd.x >> 8);
         const uint32_t n = gd.x & 0xff;
@@ -2025,8 +2019,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
                 flow_item<64, TB_SMALL>(k, gd.y + w, reinterpret_cast<TbLds<TB_SMALL>*>(smem)[wave], epoch, ctl, trace,
                     gd.x >> 8);
         }
-        if (!pf && threadIdx.x == 0) next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (threadIdx.x == 0) ticket[it ^ 1] = next;
+        if (threadIdx.x == 0) ticket[it ^ 1] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();  // the LDS tiles are free again; the next ticket is published
     }
 }
@@ -2045,8 +2038,6 @@ int flow_grid(int device, int maxPer)
             per = 1;
         per = per > 8 ? 8 : per;
         per = per > maxPer ? maxPer : per;
-        // AV1R_FLOW_PER_CU: fewer resident workgroups per CU (A/B of polling pressure)
-        if (const char* e = getenv("AV1R_FLOW_PER_CU")) per = per < atoi(e) ? per : (atoi(e) > 0 ? atoi(e) : per);
         int g = ((cus * per) / FLOW_QUEUES) * FLOW_QUEUES;
         cache[device][slot] = g < FLOW_QUEUES ? FLOW_QUEUES : g;
     }
@@ -2147,12 +2138,10 @@ void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, u
 
 // kind 0: inter tiles, `items` workgroups; kind 1: `items` = big items + ceil(small / 4);
 // kind 2 / 3: medium / small plain inter blocks, `items` groups of two / four
-void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t kc,
+void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t gI, uint32_t gM, uint32_t gS, uint32_t nb,
     unsigned long long* trace, hipStream_t s)
 {
-    // AV1R_CHROMA2=0: plain blocks' chroma planes one after the other (small_pu per plane)
-    static const int c2 = getenv("AV1R_CHROMA2") ? atoi(getenv("AV1R_CHROMA2")) : 1;
-    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, kc, c2, trace);
+    hipLaunchKernelGGL(k_inter_all, dim3(gI + gM + gS), dim3(64), 0, s, kps, tab, n, gI, gM, gS, nb, trace);
 }
 void launch_k_level(int kind, const KParams* kps, const uint32_t* tab, int n, unsigned items, unsigned long long* trace,
     uint32_t traceBase, hipStream_t s)

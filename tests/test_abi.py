@@ -216,15 +216,26 @@ def test_lean_intra_constants_match_the_tables():
         assert [sel("fi_ek0", s), sel("fi_ek1", s), sel("fi_ek2", s)] == k[:3], s
 
 
-def test_pack_walks_fused_and_separate_pack_the_same_bytes():
-    """build_schedule's fused map walks (edge level + owners in one pass, level + owner
-    painting in one pass) pack byte-identical batches to the separate walks."""
+# MD5 over the packed bytes of the first 40 fixture streams and six synthetic 1080p frames
+# (tools/pack_digest.py 40).  Round 5 checked the fused map walks of build_schedule against
+# the separate ones (AV1R_PACK_FUSED, since removed) with it.  Round 6 found the sections'
+# padding unwritten (heap contents travelled; under MALLOC_PERTURB_ the digest changed from
+# run to run) and zeroes it; pruning the library's measured-slower paths left the packed
+# bytes unchanged.  A change that alters the packed layout on purpose updates it here.
+PACK_DIGEST = "cc03d6b619e0a58470ae08c7dde09eba 82"  # (digest, frames)
+
+
+def test_pack_digest_unchanged():
+    """The packed batches (av1r_pack, host only) of the fixture streams and the bench's
+    synthetic frames are byte-identical to the committed digest."""
     import subprocess
     import sys
     tool = os.path.join(native.ROOT, "tools", "pack_digest.py")
-    out = [subprocess.run([sys.executable, tool, "40"], capture_output=True, text=True, timeout=600,
-                          env=dict(os.environ, AV1R_PACK_FUSED=v)).stdout.split() for v in ("1", "0")]
-    assert out[0] and out[0] == out[1]
+    # (glibc fills fresh allocations with the perturb byte: unwritten bytes would change it)
+    for perturb in ("17", "165"):
+        out = subprocess.run([sys.executable, tool, "40"], capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, MALLOC_PERTURB_=perturb)).stdout.split()
+        assert out == PACK_DIGEST.split(), perturb
 
 
 def test_validation_palette_window_keyed_on_the_tbs_own_block(native_lib):

@@ -228,7 +228,7 @@ def test_gpu_get_output_async_and_prefetch_match_oracle():
         finally:
             d.close()
         # async into pinned host memory (hipHostMalloc: a DMA straight into the caller's
-        # planes; AV1R_OUT_MODE=2 stores them with k_out instead), waited for in order
+        # planes), waited for in order
         from av1dec_amd.native import PinnedBuffer
         d = Decoder(0, keep_stages=False)
         bufs = []

@@ -29,4 +29,5 @@ for s in golden.streams()[:int(sys.argv[1]) if len(sys.argv) > 1 else None]:
     frames += batchfile.load(golden.batch_path(s))
 frames += bench.rank_streams("1080p", 0, 1, 6)[0]
 out = [packed(f) for f in frames if not f.show_existing]
+if os.environ.get("PD_VERBOSE"): print("\n".join(out), file=sys.stderr)
 print(hashlib.md5("".join(out).encode()).hexdigest(), len(out))
