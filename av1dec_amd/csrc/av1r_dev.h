@@ -79,13 +79,52 @@ struct WorkItem {
     uint8_t pred;       // TB prediction source: AV1R_PRED_INTRA / _PALETTE / _INTER
     uint8_t pub;        // k_flow: 1 = a dependency list names this item (store sc1, drain, flag)
     uint16_t dep_cnt;   // k_flow: the items whose pixels this one reads ...
-    uint16_t pad1;
+    uint16_t hflags;    // host only (build_schedule -> pack_frame): AV1R_WI_TINY
     uint32_t dep_off;   // ... at KParams::deps[dep_off, dep_off + dep_cnt) (item positions)
 };
 static_assert(sizeof(WorkItem) == 32, "WorkItem layout");
 #define AV1R_PRED_INTRA 0
 #define AV1R_PRED_PALETTE 1
 #define AV1R_PRED_INTER 2
+#define AV1R_WI_TINY 1u
+
+// k_flow's tiny items (round 6).  An intra transform block of at most 8x8 on the lean path
+// (intra_fast.h: not palette, not filter-intra) in a frame with edge granules is described
+// whole by the host, in the 32 bytes of its WorkItem slot: every parameter fi_setup derives
+// (the prediction class, edge-filter strengths and lengths, upsampling, dx / dy, CFL's alpha
+// and luma extent), its granule masks and residual tile.  k_flow runs them four to a wave,
+// 16 lanes each (tiny_run, recon.hip): one scalar load per item gives all it needs, and the
+// four items' memory round trips overlap.  pack_frame writes these records for the items
+// build_schedule marked AV1R_WI_TINY; the tiny groups of a level (up to 16 items, group flag
+// FLOW_G_TINY) come before its other small items.
+struct TinyItem {
+    uint16_t x, y;      // plane position
+    uint8_t shape;      // plane (bits 0-1) | log2W - 2 (bit 2) | log2H - 2 (bit 3) | class (bits 4-7, FI_*)
+    uint8_t flags;      // TI_*
+    uint8_t str;        // edge-filter strengths: above | left << 4
+    uint8_t lim;        // aboveLimit - x | (leftLimit - y) << 4
+    uint8_t nA, nL;     // edge-filter lengths (numPx + 1)
+    uint8_t nUA, nUL;   // upsampled lengths (0: none)
+    uint8_t masks;      // granule masks: above run (bits 0-3) | left run << 4
+    uint8_t mC;         // corner: bit 0 written in the launch, bit 1 its owner's right column
+    uint16_t p0, p1;    // directional: dx, dy; CFL: max_luma_w, max_luma_h
+    int8_t alpha;       // CFL
+    uint8_t pad;
+    uint16_t dep_cnt;   // dependency list (CFL's co-located luma) at KParams::deps[dep_off ..)
+    uint16_t pad2;
+    uint32_t dep_off;
+    uint32_t res;       // residual tile (int16 elements into KParams::res; ~0u: none)
+};
+static_assert(sizeof(TinyItem) == 32, "TinyItem layout");
+#define TI_HA 1u
+#define TI_HL 2u
+#define TI_CFL 4u
+#define TI_CORNER 8u
+#define TI_PUB 16u
+#define FLOW_G_TINY 0x40u  // k_flow group descriptor: n | FLOW_G_TINY = n tiny items
+#define FLOW_TINY_G 16     // tiny items per group (four per wave)
+// the lean path's prediction classes (intra_fast.h fi_setup; TinyItem::shape)
+enum { FI_DC = 0, FI_V, FI_H, FI_Z1, FI_Z2, FI_Z3, FI_SMOOTH, FI_SMOOTH_V, FI_SMOOTH_H, FI_PAETH };
 
 // The device's block record: the fields of av1r_block that the kernels read, packed (52 bytes
 // against 84: a 1080p inter frame uploads ~0.45 MB less).  Left out, into KParams::bext at

@@ -80,9 +80,11 @@ struct Level {
     // Within [1] and [2] the inter TBs come last: k_flow takes the first fcnt (inter TBs
     // are finished by k_resid there)
     // List [0] ends with pl[0] medium then pl[1] small plain blocks (k_inter_m two per wave,
-    // k_inter_s four per wave; see build_schedule).
+    // k_inter_s four per wave; see build_schedule).  List [2] starts with `tiny` items
+    // (TinyItem, k_flow's tiny groups; flow-only frames with granules).
     uint32_t off[3] = {}, cnt[3] = {}, fcnt[3] = {};
     uint32_t pl[2] = {};
+    uint32_t tiny = 0;
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -732,6 +734,90 @@ static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
     return 7;
 }
 
+// getIntraEdgeFilterStrength (IntraPredict.cpp:269-343) and getIntraEdgeUpsample (:345-358),
+// for the host's TinyItem records (the device's own copies: intra_dev.h)
+static int host_edge_strength(int w, int h, bool filterType, int delta)
+{
+    const int d = std::abs(delta), blkWh = w + h;
+    int s = 0;
+    if (!filterType) {
+        if (blkWh <= 8) s = d >= 56;
+        else if (blkWh <= 16) s = d >= 40;
+        else if (blkWh <= 24) s = d >= 32 ? 3 : d >= 16 ? 2 : d >= 8 ? 1 : 0;
+        else if (blkWh <= 32) s = d >= 32 ? 3 : d >= 4 ? 2 : 1;
+        else s = 3;
+    } else {
+        if (blkWh <= 8) s = d >= 64 ? 2 : d >= 40 ? 1 : 0;
+        else if (blkWh <= 16) s = d >= 48 ? 2 : d >= 20 ? 1 : 0;
+        else if (blkWh <= 24) s = d >= 4 ? 3 : 0;
+        else s = 3;
+    }
+    return s;
+}
+static int host_edge_upsample(int w, int h, bool filterType, int delta)
+{
+    const int d = std::abs(delta), blkWh = w + h;
+    if (d <= 0 || d >= 40) return 0;
+    return filterType ? blkWh <= 8 : blkWh <= 16;
+}
+// The TinyItem of an intra TB of at most 8x8 (av1r_dev.h): fi_setup's parameters
+// (intra_fast.h, restating IntraPredict::predict_intra, IntraPredict.cpp:563-630, with the
+// directional edge preparation :389-437) from the batch, plus the item's granule masks m[0..3]
+// (m[3]: its residual tile) and dependency list.
+static TinyItem tiny_record(const av1r_frame_hdr* h, const av1r_block& blk, const WorkItem& w, const uint32_t* m)
+{
+    TinyItem r;
+    memset(&r, 0, sizeof(r));
+    const int plane = w.plane, sub = plane ? 1 : 0, x = w.x, y = w.y;
+    const int log2W = av1r_tx_w_log2[w.tx_size], log2H = av1r_tx_h_log2[w.tx_size];
+    const int tw = 1 << log2W, th = 1 << log2H;
+    const int maxXd = (h->mi_cols * 4) >> sub, maxYd = (h->mi_rows * 4) >> sub;
+    const bool hA = w.flags & AV1R_TB_HAVE_ABOVE, hL = w.flags & AV1R_TB_HAVE_LEFT;
+    const int aboveLimit = std::min(maxXd - 1, x + ((w.flags & AV1R_TB_HAVE_AR) ? 2 * tw : tw) - 1);
+    const int leftLimit = std::min(maxYd - 1, y + ((w.flags & AV1R_TB_HAVE_BL) ? 2 * th : th) - 1);
+    const bool cfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
+    const int mode = plane == 0 ? blk.y_mode : (cfl ? AV1R_DC_PRED : blk.uv_mode);
+    const bool smooth = plane ? (blk.flags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0
+                              : (blk.flags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0;
+    int cls, strA = 0, strL = 0, nA = 0, nL = 0, nUA = 0, nUL = 0, corner = 0, dx = 0, dy = 0;
+    if (mode >= AV1R_V_PRED && mode <= AV1R_D67_PRED) {
+        const int pAngle = av1r_mode_to_angle[mode] + (plane == 0 ? blk.angle_delta_y : blk.angle_delta_uv) * 3;
+        cls = pAngle < 90 ? FI_Z1 : pAngle == 90 ? FI_V : pAngle < 180 ? FI_Z2 : pAngle == 180 ? FI_H : FI_Z3;
+        if (h->enable_intra_edge_filter && pAngle != 90 && pAngle != 180) {
+            corner = pAngle > 90 && pAngle < 180 && (tw + th) >= 24;
+            strA = hA ? host_edge_strength(tw, th, smooth, pAngle - 90) : 0;
+            strL = hL ? host_edge_strength(tw, th, smooth, pAngle - 180) : 0;
+            nA = std::min(tw, maxXd - x + 1) + (pAngle < 90 ? th : 0) + 1;
+            nL = std::min(th, maxYd - y + 1) + (pAngle > 180 ? tw : 0) + 1;
+            nUA = host_edge_upsample(tw, th, smooth, pAngle - 90) ? tw + (pAngle < 90 ? th : 0) : 0;
+            nUL = host_edge_upsample(tw, th, smooth, pAngle - 180) ? th + (pAngle > 180 ? tw : 0) : 0;
+        }
+        if (pAngle < 90) dx = av1r_dr_intra_derivative[pAngle];
+        else if (pAngle > 90 && pAngle < 180) dx = av1r_dr_intra_derivative[180 - pAngle];
+        if (pAngle > 90 && pAngle < 180) dy = av1r_dr_intra_derivative[pAngle - 90];
+        else if (pAngle > 180) dy = av1r_dr_intra_derivative[270 - pAngle];
+    } else {
+        cls = mode == AV1R_DC_PRED ? FI_DC : mode == AV1R_SMOOTH_PRED ? FI_SMOOTH : mode == AV1R_SMOOTH_V_PRED ? FI_SMOOTH_V
+            : mode == AV1R_SMOOTH_H_PRED ? FI_SMOOTH_H : FI_PAETH;
+    }
+    r.x = (uint16_t)x;
+    r.y = (uint16_t)y;
+    r.shape = (uint8_t)(plane | (log2W - 2) << 2 | (log2H - 2) << 3 | cls << 4);
+    r.flags = (uint8_t)((hA ? TI_HA : 0) | (hL ? TI_HL : 0) | (cfl ? TI_CFL : 0) | (corner ? TI_CORNER : 0) | ((w.pub & 1) ? TI_PUB : 0));
+    r.str = (uint8_t)(strA | strL << 4);
+    r.lim = (uint8_t)((aboveLimit - x) | (leftLimit - y) << 4);
+    r.nA = (uint8_t)nA, r.nL = (uint8_t)nL, r.nUA = (uint8_t)nUA, r.nUL = (uint8_t)nUL;
+    r.masks = (uint8_t)((m[0] & 15) | (m[2] & 15) << 4);
+    r.mC = (uint8_t)(m[1] & 3);
+    r.p0 = (uint16_t)(cfl ? blk.max_luma_w : dx);
+    r.p1 = (uint16_t)(cfl ? blk.max_luma_h : dy);
+    r.alpha = cfl ? (plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v) : 0;
+    r.dep_cnt = w.dep_cnt;
+    r.dep_off = w.dep_off;
+    r.res = m[3];
+    return r;
+}
+
 // k_flow's small-item groups: four items (one per wave) on a thin level, 8 (two per wave,
 // run one after the other) on a level of at least 256 small items of the frame, where the
 // workgroup's ticket, group load and closing barrier are paid once per two items per wave (a
@@ -739,7 +825,14 @@ static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
 // every level, measured slower, profiles/r05_ab_flow_groups.txt)
 static uint32_t flow_small_group(const Level& lv)
 {
-    return lv.fcnt[2] >= 256u ? 8u : 4u;
+    return lv.fcnt[2] - lv.tiny >= 256u ? 8u : 4u;
+}
+// k_flow groups of a level: its large items one each, its tiny items FLOW_TINY_G a group (four
+// per wave, 16 lanes each), its other small items flow_small_group() a group
+static size_t flow_groups(const Level& lv)
+{
+    const uint32_t G = flow_small_group(lv), rest = lv.fcnt[2] - lv.tiny;
+    return lv.fcnt[1] + (lv.tiny + FLOW_TINY_G - 1) / FLOW_TINY_G + (rest + G - 1) / G;
 }
 
 // AV1R_SCHED_CHECK=1 (debug aid): the invariants k_flow relies on, checked on the host for a
@@ -762,9 +855,15 @@ static void schedule_check(av1r_ctx* c, const av1r_frame_batch* b)
             report("items range", l, lv.off[1], lv.cnt[1]);
         if (lv.fcnt[1] > lv.cnt[1] || lv.fcnt[2] > lv.cnt[2]) report("flow counts", l, lv.fcnt[1], lv.fcnt[2]);
         for (uint32_t q = 0; q < lv.fcnt[1]; q++) grp[lv.off[1] + q] = g++;
+        if (lv.tiny > lv.fcnt[2]) report("tiny count", l, lv.tiny, lv.fcnt[2]);
+        for (uint32_t q = 0; q < lv.tiny; q++) {
+            grp[lv.off[2] + q] = g + q / FLOW_TINY_G;
+            if (!(c->items[lv.off[2] + q].hflags & AV1R_WI_TINY)) report("tiny item", lv.off[2] + q, l, q);
+        }
+        g += (lv.tiny + FLOW_TINY_G - 1) / FLOW_TINY_G;
         const uint32_t G = flow_small_group(lv);
-        for (uint32_t q = 0; q < lv.fcnt[2]; q++) grp[lv.off[2] + q] = g + q / G;
-        g += (lv.fcnt[2] + G - 1) / G;
+        for (uint32_t q = lv.tiny; q < lv.fcnt[2]; q++) grp[lv.off[2] + q] = g + (q - lv.tiny) / G;
+        g += (lv.fcnt[2] - lv.tiny + G - 1) / G;
     }
     for (uint32_t t : c->tiles)
         if (AV1R_ITEM_KIND(t) != AV1R_ITEM_INTER || (AV1R_ITEM_INDEX(t) >> 4) >= b->n_blocks) report("tile code", 0, t, b->n_blocks);
@@ -906,6 +1005,14 @@ static void schedule_check(av1r_ctx* c, const av1r_frame_batch* b)
         }
         fprintf(stderr, "av1r sched chains: critical path (time model) items %.0f us, block-plane chains %.0f us\n", tItems, tChains);
     }
+}
+
+// the context's frames run on k_flow (av1r_set_schedule; default: k_flow, AV1R_FLOW=0 the
+// level launches)
+static bool flow_schedule(const av1r_ctx* c)
+{
+    static const bool flowEnv = !getenv("AV1R_FLOW") || atoi(getenv("AV1R_FLOW")) != 0;
+    return c->schedule >= 0 ? c->schedule == 1 : flowEnv;
 }
 
 static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGran = true, bool flowOnly = false)
@@ -1258,7 +1365,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     c->items.reserve(nItems);
     c->tiles.reserve(nTiles);
     // stable partition of a level's list by a small class key (counting sort, one pass)
-    std::vector<uint32_t> bk[4];
+    std::vector<uint32_t> bk[5];
     auto partition = [&](std::vector<uint32_t>& v, int nk, uint32_t* counts, auto key) {
         for (int q = 0; q < nk; q++) bk[q].clear();
         for (uint32_t x : v) bk[key(x)].push_back(x);
@@ -1288,21 +1395,45 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                     return 0;
         return av1r_num4x4w[bs] <= 2 && av1r_num4x4h[bs] <= 2 ? 2 : 1;
     };
-    // TB lists: [large intra][large inter][small intra][small inter]; large = a side > 16
+    // TB lists: [large intra][large inter][tiny][small intra][small inter]; large = a side >
+    // 16; tiny (flow-only frames with granules, on a level of at least 256 small intra TBs):
+    // an intra TB of at most 8x8 on k_flow's lean path -- not palette, not filter-intra
+    // (intra_fast.h fi_ok) -- described by a TinyItem.  A tiny group's four items per wave run
+    // in lock step, each row waiting for the others' edges: on the thin levels of a dependency
+    // chain (a key frame: ~70 items per level) that lengthens every hop (measured: a 1080p key
+    // frame 1.70 -> 3.09 ms with every level's tiny items in tiny groups), so they stay one per
+    // wave there.
+    bool tinyOk = false;
+    auto smallIntra = [&](uint32_t code) {
+        const av1r_tb& t = b->tbs[AV1R_ITEM_INDEX(code)];
+        return av1r_tx_w[t.tx_size] <= 16 && av1r_tx_h[t.tx_size] <= 16 && !(b->blocks[t.block].flags & AV1R_BLK_INTER);
+    };
     auto tbClass = [&](uint32_t code) {
         const av1r_tb& t = b->tbs[AV1R_ITEM_INDEX(code)];
-        const bool large = av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16;
-        return (large ? 0 : 2) + ((b->blocks[t.block].flags & AV1R_BLK_INTER) ? 1 : 0);
+        const av1r_block& blk = b->blocks[t.block];
+        const bool inter = blk.flags & AV1R_BLK_INTER;
+        if (av1r_tx_w[t.tx_size] > 16 || av1r_tx_h[t.tx_size] > 16) return inter ? 1 : 0;
+        if (inter) return 4;
+        const bool tiny = tinyOk && av1r_tx_w[t.tx_size] <= 8 && av1r_tx_h[t.tx_size] <= 8 &&
+                          !(t.plane ? blk.palette_size_uv : blk.palette_size_y) && !(t.plane == 0 && (blk.flags & AV1R_BLK_FILTER_INTRA));
+        return tiny ? 2 : 3;
     };
     for (size_t l = 0; l < nl; l++) {
         // order: inter tiles, then k_tb's large items, then its small ones
-        uint32_t pc[4] = {}, tc[4] = {};
+        uint32_t pc[4] = {}, tc[5] = {};
         partition(c->lvP[l], 3, pc, plainClass);
         c->levels[l].pl[0] = pc[1];
         c->levels[l].pl[1] = pc[2];
         std::vector<uint32_t>& T = c->lvT[l];
-        partition(T, 4, tc, tbClass);
-        const uint32_t nLargeT = tc[0] + tc[1], nLargeIntra = tc[0], nSmallIntra = tc[2];
+        tinyOk = false;
+        if (flowOnly && c->granOk && T.size() >= 256) {
+            size_t nsi = 0;
+            for (uint32_t code : T) nsi += smallIntra(code);
+            tinyOk = nsi >= 256;
+        }
+        partition(T, 5, tc, tbClass);
+        const uint32_t nLargeT = tc[0] + tc[1], nLargeIntra = tc[0], nSmallIntra = tc[2] + tc[3];
+        c->levels[l].tiny = tc[2];
         c->levels[l].off[0] = (uint32_t)c->tiles.size();
         c->levels[l].cnt[0] = (uint32_t)c->lvP[l].size();
         c->tiles.insert(c->tiles.end(), c->lvP[l].begin(), c->lvP[l].end());
@@ -1341,6 +1472,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
                 c->items.push_back(w);
             }
         }
+        for (uint32_t q = 0; q < tc[2]; q++) c->items[c->levels[l].off[2] + q].hflags = AV1R_WI_TINY;
     }
     c->nLevelsLast = (int)nl;
     clk.lap(PP_SCHED_ITEMS);
@@ -1491,6 +1623,9 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
             else rest[0] += c->levels[l].fcnt[1], rest[1] += c->levels[l].fcnt[2];
         }
         fprintf(stderr, "  levels 4+: %u large %u small\n", rest[0], rest[1]);
+        uint32_t tiny = 0, small = 0;
+        for (const Level& lv : c->levels) tiny += lv.tiny, small += lv.fcnt[2];
+        fprintf(stderr, "  tiny items %u of %u small k_flow items\n", tiny, small);
     }
     if (!host) return AV1R_OK;
     size_t off = 0;
@@ -1587,6 +1722,15 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
             wi[i].coef_off = c->tbCoefOff[ti];
             wi[i].flags |= AV1R_TBD_WIDE;
         }
+        // the tiny items' slots hold their TinyItem (k_flow's tiny groups read nothing else)
+        for (const Level& lv : c->levels)
+            for (uint32_t q = 0; q < lv.tiny; q++) {
+                const size_t i = lv.off[2] + q;
+                const WorkItem& w = c->items[i];
+                if (!(w.hflags & AV1R_WI_TINY) || w.dep_off < 4) return fail(c, AV1R_E_INVALID, "tiny item %zu", i);
+                const TinyItem r = tiny_record(h, b->blocks[w.block], w, c->deps.data() + w.dep_off - 4);
+                memcpy(wi + i, &r, sizeof(r));
+            }
     }
     k.tiles = (const uint32_t*)put(c->tiles.data(), 4 * c->tiles.size(), szTiles);
     k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);
@@ -1841,8 +1985,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     const size_t kBytes = align256(sizeof(KParams) * n);
     const size_t tabBytes = align256(4 * tabW * std::max<size_t>(nLevels, 1));
     // k_flow (AV1R_FLOW=0: level launches): every frame's items are flow-schedulable
-    static const bool flowEnv = !getenv("AV1R_FLOW") || atoi(getenv("AV1R_FLOW")) != 0;
-    bool flow = lc->schedule >= 0 ? lc->schedule == 1 : flowEnv;
+    bool flow = flow_schedule(lc);
     bool allFlow = true, mustFlow = false;  // flow-only schedules (av1r_pack) run on k_flow
     for (auto& j : jobs) {
         allFlow &= j.P->flowOk;
@@ -1853,7 +1996,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // k_flow groups: one large item, or up to four small ones
     size_t nGroups = 0;
     for (auto& j : jobs)
-        for (const Level& lv : j.P->levels) nGroups += lv.fcnt[1] + (lv.fcnt[2] + flow_small_group(lv) - 1) / flow_small_group(lv);
+        for (const Level& lv : j.P->levels) nGroups += flow_groups(lv);
     const size_t resTabBytes = align256(4 * 2 * ((size_t)n + 1));
     const size_t nEntries = nGroups;
     const size_t need = kBytes + tabBytes + (flow ? FLOW_CTL_BYTES + 8 * nEntries + resTabBytes : 0);
@@ -1939,8 +2082,8 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     uint32_t* ctl = reinterpret_cast<uint32_t*>(M.dev + kBytes + tabBytes);
     if (flow) {
         // control block (zeroed) + the groups in topological order: level by level, the
-        // frames interleaved; {frame << 8 | n, first item}: n = 0 one large item, else
-        // 1..flow_small_group() small items
+        // frames interleaved; {frame << 8 | n, first item}: n = 0 one large item, n | FLOW_G_TINY
+        // 1..FLOW_TINY_G tiny items, else 1..flow_small_group() small items
         memset(M.host + kBytes + tabBytes, 0, FLOW_CTL_BYTES);
         uint32_t* hctl = reinterpret_cast<uint32_t*>(M.host + kBytes + tabBytes);
         *reinterpret_cast<uint32_t**>(hctl + FLOW_HOSTERR) = rec ? rec->err : nullptr;
@@ -1955,8 +2098,12 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
                     g[0] = (uint32_t)i << 8;
                     g[1] = lv.off[1] + q;
                 }
+                for (uint32_t q = 0; q < lv.tiny; q += FLOW_TINY_G, g += 2) {
+                    g[0] = ((uint32_t)i << 8) | FLOW_G_TINY | std::min<uint32_t>(FLOW_TINY_G, lv.tiny - q);
+                    g[1] = lv.off[2] + q;
+                }
                 const uint32_t G = flow_small_group(lv);
-                for (uint32_t q = 0; q < lv.fcnt[2]; q += G, g += 2) {
+                for (uint32_t q = lv.tiny; q < lv.fcnt[2]; q += G, g += 2) {
                     g[0] = ((uint32_t)i << 8) | std::min<uint32_t>(G, lv.fcnt[2] - q);
                     g[1] = lv.off[2] + q;
                 }
@@ -2189,7 +2336,8 @@ static int run_frame(av1r_ctx* c, const av1r_frame_batch* b)
     int rc = validate(c, b);
     c->skipSlotCheck = false;
     if (rc) return rc;
-    build_schedule(c, b);
+    // a frame for k_flow is scheduled for it alone (no level lists; tiny items): as av1r_pack
+    build_schedule(c, b, true, flow_schedule(c));
     Prepared& P = c->streamP;
     size_t need = 0;
     pack_frame(c, b, P, nullptr, nullptr, &need);
@@ -2441,7 +2589,7 @@ int av1r_prepare(av1r_ctx* c, const av1r_frame_batch* b, int* handle)
             delete P;
             return rc;
         }
-        build_schedule(c, b);
+        build_schedule(c, b, true, flow_schedule(c));
         size_t need = 0;
         pack_frame(c, b, *P, nullptr, nullptr, &need);
         std::vector<uint8_t> host(need);

@@ -20,7 +20,7 @@
 #pragma once
 #include "intra_dev.h"
 
-enum { FI_DC = 0, FI_V, FI_H, FI_Z1, FI_Z2, FI_Z3, FI_SMOOTH, FI_SMOOTH_V, FI_SMOOTH_H, FI_PAETH };
+// (the prediction classes FI_* are in av1r_dev.h: the host writes them into TinyItem)
 
 struct FiParams {
     int cls;

@@ -1947,8 +1947,406 @@ DEV void flow_item(const KParams& k, uint32_t pos, TbLds<MAX>& L, uint32_t epoch
     trace_flush(tr);
 }
 
+// ---------------------------------------------------------------------------------
+// Tiny items (round 6): intra TBs of at most 8x8 on the lean path, four per wave, one per
+// 16-lane row (TinyItem, av1r_dev.h).  fi_run (intra_fast.h) runs one item per wave with its
+// parameters uniform; an item's time there was load latency -- its record loads, the edge
+// gather's round trip, the group's barrier and ticket -- around ~1.7 us of prediction and
+// store (profiles/r05_trace_flow_levelorder.txt: 8.8 us of the 10.5 per item), with a 4x4
+// TB using 4 of the wave's 64 lanes.  Here the four rows' records arrive in one scalar round
+// trip, their residual quads, dependency polls and edge units in one vector round trip
+// (+ the polls), and the predictions run side by side: the same arithmetic as fi_run per
+// row, with the row's parameters in VGPRs (the rows' classes may differ: divergent).
+// Items of one group are of one level, so none waits for another.
+// ---------------------------------------------------------------------------------
+#define TE_OFF 16
+#define TE_LEN (TE_OFF + 48)
+struct TinyLds {
+    uint8_t above[TE_LEN], left[TE_LEN], upA[TE_LEN], upL[TE_LEN];
+    uint32_t ua[4];  // the above run's units (pixel (x + i, y - 1) at byte i)
+    uint32_t ul[8];  // the left run's units (pixel (x - 1, y + i) at byte i); [7]: the corner's
+};
+DEV uint32_t row_sel(int row, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    return row == 0 ? a : row == 1 ? b : row == 2 ? c : d;
+}
+// the total of v over each 16-lane row, in every lane of the row (fi_row_sum leaves it in
+// lane 15; ds_swizzle in bit mode reads lane (l & 0x10) | 0xf of each 32-lane half)
+DEV int row16_total(int v)
+{
+    return __builtin_amdgcn_ds_swizzle(fi_row_sum(v), 0x1F0);
+}
+DEV uint32_t bits(uint32_t v, int lo, int n) { return (v >> lo) & ((1u << n) - 1); }
+// every lane's dependency d (~0u: none) done, as flow_wait (bounded, error word 1)
+DEV void flow_wait_lanes(uint32_t d, const uint32_t* done, uint32_t epoch, uint32_t* ctl)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t spins = 0, lim = 0;
+    for (;;) {
+        const bool ok = d == ~0u || __hip_atomic_load(done + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        if (__all(ok)) break;
+        const bool dead = (spins & AV1R_ERR_POLL_MASK) == 0 && __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        if (!lim) lim = flow_spin_limit(ctl);
+        if (dead || ++spins > lim || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
+            if ((threadIdx.x & 63) == 0 && !dead) {
+                __hip_atomic_store(ctl + FLOW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(ctl + FLOW_HOSTERR)), 1u,
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// pos0: the group's first item; nIt: its items (<= 16); T: this wave's four rows
+DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uint32_t epoch, uint32_t* ctl)
+{
+    const int lane = threadIdx.x & 63, row = lane >> 4;
+    int t = lane & 15;
+    asm volatile("" : "+v"(t));  // (as coop_lane: no lane-derived address hoisted)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // ---- the rows' records: four scalar loads, merged per lane
+    uint32_t d[8];
+    {
+        uint32_t s[4][8];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t i = imin(wave + 4 * r, nIt - 1);  // (a row past the group re-reads the last)
+            const uint4 a = sload(reinterpret_cast<const uint4*>(k.items + pos0 + i));
+            const uint4 b = sload(reinterpret_cast<const uint4*>(k.items + pos0 + i) + 1);
+            s[r][0] = a.x, s[r][1] = a.y, s[r][2] = a.z, s[r][3] = a.w;
+            s[r][4] = b.x, s[r][5] = b.y, s[r][6] = b.z, s[r][7] = b.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) d[j] = row_sel(row, s[0][j], s[1][j], s[2][j], s[3][j]);
+    }
+    const bool act = wave + 4 * row < nIt;
+    const uint32_t pos = pos0 + wave + 4 * row;
+    const int x = (int)(d[0] & 0xffff), y = (int)(d[0] >> 16);
+    const int plane = (int)bits(d[1], 0, 2);
+    const int log2W = 2 + (int)bits(d[1], 2, 1), log2H = 2 + (int)bits(d[1], 3, 1);
+    const int cls = (int)bits(d[1], 4, 4);
+    const uint32_t fl = bits(d[1], 8, 8);
+    const bool hA = fl & TI_HA, hL = fl & TI_HL, cfl = fl & TI_CFL;
+    const int w = 1 << log2W, h = 1 << log2H, w4 = w >> 2;
+    const int nq = (w * h) >> 2;  // quads
+    const int qi = t >> (log2W - 2), qj = (t & (w4 - 1)) << 2;
+    // the row's plane: frame and granule arrays (uniform per plane, selected per lane)
+    const DevPlane P0 = k.cur.pl[0], P1 = k.cur.pl[1], P2 = k.cur.pl[2];
+    DevPlane dst;
+    dst.p = plane == 0 ? P0.p : plane == 1 ? P1.p : P2.p;
+    dst.stride = plane == 0 ? P0.stride : plane == 1 ? P1.stride : P2.stride;
+    dst.w = dst.h = 0;
+    const uint64_t* gh = plane == 0 ? k.gran_h[0] : plane == 1 ? k.gran_h[1] : k.gran_h[2];
+    const uint64_t* gv = plane == 0 ? k.gran_v[0] : plane == 1 ? k.gran_v[1] : k.gran_v[2];
+    const int gw = plane == 0 ? k.gran_w[0] : plane == 1 ? k.gran_w[1] : k.gran_w[2];
+    const int ghn = plane == 0 ? k.gran_hn[0] : plane == 1 ? k.gran_hn[1] : k.gran_hn[2];
+    // ---- one round trip: the residual quad, the first 16 dependencies, the edge units (the
+    // frame's pixels for units final before the launch, first granule polls for the others)
+    const uint32_t resOff = d[7];
+    uint2 res = make_uint2(0, 0);
+    if (act && resOff != ~0u && t < nq) res = reinterpret_cast<const uint2*>(k.res + resOff)[t];
+    const uint32_t depCnt = d[5] & 0xffff, depOff = d[6];
+    // (more than 16 dependencies: the rest polled first, 16 a round; rare)
+    for (uint32_t b = 16;; b += 16) {
+        const bool more = act && b < depCnt;
+        if (!__any(more)) break;
+        const uint32_t dd = more && b + t < depCnt ? k.deps[depOff + b + t] : ~0u;
+        flow_wait_lanes(dd, k.done, epoch, ctl);
+    }
+    const uint32_t dep = act && (uint32_t)t < depCnt ? k.deps[depOff + t] : ~0u;
+    const int aLim = (int)bits(d[1], 24, 4), lLim = (int)bits(d[1], 28, 4);
+    const int na = hA ? (aLim >> 2) + 1 : 0, nl = hL ? (lLim >> 2) + 1 : 0;
+    const int nu = na + nl + (hA && hL ? 1 : 0);
+    const bool uact = act && t < nu;
+    const int kind = t < na ? 0 : t < na + nl ? 1 : 2;  // above, left, corner
+    const int u = kind == 0 ? t : t - na;
+    const uint32_t masks = bits(d[3], 0, 8), mC = bits(d[3], 8, 2);
+    const bool inl = uact && (kind == 0 ? ((masks >> u) & 1) : kind == 1 ? ((masks >> (4 + u)) & 1) : (mC & 1));
+    const uint64_t* g = kind == 0 ? gh + (size_t)((y - 1) >> 2) * gw + (x >> 2) + u
+                      : kind == 1 ? gv + (size_t)((x - 1) >> 2) * ghn + (y >> 2) + u
+                      : (mC & 2) ? gv + (size_t)((x - 1) >> 2) * ghn + ((y - 1) >> 2)
+                                 : gh + (size_t)((y - 1) >> 2) * gw + ((x - 1) >> 2);
+    uint32_t val = 0;
+    // (flow read site: units written in the launch arrive as granules (inl); the frame is read
+    // only for pixels final before the launch)
+    if (uact && !inl) {
+        if (kind == 0) {
+            val = ldp4<true>(dst, x + 4 * u, y - 1);
+        } else if (kind == 1) {
+            const int py = y + 4 * u;
+            val = ldp<true>(dst, x - 1, py) | (ldp<true>(dst, x - 1, py + 1) << 8) | (ldp<true>(dst, x - 1, py + 2) << 16) |
+                  ((uint32_t)ldp<true>(dst, x - 1, py + 3) << 24);
+        } else {
+            val = (uint32_t)ldp<true>(dst, x - 1, y - 1) << 24;
+        }
+    }
+    {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t spins = 0, lim = 0;
+        bool dead = false, depOk = dep == ~0u, unitOk = !inl;
+        for (;;) {
+            if (!depOk && !dead) depOk = __hip_atomic_load(k.done + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            if (!unitOk && !dead) {
+                const uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                unitOk = (uint32_t)(v >> 32) == epoch;
+                val = (uint32_t)v;
+            }
+            if (__all(depOk && unitOk) || dead) break;
+            const bool other =
+                (spins & AV1R_ERR_POLL_MASK) == 0 && __hip_atomic_load(ctl + FLOW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (!lim) lim = flow_spin_limit(ctl);
+            if (other || ++spins > lim || __builtin_amdgcn_s_memrealtime() - t0 > FLOW_WALL) {
+                if (lane == 0 && !other) {  // 2: an edge granule wait (as gran_gather)
+                    __hip_atomic_store(ctl + FLOW_ERR, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(*reinterpret_cast<uint32_t* const*>(ctl + FLOW_HOSTERR)), 2u,
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                dead = true;
+            }
+            if (AV1R_POLL_BACKOFF && spins > AV1R_POLL_BACKOFF) __builtin_amdgcn_s_sleep(4);
+            else __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    asm volatile("" ::: "memory");  // no pixel load moves above the poll
+    TinyLds& L = T[row];
+    if (uact) (kind == 0 ? L.ua + u : kind == 1 ? L.ul + u : L.ul + 7)[0] = val;
+    // CFL: the co-located luma of this lane's quad (flow read site: the block's luma, written by
+    // the items the dependency list names -- sc1 loads after the wait)
+    int cv[4] = {0, 0, 0, 0};
+    int csum = 0;
+    if (act && cfl && t < nq) {
+        const DevPlane luma = P0;
+        const int maxLW = (int)(d[3] >> 16), maxLH = (int)(d[4] & 0xffff);
+        const int ly = imin((y + qi) << 1, maxLH - 2);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int lx = imin((x + qj + b) << 1, maxLW - 2);
+            const int v = ldp<true>(luma, lx, ly) + ldp<true>(luma, lx + 1, ly) + ldp<true>(luma, lx, ly + 1) + ldp<true>(luma, lx + 1, ly + 1);
+            cv[b] = v << 1;
+            csum += cv[b];
+        }
+    }
+    coop_sync<64>();  // (wave level: the units are in LDS)
+    // ---- AboveRow / LeftCol (fi_run's passes, per row)
+    const uint8_t* ta = reinterpret_cast<const uint8_t*>(L.ua);
+    const uint8_t* tl = reinterpret_cast<const uint8_t*>(L.ul);
+    const uint8_t* bA = hA ? ta : tl;  // (!hA: the left neighbour (x - 1, y) stands in)
+    const uint8_t* bL = hL ? tl : ta;
+    const int cA = hA ? aLim : 0, cL = hL ? lLim : 0;
+    const bool none = !hA && !hL;
+    auto rawA = [&](int i) -> int { const int v = bA[imin(cA, i)]; return none ? 127 : v; };
+    auto rawL = [&](int i) -> int { const int v = bL[imin(cL, i)]; return none ? 129 : v; };
+    const int c0 = hA && hL ? tl[31] : hA ? ta[0] : tl[0];
+    const int corner0 = none ? 128 : c0;
+    const int cs = (fl & TI_CORNER) ? r2(rawL(0) * 5 + corner0 * 6 + rawA(0) * 5, 4) : corner0;
+    const int strA = (int)bits(d[1], 16, 4), strL = (int)bits(d[1], 20, 4);
+    const int nA = (int)bits(d[2], 0, 8), nL = (int)bits(d[2], 8, 8), nUA = (int)bits(d[2], 16, 8), nUL = (int)bits(d[2], 24, 8);
+    uint8_t* EA = L.above + TE_OFF;
+    uint8_t* EL = L.left + TE_OFF;
+    const bool dirc = act && (cls == FI_Z1 || cls == FI_Z2 || cls == FI_Z3);
+    const uint8_t* A = EA;
+    const uint8_t* Lc = EL;
+    const bool filt = (strA | strL) != 0;
+    if (__any(dirc)) {
+        uint8_t* eA = filt ? L.upA : EA - 1;
+        uint8_t* eL = filt ? L.upL : EL - 1;
+        if (dirc)
+            for (int i = t; i <= w + h; i += 16) {
+                eA[i] = (uint8_t)(i == 0 ? cs : rawA(i - 1));
+                eL[i] = (uint8_t)(i == 0 ? cs : rawL(i - 1));
+            }
+        if (__any(dirc && filt)) {
+            coop_sync<64>();
+            if (dirc && filt)
+                for (int i = t; i <= w + h; i += 16) {
+                    int a = eA[i], l = eL[i];
+                    if (strA && i >= 1 && i < nA) {
+                        const int n1 = nA - 1, k0 = fi_ek0(strA), k1 = fi_ek1(strA), k2 = fi_ek2(strA);
+                        a = (k0 * (eA[imax(i - 2, 0)] + eA[imin(i + 2, n1)]) + k1 * (eA[i - 1] + eA[imin(i + 1, n1)]) + k2 * a + 8) >> 4;
+                    }
+                    if (strL && i >= 1 && i < nL) {
+                        const int n1 = nL - 1, k0 = fi_ek0(strL), k1 = fi_ek1(strL), k2 = fi_ek2(strL);
+                        l = (k0 * (eL[imax(i - 2, 0)] + eL[imin(i + 2, n1)]) + k1 * (eL[i - 1] + eL[imin(i + 1, n1)]) + k2 * l + 8) >> 4;
+                    }
+                    EA[i - 1] = (uint8_t)a;
+                    EL[i - 1] = (uint8_t)l;
+                }
+        }
+        coop_sync<64>();
+        // upsampling: buf[2i - 1], buf[2i] from the edge (index -2 .. 2n - 2)
+        if (__any(dirc && (nUA | nUL))) {
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                const int n = side ? nUL : nUA;
+                if (dirc && n) {
+                    const uint8_t* e = side ? EL : EA;
+                    uint8_t* buf = (side ? L.upL : L.upA) + TE_OFF;
+                    if (t < n) {
+                        const int d0 = t == 0 ? e[-1] : e[t - 2];
+                        const int d1 = e[t - 1], d2 = e[t];
+                        const int d3 = t + 1 <= n - 1 ? e[t + 1] : e[n - 1];
+                        buf[2 * t - 1] = (uint8_t)clip1(r2(-d0 + 9 * d1 + 9 * d2 - d3, 4));
+                        buf[2 * t] = (uint8_t)d2;
+                    }
+                    if (t == 0) buf[-2] = e[-1];
+                }
+            }
+            coop_sync<64>();
+            if (nUA) A = L.upA + TE_OFF;
+            if (nUL) Lc = L.upL + TE_OFF;
+        }
+    }
+    // DC (and CFL's DC): the edge sums over the row
+    int dc = 128;
+    {
+        const int v = act && cls == FI_DC ? (hA && t < w ? rawA(t) : 0) + (hL && t < h ? rawL(t) : 0) : 0;
+        const int s = row16_total(v);
+        if (hA && hL) {
+            // (s + (w + h) / 2) / (w + h): a shift when square, else w + h = 12 (4x8, 8x4):
+            // the quotient from a float reciprocal corrected by one either way (as fi_run)
+            const int n = s + ((w + h) >> 1);
+            if (log2W == log2H) {
+                dc = n >> (log2W + 1);
+            } else {
+                const int dd = w + h;
+                int q = (int)((float)n * __builtin_amdgcn_rcpf((float)dd));
+                q += (q + 1) * dd <= n;
+                q -= q * dd > n;
+                dc = q;
+            }
+        } else if (hL) {
+            dc = clip1((s + (h >> 1)) >> log2H);
+        } else if (hA) {
+            dc = clip1((s + (w >> 1)) >> log2W);
+        }
+    }
+    // ---- this lane's quad
+    uint32_t p = 0;
+    if (act && t < nq) {
+        const int i = qi;
+        const int upA = nUA ? 1 : 0, upL = nUL ? 1 : 0;
+        const int dx = (int)(d[3] >> 16), dy = (int)(d[4] & 0xffff);
+        switch (cls) {
+        case FI_DC: p = (uint32_t)dc * 0x01010101u; break;
+        case FI_V: p = rawA(qj) | rawA(qj + 1) << 8 | rawA(qj + 2) << 16 | (uint32_t)rawA(qj + 3) << 24; break;
+        case FI_H: p = (uint32_t)rawL(i) * 0x01010101u; break;
+        case FI_Z1: {
+            const int idx = (i + 1) * dx;
+            const int shift = ((idx << upA) >> 1) & 0x1F;
+            const int maxBaseX = (w + h - 1) << upA;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int base = (idx >> (6 - upA)) + ((qj + b) << upA);
+                const int v = base < maxBaseX ? r2(A[base] * (32 - shift) + A[base + 1] * shift, 5) : A[maxBaseX];
+                p |= (uint32_t)v << (8 * b);
+            }
+            break;
+        }
+        case FI_Z2: {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int j = qj + b;
+                int idx = (j << 6) - (i + 1) * dx;
+                int base = idx >> (6 - upA);
+                int v;
+                if (base >= -(1 << upA)) {
+                    const int shift = ((idx << upA) >> 1) & 0x1F;
+                    v = r2(A[base] * (32 - shift) + A[base + 1] * shift, 5);
+                } else {
+                    idx = (i << 6) - (j + 1) * dy;
+                    base = idx >> (6 - upL);
+                    const int shift = ((idx << upL) >> 1) & 0x1F;
+                    v = r2(Lc[base] * (32 - shift) + Lc[base + 1] * shift, 5);
+                }
+                p |= (uint32_t)v << (8 * b);
+            }
+            break;
+        }
+        case FI_Z3: {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int idx = (qj + b + 1) * dy;
+                const int base = (idx >> (6 - upL)) + (i << upL);
+                const int shift = ((idx << upL) >> 1) & 0x1F;
+                p |= (uint32_t)r2(Lc[base] * (32 - shift) + Lc[base + 1] * shift, 5) << (8 * b);
+            }
+            break;
+        }
+        case FI_PAETH: {
+            const uint32_t a4 = rawA(qj) | rawA(qj + 1) << 8 | rawA(qj + 2) << 16 | (uint32_t)rawA(qj + 3) << 24;
+            const int l = rawL(i), tl0 = corner0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int a = (a4 >> (8 * b)) & 0xff;
+                const int base = a + l - tl0;
+                const int pL = iabs(base - l), pT = iabs(base - a), pTL = iabs(base - tl0);
+                p |= (uint32_t)((pL <= pT && pL <= pTL) ? l : (pT <= pTL ? a : tl0)) << (8 * b);
+            }
+            break;
+        }
+        default: {  // SMOOTH, SMOOTH_V, SMOOTH_H
+            const uint32_t a4 = rawA(qj) | rawA(qj + 1) << 8 | rawA(qj + 2) << 16 | (uint32_t)rawA(qj + 3) << 24;
+            const uint32_t wx4 = fi_smw(log2W, qj >> 2);
+            const int wy = (fi_smw(log2H, i >> 2) >> (8 * (i & 3))) & 0xff;
+            const int l = rawL(i), bl = rawL(h - 1), tr = rawA(w - 1);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int a = (a4 >> (8 * b)) & 0xff, wx = (wx4 >> (8 * b)) & 0xff;
+                int v;
+                if (cls == FI_SMOOTH) v = r2(wy * a + (256 - wy) * bl + wx * l + (256 - wx) * tr, 9);
+                else if (cls == FI_SMOOTH_V) v = r2(wy * a + (256 - wy) * bl, 8);
+                else v = r2(wx * l + (256 - wx) * tr, 8);
+                p |= (uint32_t)v << (8 * b);
+            }
+            break;
+        }
+        }
+    }
+    {
+        // CFL: the luma average over the block (every quad of a tiny item is in its row)
+        const int s = row16_total(csum);
+        if (act && cfl) {
+            const int alpha = (int)(int8_t)bits(d[4], 16, 8);
+            const int avg = r2(s, log2W + log2H);
+            uint32_t q = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) q |= (uint32_t)clip1(dc + r2s(alpha * (cv[b] - avg), 6)) << (8 * b);
+            p = q;
+        }
+    }
+    const uint32_t o = add4(p, res);
+    // ---- the granules first (what the next items wait for), then the frame (as fi_run: the
+    // bottom row's units are the last row's quads; a right-column unit is byte 3 of four
+    // vertically adjacent quads, t + w4, + 2 w4, + 3 w4 -- in the same DPP row)
+    const uint64_t tag = (uint64_t)epoch << 32;
+    const uint32_t a1 = __builtin_amdgcn_update_dpp(0, (int)o, 0x101, 0xf, 0xf, true);  // row_shl:1
+    const uint32_t a2 = __builtin_amdgcn_update_dpp(0, (int)o, 0x102, 0xf, 0xf, true);
+    const uint32_t a3 = __builtin_amdgcn_update_dpp(0, (int)o, 0x103, 0xf, 0xf, true);
+    const uint32_t b2 = __builtin_amdgcn_update_dpp(0, (int)o, 0x104, 0xf, 0xf, true);
+    const uint32_t b3 = __builtin_amdgcn_update_dpp(0, (int)o, 0x106, 0xf, 0xf, true);
+    const uint32_t o1 = w4 == 1 ? a1 : a2, o2 = w4 == 1 ? a2 : b2, o3 = w4 == 1 ? a3 : b3;
+    if (act && t < nq && qi == h - 1)
+        __hip_atomic_store(const_cast<uint64_t*>(gh) + (size_t)((y + h - 1) >> 2) * gw + (x >> 2) + (qj >> 2), tag | o,
+            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (act && t < nq && qj == w - 4 && (qi & 3) == 0) {
+        const uint32_t v = (o >> 24) | ((o1 >> 24) << 8) | ((o2 >> 24) << 16) | ((o3 >> 24) << 24);
+        __hip_atomic_store(const_cast<uint64_t*>(gv) + (size_t)((x + w - 1) >> 2) * ghn + (y >> 2) + (qi >> 2), tag | v,
+            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (act && t < nq) stp4<true>(dst, x + qj, y + qi, o);
+    // the drain and done flag where a dependency list names the item (CFL's luma)
+    const bool pub = act && (fl & TI_PUB);
+    if (__any(pub)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (pub && t == 0) __hip_atomic_store(k.done + pos, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
-// workgroup), n >= 1 small items (wave w runs items w, w + 4, ..)
+// workgroup), n | FLOW_G_TINY: n tiny items (four per wave, tiny_run), else n >= 1 small
+// items (wave w runs items w, w + 4, ..)
 #ifndef AV1R_FLOW_WAVES
 #define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better; 8 = 64 VGPRs + spills: 4K recon +3 %, profiles/r05_ab_flow_waves8.txt)
 #endif
@@ -1965,6 +2363,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
     uint32_t* ctl, uint32_t epoch, unsigned long long* trace)
 {
     constexpr size_t kLds = sizeof(TbLds<64>) > 4 * sizeof(TbLds<TB_SMALL>) ? sizeof(TbLds<64>) : 4 * sizeof(TbLds<TB_SMALL>);
+    static_assert(16 * sizeof(TinyLds) <= kLds, "k_flow LDS: the tiny groups' rows");
     __shared__ __align__(16) uint8_t smem[kLds];
     __shared__ uint32_t ticket[2];  // double-buffered: a slow wave may still read the old one
     // The queue a workgroup serves is its ENTRY order, not its blockIdx: the first
@@ -2010,6 +2409,11 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
         const uint32_t n = gd.x & 0xff;
         if (n == 0) {
             flow_item<256, 64>(k, gd.y, *reinterpret_cast<TbLds<64>*>(smem), epoch, ctl, trace, gd.x >> 8);
+        } else if (n & FLOW_G_TINY) {
+            // tiny items: wave w runs items w, w + 4, w + 8, w + 12 side by side (tiny_run)
+            const uint32_t nt = n & (FLOW_G_TINY - 1);
+            const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            if (wave < nt) tiny_run(k, gd.y, nt, reinterpret_cast<TinyLds*>(smem) + 4 * wave, epoch, ctl);
         } else {
             // small items: wave w runs items w, w + 4, .. of the group, one after the other in
             // its own LDS tiles (the host's groups hold 4, or 8 on crowded levels: items of
