@@ -89,14 +89,16 @@ static_assert(sizeof(WorkItem) == 32, "WorkItem layout");
 #define AV1R_WI_TINY 1u
 
 // k_flow's tiny items (round 6).  An intra transform block of at most 8x8 on the lean path
-// (intra_fast.h: not palette, not filter-intra) in a frame with edge granules is described
-// whole by the host, in the 32 bytes of its WorkItem slot: every parameter fi_setup derives
-// (the prediction class, edge-filter strengths and lengths, upsampling, dx / dy, CFL's alpha
-// and luma extent), its granule masks and residual tile.  k_flow runs them four to a wave,
-// 16 lanes each (tiny_run, recon.hip): one scalar load per item gives all it needs, and the
-// four items' memory round trips overlap.  pack_frame writes these records for the items
-// build_schedule marked AV1R_WI_TINY; the tiny groups of a level (up to 16 items, group flag
-// FLOW_G_TINY) come before its other small items.
+// (intra_fast.h: not palette, not filter-intra) in a frame with edge granules, on a crowded
+// level, is described whole in the 32 bytes of its WorkItem slot: every parameter fi_setup
+// derives (the prediction class, edge-filter strengths and lengths, upsampling, dx / dy,
+// CFL's alpha and luma extent), its granule masks and residual tile.  k_flow runs them four
+// to a wave, 16 lanes each (tiny_run, recon.hip): one scalar load per item gives all it
+// needs, and the four items' memory round trips overlap.  build_schedule marks the items
+// AV1R_WI_TINY (the tiny groups of a level, up to 16 items, group flag FLOW_G_TINY, come
+// before its other small items) and k_mi_zero rewrites their slots on the device
+// (tiny_from_item, filters.hip: no host time).  Bytes 26-27 -- WorkItem::hflags -- stay 0, so
+// a rewritten slot is not rewritten again when a prepared frame is decoded twice.
 struct TinyItem {
     uint16_t x, y;      // plane position
     uint8_t shape;      // plane (bits 0-1) | log2W - 2 (bit 2) | log2H - 2 (bit 3) | class (bits 4-7, FI_*)
@@ -110,12 +112,13 @@ struct TinyItem {
     uint16_t p0, p1;    // directional: dx, dy; CFL: max_luma_w, max_luma_h
     int8_t alpha;       // CFL
     uint8_t pad;
-    uint16_t dep_cnt;   // dependency list (CFL's co-located luma) at KParams::deps[dep_off ..)
-    uint16_t pad2;
-    uint32_t dep_off;
+    uint32_t dep_off;   // dependency list (CFL's co-located luma) at KParams::deps[dep_off ..)
+    uint16_t dep_cnt;
+    uint16_t zero;      // (WorkItem::hflags' bytes: 0)
     uint32_t res;       // residual tile (int16 elements into KParams::res; ~0u: none)
 };
 static_assert(sizeof(TinyItem) == 32, "TinyItem layout");
+static_assert(offsetof(TinyItem, zero) == offsetof(WorkItem, hflags), "TinyItem / WorkItem overlay");
 #define TI_HA 1u
 #define TI_HL 2u
 #define TI_CFL 4u

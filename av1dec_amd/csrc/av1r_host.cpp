@@ -734,90 +734,6 @@ static int intra_needs(const av1r_block& blk, int p, bool hA, bool hL)
     return 7;
 }
 
-// getIntraEdgeFilterStrength (IntraPredict.cpp:269-343) and getIntraEdgeUpsample (:345-358),
-// for the host's TinyItem records (the device's own copies: intra_dev.h)
-static int host_edge_strength(int w, int h, bool filterType, int delta)
-{
-    const int d = std::abs(delta), blkWh = w + h;
-    int s = 0;
-    if (!filterType) {
-        if (blkWh <= 8) s = d >= 56;
-        else if (blkWh <= 16) s = d >= 40;
-        else if (blkWh <= 24) s = d >= 32 ? 3 : d >= 16 ? 2 : d >= 8 ? 1 : 0;
-        else if (blkWh <= 32) s = d >= 32 ? 3 : d >= 4 ? 2 : 1;
-        else s = 3;
-    } else {
-        if (blkWh <= 8) s = d >= 64 ? 2 : d >= 40 ? 1 : 0;
-        else if (blkWh <= 16) s = d >= 48 ? 2 : d >= 20 ? 1 : 0;
-        else if (blkWh <= 24) s = d >= 4 ? 3 : 0;
-        else s = 3;
-    }
-    return s;
-}
-static int host_edge_upsample(int w, int h, bool filterType, int delta)
-{
-    const int d = std::abs(delta), blkWh = w + h;
-    if (d <= 0 || d >= 40) return 0;
-    return filterType ? blkWh <= 8 : blkWh <= 16;
-}
-// The TinyItem of an intra TB of at most 8x8 (av1r_dev.h): fi_setup's parameters
-// (intra_fast.h, restating IntraPredict::predict_intra, IntraPredict.cpp:563-630, with the
-// directional edge preparation :389-437) from the batch, plus the item's granule masks m[0..3]
-// (m[3]: its residual tile) and dependency list.
-static TinyItem tiny_record(const av1r_frame_hdr* h, const av1r_block& blk, const WorkItem& w, const uint32_t* m)
-{
-    TinyItem r;
-    memset(&r, 0, sizeof(r));
-    const int plane = w.plane, sub = plane ? 1 : 0, x = w.x, y = w.y;
-    const int log2W = av1r_tx_w_log2[w.tx_size], log2H = av1r_tx_h_log2[w.tx_size];
-    const int tw = 1 << log2W, th = 1 << log2H;
-    const int maxXd = (h->mi_cols * 4) >> sub, maxYd = (h->mi_rows * 4) >> sub;
-    const bool hA = w.flags & AV1R_TB_HAVE_ABOVE, hL = w.flags & AV1R_TB_HAVE_LEFT;
-    const int aboveLimit = std::min(maxXd - 1, x + ((w.flags & AV1R_TB_HAVE_AR) ? 2 * tw : tw) - 1);
-    const int leftLimit = std::min(maxYd - 1, y + ((w.flags & AV1R_TB_HAVE_BL) ? 2 * th : th) - 1);
-    const bool cfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
-    const int mode = plane == 0 ? blk.y_mode : (cfl ? AV1R_DC_PRED : blk.uv_mode);
-    const bool smooth = plane ? (blk.flags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0
-                              : (blk.flags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0;
-    int cls, strA = 0, strL = 0, nA = 0, nL = 0, nUA = 0, nUL = 0, corner = 0, dx = 0, dy = 0;
-    if (mode >= AV1R_V_PRED && mode <= AV1R_D67_PRED) {
-        const int pAngle = av1r_mode_to_angle[mode] + (plane == 0 ? blk.angle_delta_y : blk.angle_delta_uv) * 3;
-        cls = pAngle < 90 ? FI_Z1 : pAngle == 90 ? FI_V : pAngle < 180 ? FI_Z2 : pAngle == 180 ? FI_H : FI_Z3;
-        if (h->enable_intra_edge_filter && pAngle != 90 && pAngle != 180) {
-            corner = pAngle > 90 && pAngle < 180 && (tw + th) >= 24;
-            strA = hA ? host_edge_strength(tw, th, smooth, pAngle - 90) : 0;
-            strL = hL ? host_edge_strength(tw, th, smooth, pAngle - 180) : 0;
-            nA = std::min(tw, maxXd - x + 1) + (pAngle < 90 ? th : 0) + 1;
-            nL = std::min(th, maxYd - y + 1) + (pAngle > 180 ? tw : 0) + 1;
-            nUA = host_edge_upsample(tw, th, smooth, pAngle - 90) ? tw + (pAngle < 90 ? th : 0) : 0;
-            nUL = host_edge_upsample(tw, th, smooth, pAngle - 180) ? th + (pAngle > 180 ? tw : 0) : 0;
-        }
-        if (pAngle < 90) dx = av1r_dr_intra_derivative[pAngle];
-        else if (pAngle > 90 && pAngle < 180) dx = av1r_dr_intra_derivative[180 - pAngle];
-        if (pAngle > 90 && pAngle < 180) dy = av1r_dr_intra_derivative[pAngle - 90];
-        else if (pAngle > 180) dy = av1r_dr_intra_derivative[270 - pAngle];
-    } else {
-        cls = mode == AV1R_DC_PRED ? FI_DC : mode == AV1R_SMOOTH_PRED ? FI_SMOOTH : mode == AV1R_SMOOTH_V_PRED ? FI_SMOOTH_V
-            : mode == AV1R_SMOOTH_H_PRED ? FI_SMOOTH_H : FI_PAETH;
-    }
-    r.x = (uint16_t)x;
-    r.y = (uint16_t)y;
-    r.shape = (uint8_t)(plane | (log2W - 2) << 2 | (log2H - 2) << 3 | cls << 4);
-    r.flags = (uint8_t)((hA ? TI_HA : 0) | (hL ? TI_HL : 0) | (cfl ? TI_CFL : 0) | (corner ? TI_CORNER : 0) | ((w.pub & 1) ? TI_PUB : 0));
-    r.str = (uint8_t)(strA | strL << 4);
-    r.lim = (uint8_t)((aboveLimit - x) | (leftLimit - y) << 4);
-    r.nA = (uint8_t)nA, r.nL = (uint8_t)nL, r.nUA = (uint8_t)nUA, r.nUL = (uint8_t)nUL;
-    r.masks = (uint8_t)((m[0] & 15) | (m[2] & 15) << 4);
-    r.mC = (uint8_t)(m[1] & 3);
-    r.p0 = (uint16_t)(cfl ? blk.max_luma_w : dx);
-    r.p1 = (uint16_t)(cfl ? blk.max_luma_h : dy);
-    r.alpha = cfl ? (plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v) : 0;
-    r.dep_cnt = w.dep_cnt;
-    r.dep_off = w.dep_off;
-    r.res = m[3];
-    return r;
-}
-
 // k_flow's small-item groups: four items (one per wave) on a thin level, 8 (two per wave,
 // run one after the other) on a level of at least 256 small items of the frame, where the
 // workgroup's ticket, group load and closing barrier are paid once per two items per wave (a
@@ -1722,15 +1638,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
             wi[i].coef_off = c->tbCoefOff[ti];
             wi[i].flags |= AV1R_TBD_WIDE;
         }
-        // the tiny items' slots hold their TinyItem (k_flow's tiny groups read nothing else)
-        for (const Level& lv : c->levels)
-            for (uint32_t q = 0; q < lv.tiny; q++) {
-                const size_t i = lv.off[2] + q;
-                const WorkItem& w = c->items[i];
-                if (!(w.hflags & AV1R_WI_TINY) || w.dep_off < 4) return fail(c, AV1R_E_INVALID, "tiny item %zu", i);
-                const TinyItem r = tiny_record(h, b->blocks[w.block], w, c->deps.data() + w.dep_off - 4);
-                memcpy(wi + i, &r, sizeof(r));
-            }
+        // (the tiny items' slots become TinyItems on the device: k_mi_zero)
     }
     k.tiles = (const uint32_t*)put(c->tiles.data(), 4 * c->tiles.size(), szTiles);
     k.deps = (const uint32_t*)put(c->deps.data(), 4 * c->deps.size(), szDeps);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "av1r_dev.h"
+#include "intra_dev.h"
 
 
 // ------------------------------------------------------------------------------------
@@ -1245,8 +1246,17 @@ extern "C" __global__ __launch_bounds__(256) void k_mi_zero(const KParams* kps)
 {
     const KParams& k = KP(kps, blockIdx.y);
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    // k_flow's done words start at 0, no launch's epoch (they are not uploaded)
-    if (i < k.n_items && k.done) k.done[i] = 0;
+    // k_flow's done words start at 0, no launch's epoch (they are not uploaded); a tiny item's
+    // slot gets its TinyItem (av1r_dev.h)
+    if (i < k.n_items && k.done) {
+        k.done[i] = 0;
+        WorkItem* items = const_cast<WorkItem*>(k.items);
+        const WorkItem w = items[i];
+        if (w.hflags & AV1R_WI_TINY) {
+            const TinyItem r = tiny_from_item(k, w, k.blocks[w.block], k.deps + w.dep_off - 4);
+            *reinterpret_cast<TinyItem*>(items + i) = r;
+        }
+    }
     const int r = (int)(i / (uint32_t)k.mi_stride), c = (int)(i - (uint32_t)r * k.mi_stride);
     if (r >= k.mi_rows_alloc || (r < k.mi_rows && c < k.mi_cols)) return;
     uint32_t* d = reinterpret_cast<uint32_t*>(const_cast<av1r_mi*>(k.mi) + i);

@@ -75,6 +75,67 @@ DEV int edge_upsample_used(int w, int h, int filterType, int delta)
     return filterType ? (blkWh <= 8) : (blkWh <= 16);
 }
 
+// The TinyItem of an intra TB of at most 8x8 (av1r_dev.h; k_mi_zero writes it over the
+// item's WorkItem): fi_setup's parameters (intra_fast.h, restating IntraPredict::predict_intra,
+// IntraPredict.cpp:563-630, with the directional edge preparation :389-437), per lane (the
+// tables through plain loads), plus the item's granule masks m[0..3] (m[3]: its residual tile,
+// build_schedule's fourth mask word) and dependency list.
+DEV TinyItem tiny_from_item(const KParams& k, const WorkItem& w, const DevBlock& blk, const uint32_t* m)
+{
+    const av1r_frame_hdr& hd = *k.hdr;
+    const int plane = w.plane, sub = plane ? 1 : 0, x = w.x, y = w.y;
+    const int log2W = av1r_tx_w_log2[w.tx_size], log2H = av1r_tx_h_log2[w.tx_size];
+    const int tw = 1 << log2W, th = 1 << log2H;
+    const int maxXd = (k.mi_cols * 4) >> sub, maxYd = (k.mi_rows * 4) >> sub;
+    const bool hA = w.flags & AV1R_TB_HAVE_ABOVE, hL = w.flags & AV1R_TB_HAVE_LEFT;
+    const int aboveLimit = imin(maxXd - 1, x + ((w.flags & AV1R_TB_HAVE_AR) ? 2 * tw : tw) - 1);
+    const int leftLimit = imin(maxYd - 1, y + ((w.flags & AV1R_TB_HAVE_BL) ? 2 * th : th) - 1);
+    const bool cfl = plane > 0 && blk.uv_mode == AV1R_UV_CFL_PRED;
+    const int mode = plane == 0 ? blk.y_mode : (cfl ? AV1R_DC_PRED : blk.uv_mode);
+    const int smooth = plane ? ((blk.flags & (AV1R_BLK_SMOOTH_A_UV | AV1R_BLK_SMOOTH_L_UV)) != 0)
+                             : ((blk.flags & (AV1R_BLK_SMOOTH_A_Y | AV1R_BLK_SMOOTH_L_Y)) != 0);
+    int cls, strA = 0, strL = 0, nA = 0, nL = 0, nUA = 0, nUL = 0, corner = 0, dx = 0, dy = 0;
+    if (mode >= AV1R_V_PRED && mode <= AV1R_D67_PRED) {
+        const int pAngle = av1r_mode_to_angle[mode] + (plane == 0 ? blk.angle_delta_y : blk.angle_delta_uv) * 3;
+        cls = pAngle < 90 ? FI_Z1 : pAngle == 90 ? FI_V : pAngle < 180 ? FI_Z2 : pAngle == 180 ? FI_H : FI_Z3;
+        if (hd.enable_intra_edge_filter && pAngle != 90 && pAngle != 180) {
+            corner = pAngle > 90 && pAngle < 180 && (tw + th) >= 24;
+            strA = hA ? edge_strength(tw, th, smooth, pAngle - 90) : 0;
+            strL = hL ? edge_strength(tw, th, smooth, pAngle - 180) : 0;
+            nA = imin(tw, maxXd - x + 1) + (pAngle < 90 ? th : 0) + 1;
+            nL = imin(th, maxYd - y + 1) + (pAngle > 180 ? tw : 0) + 1;
+            nUA = edge_upsample_used(tw, th, smooth, pAngle - 90) ? tw + (pAngle < 90 ? th : 0) : 0;
+            nUL = edge_upsample_used(tw, th, smooth, pAngle - 180) ? th + (pAngle > 180 ? tw : 0) : 0;
+        }
+        if (pAngle < 90) dx = av1r_dr_intra_derivative[pAngle];
+        else if (pAngle > 90 && pAngle < 180) dx = av1r_dr_intra_derivative[180 - pAngle];
+        if (pAngle > 90 && pAngle < 180) dy = av1r_dr_intra_derivative[pAngle - 90];
+        else if (pAngle > 180) dy = av1r_dr_intra_derivative[270 - pAngle];
+    } else {
+        cls = mode == AV1R_DC_PRED ? FI_DC : mode == AV1R_SMOOTH_PRED ? FI_SMOOTH : mode == AV1R_SMOOTH_V_PRED ? FI_SMOOTH_V
+            : mode == AV1R_SMOOTH_H_PRED ? FI_SMOOTH_H : FI_PAETH;
+    }
+    TinyItem r;
+    r.x = (uint16_t)x;
+    r.y = (uint16_t)y;
+    r.shape = (uint8_t)(plane | (log2W - 2) << 2 | (log2H - 2) << 3 | cls << 4);
+    r.flags = (uint8_t)((hA ? TI_HA : 0u) | (hL ? TI_HL : 0u) | (cfl ? TI_CFL : 0u) | (corner ? TI_CORNER : 0u) | ((w.pub & 1) ? TI_PUB : 0u));
+    r.str = (uint8_t)(strA | strL << 4);
+    r.lim = (uint8_t)((aboveLimit - x) | (leftLimit - y) << 4);
+    r.nA = (uint8_t)nA, r.nL = (uint8_t)nL, r.nUA = (uint8_t)nUA, r.nUL = (uint8_t)nUL;
+    r.masks = (uint8_t)((m[0] & 15) | (m[2] & 15) << 4);
+    r.mC = (uint8_t)(m[1] & 3);
+    r.p0 = (uint16_t)(cfl ? blk.max_luma_w : dx);
+    r.p1 = (uint16_t)(cfl ? blk.max_luma_h : dy);
+    r.alpha = (int8_t)(cfl ? (plane == 1 ? blk.cfl_alpha_u : blk.cfl_alpha_v) : 0);
+    r.pad = 0;
+    r.dep_off = w.dep_off;
+    r.dep_cnt = w.dep_cnt;
+    r.zero = 0;
+    r.res = m[3];
+    return r;
+}
+
 // The edge preparation of directionalIntraPredict (IntraPredict.cpp:394-437) for both
 // edges at once, three barriers in all: the corner filter (filterCorner, :204-209) folded
 // into the copy pass, both intraEdgeFilter passes (:324-337) in one, both upsamples

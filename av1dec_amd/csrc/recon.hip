@@ -2047,7 +2047,7 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
     const uint32_t resOff = d[7];
     uint2 res = make_uint2(0, 0);
     if (act && resOff != ~0u && t < nq) res = reinterpret_cast<const uint2*>(k.res + resOff)[t];
-    const uint32_t depCnt = d[5] & 0xffff, depOff = d[6];
+    const uint32_t depOff = d[5], depCnt = d[6] & 0xffff;
     // (more than 16 dependencies: the rest polled first, 16 a round; rare)
     for (uint32_t b = 16;; b += 16) {
         const bool more = act && b < depCnt;

@@ -221,8 +221,8 @@ def test_lean_intra_constants_match_the_tables():
 # the separate ones (AV1R_PACK_FUSED, since removed) with it.  Round 6 found the sections'
 # padding unwritten (heap contents travelled; under MALLOC_PERTURB_ the digest changed from
 # run to run) and zeroes it; pruning the library's measured-slower paths left the packed
-# bytes unchanged; the tiny items' records (TinyItem) then changed them.  A change that alters the packed layout on purpose updates it here.
-PACK_DIGEST = "57d6cf3815e599abc424a1517175875e 82"  # (digest, frames)
+# bytes unchanged; the tiny items' marks (WorkItem::hflags) then changed them.  A change that alters the packed layout on purpose updates it here.
+PACK_DIGEST = "ccbe78da075ff41591f6f3c6dc557f11 82"  # (digest, frames)
 
 
 def test_pack_digest_unchanged():
