@@ -1117,20 +1117,23 @@ DEV void lr_filter_tile(LrLds& L, const av1r_frame_hdr& h, int plane, int x0, in
     }
 }
 
-// one 256-lane workgroup per tile; blockIdx.z = 3 * frame + plane.  Reads the CDEF
-// frame (k.cdef) and the deblocked frame (k.dbk, stripe rows), writes k.lrout.
-extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
+// one 256-lane workgroup per tile; wg = (64-column tile, tile row, 3 * frame + plane).  Reads
+// the CDEF frame (k.cdef) and the deblocked frame (k.dbk, stripe rows), writes k.lrout.
+// What a launch must guarantee: every tile of every frame and plane is
+// some workgroup's wg, and a tile row is a LUMA half-stripe (two per 64-row stripe from -8)
+// but a whole CHROMA stripe (one per 32-row stripe from -4) -- wg.y means a different row
+// span per plane (the static_assert below).  Nothing else of the launch enters: a workgroup
+// reads only its own tile's inputs, so any order, grid shape or residency gives the same
+// output.  Round 6 re-created round 5's "one-grid" variant (k_lr1 below, every frame's luma
+// then chroma tiles in a 1-D grid): 172 streams stage-exact plus the synthetic tests
+// (profiles/r06_lr_onegrid_parity.txt), so its round-5 mismatch was that variant's own tile
+// numbering, not a property of this kernel.  The one-grid form is also the faster (LR 0.0125
+// -> 0.0121 ms per 1080p frame, profiles/r06_ab_lr_onegrid.txt) and is k_lr since.
+static_assert(64 / LR_TH == 2 && 32 / LR_TH == 1, "k_lr tile rows: luma half-stripes, chroma whole stripes");
+DEV void lr_body(const KParams* kps, const uint3 wg)
 {
     __shared__ LrLds L;
     const int t = threadIdx.x;
-#ifndef AV1R_LR_XCD  // XCD order for k_lr: 4K LR 0.080 -> 0.108 ms/frame (1080p unchanged), though
-#define AV1R_LR_XCD 0   // its fabric traffic fell 16.7 -> 6.7 MB/frame: measured, so off
-#endif
-#if AV1R_LR_XCD
-    const uint3 wg = xcd_block_xy();  // (per slice: chroma slices are half empty)
-#else
-    const uint3 wg = make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
-#endif
     const KParams& k = KP(kps, wg.z / 3);
     if (!k.hdr->uses_lr) return;  // the frame's output is its CDEF frame
     const int plane = wg.z % 3, sub = plane ? 1 : 0;
@@ -1212,6 +1215,23 @@ extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps)
     }
     __syncthreads();
     lr_filter_tile(L, h, plane, x0, tw, ty0, th, y0, us, cols, uc0, nU, planeEndX, planeEndY, O);
+}
+// Every frame's luma tiles (nxl x nyl) then its chroma tiles (nxc x nyc per plane) in one 1-D
+// grid: no empty workgroups (round 5's 3-D grid sized every plane by the luma tiles, so three
+// quarters of the chroma workgroups started and returned at once).  Dispatch order (round 4:
+// XCD order for LR fetched 16.7 -> 6.7 MB/frame but took 4K LR 0.080 -> 0.108 ms/frame).
+extern "C" __global__ __launch_bounds__(256) void k_lr(const KParams* kps, int nxl, int nyl, int nxc, int nyc)
+{
+    const int per = nxl * nyl + 2 * nxc * nyc;
+    const int f = blockIdx.x / per;
+    int r = blockIdx.x - f * per, plane = 0, nx = nxl;
+    if (r >= nxl * nyl) {
+        r -= nxl * nyl;
+        plane = 1 + r / (nxc * nyc);
+        r -= (plane - 1) * nxc * nyc;
+        nx = nxc;
+    }
+    lr_body(kps, make_uint3(r % nx, r / nx, 3 * f + plane));
 }
 
 // The launch metadata, copied by the compute queue itself from pinned host memory (the
@@ -1341,7 +1361,9 @@ void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s)
 {
     // tile rows: luma stripes (64 rows from -8) in halves; chroma stripes whole
     const int tilesY = 2 * ((maxH + 8 + 63) / 64);
-    hipLaunchKernelGGL(k_lr, dim3((maxW + LR_TW - 1) / LR_TW, tilesY, 3 * n), dim3(256), 0, s, kps);
+    const int nxl = (maxW + LR_TW - 1) / LR_TW, nxc = ((maxW + 1) / 2 + LR_TW - 1) / LR_TW;
+    const int nyc = ((maxH + 1) / 2 + 4 + 31) / 32;  // chroma stripes (32 rows from -4)
+    hipLaunchKernelGGL(k_lr, dim3(n * (nxl * tilesY + 2 * nxc * nyc)), dim3(256), 0, s, kps, nxl, tilesY, nxc, nyc);
 }
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s)
 {

@@ -1999,13 +1999,36 @@ DEV void flow_wait_lanes(uint32_t d, const uint32_t* done, uint32_t epoch, uint3
     }
 }
 
+// -DAV1R_TRACE lite stamps of a tiny item (its row's lane 0 writes its timeline row directly,
+// no waits): 2 entry, 3 records in, 4 dependencies and edge units in, 8 units in LDS, 9
+// predicted, 10 stored, 5 published; 0 / 1 / 7 as flow_item's
+#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
+#define TINY_STAMP(s) \
+    if (tr && t == 0) tr[s] = __builtin_amdgcn_s_memrealtime()
+#else
+#define TINY_STAMP(s) (void)0
+#endif
 // pos0: the group's first item; nIt: its items (<= 16); T: this wave's four rows
-DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uint32_t epoch, uint32_t* ctl)
+DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uint32_t epoch, uint32_t* ctl,
+    unsigned long long* trace, uint32_t frame)
 {
     const int lane = threadIdx.x & 63, row = lane >> 4;
     int t = lane & 15;
     asm volatile("" : "+v"(t));  // (as coop_lane: no lane-derived address hoisted)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if defined(AV1R_TRACE) && defined(AV1R_TRACE_LITE)
+    unsigned long long* tr = trace && wave + 4 * row < nIt ? trace + (size_t)(k.trace_base + pos0 + wave + 4 * row) * AV1R_TRACE_W : nullptr;
+    TINY_STAMP(2);
+    if (tr && t == 0) {
+        tr[0] = AV1R_ITEM(AV1R_ITEM_TB, 0);
+        tr[1] = (unsigned long long)frame << 32;
+        tr[7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32) |
+                ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 16);
+    }
+#else
+    (void)trace;
+    (void)frame;
+#endif
     // ---- the rows' records: four scalar loads, merged per lane
     uint32_t d[8];
     {
@@ -2023,6 +2046,7 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
     }
     const bool act = wave + 4 * row < nIt;
     const uint32_t pos = pos0 + wave + 4 * row;
+    TINY_STAMP(3);
     const int x = (int)(d[0] & 0xffff), y = (int)(d[0] >> 16);
     const int plane = (int)bits(d[1], 0, 2);
     const int log2W = 2 + (int)bits(d[1], 2, 1), log2H = 2 + (int)bits(d[1], 3, 1);
@@ -2110,6 +2134,7 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
         }
     }
     asm volatile("" ::: "memory");  // no pixel load moves above the poll
+    TINY_STAMP(4);
     TinyLds& L = T[row];
     if (uact) (kind == 0 ? L.ua + u : kind == 1 ? L.ul + u : L.ul + 7)[0] = val;
     // CFL: the co-located luma of this lane's quad (flow read site: the block's luma, written by
@@ -2129,6 +2154,7 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
         }
     }
     coop_sync<64>();  // (wave level: the units are in LDS)
+    TINY_STAMP(8);
     // ---- AboveRow / LeftCol (fi_run's passes, per row)
     const uint8_t* ta = reinterpret_cast<const uint8_t*>(L.ua);
     const uint8_t* tl = reinterpret_cast<const uint8_t*>(L.ul);
@@ -2317,6 +2343,7 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
         }
     }
     const uint32_t o = add4(p, res);
+    TINY_STAMP(9);
     // ---- the granules first (what the next items wait for), then the frame (as fi_run: the
     // bottom row's units are the last row's quads; a right-column unit is byte 3 of four
     // vertically adjacent quads, t + w4, + 2 w4, + 3 w4 -- in the same DPP row)
@@ -2336,12 +2363,14 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (act && t < nq) stp4<true>(dst, x + qj, y + qi, o);
+    TINY_STAMP(10);
     // the drain and done flag where a dependency list names the item (CFL's luma)
     const bool pub = act && (fl & TI_PUB);
     if (__any(pub)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (pub && t == 0) __hip_atomic_store(k.done + pos, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    TINY_STAMP(5);
 }
 
 // groups[g] = {frame << 8 | n, first item position}: n = 0 one large item (the whole
@@ -2413,7 +2442,7 @@ extern "C" __global__ __launch_bounds__(256, AV1R_FLOW_WAVES) void k_flow(const 
             // tiny items: wave w runs items w, w + 4, w + 8, w + 12 side by side (tiny_run)
             const uint32_t nt = n & (FLOW_G_TINY - 1);
             const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            if (wave < nt) tiny_run(k, gd.y, nt, reinterpret_cast<TinyLds*>(smem) + 4 * wave, epoch, ctl);
+            if (wave < nt) tiny_run(k, gd.y, nt, reinterpret_cast<TinyLds*>(smem) + 4 * wave, epoch, ctl, trace, gd.x >> 8);
         } else {
             // small items: wave w runs items w, w + 4, .. of the group, one after the other in
             // its own LDS tiles (the host's groups hold 4, or 8 on crowded levels: items of

@@ -16,7 +16,7 @@ from collections import defaultdict
 STAGES = {"k_inter": "recon", "k_inter_m": "recon", "k_inter_s": "recon", "k_inter_all": "recon", "k_tb": "recon",
           "k_resid_s": "recon", "k_resid_l": "recon", "k_flow": "recon",
           "k_mi_zero": "recon", "k_mi_blocks": "recon", "k_mi_tbs": "recon",
-          "k_lf": "lf", "k_lfcode": "lf", "k_deblock": "lf", "k_cdef": "cdef", "k_lr": "lr"}
+          "k_lf": "lf", "k_cdef": "cdef", "k_lr": "lr"}
 
 
 def fold(path, counter):
