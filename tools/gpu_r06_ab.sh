@@ -3,11 +3,13 @@
 # variants in rotation, twice), then the LDS / occupancy SQ pass of each build, then the
 # rocprofv3 kernel statistics of the current build.  Every GPU step time-limited; any failure
 # ends the script.
-# usage: bash tools/gpu_r06_ab.sh [--no-suite] other.so [more.so ...]
+# usage: bash tools/gpu_r06_ab.sh [--no-suite] [--quick] other.so [more.so ...]
+# (--quick: the A/B runs only, no SQ pass and no kernel statistics)
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab6 gpurun_out/prof
 export TMPDIR=/tmp
-if [ "$1" = "--no-suite" ]; then shift; else
+QUICK=0
+if [ "$1" = "--no-suite" ]; then shift; [ "$1" = "--quick" ] && { QUICK=1; shift; }; else
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1 || { tail -40 gpurun_out/pytest.log; exit 1; }
 tail -2 gpurun_out/pytest.log
 fi
@@ -25,6 +27,7 @@ PY
         v=$((v + 1))
     done
 done
+[ $QUICK = 1 ] && exit 0
 B1080="--steps 8 --warmup 2 --frames 60 --no-cpu --no-4k --ivf-frames 0 --output-steps 0 --prime-steps 1"
 v=0
 for lib in "" "$@"; do
