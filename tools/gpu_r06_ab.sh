@@ -9,6 +9,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab6 gpurun_out/prof
 export TMPDIR=/tmp
 QUICK=0
+[ "$1" = "--quick" ] && { QUICK=1; shift; }
 if [ "$1" = "--no-suite" ]; then shift; [ "$1" = "--quick" ] && { QUICK=1; shift; }; else
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1 || { tail -40 gpurun_out/pytest.log; exit 1; }
 tail -2 gpurun_out/pytest.log
