@@ -437,6 +437,43 @@ def cpu_baseline(frames, budget_s):
     return n / dt, n, dt
 
 
+def box_k(nframes=6):
+    """k on THIS host's CPU (the committed k was measured on the build
+    container's CPU): the reference decoder (oracle/_ref/av1dec_ref, built in the build
+    container from the reference's own sources by oracle/Makefile -- a CPU program, shipped
+    with the tree) on the writer's 1080p_s1 stream, and the oracle on the same frames parsed
+    by the host parser; 1 thread each (tools/calibrate_k_1080p.py's method).  None when the
+    reference binary is absent."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "av1dec_ref")
+    if not os.path.exists(ref):
+        return None
+    import re
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools", "bsw"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pybsw
+    import pyoracle
+    from av1dec_amd import parser
+    data = pybsw.stream_ivf("1080p_s1", frames=nframes, seed=0x5EED1000)
+    with tempfile.NamedTemporaryFile(suffix=".ivf") as f:
+        f.write(data)
+        f.flush()
+        out = subprocess.run([ref, "-i", f.name], capture_output=True, text=True, timeout=300).stdout
+    rfps = float(re.findall(r"decode fps = ([0-9.]+)", out)[-1])
+    frames = parser.Parser().decode_ivf(data)
+    o = pyoracle.Oracle(keep_stages=False)
+    t = time.perf_counter()
+    for fr in frames:
+        o.decode_frame(fr)
+        while o.output_pending():
+            o.get_output()
+    ofps = len(frames) / (time.perf_counter() - t)
+    o.close()
+    return {"k": round(rfps / ofps, 4), "reference_fps": round(rfps, 4), "oracle_fps": round(ofps, 4),
+            "frames": nframes, "stream": f"tools/bsw 1080p_s1 seed 0x5eed1000, {nframes} frames (1 key + {nframes - 1} inter)"}
+
+
 def load_traffic(path, config, S, stage):
     """PMC-derived HBM bytes per frame of `stage` (tools/pmc_traffic.py output) if the file
     was measured on this configuration, and which measurement (commit) it is."""
@@ -862,7 +899,26 @@ def main():
                          f"({cn} frames, {cdt:.1f} s): oracle/av1r_oracle.c, -O2, 1 thread",
                "cpu_model": cpu_model(), "host_cores": os.cpu_count()}
         cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
-        if os.path.exists(cal):
+        kb = None
+        if args.config == "1080p":
+            try:
+                kb = box_k()
+            except Exception as e:  # reported, never fatal to the line
+                errs.append(f"box k: {e}")
+        if kb:
+            # k measured here, on this host's CPU (same CPU as the oracle timing above)
+            ref_eq = cfps * kb["k"]
+            cpu.update({"k": kb["k"], "k_source": "measured in this run on " + cpu_model() + ": " + kb["stream"]
+                                                   + "; reference -O1, its decode fps incl. its parse",
+                        "k_cpu": cpu_model() + " (this host: the same CPU as the oracle timing)",
+                        "reference_measured_here": kb,
+                        "reference_equivalent_fps": round(ref_eq, 4),
+                        "speedup_end_to_end_vs_reference_equivalent": round(ivf["fps"] / ref_eq, 1) if ivf else None,
+                        "speedup_headline_vs_reference_equivalent": round(fps / max(ref_eq, 1e-9), 1),
+                        "speedup_headline_note": "parse-excluded GPU rate over a parse-inclusive reference rate"})
+            if ivf:
+                cpu["speedup_end_to_end_vs_reference_measured_here"] = round(ivf["fps"] / kb["reference_fps"], 1)
+        elif os.path.exists(cal):
             # the reference cannot travel; k = reference fps / oracle fps on the
             # same frames, measured in the build container (tools/calibrate_k_1080p.py: the
             # writer's 1080p stream, inter-dominated like this GOP; tools/calibrate_k.py: the
