@@ -36,6 +36,9 @@ void launch_k_inter_all(const KParams* kps, const uint32_t* tab, int n, uint32_t
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s);
 void launch_k_cdef(const KParams* kps, int n, int maxMiCols, int maxMiRows, hipStream_t s);
 void launch_k_lr(const KParams* kps, int n, int maxW, int maxH, hipStream_t s);
+#ifdef AV1R_FUSED_STRIPE
+void launch_k_stripe(const KParams* kps, int n, int maxW, int maxH, int runTiles, hipStream_t s);
+#endif
 void launch_k_copy_plane(const DevPlane& dst, const DevPlane& src, hipStream_t s);
 void launch_k_fetch(void* dst, const void* src, size_t bytes, hipStream_t s);
 void launch_k_mi(const KParams* kps, int n, uint32_t maxUnits, uint32_t maxBlocks, uint32_t maxTbs, hipStream_t s);
@@ -2149,6 +2152,20 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     if (snap && (rc = snapshot(AV1R_STAGE_RECON, jobs[0].R))) return rc;
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[1], st));
     // ---- the in-loop filters (decode_frame_wrapup, Av1Decoder.cpp:181-189)
+#ifdef AV1R_FUSED_STRIPE
+    // (A/B build: the three filters fused per LR stripe, filters.hip k_stripe; without stage
+    // snapshots, which need the deblocked and CDEF frames)
+    if (!snap) {
+        static const int runTiles = getenv("AV1R_STRIPE_RUN") ? std::max(1, atoi(getenv("AV1R_STRIPE_RUN"))) : 8;
+        launch_k_stripe(dk, n, maxW, maxH, runTiles, st);
+        if (lc->timing) {
+            HIPCHK(hipEventRecord(lc->ev[2], st));
+            HIPCHK(hipEventRecord(lc->ev[3], st));
+            HIPCHK(hipEventRecord(lc->ev[4], st));
+        }
+        goto filters_done;
+    }
+#endif
     // deblocking (LoopFilter::filter, LoopFilter.cpp:40-58): in place, one launch per pass
     // (k_lf).  Round 5 measured both passes of a 64x64 tile in LDS into a frame of their own
     // (k_deblock, its edge decisions from a separate k_lfcode launch): 0.0141-0.0147 ms per
@@ -2168,6 +2185,9 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
     // ---- loop restoration into its own frame (LoopRestoration.cpp:191-219)
     if (anyLr) launch_k_lr(dk, n, maxW, maxH, st);
     if (lc->timing) HIPCHK(hipEventRecord(lc->ev[4], st));
+#ifdef AV1R_FUSED_STRIPE
+filters_done:
+#endif
     HIPCHK(hipGetLastError());
     // the slot's generation moves on only once this launch is certain to record its event
     // (an early return above leaves waiters on the slot's previous launch, which completed)

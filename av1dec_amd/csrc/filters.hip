@@ -1348,6 +1348,340 @@ extern "C" __global__ void k_copy_plane(DevPlane dst, DevPlane src)
 }
 
 // ------------------------------------------------------------------------------------
+// k_stripe (round 6, A/B build -DAV1R_FUSED_STRIPE): deblocking -> CDEF
+// -> loop restoration fused, one workgroup per (frame, LR stripe, run of 64-column tiles),
+// walking its tiles left to right with every intermediate in LDS.  decode_frame_wrapup
+// (Av1Decoder.cpp:181-189) runs the three filters over the whole frame in turn; what an LR
+// stripe's output (rows [S, S + 64), S = 64 s - 8, LoopRestoration.cpp:136-189) depends on
+// is bounded:
+//   LR  rows [S, S + 64) reads CDEF rows [S, S + 64) and the deblocked rows S - 2, S - 1,
+//       S + 64, S + 65 (get_source_sample, :234-246), 3 columns either side;
+//   CDEF of the 8x8 blocks of rows [S, S + 64) (S is a multiple of 8) reads deblocked rows
+//       [S - 2, S + 66), 2 columns either side (Cdef.cpp:158-198);
+//   deblocking pass 1 (horizontal edges) writes at most 6 rows either side of an edge and reads
+//       8: the edges y in [S - 4, S + 68] give rows [S - 2, S + 66), reading pass-0 rows
+//       [S - 12, S + 76);
+//   pass 0 (vertical edges) over those 88 rows; an edge writes 6 columns either side, reads 8.
+// So the stripe's rows [S - 12, S + 76) are deblocked once (1.375x the stripe's rows, no
+// horizontal recompute), with the stages lagging one another along the walk.  At the step for
+// tile x0 (64 x0-aligned columns):
+//   pass 0 for the vertical edges x in [x0, x0 + 64)      (reads [x0 - 8, x0 + 72))
+//   pass 1 on columns [x0 - 8, x0 + 56)                   (pass 0 final left of x0 + 58)
+//   CDEF of the 8x8 blocks of columns [x0 - 16, x0 + 48)  (reads deblocked [x0 - 18, x0 + 50))
+//   LR of tile [x0 - 64, x0)                              (reads CDEF [x0 - 67, x0 + 3))
+// in a window of columns [x0 - 80, x0 + 80) that moves by 64 after each step (chroma: half
+// of everything; its LR stripe rows [S / 2, S / 2 + 32)).  A run of tiles [j0, j1) takes steps
+// j0 - 1 .. j1 (the first and the last recompute one tile of deblocking and CDEF beside the
+// run's neighbours).  The filters are the stage kernels' own device code: lf_edge / lf_unit
+// on an LDS window, cdef_cost_f / cdef_quad, lr_filter_tile.  Reads the reconstructed frame
+// (k.cur), writes the frame's output only (k.lrout, or k.cdef when the frame has no LR): no
+// deblocked or CDEF frame in HBM.
+// ------------------------------------------------------------------------------------
+#ifdef AV1R_FUSED_STRIPE
+#define FS_W 160          // luma window columns (x0 - 80 .. x0 + 80)
+#define FS_CW 80          // chroma window columns
+#define FS_DR 88          // deblocked luma rows (S - 12 .. S + 76)
+#define FS_CDR 40         // deblocked chroma rows (S/2 - 4 .. S/2 + 36)
+struct StripeLds {
+    uint8_t dy[FS_DR][FS_W];          // luma: reconstruction -> deblocked, rows S - 12 ..
+    uint8_t duv[2][FS_CDR][FS_CW];    // chroma, rows S/2 - 4 ..
+    uint8_t cy[64][FS_W];             // CDEF output, luma rows S ..
+    uint8_t cuv[2][32][FS_CW];        // chroma rows S/2 ..
+    int cost[64][8];
+    int16_t pri[64];
+    uint8_t filt[64];
+    int8_t idx[64];                   // the block's cdef_idx (-1: not filtered)
+    int16_t offY[64][6], offC[64][6];
+    LrLds lr;
+};
+DEV void fs_copy_row_dwords(uint8_t* dst, const uint8_t* src, int n4, int t0, int nt)
+{
+    for (int q = t0; q < n4; q += nt) reinterpret_cast<uint32_t*>(dst)[q] = reinterpret_cast<const uint32_t*>(src)[q];
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_stripe(const KParams* kps, int nStripes, int runTiles, int nRuns)
+{
+    extern __shared__ __align__(16) uint8_t fs_smem[];
+    StripeLds& L = *reinterpret_cast<StripeLds*>(fs_smem);
+    const int t = threadIdx.x;
+    const int per = nStripes * nRuns;
+    const int f = blockIdx.x / per, rr = blockIdx.x - f * per;
+    const int s = rr / nRuns, run = rr - s * nRuns;
+    const KParams& k = KP(kps, f);
+    const av1r_frame_hdr& h = *k.hdr;
+    const int W = k.frame_w, H = k.frame_h;
+    const int S = 64 * s - 8;
+    if (S >= H) return;
+    const int nTiles = (W + 63) / 64;
+    const int j0 = run * runTiles, j1 = imin(nTiles, j0 + runTiles);
+    if (j0 >= j1) return;
+    const bool lfOn = h.lf_level[0] || h.lf_level[1];  // else LoopFilter::filter is skipped
+    const int limX = k.mi_cols * 4, limY = k.mi_rows * 4, climX = k.mi_cols * 2, climY = k.mi_rows * 2;
+    const DevPlane* R = k.cur.pl;
+    const int Sc = S / 2;  // (S even: -8, 56, ...)
+    for (int j = j0 - 1; j <= j1; j++) {
+        const int x0 = 64 * j, cx0 = 32 * j;
+        const int wx = x0 - 80, cwx = cx0 - 40;  // window origins
+        // ---- the reconstruction of the new columns: [x0 + 8, x0 + 72) (the first step also
+        // [x0 - 8, x0 + 8)), rows [S - 12, S + 76); outside the frame's allocation: 0
+        {
+            const int c0 = j == j0 - 1 ? 72 : 88, nc = (FS_W - 8 - c0) / 4;  // window columns c0 .. 152
+            for (int q = t; q < FS_DR * nc; q += 256) {
+                const int i = q / nc, d = q - i * nc, y = S - 12 + i, x = wx + c0 + 4 * d;
+                uint32_t v = 0;
+                if (y >= 0 && y < R[0].h + 64 && x >= 0 && x + 4 <= R[0].stride)
+                    v = *reinterpret_cast<const uint32_t*>(R[0].p + (size_t)y * R[0].stride + x);
+                *reinterpret_cast<uint32_t*>(&L.dy[i][c0 + 4 * d]) = v;
+            }
+            const int cc0 = c0 / 2, cnc = (FS_CW - 4 - cc0) / 4;  // chroma columns cc0 .. 76
+            for (int q = t; q < 2 * FS_CDR * cnc; q += 256) {
+                const int pl = q >= FS_CDR * cnc, r = q - pl * FS_CDR * cnc, i = r / cnc, d = r - i * cnc;
+                const int y = Sc - 4 + i, x = cwx + cc0 + 4 * d;
+                const DevPlane& P = R[1 + pl];
+                uint32_t v = 0;
+                if (y >= 0 && y < P.h + 32 && x >= 0 && x + 4 <= P.stride) v = *reinterpret_cast<const uint32_t*>(P.p + (size_t)y * P.stride + x);
+                *reinterpret_cast<uint32_t*>(&L.duv[pl][i][cc0 + 4 * d]) = v;
+            }
+        }
+        __syncthreads();
+        const bool inFrame = x0 < W;
+        // ---- deblocking pass 0: the vertical edges x in [x0, x0 + 64) of the window's rows
+        if (lfOn && inFrame) {
+            for (int q = t; q < 22 * 16 + 2 * 10 * 8; q += 256) {
+                int plane, xP, yP, xT, yT;
+                if (q < 22 * 16) {
+                    const int ur = q >> 4, e = q & 15;
+                    plane = 0, xP = x0 + 4 * e, yP = S - 12 + 4 * ur, xT = 80 + 4 * e, yT = 4 * ur;
+                } else {
+                    const int r2_ = q - 22 * 16, pl = r2_ / 80, r3 = r2_ - pl * 80, ur = r3 >> 3, e = r3 & 7;
+                    plane = 1 + pl, xP = cx0 + 4 * e, yP = Sc - 4 + 4 * ur, xT = 40 + 4 * e, yT = 4 * ur;
+                }
+                LfEdge e;
+                if (yP < 0 || !lf_edge(k, plane, 0, xP, yP, e)) continue;
+                const LfLdsPx P{(lf_lds_u8*)(plane ? &L.duv[plane - 1][0][0] : &L.dy[0][0]), plane ? FS_CW : FS_W};
+                lf_unit(P, plane, 0, xT, yT, e);
+            }
+        }
+        __syncthreads();
+        // ---- pass 1: the horizontal edges y in [S - 4, S + 68] on columns [x0 - 8, x0 + 56)
+        // (chroma: edges [S/2, S/2 + 32] on [cx0 - 4, cx0 + 28))
+        if (lfOn && x0 - 8 < W) {
+            for (int q = t; q < 19 * 16 + 2 * 9 * 8; q += 256) {
+                int plane, xP, yP, xT, yT;
+                if (q < 19 * 16) {
+                    const int er = q >> 4, u = q & 15;
+                    plane = 0, xP = x0 - 8 + 4 * u, yP = S - 4 + 4 * er, xT = 72 + 4 * u, yT = 8 + 4 * er;
+                } else {
+                    const int r2_ = q - 19 * 16, pl = r2_ / 72, r3 = r2_ - pl * 72, er = r3 >> 3, u = r3 & 7;
+                    plane = 1 + pl, xP = cx0 - 4 + 4 * u, yP = Sc + 4 * er, xT = 36 + 4 * u, yT = 4 + 4 * er;
+                }
+                LfEdge e;
+                if (xP < 0 || yP < 0 || !lf_edge(k, plane, 1, xP, yP, e)) continue;
+                const LfLdsPx P{(lf_lds_u8*)(plane ? &L.duv[plane - 1][0][0] : &L.dy[0][0]), plane ? FS_CW : FS_W};
+                lf_unit(P, plane, 1, xT, yT, e);
+            }
+        }
+        __syncthreads();
+        // ---- CDEF of the 8x8 blocks of columns [x0 - 16, x0 + 48), rows [S, S + 64) (cdef_body
+        // per block: its 64x64 region's cdef_idx, its skip test, direction, filter)
+        const int bx0 = x0 - 16;
+        if (bx0 < limX && j >= j0 - 1) {
+            if (t < 64) {
+                const int by = t >> 3, bxi = t & 7;
+                const int yb = S + 8 * by, xb = bx0 + 8 * bxi;
+                int idx = -1, fb = 0;
+                if (yb >= 0 && yb < limY && xb >= 0 && xb < limX) {
+                    const int mr = yb >> 2, mc = xb >> 2;
+                    idx = k.cdef_idx[(mr >> 4) * h.cdef_cols + (mc >> 4)];
+                    fb = !((mi_at(k, mr, mc).flags & AV1R_MI_SKIP) && (mi_at(k, mr + 1, mc).flags & AV1R_MI_SKIP) &&
+                           (mi_at(k, mr, mc + 1).flags & AV1R_MI_SKIP) && (mi_at(k, mr + 1, mc + 1).flags & AV1R_MI_SKIP));
+                }
+                L.idx[t] = (int8_t)idx;
+                L.filt[t] = (uint8_t)(idx != -1 && fb);
+            }
+            __syncthreads();
+            {  // direction costs: wave w directions 2w, 2w + 1; lane = block
+                const int b = t & 63, w = t >> 6;
+                if (L.filt[b]) {
+                    const int c = 64 + 8 * (b & 7), r = 12 + 8 * (b >> 3);  // window position (deblocked rows from S - 12)
+                    uint32_t rw[8][2];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const uint2 v = *reinterpret_cast<const uint2*>(&L.dy[r + i][c]);
+                        rw[i][0] = v.x;
+                        rw[i][1] = v.y;
+                    }
+                    auto px8 = [&](int i, int jj) { return (int)((rw[i][jj >> 2] >> (8 * (jj & 3))) & 0xff) - 128; };
+                    int c0_, c1_;
+                    switch (__builtin_amdgcn_readfirstlane(w)) {
+                    case 0: c0_ = cdef_cost_f<0>(px8), c1_ = cdef_cost_f<1>(px8); break;
+                    case 1: c0_ = cdef_cost_f<2>(px8), c1_ = cdef_cost_f<3>(px8); break;
+                    case 2: c0_ = cdef_cost_f<4>(px8), c1_ = cdef_cost_f<5>(px8); break;
+                    default: c0_ = cdef_cost_f<6>(px8), c1_ = cdef_cost_f<7>(px8); break;
+                    }
+                    L.cost[b][2 * w] = c0_;
+                    L.cost[b][2 * w + 1] = c1_;
+                }
+            }
+            __syncthreads();
+            if (t < 64 && L.filt[t]) {
+                const int idx = L.idx[t];
+                int best = 0, yDir = 0;
+                for (int d = 0; d < 8; d++)
+                    if (L.cost[t][d] > best) {
+                        best = L.cost[t][d];
+                        yDir = d;
+                    }
+                const int var = (best - L.cost[t][(yDir + 4) & 7]) >> 10;
+                const int priStr = h.cdef_y_pri[idx];
+                const int varStr = (var >> 6) ? imin(floor_log2(var >> 6), 12) : 0;
+                L.pri[t] = (int16_t)(var ? (priStr * (4 + varStr) + 8) >> 4 : 0);
+                const int dy0 = priStr == 0 ? 0 : yDir, dc0 = h.cdef_uv_pri[idx] == 0 ? 0 : av1r_cdef_uv_dir420[yDir];
+#pragma unroll
+                for (int ss = 0; ss < 3; ss++)
+#pragma unroll
+                    for (int kk = 0; kk < 2; kk++) {
+                        const int dl = ss == 0 ? dy0 : ((dy0 + (ss == 1 ? -2 : 2)) & 7);
+                        const int dc = ss == 0 ? dc0 : ((dc0 + (ss == 1 ? -2 : 2)) & 7);
+                        L.offY[t][ss * 2 + kk] = (int16_t)(av1r_cdef_directions[dl][kk][0] * FS_W + av1r_cdef_directions[dl][kk][1]);
+                        L.offC[t][ss * 2 + kk] = (int16_t)(av1r_cdef_directions[dc][kk][0] * FS_CW + av1r_cdef_directions[dc][kk][1]);
+                    }
+            }
+            __syncthreads();
+            // luma: 64 rows x 16 four-pixel groups = 1024 groups, 4 per lane; a group's block is
+            // (row >> 3, group >> 1)
+            for (int q = t; q < 1024; q += 256) {
+                const int i = q >> 4, g = q & 15, b = (i >> 3) * 8 + (g >> 1);
+                const int y = S + i, x = bx0 + 4 * g;
+                if (y < 0 || y >= limY || x >= limX || x < 0) continue;
+                const int p = (12 + i) * FS_W + 64 + 4 * g;
+                uint32_t o;
+                if (!L.filt[b]) o = *reinterpret_cast<const uint32_t*>(&L.dy[0][0] + p);
+                else o = cdef_quad<true>(&L.dy[0][0], p, L.offY[b], L.pri[b], h.cdef_y_sec[L.idx[b]], h.cdef_damping, x, y, FS_W, limX, limY);
+                *reinterpret_cast<uint32_t*>(&L.cy[i][64 + 4 * g]) = o;
+            }
+            // chroma: 2 planes x 32 rows x 8 groups (a 4x4 block per group column, its luma block's
+            // direction and strengths)
+            for (int q = t; q < 512; q += 256) {
+                const int pl = q >> 8, r = q & 255, i = r >> 3, g = r & 7, b = (i >> 2) * 8 + g;
+                const int y = Sc + i, x = bx0 / 2 + 4 * g;
+                if (y < 0 || y >= climY || x >= climX || x < 0) continue;
+                const uint8_t* tile = &L.duv[pl][0][0];
+                const int p = (4 + i) * FS_CW + 32 + 4 * g;
+                uint32_t o;
+                if (!L.filt[b]) {
+                    o = *reinterpret_cast<const uint32_t*>(tile + p);
+                } else {
+                    const int idx = L.idx[b];
+                    o = cdef_quad<true>(tile, p, L.offC[b], h.cdef_uv_pri[idx], h.cdef_uv_sec[idx], h.cdef_damping - 1, x, y, FS_CW,
+                        climX, climY);
+                }
+                *reinterpret_cast<uint32_t*>(&L.cuv[pl][i][32 + 4 * g]) = o;
+            }
+        }
+        __syncthreads();
+        // ---- LR (or the CDEF output as it is) of tile j - 1: columns [x0 - 64, x0)
+        if (j - 1 >= j0) {
+            const int lx0 = x0 - 64;
+#pragma unroll 1
+            for (int part = 0; part < 4; part++) {  // luma rows [S, S + 32), [S + 32, S + 64); U; V
+                const int plane = part < 2 ? 0 : part - 1, sub = plane ? 1 : 0;
+                const DevPlane O = h.uses_lr ? k.lrout.pl[plane] : k.cdef.pl[plane];
+                const int pw = O.w, ph = O.h;
+                const int tx0 = lx0 >> sub, tw = imin(64 >> sub, pw - tx0);
+                const int start = plane ? Sc : S, end = start + (64 >> sub);
+                const int ty0 = imax(0, plane ? start : start + 32 * part), ty1 = imin(plane ? end : start + 32 * (part + 1), ph);
+                if (tw <= 0 || ty0 >= ty1) continue;
+                const int th = ty1 - ty0;
+                const uint8_t* cw_ = plane ? &L.cuv[plane - 1][0][0] : &L.cy[0][0];
+                const uint8_t* dw_ = plane ? &L.duv[plane - 1][0][0] : &L.dy[0][0];
+                const int ws = plane ? FS_CW : FS_W, wox = plane ? cwx : wx;
+                const int dRow0 = plane ? Sc - 4 : S - 12;  // the deblocked window's first row
+                if (!h.uses_lr || h.lr_type[plane] == AV1R_RESTORE_NONE) {
+                    for (int q = t; q < th * tw; q += 256) {
+                        const int r = q / tw, c = q - r * tw;
+                        O.p[(size_t)(ty0 + r) * O.stride + tx0 + c] = cw_[(ty0 + r - start) * ws + tx0 + c - wox];
+                    }
+                    continue;
+                }
+                // stage L.src: rows ty0 - 3 .. ty1 + 2, columns tx0 - 4 .. tx0 + 67 (get_source_sample:
+                // CDEF rows inside the stripe, deblocked rows S - 2, S - 1 / end, end + 1 outside;
+                // coordinates clamped to the plane)
+                for (int q = t; q < (th + 6) * LR_SW; q += 256) {
+                    const int i = q / LR_SW, jj = q - i * LR_SW;
+                    int y = ty0 - 3 + i;
+                    const bool pre = y < start || y >= end;
+                    if (y < start) y = imax(start - 2, y);
+                    else if (y >= end) y = imin(end + 1, y);
+                    y = CLIP3(0, ph - 1, y);
+                    const int x = CLIP3(0, pw - 1, tx0 - 4 + jj) - wox;
+                    L.lr.src[i][jj] = pre ? dw_[(y - dRow0) * ws + x] : cw_[(y - start) * ws + x];
+                }
+                const int us = h.lr_unit_size[plane], rows = h.lr_unit_rows[plane], cols = h.lr_unit_cols[plane];
+                const int off = 8 >> sub;
+                const int ur = imin((ty0 + off) / us, rows - 1);
+                const int uc0 = imin(tx0 / us, cols - 1);
+                const int nU = imin((tx0 + tw - 1) / us, cols - 1) - uc0 + 1;
+                if (t < nU) L.lr.unit[t] = k.lr[h.lr_unit_off[plane] + ur * cols + uc0 + t];
+                __syncthreads();
+                lr_filter_tile(L.lr, h, plane, tx0, tw, ty0, th, imax(start, 0), us, cols, uc0, nU, r2(k.frame_w, sub),
+                    r2(k.frame_h, sub), O);
+                __syncthreads();
+            }
+        }
+        // ---- the windows move by one tile: columns [64, 160) -> [0, 96) (chroma [32, 80) -> [0, 48))
+        {
+            constexpr int NL = FS_DR * 24 + 64 * 24, NC = 2 * (FS_CDR * 12 + 32 * 12);  // dwords
+            uint32_t v[(NL + NC + 255) / 256];
+#pragma unroll
+            for (int u = 0; u < (NL + NC + 255) / 256; u++) {
+                const int q = t + 256 * u;
+                uint32_t* src = nullptr;
+                if (q < FS_DR * 24) src = reinterpret_cast<uint32_t*>(&L.dy[q / 24][64 + 4 * (q % 24)]);
+                else if (q < NL) { const int r = q - FS_DR * 24; src = reinterpret_cast<uint32_t*>(&L.cy[r / 24][64 + 4 * (r % 24)]); }
+                else if (q < NL + NC) {
+                    int r = q - NL;
+                    const int pl = r / (FS_CDR * 12 + 32 * 12);
+                    r -= pl * (FS_CDR * 12 + 32 * 12);
+                    src = r < FS_CDR * 12 ? reinterpret_cast<uint32_t*>(&L.duv[pl][r / 12][32 + 4 * (r % 12)])
+                                          : reinterpret_cast<uint32_t*>(&L.cuv[pl][(r - FS_CDR * 12) / 12][32 + 4 * ((r - FS_CDR * 12) % 12)]);
+                }
+                v[u] = src ? *src : 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < (NL + NC + 255) / 256; u++) {
+                const int q = t + 256 * u;
+                uint32_t* dst = nullptr;
+                if (q < FS_DR * 24) dst = reinterpret_cast<uint32_t*>(&L.dy[q / 24][4 * (q % 24)]);
+                else if (q < NL) { const int r = q - FS_DR * 24; dst = reinterpret_cast<uint32_t*>(&L.cy[r / 24][4 * (r % 24)]); }
+                else if (q < NL + NC) {
+                    int r = q - NL;
+                    const int pl = r / (FS_CDR * 12 + 32 * 12);
+                    r -= pl * (FS_CDR * 12 + 32 * 12);
+                    dst = r < FS_CDR * 12 ? reinterpret_cast<uint32_t*>(&L.duv[pl][r / 12][4 * (r % 12)])
+                                          : reinterpret_cast<uint32_t*>(&L.cuv[pl][(r - FS_CDR * 12) / 12][4 * ((r - FS_CDR * 12) % 12)]);
+                }
+                if (dst) *dst = v[u];
+            }
+            __syncthreads();
+        }
+    }
+}
+void launch_k_stripe(const KParams* kps, int n, int maxW, int maxH, int runTiles, hipStream_t s)
+{
+    const int nStripes = (maxH + 8 + 63) / 64, nTiles = (maxW + 63) / 64;
+    const int nRuns = (nTiles + runTiles - 1) / runTiles;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_stripe), hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StripeLds));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_stripe, dim3(n * nStripes * nRuns), dim3(256), sizeof(StripeLds), s, kps, nStripes, runTiles, nRuns);
+}
+#endif  // AV1R_FUSED_STRIPE
+
+// ------------------------------------------------------------------------------------
 // launches over n frames: grid row / slice per frame, sized for the largest
 void launch_k_lf(const KParams* kps, int n, int pass, int maxUnits, hipStream_t s)
 {
