@@ -2377,7 +2377,7 @@ DEV void tiny_run(const KParams& k, uint32_t pos0, uint32_t nIt, TinyLds* T, uin
 // workgroup), n | FLOW_G_TINY: n tiny items (four per wave, tiny_run), else n >= 1 small
 // items (wave w runs items w, w + 4, ..)
 #ifndef AV1R_FLOW_WAVES
-#define AV1R_FLOW_WAVES 5  // resident 256-lane workgroups per CU: 5 = 95 VGPRs + 64 B/lane scratch (4 = 121 VGPRs: k_flow +2.4 %; 6 = no better; 8 = 64 VGPRs + spills: 4K recon +3 %, profiles/r05_ab_flow_waves8.txt)
+#define AV1R_FLOW_WAVES 6  // resident 256-lane workgroups per CU: 6 = 80 VGPRs (round 6, with the tiny path: k_flow -2.4 %, profiles/r06_ab_flow_waves6.txt); 5 = 95 VGPRs; 4 = 121 VGPRs: +2.4 %; 8 = 64 VGPRs + spills: 4K recon +3 %, profiles/r05_ab_flow_waves8.txt
 #endif
 #ifdef AV1R_FLOW_DEBUG
 // -DAV1R_FLOW_DEBUG: counts workgroup entries that find another launch's k_flow
