@@ -311,11 +311,13 @@ int pipe_open(av1r_ctx* const* ctxs, int n, const av1r_stream_source* src, int64
     // AV1R_PIPE_GROUPS=g: the streams form g groups whose batches go to g different HIP
     // streams (each batch runs on its first member's stream), so one group's latency-bound
     // k_flow overlaps the other groups' kernels
-    // (default: 2 groups from 8 streams up -- 8 x 1080p: 6 580-6 620 against 6 500 frames/s
-    // with one -- so a group's filters overlap the other's reconstruction; fewer streams, or
-    // frames being delivered (pipe_step): one)
-    static const int groups = getenv("AV1R_PIPE_GROUPS") ? std::max(1, atoi(getenv("AV1R_PIPE_GROUPS"))) : 0;
-    P->G = std::min(groups ? groups : (n >= 8 ? 2 : 1), n);
+    // (default: one group.  Round 4 measured two groups from 8 streams faster -- 6 580-6 620
+    // against 6 500 frames/s -- so a group's filters overlapped the other's reconstruction;
+    // with round 6's kernels one group, launching all 8 streams' frames together as the
+    // device-only leg does, is faster: 7 191-7 412 against 6 996-7 125 frames/s, 4 runs each,
+    // profiles/r06_ab_pipe_groups.txt)
+    static const int groups = getenv("AV1R_PIPE_GROUPS") ? std::max(1, atoi(getenv("AV1R_PIPE_GROUPS"))) : 1;
+    P->G = std::min(groups, n);
     P->th.reserve(W);
     for (int w = 0; w < W; w++) P->th.emplace_back(worker, &R);
     *out = P;
