@@ -105,7 +105,7 @@ struct Prepared {
     std::vector<Level> levels;
     bool flowOk = false;  // k_flow can run it: no inter tile after level 0 (intra block copy)
     bool levelsOk = true; // the level launches can run it (false: a flow-only schedule)
-    uint32_t nResidS = 0, nResidL = 0;  // k_resid workgroups (16 TBs / 1 TB each)
+    uint32_t nResidS = 0, nResidL = 0;  // k_resid workgroups (64 4x4 TBs or 16 TBs / 1 TB each)
     size_t resElems = 0;                // int16 residual tiles of the frame
     bool usedRef[8] = {};
     uint64_t bytes = 0;    // the packed layout (incl. the device-filled mode-info grid)
@@ -244,7 +244,8 @@ struct av1r_ctx {
     size_t granCap = 0;  // bytes
     // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
     // the small and large TB lists, the tiles' total size
-    std::vector<uint32_t> tbRes, residS, residL;
+    std::vector<uint32_t> tbRes, residS, residL, residT;
+    uint32_t nResidT = 0;  // k_resid_s workgroups of 4x4 TBs (the head of residS)
     size_t resElems = 0;
     // split submission (frame_begin / submit_tile / frame_end)
     bool inFrame = false;
@@ -1398,8 +1399,11 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     // k_resid: residual tiles for intra TBs and the TBs of inter-intra blocks; the other
     // inter TBs are added in place
     c->tbRes.assign(b->n_tbs, ~0u);
+    // (k_resid_s's list: the 4x4 TBs first, 64 per workgroup at 4 lanes each -- half the
+    // TBs with coefficients --, then the others up to 16x16, 16 per workgroup at 16 lanes)
     c->residS.clear();
     c->residL.clear();
+    c->residT.clear();
     c->resElems = 0;
     for (uint32_t ti = 0; ti < b->n_tbs; ti++) {
         const av1r_tb& t = b->tbs[ti];
@@ -1410,9 +1414,12 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->tbRes[ti] = (uint32_t)c->resElems;
             c->resElems += (size_t)w * hh;
         }
-        (w <= 16 && hh <= 16 ? c->residS : c->residL).push_back(ti);
+        (t.tx_size == AV1R_TX_4X4 ? c->residT : w <= 16 && hh <= 16 ? c->residS : c->residL).push_back(ti);
     }
+    while (c->residT.size() % 64) c->residT.push_back(~0u);
     while (c->residS.size() % 16) c->residS.push_back(~0u);
+    c->nResidT = (uint32_t)(c->residT.size() / 64);
+    c->residS.insert(c->residS.begin(), c->residT.begin(), c->residT.end());
     // k_flow: dependency lists as item positions (every dependency is an earlier item: it
     // has a lower level); inter tiles after level 0 (intra block copy) keep the frame on
     // the level launches
@@ -1651,6 +1658,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     P.upBytes = off;  // everything up to here travels; what follows is filled on the device
     k.done = (uint32_t*)put(nullptr, 0, szDone, 0, false);
     k.n_items = (uint32_t)c->items.size();
+    k.n_resid_t = c->nResidT;
     k.mi = (const av1r_mi*)put(nullptr, 0, szMi, 0, false);
     if (verify) {
         // every section placed, in order, inside the buffer (a section left out of the
@@ -1672,7 +1680,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
         k.gran_w[p] = c->mapW[p];
         k.gran_hn[p] = c->mapH[p];
     }
-    P.nResidS = (uint32_t)(c->residS.size() / 16);
+    P.nResidS = c->nResidT + (uint32_t)((c->residS.size() - 64 * c->nResidT) / 16);
     P.nResidL = (uint32_t)c->residL.size();
     P.resElems = c->resElems;
     k.mi_stride = h->mi_stride;
@@ -1857,7 +1865,13 @@ static double now_us()
 
 static bool deep_frame(const Prepared& P);
 
-static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
+// pro: the stream that runs the batch prologue (k_fetch, k_mi), or nullptr for lc's own.
+// The packed batches pass their upload stream: the prologue then follows the batch's uploads
+// on it and overlaps the stream's previous batch (its filters), and the launch stream waits
+// for it once, where it waited for the uploads (av1r_decode_packed_batch).  Only for buffers
+// no earlier launch may still use: the packed path's upload ring slots (a prepared frame
+// decoded twice in a row would rewrite its mode-info grid under the first decode).
+static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs, hipStream_t pro = nullptr)
 {
     const double tp0 = host_prof() ? now_us() : 0;
     double tp1 = tp0, tp2 = tp0;
@@ -2028,8 +2042,24 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         }
     }
     if (host_prof()) tp2 = now_us();
-    launch_k_fetch(M.dev, M.host, need, st);
+    hipStream_t ps = pro ? pro : st;
+    launch_k_fetch(M.dev, M.host, need, ps);
     const uint32_t* dtab = reinterpret_cast<const uint32_t*>(M.dev + kBytes);
+    // the frames' KParams head the metadata buffer (read through the constant address space)
+    const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
+    {  // the frames' mode-info grids, derived on the device from their blocks and TBs
+        uint32_t maxUnits = 0, maxBlocks = 0, maxTbs = 0;
+        for (auto& j : jobs) {
+            maxUnits = std::max({maxUnits, (uint32_t)(j.k.mi_stride * j.k.mi_rows_alloc), j.k.n_items});
+            maxBlocks = std::max(maxBlocks, j.k.n_blocks);
+            maxTbs = std::max(maxTbs, j.k.n_tbs);
+        }
+        launch_k_mi(dk, n, maxUnits, maxBlocks, maxTbs, ps);
+    }
+    if (pro) {
+        HIPCHK(hipEventRecord(lc->pkReady, pro));
+        HIPCHK(hipStreamWaitEvent(st, lc->pkReady, 0));
+    }
 
     if (lc->timing) {
         if (lc->evUsed == lc->evPool.size()) {
@@ -2055,18 +2085,7 @@ static int launch_jobs(av1r_ctx* lc, std::vector<FrameJob>& jobs)
         return AV1R_OK;
     };
 
-    // ---- reconstruction, level by level (frame parameters in a constant-memory slot)
-    // the frames' KParams head the metadata buffer (read through the constant address space)
-    const KParams* dk = reinterpret_cast<const KParams*>(M.dev);
-    {  // the frames' mode-info grids, derived on the device from their blocks and TBs
-        uint32_t maxUnits = 0, maxBlocks = 0, maxTbs = 0;
-        for (auto& j : jobs) {
-            maxUnits = std::max({maxUnits, (uint32_t)(j.k.mi_stride * j.k.mi_rows_alloc), j.k.n_items});
-            maxBlocks = std::max(maxBlocks, j.k.n_blocks);
-            maxTbs = std::max(maxTbs, j.k.n_tbs);
-        }
-        launch_k_mi(dk, n, maxUnits, maxBlocks, maxTbs, st);
-    }
+    // ---- reconstruction
     size_t allItems = 0;
     for (uint32_t v : total) allItems += v;
     allItems = std::max<size_t>(allItems, frameRows);
@@ -2230,7 +2249,7 @@ static bool deep_frame(const Prepared& P)
     return P.flowOk && (int)P.levels.size() > 400;
 }
 
-static int launch_solo(FrameJob& j)
+static int launch_solo(FrameJob& j, hipStream_t pro = nullptr)
 {
     av1r_ctx* m = j.c;
     av1r_ctx* c = m;
@@ -2238,7 +2257,7 @@ static int launch_solo(FrameJob& j)
     // one k_flow workgroup per CU for a solo deep frame
     const int per = m->flowPerCU;
     m->flowPerCU = 1;
-    int rc = launch_jobs(m, one);
+    int rc = launch_jobs(m, one, pro);
     m->flowPerCU = per;
     if (rc) return rc;
     HIPCHK(hipEventRecord(m->soloDone, m->stream));
@@ -2874,7 +2893,7 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
     }
     const double s0 = g_pipeProf ? now_s() : 0;
     for (auto& j : solo) {  // first, so that their long chains start at once
-        int rc = launch_solo(j);
+        int rc = launch_solo(j, j.c->copyStream);  // (its upload went on that stream)
         if (rc) return rc;
     }
     const double s1 = g_pipeProf ? now_s() : 0;
@@ -2893,10 +2912,9 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
                 HIPCHK(hipEventRecord(j.c->sync, j.c->stream));
                 HIPCHK(hipStreamWaitEvent(bl->stream, j.c->sync, 0));
             }
-        if (copies) {
-            HIPCHK(hipEventRecord(bl->pkReady, bl->copyStream));
-            HIPCHK(hipStreamWaitEvent(bl->stream, bl->pkReady, 0));
-        }
+        // (the uploads on bl's copy stream: launch_jobs runs the prologue after them there,
+        // and bl's stream waits for that)
+        (void)copies;
         // a flow-only frame and a level-schedule frame (intra block copy) cannot share launches
         std::vector<FrameJob> lv;
         for (size_t i = 0; i < jobs.size();)
@@ -2906,8 +2924,8 @@ int av1r_decode_packed_batch(av1r_ctx* const* ctxs, av1r_packed* const* pks, int
             } else {
                 i++;
             }
-        int rc = jobs.empty() ? AV1R_OK : launch_jobs(bl, jobs);
-        if (!rc && !lv.empty()) rc = launch_jobs(bl, lv);
+        int rc = jobs.empty() ? AV1R_OK : launch_jobs(bl, jobs, bl->copyStream);
+        if (!rc && !lv.empty()) rc = launch_jobs(bl, lv, bl->copyStream);
         if (rc) return rc;
         for (auto& j : jobs)
             if (j.c != bl) j.c->joinLead = bl;

@@ -535,31 +535,54 @@ DEV void load_window(const RefSel& R, uint8_t* win, int rx0, int ry0, int rw, in
     }
 }
 
+// The 8 taps of sub-pixel filter f (= set * 16 + phase, av1r_subpel_filters) packed for
+// the dot-product passes.  Every AV1 sub-pixel tap is even (each filter sums to 128), so the
+// horizontal pass takes them halved as signed bytes (taps 0-3 in .x, 4-7 in .y: every
+// halved tap, 64 at phase 0 included, fits), and the vertical pass as int16 pairs.
+DEV uint2 hfilt_pk(int f)
+{
+    const int16_t* c = av1r_subpel_filters + f * 8;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        lo |= (uint32_t)((c[u] >> 1) & 0xff) << (8 * u);
+        hi |= (uint32_t)((c[u + 4] >> 1) & 0xff) << (8 * u);
+    }
+    return make_uint2(lo, hi);
+}
+DEV uint4 vfilt_pk(int f)
+{
+    const int16_t* c = av1r_subpel_filters + f * 8;
+    auto pr = [&](int u) { return (uint32_t)(uint16_t)c[u] | ((uint32_t)(uint16_t)c[u + 1] << 16); };
+    return make_uint4(pr(0), pr(2), pr(4), pr(6));
+}
+typedef short sp2 __attribute__((ext_vector_type(2)));
+DEV int dot2_i16(uint32_t a, uint32_t b, int acc)
+{
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(sp2, a), __builtin_bit_cast(sp2, b), acc, false);
+}
+DEV uint32_t vf_pair(const uint4& vf, int t) { return t == 0 ? vf.x : t == 1 ? vf.y : t == 2 ? vf.z : vf.w; }
+
 // Horizontal pass of blockSubPixelPredict (InterPredict.cpp:340-362) over the (rh + 7)
 // window rows: intermediate[r][c] = Round2(sum hf[t] * ref[r][c + t - 3], R0).  Four
-// outputs per lane from three LDS dwords when rw is a multiple of 4.
+// outputs per lane from three LDS dwords when rw is a multiple of 4, each two v_dot4 of the
+// halved taps (hfilt_pk) with the pixels biased to signed bytes (p ^ 0x80 = p - 128):
+// sum hf * p = 2 * sum (hf / 2) * (p - 128) + 128 * 128.
 template <int NT = 64>
-DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* hf, int R0, int wcs = WC, int hstr = TS)
+DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, uint2 hf, int R0, int wcs = WC, int hstr = TS)
 {
     if ((rw & 3) == 0) {
         const int g4 = rw >> 2, lg = ilog2p(g4);  // (rw: a power of two)
         for (int q = il_lane<NT>(); q < (rh + 7) * g4; q += NT) {
             const int i = q >> lg, g = q & (g4 - 1);
             const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + i * wcs) + g;
-            const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2];
-            int b[12];
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-                b[m] = (d0 >> (8 * m)) & 0xff;
-                b[m + 4] = (d1 >> (8 * m)) & 0xff;
-                b[m + 8] = (d2 >> (8 * m)) & 0xff;
-            }
+            const uint32_t d0 = w32[0] ^ 0x80808080u, d1 = w32[1] ^ 0x80808080u, d2 = w32[2] ^ 0x80808080u;
             int o[4];
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                int hs = 0;
-#pragma unroll
-                for (int u = 0; u < 8; u++) hs += hf[u] * b[m + u];
+                const uint32_t a = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)m);
+                const uint32_t b = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)m);
+                const int hs = 2 * __builtin_amdgcn_sdot4((int)b, (int)hf.y, __builtin_amdgcn_sdot4((int)a, (int)hf.x, 0, false), false) + 16384;
                 o[m] = r2(hs, R0) & 0xffff;
             }
             uint2 v;
@@ -574,25 +597,28 @@ DEV void hpass(const uint8_t* win, int16_t* hb, int rw, int rh, const int16_t* h
         const uint8_t* row = win + i * wcs + j;
         int hs = 0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) hs += hf[u] * row[u];
+        for (int u = 0; u < 8; u++) hs += 2 * (int)(int8_t)((u < 4 ? hf.x : hf.y) >> (8 * (u & 3))) * row[u];
         hb[i * hstr + j] = (int16_t)r2(hs, R0);
     }
 }
 
 // The same sample as pred_direct for an unscaled, unwarped reference: the vertical pass
-// over the staged intermediate rows (or the integer-position copy from the window).
-DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer,
+// over the staged intermediate rows (or the integer-position copy from the window), the
+// taps as int16 pairs (vfilt_pk) against row pairs: four v_dot2.
+DEV int pred_win(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const uint4& vf, int integer,
     int wcs = WC, int hstr = TS)
 {
     if (integer) return (int16_t)(win[(rr + 3) * wcs + cc + 3] << (14 - R0 - R1));
     const int16_t* col = hb + rr * hstr + cc;
     int s = 0;
 #pragma unroll
-    for (int t = 0; t < 8; t++) s += vf[t] * col[t * hstr];
+    for (int t = 0; t < 4; t++)
+        s = dot2_i16((uint32_t)(uint16_t)col[2 * t * hstr] | ((uint32_t)(uint16_t)col[(2 * t + 1) * hstr] << 16), vf_pair(vf, t), s);
     return (int16_t)r2(s, R1);
 }
-// Four horizontally adjacent samples (cc a multiple of 4): 8 LDS reads of 4 int16.
-DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const int16_t* vf, int integer, int* out,
+// Four horizontally adjacent samples (cc a multiple of 4): 8 LDS reads of 4 int16, each
+// column's row pairs gathered by v_perm into v_dot2 operands.
+DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0, int R1, const uint4& vf, int integer, int* out,
     int wcs = WC, int hstr = TS)
 {
     if (integer) {
@@ -602,20 +628,19 @@ DEV void pred_win4(const uint8_t* win, const int16_t* hb, int rr, int cc, int R0
     }
     int s[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint2 v = *reinterpret_cast<const uint2*>(hb + (rr + t) * hstr + cc);
-        s[0] += vf[t] * (int16_t)(v.x & 0xffff);
-        s[1] += vf[t] * (int16_t)(v.x >> 16);
-        s[2] += vf[t] * (int16_t)(v.y & 0xffff);
-        s[3] += vf[t] * (int16_t)(v.y >> 16);
+    for (int t = 0; t < 4; t++) {
+        const uint2 a = *reinterpret_cast<const uint2*>(hb + (rr + 2 * t) * hstr + cc);
+        const uint2 b = *reinterpret_cast<const uint2*>(hb + (rr + 2 * t + 1) * hstr + cc);
+        const uint32_t f = vf_pair(vf, t);
+        s[0] = dot2_i16(__builtin_amdgcn_perm(b.x, a.x, 0x05040100u), f, s[0]);
+        s[1] = dot2_i16(__builtin_amdgcn_perm(b.x, a.x, 0x07060302u), f, s[1]);
+        s[2] = dot2_i16(__builtin_amdgcn_perm(b.y, a.y, 0x05040100u), f, s[2]);
+        s[3] = dot2_i16(__builtin_amdgcn_perm(b.y, a.y, 0x07060302u), f, s[3]);
     }
 #pragma unroll
     for (int m = 0; m < 4; m++) out[m] = (int16_t)r2(s[m], R1);
 }
 
-// blockWarp (InterPredict.cpp:507-553), split like the reference into its horizontal
-// pass -- the 15 x 8 intermediate of every 8x8 block of the region, read straight from
-// the reference plane -- and the vertical pass per output sample.
 DEV void warp_origin(const RefSel& R, int i8, int j8, int puX, int puY, int sub, int& ix4, int& sx4, int& iy4, int& sy4)
 {
     const int32_t* wp = R.wp;
@@ -819,18 +844,16 @@ DEV void predict_pu(const KParams& k, const DevBlock& blk, InterLdsT<TSZ>& L, in
     RefSel R[2];
     const int isCompound = setup_refs(k, blk, plane, x, y, w, h, candRow, candCol, R, lw);
     const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
-    int16_t hf[2][8], vf[2][8];
+    uint2 hf[2];
+    uint4 vf[2];
     int integer[2];
 #pragma unroll
     for (int l = 0; l < 2; l++) {
         if (l > isCompound) break;
         const int hph = (R[l].startX >> 6) & 15, vph = (R[l].startY >> 6) & 15;
         integer[l] = !hph && !vph;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            hf[l][u] = av1r_subpel_filters[(R[l].filtX * 16 + hph) * 8 + u];
-            vf[l][u] = av1r_subpel_filters[(R[l].filtY * 16 + vph) * 8 + u];
-        }
+        hf[l] = hfilt_pk(R[l].filtX * 16 + hph);
+        vf[l] = vfilt_pk(R[l].filtY * 16 + vph);
     }
     const int ct = blk.compound_type;
     int mode;  // 0 single reference (inter-intra: blended later by ii_item), 1 average, 2 distance, 3 mask
@@ -962,18 +985,16 @@ DEV bool predict_chroma2(const KParams& k, const DevBlock& blk, InterLds& L, int
     if (!R[0][0].useWin || (isCompound && !R[0][1].useWin)) return false;
     setup_refs(k, blk, 2, x, y, w, h, blk.mi_row, blk.mi_col, R[1], lw);
     const int R0 = 3, R1 = isCompound ? 7 : 11, PostRound = 14 - (R0 + R1);
-    int16_t hf[2][8], vf[2][8];
+    uint2 hf[2];
+    uint4 vf[2];
     int integer[2] = {1, 1};
 #pragma unroll
     for (int l = 0; l < 2; l++) {
         if (l > isCompound) break;
         const int hph = (R[0][l].startX >> 6) & 15, vph = (R[0][l].startY >> 6) & 15;
         integer[l] = !hph && !vph;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            hf[l][u] = av1r_subpel_filters[(R[0][l].filtX * 16 + hph) * 8 + u];
-            vf[l][u] = av1r_subpel_filters[(R[0][l].filtY * 16 + vph) * 8 + u];
-        }
+        hf[l] = hfilt_pk(R[0][l].filtX * 16 + hph);
+        vf[l] = vfilt_pk(R[0][l].filtY * 16 + vph);
     }
     const int ct = blk.compound_type;
     int mode;  // as predict_pu
@@ -1089,12 +1110,8 @@ DEV void obmc(const KParams& k, const DevBlock& blk, InterLdsT<TSZ>& L, int plan
                     R.useWin = R.xStep == 1024 && R.yStep == 1024;
                     const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
                     const int integer = !hph && !vph;
-                    int16_t hf[8], vf[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        hf[u] = av1r_subpel_filters[(R.filtX * 16 + hph) * 8 + u];
-                        vf[u] = av1r_subpel_filters[(R.filtY * 16 + vph) * 8 + u];
-                    }
+                    const uint2 hf = hfilt_pk(R.filtX * 16 + hph);
+                    const uint4 vf = vfilt_pk(R.filtY * 16 + vph);
                     if (R.useWin) {
                         load_window<NT, TSZ>(R, L.win[0], rx0, ry0, rw, rh, L.WCS);
                         il_sync<NT>();
@@ -1513,7 +1530,8 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int pl
     const int ct = blk.compound_type;
     const PuInfo info = pu_info(k, blk, candRow, candCol);
     const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
-    int16_t hf[2][8], vf[2][8];
+    uint2 hf[2];
+    uint4 vf[2];
     int integer[2] = {1, 1};
 #pragma unroll
     for (int l = 0; l < 2; l++) {
@@ -1523,11 +1541,8 @@ DEV void small_pu(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int pl
         const int fx = filter_idx(info.filt, w, 1), fy = filter_idx(info.filt, h, 0);
         const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
         integer[l] = !hph && !vph;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            hf[l][u] = av1r_subpel_filters[(fx * 16 + hph) * 8 + u];
-            vf[l][u] = av1r_subpel_filters[(fy * 16 + vph) * 8 + u];
-        }
+        hf[l] = hfilt_pk(fx * 16 + hph);
+        vf[l] = vfilt_pk(fy * 16 + vph);
         load_window<NT, MS>(R, L.win[l], 0, 0, w, h, MS + 8);
     }
     coop_sync<NT>();
@@ -1587,7 +1602,8 @@ DEV void small_pu_c2(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int
     const int ct = blk.compound_type;
     const PuInfo info = pu_info(k, blk, candRow, candCol);
     const int isCompound = info.ref_frame[1] > AV1R_INTRA_FRAME;
-    int16_t hf[2][8], vf[2][8];
+    uint2 hf[2];
+    uint4 vf[2];
     int integer[2] = {1, 1};
 #pragma unroll
     for (int l = 0; l < 2; l++) {
@@ -1598,11 +1614,8 @@ DEV void small_pu_c2(const KParams& k, SmallLds<MS>& L, const DevBlock& blk, int
         const int fx = filter_idx(info.filt, w, 1), fy = filter_idx(info.filt, h, 0);
         const int hph = (R.startX >> 6) & 15, vph = (R.startY >> 6) & 15;
         integer[l] = !hph && !vph;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            hf[l][u] = av1r_subpel_filters[(fx * 16 + hph) * 8 + u];
-            vf[l][u] = av1r_subpel_filters[(fy * 16 + vph) * 8 + u];
-        }
+        hf[l] = hfilt_pk(fx * 16 + hph);
+        vf[l] = vfilt_pk(fy * 16 + vph);
         load_window<NT, CS>(R, win + l * WSZ, 0, 0, w, h, WS);
         R.p = k.ref[slot].pl[2];  // V: the same extent as U
         load_window<NT, CS>(R, win + (2 + l) * WSZ, 0, 0, w, h, WS);
@@ -2513,7 +2526,8 @@ void launch_k_flow(const KParams* kps, const void* groups, uint32_t nGroups, uin
 // dependencies at all.  An inter TB outside an inter-intra block is added to its
 // prediction in the frame right here (TransformBlock.cpp:2440-2456); every other residual
 // is stored as an int16 tile for the k_flow item (intra TB, inter-intra blend) that adds
-// it.  k_resid_s: 16 TBs with sides <= 16 per 256-lane workgroup, 16 lanes each;
+// it.  k_resid_s: 64 4x4 TBs (4 lanes each) or 16 other TBs with sides <= 16 (16 lanes
+// each) per 256-lane workgroup;
 // k_resid_l: one larger TB per 64-lane workgroup.  tab: [prefix of the frames' workgroup
 // counts (n + 1)].
 // ---------------------------------------------------------------------------------
@@ -2539,17 +2553,29 @@ DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
     }
 }
 
+// (a frame's first n_resid_t workgroups take 64 4x4 TBs at 4 lanes each: with 16 lanes a
+// 4x4 TB -- half the TBs with coefficients -- left 12 idle through both passes)
 extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
-    __shared__ __align__(16) int16_t res[16][16 * 18];
+    __shared__ __align__(16) union {
+        int16_t s[16][16 * 18];
+        int16_t t[64][4 * 6];
+    } res;
     const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     const KParams& k = KP(kps, s);
+    const uint32_t bl = b - tab[s], nt = k.n_resid_t;
+    if (bl < nt) {
+        const int g = threadIdx.x >> 2;
+        const uint32_t ti = k.resid_s[bl * 64 + g];
+        if (ti != ~0u) resid_one<4, 4>(k, ti, res.t[g]);
+        return;
+    }
     const int g = threadIdx.x >> 4;
-    const uint32_t ti = k.resid_s[(b - tab[s]) * 16 + g];
-    if (ti != ~0u) resid_one<16, 16>(k, ti, res[g]);
+    const uint32_t ti = k.resid_s[nt * 64 + (bl - nt) * 16 + g];
+    if (ti != ~0u) resid_one<16, 16>(k, ti, res.s[g]);
 }
 
 extern "C" __global__ __launch_bounds__(64) void k_resid_l(const KParams* kps, const uint32_t* __restrict__ tab, int n)
