@@ -469,6 +469,14 @@ static FrameBuf* frame_get(av1r_ctx* c, int width, int height)
 // ------------------------------------------------------------------------------------
 // batch validation: everything a kernel dereferences is checked here
 // ------------------------------------------------------------------------------------
+// KParams' section pointers in their packing order (pack_frame).  The packed path keeps
+// them as offsets into the frame's buffer and rebases every one at launch (job_begin): one
+// list for the packing check and the rebase, so that no section is placed and left
+// unrebased (round 6: a residual-tile section added to the packing and not to the rebase
+// faulted on the device)
+#define AV1R_KP_SECTIONS(X) X(hdr) X(blocks) X(bext) X(tbs) X(coefs) X(coefs16) X(palette) X(cdef_idx) X(lr) X(items) \
+    X(tiles) X(deps) X(tb_res) X(resid_s) X(resid_l) X(done) X(mi)
+
 static int validate(av1r_ctx* c, const av1r_frame_batch* b)
 {
     const av1r_frame_hdr* h = b->hdr;
@@ -1640,6 +1648,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
         // the items' coefficient references follow their TBs' (offset and width)
         WorkItem* wi = reinterpret_cast<WorkItem*>(host + off);
         P.dItems = (const WorkItem*)put(c->items.data(), sizeof(WorkItem) * c->items.size(), szItems);
+        k.items = P.dItems;
         for (size_t i = 0; c->anyWide && i < c->items.size(); i++) {
             const uint32_t code = wi[i].code;
             if (AV1R_ITEM_KIND(code) != AV1R_ITEM_TB) continue;
@@ -1663,8 +1672,9 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     if (verify) {
         // every section placed, in order, inside the buffer (a section left out of the
         // packing sequence keeps the null of the memset: below the header's successors)
-        const void* secs[] = {k.hdr, k.blocks, k.bext, k.tbs, k.coefs, k.coefs16, k.palette, k.cdef_idx, k.lr, P.dItems,
-                              k.tiles, k.deps, k.tb_res, k.resid_s, k.resid_l, k.done, k.mi};
+#define KP_SEC(f) (const void*)k.f,
+        const void* secs[] = {AV1R_KP_SECTIONS(KP_SEC)};
+#undef KP_SEC
         const uint8_t* prev = dev;
         for (size_t i = 0; i < sizeof(secs) / sizeof(secs[0]); i++) {
             const uint8_t* q = (const uint8_t*)secs[i];
@@ -1736,8 +1746,9 @@ static int job_begin(FrameJob& j)
         auto rb = [&](auto& ptr) {
             ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(j.dev + reinterpret_cast<uintptr_t>(ptr));
         };
-        rb(j.k.hdr), rb(j.k.mi), rb(j.k.blocks), rb(j.k.bext), rb(j.k.tbs), rb(j.k.coefs), rb(j.k.coefs16), rb(j.k.palette), rb(j.k.cdef_idx);
-        rb(j.k.lr), rb(j.k.items), rb(j.k.tiles), rb(j.k.deps), rb(j.k.done), rb(j.k.tb_res), rb(j.k.resid_s), rb(j.k.resid_l);
+#define KP_RB(f) rb(j.k.f);
+        AV1R_KP_SECTIONS(KP_RB)
+#undef KP_RB
     }
     for (int s = 0; s < 8; s++)
         if (c->slots[s]) j.k.ref[s] = c->slots[s]->d;
