@@ -1802,7 +1802,7 @@ extern "C" __global__ K_INTER_BOUNDS void k_inter_all(const KParams* kps, const 
 // progresses whatever the residency or placement.  Several overlapping k_flow grids (from
 // different streams) cannot starve each other either: they never wait on one another, so
 // while the chip holds >= 8 workgroups of some grid that grid finishes and frees its
-// slots (1280 slots at 5 per CU: up to 160 overlapping grids).
+// slots (1536 slots at 6 per CU: up to 192 overlapping grids).
 //
 // Hand-off between items (cdna_hip_programming.md §6 Guideline 16, R1): a producer stores
 // its pixels write-through (stp/stp4<true>: sc1), every storing wave drains them
