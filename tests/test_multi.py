@@ -233,3 +233,59 @@ def test_gpu_all_64_configs4_streams_match_oracle():
             for j, r in enumerate(ref):
                 assert got[j] == r.result(), f"stream {ids[j]} (rank {rank} shard)"
     assert seen == set(range(64))
+
+
+GOLDEN_GOP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs4_gop_md5.json")
+
+
+def test_configs4_gop_golden_covers_every_stream():
+    """The whole-GOP fixture (tests/golden/make_configs4_gop.py, CPU oracle) holds the 64
+    streams of configs[4], 60 output frames each, and its streams' first frames agree with
+    the oracle run here on stream 0 (a spot check of the generator)."""
+    import json
+    g = json.load(open(GOLDEN_GOP))
+    assert g["streams"] == 64 and g["frames"] == 60
+    assert sorted(int(k) for k in g["md5"]) == list(range(64))
+    assert all(len(v) == 60 and len(set(v)) > 1 for v in g["md5"].values())
+    # different seeds, different pictures
+    assert len({v[0] for v in g["md5"].values()}) == 64
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gpu_configs4_whole_gop_matches_golden():
+    """BASELINE configs[4] over a whole GOP: the 64 streams as the 8 ranks' shards
+    (bench.rank_streams(r, 8), 60 frames each: the key frame and all 59 inter frames, so
+    every frame's references are the GPU's own earlier outputs), decoded one shard after
+    another on this GPU through the bench's native pipeline; every output frame's hash equals
+    the CPU oracle's (tests/golden/configs4_gop_md5.json, made by make_configs4_gop.py)."""
+    import hashlib
+    import json
+    from concurrent.futures import ThreadPoolExecutor
+    from av1dec_amd import Decoder
+    from av1dec_amd.pipeline import run_native
+
+    g = json.load(open(GOLDEN_GOP))["md5"]
+    S, F, world = 8, 60, 8
+
+    def h(planes):
+        return hashlib.md5(b"".join(hashlib.md5(p.tobytes()).digest() for p in planes)).hexdigest()
+
+    with ThreadPoolExecutor(16) as ex:
+        for rank in range(world):
+            ids = bench.rank_stream_ids(rank, S)
+            streams = bench.rank_streams("1080p", rank, S, F)
+            decs = [Decoder(0, keep_stages=False) for _ in range(S)]
+            try:
+                st = run_native(decs, "cycle", streams, [0] * S, max_frames=F)
+                assert st["frames"] == S * F
+                for j, d in enumerate(decs):
+                    outs = []
+                    while d.output_pending():
+                        outs.append(d.get_output())
+                    got = list(ex.map(h, outs))
+                    assert got == g[str(ids[j])], f"stream {ids[j]} (rank {rank} shard)"
+            finally:
+                for d in decs:
+                    d.close()
+            print(f"configs[4] GOP: rank {rank} shard ({S} streams x {F} frames) equal", flush=True)
