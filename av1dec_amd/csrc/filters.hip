@@ -361,7 +361,11 @@ DEV void lf_unit(const PX& P, int plane, int pass, int xP, int yP, const LfEdge&
                 __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi[r]), __builtin_bit_cast(uint32_t, lo[r]), 0x06040200u));
 }
 
-// one lane per (plane, 4x4 unit) edge of pass `pass`
+// one lane per (plane, 4x4 unit) edge of pass `pass`: the decision; then (AV1R_LF_COMPACT)
+// the units that filter, packed in order to the workgroup's first lanes, one per lane
+#ifndef AV1R_LF_COMPACT
+#define AV1R_LF_COMPACT 1
+#endif
 DEV void lf_body(const KParams* kps, int pass)
 {
     // (each XCD a contiguous eighth of the whole launch, i.e. about one frame; round 5: an
@@ -369,11 +373,12 @@ DEV void lf_body(const KParams* kps, int pass)
     const uint3 wg = xcd_block();
     const KParams& k = KP(kps, wg.y);  // frame of this launch row
     const av1r_frame_hdr& hd = *k.hdr;
-    if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped
+    if (!(hd.lf_level[0] || hd.lf_level[1])) return;  // LoopFilter::filter is skipped (the whole workgroup)
     const int nY = k.mi_rows * k.mi_cols;
     const int cCols = (k.mi_cols + 1) / 2, nC = ((k.mi_rows + 1) / 2) * cCols;
     int id = wg.x * blockDim.x + threadIdx.x;
-    int plane, row0, col0;
+    int plane = 0, row0 = 0, col0 = 0;
+    bool valid = true;
     if (id < nY) {
         plane = 0;
         row0 = id / k.mi_cols;
@@ -386,7 +391,7 @@ DEV void lf_body(const KParams* kps, int pass)
         row0 = r * 2;
         col0 = (u - r * cCols) * 2;
     } else {
-        return;
+        valid = false;
     }
     const int sub = plane ? 1 : 0;
     const int xP = (col0 * 4) >> sub, yP = (row0 * 4) >> sub;
@@ -396,9 +401,45 @@ DEV void lf_body(const KParams* kps, int pass)
     // the unit's samples loaded speculatively with the mode info, before the decision:
     // 0.0119 against 0.0105, profiles/r05_ab_lf_spec.txt -- most units filter nothing)
     LfEdge e;
-    if (!lf_edge(k, plane, pass, xP, yP, e)) return;
+    const bool on = valid && lf_edge(k, plane, pass, xP, yP, e);
+#if AV1R_LF_COMPACT
+    // Round 6: most units filter nothing, and a wave whose few filtering lanes ran the filter
+    // paid for all 64.  The filtering units of the workgroup go, in unit order (ballot +
+    // per-wave prefix: rows stay contiguous for the pixel loads), to its first lanes.  A
+    // pass's edges are independent -- a filter's length is bounded by the transform sizes on
+    // both sides, so no edge of the pass reads or writes inside another's footprint -- so
+    // the lane an edge lands on does not matter.
+    __shared__ uint2 lst[256];
+    __shared__ uint32_t wcnt[4];
+    const uint64_t bal = __ballot(on);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < w; i++) base += wcnt[i];
+    const uint32_t total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (on) {
+        const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        lst[pos] = make_uint2((uint32_t)xP | ((uint32_t)yP << 16),
+            (uint32_t)plane | ((uint32_t)e.filterSize << 2) | ((uint32_t)e.limit << 8) | ((uint32_t)e.blimit << 16) |
+                ((uint32_t)e.thresh << 24));
+    }
+    __syncthreads();
+    if (threadIdx.x >= total) return;
+    const uint2 c = lst[threadIdx.x];
+    LfEdge f;
+    const int pl = (int)(c.y & 3);
+    f.filterSize = (int)((c.y >> 2) & 31);
+    f.limit = (int)((c.y >> 8) & 255);
+    f.blimit = (int)((c.y >> 16) & 255);
+    f.thresh = (int)(c.y >> 24);
+    const DevPlane& P = k.cur.pl[pl];
+    lf_unit(LfGlobalPx{P.p, P.stride}, pl, pass, (int)(c.x & 0xffff), (int)(c.x >> 16), f);
+#else
+    if (!on) return;
     const DevPlane& P = k.cur.pl[plane];
     lf_unit(LfGlobalPx{P.p, P.stride}, plane, pass, xP, yP, e);
+#endif
 }
 // (forcing 6 waves per SIMD -- at most 80 VGPRs, 12 bytes of scratch -- measured no faster)
 extern "C" __global__ __launch_bounds__(256) void k_lf(const KParams* kps, int pass) { lf_body(kps, pass); }
