@@ -199,7 +199,7 @@ struct KParams {
     // TB outside an inter-intra block: k_resid adds it into the frame directly)
     const uint32_t* tb_res;
     int16_t* res;
-    const uint32_t* resid_s;  // TBs with coefficients and sides <= 16: n_resid_t workgroups of 64 4x4 TBs, then 16 per workgroup (~0u pads)
+    const uint32_t* resid_s;  // TBs with coefficients and sides <= 16: n_resid_t workgroups of 64 4x4 TBs, n_resid_e of 32 TBs <= 8x8, then 16 per workgroup (~0u pads)
     const uint32_t* resid_l;  // the larger ones
     // k_flow edge granules (cdna_hip_programming.md §6 Guideline 16 R2: the data is the
     // flag).  Per plane and 4x4 unit, the unit's bottom row (gran_h[row * gw + col]) and
@@ -213,6 +213,7 @@ struct KParams {
     int fi;  // k_flow: small intra TBs take the lean path (intra_fast.h; AV1R_FI=0: off)
     uint32_t n_items;
     uint32_t n_resid_t;     // k_resid_s: workgroups of 4x4 TBs heading resid_s
+    uint32_t n_resid_e;     // k_resid_s: then workgroups of 32 TBs with both sides <= 8
     uint32_t trace_base;    // -DAV1R_TRACE, k_flow mode: this frame's first timeline row
     int mi_stride;
     int mi_cols, mi_rows;

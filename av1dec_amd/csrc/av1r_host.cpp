@@ -244,8 +244,9 @@ struct av1r_ctx {
     size_t granCap = 0;  // bytes
     // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
     // the small and large TB lists, the tiles' total size
-    std::vector<uint32_t> tbRes, residS, residL, residT;
+    std::vector<uint32_t> tbRes, residS, residL, residT, residE;
     uint32_t nResidT = 0;  // k_resid_s workgroups of 4x4 TBs (the head of residS)
+    uint32_t nResidE = 0;  // then workgroups of 32 TBs with both sides <= 8 (8 lanes each)
     size_t resElems = 0;
     // split submission (frame_begin / submit_tile / frame_end)
     bool inFrame = false;
@@ -1408,10 +1409,13 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     // inter TBs are added in place
     c->tbRes.assign(b->n_tbs, ~0u);
     // (k_resid_s's list: the 4x4 TBs first, 64 per workgroup at 4 lanes each -- half the
-    // TBs with coefficients --, then the others up to 16x16, 16 per workgroup at 16 lanes)
+    // TBs with coefficients --, then the 8x8 / 8x4 / 4x8 ones, 32 per workgroup at 8 lanes
+    // (with 16, half the lanes idled through both passes of an 8x8), then the others up to
+    // 16x16, 16 per workgroup at 16 lanes)
     c->residS.clear();
     c->residL.clear();
     c->residT.clear();
+    c->residE.clear();
     c->resElems = 0;
     for (uint32_t ti = 0; ti < b->n_tbs; ti++) {
         const av1r_tb& t = b->tbs[ti];
@@ -1422,11 +1426,14 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->tbRes[ti] = (uint32_t)c->resElems;
             c->resElems += (size_t)w * hh;
         }
-        (t.tx_size == AV1R_TX_4X4 ? c->residT : w <= 16 && hh <= 16 ? c->residS : c->residL).push_back(ti);
+        (t.tx_size == AV1R_TX_4X4 ? c->residT : w <= 8 && hh <= 8 ? c->residE : w <= 16 && hh <= 16 ? c->residS : c->residL).push_back(ti);
     }
     while (c->residT.size() % 64) c->residT.push_back(~0u);
+    while (c->residE.size() % 32) c->residE.push_back(~0u);
     while (c->residS.size() % 16) c->residS.push_back(~0u);
     c->nResidT = (uint32_t)(c->residT.size() / 64);
+    c->nResidE = (uint32_t)(c->residE.size() / 32);
+    c->residS.insert(c->residS.begin(), c->residE.begin(), c->residE.end());
     c->residS.insert(c->residS.begin(), c->residT.begin(), c->residT.end());
     // k_flow: dependency lists as item positions (every dependency is an earlier item: it
     // has a lower level); inter tiles after level 0 (intra block copy) keep the frame on
@@ -1668,6 +1675,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
     k.done = (uint32_t*)put(nullptr, 0, szDone, 0, false);
     k.n_items = (uint32_t)c->items.size();
     k.n_resid_t = c->nResidT;
+    k.n_resid_e = c->nResidE;
     k.mi = (const av1r_mi*)put(nullptr, 0, szMi, 0, false);
     if (verify) {
         // every section placed, in order, inside the buffer (a section left out of the
@@ -1690,7 +1698,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
         k.gran_w[p] = c->mapW[p];
         k.gran_hn[p] = c->mapH[p];
     }
-    P.nResidS = c->nResidT + (uint32_t)((c->residS.size() - 64 * c->nResidT) / 16);
+    P.nResidS = c->nResidT + c->nResidE + (uint32_t)((c->residS.size() - 64 * c->nResidT - 32 * c->nResidE) / 16);
     P.nResidL = (uint32_t)c->residL.size();
     P.resElems = c->resElems;
     k.mi_stride = h->mi_stride;

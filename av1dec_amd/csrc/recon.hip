@@ -2554,11 +2554,13 @@ DEV void resid_one(const KParams& k, uint32_t ti, int16_t* res)
 }
 
 // (a frame's first n_resid_t workgroups take 64 4x4 TBs at 4 lanes each: with 16 lanes a
-// 4x4 TB -- half the TBs with coefficients -- left 12 idle through both passes)
+// 4x4 TB -- half the TBs with coefficients -- left 12 idle through both passes; the next
+// n_resid_e 32 TBs of at most 8x8 at 8 lanes each, round 6)
 extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
     __shared__ __align__(16) union {
         int16_t s[16][16 * 18];
+        int16_t e[32][8 * 10];
         int16_t t[64][4 * 6];
     } res;
     const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
@@ -2566,15 +2568,21 @@ extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, 
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     const KParams& k = KP(kps, s);
-    const uint32_t bl = b - tab[s], nt = k.n_resid_t;
+    const uint32_t bl = b - tab[s], nt = k.n_resid_t, ne = k.n_resid_e;
     if (bl < nt) {
         const int g = threadIdx.x >> 2;
         const uint32_t ti = k.resid_s[bl * 64 + g];
         if (ti != ~0u) resid_one<4, 4>(k, ti, res.t[g]);
         return;
     }
+    if (bl < nt + ne) {  // 32 TBs of at most 8x8 (8x8, 8x4, 4x8), 8 lanes each
+        const int g = threadIdx.x >> 3;
+        const uint32_t ti = k.resid_s[nt * 64 + (bl - nt) * 32 + g];
+        if (ti != ~0u) resid_one<8, 8>(k, ti, res.e[g]);
+        return;
+    }
     const int g = threadIdx.x >> 4;
-    const uint32_t ti = k.resid_s[nt * 64 + (bl - nt) * 16 + g];
+    const uint32_t ti = k.resid_s[nt * 64 + ne * 32 + (bl - nt - ne) * 16 + g];
     if (ti != ~0u) resid_one<16, 16>(k, ti, res.s[g]);
 }
 
