@@ -200,7 +200,7 @@ struct KParams {
     const uint32_t* tb_res;
     int16_t* res;
     const uint32_t* resid_s;  // TBs with coefficients and sides <= 16: n_resid_t workgroups of 64 4x4 TBs, n_resid_e of 32 TBs <= 8x8, then 16 per workgroup (~0u pads)
-    const uint32_t* resid_l;  // the larger ones
+    const uint32_t* resid_l;  // the larger ones: [nm][nm workgroups of two TBs <= 32x32 (~0u pads)][then one per workgroup]
     // k_flow edge granules (cdna_hip_programming.md §6 Guideline 16 R2: the data is the
     // flag).  Per plane and 4x4 unit, the unit's bottom row (gran_h[row * gw + col]) and
     // right column (gran_v[col * gh + row], top to bottom) as {4 pixels, epoch << 32},
@@ -226,6 +226,10 @@ struct KParams {
     DevFrame lrout;   // loop-restoration output (LoopRestoration.cpp:216)
     DevFrame ref[8];  // reference store slots
 };
+// (resid_l carries its own class count: a KParams field for it, beside n_resid_e or appended,
+// changed the filters' code -- field offsets, the per-frame KParams stride -- and LF measured
+// 0.0098 -> 0.0107-0.0112 ms/frame, round 6, profiles/r06_ab_residm.txt)
+static_assert(sizeof(KParams) == 1232, "KParams layout");
 
 // Coefficient q of a TB whose first coefficient is `off` (DevTb / WorkItem coef_off), in
 // av1r_tb's 32-bit form: a 16-bit word (level << 10 | pos, |level| < 32) sign-extends to it.

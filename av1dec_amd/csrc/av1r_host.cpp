@@ -244,7 +244,8 @@ struct av1r_ctx {
     size_t granCap = 0;  // bytes
     // k_resid: per TB its residual tile offset (int16 elements, ~0u: none / added in place),
     // the small and large TB lists, the tiles' total size
-    std::vector<uint32_t> tbRes, residS, residL, residT, residE;
+    std::vector<uint32_t> tbRes, residS, residL, residT, residE, residM;
+    uint32_t nResidM = 0;  // k_resid_l workgroups of two TBs with both sides <= 32 (32 lanes each), heading residL
     uint32_t nResidT = 0;  // k_resid_s workgroups of 4x4 TBs (the head of residS)
     uint32_t nResidE = 0;  // then workgroups of 32 TBs with both sides <= 8 (8 lanes each)
     size_t resElems = 0;
@@ -1416,6 +1417,7 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
     c->residL.clear();
     c->residT.clear();
     c->residE.clear();
+    c->residM.clear();
     c->resElems = 0;
     for (uint32_t ti = 0; ti < b->n_tbs; ti++) {
         const av1r_tb& t = b->tbs[ti];
@@ -1426,8 +1428,15 @@ static void build_schedule(av1r_ctx* c, const av1r_frame_batch* b, bool allowGra
             c->tbRes[ti] = (uint32_t)c->resElems;
             c->resElems += (size_t)w * hh;
         }
-        (t.tx_size == AV1R_TX_4X4 ? c->residT : w <= 8 && hh <= 8 ? c->residE : w <= 16 && hh <= 16 ? c->residS : c->residL).push_back(ti);
+        (t.tx_size == AV1R_TX_4X4 ? c->residT : w <= 8 && hh <= 8 ? c->residE : w <= 16 && hh <= 16 ? c->residS
+         : w <= 32 && hh <= 32 ? c->residM : c->residL).push_back(ti);
     }
+    // (k_resid_l: two TBs of at most 32x32 per 64-lane workgroup, 32 lanes each -- one lane
+    // per row / column, so a 32-wide TB left half of 64 idle --, then the 64-sided ones)
+    while (c->residM.size() % 2) c->residM.push_back(~0u);
+    c->nResidM = (uint32_t)(c->residM.size() / 2);
+    c->residL.insert(c->residL.begin(), c->residM.begin(), c->residM.end());
+    c->residL.insert(c->residL.begin(), c->nResidM);  // (its head: the pairs' workgroup count)
     while (c->residT.size() % 64) c->residT.push_back(~0u);
     while (c->residE.size() % 32) c->residE.push_back(~0u);
     while (c->residS.size() % 16) c->residS.push_back(~0u);
@@ -1699,7 +1708,7 @@ static int pack_frame(av1r_ctx* c, const av1r_frame_batch* b, Prepared& P, uint8
         k.gran_hn[p] = c->mapH[p];
     }
     P.nResidS = c->nResidT + c->nResidE + (uint32_t)((c->residS.size() - 64 * c->nResidT - 32 * c->nResidE) / 16);
-    P.nResidL = (uint32_t)c->residL.size();
+    P.nResidL = c->nResidM + (uint32_t)(c->residL.size() - 1 - 2 * c->nResidM);
     P.resElems = c->resElems;
     k.mi_stride = h->mi_stride;
     k.mi_cols = h->mi_cols;

@@ -2588,13 +2588,23 @@ extern "C" __global__ __launch_bounds__(256) void k_resid_s(const KParams* kps, 
 
 extern "C" __global__ __launch_bounds__(64) void k_resid_l(const KParams* kps, const uint32_t* __restrict__ tab, int n)
 {
-    __shared__ __align__(16) int16_t res[64 * 66];
+    __shared__ __align__(16) union {
+        int16_t l[64 * 66];
+        int16_t m[2][32 * 34];
+    } res;
     const uint32_t b = xcd_order(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const uint32_t pre = lane + 1 < n ? tab[lane + 1] : 0xffffffffu;
     const int s = __builtin_amdgcn_readfirstlane(__popcll(__ballot(b >= pre)));
     const KParams& k = KP(kps, s);
-    resid_one<64, 64>(k, k.resid_l[b - tab[s]], res);
+    const uint32_t bl = b - tab[s], nm = sload(k.resid_l);  // (the list's head: its pair count)
+    if (bl < nm) {  // two TBs of at most 32x32, 32 lanes each (round 6)
+        const int g = lane >> 5;
+        const uint32_t ti = k.resid_l[1 + 2 * bl + g];
+        if (ti != ~0u) resid_one<32, 32>(k, ti, res.m[g]);
+        return;
+    }
+    resid_one<64, 64>(k, k.resid_l[1 + 2 * nm + (bl - nm)], res.l);
 }
 
 void launch_k_resid(int large, const KParams* kps, const uint32_t* tab, int n, unsigned groups, hipStream_t s)
