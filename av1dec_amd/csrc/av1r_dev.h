@@ -226,9 +226,9 @@ struct KParams {
     DevFrame lrout;   // loop-restoration output (LoopRestoration.cpp:216)
     DevFrame ref[8];  // reference store slots
 };
-// (resid_l carries its own class count: a KParams field for it, beside n_resid_e or appended,
-// changed the filters' code -- field offsets, the per-frame KParams stride -- and LF measured
-// 0.0098 -> 0.0107-0.0112 ms/frame, round 6, profiles/r06_ab_residm.txt)
+// (resid_l carries its own class count at its head rather than a KParams field: a field
+// changed every kernel's code through the field offsets and the per-frame KParams stride,
+// which made the filters' A/B readings hard to attribute -- round 6, profiles/r06_ab_residm.txt)
 static_assert(sizeof(KParams) == 1232, "KParams layout");
 
 // Coefficient q of a TB whose first coefficient is `off` (DevTb / WorkItem coef_off), in
